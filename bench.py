@@ -1,0 +1,206 @@
+"""Benchmark: point-cloud pairs/sec of the HRegNet forward (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): HRegNet forward, batch = 8 pairs per GPU,
+2 x 16384-point KITTI-shape synthetic LiDAR pairs (pcd_reg_hregnet_amd.synthetic),
+eval mode, fp32, weights = nusc_feats (pretrained feature extractor) + seeded
+heads.  A step = one forward over one batch; inputs are resident in HBM before
+the timed region.  Multi-GPU: one process per GPU, each rank runs its own 8
+pairs (pairs are independent in eval mode: no collective on the data path),
+weak scaling; value = all pairs / max-over-ranks time.
+
+Extra fields: ``roofline`` for the dominant kernel family (the fp32 MFMA GEMM,
+timed live with HIP events on the launch stream inside the timed region) and
+``cpu_baseline`` (the CPU oracle restatement on the host cores, bounded sample,
+rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak BW (spec)
+POINTS = 16384
+PAIRS_PER_GPU = 8
+
+
+class _Args:
+    use_fps = True
+    use_weights = True
+    freeze_detector = False
+    freeze_feats = False
+
+
+def make_model(device):
+    from pcd_reg_hregnet_amd import weights
+    from pcd_reg_hregnet_amd.models import HRegNet
+    net = HRegNet(_Args())
+    net.load_state_dict(weights.make_state_dict(net.state_dict(), seed=0, pretrained_feats=True))
+    return net.to(device).eval()
+
+
+class GemmTimer:
+    """Brackets every GEMM launch with HIP events on the launch stream."""
+
+    def __init__(self):
+        self.events = []
+        self.flops = 0.0
+        self.enabled = False
+
+    def install(self):
+        from pcd_reg_hregnet_amd import _lib
+        orig = _lib.gemm
+
+        def timed(g):
+            if not self.enabled:
+                return orig(g)
+            st = torch.cuda.current_stream()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            orig(g)
+            e1.record(st)
+            self.events.append((e0, e1))
+            self.flops += 2.0 * g.R * g.N * g.K * g.batch
+        _lib.gemm = timed
+
+    def result(self):
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in self.events)
+        n = len(self.events)
+        return ms, n, self.flops
+
+
+def cpu_baseline(budget_s: float = 12.0):
+    """Oracle (numpy + C restatement) on host cores, bounded sample of the same workload."""
+    from oracle import oracle
+    from pcd_reg_hregnet_amd import synthetic, weights
+    from pcd_reg_hregnet_amd.models import HRegNet
+    sd = {k: v.numpy() for k, v in
+          weights.make_state_dict(HRegNet(_Args()).state_dict(), seed=0).items()}
+    s, d, _, _ = synthetic.lidar_batch(1, POINTS, seed0=0)
+    oracle.hregnet_forward(sd, s, d)  # warm-up
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        oracle.hregnet_forward(sd, s, d)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 64:
+            break
+    threads = oracle.lib().oracle_num_threads()
+    return {"value": n / el, "unit": "pairs/s", "cores": int(threads), "kind": "port",
+            "sample": f"{n} pair(s) of 2x{POINTS}-pt KITTI-shape synthetic LiDAR, B=1, "
+                      f"{el:.1f} s wall, numpy BLAS + OpenMP C oracle (oracle/)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=PAIRS_PER_GPU, help="pairs per GPU")
+    ap.add_argument("--points", type=int, default=POINTS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+
+    from pcd_reg_hregnet_amd import _lib, engine, synthetic
+    _lib.load()
+    net = make_model(device)
+    P = net.prepared(device)
+    B = args.batch
+    s, d, _, _ = synthetic.lidar_batch(B, args.points, seed0=1000 * rank)
+    src = torch.from_numpy(s).to(device)
+    dst = torch.from_numpy(d).to(device)
+
+    timer = GemmTimer()
+    timer.install()
+
+    def step():
+        with torch.no_grad():
+            return engine.hregnet_forward(P, src, dst)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    gemm_ms, n_gemm, gemm_flops = timer.result()
+
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_pairs = B * args.steps * world
+    value = total_pairs / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        per_launch_flops = gemm_flops / max(n_gemm, 1)
+        per_launch_s = gemm_ms / max(n_gemm, 1) / 1e3
+        achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
+        roof = {"kernel": "gemm_nt_kernel (fp32 MFMA 32x32x2, all conv/BN/ReLU layers + cosine)",
+                "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                "traffic": None,
+                "launches_per_step": n_gemm // args.steps,
+                "avg_launch_us": round(per_launch_s * 1e6, 2),
+                "gemm_ms_per_step": round(gemm_ms / args.steps, 3),
+                "algorithmic_gflop_per_pair": round(gemm_flops / args.steps / B / 1e9, 3)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(args.cpu_budget)
+            except Exception as e:  # the baseline must never sink the GPU number
+                cpu = {"error": repr(e)}
+        line = {
+            "metric": "point-cloud pairs/sec, HRegNet forward, 16384-pt pairs",
+            "value": round(value, 3), "unit": "pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded KITTI-shape LiDAR pairs; nusc_feats + seeded heads)",
+            "config": {"workload": f"HRegNet forward (eval), batch={B} pairs/GPU, "
+                                   f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])",
+                       "global_batch": B * world, "points": args.points,
+                       "parallelism": f"dp{world} (pairs sharded, no collective)"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    del out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,196 @@
+/*
+ * hregnet_amd.h -- C ABI of the MI355X-native HRegNet forward path.
+ *
+ * Plain pointers and sizes only: every float/int pointer is a DEVICE pointer
+ * (HBM), `stream` is a hipStream_t passed as void*.  Calls enqueue work on
+ * that stream and return immediately (asynchronous, like the reference's
+ * launches on at::cuda::getCurrentCUDAStream(), furthest_point_sampling.cpp:16).
+ * Every entry returns a status code instead of printing and calling exit(-1)
+ * as the reference launchers do (furthest_point_sampling_gpu.cu:35-38).
+ * Callers allocate every buffer (reference models/utils.py:24-25,48-49,71,84).
+ *
+ * Reference interface replaced by each entry (reference = UpendraArun/pcd_reg_hregnet):
+ *   hreg_furthest_point_sampling          <- point_utils_cuda.furthest_point_sampling_wrapper
+ *                                            (models/PointUtils/src/furthest_point_sampling.cpp:33-43,
+ *                                             point_utils_api.cpp:10)
+ *   hreg_weighted_furthest_point_sampling <- point_utils_cuda.weighted_furthest_point_sampling_wrapper
+ *                                            (furthest_point_sampling.cpp:45-55, point_utils_api.cpp:11)
+ *   hreg_gather_points                    <- point_utils_cuda.gather_points_wrapper
+ *                                            (furthest_point_sampling.cpp:10-19, point_utils_api.cpp:8)
+ *   hreg_gather_points_grad               <- point_utils_cuda.gather_points_grad_wrapper
+ *                                            (furthest_point_sampling.cpp:21-31, point_utils_api.cpp:9)
+ *   hreg_knn_points                       <- pytorch3d.ops.knn_points (pytorch3d 0.7.8, Dockerfile:44-46;
+ *                                            call sites models/HRegNet/layers.py:20,278,316,322,434)
+ *   hreg_knn_gather                       <- pytorch3d.ops.knn_gather (layers.py:25,279,288,317,...)
+ *   hreg_knn_group                        <- knn_group() (models/HRegNet/layers.py:9-27), fused
+ *   hreg_gemm                             <- nn.Conv1d/Conv2d 1x1 + BatchNorm(eval) + ReLU stacks
+ *                                            (layers.py:115-130,183-198,246-268,417-431) and the
+ *                                            cosine-similarity contraction (layers.py:29-41,290-301)
+ *   hreg_attend                           <- channel-max -> softmax_k -> attentive sums
+ *                                            (layers.py:150-159, 329-337, 384-390, 446-450)
+ *   hreg_group_max                        <- torch.max(x, dim=k) (layers.py:202, 208)
+ *   hreg_head_out                         <- mlp3 + softplus(+0.001) / sigmoid (layers.py:161-163,393-394,451-452)
+ *                                            and the sigma->weight normalisation (models/HRegNet/models.py:30-32)
+ *   hreg_row_norms                        <- torch.norm(desc, dim=-1) inside calc_cosine_similarity (layers.py:38-39)
+ *   hreg_sim_gather                       <- max-normalised similarity gathered at the desc kNN (layers.py:296-313,345-362)
+ *   hreg_pair_feats                       <- geometric/weight/similarity feature rows (layers.py:279-288,364-370,437-445)
+ *   hreg_weighted_svd                     <- WeightedSVDHead.forward (layers.py:469-504) + T = T_ @ T_prev
+ *                                            composition (models/HRegNet/models.py:100-127)
+ *   hreg_transform_points                 <- R @ xyz^T + t (models/HRegNet/models.py:91-92,113-114)
+ */
+#ifndef HREGNET_AMD_H
+#define HREGNET_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    HREG_OK = 0,
+    HREG_ERR_INVALID = 1,     /* bad argument (null pointer, negative size, unsupported shape) */
+    HREG_ERR_LAUNCH = 2,      /* hipGetLastError() after a launch */
+    HREG_ERR_UNSUPPORTED = 3  /* shape outside what the kernels implement (e.g. K > 64) */
+};
+
+/* ---------------- point_utils_cuda boundary ---------------- */
+
+/* points [b,n,3] f32, temp [b,n] f32 (may be NULL for n <= 16384; receives the
+ * final running-min distances), idx [b,m] int32 (out), sampled_xyz [b,m,3]
+ * (optional out: gathered coordinates of idx). */
+int hreg_furthest_point_sampling(int b, int n, int m, const float *points, float *temp,
+                                 int32_t *idx, float *sampled_xyz, void *stream);
+
+/* as above with weights [b,n]: d = w_k * |p_k - p_old|^2 */
+int hreg_weighted_furthest_point_sampling(int b, int n, int m, const float *points,
+                                          const float *weights, float *temp, int32_t *idx,
+                                          float *sampled_xyz, void *stream);
+
+/* points [b,c,n], idx [b,npoints] -> out [b,c,npoints] */
+int hreg_gather_points(int b, int c, int n, int npoints, const float *points, const int32_t *idx,
+                       float *out, void *stream);
+
+/* grad_out [b,c,npoints] scatter-added into grad_points [b,c,n] (caller zeroes it) */
+int hreg_gather_points_grad(int b, int c, int n, int npoints, const float *grad_out,
+                            const int32_t *idx, float *grad_points, void *stream);
+
+/* ---------------- pytorch3d.ops boundary ---------------- */
+
+/* p1 [b,n1,dim], p2 [b,n2,dim] -> K nearest of each p1 row in p2 by squared L2,
+ * ascending (dist, idx).  dists [b,n1,k] f32; idx64 [b,n1,k] int64 and/or
+ * idx32 [b,n1,k] int32 (either may be NULL); nn [b,n1,k,dim] optional.
+ * k <= 64.  Rows beyond n2 (k > n2) get idx -1, dist 0, nn 0. */
+int hreg_knn_points(const float *p1, const float *p2, int b, int n1, int n2, int dim, int k,
+                    float *dists, int64_t *idx64, int32_t *idx32, float *nn, void *stream);
+
+/* x [b,n,c], idx [b,m,k] int64 -> out [b,m,k,c]; idx < 0 gives zeros */
+int hreg_knn_gather(const float *x, const int64_t *idx, int b, int n, int c, int m, int k,
+                    float *out, void *stream);
+
+/* ---------------- fused stages of the HRegNet forward ---------------- */
+
+/* knn_group (layers.py:9-27) for nb clouds: query q [nb,m,3], database p [nb,n,3].
+ * Outputs per (cloud, query, neighbour) row r = (c*m + i)*k + j:
+ *   gidx [nb*m*k] int32 = c*n + idx (global row of the neighbour in p),
+ *   geom [nb*m*k][4] = (p - q, |p - q|), knn_xyz [nb*m*k][3] (optional). */
+int hreg_knn_group(const float *q, const float *p, int nb, int m, int n, int k, int32_t *gidx,
+                   float *geom, float *knn_xyz, void *stream);
+
+/* One K-segment of the GEMM's activation operand A (rows x K, row-major). */
+typedef struct {
+    const float *base;       /* [rows][ld] */
+    const int32_t *gather;   /* optional: source row = gather[r] */
+    const float *rowscale;   /* optional: value *= rowscale[r] (attentive map, layers.py:158) */
+    int64_t batch_stride;    /* floats added per grid.z batch to base */
+    int ld;                  /* row stride in floats, multiple of 4 */
+    int k0;                  /* first K column of this segment, multiple of 4 */
+    int kc;                  /* K columns in this segment, multiple of 4 */
+    int row_div;             /* source row = r / row_div when gather == NULL (>= 1) */
+} hreg_seg_t;
+
+#define HREG_MAX_SEGS 4
+#define HREG_EPI_AFFINE 0 /* y = acc * scale[n] + shift[n]; optional ReLU */
+#define HREG_EPI_COSINE 1 /* y = acc / (rnorm[r] * cnorm[n] + 1e-6) */
+
+/* out[r][n] = epi( sum_k A[r][k] * W[n][k] ), r < R, n < N, k < K, fp32 MFMA. */
+typedef struct {
+    hreg_seg_t seg[HREG_MAX_SEGS];
+    int nseg;
+    int R, N, K;
+    int batch;               /* grid.z batches (>= 1) */
+    int ldw;                 /* W row stride (>= K), multiple of 4 */
+    int64_t w_batch_stride;
+    const float *W;          /* [N][ldw] */
+    const float *scale;      /* [N] or NULL (1) */
+    const float *shift;      /* [N] or NULL (0) */
+    int relu;
+    int epi;
+    const float *rnorm;      /* [R] per batch (EPI_COSINE) */
+    const float *cnorm;      /* [N] per batch (EPI_COSINE) */
+    int64_t rnorm_batch_stride, cnorm_batch_stride;
+    float *out;              /* [R][ldo] */
+    int ldo;
+    int64_t out_batch_stride;
+} hreg_gemm_t;
+
+int hreg_gemm(const hreg_gemm_t *g, void *stream);
+
+/* Attentive pooling over groups of k rows (layers.py:150-159 and siblings).
+ * logits_src [G*k][C] : a = softmax_k(max_c logits_src[r][c])  -> attw [G*k] (optional)
+ * values: att[g][c] = sum_j a[g,j] * V[row(g,j)][c], V = vals (row = g*k+j) or
+ *         vals gathered by vgather[g*k+j]; att optional [G][ldatt]
+ * xyz: kp[g][:] = sum_j a[g,j] * xyz_rows[g*k+j][:] (optional, [G*k][3] -> [G][3]) */
+int hreg_attend(const float *logits_src, int C, int ldl, int G, int k, float *attw,
+                const float *vals, const int32_t *vgather, int Cv, int ldv, float *att, int ldatt,
+                const float *xyz_rows, float *kp, void *stream);
+
+/* out[g][c] = max_j x[g*k+j][c] over groups of k rows, x [G*k][ldx] */
+int hreg_group_max(const float *x, int G, int k, int C, int ldx, float *out, int ldo, void *stream);
+
+#define HREG_HEAD_SOFTPLUS 0 /* sigma = softplus(z) + 0.001 (layers.py:162) */
+#define HREG_HEAD_SIGMOID 1  /* w = sigmoid(z) (layers.py:394) */
+/* z[r] = dot(x[r][:C], w3) + b3 for rows of nclouds x rows_per_cloud; writes
+ * out[r]; if weights_out != NULL also w = 1/(sigma+1e-5) / mean_cloud(.) (models.py:30-32). */
+int hreg_head_out(const float *x, int C, int ldx, int nclouds, int rows_per_cloud,
+                  const float *w3, const float *b3, int mode, float *out, float *weights_out,
+                  void *stream);
+
+/* norms[r] = sqrt(sum_c x[r][c]^2), x [R][ldx] */
+int hreg_row_norms(const float *x, int R, int C, int ldx, float *norms, void *stream);
+
+/* S [nb][N1][N2]; kidx [nb][N1][k] int32 (local dst index) ->
+ * sims[(b*N1+i)*k+j][2] = (S[i][n]/(rowmax_i + 1e-6), S[i][n]/(colmax_n + 1e-6)), n = kidx */
+int hreg_sim_gather(const float *S, int nb, int N1, int N2, const int32_t *kidx, int k,
+                    float *sims, int ld_sims, void *stream);
+
+/* Small per-(query,neighbour) feature rows for CoarseReg/FineReg (16 floats):
+ * [p-q (3), |p-q| (1), q (3), p (3), w_src (1), w_dst[n] (1), sims (ns: 0 or 4), pad].
+ * q = src_xyz [nb][M][3], p = dst_xyz [nb][N][3] gathered by kidx (local), w from
+ * src_w [nb][M], dst_w [nb][N]; sims [rows][2] x 2 (sim_a, sim_b) optional. */
+int hreg_pair_feats(const float *src_xyz, const float *dst_xyz, const float *src_w,
+                    const float *dst_w, const int32_t *kidx, int nb, int M, int N, int k,
+                    const float *sims_a, const float *sims_b, float *feats, int ldf,
+                    float *knn_xyz, int32_t *gidx, void *stream);
+
+/* WeightedSVDHead (layers.py:469-504) for nb pairs of n points:
+ * src, corres [nb][n][3], w [nb][n] -> R_ [nb][9], t_ [nb][3]; if prev_R/prev_t
+ * are given, also R = R_ prev_R, t = R_ prev_t + t_ (models.py:100-127) into R/t.
+ * A non-finite covariance anywhere in the batch gives R_ = I, t_ = 0 for the
+ * whole batch (the reference's try/except, layers.py:485-493). */
+int hreg_weighted_svd(const float *src, const float *corres, const float *w, int nb, int n,
+                      const float *prev_R, const float *prev_t, float *R_, float *t_, float *R,
+                      float *t, void *stream);
+
+/* out[b][i] = R[b] xyz[b][i] + t[b], xyz/out [nb][n][3] */
+int hreg_transform_points(const float *xyz, const float *R, const float *t, int nb, int n,
+                          float *out, void *stream);
+
+/* library build id (for the loaded-.so audit) */
+const char *hreg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HREGNET_AMD_H */

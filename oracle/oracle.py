@@ -1,0 +1,405 @@
+"""CPU oracle for the HRegNet forward hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker (or the timed CPU
+baseline).  The product path (``pcd_reg_hregnet_amd``) never imports it.
+
+It is a numpy (float32) restatement of the reference's algorithm, with the
+index-exact ops (FPS, WFPS, kNN, gather) in ``hregnet_oracle.c``
+(``liboracle.so``, built by ``oracle/Makefile``).  Every function cites the
+reference file:line it follows (reference = /root/reference, read as text).
+
+Parity pinning: ``tests/golden/make_golden.py`` ran the reference's own Python
+model (``models/HRegNet``) in this container with shims for the unbuilt CUDA
+extension (a literal thread-level emulation of ``furthest_point_sampling_gpu.cu``)
+and the absent ``pytorch3d`` (brute-force kNN); the fixtures it wrote under
+``tests/golden/`` pin this oracle (``tests/test_oracle_golden.py``).
+kNN tie order against pytorch3d itself is "parity unpinned" (SURVEY.md 8c).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-C", _HERE, "-s"])
+        L = ctypes.CDLL(path)
+        f32p = ctypes.POINTER(ctypes.c_float)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        L.oracle_opt_n_threads.argtypes = [ctypes.c_int]
+        L.oracle_opt_n_threads.restype = ctypes.c_int
+        L.oracle_fps.argtypes = [f32p, f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, i32p]
+        L.oracle_fps.restype = ctypes.c_int
+        L.oracle_knn.argtypes = [f32p, f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, i32p, f32p]
+        L.oracle_knn.restype = ctypes.c_int
+        L.oracle_gather_points.argtypes = [f32p, i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, f32p]
+        L.oracle_gather_points_grad.argtypes = [f32p, i32p, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int, f32p]
+        L.oracle_num_threads.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _ip(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def opt_n_threads(n: int) -> int:
+    """cuda_utils.h:22-26"""
+    return lib().oracle_opt_n_threads(int(n))
+
+
+def fps(xyz: np.ndarray, npoint: int, weights: np.ndarray | None = None) -> np.ndarray:
+    """furthest_point_sampling_gpu.cu:84-206 (weights=None) / :254-375 (weighted).
+
+    xyz [B,N,3] f32, weights [B,N] f32 -> idx [B,npoint] int32.
+    """
+    xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+    B, N, _ = xyz.shape
+    out = np.zeros((B, npoint), dtype=np.int32)
+    w = None
+    if weights is not None:
+        w = np.ascontiguousarray(weights, dtype=np.float32)
+        assert w.shape == (B, N)
+    rc = lib().oracle_fps(_fp(xyz), _fp(w) if w is not None else None, B, N, npoint, _ip(out))
+    assert rc == 0
+    return out
+
+
+def gather_points(points: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """gather_points_kernel_fast (.cu:7-21): [B,C,N] x [B,M] -> [B,C,M]"""
+    points = np.ascontiguousarray(points, dtype=np.float32)
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    B, C, N = points.shape
+    M = idx.shape[1]
+    out = np.empty((B, C, M), dtype=np.float32)
+    lib().oracle_gather_points(_fp(points), _ip(idx), B, C, N, M, _fp(out))
+    return out
+
+
+def gather_points_grad(grad_out: np.ndarray, idx: np.ndarray, n: int) -> np.ndarray:
+    """gather_points_grad_kernel_fast (.cu:41-55): scatter-add into [B,C,N]."""
+    grad_out = np.ascontiguousarray(grad_out, dtype=np.float32)
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    B, C, M = grad_out.shape
+    out = np.zeros((B, C, n), dtype=np.float32)
+    lib().oracle_gather_points_grad(_fp(grad_out), _ip(idx), B, C, n, M, _fp(out))
+    return out
+
+
+def knn(p1: np.ndarray, p2: np.ndarray, K: int):
+    """pytorch3d.ops.knn_points (0.7.8) semantics, canonical (dist, idx) order.
+
+    p1 [B,N1,D], p2 [B,N2,D] -> (dists [B,N1,K] f32, idx [B,N1,K] int64).
+    """
+    p1 = np.ascontiguousarray(p1, dtype=np.float32)
+    p2 = np.ascontiguousarray(p2, dtype=np.float32)
+    B, N1, D = p1.shape
+    N2 = p2.shape[1]
+    idx = np.empty((B, N1, K), dtype=np.int32)
+    dist = np.empty((B, N1, K), dtype=np.float32)
+    rc = lib().oracle_knn(_fp(p1), _fp(p2), B, N1, N2, D, K, _ip(idx), _fp(dist))
+    assert rc == 0
+    return dist, idx.astype(np.int64)
+
+
+def knn_gather(x: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """pytorch3d.ops.knn_gather: x [B,N,C], idx [B,M,K] -> [B,M,K,C]"""
+    B = x.shape[0]
+    return x[np.arange(B)[:, None, None], idx]
+
+
+# --------------------------------------------------------------------------
+# Layer restatements (models/HRegNet/layers.py), numpy float32, eval-mode BN.
+# --------------------------------------------------------------------------
+BN_EPS = 1e-5
+
+
+def _bn(x, sd, pre, axis=1):
+    """nn.BatchNorm{1,2}d eval: (x - mean) / sqrt(var + eps) * gamma + beta."""
+    shape = [1] * x.ndim
+    shape[axis] = -1
+    mean = sd[pre + ".running_mean"].reshape(shape)
+    var = sd[pre + ".running_var"].reshape(shape)
+    g = sd[pre + ".weight"].reshape(shape)
+    b = sd[pre + ".bias"].reshape(shape)
+    return ((x - mean) / np.sqrt(var + np.float32(BN_EPS)) * g + b).astype(np.float32)
+
+
+def _conv(x, w, b=None):
+    """1x1 Conv{1,2}d over [B,C,...]: y[b,o,...] = sum_c W[o,c] x[b,c,...] (+ bias)."""
+    B, C = x.shape[:2]
+    rest = x.shape[2:]
+    W = w.reshape(w.shape[0], -1)
+    y = np.matmul(W[None], x.reshape(B, C, -1)).reshape((B, W.shape[0]) + rest)
+    if b is not None:
+        y = y + b.reshape((1, -1) + (1,) * len(rest))
+    return y.astype(np.float32)
+
+
+def _conv_stack(x, sd, pre, n):
+    """nn.Sequential of n x [Conv(bias=False), BN, ReLU] (layers.py:115-121, 183-189, 246-260)."""
+    for i in range(n):
+        x = _conv(x, sd[f"{pre}.{3 * i}.weight"])
+        x = _bn(x, sd, f"{pre}.{3 * i + 1}")
+        x = np.maximum(x, 0)
+    return x
+
+
+def _mlp(x, sd, pre, act=True):
+    """Conv1d(bias) [+ BN + ReLU] (layers.py:124-130, 262-268, 425-431)."""
+    x = _conv(x, sd[pre + ".0.weight"], sd[pre + ".0.bias"])
+    if act:
+        x = _bn(x, sd, pre + ".1")
+        x = np.maximum(x, 0)
+    return x
+
+
+def _softmax(x, axis=-1):
+    m = np.max(x, axis=axis, keepdims=True)
+    e = np.exp(x - m)
+    return (e / np.sum(e, axis=axis, keepdims=True)).astype(np.float32)
+
+
+def _softplus(x):
+    """nn.Softplus (beta=1, threshold=20)."""
+    return np.where(x > 20, x, np.log1p(np.exp(np.minimum(x, 20)))).astype(np.float32)
+
+
+def _sigmoid(x):
+    return (1.0 / (1.0 + np.exp(-x))).astype(np.float32)
+
+
+def knn_group(xyz1, xyz2, feats2, k):
+    """layers.py:9-27: grouped [B,4+C,M,k], knn_xyz [B,M,k,3]."""
+    _, idx = knn(xyz1, xyz2, k)
+    knn_xyz = knn_gather(xyz2, idx)
+    rela = knn_xyz - xyz1[:, :, None, :]
+    dist = np.sqrt(np.sum(rela * rela, axis=-1, keepdims=True)).astype(np.float32)
+    parts = [rela, dist]
+    if feats2 is not None:
+        parts.append(knn_gather(np.ascontiguousarray(feats2.transpose(0, 2, 1)), idx))
+    g = np.concatenate(parts, axis=-1)
+    return np.ascontiguousarray(g.transpose(0, 3, 1, 2)), knn_xyz, idx
+
+
+def keypoint_detector(sd, pre, xyz, feats, weights, nsample, k):
+    """KeypointDetector.forward, layers.py:134-165 (fps=True)."""
+    idx = fps(xyz, nsample, weights)
+    sampled = gather_points(np.ascontiguousarray(xyz.transpose(0, 2, 1)), idx).transpose(0, 2, 1)
+    grouped, knn_xyz, _ = knn_group(np.ascontiguousarray(sampled), xyz, feats, k)
+    emb = _conv_stack(grouped, sd, pre + ".convs", 3)
+    x1 = np.max(emb, axis=1)
+    a = _softmax(x1, -1)
+    keypoints = np.sum(a[..., None] * knn_xyz, axis=2).astype(np.float32)
+    att_map = (emb * a[:, None]).astype(np.float32)
+    att_feat = np.sum(att_map, axis=-1).astype(np.float32)
+    s = _mlp(_mlp(att_feat, sd, pre + ".mlp1"), sd, pre + ".mlp2")
+    s = _mlp(s, sd, pre + ".mlp3", act=False)
+    sigmas = (_softplus(s) + np.float32(0.001))[:, 0]
+    return keypoints, sigmas, att_feat, grouped, att_map, idx
+
+
+def desc_extractor(sd, pre, grouped, att_map):
+    """DescExtractor.forward, layers.py:200-209."""
+    x1 = _conv_stack(grouped, sd, pre + ".convs", 3)
+    k = x1.shape[-1]
+    x2 = np.repeat(np.max(x1, axis=3, keepdims=True), k, axis=3)
+    x2 = np.concatenate([x2, x1, att_map], axis=1)
+    x2 = _conv_stack(x2, sd, pre + ".mlp1", 1)
+    x2 = _conv_stack(x2, sd, pre + ".mlp2", 1)
+    return np.max(x2, axis=3)
+
+
+def _norm_weights(s):
+    """models.py:30-32 / :36-38"""
+    w = (np.float32(1.0) / (s + np.float32(1e-5))).astype(np.float32)
+    return (w / np.mean(w, axis=1, keepdims=True)).astype(np.float32)
+
+
+def feature_extraction(sd, points, use_weights=True):
+    """HierFeatureExtraction.forward, models.py:26-58 (use_fps=True)."""
+    p = "feature_extraction."
+    xyz1, s1, f1, g1, m1, i1 = keypoint_detector(sd, p + "detector_1", points, None, None, 1024, 64)
+    d1 = desc_extractor(sd, p + "desc_extractor_1", g1, m1)
+    w1 = _norm_weights(s1) if use_weights else None
+    xyz2, s2, f2, g2, m2, i2 = keypoint_detector(sd, p + "detector_2", xyz1, f1, w1, 512, 32)
+    d2 = desc_extractor(sd, p + "desc_extractor_2", g2, m2)
+    w2 = _norm_weights(s2) if use_weights else None
+    xyz3, s3, f3, g3, m3, i3 = keypoint_detector(sd, p + "detector_3", xyz2, f2, w2, 256, 16)
+    d3 = desc_extractor(sd, p + "desc_extractor_3", g3, m3)
+    return dict(xyz_1=xyz1, xyz_2=xyz2, xyz_3=xyz3, sigmas_1=s1, sigmas_2=s2, sigmas_3=s3,
+                desc_1=d1, desc_2=d2, desc_3=d3, fps_idx_1=i1, fps_idx_2=i2, fps_idx_3=i3)
+
+
+def cosine_similarity_matrix(a, b):
+    """calc_cosine_similarity (layers.py:29-41) over all pairs:
+    S[b,i,j] = <a_i, b_j> / (|a_i| |b_j| + 1e-6); a [B,N,C], b [B,M,C]."""
+    ip = np.matmul(a, b.transpose(0, 2, 1))
+    na = np.sqrt(np.sum(a * a, axis=-1))
+    nb = np.sqrt(np.sum(b * b, axis=-1))
+    return (ip / (na[:, :, None] * nb[:, None, :] + np.float32(1e-6))).astype(np.float32)
+
+
+def _sim_feats(src_d, dst_d, knn_idx):
+    """layers.py:292-313 (and :341-362 for the neighbour branch).
+
+    dst_src_cos[b,i,j] = S[b,i,n] / (max_i' S[b,i',n] + 1e-6), n = knn_idx[b,i,j]
+    src_dst_cos[b,i,j] = S[b,i,n] / (max_n' S[b,i,n'] + 1e-6)
+    where S[b,i,n] = cos(src_i, dst_n).  Returns (src_dst, dst_src) [B,N1,k].
+    """
+    S = cosine_similarity_matrix(src_d, dst_d)  # [B,N1,N2]
+    col_max = np.max(S, axis=1, keepdims=True)  # per dst n (dst_src_cos_max)
+    row_max = np.max(S, axis=2, keepdims=True)  # per src i (src_dst_cos_max)
+    g = np.take_along_axis(S, knn_idx, axis=2)  # S[b,i,n_ij]
+    cm = np.take_along_axis(np.broadcast_to(col_max, S.shape), knn_idx, axis=2)
+    src_dst = (g / (row_max + np.float32(1e-6))).astype(np.float32)
+    dst_src = (g / (cm + np.float32(1e-6))).astype(np.float32)
+    return src_dst, dst_src
+
+
+def _nbr_desc(sd, pre, xyz, desc, k):
+    """neighbour-aware descriptor, layers.py:316-337."""
+    _, idx = knn(xyz, xyz, k)
+    knn_xyz = knn_gather(xyz, idx)
+    feats = knn_gather(desc, idx)
+    rela = knn_xyz - xyz[:, :, None, :]
+    dist = np.sqrt(np.sum(rela * rela, axis=-1, keepdims=True)).astype(np.float32)
+    f = np.concatenate([feats, rela, dist], axis=-1)
+    w = _conv_stack(np.ascontiguousarray(f.transpose(0, 3, 1, 2)), sd, pre + ".convs_2", 3)
+    w = _softmax(np.max(w, axis=1), -1)
+    return np.sum(feats * w[..., None], axis=2).astype(np.float32)
+
+
+def coarse_reg(sd, pre, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w, k=8):
+    """CoarseReg.forward, layers.py:273-396 (use_sim = use_neighbor = True)."""
+    sdsc = np.ascontiguousarray(src_desc.transpose(0, 2, 1))
+    ddsc = np.ascontiguousarray(dst_desc.transpose(0, 2, 1))
+    _, kidx = knn(sdsc, ddsc, k)
+    knn_desc = knn_gather(ddsc, kidx)
+    knn_xyz = knn_gather(dst_xyz, kidx)
+    xyz_e = np.repeat(src_xyz[:, :, None, :], k, axis=2)
+    desc_e = np.repeat(sdsc[:, :, None, :], k, axis=2)
+    rela = knn_xyz - xyz_e
+    dist = np.sqrt(np.sum(rela * rela, axis=-1, keepdims=True)).astype(np.float32)
+    w_e = np.repeat(src_w[:, :, None, None], k, axis=2)
+    knn_w = knn_gather(dst_w[..., None], kidx)
+    sd_cos, ds_cos = _sim_feats(sdsc, ddsc, kidx)
+    snb = _nbr_desc(sd, pre, src_xyz, sdsc, k)
+    dnb = _nbr_desc(sd, pre, dst_xyz, ddsc, k)
+    sd_ncos, ds_ncos = _sim_feats(snb, dnb, kidx)
+    feats = np.concatenate([rela, dist, xyz_e, knn_xyz, desc_e, knn_desc, w_e, knn_w,
+                            sd_cos[..., None], ds_cos[..., None], sd_ncos[..., None],
+                            ds_ncos[..., None]], axis=-1)
+    f = _conv_stack(np.ascontiguousarray(feats.transpose(0, 3, 1, 2)), sd, pre + ".convs_1", 3)
+    a = _softmax(np.max(f, axis=1), -1)
+    corres = np.sum(a[..., None] * knn_xyz, axis=2).astype(np.float32)
+    att = np.sum(a[:, None] * f, axis=-1).astype(np.float32)
+    w = _mlp(_mlp(att, sd, pre + ".mlp1"), sd, pre + ".mlp2")
+    w = _mlp(w, sd, pre + ".mlp3", act=False)
+    return corres, _sigmoid(w[:, 0]), kidx
+
+
+def fine_reg(sd, pre, src_xyz, src_feat, dst_xyz, dst_feat, src_w, dst_w, k=8):
+    """FineReg.forward, layers.py:433-454."""
+    _, kidx = knn(src_xyz, dst_xyz, k)
+    knn_xyz = knn_gather(dst_xyz, kidx)
+    sf = np.ascontiguousarray(src_feat.transpose(0, 2, 1))
+    df = np.ascontiguousarray(dst_feat.transpose(0, 2, 1))
+    knn_f = knn_gather(df, kidx)
+    xyz_e = np.repeat(src_xyz[:, :, None, :], k, axis=2)
+    f_e = np.repeat(sf[:, :, None, :], k, axis=2)
+    rela = knn_xyz - xyz_e
+    dist = np.sqrt(np.sum(rela * rela, axis=-1, keepdims=True)).astype(np.float32)
+    w_e = np.repeat(src_w[:, :, None, None], k, axis=2)
+    knn_w = knn_gather(dst_w[..., None], kidx)
+    feats = np.concatenate([rela, dist, xyz_e, knn_xyz, f_e, knn_f, w_e, knn_w], axis=-1)
+    f = _conv_stack(np.ascontiguousarray(feats.transpose(0, 3, 1, 2)), sd, pre + ".convs_1", 3)
+    a = _softmax(np.max(f, axis=1), -1)
+    corres = np.sum(a[..., None] * knn_xyz, axis=2).astype(np.float32)
+    att = np.sum(a[:, None] * f, axis=-1).astype(np.float32)
+    w = _mlp(_mlp(att, sd, pre + ".mlp1"), sd, pre + ".mlp2")
+    w = _mlp(w, sd, pre + ".mlp3", act=False)
+    return corres, _sigmoid(w[:, 0]), kidx
+
+
+def weighted_svd(src, corres, weights):
+    """WeightedSVDHead.forward, layers.py:469-504 (fp64 SVD, cast to f32).
+
+    Returns (R [B,3,3], t [B,3]); R = I, t = 0 for the whole batch when the
+    SVD cannot run (layers.py:485-493)."""
+    eps = 1e-4
+    w = weights.astype(np.float64)
+    w = w / (np.sum(w, axis=1, keepdims=True) + eps)
+    ws = np.sum(w, axis=1)[:, None] + eps
+    s = src.astype(np.float64)
+    c = corres.astype(np.float64)
+    ms = np.einsum("bn,bnd->bd", w, s) / ws
+    mc = np.einsum("bn,bnd->bd", w, c) / ws
+    sc = s - ms[:, None]
+    cc = c - mc[:, None]
+    H = np.einsum("bna,bn,bnc->bac", sc, w, cc)
+    B = src.shape[0]
+    if not np.all(np.isfinite(H)):
+        return np.tile(np.eye(3, dtype=np.float32), (B, 1, 1)), np.zeros((B, 3), np.float32)
+    U, S, Vt = np.linalg.svd(H)
+    V = Vt.transpose(0, 2, 1)
+    det = np.linalg.det(np.matmul(V, U.transpose(0, 2, 1)))
+    D = np.zeros((B, 3, 3))
+    D[:, 0, 0] = 1
+    D[:, 1, 1] = 1
+    D[:, 2, 2] = det
+    R = np.matmul(V, np.matmul(D, U.transpose(0, 2, 1)))
+    t = mc - np.einsum("bij,bj->bi", R, ms)
+    return R.astype(np.float32), t.astype(np.float32)
+
+
+def _compose(R_, t_, R, t):
+    """T = T_ @ T_prev on 4x4 homogeneous (models.py:100-110, 120-127)."""
+    Rn = np.matmul(R_.astype(np.float64), R.astype(np.float64))
+    tn = np.einsum("bij,bj->bi", R_.astype(np.float64), t.astype(np.float64)) + t_
+    return Rn.astype(np.float32), tn.astype(np.float32)
+
+
+def _transform(R, t, xyz):
+    """R @ xyz^T + t (models.py:91-92, 113-114)."""
+    return (np.einsum("bij,bnj->bni", R, xyz) + t[:, None, :]).astype(np.float32)
+
+
+def hregnet_forward(sd, src, dst, use_weights=True):
+    """HRegNet.forward, models/HRegNet/models.py:77-148 (eval mode)."""
+    sf = feature_extraction(sd, src, use_weights)
+    df = feature_extraction(sd, dst, use_weights)
+    c3, w3, _ = coarse_reg(sd, "coarse_corres", sf["xyz_3"], sf["desc_3"], df["xyz_3"],
+                           df["desc_3"], sf["sigmas_3"], df["sigmas_3"])
+    R3, t3 = weighted_svd(sf["xyz_3"], c3, w3)
+    x2t = _transform(R3, t3, sf["xyz_2"])
+    c2, w2, _ = fine_reg(sd, "fine_corres_2", x2t, sf["desc_2"], df["xyz_2"], df["desc_2"],
+                         sf["sigmas_2"], df["sigmas_2"])
+    R2_, t2_ = weighted_svd(x2t, c2, w2)
+    R2, t2 = _compose(R2_, t2_, R3, t3)
+    x1t = _transform(R2, t2, sf["xyz_1"])
+    c1, w1, _ = fine_reg(sd, "fine_corres_1", x1t, sf["desc_1"], df["xyz_1"], df["desc_1"],
+                         sf["sigmas_1"], df["sigmas_1"])
+    R1_, t1_ = weighted_svd(x1t, c1, w1)
+    R1, t1 = _compose(R1_, t1_, R2, t2)
+    return dict(src_xyz_corres_3=c3, src_xyz_corres_2=c2, src_xyz_corres_1=c1,
+                src_dst_weights_3=w3, src_dst_weights_2=w2, src_dst_weights_1=w1,
+                rotation=[R3, R2, R1], translation=[t3, t2, t1], src_feats=sf, dst_feats=df)

@@ -1,0 +1,121 @@
+"""ctypes binding of ``libhregnet_amd.so`` (the C ABI in include/hregnet_amd.h).
+
+The HIP library is the product path: there is no CPU or PyTorch fallback.
+If the library is missing or no GPU is visible, every op raises.
+``torch`` is imported first so the process shares PyTorch's HIP runtime
+(libamdhip64.so.7) with the library; tensors pass as raw device pointers and
+work is enqueued on PyTorch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhregnet_amd.so")
+
+HREG_OK = 0
+_ERRORS = {1: "invalid argument", 2: "kernel launch failed", 3: "unsupported shape"}
+
+HREG_EPI_AFFINE = 0
+HREG_EPI_COSINE = 1
+HREG_HEAD_SOFTPLUS = 0
+HREG_HEAD_SIGMOID = 1
+MAX_SEGS = 4
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+
+
+class Seg(ctypes.Structure):
+    _fields_ = [("base", _vp), ("gather", _vp), ("rowscale", _vp), ("batch_stride", _i64),
+                ("ld", _i), ("k0", _i), ("kc", _i), ("row_div", _i)]
+
+
+class Gemm(ctypes.Structure):
+    _fields_ = [("seg", Seg * MAX_SEGS), ("nseg", _i), ("R", _i), ("N", _i), ("K", _i),
+                ("batch", _i), ("ldw", _i), ("w_batch_stride", _i64), ("W", _vp),
+                ("scale", _vp), ("shift", _vp), ("relu", _i), ("epi", _i), ("rnorm", _vp),
+                ("cnorm", _vp), ("rnorm_batch_stride", _i64), ("cnorm_batch_stride", _i64),
+                ("out", _vp), ("ldo", _i), ("out_batch_stride", _i64)]
+
+
+_SIGS = {
+    "hreg_furthest_point_sampling": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_weighted_furthest_point_sampling": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_gather_points": [_i, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "hreg_gather_points_grad": [_i, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "hreg_knn_points": [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_knn_gather": [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
+    "hreg_knn_group": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "hreg_gemm": [ctypes.POINTER(Gemm), _vp],
+    "hreg_attend": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp],
+    "hreg_group_max": [_vp, _i, _i, _i, _i, _vp, _i, _vp],
+    "hreg_head_out": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp],
+    "hreg_row_norms": [_vp, _i, _i, _i, _vp, _vp],
+    "hreg_sim_gather": [_vp, _i, _i, _i, _vp, _i, _vp, _i, _vp],
+    "hreg_pair_feats": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp,
+                        _vp],
+    "hreg_weighted_svd": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_transform_points": [_vp, _vp, _vp, _i, _i, _vp, _vp],
+}
+
+EXPORTS = tuple(_SIGS) + ("hreg_version",)
+
+_lib = None
+
+
+def load(require_gpu: bool = True):
+    """Load the library (and check a GPU is visible unless require_gpu=False)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} not found: build it with `python -m pcd_reg_hregnet_amd.build` "
+                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        L.hreg_version.restype = ctypes.c_char_p
+        L.hreg_version.argtypes = []
+        _lib = L
+    if require_gpu and not torch.cuda.is_available():
+        raise RuntimeError("pcd_reg_hregnet_amd: no GPU visible; the HIP path has no CPU fallback")
+    return _lib
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name: str, *args) -> None:
+    L = load()
+    conv = []
+    for a in args:
+        if isinstance(a, torch.Tensor):
+            conv.append(a.data_ptr())
+        else:
+            conv.append(a)
+    rc = getattr(L, name)(*conv)
+    if rc != HREG_OK:
+        raise RuntimeError(f"{name} failed: {_ERRORS.get(rc, rc)} (code {rc})")
+
+
+def gemm(g: Gemm) -> None:
+    L = load()
+    rc = L.hreg_gemm(ctypes.byref(g), stream_handle())
+    if rc != HREG_OK:
+        raise RuntimeError(f"hreg_gemm failed: {_ERRORS.get(rc, rc)} (code {rc})")

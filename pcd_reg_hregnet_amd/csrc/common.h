@@ -1,0 +1,106 @@
+// common.h -- shared helpers for the HRegNet gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hregnet_amd.h"
+
+#define HREG_WAVE 64
+
+// Launch-check helper: every C-ABI entry returns a status code, never exits
+// (the reference prints and calls exit(-1): furthest_point_sampling_gpu.cu:35-38).
+#define HREG_CHECK_LAUNCH()                                       \
+    do {                                                          \
+        hipError_t _e = hipGetLastError();                        \
+        if (_e != hipSuccess) return HREG_ERR_LAUNCH;             \
+    } while (0)
+
+static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// cuda_utils.h:22-26: block size the reference picks for n points.
+static inline int hreg_opt_n_threads(int work_size) {
+    if (work_size < 1) return 1;
+    const int pow_2 = (int)(__builtin_log((double)work_size) / __builtin_log(2.0));
+    int v = 1 << pow_2;
+    if (v > 1024) v = 1024;
+    if (v < 1) v = 1;
+    return v;
+}
+
+static inline int hreg_ilog2(int v) {
+    int l = 0;
+    while ((1 << (l + 1)) <= v) ++l;
+    return l;
+}
+
+// ---------------------------------------------------------------- device --
+
+// Non-contracted float arithmetic: the whole library builds with
+// -ffp-contract=off; these make the intent explicit where order matters.
+__device__ __forceinline__ float fmul_rn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float fadd_rn(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fsub_rn(float a, float b) { return __fsub_rn(a, b); }
+
+// Squared distance in the reference's order: (dx*dx + dy*dy) + dz*dz, two
+// roundings per term (furthest_point_sampling_gpu.cu:129; pytorch3d knn loop).
+__device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx, float by,
+                                         float bz) {
+    const float dx = fsub_rn(ax, bx), dy = fsub_rn(ay, by), dz = fsub_rn(az, bz);
+    return fadd_rn(fadd_rn(fmul_rn(dx, dx), fmul_rn(dy, dy)), fmul_rn(dz, dz));
+}
+
+// IEEE float -> uint32 with the same total order (negative values included).
+__device__ __forceinline__ uint32_t float_orderable(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float orderable_float(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__device__ __forceinline__ uint32_t bitrev_bits(uint32_t x, int L) {
+    return L == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - L));
+}
+
+// Wave-level LDS hand-off between lanes (rocPRIM's wave_barrier pattern):
+// release fence + wave barrier + acquire fence, so the compiler cannot move
+// one lane's LDS store past another lane's later LDS load.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    const uint32_t lo = __shfl_xor((unsigned)(v & 0xffffffffu), m);
+    const uint32_t hi = __shfl_xor((unsigned)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = shfl_xor_u64(v, m);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ float wave_max_f32(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+    return v;
+}
+
+__device__ __forceinline__ float wave_sum_f32(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fadd_rn(v, __shfl_xor(v, m));
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    return v;
+}

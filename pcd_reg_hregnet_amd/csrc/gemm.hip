@@ -1,0 +1,218 @@
+// gemm.hip -- fp32 MFMA "NT" GEMM with fused BN/ReLU or cosine epilogue.
+//
+// Every 1x1 Conv1d/Conv2d + BatchNorm(eval) + ReLU of the HRegNet forward is
+// out[r][n] = act(scale[n] * sum_k A[r][k] W[n][k] + shift[n]) over point rows
+// r (layers.py:115-130, 183-198, 246-268, 417-431).  fp32 is required: a
+// bf16-scale perturbation flips most level-2 kNN indices, and
+// gfx950 has no xf32, so the contraction runs on v_mfma_f32_32x32x2_f32.
+//
+// The A operand is assembled on the fly from up to four K-segments (a plain
+// row, a row gathered through a kNN index, a per-group row r/k, or a row scaled
+// by an attention weight), so the reference's cat/repeat/knn_gather tensors
+// (layers.py:23-27, 204-206, 364-380, 444-445) are never materialised.
+//
+// Layout: activations are point-major ([rows][channels]) in HBM.  A block
+// computes a BM x BN tile; K is staged through LDS in BK=16 chunks, double
+// buffered with one barrier per chunk.  Inside a chunk lane half h takes
+// k = h*8 + s for MFMA k-step s, so each lane's 8 k-values are contiguous and
+// come out of LDS with two ds_read_b128 (rows padded to 20 floats: the 16
+// rows of a ds_read_b128 lane group hit 16 distinct 16-byte slots).
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 16;
+constexpr int LDS_STRIDE = 20;  // floats per LDS row (16 + 4 pad)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float4 load_a4(const hreg_gemm_t &g, int b, int r, int k) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r >= g.R || k >= g.K) return v;
+#pragma unroll
+    for (int s = 0; s < HREG_MAX_SEGS; ++s) {
+        if (s < g.nseg) {
+            const hreg_seg_t &sg = g.seg[s];
+            if (k >= sg.k0 && k < sg.k0 + sg.kc) {
+                const int row = sg.gather ? sg.gather[r] : r / sg.row_div;
+                const float *p = sg.base + (size_t)b * sg.batch_stride + (size_t)row * sg.ld +
+                                 (k - sg.k0);
+                v = *reinterpret_cast<const float4 *>(p);
+                if (sg.rowscale) {
+                    const float a = sg.rowscale[r];
+                    v.x = fmul_rn(v.x, a); v.y = fmul_rn(v.y, a);
+                    v.z = fmul_rn(v.z, a); v.w = fmul_rn(v.w, a);
+                }
+            }
+        }
+    }
+    return v;
+}
+
+__device__ __forceinline__ float4 load_w4(const hreg_gemm_t &g, int b, int n, int k) {
+    if (n >= g.N || k >= g.K) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float *p = g.W + (size_t)b * g.w_batch_stride + (size_t)n * g.ldw + k;
+    return *reinterpret_cast<const float4 *>(p);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
+    static_assert(WM * WN == 4, "4 waves");
+    constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
+    constexpr int TM = WTM / 32, TN = WTN / 32;  // 32x32 MFMA tiles per wave
+    constexpr int A_LD = BM * 4 / 256;           // float4 loads per thread per chunk
+    constexpr int B_LD = (BN * 4 + 255) / 256;
+
+    __shared__ __attribute__((aligned(16))) float As[2][BM * LDS_STRIDE];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDS_STRIDE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wr = wave / WN, wc = wave % WN;
+    const int b = blockIdx.z;
+    const int r0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int nchunks = (g.K + BK - 1) / BK;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+    float4 ra[A_LD], rb[B_LD];
+    auto gload = [&](int c) {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+            const int e = tid + i * 256;
+            ra[i] = load_a4(g, b, r0 + (e >> 2), c * BK + (e & 3) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) {
+            const int e = tid + i * 256;
+            rb[i] = (e < BN * 4) ? load_w4(g, b, n0 + (e >> 2), c * BK + (e & 3) * 4)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+            const int e = tid + i * 256;
+            *reinterpret_cast<float4 *>(&As[buf][(e >> 2) * LDS_STRIDE + (e & 3) * 4]) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) {
+            const int e = tid + i * 256;
+            if (e < BN * 4)
+                *reinterpret_cast<float4 *>(&Bs[buf][(e >> 2) * LDS_STRIDE + (e & 3) * 4]) = rb[i];
+        }
+    };
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+
+    const int h = lane >> 5, l32 = lane & 31;
+    for (int c = 0; c < nchunks; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nchunks) gload(c + 1);
+        float4 fa[TM][2], fb[TN][2];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const float *p = &As[buf][(wr * WTM + i * 32 + l32) * LDS_STRIDE + h * 8];
+            fa[i][0] = *reinterpret_cast<const float4 *>(p);
+            fa[i][1] = *reinterpret_cast<const float4 *>(p + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const float *p = &Bs[buf][(wc * WTN + j * 32 + l32) * LDS_STRIDE + h * 8];
+            fb[j][0] = *reinterpret_cast<const float4 *>(p);
+            fb[j][1] = *reinterpret_cast<const float4 *>(p + 4);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const float av = s < 4 ? (&fa[i][0].x)[s] : (&fa[i][1].x)[s - 4];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const float bv = s < 4 ? (&fb[j][0].x)[s] : (&fb[j][1].x)[s - 4];
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        if (c + 1 < nchunks) lstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: lane l, reg q -> row (q&3) + 8*(q>>2) + 4*h, col l&31
+    float *out = g.out + (size_t)b * g.out_batch_stride;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wc * WTN + j * 32 + l32;
+        if (n >= g.N) continue;
+        float sc = 1.f, sh = 0.f, cn = 1.f;
+        if (g.epi == HREG_EPI_AFFINE) {
+            if (g.scale) sc = g.scale[n];
+            if (g.shift) sh = g.shift[n];
+        } else {
+            cn = g.cnorm[(size_t)b * g.cnorm_batch_stride + n];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int r = r0 + wr * WTM + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (r < g.R) {
+                    float y = acc[i][j][q];
+                    if (g.epi == HREG_EPI_AFFINE) {
+                        y = fadd_rn(fmul_rn(y, sc), sh);
+                        if (g.relu) y = fmaxf(y, 0.f);
+                    } else {
+                        const float rn = g.rnorm[(size_t)b * g.rnorm_batch_stride + r];
+                        y = y / fadd_rn(fmul_rn(rn, cn), 1e-6f);
+                    }
+                    out[(size_t)r * g.ldo + n] = y;
+                }
+            }
+        }
+    }
+}
+
+bool seg_ok(const hreg_seg_t &s) {
+    if (!s.base || s.ld <= 0 || (s.ld & 3) || (s.k0 & 3) || (s.kc & 3) || s.kc <= 0) return false;
+    if (!s.gather && s.row_div < 1) return false;
+    if (reinterpret_cast<uintptr_t>(s.base) & 15) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
+    if (!gp) return HREG_ERR_INVALID;
+    const hreg_gemm_t &g = *gp;
+    if (g.R < 0 || g.N <= 0 || g.K <= 0 || g.batch < 1 || !g.W || !g.out) return HREG_ERR_INVALID;
+    if (g.nseg < 1 || g.nseg > HREG_MAX_SEGS) return HREG_ERR_INVALID;
+    if ((g.ldw & 3) || g.ldw < g.K || (reinterpret_cast<uintptr_t>(g.W) & 15)) return HREG_ERR_INVALID;
+    if (g.ldo < g.N) return HREG_ERR_INVALID;
+    if (g.epi == HREG_EPI_COSINE && (!g.rnorm || !g.cnorm)) return HREG_ERR_INVALID;
+    for (int s = 0; s < g.nseg; ++s)
+        if (!seg_ok(g.seg[s])) return HREG_ERR_INVALID;
+    if (g.R == 0) return HREG_OK;
+    hipStream_t st = as_stream(stream);
+    if (g.N <= 32) {
+        dim3 grid((g.R + 255) / 256, (g.N + 31) / 32, g.batch);
+        hipLaunchKernelGGL((gemm_nt_kernel<256, 32, 4, 1>), grid, dim3(256), 0, st, g);
+    } else if (g.N <= 64) {
+        dim3 grid((g.R + 255) / 256, (g.N + 63) / 64, g.batch);
+        hipLaunchKernelGGL((gemm_nt_kernel<256, 64, 4, 1>), grid, dim3(256), 0, st, g);
+    } else {
+        dim3 grid((g.R + 127) / 128, (g.N + 127) / 128, g.batch);
+        hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, g);
+    }
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}

@@ -1,0 +1,481 @@
+"""HRegNet forward on the HIP library: weight preparation + launch sequence.
+
+This is the host side of the hot path (models/HRegNet/models.py:77-148).  It
+holds no math of its own: every stage is one or more C-ABI launches
+(include/hregnet_amd.h) on PyTorch's current stream; torch only provides
+device memory.  Activations are point-major ([rows][channels]) in HBM, rows
+ordered (cloud, keypoint, neighbour).  src and dst clouds run through the
+feature extractor together (2B clouds per launch; the reference makes two
+passes, models.py:79-80).
+
+Weight preparation folds eval-mode BatchNorm into a per-channel affine epilogue
+(y = acc * alpha + beta, alpha = gamma / sqrt(var + eps), beta = b - mean * alpha,
+the same fold torch's CPU batch_norm uses), and permutes the input columns of
+the correspondence heads so the GEMM reads one packed 16/12-float small-feature
+segment followed by the two descriptor segments (the sum over channels is
+order-independent up to fp32 rounding).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import Gemm, Seg, call
+
+BN_EPS = 1e-5
+
+# (nsample, k, in_feat, det_channels, desc_channels, desc_dim) per level:
+# models/HRegNet/models.py:14-24
+LEVELS = (
+    (1024, 64, 0, (32, 32, 64), (32, 32, 64), 64),
+    (512, 32, 64, (64, 64, 128), (64, 64, 128), 128),
+    (256, 16, 128, (128, 128, 256), (128, 128, 256), 256),
+)
+K_HEAD = 8  # CoarseReg/FineReg k (models.py:71-73)
+
+
+@dataclass
+class Lin:
+    W: torch.Tensor       # [N][K] contiguous f32
+    alpha: torch.Tensor   # [N]
+    beta: torch.Tensor    # [N]
+    relu: bool = True
+
+    @property
+    def N(self):
+        return self.W.shape[0]
+
+    @property
+    def K(self):
+        return self.W.shape[1]
+
+
+def _bn_fold(sd, pre, bias=None):
+    g = sd[pre + ".weight"].float()
+    b = sd[pre + ".bias"].float()
+    mean = sd[pre + ".running_mean"].float()
+    var = sd[pre + ".running_var"].float()
+    alpha = g * (1.0 / torch.sqrt(var + BN_EPS))
+    if bias is None:
+        beta = b - mean * alpha
+    else:
+        beta = b + (bias.float() - mean) * alpha
+    return alpha.contiguous(), beta.contiguous()
+
+
+def _conv_bn(sd, conv, bn, perm=None):
+    W = sd[conv + ".weight"].float()
+    W = W.reshape(W.shape[0], -1)
+    if perm is not None:
+        W = W[:, perm]
+    bias = sd.get(conv + ".bias")
+    a, b = _bn_fold(sd, bn, bias)
+    return Lin(W.contiguous(), a, b, True)
+
+
+def _stack(sd, pre, n, perm0=None):
+    return [_conv_bn(sd, f"{pre}.{3 * i}", f"{pre}.{3 * i + 1}", perm0 if i == 0 else None)
+            for i in range(n)]
+
+
+def _mlp_head(sd, pre):
+    """mlp1, mlp2 (Conv1d+BN+ReLU) and mlp3 (Conv1d C->1)."""
+    m1 = _conv_bn(sd, pre + ".mlp1.0", pre + ".mlp1.1")
+    m2 = _conv_bn(sd, pre + ".mlp2.0", pre + ".mlp2.1")
+    w3 = sd[pre + ".mlp3.0.weight"].float().reshape(-1).contiguous()
+    b3 = sd[pre + ".mlp3.0.bias"].float().reshape(-1).contiguous()
+    return m1, m2, w3, b3
+
+
+def _perm_coarse(C):
+    """CoarseReg input order (layers.py:364-380) -> [geom10, w2, sims4, desc C, knn_desc C]."""
+    return (list(range(10)) + [10 + 2 * C, 11 + 2 * C] + list(range(12 + 2 * C, 16 + 2 * C))
+            + list(range(10, 10 + C)) + list(range(10 + C, 10 + 2 * C)))
+
+
+def _perm_fine(C):
+    """FineReg input order (layers.py:444-445) -> [geom10, w2, feat C, knn_feat C]."""
+    return (list(range(10)) + [10 + 2 * C, 11 + 2 * C] + list(range(10, 10 + C))
+            + list(range(10 + C, 10 + 2 * C)))
+
+
+class PreparedWeights:
+    """Device-resident folded weights for one HRegNet state dict."""
+
+    def __init__(self, sd: dict, device):
+        # fold on the host in fp32, then move the folded tensors to the device
+        sd = {k: v.detach().to("cpu", torch.float32) if v.is_floating_point() else v
+              for k, v in sd.items()}
+        fe = "feature_extraction."
+        self.det, self.det_head, self.desc, self.desc_mlp = [], [], [], []
+        for lvl in range(3):
+            d = f"{fe}detector_{lvl + 1}"
+            self.det.append(_stack(sd, d + ".convs", 3))
+            self.det_head.append(_mlp_head(sd, d))
+            e = f"{fe}desc_extractor_{lvl + 1}"
+            self.desc.append(_stack(sd, e + ".convs", 3))
+            self.desc_mlp.append([_conv_bn(sd, e + ".mlp1.0", e + ".mlp1.1"),
+                                  _conv_bn(sd, e + ".mlp2.0", e + ".mlp2.1")])
+        C = 256
+        self.coarse_convs1 = _stack(sd, "coarse_corres.convs_1", 3, _perm_coarse(C))
+        self.coarse_convs2 = _stack(sd, "coarse_corres.convs_2", 3)
+        self.coarse_head = _mlp_head(sd, "coarse_corres")
+        self.fine = {}
+        for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64)):
+            self.fine[name] = (_stack(sd, name + ".convs_1", 3, _perm_fine(C)), _mlp_head(sd, name))
+        for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
+                     "coarse_head", "fine"):
+            setattr(self, attr, _to_device(getattr(self, attr), device))
+
+
+def _to_device(x, device):
+    if isinstance(x, torch.Tensor):
+        return x.to(device).contiguous()
+    if isinstance(x, Lin):
+        return Lin(_to_device(x.W, device), _to_device(x.alpha, device),
+                   _to_device(x.beta, device), x.relu)
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_device(v, device) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_device(v, device) for k, v in x.items()}
+    return x
+
+
+# ---------------------------------------------------------------- launchers
+
+def _seg(base, k0, kc, ld=None, gather=None, rowscale=None, row_div=1, batch_stride=0):
+    s = Seg()
+    s.base = base.data_ptr()
+    s.gather = gather.data_ptr() if gather is not None else None
+    s.rowscale = rowscale.data_ptr() if rowscale is not None else None
+    s.batch_stride = batch_stride
+    s.ld = base.shape[-1] if ld is None else ld
+    s.k0, s.kc, s.row_div = k0, kc, row_div
+    return s
+
+
+def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None):
+    """out[R][N] = act(alpha * (A @ W^T) + beta), A assembled from segs."""
+    if out is None:
+        out = torch.empty((R, lin.N), device=lin.W.device, dtype=torch.float32)
+    g = Gemm()
+    for i, s in enumerate(segs):
+        g.seg[i] = s
+    g.nseg = len(segs)
+    g.R, g.N, g.K = R, lin.N, lin.K
+    g.batch = 1
+    g.ldw = lin.K
+    g.w_batch_stride = 0
+    g.W = lin.W.data_ptr()
+    g.scale = lin.alpha.data_ptr()
+    g.shift = lin.beta.data_ptr()
+    g.relu = 1 if lin.relu else 0
+    g.epi = _lib.HREG_EPI_AFFINE
+    g.out = out.data_ptr()
+    g.ldo = out.shape[-1]
+    g.out_batch_stride = 0
+    _lib.gemm(g)
+    return out
+
+
+def cosine_gemm(a, b, na, nb_, nb: int, n1: int, n2: int, C: int, out):
+    """S[b][i][j] = <a_i, b_j> / (|a_i||b_j| + 1e-6) per pair (layers.py:29-41)."""
+    g = Gemm()
+    g.seg[0] = _seg(a, 0, C, ld=C, batch_stride=n1 * C)
+    g.nseg = 1
+    g.R, g.N, g.K = n1, n2, C
+    g.batch = nb
+    g.ldw = C
+    g.w_batch_stride = n2 * C
+    g.W = b.data_ptr()
+    g.relu = 0
+    g.epi = _lib.HREG_EPI_COSINE
+    g.rnorm = na.data_ptr()
+    g.cnorm = nb_.data_ptr()
+    g.rnorm_batch_stride = n1
+    g.cnorm_batch_stride = n2
+    g.out = out.data_ptr()
+    g.ldo = n2
+    g.out_batch_stride = n1 * n2
+    _lib.gemm(g)
+    return out
+
+
+def _stream():
+    return _lib.stream_handle()
+
+
+def _empty(*shape, dtype=torch.float32, device):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+def fps(xyz, npoint, weights=None, want_idx=True):
+    nb, n, _ = xyz.shape
+    dev = xyz.device
+    idx = _empty(nb, npoint, dtype=torch.int32, device=dev)
+    sampled = _empty(nb, npoint, 3, device=dev)
+    temp = _empty(nb, n, device=dev) if n > 16384 else None
+    if weights is None:
+        call("hreg_furthest_point_sampling", nb, n, npoint, xyz, temp, idx, sampled, _stream())
+    else:
+        call("hreg_weighted_furthest_point_sampling", nb, n, npoint, xyz, weights, temp, idx,
+             sampled, _stream())
+    return idx, sampled
+
+
+def head_out(x, C, nclouds, rows, w3, b3, mode, want_weights=False):
+    dev = x.device
+    out = _empty(nclouds * rows, device=dev)
+    wout = _empty(nclouds * rows, device=dev) if want_weights else None
+    call("hreg_head_out", x, C, x.shape[-1], nclouds, rows, w3, b3, mode, out, wout, _stream())
+    return out, wout
+
+
+def attend(logits, G, k, vals=None, vgather=None, xyz_rows=None, want_attw=False):
+    dev = logits.device
+    C = logits.shape[-1]
+    attw = _empty(G * k, device=dev) if want_attw else None
+    att = None
+    Cv = 0
+    if vals is not None:
+        Cv = vals.shape[-1]
+        att = _empty(G, Cv, device=dev)
+    kp = _empty(G, 3, device=dev) if xyz_rows is not None else None
+    call("hreg_attend", logits, C, C, G, k, attw, vals, vgather, Cv, Cv, att, Cv, xyz_rows, kp,
+         _stream())
+    return attw, att, kp
+
+
+def group_max(x, G, k):
+    C = x.shape[-1]
+    out = _empty(G, C, device=x.device)
+    call("hreg_group_max", x, G, k, C, C, out, C, _stream())
+    return out
+
+
+def row_norms(x):
+    out = _empty(x.shape[0], device=x.device)
+    call("hreg_row_norms", x, x.shape[0], x.shape[1], x.shape[1], out, _stream())
+    return out
+
+
+def knn_group(q, p, k):
+    """q [nb,m,3], p [nb,n,3] -> gidx [nb*m*k] int32 (global rows of p), geom [nb*m*k,4], knn_xyz."""
+    nb, m, _ = q.shape
+    n = p.shape[1]
+    dev = q.device
+    R = nb * m * k
+    gidx = _empty(R, dtype=torch.int32, device=dev)
+    geom = _empty(R, 4, device=dev)
+    kx = _empty(R, 3, device=dev)
+    call("hreg_knn_group", q, p, nb, m, n, k, gidx, geom, kx, _stream())
+    return gidx, geom, kx
+
+
+def knn_idx32(p1, p2, k):
+    b, n1, d = p1.shape
+    n2 = p2.shape[1]
+    idx = _empty(b, n1, k, dtype=torch.int32, device=p1.device)
+    call("hreg_knn_points", p1, p2, b, n1, n2, d, k, None, None, idx, None, _stream())
+    return idx
+
+
+# ------------------------------------------------------------------ stages
+
+def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights):
+    """KeypointDetector (layers.py:134-165) + DescExtractor (layers.py:200-209) for one level.
+
+    xyz [nb,n,3]; feats [nb*n, Cf] point-major or None; weights [nb*n] or None.
+    Returns keypoints [nb,M,3], sigmas [nb*M], att_feat [nb*M,Cdet], desc [nb*M,Cdesc],
+    next weights [nb*M] (or None) and the FPS indices [nb,M].
+    """
+    M, k, Cf, _, _, _ = LEVELS[lvl]
+    nb, n, _ = xyz.shape
+    G = nb * M
+    R = G * k
+    idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n))
+    gidx, geom, kx = knn_group(sampled, xyz, k)
+    segs = [_seg(geom, 0, 4)]
+    if feats is not None:
+        segs.append(_seg(feats, 4, Cf, gather=gidx))
+    # detector convs (layers.py:150)
+    h = gemm(segs, P.det[lvl][0], R)
+    h = gemm([_seg(h, 0, h.shape[1])], P.det[lvl][1], R)
+    emb = gemm([_seg(h, 0, h.shape[1])], P.det[lvl][2], R)
+    attw, att_feat, kp = attend(emb, G, k, vals=emb, xyz_rows=kx, want_attw=True)
+    m1, m2, w3, b3 = P.det_head[lvl]
+    s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)
+    s = gemm([_seg(s, 0, s.shape[1])], m2, G)
+    sig, wnext = head_out(s, s.shape[1], nb, M, w3, b3, _lib.HREG_HEAD_SOFTPLUS, want_weights=True)
+    # descriptor (layers.py:200-209)
+    x = gemm(segs, P.desc[lvl][0], R)
+    x = gemm([_seg(x, 0, x.shape[1])], P.desc[lvl][1], R)
+    x1 = gemm([_seg(x, 0, x.shape[1])], P.desc[lvl][2], R)
+    C1 = x1.shape[1]
+    x2 = group_max(x1, G, k)
+    Cd = emb.shape[1]
+    y = gemm([_seg(x2, 0, C1, row_div=k), _seg(x1, C1, C1),
+              _seg(emb, 2 * C1, Cd, rowscale=attw)], P.desc_mlp[lvl][0], R)
+    y = gemm([_seg(y, 0, y.shape[1])], P.desc_mlp[lvl][1], R)
+    desc = group_max(y, G, k)
+    return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
+
+
+def feature_extraction(P: PreparedWeights, points, use_weights=True):
+    """HierFeatureExtraction.forward (models.py:26-58) over nb clouds at once."""
+    nb = points.shape[0]
+    out = {}
+    xyz, feats, w = points, None, None
+    for lvl in range(3):
+        kp, sig, att, desc, wnext, idx = keypoint_level(P, lvl, xyz, feats, w)
+        out[f"xyz_{lvl + 1}"] = kp
+        out[f"sigmas_{lvl + 1}"] = sig
+        out[f"desc_{lvl + 1}"] = desc
+        out[f"fps_idx_{lvl + 1}"] = idx
+        xyz, feats = kp, att
+        w = wnext if use_weights else None
+    return out
+
+
+def _mlp_weights(x, head, G, nclouds, rows):
+    m1, m2, w3, b3 = head
+    s = gemm([_seg(x, 0, x.shape[1])], m1, G)
+    s = gemm([_seg(s, 0, s.shape[1])], m2, G)
+    w, _ = head_out(s, s.shape[1], nclouds, rows, w3, b3, _lib.HREG_HEAD_SIGMOID)
+    return w
+
+
+def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
+    """CoarseReg.forward (layers.py:273-396); xyz3 [2B,256,3], desc3 [2B*256,256], sig3 [2B*256]."""
+    dev = xyz3.device
+    k = K_HEAD
+    N1 = xyz3.shape[1]
+    C = desc3.shape[1]
+    s_desc, d_desc = desc3[:B * N1], desc3[B * N1:]
+    s_xyz, d_xyz = xyz3[:B], xyz3[B:]
+    s_sig, d_sig = sig3[:B * N1], sig3[B * N1:]
+    # desc-space kNN (layers.py:278)
+    kidx = knn_idx32(s_desc.view(B, N1, C), d_desc.view(B, N1, C), k)
+    # original similarity (layers.py:290-313)
+    norms = row_norms(desc3)
+    S = _empty(B, N1, N1, device=dev)
+    cosine_gemm(s_desc, d_desc, norms[:B * N1], norms[B * N1:], B, N1, N1, C, S)
+    sims_a = _empty(B * N1 * k, 2, device=dev)
+    call("hreg_sim_gather", S, B, N1, N1, kidx, k, sims_a, 2, _stream())
+    # neighbour-aware descriptors for src and dst together (layers.py:315-337)
+    gself, geom_self, _ = knn_group(xyz3, xyz3, k)
+    G2 = 2 * B * N1
+    R2 = G2 * k
+    segs = [_seg(desc3, 0, C, gather=gself), _seg(geom_self, C, 4)]
+    h = gemm(segs, P.coarse_convs2[0], R2)
+    h = gemm([_seg(h, 0, h.shape[1])], P.coarse_convs2[1], R2)
+    h = gemm([_seg(h, 0, h.shape[1])], P.coarse_convs2[2], R2)
+    _, nbr, _ = attend(h, G2, k, vals=desc3, vgather=gself)
+    nnorm = row_norms(nbr)
+    cosine_gemm(nbr[:B * N1], nbr[B * N1:], nnorm[:B * N1], nnorm[B * N1:], B, N1, N1, C, S)
+    sims_b = _empty(B * N1 * k, 2, device=dev)
+    call("hreg_sim_gather", S, B, N1, N1, kidx, k, sims_b, 2, _stream())
+    # correspondence features + convs_1 (layers.py:364-384)
+    R = B * N1 * k
+    small = _empty(R, 16, device=dev)
+    kx = _empty(R, 3, device=dev)
+    gidx = _empty(R, dtype=torch.int32, device=dev)
+    call("hreg_pair_feats", s_xyz, d_xyz, s_sig, d_sig, kidx, B, N1, N1, k, sims_a, sims_b,
+         small, 16, kx, gidx, _stream())
+    segs = [_seg(small, 0, 16), _seg(s_desc, 16, C, row_div=k), _seg(d_desc, 16 + C, C, gather=gidx)]
+    f = gemm(segs, P.coarse_convs1[0], R)
+    f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[1], R)
+    f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[2], R)
+    _, att, corres = attend(f, B * N1, k, vals=f, xyz_rows=kx)
+    w = _mlp_weights(att, P.coarse_head, B * N1, B, N1)
+    return corres.view(B, N1, 3), w.view(B, N1)
+
+
+def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w):
+    """FineReg.forward (layers.py:433-454); xyz [B,N,3], desc [B*N,C], w [B*N]."""
+    dev = src_xyz.device
+    k = K_HEAD
+    N = src_xyz.shape[1]
+    C = src_desc.shape[1]
+    convs, head = P.fine[name]
+    kidx = knn_idx32(src_xyz, dst_xyz, k)
+    R = B * N * k
+    small = _empty(R, 12, device=dev)
+    kx = _empty(R, 3, device=dev)
+    gidx = _empty(R, dtype=torch.int32, device=dev)
+    call("hreg_pair_feats", src_xyz, dst_xyz, src_w, dst_w, kidx, B, N, N, k, None, None, small, 12,
+         kx, gidx, _stream())
+    segs = [_seg(small, 0, 12), _seg(src_desc, 12, C, row_div=k), _seg(dst_desc, 12 + C, C, gather=gidx)]
+    f = gemm(segs, convs[0], R)
+    f = gemm([_seg(f, 0, f.shape[1])], convs[1], R)
+    f = gemm([_seg(f, 0, f.shape[1])], convs[2], R)
+    _, att, corres = attend(f, B * N, k, vals=f, xyz_rows=kx)
+    w = _mlp_weights(att, head, B * N, B, N)
+    return corres.view(B, N, 3), w.view(B, N)
+
+
+def weighted_svd(src, corres, w, prev=None):
+    """WeightedSVDHead (layers.py:469-504) (+ T = T_ @ T_prev, models.py:100-127)."""
+    B, n, _ = src.shape
+    dev = src.device
+    R_ = _empty(B, 3, 3, device=dev)
+    t_ = _empty(B, 3, device=dev)
+    R = _empty(B, 3, 3, device=dev)
+    t = _empty(B, 3, device=dev)
+    pR, pt = (prev if prev is not None else (None, None))
+    call("hreg_weighted_svd", src, corres, w, B, n, pR, pt, R_, t_, R, t, _stream())
+    return R_, t_, R, t
+
+
+def transform(xyz, R, t):
+    B, n, _ = xyz.shape
+    out = torch.empty_like(xyz)
+    call("hreg_transform_points", xyz, R, t, B, n, out, _stream())
+    return out
+
+
+def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True):
+    """HRegNet.forward (models/HRegNet/models.py:77-148), eval mode."""
+    B, N, _ = src.shape
+    pts = torch.cat([src, dst], 0).contiguous()
+    fe = feature_extraction(P, pts, use_weights)
+
+    def split(t, rows):
+        return t[:B * rows], t[B * rows:]
+
+    M = [lv[0] for lv in LEVELS]
+    xyz = [fe[f"xyz_{i + 1}"] for i in range(3)]
+    sig = [fe[f"sigmas_{i + 1}"] for i in range(3)]
+    desc = [fe[f"desc_{i + 1}"] for i in range(3)]
+    c3, w3 = coarse_reg(P, B, xyz[2], desc[2], sig[2])
+    _, _, R3, t3 = weighted_svd(xyz[2][:B], c3, w3)
+    x2t = transform(xyz[1][:B], R3, t3)
+    sd2, dd2 = split(desc[1], M[1])
+    ss2, ds2 = split(sig[1], M[1])
+    c2, w2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2)
+    _, _, R2, t2 = weighted_svd(x2t, c2, w2, prev=(R3, t3))
+    x1t = transform(xyz[0][:B], R2, t2)
+    sd1, dd1 = split(desc[0], M[0])
+    ss1, ds1 = split(sig[0], M[0])
+    c1, w1 = fine_reg(P, "fine_corres_1", B, x1t, sd1, xyz[0][B:], dd1, ss1, ds1)
+    _, _, R1, t1 = weighted_svd(x1t, c1, w1, prev=(R2, t2))
+
+    def feats(part):
+        sl = slice(0, B) if part == 0 else slice(B, 2 * B)
+        d = {}
+        for i in range(3):
+            m = M[i]
+            d[f"xyz_{i + 1}"] = xyz[i][sl]
+            d[f"sigmas_{i + 1}"] = sig[i].view(2 * B, m)[sl]
+            d[f"desc_{i + 1}"] = desc[i].view(2 * B, m, -1)[sl].transpose(1, 2)
+        return d
+
+    return {
+        "src_xyz_corres_3": c3, "src_xyz_corres_2": c2, "src_xyz_corres_1": c1,
+        "src_dst_weights_3": w3, "src_dst_weights_2": w2, "src_dst_weights_1": w1,
+        "rotation": [R3, R2, R1], "translation": [t3, t2, t1],
+        "src_feats": feats(0), "dst_feats": feats(1),
+        "_fps_idx": [fe[f"fps_idx_{i + 1}"] for i in range(3)],
+    }

@@ -1,0 +1,277 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Runs in the build container only (the GPU box has no /root/reference).  It
+imports the reference's own Python model code (models/HRegNet/*.py,
+models/utils.py) unmodified from /root/reference, with shims for what the
+container lacks:
+
+* ``point_utils_cuda`` (the unbuilt CUDA extension): a literal numpy
+  emulation of furthest_point_sampling_gpu.cu -- bs = opt_n_threads(n)
+  virtual threads each keep the FIRST strictly larger d2 over k = t, t+bs, ...
+  (.cu:122-134), then the shared-memory tree with __update keeping the lower
+  slot on ties (.cu:75-80, 140-199) -- plus gather_points (.cu:7-21).  This is
+  written independently of oracle/hregnet_oracle.c so each pins the other.
+* ``pytorch3d`` (not installed, no network): knn_points = brute force with the
+  distance summed sequentially over d, ordered by (dist, idx); knn_gather =
+  indexing.  pytorch3d's own tie order is an unstable sort (parity unpinned).
+* ``.cuda()`` -> identity; torch.cuda.IntTensor/FloatTensor -> CPU tensors.
+
+Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
+(torch.load(weights_only=True)), saved as tests/golden/nusc_feats.npz; heads
+from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
+from the snapshot, .MISSING_LARGE_BLOBS:2-4).
+
+Usage: python tests/golden/make_golden.py   (a few minutes on 8 CPUs)
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = "/root/reference"
+sys.dont_write_bytecode = True
+sys.path.insert(0, REPO)
+
+
+# ------------------------------------------------------------------ shims
+def opt_n_threads(n: int) -> int:
+    p = int(math.log(float(n)) / math.log(2.0))
+    return max(min(1 << p, 1024), 1)
+
+
+def fps_literal(xyz: np.ndarray, m: int, w: np.ndarray | None = None) -> np.ndarray:
+    """Thread-level emulation of (weighted_)furthest_point_sampling_kernel, one cloud."""
+    n = xyz.shape[0]
+    bs = opt_n_threads(n)
+    rows = -(-n // bs)
+    pad = rows * bs - n
+    X = np.concatenate([xyz.astype(np.float32), np.zeros((pad, 3), np.float32)])
+    W = None if w is None else np.concatenate([w.astype(np.float32), np.ones(pad, np.float32)])
+    valid = np.arange(rows * bs) < n
+    temp = np.full(rows * bs, 1e10, np.float32)
+    kidx = np.arange(rows * bs).reshape(rows, bs)
+    out = np.zeros(m, np.int32)
+    old = 0
+    for j in range(1, m):
+        x1, y1, z1 = X[old]
+        dx = X[:, 0] - x1
+        dy = X[:, 1] - y1
+        dz = X[:, 2] - z1
+        d = (dx * dx + dy * dy) + dz * dz
+        if W is not None:
+            d = W * d
+        d2 = np.fmin(d, temp).astype(np.float32)
+        temp = np.where(valid, d2, temp)
+        d2 = np.where(valid, d2, -np.inf).reshape(rows, bs)
+        # per thread: first occurrence of the maximum if it is > -1, else (-1, 0)
+        am = np.argmax(d2, axis=0)
+        best = d2[am, np.arange(bs)]
+        besti = kidx[am, np.arange(bs)]
+        ok = best > -1.0
+        dists = np.where(ok, best, np.float32(-1.0)).astype(np.float32)
+        dists_i = np.where(ok, besti, 0)
+        s = bs // 2
+        while s >= 1:
+            v1, v2 = dists[:s], dists[s:2 * s]
+            i1, i2 = dists_i[:s], dists_i[s:2 * s]
+            dists_i = np.where(v2 > v1, i2, i1)
+            dists = np.maximum(v1, v2)
+            s //= 2
+        old = int(dists_i[0])
+        out[j] = old
+    return out
+
+
+class _PointUtils(types.ModuleType):
+    calls: list
+
+    def furthest_point_sampling_wrapper(self, b, n, m, points, temp, idx):
+        P = points.detach().cpu().numpy()
+        for c in range(b):
+            idx[c] = torch.from_numpy(fps_literal(P[c], m))
+        self.calls.append(("fps", idx.clone()))
+        return 1
+
+    def weighted_furthest_point_sampling_wrapper(self, b, n, m, points, weights, temp, idx):
+        P = points.detach().cpu().numpy()
+        Wt = weights.detach().cpu().numpy()
+        for c in range(b):
+            idx[c] = torch.from_numpy(fps_literal(P[c], m, Wt[c]))
+        self.calls.append(("wfps", idx.clone()))
+        return 1
+
+    def gather_points_wrapper(self, b, c, n, npoints, points, idx, out):
+        out.copy_(torch.gather(points, 2, idx.long().unsqueeze(1).expand(b, c, npoints)))
+        return 1
+
+    def gather_points_grad_wrapper(self, b, c, n, npoints, grad_out, idx, grad_points):
+        grad_points.scatter_add_(2, idx.long().unsqueeze(1).expand(b, c, npoints), grad_out)
+        return 1
+
+
+def knn_brute(p1: torch.Tensor, p2: torch.Tensor, K: int):
+    """sum_d (p1_d - p2_d)^2 sequentially over d; stable ascending sort -> (dist, idx)."""
+    d = torch.zeros(p1.shape[0], p1.shape[1], p2.shape[1], dtype=torch.float32)
+    for e in range(p1.shape[2]):
+        diff = p1[:, :, None, e] - p2[:, None, :, e]
+        d = d + diff * diff
+    dist, idx = torch.sort(d, dim=2, stable=True)
+    return dist[:, :, :K].contiguous(), idx[:, :, :K].contiguous()
+
+
+def knn_points(p1, p2, lengths1=None, lengths2=None, norm=2, K=1, version=-1, return_nn=False,
+               return_sorted=True):
+    dist, idx = knn_brute(p1.detach().float(), p2.detach().float(), K)
+    nn = knn_gather(p2, idx) if return_nn else None
+    return dist, idx, nn
+
+
+def knn_gather(x, idx, lengths=None):
+    B = x.shape[0]
+    return x[torch.arange(B)[:, None, None], idx]
+
+
+def install_shims():
+    pu = _PointUtils("point_utils_cuda")
+    pu.calls = []
+    sys.modules["point_utils_cuda"] = pu
+    p3d = types.ModuleType("pytorch3d")
+    ops = types.ModuleType("pytorch3d.ops")
+    ops.knn_points = knn_points
+    ops.knn_gather = knn_gather
+    loss = types.ModuleType("pytorch3d.loss")
+    loss.chamfer_distance = lambda *a, **k: (_ for _ in ()).throw(NotImplementedError())
+    tr = types.ModuleType("pytorch3d.transforms")
+    tr.matrix_to_euler_angles = lambda *a, **k: (_ for _ in ()).throw(NotImplementedError())
+    p3d.ops, p3d.loss, p3d.transforms = ops, loss, tr
+    sys.modules.update({"pytorch3d": p3d, "pytorch3d.ops": ops, "pytorch3d.loss": loss,
+                        "pytorch3d.transforms": tr})
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    torch.cuda.IntTensor = lambda *s: torch.empty(*s, dtype=torch.int32)
+    torch.cuda.FloatTensor = lambda *s: torch.empty(*s, dtype=torch.float32)
+    # a bare package for /root/reference/models: skips models/__init__.py, which
+    # eagerly imports V5/V6 (spconv/flash-attn are absent)
+    pkg = types.ModuleType("models")
+    pkg.__path__ = [os.path.join(REF, "models")]
+    sys.modules["models"] = pkg
+    sys.path.insert(0, REF)
+    return pu
+
+
+# ---------------------------------------------------------------- fixtures
+def ops_fixtures(rng: np.random.Generator) -> dict:
+    out = {}
+    # FPS: uniform, tie-heavy (grid-quantised + duplicates), non-power-of-two, m >= n
+    cases = []
+    x = rng.uniform(-40, 40, (2, 4096, 3)).astype(np.float32)
+    cases.append(("uniform4096", x, 512, None))
+    g = np.round(rng.uniform(-4, 4, (2, 2048, 3))).astype(np.float32)  # many equal distances
+    g[:, 1500:] = g[:, :548]  # exact duplicates
+    cases.append(("ties2048", g, 300, None))
+    cases.append(("n1000", rng.uniform(-1, 1, (1, 1000, 3)).astype(np.float32), 257, None))
+    cases.append(("n100_m100", rng.uniform(-1, 1, (1, 100, 3)).astype(np.float32), 100, None))
+    cases.append(("n40_m60", rng.uniform(-1, 1, (1, 40, 3)).astype(np.float32), 60, None))
+    cases.append(("l1_16384", rng.uniform(-40, 40, (1, 16384, 3)).astype(np.float32), 1024, None))
+    w = rng.uniform(0.2, 3.0, (2, 1024)).astype(np.float32)
+    cases.append(("w1024", rng.uniform(-40, 40, (2, 1024, 3)).astype(np.float32), 512, w))
+    w2 = np.ones((2, 512), np.float32)
+    w2[:, ::3] = 2.0
+    cases.append(("wties512", np.round(rng.uniform(-3, 3, (2, 512, 3))).astype(np.float32), 256, w2))
+    for name, xyz, m, wt in cases:
+        idx = np.stack([fps_literal(xyz[c], m, None if wt is None else wt[c])
+                        for c in range(xyz.shape[0])])
+        out[f"fps_{name}_xyz"] = xyz
+        out[f"fps_{name}_m"] = np.array(m)
+        if wt is not None:
+            out[f"fps_{name}_w"] = wt
+        out[f"fps_{name}_idx"] = idx
+    # kNN: xyz K=64 / 8, ties from duplicates, desc-space D=256 K=8, K == n2
+    kcases = [
+        ("xyz_k64", rng.uniform(-40, 40, (2, 256, 3)), rng.uniform(-40, 40, (2, 4096, 3)), 64),
+        ("xyz_ties_k16", np.round(rng.uniform(-3, 3, (1, 128, 3))), np.round(rng.uniform(-3, 3, (1, 700, 3))), 16),
+        ("desc_k8", rng.normal(0, 1, (2, 256, 256)), rng.normal(0, 1, (2, 256, 256)), 8),
+        ("k_eq_n", rng.uniform(-1, 1, (1, 50, 3)), rng.uniform(-1, 1, (1, 8, 3)), 8),
+    ]
+    for name, p1, p2, K in kcases:
+        p1 = p1.astype(np.float32)
+        p2 = p2.astype(np.float32)
+        d, i = knn_brute(torch.from_numpy(p1), torch.from_numpy(p2), K)
+        out[f"knn_{name}_p1"] = p1
+        out[f"knn_{name}_p2"] = p2
+        out[f"knn_{name}_dist"] = d.numpy()
+        out[f"knn_{name}_idx"] = i.numpy().astype(np.int64)
+    return out
+
+
+class _Args:
+    use_fps = True
+    use_weights = True
+    freeze_detector = False
+    freeze_feats = False
+
+
+def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict) -> dict:
+    net = HRegNet(_Args())
+    net.load_state_dict(sd)
+    net.eval()
+    pu.calls.clear()
+    with torch.no_grad():
+        r = net(torch.from_numpy(src), torch.from_numpy(dst))
+    out = {"src": src, "dst": dst}
+    for i, (R, t) in enumerate(zip(r["rotation"], r["translation"])):
+        out[f"R{3 - i}"] = R.numpy()
+        out[f"t{3 - i}"] = t.numpy()
+    for lv in (1, 2, 3):
+        out[f"corres_{lv}"] = r[f"src_xyz_corres_{lv}"].numpy()
+        out[f"weights_{lv}"] = r[f"src_dst_weights_{lv}"].numpy()
+        for part in ("src", "dst"):
+            f = r[f"{part}_feats"]
+            out[f"{part}_xyz_{lv}"] = f[f"xyz_{lv}"].numpy()
+            out[f"{part}_sigmas_{lv}"] = f[f"sigmas_{lv}"].numpy()
+            out[f"{part}_desc_{lv}"] = f[f"desc_{lv}"].numpy()
+    # FPS calls in order: src L1, L2, L3, dst L1, L2, L3
+    names = ["src_fps_1", "src_fps_2", "src_fps_3", "dst_fps_1", "dst_fps_2", "dst_fps_3"]
+    for name, (_, idx) in zip(names, pu.calls):
+        out[name] = idx.numpy()
+    return out
+
+
+def main():
+    pu = install_shims()
+    from models.HRegNet.models import HRegNet  # noqa: E402  (reference code)
+    from pcd_reg_hregnet_amd import synthetic, weights
+
+    feats = torch.load(os.path.join(REF, "ckpt/pretrained/nusc_feats.pth"), map_location="cpu",
+                       weights_only=True)
+    np.savez_compressed(os.path.join(HERE, "nusc_feats.npz"),
+                        **{k: v.numpy() for k, v in feats.items()})
+    template = HRegNet(_Args()).state_dict()
+    sd = weights.make_state_dict(template, seed=0, pretrained_feats=True)
+
+    rng = np.random.default_rng(1234)
+    np.savez_compressed(os.path.join(HERE, "ops.npz"), **ops_fixtures(rng))
+    print("ops.npz written", flush=True)
+
+    # config 1 (BASELINE.json configs[0]): B=1, 2 x 16384 uniform cube, seed 1
+    src, dst = synthetic.cube_batch(1, 16384, seed=1)
+    np.savez_compressed(os.path.join(HERE, "hregnet_cube_b1_n16384.npz"),
+                        **model_fixture(HRegNet, pu, src, dst, sd))
+    print("cube fixture written", flush=True)
+    # LiDAR-shaped pairs, B=2, N=4096
+    s, d, Rg, tg = synthetic.lidar_batch(2, 4096, seed0=0)
+    fx = model_fixture(HRegNet, pu, s, d, sd)
+    fx["R_gt"], fx["t_gt"] = Rg, tg
+    np.savez_compressed(os.path.join(HERE, "hregnet_lidar_b2_n4096.npz"), **fx)
+    print("lidar fixture written", flush=True)
+
+
+if __name__ == "__main__":
+    main()

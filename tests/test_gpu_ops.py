@@ -1,0 +1,270 @@
+"""GPU parity of every C-ABI op against the oracle / reference fixtures.
+
+Index outputs (FPS, kNN) must be bit-exact; float outputs are compared with a
+plain fp32 reference (numpy / torch CPU) at the tolerance stated per test.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import load_npz
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+OPS = load_npz("ops.npz")
+FPS_CASES = sorted({k[4:-4] for k in OPS if k.startswith("fps_") and k.endswith("_idx")})
+KNN_CASES = sorted({k[4:-4] for k in OPS if k.startswith("knn_") and k.endswith("_idx")})
+
+
+def dev(x, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    return t if dtype is None else t.to(dtype)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from pcd_reg_hregnet_amd import _lib as L
+    L.load()
+    yield
+
+
+@pytest.mark.parametrize("case", FPS_CASES)
+def test_fps_vs_reference_fixture(case):
+    from pcd_reg_hregnet_amd.utils import furthest_point_sample, weighted_furthest_point_sample
+    xyz = OPS[f"fps_{case}_xyz"]
+    m = int(OPS[f"fps_{case}_m"])
+    w = OPS.get(f"fps_{case}_w")
+    if w is None:
+        got = furthest_point_sample(dev(xyz), m)
+    else:
+        got = weighted_furthest_point_sample(dev(xyz), dev(w), m)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy(), OPS[f"fps_{case}_idx"])
+
+
+@pytest.mark.parametrize("n,m,weighted", [(16384, 1024, False), (1024, 512, True), (512, 256, True),
+                                          (2048, 700, False), (20000, 64, False), (20000, 64, True),
+                                          (3, 5, False), (1, 4, False), (777, 300, True)])
+def test_fps_vs_oracle(n, m, weighted):
+    from pcd_reg_hregnet_amd import point_utils_cuda as pu
+    rng = np.random.default_rng(n * 7 + m)
+    B = 3
+    xyz = rng.uniform(-40, 40, (B, n, 3)).astype(np.float32)
+    xyz[:, n // 2:] = np.round(xyz[:, n // 2:])  # ties
+    w = rng.uniform(0.1, 2.0, (B, n)).astype(np.float32) if weighted else None
+    idx = torch.empty((B, m), dtype=torch.int32, device="cuda")
+    temp = torch.full((B, n), 1e10, device="cuda")
+    if weighted:
+        pu.weighted_furthest_point_sampling_wrapper(B, n, m, dev(xyz), dev(w), temp, idx)
+    else:
+        pu.furthest_point_sampling_wrapper(B, n, m, dev(xyz), temp, idx)
+    ref = oracle.fps(xyz, m, w)
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+
+
+def test_fps_zero_points_requested():
+    from pcd_reg_hregnet_amd import point_utils_cuda as pu
+    idx = torch.full((2, 1), -7, dtype=torch.int32, device="cuda")
+    x = torch.zeros((2, 10, 3), device="cuda")
+    pu.furthest_point_sampling_wrapper(2, 10, 0, x, torch.zeros((2, 10), device="cuda"), idx)
+    torch.cuda.synchronize()
+    assert (idx.cpu() == -7).all()  # m <= 0: kernel returns without writing (.cu:92)
+
+
+@pytest.mark.parametrize("case", KNN_CASES)
+def test_knn_vs_reference_fixture(case):
+    from pcd_reg_hregnet_amd.knn import knn_points
+    p1, p2 = OPS[f"knn_{case}_p1"], OPS[f"knn_{case}_p2"]
+    K = OPS[f"knn_{case}_idx"].shape[-1]
+    d, i, nn = knn_points(dev(p1), dev(p2), K=K, return_nn=True)
+    np.testing.assert_array_equal(i.cpu().numpy(), OPS[f"knn_{case}_idx"])
+    np.testing.assert_array_equal(d.cpu().numpy(), OPS[f"knn_{case}_dist"])
+    ref_nn = oracle.knn_gather(p2, OPS[f"knn_{case}_idx"])
+    np.testing.assert_array_equal(nn.cpu().numpy(), ref_nn)
+
+
+@pytest.mark.parametrize("n1,n2,dim,K", [(1024, 16384, 3, 64), (512, 1024, 3, 32), (256, 512, 3, 16),
+                                         (256, 256, 256, 8), (33, 70, 5, 8), (10, 5, 3, 8)])
+def test_knn_vs_oracle(n1, n2, dim, K):
+    from pcd_reg_hregnet_amd.knn import knn_points
+    rng = np.random.default_rng(n1 + n2 + dim + K)
+    p1 = rng.normal(size=(2, n1, dim)).astype(np.float32)
+    p2 = rng.normal(size=(2, n2, dim)).astype(np.float32)
+    p2[:, n2 // 2:] = p2[:, : n2 - n2 // 2]  # duplicate points -> distance ties
+    d, i, _ = knn_points(dev(p1), dev(p2), K=K)
+    rd, ri = oracle.knn(p1, p2, K)
+    np.testing.assert_array_equal(i.cpu().numpy(), ri)
+    np.testing.assert_array_equal(d.cpu().numpy(), rd)
+
+
+def test_knn_group_matches_oracle():
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(5)
+    nb, n, m, k = 3, 4096, 256, 64
+    p = rng.uniform(-40, 40, (nb, n, 3)).astype(np.float32)
+    q = p[:, rng.choice(n, m, replace=False)]
+    gidx, geom, kx = engine.knn_group(dev(q), dev(p), k)
+    _, ri = oracle.knn(q, p, k)
+    glob = (ri + (np.arange(nb) * n)[:, None, None]).reshape(-1)
+    np.testing.assert_array_equal(gidx.cpu().numpy(), glob)
+    nnp = oracle.knn_gather(p, ri).reshape(-1, 3)
+    np.testing.assert_array_equal(kx.cpu().numpy(), nnp)
+    rela = nnp - np.repeat(q.reshape(-1, 3), k, 0)
+    np.testing.assert_array_equal(geom.cpu().numpy()[:, :3], rela)
+    np.testing.assert_allclose(geom.cpu().numpy()[:, 3], np.linalg.norm(rela, axis=-1), rtol=1e-6)
+
+
+def test_gather_points_and_grad():
+    from pcd_reg_hregnet_amd.utils import gather_operation
+    rng = np.random.default_rng(1)
+    feats = rng.normal(size=(2, 3, 1000)).astype(np.float32)
+    idx = rng.integers(0, 1000, (2, 300)).astype(np.int32)
+    f = dev(feats).requires_grad_(True)
+    out = gather_operation(f, dev(idx))
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), oracle.gather_points(feats, idx))
+    go = rng.normal(size=(2, 3, 300)).astype(np.float32)
+    out.backward(dev(go))
+    np.testing.assert_allclose(f.grad.cpu().numpy(), oracle.gather_points_grad(go, idx, 1000),
+                               rtol=1e-6, atol=1e-6)
+
+
+def test_knn_gather_and_grad():
+    from pcd_reg_hregnet_amd.knn import knn_gather
+    rng = np.random.default_rng(2)
+    x = rng.normal(size=(2, 50, 7)).astype(np.float32)
+    idx = rng.integers(0, 50, (2, 20, 4)).astype(np.int64)
+    xt = dev(x).requires_grad_(True)
+    out = knn_gather(xt, dev(idx))
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), oracle.knn_gather(x, idx))
+    out.sum().backward()
+    cnt = np.zeros((2, 50))
+    for b in range(2):
+        np.add.at(cnt[b], idx[b].reshape(-1), 1)
+    np.testing.assert_allclose(xt.grad.cpu().numpy(), np.repeat(cnt[..., None], 7, -1), rtol=1e-6)
+
+
+@pytest.mark.parametrize("R,N,segs", [
+    (1000, 32, [(4, "plain")]),
+    (4096, 64, [(4, "plain"), (64, "gather")]),
+    (3000, 128, [(128, "div"), (128, "plain"), (256, "scale")]),
+    (2048, 512, [(16, "plain"), (256, "div"), (256, "gather")]),
+    (777, 96, [(12, "plain"), (64, "gather")]),
+])
+def test_gemm_segments_vs_torch_fp32(R, N, segs):
+    """fp32 MFMA GEMM with gathered/repeated/scaled segments vs torch fp32 on CPU.
+    Tolerance: 1e-5 relative to sum|a*w| (fp32 accumulation-order differences)."""
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(R + N)
+    K = sum(c for c, _ in segs)
+    W = (rng.normal(size=(N, K)) / np.sqrt(K)).astype(np.float32)
+    alpha = rng.uniform(0.5, 1.5, N).astype(np.float32)
+    beta = rng.normal(0, 0.1, N).astype(np.float32)
+    lin = engine.Lin(dev(W), dev(alpha), dev(beta), True)
+    parts, dsegs, keep = [], [], []
+    k0 = 0
+    k = 8
+    for c, kind in segs:
+        if kind == "plain":
+            src = rng.normal(size=(R, c)).astype(np.float32)
+            parts.append(src)
+            t = dev(src); keep.append(t)
+            dsegs.append(engine._seg(t, k0, c))
+        elif kind == "gather":
+            src = rng.normal(size=(500, c)).astype(np.float32)
+            gi = rng.integers(0, 500, R).astype(np.int32)
+            parts.append(src[gi])
+            t, tg = dev(src), dev(gi); keep += [t, tg]
+            dsegs.append(engine._seg(t, k0, c, gather=tg))
+        elif kind == "div":
+            src = rng.normal(size=((R + k - 1) // k, c)).astype(np.float32)
+            parts.append(src[np.arange(R) // k])
+            t = dev(src); keep.append(t)
+            dsegs.append(engine._seg(t, k0, c, row_div=k))
+        else:
+            src = rng.normal(size=(R, c)).astype(np.float32)
+            sc = rng.uniform(0, 1, R).astype(np.float32)
+            parts.append((src * sc[:, None]).astype(np.float32))
+            t, ts = dev(src), dev(sc); keep += [t, ts]
+            dsegs.append(engine._seg(t, k0, c, rowscale=ts))
+        k0 += c
+    A = np.concatenate(parts, 1)
+    out = engine.gemm(dsegs, lin, R).cpu().numpy()
+    ref = torch.from_numpy(A) @ torch.from_numpy(W).T
+    ref = torch.relu(ref * torch.from_numpy(alpha) + torch.from_numpy(beta)).numpy()
+    scale = (np.abs(A) @ np.abs(W).T) * alpha + np.abs(beta)
+    assert np.all(np.abs(out - ref) <= 1e-5 * scale + 1e-6)
+
+
+def test_cosine_gemm_vs_torch():
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(3)
+    B, n1, n2, C = 3, 256, 256, 256
+    a = rng.normal(size=(B * n1, C)).astype(np.float32)
+    b = rng.normal(size=(B * n2, C)).astype(np.float32)
+    S = torch.empty((B, n1, n2), device="cuda")
+    ta, tb = dev(a), dev(b)
+    na, nb = engine.row_norms(ta), engine.row_norms(tb)
+    engine.cosine_gemm(ta, tb, na, nb, B, n1, n2, C, S)
+    ref = oracle.cosine_similarity_matrix(a.reshape(B, n1, C), b.reshape(B, n2, C))
+    np.testing.assert_allclose(S.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
+
+
+def test_attend_and_group_max_vs_numpy():
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(4)
+    G, k, C = 300, 32, 128
+    emb = np.maximum(rng.normal(size=(G * k, C)), 0).astype(np.float32)
+    xyz = rng.normal(size=(G * k, 3)).astype(np.float32)
+    attw, att, kp = engine.attend(dev(emb), G, k, vals=dev(emb), xyz_rows=dev(xyz), want_attw=True)
+    x1 = emb.reshape(G, k, C).max(-1)
+    a = oracle._softmax(x1, -1)
+    np.testing.assert_allclose(attw.cpu().numpy().reshape(G, k), a, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(kp.cpu().numpy(), (a[..., None] * xyz.reshape(G, k, 3)).sum(1),
+                               rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(att.cpu().numpy(), (emb.reshape(G, k, C) * a[..., None]).sum(1),
+                               rtol=1e-5, atol=1e-6)
+    gm = engine.group_max(dev(emb), G, k)
+    np.testing.assert_array_equal(gm.cpu().numpy(), emb.reshape(G, k, C).max(1))
+
+
+def test_weighted_svd_recovers_planted_transform():
+    """Known answer: corres = R s + t exactly -> (R, t) recovered."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    rng = np.random.default_rng(6)
+    B, n = 5, 1024
+    src = rng.uniform(-20, 20, (B, n, 3)).astype(np.float32)
+    Rs, ts = zip(*(synthetic.random_se3(rng) for _ in range(B)))
+    Rs, ts = np.stack(Rs).astype(np.float32), np.stack(ts).astype(np.float32)
+    cor = (np.einsum("bij,bnj->bni", Rs, src) + ts[:, None]).astype(np.float32)
+    w = rng.uniform(0.1, 1.0, (B, n)).astype(np.float32)
+    _, _, R, t = engine.weighted_svd(dev(src), dev(cor), dev(w))
+    np.testing.assert_allclose(R.cpu().numpy(), Rs, atol=2e-5)
+    np.testing.assert_allclose(t.cpu().numpy(), ts, atol=2e-4)
+    oR, ot = oracle.weighted_svd(src, cor, w)
+    np.testing.assert_allclose(R.cpu().numpy(), oR, atol=1e-5)
+    np.testing.assert_allclose(t.cpu().numpy(), ot, atol=1e-4)
+
+
+def test_weighted_svd_nonfinite_batch_fallback():
+    """layers.py:485-493: a failing SVD gives R = I, t = 0 for the whole batch."""
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(7)
+    src = rng.normal(size=(3, 64, 3)).astype(np.float32)
+    cor = src.copy()
+    cor[1, 5, 0] = np.nan
+    w = np.ones((3, 64), np.float32)
+    _, _, R, t = engine.weighted_svd(dev(src), dev(cor), dev(w))
+    np.testing.assert_array_equal(R.cpu().numpy(), np.tile(np.eye(3, dtype=np.float32), (3, 1, 1)))
+    np.testing.assert_array_equal(t.cpu().numpy(), np.zeros((3, 3), np.float32))
+
+
+def test_transform_points():
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(8)
+    x = rng.normal(size=(2, 100, 3)).astype(np.float32)
+    R = rng.normal(size=(2, 3, 3)).astype(np.float32)
+    t = rng.normal(size=(2, 3)).astype(np.float32)
+    out = engine.transform(dev(x), dev(R), dev(t)).cpu().numpy()
+    np.testing.assert_allclose(out, np.einsum("bij,bnj->bni", R, x) + t[:, None], rtol=1e-5,
+                               atol=1e-5)
