@@ -50,6 +50,18 @@ __device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx,
     return fadd_rn(fadd_rn(fmul_rn(dx, dx), fmul_rn(dy, dy)), fmul_rn(dz, dz));
 }
 
+// min/max through v_med3_f32: one instruction, without the canonicalising
+// v_max the compiler puts around fminf/fmaxf on loop-carried values.
+// med3(a, b, -inf) = min(a, b), med3(a, b, +inf) = max(a, b) for non-NaN a, b.
+// `inf` must be a runtime +infinity (e.g. a kernel argument): with a literal
+// the compiler folds med3 back into minnum/maxnum.
+__device__ __forceinline__ float fmin_nc(float a, float b, float inf) {
+    return __builtin_amdgcn_fmed3f(a, b, -inf);
+}
+__device__ __forceinline__ float fmax_nc(float a, float b, float inf) {
+    return __builtin_amdgcn_fmed3f(a, b, inf);
+}
+
 // IEEE float -> uint32 with the same total order (negative values included).
 __device__ __forceinline__ uint32_t float_orderable(float f) {
     const uint32_t u = __float_as_uint(f);

@@ -28,38 +28,73 @@
 
 namespace {
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
+// max over each 16-lane row (quad_perm 1032, 2301, row_half_mirror, row_mirror)
+__device__ __forceinline__ float row_max16(float v, float inf) {
+    v = fmax_nc(v, dppf<0xb1>(v), inf);
+    v = fmax_nc(v, dppf<0x4e>(v), inf);
+    v = fmax_nc(v, dppf<0x141>(v), inf);
+    v = fmax_nc(v, dppf<0x140>(v), inf);
+    return v;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ float wave_max_uniform(float v, float inf) {
+    v = row_max16(v, inf);
+    return fmax_nc(fmax_nc(readlane_f(v, 0), readlane_f(v, 16), inf),
+                   fmax_nc(readlane_f(v, 32), readlane_f(v, 48), inf), inf);
+}
+
+// Per iteration: packed (v_pk_*) distance update of S register-resident points,
+// running max via max3; the wave's winner = max value, lowest lane (= lowest
+// rank), first slot; DPP row reductions + ballot instead of a shuffle tree.
+// Each wave publishes (x, y, z, d2, rank) of its winner in LDS (double
+// buffered), one barrier, then a 16-lane DPP reduction picks the block winner.
 template <int T, int S, bool WEIGHTED>
 __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xyz,
                                                     const float *__restrict__ wts,
                                                     float *__restrict__ temp_out,
                                                     int32_t *__restrict__ idx_out,
                                                     float *__restrict__ sampled_out, int n,
-                                                    int m, int bs, int L, int G, int Q) {
+                                                    int m, int bs, int L, int G, int Q,
+                                                    float inf) {
     constexpr int NW = T / HREG_WAVE;
-    __shared__ uint64_t red[2][NW];
+    constexpr int S2 = (S + 1) / 2;
+    static_assert(NW <= 16, "block winner reduction uses one 16-lane row");
+    __shared__ float4 s_cand[2][NW];
+    __shared__ int s_rank[2][NW];
 
     const int cloud = blockIdx.x;
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
     const float *P = xyz + (size_t)cloud * n * 3;
     const float *W = WEIGHTED ? wts + (size_t)cloud * n : nullptr;
 
-    float px[S], py[S], pz[S], pt[S], pw[S];
+    f2 PX[S2], PY[S2], PZ[S2], PT[S2], PW[S2];
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
+    for (int s = 0; s < 2 * S2; ++s) {
         const int g = s / Q, i = s % Q;
         const int rp = tid * G + g;  // position in bit-reversed thread order
         const int k = (int)bitrev_bits((uint32_t)rp, L) + i * bs;
-        const bool ok = (s < G * Q) && (rp < bs) && (k < n);
+        const bool ok = (s < S) && (s < G * Q) && (rp < bs) && (k < n);
         const int kk = ok ? k : 0;
-        px[s] = P[kk * 3 + 0];
-        py[s] = P[kk * 3 + 1];
-        pz[s] = P[kk * 3 + 2];
-        pw[s] = WEIGHTED ? W[kk] : 1.0f;
-        // invalid slots can never be selected: d2 = -inf is never > best
-        pt[s] = ok ? 1e10f : -__builtin_huge_valf();
+        PX[s / 2][s % 2] = P[kk * 3 + 0];
+        PY[s / 2][s % 2] = P[kk * 3 + 1];
+        PZ[s / 2][s % 2] = P[kk * 3 + 2];
+        PW[s / 2][s % 2] = WEIGHTED ? W[kk] : 1.0f;
+        // invalid slots can never be selected: d2 = -inf never reaches the max
+        PT[s / 2][s % 2] = ok ? 1e10f : -__builtin_huge_valf();
     }
 
-    int old = 0;
     float x1 = P[0], y1 = P[1], z1 = P[2];
     if (tid == 0) {
         idx_out[(size_t)cloud * m] = 0;
@@ -70,40 +105,53 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
     }
 
     for (int j = 1; j < m; ++j) {
+        const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
         float best = -1.0f;
-        int bslot = -1;  // -1 == the reference's (best=-1, besti=0) start
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-            float d = sqdist3(px[s], py[s], pz[s], x1, y1, z1);
-            if (WEIGHTED) d = fmul_rn(pw[s], d);
-            const float d2 = fminf(d, pt[s]);
-            pt[s] = d2;
-            const bool gt = d2 > best;
-            best = gt ? d2 : best;
-            bslot = gt ? s : bslot;
+        for (int s = 0; s < S2; ++s) {
+            const f2 dx = PX[s] - X1, dy = PY[s] - Y1, dz = PZ[s] - Z1;
+            f2 d = (dx * dx + dy * dy) + dz * dz;
+            if (WEIGHTED) d = PW[s] * d;
+            f2 t;
+            t.x = fmin_nc(d.x, PT[s].x, inf);
+            t.y = fmin_nc(d.y, PT[s].y, inf);
+            PT[s] = t;
+            best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
         }
-        uint32_t rank = 0;
-        if (bslot >= 0) {
-            const int g = bslot / Q, i = bslot % Q;
-            rank = (uint32_t)((tid * G + g) * Q + i);
-        }
-        uint64_t key = ((uint64_t)float_orderable(best) << 32) | (uint64_t)(0xffffffffu - rank);
-        key = wave_max_u64(key);
+        const float wmax = wave_max_uniform(best, inf);
+        // first slot holding the wave max, in this lane
+        int myslot = 2 * S2;
+#pragma unroll
+        for (int s = 2 * S2 - 1; s >= 0; --s)
+            myslot = (PT[s / 2][s % 2] == wmax) ? s : myslot;
+        const uint64_t hit = __ballot(best == wmax);
+        const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest rank
+        const int sl = __builtin_amdgcn_readlane(myslot, wl);
+        const int rp = (wv * 64 + wl) * G + sl / Q;
+        const int rank = rp * Q + sl % Q;
+        const int kw = (int)bitrev_bits((uint32_t)rp, L) + (sl % Q) * bs;
         const int buf = j & 1;
-        if ((tid & (HREG_WAVE - 1)) == 0) red[buf][tid / HREG_WAVE] = key;
-        __syncthreads();
-        uint64_t k2 = red[buf][0];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) {
-            const uint64_t o = red[buf][w];
-            k2 = o > k2 ? o : k2;
+        if (lane == 0) {
+            const float *pw = P + (size_t)kw * 3;
+            s_cand[buf][wv] = make_float4(pw[0], pw[1], pw[2], wmax);
+            s_rank[buf][wv] = rank;
         }
-        const uint32_t wr = 0xffffffffu - (uint32_t)(k2 & 0xffffffffu);
-        const int rp = (int)(wr / (uint32_t)Q), i = (int)(wr % (uint32_t)Q);
-        old = (int)bitrev_bits((uint32_t)rp, L) + i * bs;
-        x1 = P[old * 3 + 0];
-        y1 = P[old * 3 + 1];
-        z1 = P[old * 3 + 2];
+        __syncthreads();
+        const float4 c = lane < NW ? s_cand[buf][lane] : make_float4(0.f, 0.f, 0.f, -__builtin_huge_valf());
+        const float gmax = readlane_f(row_max16(c.w, inf), 0);
+        const uint64_t ghit = __ballot(lane < NW && c.w == gmax);
+        const int gw = (int)__builtin_ctzll(ghit);
+        int old;
+        if (gmax > -1.0f) {
+            const int grank = __builtin_amdgcn_readlane(s_rank[buf][lane < NW ? lane : 0], gw);
+            old = (int)bitrev_bits((uint32_t)(grank / Q), L) + (grank % Q) * bs;
+            x1 = readlane_f(c.x, gw);
+            y1 = readlane_f(c.y, gw);
+            z1 = readlane_f(c.z, gw);
+        } else {  // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0)
+            old = 0;
+            x1 = P[0]; y1 = P[1]; z1 = P[2];
+        }
         if (tid == 0) {
             idx_out[(size_t)cloud * m + j] = old;
             if (sampled_out) {
@@ -120,7 +168,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             const int g = s / Q, i = s % Q;
             const int rp = tid * G + g;
             const int k = (int)bitrev_bits((uint32_t)rp, L) + i * bs;
-            if ((s < G * Q) && (rp < bs) && (k < n)) tp[k] = pt[s];
+            if ((s < G * Q) && (rp < bs) && (k < n)) tp[k] = PT[s / 2][s % 2];
         }
     }
 }
@@ -214,7 +262,7 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
 #define HREG_FPS_CASE(TT, SS)                                                                 \
     if (T == TT && S <= SS) {                                                                 \
         hipLaunchKernelGGL((fps_reg_kernel<TT, SS, WEIGHTED>), dim3(b), dim3(TT), 0, st, xyz, \
-                           w, temp, idx, sampled, n, m, bs, L, G, Q);                         \
+                           w, temp, idx, sampled, n, m, bs, L, G, Q, __builtin_huge_valf());  \
         HREG_CHECK_LAUNCH();                                                                  \
         return HREG_OK;                                                                       \
     }

@@ -81,47 +81,47 @@ __global__ void group_max_kernel(const float *__restrict__ x, int G, int k, int 
 
 // ---------------------------------------------------------------- head out
 // z = dot(x[r], w3) + b3 (mlp3 Conv1d(C,1), layers.py:130/268/431), then
-// softplus(z) + 0.001 (layers.py:161-163) or sigmoid(z) (layers.py:393-394);
-// optionally weights = (1/(sigma+1e-5)) / mean_cloud (models.py:30-32).
+// softplus(z) + 0.001 (layers.py:161-163) or sigmoid(z) (layers.py:393-394).
+// One wave per row over the whole grid.
 __global__ __launch_bounds__(256) void head_out_kernel(const float *__restrict__ x, int C, int ldx,
-                                                       int rows, const float *__restrict__ w3,
+                                                       int R, const float *__restrict__ w3,
                                                        const float *__restrict__ b3, int mode,
-                                                       float *__restrict__ out,
-                                                       float *__restrict__ wout) {
+                                                       float *__restrict__ out) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * WAVES + w;
+    if (r >= R) return;
+    const float *row = x + (size_t)r * ldx;
+    float t = 0.f;
+    for (int c = lane; c < C; c += 64) t = fadd_rn(t, fmul_rn(row[c], w3[c]));
+    t = wave_sum_f32(t);
+    const float z = fadd_rn(t, b3[0]);
+    float o;
+    if (mode == HREG_HEAD_SOFTPLUS) {
+        const float sp = z > 20.f ? z : log1pf(expf(z));
+        o = fadd_rn(sp, 0.001f);
+    } else {
+        o = 1.0f / fadd_rn(1.0f, expf(-z));
+    }
+    if (lane == 0) out[r] = o;
+}
+
+// weights = (1/(sigma+1e-5)) / mean_cloud(1/(sigma+1e-5)) (models.py:30-32); block per cloud
+__global__ __launch_bounds__(256) void sigma_weights_kernel(const float *__restrict__ sig, int rows,
+                                                            float *__restrict__ wout) {
     __shared__ float red[WAVES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int cloud = blockIdx.x;
-    const float bias = b3[0];
-    float part = 0.f;  // partial sum of 1/(sigma+1e-5) for this wave
-    for (int i = w; i < rows; i += WAVES) {
-        const size_t r = (size_t)cloud * rows + i;
-        const float *row = x + r * ldx;
-        float t = 0.f;
-        for (int c = lane; c < C; c += 64) t = fadd_rn(t, fmul_rn(row[c], w3[c]));
-        t = wave_sum_f32(t);
-        const float z = fadd_rn(t, bias);
-        float o;
-        if (mode == HREG_HEAD_SOFTPLUS) {
-            const float sp = z > 20.f ? z : log1pf(expf(z));
-            o = fadd_rn(sp, 0.001f);
-            part = fadd_rn(part, 1.0f / fadd_rn(o, 1e-5f));
-        } else {
-            o = 1.0f / fadd_rn(1.0f, expf(-z));
-        }
-        if (lane == 0) out[r] = o;
-    }
-    if (!wout) return;
+    const float *s = sig + (size_t)blockIdx.x * rows;
+    float part = 0.f;
+    for (int i = threadIdx.x; i < rows; i += blockDim.x)
+        part = fadd_rn(part, 1.0f / fadd_rn(s[i], 1e-5f));
+    part = wave_sum_f32(part);
     if (lane == 0) red[w] = part;
     __syncthreads();
     float tot = 0.f;
     for (int i = 0; i < WAVES; ++i) tot = fadd_rn(tot, red[i]);
     const float mean = tot / (float)rows;
-    __syncthreads();
-    for (int i = threadIdx.x; i < rows; i += blockDim.x) {
-        const size_t r = (size_t)cloud * rows + i;
-        const float wi = 1.0f / fadd_rn(out[r], 1e-5f);
-        wout[r] = wi / mean;
-    }
+    float *o = wout + (size_t)blockIdx.x * rows;
+    for (int i = threadIdx.x; i < rows; i += blockDim.x) o[i] = (1.0f / fadd_rn(s[i], 1e-5f)) / mean;
 }
 
 // --------------------------------------------------------------- row norms
@@ -480,9 +480,15 @@ extern "C" int hreg_head_out(const float *x, int C, int ldx, int nclouds, int ro
     if (mode != HREG_HEAD_SOFTPLUS && mode != HREG_HEAD_SIGMOID) return HREG_ERR_INVALID;
     if (weights_out && mode != HREG_HEAD_SOFTPLUS) return HREG_ERR_INVALID;
     if (!nclouds) return HREG_OK;
-    hipLaunchKernelGGL(head_out_kernel, dim3(nclouds), dim3(256), 0, as_stream(stream), x, C, ldx,
-                       rows_per_cloud, w3, b3, mode, out, weights_out);
+    const int R = nclouds * rows_per_cloud;
+    hipLaunchKernelGGL(head_out_kernel, dim3((R + WAVES - 1) / WAVES), dim3(256), 0,
+                       as_stream(stream), x, C, ldx, R, w3, b3, mode, out);
     HREG_CHECK_LAUNCH();
+    if (weights_out) {
+        hipLaunchKernelGGL(sigma_weights_kernel, dim3(nclouds), dim3(256), 0, as_stream(stream),
+                           out, rows_per_cloud, weights_out);
+        HREG_CHECK_LAUNCH();
+    }
     return HREG_OK;
 }
 
