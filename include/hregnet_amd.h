@@ -160,9 +160,10 @@ int hreg_head_out(const float *x, int C, int ldx, int nclouds, int rows_per_clou
 int hreg_row_norms(const float *x, int R, int C, int ldx, float *norms, void *stream);
 
 /* S [nb][N1][N2]; kidx [nb][N1][k] int32 (local dst index) ->
- * sims[(b*N1+i)*k+j][2] = (S[i][n]/(rowmax_i + 1e-6), S[i][n]/(colmax_n + 1e-6)), n = kidx */
+ * sims[(b*N1+i)*k+j][2] = (S[i][n]/(rowmax_i + 1e-6), S[i][n]/(colmax_n + 1e-6)), n = kidx;
+ * maxes [nb][N1+N2] receives (rowmax, colmax) (caller-allocated scratch/output). */
 int hreg_sim_gather(const float *S, int nb, int N1, int N2, const int32_t *kidx, int k,
-                    float *sims, int ld_sims, void *stream);
+                    float *maxes, float *sims, int ld_sims, void *stream);
 
 /* Small per-(query,neighbour) feature rows for CoarseReg/FineReg (16 floats):
  * [p-q (3), |p-q| (1), q (3), p (3), w_src (1), w_dst[n] (1), sims (ns: 0 or 4), pad].

@@ -56,7 +56,7 @@ _SIGS = {
     "hreg_group_max": [_vp, _i, _i, _i, _i, _vp, _i, _vp],
     "hreg_head_out": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_row_norms": [_vp, _i, _i, _i, _vp, _vp],
-    "hreg_sim_gather": [_vp, _i, _i, _i, _vp, _i, _vp, _i, _vp],
+    "hreg_sim_gather": [_vp, _i, _i, _i, _vp, _i, _vp, _vp, _i, _vp],
     "hreg_pair_feats": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp,
                         _vp],
     "hreg_weighted_svd": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],

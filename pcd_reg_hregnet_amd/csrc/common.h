@@ -75,6 +75,14 @@ __device__ __forceinline__ uint32_t bitrev_bits(uint32_t x, int L) {
     return L == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - L));
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt) but NOT for its outstanding global stores, unlike __syncthreads()
+// whose release fence adds s_waitcnt vmcnt(0) -- in a loop that stores results
+// every iteration that puts store-completion latency on the critical path.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Wave-level LDS hand-off between lanes (rocPRIM's wave_barrier pattern):
 // release fence + wave barrier + acquire fence, so the compiler cannot move
 // one lane's LDS store past another lane's later LDS load.

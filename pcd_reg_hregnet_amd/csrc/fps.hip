@@ -4,10 +4,7 @@
 // (reference models/PointUtils/src/furthest_point_sampling_gpu.cu:84-206, :254-375).
 // Not a translation: one workgroup per cloud keeps every point, its running
 // minimum distance ("temp") and its weight in VGPRs for all m-1 dependent
-// iterations (no HBM traffic inside the loop), and the per-iteration argmax
-// is one 64-bit max over a packed key
-//     key = orderable(d2) << 32 | ~rank,   rank = r' * Q + i
-// which is tree-independent and reproduces the reference winner exactly.
+// iterations (no HBM traffic inside the loop).
 //
 // The reference winner ("FPS tie rule"): with bs =
 // opt_n_threads(n) "threads" (cuda_utils.h:22-26), reference thread r scans
@@ -15,16 +12,22 @@
 // shared-memory tree keeps the lower slot on ties (.cu:75-80), so among equal
 // maxima the thread with the smallest bit-reversed id wins, then the smallest
 // k.  Here reference thread r = bitrev_L(r') is handled by our thread r'/G
-// (slot g = r' % G), and its points k = r + i*bs are scanned in order i, so
-// "first strictly larger" inside our thread plus "smallest rank" across
-// threads is the same order.  Initial best = -1 at k = 0 (rank 0) reproduces
-// the reference's (best=-1, besti=0) start (.cu:115-116).
+// (slot g = r' % G) and its points k = r + i*bs sit in slots g*QT + i, so the
+// order (thread, slot) is the reference order: "max value, then lowest lane,
+// then lowest slot" reproduces the reference winner exactly.  A start value of
+// -1 with fallback k = 0 reproduces the reference's (best=-1, besti=0) start
+// (.cu:115-116).
 //
-// The winner's coordinates come back through one broadcast global load
-// (L2-resident cloud); the LDS slot is double-buffered by iteration parity so
-// there is exactly one barrier per iteration (the reference re-reads
-// dists_i[0] without a barrier: SURVEY.md 5, latent WAR race).
+// Per iteration: a packed (v_pk_*) distance update + running max, a DPP row
+// reduction + ballot per wave (lowest lane wins ties), the wave winner's slot
+// from a bit mask, its coordinates straight out of its registers (uniform slot
+// index -> scalar branch tree + v_readlane), one double-buffered LDS slot per
+// wave and ONE barrier that waits on LDS only (not on the per-iteration output
+// stores), then a 16-lane DPP reduction over the waves.  (The reference
+// re-reads dists_i[0] without a barrier: SURVEY.md 5, latent WAR race.)
 #include "common.h"
+
+#include <stdlib.h>
 
 namespace {
 
@@ -54,24 +57,47 @@ __device__ __forceinline__ float wave_max_uniform(float v, float inf) {
                    fmax_nc(readlane_f(v, 32), readlane_f(v, 48), inf), inf);
 }
 
-// Per iteration: packed (v_pk_*) distance update of S register-resident points,
-// running max via max3; the wave's winner = max value, lowest lane (= lowest
-// rank), first slot; DPP row reductions + ballot instead of a shuffle tree.
-// Each wave publishes (x, y, z, d2, rank) of its winner in LDS (double
-// buffered), one barrier, then a 16-lane DPP reduction picks the block winner.
-template <int T, int S, bool WEIGHTED>
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+// Binary branch tree over a wave-uniform slot index -> three v_readlane.
+template <int LO, int HI, int N2>
+__device__ __forceinline__ void pick_slot(int sl, int wl, const f2 (&PX)[N2], const f2 (&PY)[N2],
+                                          const f2 (&PZ)[N2], float &x, float &y, float &z) {
+    if constexpr (HI - LO == 1) {
+        x = readlane_f(PX[LO / 2][LO % 2], wl);
+        y = readlane_f(PY[LO / 2][LO % 2], wl);
+        z = readlane_f(PZ[LO / 2][LO % 2], wl);
+    } else {
+        constexpr int MID = (LO + HI) / 2;
+        if (sl < MID) pick_slot<LO, MID>(sl, wl, PX, PY, PZ, x, y, z);
+        else pick_slot<MID, HI>(sl, wl, PX, PY, PZ, x, y, z);
+    }
+}
+
+// T threads, G reference threads per thread, QT >= ceil(n/bs) points per
+// reference thread (slots beyond n are invalid), S = G*QT slots per thread.
+template <int T, int G, int QT, bool WEIGHTED, bool STAMP = false>
 __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xyz,
                                                     const float *__restrict__ wts,
                                                     float *__restrict__ temp_out,
                                                     int32_t *__restrict__ idx_out,
                                                     float *__restrict__ sampled_out, int n,
-                                                    int m, int bs, int L, int G, int Q,
-                                                    float inf) {
-    constexpr int NW = T / HREG_WAVE;
+                                                    int m, int bs, int L, float inf,
+                                                    uint64_t *stamps = nullptr) {
+    constexpr int S = G * QT;
     constexpr int S2 = (S + 1) / 2;
+    constexpr int NW = T / HREG_WAVE;
     static_assert(NW <= 16, "block winner reduction uses one 16-lane row");
+    static_assert(2 * S2 <= 32, "slot mask is 32 bits");
     __shared__ float4 s_cand[2][NW];
-    __shared__ int s_rank[2][NW];
+    __shared__ int s_k[2][NW];
+    uint64_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, r0 = 0, c0 = 0;
 
     const int cloud = blockIdx.x;
     const int tid = threadIdx.x;
@@ -82,10 +108,10 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
     f2 PX[S2], PY[S2], PZ[S2], PT[S2], PW[S2];
 #pragma unroll
     for (int s = 0; s < 2 * S2; ++s) {
-        const int g = s / Q, i = s % Q;
+        const int g = s / QT, i = s % QT;
         const int rp = tid * G + g;  // position in bit-reversed thread order
         const int k = (int)bitrev_bits((uint32_t)rp, L) + i * bs;
-        const bool ok = (s < S) && (s < G * Q) && (rp < bs) && (k < n);
+        const bool ok = (s < S) && (rp < bs) && (k < n);
         const int kk = ok ? k : 0;
         PX[s / 2][s % 2] = P[kk * 3 + 0];
         PY[s / 2][s % 2] = P[kk * 3 + 1];
@@ -103,8 +129,14 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             o[0] = x1; o[1] = y1; o[2] = z1;
         }
     }
+    if constexpr (STAMP) {
+        r0 = __builtin_amdgcn_s_memrealtime();
+        c0 = stamp();
+    }
 
     for (int j = 1; j < m; ++j) {
+        uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        if constexpr (STAMP) t0 = stamp();
         const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
         float best = -1.0f;
 #pragma unroll
@@ -118,33 +150,41 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             PT[s] = t;
             best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
         }
+        if constexpr (STAMP) t1 = stamp();
         const float wmax = wave_max_uniform(best, inf);
-        // first slot holding the wave max, in this lane
-        int myslot = 2 * S2;
+        // this lane's first slot holding the wave max (bit mask + find-first-set)
+        uint32_t smask = 0;
 #pragma unroll
-        for (int s = 2 * S2 - 1; s >= 0; --s)
-            myslot = (PT[s / 2][s % 2] == wmax) ? s : myslot;
+        for (int s = 0; s < 2 * S2; ++s)
+            smask |= (PT[s / 2][s % 2] == wmax) ? (1u << s) : 0u;
+        const int myslot = smask ? (int)__builtin_ctz(smask) : 0;
         const uint64_t hit = __ballot(best == wmax);
-        const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest rank
+        const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest reference order
         const int sl = __builtin_amdgcn_readlane(myslot, wl);
-        const int rp = (wv * 64 + wl) * G + sl / Q;
-        const int rank = rp * Q + sl % Q;
-        const int kw = (int)bitrev_bits((uint32_t)rp, L) + (sl % Q) * bs;
+        const int rp = (wv * 64 + wl) * G + sl / QT;
+        const int kwin = (int)bitrev_bits((uint32_t)rp, L) + (sl % QT) * bs;
+        float wx = 0.f, wy = 0.f, wz = 0.f;
+        pick_slot<0, 2 * S2>(sl, wl, PX, PY, PZ, wx, wy, wz);
+        if constexpr (STAMP) t2 = stamp();
         const int buf = j & 1;
         if (lane == 0) {
-            const float *pw = P + (size_t)kw * 3;
-            s_cand[buf][wv] = make_float4(pw[0], pw[1], pw[2], wmax);
-            s_rank[buf][wv] = rank;
+            s_cand[buf][wv] = make_float4(wx, wy, wz, wmax);
+            s_k[buf][wv] = kwin;
         }
-        __syncthreads();
-        const float4 c = lane < NW ? s_cand[buf][lane] : make_float4(0.f, 0.f, 0.f, -__builtin_huge_valf());
+        lds_barrier();
+        if constexpr (STAMP) t3 = stamp();
+        float4 c = make_float4(0.f, 0.f, 0.f, -__builtin_huge_valf());
+        int ck = 0;
+        if (lane < NW) {
+            c = s_cand[buf][lane];
+            ck = s_k[buf][lane];
+        }
         const float gmax = readlane_f(row_max16(c.w, inf), 0);
         const uint64_t ghit = __ballot(lane < NW && c.w == gmax);
-        const int gw = (int)__builtin_ctzll(ghit);
+        const int gw = (int)__builtin_ctzll(ghit);  // lowest wave = lowest reference order
         int old;
         if (gmax > -1.0f) {
-            const int grank = __builtin_amdgcn_readlane(s_rank[buf][lane < NW ? lane : 0], gw);
-            old = (int)bitrev_bits((uint32_t)(grank / Q), L) + (grank % Q) * bs;
+            old = __builtin_amdgcn_readlane(ck, gw);
             x1 = readlane_f(c.x, gw);
             y1 = readlane_f(c.y, gw);
             z1 = readlane_f(c.z, gw);
@@ -159,21 +199,37 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
                 o[0] = x1; o[1] = y1; o[2] = z1;
             }
         }
+        if constexpr (STAMP) {
+            const uint64_t t4 = stamp();
+            acc0 += t1 - t0; acc1 += t2 - t1; acc2 += t3 - t2; acc3 += t4 - t3;
+        }
+    }
+    if constexpr (STAMP) {
+        const uint64_t c1 = stamp();
+        const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+        if (cloud == 0 && tid == 0) {
+            stamps[0] = acc0; stamps[1] = acc1; stamps[2] = acc2; stamps[3] = acc3;
+            stamps[4] = c1 - c0; stamps[5] = r1 - r0;
+        }
     }
 
     if (temp_out) {
+        // recompute the slot indices from an opaque copy of bs/L so the compiler
+        // does not keep the prologue's S indices live across the whole loop
+        int bs2 = bs, L2 = L;
+        asm volatile("" : "+s"(bs2), "+s"(L2));
         float *tp = temp_out + (size_t)cloud * n;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            const int g = s / Q, i = s % Q;
+            const int g = s / QT, i = s % QT;
             const int rp = tid * G + g;
-            const int k = (int)bitrev_bits((uint32_t)rp, L) + i * bs;
-            if ((s < G * Q) && (rp < bs) && (k < n)) tp[k] = PT[s / 2][s % 2];
+            const int k = (int)bitrev_bits((uint32_t)rp, L2) + i * bs2;
+            if ((rp < bs2) && (k < n)) tp[k] = PT[s / 2][s % 2];
         }
     }
 }
 
-// Fallback for clouds too large for the register-resident path (S > 16):
+// Fallback for clouds too large for the register-resident path (n > 16384):
 // temp lives in the caller's buffer; same key, same winner.
 template <bool WEIGHTED>
 __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__ xyz,
@@ -241,6 +297,41 @@ __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__
     }
 }
 
+template <bool WEIGHTED, bool STAMP = false>
+bool launch_reg(int T, int G, int QT, int b, int n, int m, int bs, int L, const float *xyz,
+                const float *w, float *temp, int32_t *idx, float *sampled, uint64_t *stamps,
+                hipStream_t st) {
+#define HREG_FPS_CASE(TT, GG, QQ)                                                              \
+    if (T == TT && G == GG && QT == QQ) {                                                      \
+        hipLaunchKernelGGL((fps_reg_kernel<TT, GG, QQ, WEIGHTED, STAMP>), dim3(b), dim3(TT), 0, \
+                           st, xyz, w, temp, idx, sampled, n, m, bs, L, __builtin_huge_valf(), \
+                           stamps);                                                            \
+        return true;                                                                           \
+    }
+    HREG_FPS_CASE(1024, 1, 1) HREG_FPS_CASE(1024, 1, 2) HREG_FPS_CASE(1024, 1, 4)
+    HREG_FPS_CASE(1024, 1, 8)
+    if constexpr (!WEIGHTED) { HREG_FPS_CASE(1024, 1, 16) }
+    HREG_FPS_CASE(512, 1, 1) HREG_FPS_CASE(512, 1, 2)
+    HREG_FPS_CASE(256, 4, 1) HREG_FPS_CASE(256, 1, 1) HREG_FPS_CASE(256, 1, 2)
+    HREG_FPS_CASE(128, 4, 1) HREG_FPS_CASE(128, 1, 1) HREG_FPS_CASE(128, 1, 2)
+    HREG_FPS_CASE(64, 4, 1) HREG_FPS_CASE(64, 1, 1) HREG_FPS_CASE(64, 1, 2)
+#undef HREG_FPS_CASE
+    return false;
+}
+
+// choose (T threads, G reference threads per thread, QT slots per reference thread)
+void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
+    const int bs = hreg_opt_n_threads(n);
+    const int Q = (n + bs - 1) / bs;
+    QT = 1;
+    while (QT < Q) QT <<= 1;
+    if (Q == 1 && bs >= 256) { T = bs / 4; G = 4; QT = 1; return; }
+    if (bs >= 64) { T = bs; G = 1; }
+    else { T = 64; G = 1; }
+    // per-slot registers (x, y, z, temp[, w]) must fit the VGPR budget
+    if (T == 1024 && QT > (weighted ? 8 : 16)) { T = 512; G = 2; }
+}
+
 template <bool WEIGHTED>
 int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *temp, int32_t *idx,
                float *sampled, hipStream_t st) {
@@ -250,32 +341,12 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
     const int bs = hreg_opt_n_threads(n);
     const int L = hreg_ilog2(bs);
     const int Q = (n + bs - 1) / bs;
-    // choose our thread count T and slots per thread S = G * Q (T * G == bs)
-    int T, G;
-    if (Q == 1 && bs >= 256) { T = bs / 4; G = 4; }
-    else if (bs >= 64) { T = bs; G = 1; }
-    else { T = 64; G = 1; }
-    // keep the per-slot registers (x, y, z, temp[, w]) inside the VGPR budget
-    const int smax1024 = WEIGHTED ? 8 : 16;
-    if (T == 1024 && G * Q > smax1024) { T = 512; G = 2; }
-    const int S = G * Q;
-#define HREG_FPS_CASE(TT, SS)                                                                 \
-    if (T == TT && S <= SS) {                                                                 \
-        hipLaunchKernelGGL((fps_reg_kernel<TT, SS, WEIGHTED>), dim3(b), dim3(TT), 0, st, xyz, \
-                           w, temp, idx, sampled, n, m, bs, L, G, Q, __builtin_huge_valf());  \
-        HREG_CHECK_LAUNCH();                                                                  \
-        return HREG_OK;                                                                       \
+    int T, G, QT;
+    choose_geometry(n, WEIGHTED, T, G, QT);
+    if (launch_reg<WEIGHTED>(T, G, QT, b, n, m, bs, L, xyz, w, temp, idx, sampled, nullptr, st)) {
+        HREG_CHECK_LAUNCH();
+        return HREG_OK;
     }
-    HREG_FPS_CASE(1024, 1) HREG_FPS_CASE(1024, 2) HREG_FPS_CASE(1024, 4)
-    HREG_FPS_CASE(1024, 8)
-    if constexpr (!WEIGHTED) { HREG_FPS_CASE(1024, 16) }
-    HREG_FPS_CASE(512, 2) HREG_FPS_CASE(512, 4) HREG_FPS_CASE(512, 8) HREG_FPS_CASE(512, 16)
-    HREG_FPS_CASE(512, 32)
-    HREG_FPS_CASE(256, 4) HREG_FPS_CASE(256, 8) HREG_FPS_CASE(256, 16)
-    HREG_FPS_CASE(128, 4) HREG_FPS_CASE(128, 8) HREG_FPS_CASE(128, 16)
-    HREG_FPS_CASE(64, 1) HREG_FPS_CASE(64, 2) HREG_FPS_CASE(64, 4) HREG_FPS_CASE(64, 8)
-    HREG_FPS_CASE(64, 16)
-#undef HREG_FPS_CASE
     // large clouds: temp through memory (caller's temp buffer is required)
     if (temp == nullptr) return HREG_ERR_INVALID;
     hipLaunchKernelGGL((fps_mem_kernel<WEIGHTED>), dim3(b), dim3(1024), 0, st, xyz, w, temp, idx,
@@ -285,6 +356,25 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
 }
 
 }  // namespace
+
+// Diagnostic: per-phase cycle sums of block 0 / wave 0 of the register path
+// (stamps[6] = scan, wave reduce + pick, LDS write + barrier, final reduce,
+// total cycles, total 100 MHz ticks).  Not part of the product path.
+extern "C" int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,
+                                     int32_t *idx, uint64_t *stamps, void *stream) {
+    if (b <= 0 || n <= 0 || m <= 0 || !points || !idx || !stamps) return HREG_ERR_INVALID;
+    const int bs = hreg_opt_n_threads(n);
+    int T, G, QT;
+    choose_geometry(n, weights != nullptr, T, G, QT);
+    const bool ok =
+        weights ? launch_reg<true, true>(T, G, QT, b, n, m, bs, hreg_ilog2(bs), points, weights,
+                                         nullptr, idx, nullptr, stamps, as_stream(stream))
+                : launch_reg<false, true>(T, G, QT, b, n, m, bs, hreg_ilog2(bs), points, nullptr,
+                                          nullptr, idx, nullptr, stamps, as_stream(stream));
+    if (!ok) return HREG_ERR_UNSUPPORTED;
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
 
 extern "C" int hreg_furthest_point_sampling(int b, int n, int m, const float *points,
                                             float *temp, int32_t *idx, float *sampled_xyz,

@@ -142,36 +142,52 @@ __global__ __launch_bounds__(256) void row_norms_kernel(const float *__restrict_
 // -------------------------------------------------------------- sim gather
 // layers.py:296-313: per pair, row max over n and column max over i of S,
 // then (S[i][n]/(rowmax_i+1e-6), S[i][n]/(colmax_n+1e-6)) at n = kidx[i][j].
-__global__ __launch_bounds__(256) void sim_gather_kernel(const float *__restrict__ S, int N1,
-                                                         int N2, const int32_t *__restrict__ kidx,
-                                                         int k, float *__restrict__ sims,
-                                                         int ld_sims) {
-    extern __shared__ float sm[];
-    float *rowmax = sm;       // [N1]
-    float *colmax = sm + N1;  // [N2]
-    const int b = blockIdx.x;
-    const float *Sb = S + (size_t)b * N1 * N2;
+// maxes [nb][N1 + N2] = (rowmax, colmax).
+__global__ __launch_bounds__(256) void sim_rowmax_kernel(const float *__restrict__ S, int nb, int N1,
+                                                         int N2, float *__restrict__ maxes) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int n = threadIdx.x; n < N2; n += blockDim.x) {
-        float m = Sb[n];
-        for (int i = 1; i < N1; ++i) m = fmaxf(m, Sb[(size_t)i * N2 + n]);
-        colmax[n] = m;
-    }
-    for (int i = w; i < N1; i += WAVES) {
-        float m = -__builtin_huge_valf();
-        for (int n = lane; n < N2; n += 64) m = fmaxf(m, Sb[(size_t)i * N2 + n]);
-        m = wave_max_f32(m);
-        if (lane == 0) rowmax[i] = m;
-    }
+    const int r = blockIdx.x * WAVES + w;  // global row b*N1 + i
+    if (r >= nb * N1) return;
+    const float *row = S + (size_t)r * N2;
+    float m = -__builtin_huge_valf();
+    for (int n = lane; n < N2; n += 64) m = fmaxf(m, row[n]);
+    m = wave_max_f32(m);
+    if (lane == 0) maxes[(size_t)(r / N1) * (N1 + N2) + (r % N1)] = m;
+}
+
+__global__ __launch_bounds__(256) void sim_colmax_kernel(const float *__restrict__ S, int N1, int N2,
+                                                         float *__restrict__ maxes) {
+    __shared__ float part[4][64];
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int g = threadIdx.x >> 6;
+    const float *Sb = S + (size_t)b * N1 * N2;
+    float m = -__builtin_huge_valf();
+    if (c < N2)
+        for (int i = g; i < N1; i += 4) m = fmaxf(m, Sb[(size_t)i * N2 + c]);
+    part[g][threadIdx.x & 63] = m;
     __syncthreads();
-    for (int e = threadIdx.x; e < N1 * k; e += blockDim.x) {
-        const int i = e / k;
-        const int n = kidx[(size_t)b * N1 * k + e];
-        const float s = Sb[(size_t)i * N2 + n];
-        float *o = sims + ((size_t)b * N1 * k + e) * ld_sims;
-        o[0] = s / fadd_rn(rowmax[i], 1e-6f);
-        o[1] = s / fadd_rn(colmax[n], 1e-6f);
+    if (g == 0 && c < N2) {
+        const int l = threadIdx.x;
+        maxes[(size_t)b * (N1 + N2) + N1 + c] =
+            fmaxf(fmaxf(part[0][l], part[1][l]), fmaxf(part[2][l], part[3][l]));
     }
+}
+
+__global__ void sim_gather_kernel(const float *__restrict__ S, int nb, int N1, int N2,
+                                  const int32_t *__restrict__ kidx, int k,
+                                  const float *__restrict__ maxes, float *__restrict__ sims,
+                                  int ld_sims) {
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (size_t)nb * N1 * k) return;
+    const size_t bi = e / k;  // b*N1 + i
+    const int b = (int)(bi / N1), i = (int)(bi % N1);
+    const int n = kidx[e];
+    const float s = S[bi * N2 + n];
+    const float *mx = maxes + (size_t)b * (N1 + N2);
+    float *o = sims + e * ld_sims;
+    o[0] = s / fadd_rn(mx[i], 1e-6f);
+    o[1] = s / fadd_rn(mx[N1 + n], 1e-6f);
 }
 
 // -------------------------------------------------------------- pair feats
@@ -502,14 +518,20 @@ extern "C" int hreg_row_norms(const float *x, int R, int C, int ldx, float *norm
 }
 
 extern "C" int hreg_sim_gather(const float *S, int nb, int N1, int N2, const int32_t *kidx, int k,
-                               float *sims, int ld_sims, void *stream) {
-    if (!S || !kidx || !sims || nb < 0 || N1 <= 0 || N2 <= 0 || k <= 0 || ld_sims < 2)
+                               float *maxes, float *sims, int ld_sims, void *stream) {
+    if (!S || !kidx || !sims || !maxes || nb < 0 || N1 <= 0 || N2 <= 0 || k <= 0 || ld_sims < 2)
         return HREG_ERR_INVALID;
-    const size_t lds = (size_t)(N1 + N2) * sizeof(float);
-    if (lds > 64 * 1024) return HREG_ERR_UNSUPPORTED;
     if (!nb) return HREG_OK;
-    hipLaunchKernelGGL(sim_gather_kernel, dim3(nb), dim3(256), lds, as_stream(stream), S, N1, N2,
-                       kidx, k, sims, ld_sims);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(sim_rowmax_kernel, dim3((nb * N1 + WAVES - 1) / WAVES), dim3(256), 0, st, S,
+                       nb, N1, N2, maxes);
+    HREG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(sim_colmax_kernel, dim3((N2 + 63) / 64, nb), dim3(256), 0, st, S, N1, N2,
+                       maxes);
+    HREG_CHECK_LAUNCH();
+    const size_t total = (size_t)nb * N1 * k;
+    hipLaunchKernelGGL(sim_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, S,
+                       nb, N1, N2, kidx, k, maxes, sims, ld_sims);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

@@ -176,8 +176,13 @@ __global__ __launch_bounds__(256) void knn_group_kernel(const float *__restrict_
 }
 
 // ---- general dim (descriptor space) ------------------------------------
-// The wave stages 64 database rows x 64 dims into LDS (padded stride 65) so
-// each lane reads its own row conflict-free; dims accumulate in order.
+// A block takes 16 queries (4 per wave) against 64 database rows at a time:
+// the 64 rows x 64 dims and the 16 queries x 64 dims are staged in LDS
+// (padded stride 65), lane = database row, so each wave ends a chunk with the
+// 64 distances of its 4 queries in registers, one per lane, and offers them to
+// the queries' lists.  Dims accumulate in order (canonical distance).
+constexpr int QPW = 4;  // queries per wave
+
 template <int K>
 __global__ __launch_bounds__(256) void knnd_kernel(const float *__restrict__ q,
                                                    const float *__restrict__ p, int nb, int n1,
@@ -185,48 +190,68 @@ __global__ __launch_bounds__(256) void knnd_kernel(const float *__restrict__ q,
                                                    int64_t *__restrict__ idx64,
                                                    int32_t *__restrict__ idx32,
                                                    float *__restrict__ nn, int k) {
-    __shared__ uint64_t sbuf[WAVES][128];
-    __shared__ float tile[WAVES][64 * 65];
-    __shared__ float qv[WAVES][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = blockIdx.x * WAVES + w;
-    if (qi >= nb * n1) return;
-    const int cloud = qi / n1;
+    constexpr int QB = WAVES * QPW;
+    __shared__ uint64_t sbuf[WAVES][QPW][128];
+    __shared__ float tile[64 * 65];
+    __shared__ float qt[QB * 65];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, w = tid >> 6;
+    const int nq = nb * n1;
+    const int q0 = blockIdx.x * QB;  // queries of one block never straddle clouds: n1 % QB == 0
+    const int cloud = q0 / n1;
     const float *P = p + (size_t)cloud * n2 * dim;
-    const float *Q = q + (size_t)qi * dim;
-    float *T = tile[w];
-    WaveList L;
-    L.key = KEY_INF; L.tau = KEY_INF; L.cnt = 0;
+    WaveList L[QPW];
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) { L[u].key = KEY_INF; L[u].tau = KEY_INF; L[u].cnt = 0; }
     for (int base = 0; base < n2; base += 64) {
-        float acc = 0.f;
+        float acc[QPW];
+#pragma unroll
+        for (int u = 0; u < QPW; ++u) acc[u] = 0.f;
         for (int d0 = 0; d0 < dim; d0 += 64) {
             const int dc = min(64, dim - d0);
-            wave_fence();
-            qv[w][lane] = lane < dc ? Q[d0 + lane] : 0.f;
-            for (int rr = 0; rr < 64; ++rr) {
+            __syncthreads();
+            for (int e = tid; e < 64 * 64; e += 256) {
+                const int rr = e >> 6, cc = e & 63;
                 const int row = base + rr;
-                T[rr * 65 + lane] = (row < n2 && lane < dc) ? P[(size_t)row * dim + d0 + lane] : 0.f;
+                tile[rr * 65 + cc] = (row < n2 && cc < dc) ? P[(size_t)row * dim + d0 + cc] : 0.f;
             }
-            wave_fence();
+            for (int e = tid; e < QB * 64; e += 256) {
+                const int rr = e >> 6, cc = e & 63;
+                const int qi = q0 + rr;
+                qt[rr * 65 + cc] = (qi < nq && cc < dc) ? q[(size_t)qi * dim + d0 + cc] : 0.f;
+            }
+            __syncthreads();
             for (int e = 0; e < dc; ++e) {
-                const float diff = fsub_rn(qv[w][e], T[lane * 65 + e]);
-                acc = fadd_rn(acc, fmul_rn(diff, diff));
+                const float pv = tile[lane * 65 + e];
+#pragma unroll
+                for (int u = 0; u < QPW; ++u) {
+                    const float diff = fsub_rn(qt[(w * QPW + u) * 65 + e], pv);
+                    acc[u] = fadd_rn(acc[u], fmul_rn(diff, diff));
+                }
             }
         }
         const int pi = base + lane;
-        const uint64_t key = pi < n2 ? (((uint64_t)__float_as_uint(acc) << 32) | (uint32_t)pi) : KEY_INF;
-        offer<K>(L, sbuf[w], key, lane);
+#pragma unroll
+        for (int u = 0; u < QPW; ++u) {
+            const uint64_t key =
+                pi < n2 ? (((uint64_t)__float_as_uint(acc[u]) << 32) | (uint32_t)pi) : KEY_INF;
+            offer<K>(L[u], sbuf[w][u], key, lane);
+        }
     }
-    if (L.cnt > 0) flush64<K>(L, sbuf[w], lane);
-    if (lane < k) {
-        const bool valid = L.key != KEY_INF;
-        const int id = valid ? (int)(uint32_t)(L.key & 0xffffffffu) : -1;
-        const size_t o = (size_t)qi * k + lane;
-        if (dists) dists[o] = valid ? __uint_as_float((uint32_t)(L.key >> 32)) : 0.f;
-        if (idx64) idx64[o] = id;
-        if (idx32) idx32[o] = id;
-        if (nn)
-            for (int e = 0; e < dim; ++e) nn[o * dim + e] = valid ? P[(size_t)id * dim + e] : 0.f;
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) {
+        if (L[u].cnt > 0) flush64<K>(L[u], sbuf[w][u], lane);
+        const int qi = q0 + w * QPW + u;
+        if (qi < nq && lane < k) {
+            const bool valid = L[u].key != KEY_INF;
+            const int id = valid ? (int)(uint32_t)(L[u].key & 0xffffffffu) : -1;
+            const size_t o = (size_t)qi * k + lane;
+            if (dists) dists[o] = valid ? __uint_as_float((uint32_t)(L[u].key >> 32)) : 0.f;
+            if (idx64) idx64[o] = id;
+            if (idx32) idx32[o] = id;
+            if (nn)
+                for (int e = 0; e < dim; ++e) nn[o * dim + e] = valid ? P[(size_t)id * dim + e] : 0.f;
+        }
     }
 }
 
@@ -234,13 +259,25 @@ template <int K>
 int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim, int k,
                float *dists, int64_t *idx64, int32_t *idx32, float *nn, hipStream_t st) {
     const int nq = b * n1;
-    dim3 grid((nq + WAVES - 1) / WAVES);
-    if (dim == 3)
-        hipLaunchKernelGGL((knn3_kernel<K>), grid, dim3(256), 0, st, p1, p2, b, n1, n2, dists,
-                           idx64, idx32, nn, k);
-    else
-        hipLaunchKernelGGL((knnd_kernel<K>), grid, dim3(256), 0, st, p1, p2, b, n1, n2, dim,
-                           dists, idx64, idx32, nn, k);
+    if (dim == 3) {
+        hipLaunchKernelGGL((knn3_kernel<K>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
+                           p2, b, n1, n2, dists, idx64, idx32, nn, k);
+    } else {
+        constexpr int QB = WAVES * QPW;
+        if (b > 1 && n1 % QB) {  // a block's queries must belong to one cloud
+            for (int c = 0; c < b; ++c) {
+                const int rc = launch_knn<K>(p1 + (size_t)c * n1 * dim, p2 + (size_t)c * n2 * dim, 1,
+                                             n1, n2, dim, k, dists ? dists + (size_t)c * n1 * k : nullptr,
+                                             idx64 ? idx64 + (size_t)c * n1 * k : nullptr,
+                                             idx32 ? idx32 + (size_t)c * n1 * k : nullptr,
+                                             nn ? nn + (size_t)c * n1 * k * dim : nullptr, st);
+                if (rc) return rc;
+            }
+            return HREG_OK;
+        }
+        hipLaunchKernelGGL((knnd_kernel<K>), dim3((nq + QB - 1) / QB), dim3(256), 0, st, p1, p2, b,
+                           n1, n2, dim, dists, idx64, idx32, nn, k);
+    }
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

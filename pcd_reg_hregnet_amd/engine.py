@@ -363,7 +363,8 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     S = _empty(B, N1, N1, device=dev)
     cosine_gemm(s_desc, d_desc, norms[:B * N1], norms[B * N1:], B, N1, N1, C, S)
     sims_a = _empty(B * N1 * k, 2, device=dev)
-    call("hreg_sim_gather", S, B, N1, N1, kidx, k, sims_a, 2, _stream())
+    maxes = _empty(B, 2 * N1, device=dev)
+    call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_a, 2, _stream())
     # neighbour-aware descriptors for src and dst together (layers.py:315-337)
     gself, geom_self, _ = knn_group(xyz3, xyz3, k)
     G2 = 2 * B * N1
@@ -376,7 +377,7 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     nnorm = row_norms(nbr)
     cosine_gemm(nbr[:B * N1], nbr[B * N1:], nnorm[:B * N1], nnorm[B * N1:], B, N1, N1, C, S)
     sims_b = _empty(B * N1 * k, 2, device=dev)
-    call("hreg_sim_gather", S, B, N1, N1, kidx, k, sims_b, 2, _stream())
+    call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_b, 2, _stream())
     # correspondence features + convs_1 (layers.py:364-384)
     R = B * N1 * k
     small = _empty(R, 16, device=dev)

@@ -1,0 +1,89 @@
+"""Micro-benchmarks of single C-ABI ops on the GPU (HIP events, median of reps).
+
+usage: python tools/op_bench.py fps|wfps|knn|all [--b 16]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pcd_reg_hregnet_amd import _lib, engine  # noqa: E402
+
+
+def timeit(fn, reps=10, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", default="all", nargs="?")
+    ap.add_argument("--b", type=int, default=16)
+    a = ap.parse_args()
+    _lib.load()
+    rng = np.random.default_rng(0)
+    res = {}
+    if a.what in ("fps", "all"):
+        x = torch.from_numpy(rng.uniform(-40, 40, (a.b, 16384, 3)).astype(np.float32)).cuda()
+        res["fps_l1_ms"] = timeit(lambda: engine.fps(x, 1024))
+    if a.what in ("wfps", "all"):
+        for n, m in ((1024, 512), (512, 256)):
+            x = torch.from_numpy(rng.uniform(-40, 40, (a.b, n, 3)).astype(np.float32)).cuda()
+            w = torch.from_numpy(rng.uniform(0.5, 2, (a.b, n)).astype(np.float32)).cuda()
+            res[f"wfps_{n}_ms"] = timeit(lambda: engine.fps(x, m, w))
+    if a.what in ("knn", "all"):
+        p = torch.from_numpy(rng.uniform(-40, 40, (a.b, 16384, 3)).astype(np.float32)).cuda()
+        q = p[:, :1024].contiguous()
+        res["knn_group_l1_ms"] = timeit(lambda: engine.knn_group(q, p, 64))
+        d = torch.from_numpy(rng.normal(size=(a.b // 2, 256, 256)).astype(np.float32)).cuda()
+        res["knn_desc_ms"] = timeit(lambda: engine.knn_idx32(d, d, 8))
+    print({k: round(v, 4) for k, v in res.items()}, "HREG_FPS_THREADS=",
+          os.environ.get("HREG_FPS_THREADS"))
+
+
+if __name__ == "__main__" and "stamps" not in sys.argv:
+    main()
+
+
+def fps_stamps():
+    """Per-phase cycle split of the FPS register kernel (diagnostic build)."""
+    import ctypes
+    L = _lib.load()
+    fn = L.hreg_debug_fps_stamps
+    fn.restype = ctypes.c_int
+    vp, i = ctypes.c_void_p, ctypes.c_int
+    fn.argtypes = [i, i, i, vp, vp, vp, vp, vp]
+    rng = np.random.default_rng(0)
+    for n, m, weighted in ((16384, 1024, False), (1024, 512, True)):
+        x = torch.from_numpy(rng.uniform(-40, 40, (16, n, 3)).astype(np.float32)).cuda()
+        w = torch.from_numpy(rng.uniform(0.5, 2, (16, n)).astype(np.float32)).cuda() if weighted else None
+        idx = torch.empty((16, m), dtype=torch.int32, device="cuda")
+        st = torch.zeros(8, dtype=torch.int64, device="cuda")
+        for _ in range(2):
+            rc = fn(16, n, m, x.data_ptr(), w.data_ptr() if w is not None else None, idx.data_ptr(),
+                    st.data_ptr(), _lib.stream_handle())
+            assert rc == 0
+        torch.cuda.synchronize()
+        s = st.cpu().numpy().astype(float)
+        it = m - 1
+        print(f"n={n} m={m}: cycles/iter scan={s[0]/it:.0f} wavered+pick={s[1]/it:.0f} "
+              f"lds+barrier={s[2]/it:.0f} final={s[3]/it:.0f} total={s[4]/it:.0f}; "
+              f"clock={s[4] / (s[5] / 100e6) / 1e9:.3f} GHz, {s[5] / 100e6 * 1e3:.3f} ms")
+
+
+if __name__ == "__main__" and "stamps" in sys.argv:
+    fps_stamps()
