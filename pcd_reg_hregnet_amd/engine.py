@@ -34,6 +34,7 @@ LEVELS = (
     (256, 16, 128, (128, 128, 256), (128, 128, 256), 256),
 )
 K_HEAD = 8  # CoarseReg/FineReg k (models.py:71-73)
+FUSED_L1 = True  # level 1 through the fused group_l1 kernel (False: layer-by-layer GEMMs)
 
 
 @dataclass
@@ -125,9 +126,42 @@ class PreparedWeights:
         self.fine = {}
         for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64)):
             self.fine[name] = (_stack(sd, name + ".convs_1", 3, _perm_fine(C)), _mlp_head(sd, name))
+        self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
-                     "coarse_head", "fine"):
+                     "coarse_head", "fine", "l1_table"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
+
+
+# ---------------------------------------------------------- fused level 1
+def frag_layer(W: torch.Tensor) -> torch.Tensor:
+    """MFMA A-fragments of a layer W [Cout][Cin] (Cin, Cout multiples of 32) for the
+    accumulator-chaining order of group_l1.hip: [co][ct][q][lane] =
+    W[co*32 + (lane & 31)][ct*32 + (q & 3) + 8*(q >> 2) + 4*(lane >> 5)]."""
+    Cout, Cin = W.shape
+    co = torch.arange(Cout // 32).view(-1, 1, 1, 1)
+    ct = torch.arange(Cin // 32).view(1, -1, 1, 1)
+    q = torch.arange(16).view(1, 1, -1, 1)
+    lane = torch.arange(64).view(1, 1, 1, -1)
+    rows = co * 32 + (lane & 31)
+    cols = ct * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5)
+    return W[rows, cols].reshape(-1)
+
+
+def frag_geom(W: torch.Tensor) -> torch.Tensor:
+    """First layer (Cin = 4): k-step s, lane half h takes channel 2h + s -> [s][lane]."""
+    s = torch.arange(2).view(-1, 1)
+    lane = torch.arange(64).view(1, -1)
+    return W[lane & 31, 2 * (lane >> 5) + s].reshape(-1)
+
+
+def l1_table(det, desc, mlp) -> torch.Tensor:
+    """Weight/epilogue table of the fused level-1 kernel (layout: group_l1.hip F_*/E_*)."""
+    parts = [frag_geom(det[0].W), frag_layer(det[1].W), frag_layer(det[2].W),
+             frag_geom(desc[0].W), frag_layer(desc[1].W), frag_layer(desc[2].W),
+             frag_layer(mlp[0].W), frag_layer(mlp[1].W)]
+    for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
 
 
 def _to_device(x, device):
@@ -297,6 +331,18 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights):
     R = G * k
     idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n))
     gidx, geom, kx = knn_group(sampled, xyz, k)
+    if lvl == 0 and FUSED_L1:
+        dev = xyz.device
+        kp = _empty(G, 3, device=dev)
+        att_feat = _empty(G, LEVELS[0][3][-1], device=dev)
+        desc = _empty(G, LEVELS[0][5], device=dev)
+        call("hreg_group_l1", P.l1_table, geom, kx, G, kp, att_feat, desc, _stream())
+        m1, m2, w3, b3 = P.det_head[lvl]
+        s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)
+        s = gemm([_seg(s, 0, s.shape[1])], m2, G)
+        sig, wnext = head_out(s, s.shape[1], nb, M, w3, b3, _lib.HREG_HEAD_SOFTPLUS,
+                              want_weights=True)
+        return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
     segs = [_seg(geom, 0, 4)]
     if feats is not None:
         segs.append(_seg(feats, 4, Cf, gather=gidx))
