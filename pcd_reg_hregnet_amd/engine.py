@@ -318,10 +318,20 @@ def knn_idx32(p1, p2, k):
 
 # ------------------------------------------------------------------ stages
 
-def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights):
+def grouping(xyz, lvl: int, weights=None):
+    """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz)."""
+    M, k = LEVELS[lvl][:2]
+    nb, n, _ = xyz.shape
+    idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n))
+    gidx, geom, kx = knn_group(sampled, xyz, k)
+    return idx, sampled, gidx, geom, kx
+
+
+def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=None):
     """KeypointDetector (layers.py:134-165) + DescExtractor (layers.py:200-209) for one level.
 
-    xyz [nb,n,3]; feats [nb*n, Cf] point-major or None; weights [nb*n] or None.
+    xyz [nb,n,3]; feats [nb*n, Cf] point-major or None; weights [nb*n] or None;
+    grouped: this level's grouping() result when computed ahead (pipelined level 1).
     Returns keypoints [nb,M,3], sigmas [nb*M], att_feat [nb*M,Cdet], desc [nb*M,Cdesc],
     next weights [nb*M] (or None) and the FPS indices [nb,M].
     """
@@ -329,8 +339,9 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights):
     nb, n, _ = xyz.shape
     G = nb * M
     R = G * k
-    idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n))
-    gidx, geom, kx = knn_group(sampled, xyz, k)
+    if grouped is None:
+        grouped = grouping(xyz, lvl, weights)
+    idx, sampled, gidx, geom, kx = grouped
     if lvl == 0 and FUSED_L1:
         dev = xyz.device
         kp = _empty(G, 3, device=dev)
@@ -369,13 +380,14 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights):
     return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
 
 
-def feature_extraction(P: PreparedWeights, points, use_weights=True):
-    """HierFeatureExtraction.forward (models.py:26-58) over nb clouds at once."""
-    nb = points.shape[0]
+def feature_extraction(P: PreparedWeights, points, use_weights=True, l1=None):
+    """HierFeatureExtraction.forward (models.py:26-58) over nb clouds at once.
+    l1: level-1 grouping computed ahead (see Pipeline)."""
     out = {}
     xyz, feats, w = points, None, None
     for lvl in range(3):
-        kp, sig, att, desc, wnext, idx = keypoint_level(P, lvl, xyz, feats, w)
+        kp, sig, att, desc, wnext, idx = keypoint_level(P, lvl, xyz, feats, w,
+                                                        l1 if lvl == 0 else None)
         out[f"xyz_{lvl + 1}"] = kp
         out[f"sigmas_{lvl + 1}"] = sig
         out[f"desc_{lvl + 1}"] = desc
@@ -483,11 +495,12 @@ def transform(xyz, R, t):
     return out
 
 
-def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True):
+def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=None):
     """HRegNet.forward (models/HRegNet/models.py:77-148), eval mode."""
     B, N, _ = src.shape
-    pts = torch.cat([src, dst], 0).contiguous()
-    fe = feature_extraction(P, pts, use_weights)
+    if pts is None:
+        pts = torch.cat([src, dst], 0).contiguous()
+    fe = feature_extraction(P, pts, use_weights, l1)
 
     def split(t, rows):
         return t[:B * rows], t[B * rows:]
@@ -526,3 +539,55 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True):
         "src_feats": feats(0), "dst_feats": feats(1),
         "_fps_idx": [fe[f"fps_idx_{i + 1}"] for i in range(3)],
     }
+
+
+class Pipeline:
+    """Throughput executor: level-1 FPS + kNN grouping of batch i+1 runs on a side
+    stream while the rest of batch i runs on the caller's stream.
+
+    Level 1 depends only on the input points, and FPS is a serial 1023-step
+    chain on one CU per cloud (2B CUs busy), so overlapping it with the
+    previous batch's GEMM-heavy levels hides it.  Every batch still goes
+    through the complete forward; results are identical to hregnet_forward.
+    """
+
+    def __init__(self, P: PreparedWeights, device):
+        self.P = P
+        self.side = torch.cuda.Stream(device=device)
+
+    def _stage1(self, src, dst):
+        pts = torch.cat([src, dst], 0).contiguous()
+        return pts, grouping(pts, 0)
+
+    def run(self, batches, use_weights=True):
+        """batches: iterable of (src [B,N,3], dst [B,N,3]) on the GPU -> list of output dicts."""
+        main = torch.cuda.current_stream()
+        ev_in = torch.cuda.Event()
+        ev_in.record(main)
+        self.side.wait_event(ev_in)
+        batches = list(batches)
+        pending = []
+
+        def launch(i):
+            src, dst = batches[i]
+            with torch.cuda.stream(self.side):
+                pts, g = self._stage1(src, dst)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            for t in (src, dst):
+                t.record_stream(self.side)
+            pending.append((pts, g, ev))
+
+        outs = []
+        if batches:
+            launch(0)
+        for i, (src, dst) in enumerate(batches):
+            if i + 1 < len(batches):
+                launch(i + 1)
+            pts, g, ev = pending.pop(0)
+            main.wait_event(ev)
+            pts.record_stream(main)
+            for t in g:
+                t.record_stream(main)
+            outs.append(hregnet_forward(self.P, src, dst, use_weights, l1=g, pts=pts))
+        return outs

@@ -114,3 +114,23 @@ def test_vs_oracle_lidar_b8(net):
     np.testing.assert_array_equal(r["_fps_idx"][0][:2], o["src_feats"]["fps_idx_1"])
     np.testing.assert_array_equal(r["_fps_idx"][0][2:], o["dst_feats"]["fps_idx_1"])
     compare_forward(r, g)
+
+
+def test_pipeline_matches_serial(net):
+    """The pipelined executor runs level 1 on a side stream; outputs must be bitwise
+    identical to the serial forward for every batch."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    batches = []
+    for sd in (30, 31, 32):
+        s, d, _, _ = synthetic.lidar_batch(2, 4096, seed0=sd)
+        batches.append((torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()))
+    with torch.no_grad():
+        piped = engine.Pipeline(P, torch.device("cuda")).run(batches)
+        serial = [engine.hregnet_forward(P, s, d) for s, d in batches]
+    torch.cuda.synchronize()
+    for a, b in zip(piped, serial):
+        for i in range(3):
+            assert torch.equal(a["rotation"][i], b["rotation"][i])
+            assert torch.equal(a["translation"][i], b["translation"][i])
+        assert torch.equal(a["src_feats"]["desc_1"], b["src_feats"]["desc_1"])
