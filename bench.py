@@ -129,8 +129,9 @@ def main():
     ap.add_argument("--batch", type=int, default=PAIRS_PER_GPU, help="pairs per GPU")
     ap.add_argument("--points", type=int, default=POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--serial", action="store_true",
-                    help="no cross-batch pipelining (each step waits for the previous)")
+    ap.add_argument("--executor", choices=("graph", "pipeline", "serial"), default="graph",
+                    help="graph: pipelined forward replayed as HIP graphs; pipeline: same "
+                         "eagerly; serial: no cross-batch overlap")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -155,11 +156,17 @@ def main():
     timer.install()
 
     pipe = engine.Pipeline(P, device)
+    gpipe = None
+    if args.executor == "graph":
+        with torch.no_grad():
+            gpipe = engine.GraphPipeline(P, src, dst)
 
     def run(n):
         with torch.no_grad():
-            if args.serial:
+            if args.executor == "serial":
                 return [engine.hregnet_forward(P, src, dst) for _ in range(n)]
+            if args.executor == "graph":
+                return gpipe.run(n)
             return pipe.run([(src, dst)] * n)
 
     run(args.warmup)
@@ -213,8 +220,8 @@ def main():
             "data": "synthetic (seeded KITTI-shape LiDAR pairs; nusc_feats + seeded heads)",
             "config": {"workload": f"HRegNet forward (eval), batch={B} pairs/GPU, "
                                    f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])",
-                       "executor": "serial" if args.serial else
-                                   "pipelined (level-1 FPS of step i+1 overlaps step i)",
+                       "executor": args.executor + ("" if args.executor == "serial" else
+                                   " (level-1 FPS of step i+1 overlaps step i)"),
                        "global_batch": B * world, "points": args.points,
                        "parallelism": f"dp{world} (pairs sharded, no collective)"},
             "roofline": roof,

@@ -245,11 +245,14 @@ def _empty(*shape, dtype=torch.float32, device):
     return torch.empty(shape, dtype=dtype, device=device)
 
 
-def fps(xyz, npoint, weights=None, want_idx=True):
+def fps(xyz, npoint, weights=None, out=None):
     nb, n, _ = xyz.shape
     dev = xyz.device
-    idx = _empty(nb, npoint, dtype=torch.int32, device=dev)
-    sampled = _empty(nb, npoint, 3, device=dev)
+    if out is None:
+        idx = _empty(nb, npoint, dtype=torch.int32, device=dev)
+        sampled = _empty(nb, npoint, 3, device=dev)
+    else:
+        idx, sampled = out
     temp = _empty(nb, n, device=dev) if n > 16384 else None
     if weights is None:
         call("hreg_furthest_point_sampling", nb, n, npoint, xyz, temp, idx, sampled, _stream())
@@ -295,15 +298,18 @@ def row_norms(x):
     return out
 
 
-def knn_group(q, p, k):
+def knn_group(q, p, k, out=None):
     """q [nb,m,3], p [nb,n,3] -> gidx [nb*m*k] int32 (global rows of p), geom [nb*m*k,4], knn_xyz."""
     nb, m, _ = q.shape
     n = p.shape[1]
     dev = q.device
     R = nb * m * k
-    gidx = _empty(R, dtype=torch.int32, device=dev)
-    geom = _empty(R, 4, device=dev)
-    kx = _empty(R, 3, device=dev)
+    if out is None:
+        gidx = _empty(R, dtype=torch.int32, device=dev)
+        geom = _empty(R, 4, device=dev)
+        kx = _empty(R, 3, device=dev)
+    else:
+        gidx, geom, kx = out
     call("hreg_knn_group", q, p, nb, m, n, k, gidx, geom, kx, _stream())
     return gidx, geom, kx
 
@@ -318,13 +324,33 @@ def knn_idx32(p1, p2, k):
 
 # ------------------------------------------------------------------ stages
 
-def grouping(xyz, lvl: int, weights=None):
-    """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz)."""
+def grouping(xyz, lvl: int, weights=None, out=None):
+    """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz).
+    out: optional preallocated tensors of the same tuple."""
     M, k = LEVELS[lvl][:2]
     nb, n, _ = xyz.shape
-    idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n))
-    gidx, geom, kx = knn_group(sampled, xyz, k)
+    idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
+                       out=None if out is None else out[:2])
+    gidx, geom, kx = knn_group(sampled, xyz, k, out=None if out is None else out[2:])
     return idx, sampled, gidx, geom, kx
+
+
+def alloc_stage1(B: int, N: int, device):
+    """Buffers of the input-only stage: points [2B,N,3] + level-1 grouping outputs."""
+    nb = 2 * B
+    M, k = LEVELS[0][:2]
+    R = nb * M * k
+    return (_empty(nb, N, 3, device=device),
+            (_empty(nb, M, dtype=torch.int32, device=device), _empty(nb, M, 3, device=device),
+             _empty(R, dtype=torch.int32, device=device), _empty(R, 4, device=device),
+             _empty(R, 3, device=device)))
+
+
+def stage1_into(bufs, src, dst):
+    """cat(src, dst) + level-1 FPS + knn_group into preallocated buffers."""
+    pts, g = bufs
+    torch.cat([src, dst], 0, out=pts)
+    grouping(pts, 0, out=g)
 
 
 def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=None):
@@ -591,3 +617,73 @@ class Pipeline:
                 t.record_stream(main)
             outs.append(hregnet_forward(self.P, src, dst, use_weights, l1=g, pts=pts))
         return outs
+
+
+class GraphPipeline:
+    """The pipelined forward captured as HIP graphs (kernel boundaries ~1.5 us
+    instead of a host launch each).
+
+    Static inputs ``src``/``dst`` (copy new data in with ``load``) and two
+    level-1 buffer sets A/B.  g_AB = {side stream: stage 1 of the next batch
+    into B ; main: the rest of the forward from A}, g_BA symmetric; replaying
+    them alternately overlaps batch i+1's FPS with batch i inside each graph.
+    """
+
+    def __init__(self, P: PreparedWeights, src, dst, use_weights=True):
+        self.P = P
+        self.use_weights = use_weights
+        dev = src.device
+        B, N, _ = src.shape
+        self.src = src.clone()
+        self.dst = dst.clone()
+        self.bufs = [alloc_stage1(B, N, dev), alloc_stage1(B, N, dev)]
+        self.side = torch.cuda.Stream(device=dev)
+        # eager warm-up: library, allocator and workspace shapes
+        stage1_into(self.bufs[0], self.src, self.dst)
+        self._rest(0)
+        torch.cuda.synchronize()
+        self.pool = torch.cuda.graph_pool_handle()
+        self.g_first = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_first, pool=self.pool):
+            stage1_into(self.bufs[0], self.src, self.dst)
+        self.g_step, self.outs = [], []
+        for cur in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                main = torch.cuda.current_stream()
+                self.side.wait_stream(main)
+                with torch.cuda.stream(self.side):
+                    stage1_into(self.bufs[1 - cur], self.src, self.dst)
+                out = self._rest(cur)
+                main.wait_stream(self.side)
+            self.g_step.append(g)
+            self.outs.append(out)
+        self.g_last, self.outs_last = [], []
+        for cur in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                out = self._rest(cur)
+            self.g_last.append(g)
+            self.outs_last.append(out)
+        torch.cuda.synchronize()
+
+    def _rest(self, cur):
+        pts, g = self.bufs[cur]
+        return hregnet_forward(self.P, self.src, self.dst, self.use_weights, l1=g, pts=pts)
+
+    def load(self, src, dst):
+        self.src.copy_(src)
+        self.dst.copy_(dst)
+
+    def run(self, steps: int):
+        """Runs `steps` complete forwards of the static batch; returns the last output
+        dict (views into graph-owned memory, valid until the next run)."""
+        if steps <= 0:
+            return None
+        self.g_first.replay()
+        cur = 0
+        for i in range(steps - 1):
+            self.g_step[cur].replay()
+            cur = 1 - cur
+        self.g_last[cur].replay()
+        return self.outs_last[cur]

@@ -134,3 +134,26 @@ def test_pipeline_matches_serial(net):
             assert torch.equal(a["rotation"][i], b["rotation"][i])
             assert torch.equal(a["translation"][i], b["translation"][i])
         assert torch.equal(a["src_feats"]["desc_1"], b["src_feats"]["desc_1"])
+
+
+def test_graph_pipeline_matches_eager(net):
+    """HIP-graph replay of the pipelined forward == the eager forward, bitwise."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    s, d, _, _ = synthetic.lidar_batch(2, 4096, seed0=40)
+    src, dst = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    with torch.no_grad():
+        gp = engine.GraphPipeline(P, src, dst)
+        ref = engine.hregnet_forward(P, src, dst)
+        for steps in (1, 2, 5):
+            out = gp.run(steps)
+            torch.cuda.synchronize()
+            for i in range(3):
+                assert torch.equal(out["rotation"][i], ref["rotation"][i])
+                assert torch.equal(out["translation"][i], ref["translation"][i])
+        s2, d2, _, _ = synthetic.lidar_batch(2, 4096, seed0=41)
+        gp.load(torch.from_numpy(s2).cuda(), torch.from_numpy(d2).cuda())
+        out = gp.run(3)
+        ref2 = engine.hregnet_forward(P, torch.from_numpy(s2).cuda(), torch.from_numpy(d2).cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(out["rotation"][-1], ref2["rotation"][-1])
