@@ -12,17 +12,14 @@
 // (layers.py:23-27, 204-206, 364-380, 444-445) are never materialised.
 //
 // Layout: activations are point-major ([rows][channels]) in HBM.  A block
-// computes a BM x BN tile; K is staged through LDS in BK=16 chunks, double
-// buffered with one barrier per chunk.  Inside a chunk lane half h takes
-// k = h*8 + s for MFMA k-step s, so each lane's 8 k-values are contiguous and
-// come out of LDS with two ds_read_b128 (rows padded to 20 floats: the 16
-// rows of a ds_read_b128 lane group hit 16 distinct 16-byte slots).
+// computes a BM x BN tile; K is staged through LDS in BK = 16/32 chunks, double
+// buffered with one barrier per chunk.  Inside each 16-deep sub-chunk lane half
+// h takes k = h*8 + s for MFMA k-step s, so each lane's k-values are contiguous and
+// come out of LDS with ds_read_b128 (rows padded by 4 floats: the 16 rows of a
+// ds_read_b128 lane group hit 16 distinct 16-byte slots).
 #include "common.h"
 
 namespace {
-
-constexpr int BK = 16;
-constexpr int LDS_STRIDE = 20;  // floats per LDS row (16 + 4 pad)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -55,13 +52,16 @@ __device__ __forceinline__ float4 load_w4(const hreg_gemm_t &g, int b, int n, in
     return *reinterpret_cast<const float4 *>(p);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BK>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     static_assert(WM * WN == 4, "4 waves");
+    static_assert(BK == 16 || BK == 32, "BK");
+    constexpr int LDS_STRIDE = BK + 4;          // pad: 16-row ds_read_b128 groups hit distinct slots
+    constexpr int F4 = BK / 4;                  // float4 per row per chunk
     constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
     constexpr int TM = WTM / 32, TN = WTN / 32;  // 32x32 MFMA tiles per wave
-    constexpr int A_LD = BM * 4 / 256;           // float4 loads per thread per chunk
-    constexpr int B_LD = (BN * 4 + 255) / 256;
+    constexpr int A_LD = (BM * F4 + 255) / 256;  // float4 loads per thread per chunk
+    constexpr int B_LD = (BN * F4 + 255) / 256;
 
     __shared__ __attribute__((aligned(16))) float As[2][BM * LDS_STRIDE];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDS_STRIDE];
@@ -88,26 +88,28 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
 #pragma unroll
         for (int i = 0; i < A_LD; ++i) {
             const int e = tid + i * 256;
-            ra[i] = load_a4(g, b, r0 + (e >> 2), c * BK + (e & 3) * 4);
+            ra[i] = (e < BM * F4) ? load_a4(g, b, r0 + e / F4, c * BK + (e % F4) * 4)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int i = 0; i < B_LD; ++i) {
             const int e = tid + i * 256;
-            rb[i] = (e < BN * 4) ? load_w4(g, b, n0 + (e >> 2), c * BK + (e & 3) * 4)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+            rb[i] = (e < BN * F4) ? load_w4(g, b, n0 + e / F4, c * BK + (e % F4) * 4)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto lstore = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < A_LD; ++i) {
             const int e = tid + i * 256;
-            *reinterpret_cast<float4 *>(&As[buf][(e >> 2) * LDS_STRIDE + (e & 3) * 4]) = ra[i];
+            if (e < BM * F4)
+                *reinterpret_cast<float4 *>(&As[buf][(e / F4) * LDS_STRIDE + (e % F4) * 4]) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < B_LD; ++i) {
             const int e = tid + i * 256;
-            if (e < BN * 4)
-                *reinterpret_cast<float4 *>(&Bs[buf][(e >> 2) * LDS_STRIDE + (e & 3) * 4]) = rb[i];
+            if (e < BN * F4)
+                *reinterpret_cast<float4 *>(&Bs[buf][(e / F4) * LDS_STRIDE + (e % F4) * 4]) = rb[i];
         }
     };
 
@@ -119,30 +121,29 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     for (int c = 0; c < nchunks; ++c) {
         const int buf = c & 1;
         if (c + 1 < nchunks) gload(c + 1);
-        float4 fa[TM][2], fb[TN][2];
+        // per 16-deep sub-chunk, lane half h takes k = sub*16 + h*8 + s for k-step s
+        // (its 8 k-values are contiguous): the accumulation order of every output is
+        // the same for every BK and tile shape, so results do not depend on R
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const float *p = &As[buf][(wr * WTM + i * 32 + l32) * LDS_STRIDE + h * 8];
-            fa[i][0] = *reinterpret_cast<const float4 *>(p);
-            fa[i][1] = *reinterpret_cast<const float4 *>(p + 4);
-        }
+        for (int s4 = 0; s4 < BK / 4 / 2; ++s4) {
+            const int koff = (s4 >> 1) * 16 + h * 8 + (s4 & 1) * 4;
+            float4 fa[TM], fb[TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const float *p = &Bs[buf][(wc * WTN + j * 32 + l32) * LDS_STRIDE + h * 8];
-            fb[j][0] = *reinterpret_cast<const float4 *>(p);
-            fb[j][1] = *reinterpret_cast<const float4 *>(p + 4);
-        }
+            for (int i = 0; i < TM; ++i)
+                fa[i] = *reinterpret_cast<const float4 *>(
+                    &As[buf][(wr * WTM + i * 32 + l32) * LDS_STRIDE + koff]);
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
+            for (int j = 0; j < TN; ++j)
+                fb[j] = *reinterpret_cast<const float4 *>(
+                    &Bs[buf][(wc * WTN + j * 32 + l32) * LDS_STRIDE + koff]);
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const float av = s < 4 ? (&fa[i][0].x)[s] : (&fa[i][1].x)[s - 4];
+            for (int s = 0; s < 4; ++s)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const float bv = s < 4 ? (&fb[j][0].x)[s] : (&fb[j][1].x)[s - 4];
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
-                }
-            }
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32((&fa[i].x)[s], (&fb[j].x)[s],
+                                                                         acc[i][j], 0, 0, 0);
         }
         if (c + 1 < nchunks) lstore(buf ^ 1);
         __syncthreads();
@@ -203,15 +204,22 @@ extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
         if (!seg_ok(g.seg[s])) return HREG_ERR_INVALID;
     if (g.R == 0) return HREG_OK;
     hipStream_t st = as_stream(stream);
+    // tile choice: wide tiles (K in 16-deep chunks) for the big layers; 64x64 tiles
+    // with 32-deep K chunks when a 128x128 grid would leave most of the 256 CUs idle
+    // (the small mlp-head GEMMs: 2x fewer serial chunk round trips per block)
+    const long tiles128 = (long)((g.R + 127) / 128) * ((g.N + 127) / 128) * g.batch;
     if (g.N <= 32) {
         dim3 grid((g.R + 255) / 256, (g.N + 31) / 32, g.batch);
-        hipLaunchKernelGGL((gemm_nt_kernel<256, 32, 4, 1>), grid, dim3(256), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<256, 32, 4, 1, 16>), grid, dim3(256), 0, st, g);
     } else if (g.N <= 64) {
         dim3 grid((g.R + 255) / 256, (g.N + 63) / 64, g.batch);
-        hipLaunchKernelGGL((gemm_nt_kernel<256, 64, 4, 1>), grid, dim3(256), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<256, 64, 4, 1, 16>), grid, dim3(256), 0, st, g);
+    } else if (tiles128 < 256) {
+        dim3 grid((g.R + 63) / 64, (g.N + 63) / 64, g.batch);
+        hipLaunchKernelGGL((gemm_nt_kernel<64, 64, 2, 2, 32>), grid, dim3(256), 0, st, g);
     } else {
         dim3 grid((g.R + 127) / 128, (g.N + 127) / 128, g.batch);
-        hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2, 16>), grid, dim3(256), 0, st, g);
     }
     HREG_CHECK_LAUNCH();
     return HREG_OK;
