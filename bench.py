@@ -121,6 +121,26 @@ def cpu_baseline(budget_s: float = 12.0):
                       f"{el:.1f} s wall, numpy BLAS + OpenMP C oracle (oracle/)"}
 
 
+def shard_batch(rank: int, pairs: int, points: int):
+    """Rank r's own pairs (seeded by rank: shards are disjoint, no data exchange)."""
+    from pcd_reg_hregnet_amd import synthetic
+    return synthetic.lidar_batch(pairs, points, seed0=1000 * rank)
+
+
+def max_over_ranks(elapsed: float, device) -> float:
+    """The job's time = the slowest rank's (the only collective: one scalar, after timing)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return elapsed
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_throughput(pairs_per_rank: int, steps: int, world: int, elapsed_max: float):
+    """value = pairs processed by ALL ranks / max-over-ranks wall time (weak scaling)."""
+    return pairs_per_rank * steps * world / elapsed_max
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -143,12 +163,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
 
-    from pcd_reg_hregnet_amd import _lib, engine, synthetic
+    from pcd_reg_hregnet_amd import _lib, engine
     _lib.load()
     net = make_model(device)
     P = net.prepared(device)
     B = args.batch
-    s, d, _, _ = synthetic.lidar_batch(B, args.points, seed0=1000 * rank)
+    s, d, _, _ = shard_batch(rank, B, args.points)
     src = torch.from_numpy(s).to(device)
     dst = torch.from_numpy(d).to(device)
 
@@ -194,12 +214,8 @@ def main():
     timer.enabled = False
     gemm_ms, n_gemm, gemm_flops = timer.result()
 
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    total_pairs = B * args.steps * world
-    value = total_pairs / elapsed
+    elapsed = max_over_ranks(elapsed, device)
+    value = job_throughput(B, args.steps, world, elapsed)
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank == 0:

@@ -187,6 +187,22 @@ int hreg_weighted_svd(const float *src, const float *corres, const float *w, int
 int hreg_transform_points(const float *xyz, const float *R, const float *t, int nb, int n,
                           float *out, void *stream);
 
+/* Fused level-1 grouping stage (KeypointDetector.convs/mlp + attention + DescExtractor
+ * convs + k-max + mlp, layers.py:115-130 and 183-198, with C=64, nsample=32):
+ * one wavefront per group of 32 neighbours, every 1x1-conv+BN+ReLU layer chained
+ * through MFMA accumulators.  table = the folded, fragment-permuted weights
+ * (hreg_group_l1_table_floats() floats, built by engine.l1_table);
+ * geom [G][32] float4 and knn_xyz [G][32][3] from hreg_knn_group ->
+ * kp [G][3], att_feat [G][64] (attentive feature), desc [G][64]. */
+int hreg_group_l1_table_floats(void);
+int hreg_group_l1(const float *table, const float *geom, const float *knn_xyz, int G,
+                  float *kp, float *att_feat, float *desc, void *stream);
+
+/* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
+ * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */
+int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,
+                          int32_t *idx, uint64_t *stamps, void *stream);
+
 /* library build id (for the loaded-.so audit) */
 const char *hreg_version(void);
 

@@ -1,0 +1,152 @@
+"""Host-side logic of the HIP path, checked on the CPU: BN folding, the correspondence
+heads' column permutations, the MFMA fragment tables of the fused level-1 kernel (by
+emulating v_mfma_f32_32x32x2_f32 lane maps), weights, state-dict keys, synthetic data."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import Args, state_dict_torch
+
+
+@pytest.fixture(scope="module")
+def P():
+    from pcd_reg_hregnet_amd import engine
+    from pcd_reg_hregnet_amd.models import HRegNet
+    m = HRegNet(Args())
+    m.load_state_dict(state_dict_torch())
+    return m, engine.PreparedWeights(m.state_dict(), torch.device("cpu"))
+
+
+def test_state_dict_keys_match_reference_checkpoint():
+    """feature_extraction.* keys == ckpt/pretrained/nusc_feats.pth keys (192)."""
+    from pcd_reg_hregnet_amd import weights
+    from pcd_reg_hregnet_amd.models import HRegNet
+    feats = weights.load_feats_npz()
+    assert feats is not None and len(feats) == 192
+    sd = HRegNet(Args()).state_dict()
+    fe = {k[len("feature_extraction."):] for k in sd if k.startswith("feature_extraction.")}
+    assert fe == set(feats)
+    for k, v in feats.items():
+        assert tuple(sd["feature_extraction." + k].shape) == tuple(v.shape), k
+    n_params = sum(p.numel() for p in HRegNet(Args()).parameters())
+    assert n_params == 2467846  # SURVEY.md 5 (DDP all-reduce size)
+
+
+def test_weights_deterministic():
+    a = state_dict_torch()
+    b = state_dict_torch()
+    assert all(torch.equal(a[k], b[k]) for k in a)
+
+
+def test_bn_fold_matches_torch_eval(P):
+    m, prep = P
+    bn = m.feature_extraction.detector_2.convs[1].eval()
+    conv = m.feature_extraction.detector_2.convs[0]
+    x = torch.randn(2, 68, 16, 8)
+    ref = bn(conv(x))
+    lin = prep.det[1][0]
+    acc = torch.einsum("oc,bcmk->bomk", lin.W, x)
+    got = acc * lin.alpha.view(1, -1, 1, 1) + lin.beta.view(1, -1, 1, 1)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("C,kind", [(256, "coarse"), (128, "fine"), (64, "fine")])
+def test_head_column_permutations(C, kind):
+    """W[:, perm] applied to the packed small-feature layout == W applied to the
+    reference concat order (layers.py:364-380, 444-445)."""
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(C)
+    K = 2 * C + (16 if kind == "coarse" else 12)
+    W = rng.normal(size=(8, K))
+    feats_ref = rng.normal(size=(5, K))
+    if kind == "coarse":
+        perm = engine._perm_coarse(C)
+    else:
+        perm = engine._perm_fine(C)
+    assert sorted(perm) == list(range(K))
+    packed = feats_ref[:, perm]
+    np.testing.assert_allclose(packed @ W[:, perm].T, feats_ref @ W.T, rtol=1e-12)
+    # the packed layout the kernels produce: [geom10, w_src, w_dst, (sims4), desc, knn_desc]
+    if kind == "coarse":
+        assert perm[10:16] == [10 + 2 * C, 11 + 2 * C, 12 + 2 * C, 13 + 2 * C, 14 + 2 * C,
+                               15 + 2 * C]
+    else:
+        assert perm[10:12] == [10 + 2 * C, 11 + 2 * C]
+
+
+def _mfma_32x32x2(a_lane, b_lane, acc):
+    """Exact lane semantics of v_mfma_f32_32x32x2_f32 (cdna_hip_programming.md 3):
+    A[i][k] = a[i + 32k], B[k][j] = b[j + 32k], D[i][j] += sum_k A[i][k] B[k][j];
+    acc[l][q] <-> D[(q&3) + 8(q>>2) + 4(l>>5)][l&31]."""
+    A = np.stack([a_lane[:32], a_lane[32:]], 1)          # [32 i][2 k]
+    B = np.stack([b_lane[:32], b_lane[32:]], 0)          # [2 k][32 j]
+    D = A @ B
+    out = acc.copy()
+    for l in range(64):
+        for q in range(16):
+            out[l, q] += D[(q & 3) + 8 * (q >> 2) + 4 * (l >> 5), l & 31]
+    return out
+
+
+def _to_acc(X):
+    """[C=32*T][32 rows] activations -> accumulator layout [T][64 lanes][16]."""
+    T = X.shape[0] // 32
+    acc = np.zeros((T, 64, 16))
+    for t in range(T):
+        for l in range(64):
+            for q in range(16):
+                acc[t, l, q] = X[t * 32 + (q & 3) + 8 * (q >> 2) + 4 * (l >> 5), l & 31]
+    return acc
+
+
+def test_l1_fragment_tables_emulated():
+    """frag_layer / frag_geom reproduce W @ X through the accumulator-chaining order of
+    group_l1.hip (B operand of k-step q = the previous layer's accumulator register q)."""
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(0)
+    # a 64 -> 64 layer (2 input tiles, 2 output tiles) on 32 rows
+    W = rng.normal(size=(64, 64)).astype(np.float32)
+    X = rng.normal(size=(64, 32)).astype(np.float32)
+    frag = engine.frag_layer(torch.from_numpy(W)).numpy().reshape(2, 2, 16, 64)
+    xin = _to_acc(X.astype(np.float64))
+    out = np.zeros((2, 64, 16))
+    for co in range(2):
+        for ct in range(2):
+            for q in range(16):
+                out[co] = _mfma_32x32x2(frag[co, ct, q].astype(np.float64), xin[ct][:, q], out[co])
+    np.testing.assert_allclose(out, _to_acc(W.astype(np.float64) @ X), rtol=1e-10, atol=1e-9)
+    # the first layer (4 geometric channels): k-step s, lane half h -> channel 2h + s
+    W1 = rng.normal(size=(32, 4)).astype(np.float32)
+    G = rng.normal(size=(32, 4)).astype(np.float32)   # [rows][4]
+    f1 = engine.frag_geom(torch.from_numpy(W1)).numpy().reshape(2, 64)
+    acc = np.zeros((64, 16))
+    for s in range(2):
+        b = np.array([G[l & 31, 2 * (l >> 5) + s] for l in range(64)], np.float64)
+        acc = _mfma_32x32x2(f1[s].astype(np.float64), b, acc)
+    np.testing.assert_allclose(acc, _to_acc((W1 @ G.T).astype(np.float64))[0], rtol=1e-6,
+                               atol=1e-6)
+
+
+def test_l1_table_size_matches_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.l1_table.numel() == L.hreg_group_l1_table_floats()
+
+
+def test_synthetic_pairs_deterministic_and_shaped():
+    from pcd_reg_hregnet_amd import synthetic
+    a = synthetic.lidar_batch(2, 4096, seed0=5)
+    b = synthetic.lidar_batch(2, 4096, seed0=5)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    s, d, R, t = a
+    assert s.shape == (2, 4096, 3) and d.shape == (2, 4096, 3) and s.dtype == np.float32
+    np.testing.assert_allclose(R[0] @ R[0].T, np.eye(3), atol=1e-5)
+    assert np.linalg.norm(d, axis=-1).max() <= 80.5
+    # ~2 % exact duplicates exercise FPS/kNN ties
+    u = np.unique(d[0], axis=0).shape[0]
+    assert 0.95 * 4096 < u < 4096
+    # the generator's perturbation is the dataset's: |angle| <= 20 deg, |t| <= 0.5 m per axis
+    ang = np.degrees(np.arccos(np.clip((np.trace(R, axis1=1, axis2=2) - 1) / 2, -1, 1)))
+    assert np.all(ang <= 20 * np.sqrt(3) + 1e-3) and np.all(np.abs(t) <= 0.5)
