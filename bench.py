@@ -52,18 +52,21 @@ def make_model(device):
 # level-1 fused kernel: per group 64 rows x (det 4*32+32*32+32*64, desc same,
 # mlp1 192*32, mlp2 32*64) MACs = 64 * 14592 MAC (layers.py:115-121,183-198)
 L1_FLOPS_PER_GROUP = 2.0 * 64 * (2 * (4 * 32 + 32 * 32 + 32 * 64) + 192 * 32 + 32 * 64)
+# per group: geom 64 x float4 + knn_xyz 64 x 3 in, kp 3 + att_feat 64 + desc 64 out
+L1_BYTES_PER_GROUP = 4.0 * (64 * 4 + 64 * 3 + 3 + 64 + 64)
 
 
 class MfmaTimer:
     """Brackets every fp32-MFMA launch (gemm_nt_kernel, group_l1_kernel) with HIP
-    events on the launch stream and counts its algorithmic FLOPs."""
+    events on the launch stream and counts its algorithmic FLOPs and bytes."""
 
     def __init__(self):
-        self.events = []
-        self.flops = 0.0
+        self.events = {"gemm": [], "l1": []}
+        self.flops = {"gemm": 0.0, "l1": 0.0}
+        self.bytes = {"gemm": 0.0, "l1": 0.0}
         self.enabled = False
 
-    def _timed(self, fn, flops):
+    def _timed(self, kind, fn, flops, nbytes):
         if not self.enabled:
             return fn()
         st = torch.cuda.current_stream()
@@ -72,8 +75,9 @@ class MfmaTimer:
         e0.record(st)
         r = fn()
         e1.record(st)
-        self.events.append((e0, e1))
-        self.flops += flops
+        self.events[kind].append((e0, e1))
+        self.flops[kind] += flops
+        self.bytes[kind] += nbytes
         return r
 
     def install(self):
@@ -82,20 +86,36 @@ class MfmaTimer:
         orig_call = engine.call
 
         def gemm(g):
-            return self._timed(lambda: orig_gemm(g), 2.0 * g.R * g.N * g.K * g.batch)
+            # algorithmic bytes: the A operand as presented (R x K, gathered rows
+            # counted once per use), W and the output, fp32
+            nbytes = 4.0 * g.batch * (g.R * g.K + g.N * g.K + g.R * g.N)
+            return self._timed("gemm", lambda: orig_gemm(g), 2.0 * g.R * g.N * g.K * g.batch,
+                               nbytes)
 
         def call(name, *args):
             if name == "hreg_group_l1":
-                return self._timed(lambda: orig_call(name, *args), L1_FLOPS_PER_GROUP * args[3])
+                G = args[3]
+                return self._timed("l1", lambda: orig_call(name, *args), L1_FLOPS_PER_GROUP * G,
+                                   L1_BYTES_PER_GROUP * G)
             return orig_call(name, *args)
         _lib.gemm = gemm
         engine.call = call
 
-    def result(self):
+    def result(self, kind):
         torch.cuda.synchronize()
-        ms = sum(a.elapsed_time(b) for a, b in self.events)
-        n = len(self.events)
-        return ms, n, self.flops
+        ev = self.events[kind]
+        ms = sum(a.elapsed_time(b) for a, b in ev)
+        return ms, len(ev), self.flops[kind], self.bytes[kind]
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/r1_traffic.json, made by tools/rocpd_summary.py traffic)."""
+    path = os.path.join(REPO, "profiles", "r1_traffic.json")
+    try:
+        return json.load(open(path))["bytes_per_launch"][kernel], os.path.relpath(path, REPO)
+    except Exception:
+        return None, None
 
 
 def cpu_baseline(budget_s: float = 12.0):
@@ -212,28 +232,36 @@ def main():
             pipe.run([(src, dst)] * args.steps)
         torch.cuda.synchronize()
     timer.enabled = False
-    gemm_ms, n_gemm, gemm_flops = timer.result()
+    gemm_ms, n_gemm, gemm_flops, gemm_bytes = timer.result("gemm")
+    l1_ms, n_l1, l1_flops, _ = timer.result("l1")
 
     elapsed = max_over_ranks(elapsed, device)
     value = job_throughput(B, args.steps, world, elapsed)
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank == 0:
-        per_launch_flops = gemm_flops / max(n_gemm, 1)
         per_launch_s = gemm_ms / max(n_gemm, 1) / 1e3
+        per_launch_flops = gemm_flops / max(n_gemm, 1)
         achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
-        roof = {"kernel": "fp32 MFMA family: gemm_nt_kernel + group_l1_kernel "
-                          "(all 1x1-conv/BN/ReLU layers + cosine contraction)",
+        traffic, traffic_src = pmc_traffic("gemm_nt_kernel")
+        roof = {"kernel": "gemm_nt_kernel (all tile instantiations): every 1x1-conv/BN/ReLU "
+                          "layer outside the fused level-1 stage + the cosine contraction",
                 "timing": "HIP events on the launch stream, " + (
                     "instrumented eager pipelined pass of the same steps after the timed "
                     "graph region" if args.executor == "graph" else "inside the timed region"),
                 "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-                "traffic": None,
+                "traffic": None if traffic is None else round(traffic),
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": round(gemm_bytes / max(n_gemm, 1)),
+                "flop_per_launch": round(per_launch_flops),
                 "launches_per_step": n_gemm // args.steps,
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
-                "mfma_ms_per_step": round(gemm_ms / args.steps, 3),
-                "algorithmic_gflop_per_pair": round(gemm_flops / args.steps / B / 1e9, 3)}
+                "gemm_ms_per_step": round(gemm_ms / args.steps, 3),
+                "algorithmic_gflop_per_pair": round(gemm_flops / args.steps / B / 1e9, 3),
+                "group_l1": {"avg_launch_us": round(l1_ms / max(n_l1, 1) * 1e3, 2),
+                             "tflops": round(l1_flops / max(l1_ms, 1e-9) / 1e9, 3),
+                             "gflop_per_pair": round(l1_flops / args.steps / B / 1e9, 3)}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

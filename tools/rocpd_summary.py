@@ -1,0 +1,109 @@
+"""Summaries of rocprofv3 runs for profiles/ (reads the rocpd SQLite output or the
+--output-format csv files).
+
+  kernel stats:  python tools/rocpd_summary.py stats <run_results.db | kernel_stats.csv> <steps> [out.md]
+  HBM traffic:   python tools/rocpd_summary.py traffic <fetch .db|csv> <write .db|csv> [out.md] [out.json]
+
+Traffic follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE come
+from separate --pmc passes (TCC slots 3 + 2 > 4), both in KiB; on gfx950
+FETCH_SIZE counts half the bytes of wide (16 B/lane) coalesced reads -- every HBM
+read of these kernels is a float4 per lane -- so bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024.
+"""
+import csv
+import json
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+FAMILIES = ("gemm_nt_kernel", "group_l1_kernel", "fps_reg_kernel", "knn_group_kernel",
+            "attend_kernel", "group_max_kernel", "knnd_kernel")
+
+
+def short(name):
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+
+
+def kernel_rows(path):
+    """-> list of (name, calls, total_ns)"""
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        agg = defaultdict(lambda: [0, 0.0])
+        for name, dur in c.execute("select name, duration from kernels"):
+            agg[name][0] += 1
+            agg[name][1] += float(dur)
+        return [(n, v[0], v[1]) for n, v in agg.items()]
+    return [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"])) for r in csv.DictReader(open(path))]
+
+
+def counter_values(path, counter):
+    acc = defaultdict(list)
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        q = "select kernel_name, value from counters_collection where counter_name = ?"
+        for name, v in c.execute(q, (counter,)):
+            acc[short(name)].append(float(v))
+    else:
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] == counter:
+                acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return acc
+
+
+def stats(path, steps, out=None):
+    rows = kernel_rows(path)
+    tot = sum(r[2] for r in rows)
+    lines = ["| kernel | calls | calls/step | avg us | ms/step | % |", "|---|---|---|---|---|---|"]
+    for name, calls, ns in sorted(rows, key=lambda r: -r[2]):
+        lines.append(f"| `{short(name)[:90]}` | {calls} | {calls / steps:.1f} | {ns / calls / 1e3:.2f} | "
+                     f"{ns / 1e6 / steps:.3f} | {100 * ns / tot:.1f} |")
+    lines.append(f"| **total kernel time** | | | | {tot / 1e6 / steps:.3f} | 100 |")
+    lines += ["", "| kernel family | calls | avg us | ms/step | % |", "|---|---|---|---|---|"]
+    for fam in FAMILIES:
+        sel = [r for r in rows if fam in r[0]]
+        if sel:
+            c, ns = sum(r[1] for r in sel), sum(r[2] for r in sel)
+            lines.append(f"| `{fam}` | {c} | {ns / c / 1e3:.2f} | {ns / 1e6 / steps:.3f} | "
+                         f"{100 * ns / tot:.1f} |")
+    text = "\n".join(lines)
+    print(text)
+    if out:
+        open(out, "w").write(text + "\n")
+
+
+def traffic(fetch_path, write_path, out=None, out_json=None):
+    fetch = counter_values(fetch_path, "FETCH_SIZE")
+    write = counter_values(write_path, "WRITE_SIZE")
+    lines = ["| kernel | launches | read MB/launch (2 x FETCH_SIZE) | write MB/launch | HBM MB/launch |",
+             "|---|---|---|---|---|"]
+    for name in sorted(fetch, key=lambda n: -sum(fetch[n])):
+        f, w = fetch[name], write.get(name, [0.0])
+        rd = 2 * sum(f) / len(f) * 1024 / 1e6
+        wr = sum(w) / len(w) * 1024 / 1e6
+        lines.append(f"| `{name[:90]}` | {len(f)} | {rd:.3f} | {wr:.3f} | {rd + wr:.3f} |")
+    fam_bytes = {}
+    lines += ["", "| kernel family | launches | HBM bytes/launch |", "|---|---|---|"]
+    for fam in FAMILIES:
+        fs = [v for n, vs in fetch.items() if fam in n for v in vs]
+        ws = [v for n, vs in write.items() if fam in n for v in vs]
+        if fs:
+            b = (2 * sum(fs) / len(fs) + (sum(ws) / len(ws) if ws else 0.0)) * 1024
+            fam_bytes[fam] = b
+            lines.append(f"| `{fam}` | {len(fs)} | {b:.4g} |")
+    text = "\n".join(lines)
+    print(text)
+    if out:
+        open(out, "w").write(text + "\n")
+    if out_json:
+        json.dump({"bytes_per_launch": fam_bytes, "fetch_source": fetch_path,
+                   "write_source": write_path,
+                   "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024, per-launch mean over the family"},
+                  open(out_json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else None)
+    else:
+        traffic(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None,
+                sys.argv[5] if len(sys.argv) > 5 else None)
