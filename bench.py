@@ -172,8 +172,13 @@ def main():
     ap.add_argument("--executor", choices=("graph", "pipeline", "serial"), default="graph",
                     help="graph: pipelined forward replayed as HIP graphs; pipeline: same "
                          "eagerly; serial: no cross-batch overlap")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="graph executor: batches in flight at once, one stream each "
+                         "(a step is still one forward over one batch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
+    if args.executor == "graph" and args.steps % args.lanes:
+        ap.error("--steps must be a multiple of --lanes")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -199,14 +204,14 @@ def main():
     gpipe = None
     if args.executor == "graph":
         with torch.no_grad():
-            gpipe = engine.GraphPipeline(P, src, dst)
+            gpipe = engine.GraphPipeline(P, src, dst, lanes=args.lanes)
 
     def run(n):
         with torch.no_grad():
             if args.executor == "serial":
                 return [engine.hregnet_forward(P, src, dst) for _ in range(n)]
             if args.executor == "graph":
-                return gpipe.run(n)
+                return gpipe.run(-(-n // args.lanes))
             return pipe.run([(src, dst)] * n)
 
     run(args.warmup)
@@ -277,7 +282,9 @@ def main():
             "config": {"workload": f"HRegNet forward (eval), batch={B} pairs/GPU, "
                                    f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])",
                        "executor": args.executor + ("" if args.executor == "serial" else
-                                   " (level-1 FPS of step i+1 overlaps step i)"),
+                                   " (level-1 FPS of step i+1 overlaps step i)") + (
+                                   f", {args.lanes} batches in flight" if args.lanes > 1 and
+                                   args.executor == "graph" else ""),
                        "global_batch": B * world, "points": args.points,
                        "parallelism": f"dp{world} (pairs sharded, no collective)"},
             "roofline": roof,

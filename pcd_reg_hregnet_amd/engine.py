@@ -623,61 +623,98 @@ class GraphPipeline:
     """The pipelined forward captured as HIP graphs (kernel boundaries ~1.5 us
     instead of a host launch each).
 
-    Static inputs ``src``/``dst`` (copy new data in with ``load``) and two
-    level-1 buffer sets A/B.  g_AB = {side stream: stage 1 of the next batch
-    into B ; main: the rest of the forward from A}, g_BA symmetric; replaying
-    them alternately overlaps batch i+1's FPS with batch i inside each graph.
+    ``lanes`` independent batches are in flight at once, each on its own stream
+    inside one graph: the forward is a chain of kernels of very different widths
+    (the WFPS levels and the small head GEMMs occupy a handful of CUs for
+    hundreds of us, the level-2/3 conv GEMMs fill the chip), so a second batch
+    fills one batch's narrow phases.  Per lane: static inputs ``src``/``dst``
+    (copy new data in with ``load``) and two level-1 buffer sets A/B.  g_AB =
+    {lane side stream: stage 1 of the lane's next batch into B ; lane stream: the
+    rest of the forward from A}, g_BA symmetric; replaying them alternately
+    overlaps batch i+1's level-1 FPS with batch i.  Every batch runs the
+    complete forward; outputs are bitwise those of ``hregnet_forward``.
     """
 
-    def __init__(self, P: PreparedWeights, src, dst, use_weights=True):
+    def __init__(self, P: PreparedWeights, src, dst, use_weights=True, lanes: int = 1):
         self.P = P
         self.use_weights = use_weights
+        self.lanes = lanes
         dev = src.device
         B, N, _ = src.shape
-        self.src = src.clone()
-        self.dst = dst.clone()
-        self.bufs = [alloc_stage1(B, N, dev), alloc_stage1(B, N, dev)]
-        self.side = torch.cuda.Stream(device=dev)
+        self.src = [src.clone() for _ in range(lanes)]
+        self.dst = [dst.clone() for _ in range(lanes)]
+        self.bufs = [[alloc_stage1(B, N, dev), alloc_stage1(B, N, dev)] for _ in range(lanes)]
+        self.side = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
+        self.lane_streams = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
         # eager warm-up: library, allocator and workspace shapes
-        stage1_into(self.bufs[0], self.src, self.dst)
-        self._rest(0)
+        stage1_into(self.bufs[0][0], self.src[0], self.dst[0])
+        self._rest(0, 0)
         torch.cuda.synchronize()
         self.pool = torch.cuda.graph_pool_handle()
         self.g_first = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_first, pool=self.pool):
-            stage1_into(self.bufs[0], self.src, self.dst)
+            self._fork(lambda ln: stage1_into(self.bufs[ln][0], self.src[ln], self.dst[ln]))
         self.g_step, self.outs = [], []
         for cur in (0, 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.pool):
-                main = torch.cuda.current_stream()
-                self.side.wait_stream(main)
-                with torch.cuda.stream(self.side):
-                    stage1_into(self.bufs[1 - cur], self.src, self.dst)
-                out = self._rest(cur)
-                main.wait_stream(self.side)
+                out = self._fork(
+                    lambda ln: self._rest(ln, cur),
+                    side=lambda ln: stage1_into(self.bufs[ln][1 - cur], self.src[ln], self.dst[ln]))
             self.g_step.append(g)
             self.outs.append(out)
         self.g_last, self.outs_last = [], []
         for cur in (0, 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.pool):
-                out = self._rest(cur)
+                out = self._fork(lambda ln: self._rest(ln, cur))
             self.g_last.append(g)
             self.outs_last.append(out)
         torch.cuda.synchronize()
 
-    def _rest(self, cur):
-        pts, g = self.bufs[cur]
-        return hregnet_forward(self.P, self.src, self.dst, self.use_weights, l1=g, pts=pts)
+    def _fork(self, body, side=None):
+        """Inside a capture: body(lane) for every lane on its own stream (lane 0 on
+        the capturing stream) and side(lane) on the lane's side stream, all forked
+        from the capturing stream and joined back to it (one level of fork/join:
+        consecutive graph launches on one stream are ordered, so the side work of
+        this launch cannot overlap the previous launch's reads of its buffers).
+        Returns the per-lane results of body."""
+        main = torch.cuda.current_stream()
+        jobs = []
+        for ln in range(self.lanes):
+            if side is not None:
+                jobs.append((self.side[ln], side, ln))
+            jobs.append((None if ln == 0 else self.lane_streams[ln], body, ln))
+        for st, _, _ in jobs:
+            if st is not None:
+                st.wait_stream(main)
+        res = []
+        for st, fn, ln in jobs:
+            if st is None:
+                r = fn(ln)
+            else:
+                with torch.cuda.stream(st):
+                    r = fn(ln)
+            if fn is body:
+                res.append(r)
+        for st, _, _ in jobs:
+            if st is not None:
+                main.wait_stream(st)
+        return res
 
-    def load(self, src, dst):
-        self.src.copy_(src)
-        self.dst.copy_(dst)
+    def _rest(self, ln, cur):
+        pts, g = self.bufs[ln][cur]
+        return hregnet_forward(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g,
+                               pts=pts)
+
+    def load(self, src, dst, lane: int = 0):
+        self.src[lane].copy_(src)
+        self.dst[lane].copy_(dst)
 
     def run(self, steps: int):
-        """Runs `steps` complete forwards of the static batch; returns the last output
-        dict (views into graph-owned memory, valid until the next run)."""
+        """Runs `steps` rounds; a round is one complete forward of every lane's static
+        batch.  Returns the last round's output dict (lanes == 1) or the list of
+        per-lane dicts (views into graph-owned memory, valid until the next run)."""
         if steps <= 0:
             return None
         self.g_first.replay()
@@ -686,4 +723,5 @@ class GraphPipeline:
             self.g_step[cur].replay()
             cur = 1 - cur
         self.g_last[cur].replay()
-        return self.outs_last[cur]
+        out = self.outs_last[cur]
+        return out[0] if self.lanes == 1 else out

@@ -157,3 +157,24 @@ def test_graph_pipeline_matches_eager(net):
         ref2 = engine.hregnet_forward(P, torch.from_numpy(s2).cuda(), torch.from_numpy(d2).cuda())
         torch.cuda.synchronize()
         assert torch.equal(out["rotation"][-1], ref2["rotation"][-1])
+
+
+def test_graph_lanes_match_eager(net):
+    """Two batches in flight (one stream each inside the graph): each lane's output
+    is bitwise the eager forward of its own batch."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    data = [synthetic.lidar_batch(2, 4096, seed0=sd)[:2] for sd in (50, 51)]
+    dev = [(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()) for s, d in data]
+    with torch.no_grad():
+        gp = engine.GraphPipeline(P, dev[0][0], dev[0][1], lanes=2)
+        gp.load(dev[1][0], dev[1][1], lane=1)
+        refs = [engine.hregnet_forward(P, s, d) for s, d in dev]
+        for steps in (1, 3):
+            outs = gp.run(steps)
+            torch.cuda.synchronize()
+            for out, ref in zip(outs, refs):
+                for i in range(3):
+                    assert torch.equal(out["rotation"][i], ref["rotation"][i])
+                    assert torch.equal(out["translation"][i], ref["translation"][i])
+                assert torch.equal(out["src_feats"]["desc_3"], ref["src_feats"]["desc_3"])
