@@ -54,6 +54,11 @@ def make_model(device):
 L1_FLOPS_PER_GROUP = 2.0 * 64 * (2 * (4 * 32 + 32 * 32 + 32 * 64) + 192 * 32 + 32 * 64)
 # per group: geom 64 x float4 + knn_xyz 64 x 3 in, kp 3 + att_feat 64 + desc 64 out
 L1_BYTES_PER_GROUP = 4.0 * (64 * 4 + 64 * 3 + 3 + 64 + 64)
+# level-2 fused kernel: 32 rows x (det 68*64+64*64+64*128, desc same, mlp1 384*64,
+# mlp2 64*128) MACs; bytes: geom 32 x float4, knn_xyz 32 x 3, gidx 32, gathered
+# features 32 x 64, out kp 3 + att_feat 128 + desc 128
+L2_FLOPS_PER_GROUP = 2.0 * 32 * (2 * (68 * 64 + 64 * 64 + 64 * 128) + 384 * 64 + 64 * 128)
+L2_BYTES_PER_GROUP = 4.0 * (32 * 4 + 32 * 3 + 32 + 32 * 64 + 3 + 128 + 128)
 
 
 class MfmaTimer:
@@ -61,9 +66,9 @@ class MfmaTimer:
     events on the launch stream and counts its algorithmic FLOPs and bytes."""
 
     def __init__(self):
-        self.events = {"gemm": [], "l1": []}
-        self.flops = {"gemm": 0.0, "l1": 0.0}
-        self.bytes = {"gemm": 0.0, "l1": 0.0}
+        self.events = {"gemm": [], "l1": [], "l2": []}
+        self.flops = {"gemm": 0.0, "l1": 0.0, "l2": 0.0}
+        self.bytes = {"gemm": 0.0, "l1": 0.0, "l2": 0.0}
         self.enabled = False
 
     def _timed(self, kind, fn, flops, nbytes):
@@ -97,6 +102,10 @@ class MfmaTimer:
                 G = args[3]
                 return self._timed("l1", lambda: orig_call(name, *args), L1_FLOPS_PER_GROUP * G,
                                    L1_BYTES_PER_GROUP * G)
+            if name == "hreg_group_l2":
+                G = args[5]
+                return self._timed("l2", lambda: orig_call(name, *args), L2_FLOPS_PER_GROUP * G,
+                                   L2_BYTES_PER_GROUP * G)
             return orig_call(name, *args)
         _lib.gemm = gemm
         engine.call = call
@@ -239,6 +248,7 @@ def main():
     timer.enabled = False
     gemm_ms, n_gemm, gemm_flops, gemm_bytes = timer.result("gemm")
     l1_ms, n_l1, l1_flops, _ = timer.result("l1")
+    l2_ms, n_l2, l2_flops, _ = timer.result("l2")
 
     elapsed = max_over_ranks(elapsed, device)
     value = job_throughput(B, args.steps, world, elapsed)
@@ -250,7 +260,7 @@ def main():
         achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
         traffic, traffic_src = pmc_traffic("gemm_nt_kernel")
         roof = {"kernel": "gemm_nt_kernel (all tile instantiations): every 1x1-conv/BN/ReLU "
-                          "layer outside the fused level-1 stage + the cosine contraction",
+                          "layer outside the fused level-1/2 stages + the cosine contraction",
                 "timing": "HIP events on the launch stream, " + (
                     "instrumented eager pipelined pass of the same steps after the timed "
                     "graph region" if args.executor == "graph" else "inside the timed region"),
@@ -266,7 +276,10 @@ def main():
                 "algorithmic_gflop_per_pair": round(gemm_flops / args.steps / B / 1e9, 3),
                 "group_l1": {"avg_launch_us": round(l1_ms / max(n_l1, 1) * 1e3, 2),
                              "tflops": round(l1_flops / max(l1_ms, 1e-9) / 1e9, 3),
-                             "gflop_per_pair": round(l1_flops / args.steps / B / 1e9, 3)}}
+                             "gflop_per_pair": round(l1_flops / args.steps / B / 1e9, 3)},
+                "group_l2": {"avg_launch_us": round(l2_ms / max(n_l2, 1) * 1e3, 2),
+                             "tflops": round(l2_flops / max(l2_ms, 1e-9) / 1e9, 3),
+                             "gflop_per_pair": round(l2_flops / args.steps / B / 1e9, 3)}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

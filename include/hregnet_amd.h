@@ -198,6 +198,17 @@ int hreg_group_l1_table_floats(void);
 int hreg_group_l1(const float *table, const float *geom, const float *knn_xyz, int G,
                   float *kp, float *att_feat, float *desc, void *stream);
 
+/* Fused level-2 grouping stage (same layers as hreg_group_l1 with C_in = 4 + 64,
+ * convs 68->64->64->128, mlp 384->64->128, nsample = 32): one wavefront per group.
+ * table = hreg_group_l2_table_floats() floats (engine.l2_table); geom [G][32] float4
+ * and knn_xyz [G][32][3] from hreg_knn_group; gidx [G*32] rows of feats
+ * [*][64] (the level-1 attentive features, 16-byte aligned) ->
+ * kp [G][3], att_feat [G][128], desc [G][128]. */
+int hreg_group_l2_table_floats(void);
+int hreg_group_l2(const float *table, const float *geom, const float *knn_xyz,
+                  const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
+                  float *desc, void *stream);
+
 /* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */
 int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,

@@ -124,3 +124,48 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
     return v;
 }
+
+// ------------------------------------------- half-wave (32-lane) reductions --
+// Sum / max over the 32 lanes of each wave half on the VALU (DPP), instead of
+// __shfl_xor's ds_bpermute round trips through the LDS crossbar: quad_perm
+// [1,0,3,2], [2,3,0,1], row_half_mirror and row_mirror reduce each 16-lane row,
+// row_bcast:15 (rows 1 and 3 only) adds row 0 / row 2.  The result is valid in
+// lanes 16..31 (half 0) and 48..63 (half 1); half_bcast() spreads it.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_mov(float v, float old) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
+                                                      ROW_MASK, 0xf, false));
+}
+// full-mask DPP move (every lane written): lets the compiler fold it into v_add_f32_dpp
+template <int CTRL>
+__device__ __forceinline__ float dpp_all(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_all_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ float half_sum_hi(float v) {
+    v = fadd_rn(v, dpp_all<0xb1>(v));
+    v = fadd_rn(v, dpp_all<0x4e>(v));
+    v = fadd_rn(v, dpp_all<0x141>(v));
+    v = fadd_rn(v, dpp_all<0x140>(v));
+    return fadd_rn(v, dpp_mov<0x142, 0xa>(v, 0.f));
+}
+// max of non-negative floats (ReLU outputs): their IEEE bit patterns order like
+// signed integers, so the reduction runs on v_max_i32 (no NaN canonicalisation)
+__device__ __forceinline__ float half_max_hi_nonneg(float f) {
+    int v = __float_as_int(f);
+    v = max(v, dpp_all_i<0xb1>(v));
+    v = max(v, dpp_all_i<0x4e>(v));
+    v = max(v, dpp_all_i<0x141>(v));
+    v = max(v, dpp_all_i<0x140>(v));
+    v = max(v, __builtin_amdgcn_update_dpp((int)0x80000000, v, 0x142, 0xa, 0xf, false));
+    return __int_as_float(v);
+}
+// the half's reduced value (from lane 31 / 63) in every lane of that half
+__device__ __forceinline__ float half_bcast(float v, int h) {
+    const float lo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 31));
+    const float hi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+    return h ? hi : lo;
+}

@@ -166,31 +166,42 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         float wx = 0.f, wy = 0.f, wz = 0.f;
         pick_slot<0, 2 * S2>(sl, wl, PX, PY, PZ, wx, wy, wz);
         if constexpr (STAMP) t2 = stamp();
-        const int buf = j & 1;
-        if (lane == 0) {
-            s_cand[buf][wv] = make_float4(wx, wy, wz, wmax);
-            s_k[buf][wv] = kwin;
-        }
-        lds_barrier();
-        if constexpr (STAMP) t3 = stamp();
-        float4 c = make_float4(0.f, 0.f, 0.f, -__builtin_huge_valf());
-        int ck = 0;
-        if (lane < NW) {
-            c = s_cand[buf][lane];
-            ck = s_k[buf][lane];
-        }
-        const float gmax = readlane_f(row_max16(c.w, inf), 0);
-        const uint64_t ghit = __ballot(lane < NW && c.w == gmax);
-        const int gw = (int)__builtin_ctzll(ghit);  // lowest wave = lowest reference order
         int old;
-        if (gmax > -1.0f) {
-            old = __builtin_amdgcn_readlane(ck, gw);
-            x1 = readlane_f(c.x, gw);
-            y1 = readlane_f(c.y, gw);
-            z1 = readlane_f(c.z, gw);
-        } else {  // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0)
-            old = 0;
-            x1 = P[0]; y1 = P[1]; z1 = P[2];
+        if constexpr (NW == 1) {
+            // one wave: its winner is the block winner, no LDS round trip or barrier
+            if (wmax > -1.0f) {
+                old = kwin;
+                x1 = wx; y1 = wy; z1 = wz;
+            } else {  // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0)
+                old = 0;
+                x1 = P[0]; y1 = P[1]; z1 = P[2];
+            }
+        } else {
+            const int buf = j & 1;
+            if (lane == 0) {
+                s_cand[buf][wv] = make_float4(wx, wy, wz, wmax);
+                s_k[buf][wv] = kwin;
+            }
+            lds_barrier();
+            if constexpr (STAMP) t3 = stamp();
+            float4 c = make_float4(0.f, 0.f, 0.f, -__builtin_huge_valf());
+            int ck = 0;
+            if (lane < NW) {
+                c = s_cand[buf][lane];
+                ck = s_k[buf][lane];
+            }
+            const float gmax = readlane_f(row_max16(c.w, inf), 0);
+            const uint64_t ghit = __ballot(lane < NW && c.w == gmax);
+            const int gw = (int)__builtin_ctzll(ghit);  // lowest wave = lowest reference order
+            if (gmax > -1.0f) {
+                old = __builtin_amdgcn_readlane(ck, gw);
+                x1 = readlane_f(c.x, gw);
+                y1 = readlane_f(c.y, gw);
+                z1 = readlane_f(c.z, gw);
+            } else {  // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0)
+                old = 0;
+                x1 = P[0]; y1 = P[1]; z1 = P[2];
+            }
         }
         if (tid == 0) {
             idx_out[(size_t)cloud * m + j] = old;
@@ -314,6 +325,7 @@ bool launch_reg(int T, int G, int QT, int b, int n, int m, int bs, int L, const 
     HREG_FPS_CASE(512, 1, 1) HREG_FPS_CASE(512, 1, 2)
     HREG_FPS_CASE(256, 4, 1) HREG_FPS_CASE(256, 1, 1) HREG_FPS_CASE(256, 1, 2)
     HREG_FPS_CASE(128, 4, 1) HREG_FPS_CASE(128, 1, 1) HREG_FPS_CASE(128, 1, 2)
+    HREG_FPS_CASE(64, 16, 1) HREG_FPS_CASE(64, 8, 1) HREG_FPS_CASE(128, 8, 1)
     HREG_FPS_CASE(64, 4, 1) HREG_FPS_CASE(64, 1, 1) HREG_FPS_CASE(64, 1, 2)
 #undef HREG_FPS_CASE
     return false;
@@ -325,7 +337,15 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     const int Q = (n + bs - 1) / bs;
     QT = 1;
     while (QT < Q) QT <<= 1;
-    if (Q == 1 && bs >= 256) { T = bs / 4; G = 4; QT = 1; return; }
+    if (Q == 1 && bs >= 256) {
+        // one wave (no barrier) while its scan stays short; 4 waves at bs = 1024
+        // (measured, 16 clouds: n=512 0.130 ms at 1 wave vs 0.150 at 2; n=1024 0.300 ms
+        // at 4 waves vs 0.331 at 1)
+        T = bs >= 1024 ? bs / 4 : 64;
+        G = bs / T;
+        QT = 1;
+        return;
+    }
     if (bs >= 64) { T = bs; G = 1; }
     else { T = 64; G = 1; }
     // per-slot registers (x, y, z, temp[, w]) must fit the VGPR budget

@@ -35,6 +35,7 @@ LEVELS = (
 )
 K_HEAD = 8  # CoarseReg/FineReg k (models.py:71-73)
 FUSED_L1 = True  # level 1 through the fused group_l1 kernel (False: layer-by-layer GEMMs)
+FUSED_L2 = True  # level 2 through the fused group_l2 kernel
 
 
 @dataclass
@@ -127,8 +128,9 @@ class PreparedWeights:
         for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64)):
             self.fine[name] = (_stack(sd, name + ".convs_1", 3, _perm_fine(C)), _mlp_head(sd, name))
         self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
+        self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
-                     "coarse_head", "fine", "l1_table"):
+                     "coarse_head", "fine", "l1_table", "l2_table"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
 
@@ -152,6 +154,32 @@ def frag_geom(W: torch.Tensor) -> torch.Tensor:
     s = torch.arange(2).view(-1, 1)
     lane = torch.arange(64).view(1, -1)
     return W[lane & 31, 2 * (lane >> 5) + s].reshape(-1)
+
+
+def frag_input(W: torch.Tensor) -> torch.Tensor:
+    """First layer over [geom 4 | feature CF] (group_l2.hip conv_in): geom k-step s, lane
+    half h -> channel 2h + s, [co][s][lane]; feature k-step s, half h -> channel
+    4 + h*CF/2 + s, [co][s][lane].  Returns (geom fragments, feature fragments)."""
+    Cout, K = W.shape
+    TF = (K - 4) // 2
+    co = torch.arange(Cout // 32).view(-1, 1, 1)
+    lane = torch.arange(64).view(1, 1, -1)
+    rows = co * 32 + (lane & 31)
+    sg = torch.arange(2).view(1, -1, 1)
+    geom = W[rows, 2 * (lane >> 5) + sg]
+    sf = torch.arange(TF).view(1, -1, 1)
+    feat = W[rows, 4 + (lane >> 5) * TF + sf]
+    return geom.reshape(-1), feat.reshape(-1)
+
+
+def l2_table(det, desc, mlp) -> torch.Tensor:
+    """Weight/epilogue table of the fused level-2 kernel (layout: group_l2.hip Cfg)."""
+    parts = [*frag_input(det[0].W), frag_layer(det[1].W), frag_layer(det[2].W),
+             *frag_input(desc[0].W), frag_layer(desc[1].W), frag_layer(desc[2].W),
+             frag_layer(mlp[0].W), frag_layer(mlp[1].W)]
+    for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
 
 
 def l1_table(det, desc, mlp) -> torch.Tensor:
@@ -374,6 +402,18 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         att_feat = _empty(G, LEVELS[0][3][-1], device=dev)
         desc = _empty(G, LEVELS[0][5], device=dev)
         call("hreg_group_l1", P.l1_table, geom, kx, G, kp, att_feat, desc, _stream())
+        m1, m2, w3, b3 = P.det_head[lvl]
+        s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)
+        s = gemm([_seg(s, 0, s.shape[1])], m2, G)
+        sig, wnext = head_out(s, s.shape[1], nb, M, w3, b3, _lib.HREG_HEAD_SOFTPLUS,
+                              want_weights=True)
+        return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
+    if lvl == 1 and FUSED_L2:
+        dev = xyz.device
+        kp = _empty(G, 3, device=dev)
+        att_feat = _empty(G, LEVELS[1][3][-1], device=dev)
+        desc = _empty(G, LEVELS[1][5], device=dev)
+        call("hreg_group_l2", P.l2_table, geom, kx, gidx, feats, G, kp, att_feat, desc, _stream())
         m1, m2, w3, b3 = P.det_head[lvl]
         s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)
         s = gemm([_seg(s, 0, s.shape[1])], m2, G)

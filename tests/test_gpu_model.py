@@ -178,3 +178,34 @@ def test_graph_lanes_match_eager(net):
                     assert torch.equal(out["rotation"][i], ref["rotation"][i])
                     assert torch.equal(out["translation"][i], ref["translation"][i])
                 assert torch.equal(out["src_feats"]["desc_3"], ref["src_feats"]["desc_3"])
+
+
+@pytest.mark.parametrize("lvl", [0, 1])
+def test_fused_level_matches_layerwise(net, lvl):
+    """The fused level kernels (group_l1 / group_l2: activations in MFMA accumulators)
+    against the layer-by-layer GEMM path on the same grouping; fp32 summation order
+    differs, so within 1e-4."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    s, _, _, _ = synthetic.lidar_batch(2, 4096, seed0=60)
+    pts = torch.from_numpy(s).cuda()
+    with torch.no_grad():
+        feats = w = None
+        xyz = pts
+        for level in range(lvl):
+            kp, _, att, _, w, _ = engine.keypoint_level(P, level, xyz, feats, w)
+            xyz, feats = kp, att
+        grouped = engine.grouping(xyz, lvl, w)
+        flag = "FUSED_L1" if lvl == 0 else "FUSED_L2"
+        outs = []
+        for fused in (True, False):
+            old = getattr(engine, flag)
+            setattr(engine, flag, fused)
+            try:
+                outs.append(engine.keypoint_level(P, lvl, xyz, feats, w, grouped=grouped))
+            finally:
+                setattr(engine, flag, old)
+    torch.cuda.synchronize()
+    (kp_f, sig_f, att_f, desc_f, w_f, _), (kp_r, sig_r, att_r, desc_r, w_r, _) = outs
+    for a, b in ((kp_f, kp_r), (sig_f, sig_r), (att_f, att_r), (desc_f, desc_r)):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)

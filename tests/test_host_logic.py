@@ -150,3 +150,34 @@ def test_synthetic_pairs_deterministic_and_shaped():
     # the generator's perturbation is the dataset's: |angle| <= 20 deg, |t| <= 0.5 m per axis
     ang = np.degrees(np.arccos(np.clip((np.trace(R, axis1=1, axis2=2) - 1) / 2, -1, 1)))
     assert np.all(ang <= 20 * np.sqrt(3) + 1e-3) and np.all(np.abs(t) <= 0.5)
+
+
+def test_l2_input_fragments_emulated():
+    """frag_input: the first level-2 layer over [geom 4 | feature CF] as group_l2.hip feeds
+    it (geom k-step s, half h -> channel 2h+s; feature k-step s, half h -> 4 + h*CF/2 + s)."""
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(1)
+    CF, Cout = 64, 64
+    W = rng.normal(size=(Cout, 4 + CF)).astype(np.float32)
+    X = rng.normal(size=(32, 4 + CF)).astype(np.float32)     # [rows][channels]
+    fg, ff = (t.numpy() for t in engine.frag_input(torch.from_numpy(W)))
+    T1, TF = Cout // 32, CF // 2
+    fg = fg.reshape(T1, 2, 64)
+    ff = ff.reshape(T1, TF, 64)
+    acc = np.zeros((T1, 64, 16))
+    for co in range(T1):
+        for s in range(2):
+            b = np.array([X[l & 31, 2 * (l >> 5) + s] for l in range(64)], np.float64)
+            acc[co] = _mfma_32x32x2(fg[co, s].astype(np.float64), b, acc[co])
+        for s in range(TF):
+            b = np.array([X[l & 31, 4 + (l >> 5) * TF + s] for l in range(64)], np.float64)
+            acc[co] = _mfma_32x32x2(ff[co, s].astype(np.float64), b, acc[co])
+    np.testing.assert_allclose(acc, _to_acc((W.astype(np.float64) @ X.T.astype(np.float64))),
+                               rtol=1e-9, atol=1e-9)
+
+
+def test_l2_table_size_matches_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.l2_table.numel() == L.hreg_group_l2_table_floats()

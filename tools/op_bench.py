@@ -51,8 +51,23 @@ def main():
         res["knn_group_l1_ms"] = timeit(lambda: engine.knn_group(q, p, 64))
         d = torch.from_numpy(rng.normal(size=(a.b // 2, 256, 256)).astype(np.float32)).cuda()
         res["knn_desc_ms"] = timeit(lambda: engine.knn_idx32(d, d, 8))
-    print({k: round(v, 4) for k, v in res.items()}, "HREG_FPS_THREADS=",
-          os.environ.get("HREG_FPS_THREADS"))
+    if a.what in ("l2", "all"):
+        L = _lib.load()
+        G = a.b * 512
+        nt = L.hreg_group_l2_table_floats()
+        tb = torch.from_numpy(rng.normal(0, 0.1, nt).astype(np.float32)).cuda()
+        geom = torch.from_numpy(rng.normal(size=(G * 32, 4)).astype(np.float32)).cuda()
+        kx = torch.from_numpy(rng.normal(size=(G * 32, 3)).astype(np.float32)).cuda()
+        gidx = torch.from_numpy(rng.integers(0, a.b * 1024, G * 32).astype(np.int32)).cuda()
+        feats = torch.from_numpy(rng.normal(size=(a.b * 1024, 64)).astype(np.float32)).cuda()
+        kp = torch.empty(G, 3, device="cuda")
+        att = torch.empty(G, 128, device="cuda")
+        desc = torch.empty(G, 128, device="cuda")
+        res["group_l2_ms"] = timeit(lambda: _lib.call("hreg_group_l2", tb, geom, kx, gidx, feats, G,
+                                                      kp, att, desc, _lib.stream_handle()))
+        flops = 2.0 * 32 * (2 * (68 * 64 + 64 * 64 + 64 * 128) + 384 * 64 + 64 * 128) * G
+        res["group_l2_tflops"] = flops / res["group_l2_ms"] / 1e9
+    print({k: round(v, 4) for k, v in res.items()})
 
 
 if __name__ == "__main__" and "stamps" not in sys.argv:
