@@ -22,6 +22,12 @@
 // (keypoint 3, attentive feature C3, descriptor CM2 floats) reach HBM.
 #include "common.h"
 
+// tools/l2_experiment.py builds variants: 1 = no epilogue / reductions (MFMA +
+// loads only), 2 = additionally no weight loads (MFMA issue structure only)
+#ifndef HREG_L2_EXP
+#define HREG_L2_EXP 0
+#endif
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -66,22 +72,43 @@ __device__ __forceinline__ int chan(int co, int q, int h) {
     return co * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
 }
 
-// acc[co] += sum_{step < NSTEP} A(co, step) x B(step) on v_mfma_f32_32x32x2_f32, with
-// the A fragments (wf + frag(co, step) * 64 + lane, L2-resident) software-
-// pipelined one window of WIN k-steps ahead: the loads of window w+1 are issued
-// before the MFMAs of window w, so the ~200-500-cycle L2 latency hides behind
-// WIN * COUT_T * 64 cycles of MFMA work (sched_barrier keeps that order).
-template <int NSTEP, int COUT_T, int WIN, class Frag, class BVal>
-__device__ __forceinline__ void mfma_pipe(const gfloat *__restrict__ wf, int lane, Frag frag, BVal bval,
-                                          f32x16 (&acc)[COUT_T]) {
-    static_assert(NSTEP % WIN == 0, "window");
+// ------------------------------------------------------------------------
+// The A fragments of one group form a fixed sequence of ~1032 loads.  They are
+// streamed one window ahead of the MFMAs that use them -- across layer
+// boundaries too: the last window of each call loads the first window of the
+// next call (into `carry`), and the last call of a group the first window of
+// the next group, so no call starts on a cold L2 round trip.
+
+constexpr int CARRY = 16;  // max WIN * COUT_T
+
+// fragment f of call: index base + co * stride + step, in 64-float fragments
+struct FragSeq {
+    int base, stride;
+};
+
+__device__ __forceinline__ float ldfrag(const gfloat *__restrict__ wf, int f, int lane) {
+    return HREG_L2_EXP == 2 ? (float)(lane + f) : wf[f * 64 + lane];
+}
+
+template <int COUT_T>
+constexpr int win_for() { return COUT_T >= 4 ? 4 : 8; }
+
+// acc[co] += sum_{st < NSTEP} A(co, st) x bval(st) on v_mfma_f32_32x32x2_f32.
+// cin: this call's first window (loaded by the previous call); cout: receives the
+// first window (NWIN steps x NCOUT tiles) of the next call `nf`.
+template <int NSTEP, int COUT_T, int NCOUT, int NWIN, class BVal>
+__device__ __forceinline__ void mfma_pipe(const gfloat *__restrict__ wf, int lane, FragSeq f, BVal bval,
+                                          f32x16 (&acc)[COUT_T], const float (&cin)[CARRY],
+                                          FragSeq nf, float (&cout)[CARRY]) {
+    constexpr int WIN = NSTEP < win_for<COUT_T>() ? NSTEP : win_for<COUT_T>();
+    static_assert(NSTEP % WIN == 0 && WIN * COUT_T <= CARRY && NWIN * NCOUT <= CARRY, "window");
     constexpr int NW = NSTEP / WIN;
     // two fragment buffers used alternately (window index is compile-time: no copies)
     float buf[2][WIN][COUT_T];
 #pragma unroll
     for (int s = 0; s < WIN; ++s)
 #pragma unroll
-        for (int co = 0; co < COUT_T; ++co) buf[0][s][co] = wf[frag(co, s) * 64 + lane];
+        for (int co = 0; co < COUT_T; ++co) buf[0][s][co] = cin[s * COUT_T + co];
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
         if (w + 1 < NW) {
@@ -89,7 +116,13 @@ __device__ __forceinline__ void mfma_pipe(const gfloat *__restrict__ wf, int lan
             for (int s = 0; s < WIN; ++s)
 #pragma unroll
                 for (int co = 0; co < COUT_T; ++co)
-                    buf[(w + 1) & 1][s][co] = wf[frag(co, (w + 1) * WIN + s) * 64 + lane];
+                    buf[(w + 1) & 1][s][co] = ldfrag(wf, f.base + co * f.stride + (w + 1) * WIN + s, lane);
+        } else {
+#pragma unroll
+            for (int s = 0; s < NWIN; ++s)
+#pragma unroll
+                for (int co = 0; co < NCOUT; ++co)
+                    cout[s * NCOUT + co] = ldfrag(wf, nf.base + co * nf.stride + s, lane);
         }
 #pragma unroll
         for (int s = 0; s < WIN; ++s) {
@@ -102,27 +135,12 @@ __device__ __forceinline__ void mfma_pipe(const gfloat *__restrict__ wf, int lan
     }
 }
 
-template <int COUT_T>
-constexpr int win_for() { return COUT_T >= 4 ? 4 : 8; }
-
-// acc[co] += sum over input tiles ct of W-fragments x in[ct] (accumulator layout);
-// fragment block of (co, ct) at wf + ((co * CIN_ALL + CT0 + ct) * 16 + q) * 64
-template <int CIN_T, int COUT_T, int CIN_ALL, int CT0, bool SCALED>
-__device__ __forceinline__ void mfma_accum(const gfloat *__restrict__ wf, int lane,
-                                           const f32x16 (&in)[CIN_T], f32x16 (&acc)[COUT_T],
-                                           float scale = 1.f) {
-    mfma_pipe<CIN_T * 16, COUT_T, win_for<COUT_T>()>(
-        wf, lane, [](int co, int st) { return (co * CIN_ALL + CT0 + (st >> 4)) * 16 + (st & 15); },
-        [&](int st) {
-            float b = in[st >> 4][st & 15];
-            if (SCALED) b = fmul_rn(b, scale);
-            return b;
-        },
-        acc);
-}
+template <int NSTEP, int COUT_T>
+constexpr int first_win() { return NSTEP < win_for<COUT_T>() ? NSTEP : win_for<COUT_T>(); }
 
 template <int COUT_T>
 __device__ __forceinline__ void epilogue(const float *ab, int lane, f32x16 (&acc)[COUT_T]) {
+    if (HREG_L2_EXP) return;
     const int h = lane >> 5;
     constexpr int C = COUT_T * 32;
 #pragma unroll
@@ -134,37 +152,40 @@ __device__ __forceinline__ void epilogue(const float *ab, int lane, f32x16 (&acc
         }
 }
 
-// first conv over [geom (4) | gathered feature (CF)]
-template <class K>
-__device__ __forceinline__ void conv_in(const gfloat *__restrict__ tb, const float *eb, int fg, int ff, int e, int lane,
-                                        float2 gin, const float4 (&fin)[K::TF / 4],
-                                        f32x16 (&acc)[K::T1]) {
+template <int N>
+__device__ __forceinline__ void zero_tiles(f32x16 (&t)[N]) {
 #pragma unroll
-    for (int co = 0; co < K::T1; ++co) acc[co] = zero16();
-    // geom part: 2 k-steps (channel 2h + s); feature part: TF k-steps (channel h*TF + s)
-    mfma_pipe<2, K::T1, 2>(
-        tb + fg, lane, [](int co, int st) { return co * 2 + st; },
-        [&](int st) { return st == 0 ? gin.x : gin.y; }, acc);
-    mfma_pipe<K::TF, K::T1, win_for<K::T1>()>(
-        tb + ff, lane, [](int co, int st) { return co * K::TF + st; },
-        [&](int st) { return (&fin[st >> 2].x)[st & 3]; }, acc);
-    epilogue<K::T1>(eb + e, lane, acc);
+    for (int i = 0; i < N; ++i) t[i] = zero16();
 }
 
-template <class K>
-__device__ __forceinline__ void conv_stack(const gfloat *__restrict__ tb, const float *eb, int fg, int ff, int f2, int f3,
-                                           int e1, int e2, int e3, int lane, float2 gin,
-                                           const float4 (&fin)[K::TF / 4], f32x16 (&out)[K::T3]) {
-    f32x16 h1[K::T1], h2[K::T1];
-    conv_in<K>(tb, eb, fg, ff, e1, lane, gin, fin, h1);
-#pragma unroll
-    for (int co = 0; co < K::T1; ++co) h2[co] = zero16();
-    mfma_accum<K::T1, K::T1, K::T1, 0, false>(tb + f2, lane, h1, h2);
-    epilogue<K::T1>(eb + e2, lane, h2);
-#pragma unroll
-    for (int co = 0; co < K::T3; ++co) out[co] = zero16();
-    mfma_accum<K::T1, K::T3, K::T1, 0, false>(tb + f3, lane, h2, out);
-    epilogue<K::T3>(eb + e3, lane, out);
+// conv stack [geom 4 | gathered feature CF] -> C1 -> C1 -> C3 (+ BN/ReLU epilogues).
+// Offsets (in floats) of the stack's four fragment blocks and three epilogues;
+// NC/NWN/next describe the call that follows the stack (for its prefetch).
+template <class K, int NC, int NWN>
+__device__ __forceinline__ void conv_stack(const gfloat *__restrict__ tb, const float *eb, int fg, int ff,
+                                           int f2, int f3, int e1, int e2, int e3, int lane, float2 gin,
+                                           const float4 (&fin)[K::TF / 4], f32x16 (&out)[K::T3],
+                                           const float (&cin)[CARRY], FragSeq next,
+                                           float (&cout)[CARRY]) {
+    constexpr int T1 = K::T1, T3 = K::T3, TF = K::TF;
+    const FragSeq sg{fg / 64, 2}, sf{ff / 64, TF}, s2{f2 / 64, T1 * 16}, s3{f3 / 64, T1 * 16};
+    f32x16 h1[T1], h2[T1];
+    float c1[CARRY], c2[CARRY], c3[CARRY];
+    zero_tiles(h1);
+    // geom part: 2 k-steps (channel 2h + s); feature part: TF k-steps (channel h*TF + s)
+    mfma_pipe<2, T1, T1, first_win<TF, T1>()>(
+        tb, lane, sg, [&](int st) { return st == 0 ? gin.x : gin.y; }, h1, cin, sf, c1);
+    mfma_pipe<TF, T1, T1, first_win<T1 * 16, T1>()>(
+        tb, lane, sf, [&](int st) { return (&fin[st >> 2].x)[st & 3]; }, h1, c1, s2, c2);
+    epilogue<T1>(eb + e1, lane, h1);
+    zero_tiles(h2);
+    mfma_pipe<T1 * 16, T1, T3, first_win<T1 * 16, T3>()>(
+        tb, lane, s2, [&](int st) { return h1[st >> 4][st & 15]; }, h2, c2, s3, c3);
+    epilogue<T1>(eb + e2, lane, h2);
+    zero_tiles(out);
+    mfma_pipe<T1 * 16, T3, NC, NWN>(
+        tb, lane, s3, [&](int st) { return h2[st >> 4][st & 15]; }, out, c3, next, cout);
+    epilogue<T3>(eb + e3, lane, out);
 }
 
 // one channel tile of a per-group result reduced over the rows (valid in lanes 31 /
@@ -184,6 +205,7 @@ __global__ __launch_bounds__(256, 2) void group_l2_kernel(
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
     float *__restrict__ att_feat, float *__restrict__ desc) {
     constexpr int CF = K::TF * 2, C3 = K::T3 * 32, CM2 = K::TM2 * 32;
+    constexpr int T1 = K::T1, T3 = K::T3, TM1 = K::TM1, TM2 = K::TM2;
     constexpr int NE = K::TABLE - K::F_END;
     // epilogue (alpha, beta) of every layer in LDS: LDS-indexed like the table so the
     // conv helpers take one base pointer (ep - F_END)
@@ -193,6 +215,23 @@ __global__ __launch_bounds__(256, 2) void group_l2_kernel(
     const float *eb = ep - K::F_END;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int h = lane >> 5, j = lane & 31;
+
+    // the group's call sequence (fragment blocks, see Cfg)
+    const FragSeq det_g{K::F_DG / 64, 2}, desc_g{K::F_EG / 64, 2};
+    const FragSeq m1x2{K::F_M1 / 64, 3 * T3 * 16};            // + ct * 16
+    const FragSeq m1x1{K::F_M1 / 64 + T3 * 16, 3 * T3 * 16};
+    const FragSeq m1em{K::F_M1 / 64 + 2 * T3 * 16, 3 * T3 * 16};
+    const FragSeq m2{K::F_M2 / 64, TM1 * 16};
+    constexpr int WM1 = win_for<TM1>(), WM2 = win_for<TM2>();
+
+    float carry[CARRY];
+    {
+        const gfloat *tb = reinterpret_cast<const gfloat *>(reinterpret_cast<uint64_t>(table));
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int co = 0; co < T1; ++co) carry[s * T1 + co] = ldfrag(tb, det_g.base + co * 2 + s, lane);
+    }
     for (int g = blockIdx.x * WAVES + w; g < G; g += gridDim.x * WAVES) {
         // the weight fragments are loop-invariant: an opaque per-group copy of the
         // table pointer keeps the compiler from hoisting all 1032 fragment loads
@@ -206,17 +245,18 @@ __global__ __launch_bounds__(256, 2) void group_l2_kernel(
         float4 fin[K::TF / 4];
 #pragma unroll
         for (int i = 0; i < K::TF / 4; ++i) fin[i] = *reinterpret_cast<const float4 *>(fr + 4 * i);
+        float ca[CARRY], cb[CARRY];
 
         // ---- detector convs -> emb [C3][32 rows]
-        f32x16 emb[K::T3];
-        conv_stack<K>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1, K::E_D2, K::E_D3, lane, gin,
-                      fin, emb);
+        f32x16 emb[T3];
+        conv_stack<K, T1, 2>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1, K::E_D2, K::E_D3,
+                             lane, gin, fin, emb, carry, desc_g, ca);
 
         // ---- attention: x1 = max_c emb, a = softmax over the 32 rows (emb >= 0 after
         // ReLU: maxima on the integer bit patterns)
         int mi = __float_as_int(emb[0][0]);
 #pragma unroll
-        for (int co = 0; co < K::T3; ++co)
+        for (int co = 0; co < T3; ++co)
 #pragma unroll
             for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(emb[co][q]));
         const float x1 = __int_as_float(max(mi, __shfl_xor(mi, 32)));
@@ -234,44 +274,57 @@ __global__ __launch_bounds__(256, 2) void group_l2_kernel(
             kp[(size_t)g * 3 + 2] = kz;
         }
 #pragma unroll
-        for (int co = 0; co < K::T3; ++co) {
+        for (int co = 0; co < T3; ++co) {
             f32x16 v;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = half_sum_hi(fmul_rn(emb[co][q], a));
+            for (int q = 0; q < 16; ++q)
+                v[q] = HREG_L2_EXP ? emb[co][q] : half_sum_hi(fmul_rn(emb[co][q], a));
             store_tile(att_feat + (size_t)g * C3, co, v, j, h);
         }
 
         // ---- descriptor convs -> x1d [C3][32]
-        f32x16 x1d[K::T3];
-        conv_stack<K>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1, K::E_E2, K::E_E3, lane, gin,
-                      fin, x1d);
+        f32x16 x1d[T3];
+        conv_stack<K, TM1, WM1>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1, K::E_E2,
+                                K::E_E3, lane, gin, fin, x1d, ca, m1x2, cb);
 
         // ---- mlp1: cat[x2 = k-max of x1d (repeated over rows), x1d, emb * a] -> CM1
-        f32x16 y1[K::TM1];
+        f32x16 y1[TM1];
+        zero_tiles(y1);
 #pragma unroll
-        for (int co = 0; co < K::TM1; ++co) y1[co] = zero16();
-#pragma unroll
-        for (int ct = 0; ct < K::T3; ++ct) {
+        for (int ct = 0; ct < T3; ++ct) {
             f32x16 x2[1];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) x2[0][q] = half_bcast(half_max_hi_nonneg(x1d[ct][q]), h);
-            mfma_accum<1, K::TM1, 3 * K::T3, 0, false>(tb + K::F_M1 + ct * 16 * 64, lane, x2, y1);
+            for (int q = 0; q < 16; ++q)
+                x2[0][q] = HREG_L2_EXP ? x1d[ct][q] : half_bcast(half_max_hi_nonneg(x1d[ct][q]), h);
+            const FragSeq cur{m1x2.base + ct * 16, m1x2.stride};
+            const FragSeq nxt = ct + 1 < T3 ? FragSeq{m1x2.base + (ct + 1) * 16, m1x2.stride} : m1x1;
+            // ct even: cb -> ca, odd: ca -> cb
+            if (ct & 1)
+                mfma_pipe<16, TM1, TM1, WM1>(tb, lane, cur, [&](int st) { return x2[0][st]; }, y1, ca,
+                                             nxt, cb);
+            else
+                mfma_pipe<16, TM1, TM1, WM1>(tb, lane, cur, [&](int st) { return x2[0][st]; }, y1, cb,
+                                             nxt, ca);
         }
-        mfma_accum<K::T3, K::TM1, 3 * K::T3, K::T3, false>(tb + K::F_M1, lane, x1d, y1);
-        mfma_accum<K::T3, K::TM1, 3 * K::T3, 2 * K::T3, true>(tb + K::F_M1, lane, emb, y1, a);
-        epilogue<K::TM1>(eb + K::E_M1, lane, y1);
+        static_assert(T3 % 2 == 0, "carry parity");
+        mfma_pipe<T3 * 16, TM1, TM1, WM1>(tb, lane, m1x1, [&](int st) { return x1d[st >> 4][st & 15]; },
+                                          y1, cb, m1em, ca);
+        mfma_pipe<T3 * 16, TM1, TM2, WM2>(
+            tb, lane, m1em, [&](int st) { return fmul_rn(emb[st >> 4][st & 15], a); }, y1, ca, m2, cb);
+        epilogue<TM1>(eb + K::E_M1, lane, y1);
 
-        // ---- mlp2: CM1 -> CM2, then max over the rows
-        f32x16 y2[K::TM2];
+        // ---- mlp2: CM1 -> CM2, then max over the rows; prefetches the next group's
+        // first window into carry
+        f32x16 y2[TM2];
+        zero_tiles(y2);
+        mfma_pipe<TM1 * 16, TM2, T1, 2>(tb, lane, m2, [&](int st) { return y1[st >> 4][st & 15]; },
+                                        y2, cb, det_g, carry);
+        epilogue<TM2>(eb + K::E_M2, lane, y2);
 #pragma unroll
-        for (int co = 0; co < K::TM2; ++co) y2[co] = zero16();
-        mfma_accum<K::TM1, K::TM2, K::TM1, 0, false>(tb + K::F_M2, lane, y1, y2);
-        epilogue<K::TM2>(eb + K::E_M2, lane, y2);
-#pragma unroll
-        for (int co = 0; co < K::TM2; ++co) {
+        for (int co = 0; co < TM2; ++co) {
             f32x16 v;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = half_max_hi_nonneg(y2[co][q]);
+            for (int q = 0; q < 16; ++q) v[q] = HREG_L2_EXP ? y2[co][q] : half_max_hi_nonneg(y2[co][q]);
             store_tile(desc + (size_t)g * CM2, co, v, j, h);
         }
     }
