@@ -59,6 +59,10 @@ L1_BYTES_PER_GROUP = 4.0 * (64 * 4 + 64 * 3 + 3 + 64 + 64)
 # features 32 x 64, out kp 3 + att_feat 128 + desc 128
 L2_FLOPS_PER_GROUP = 2.0 * 32 * (2 * (68 * 64 + 64 * 64 + 64 * 128) + 384 * 64 + 64 * 128)
 L2_BYTES_PER_GROUP = 4.0 * (32 * 4 + 32 * 3 + 32 + 32 * 64 + 3 + 128 + 128)
+# level-3 fused kernel: 16 rows x (det 132*128+128*128+128*256, desc same, mlp1 768*128,
+# mlp2 128*256) MACs
+L3_FLOPS_PER_GROUP = 2.0 * 16 * (2 * (132 * 128 + 128 * 128 + 128 * 256) + 768 * 128 + 128 * 256)
+L3_BYTES_PER_GROUP = 4.0 * (16 * 4 + 16 * 3 + 16 + 16 * 128 + 3 + 256 + 256)
 
 
 class MfmaTimer:
@@ -66,9 +70,9 @@ class MfmaTimer:
     events on the launch stream and counts its algorithmic FLOPs and bytes."""
 
     def __init__(self):
-        self.events = {"gemm": [], "l1": [], "l2": []}
-        self.flops = {"gemm": 0.0, "l1": 0.0, "l2": 0.0}
-        self.bytes = {"gemm": 0.0, "l1": 0.0, "l2": 0.0}
+        self.events = {"gemm": [], "l1": [], "l2": [], "l3": []}
+        self.flops = {"gemm": 0.0, "l1": 0.0, "l2": 0.0, "l3": 0.0}
+        self.bytes = {"gemm": 0.0, "l1": 0.0, "l2": 0.0, "l3": 0.0}
         self.enabled = False
 
     def _timed(self, kind, fn, flops, nbytes):
@@ -106,6 +110,10 @@ class MfmaTimer:
                 G = args[5]
                 return self._timed("l2", lambda: orig_call(name, *args), L2_FLOPS_PER_GROUP * G,
                                    L2_BYTES_PER_GROUP * G)
+            if name == "hreg_group_l3":
+                G = args[5]
+                return self._timed("l3", lambda: orig_call(name, *args), L3_FLOPS_PER_GROUP * G,
+                                   L3_BYTES_PER_GROUP * G)
             return orig_call(name, *args)
         _lib.gemm = gemm
         engine.call = call
@@ -185,6 +193,8 @@ def main():
                     help="graph executor: batches in flight at once, one stream each "
                          "(a step is still one forward over one batch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--layerwise", default="",
+                    help="comma list of levels (1,2,3) to run layer by layer instead of fused")
     args = ap.parse_args()
     if args.executor == "graph" and args.steps % args.lanes:
         ap.error("--steps must be a multiple of --lanes")
@@ -199,6 +209,8 @@ def main():
 
     from pcd_reg_hregnet_amd import _lib, engine
     _lib.load()
+    for lv in filter(None, args.layerwise.split(",")):
+        setattr(engine, f"FUSED_L{int(lv)}", False)
     net = make_model(device)
     P = net.prepared(device)
     B = args.batch
@@ -249,6 +261,7 @@ def main():
     gemm_ms, n_gemm, gemm_flops, gemm_bytes = timer.result("gemm")
     l1_ms, n_l1, l1_flops, _ = timer.result("l1")
     l2_ms, n_l2, l2_flops, _ = timer.result("l2")
+    l3_ms, n_l3, l3_flops, _ = timer.result("l3")
 
     elapsed = max_over_ranks(elapsed, device)
     value = job_throughput(B, args.steps, world, elapsed)
@@ -260,7 +273,8 @@ def main():
         achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
         traffic, traffic_src = pmc_traffic("gemm_nt_kernel")
         roof = {"kernel": "gemm_nt_kernel (all tile instantiations): every 1x1-conv/BN/ReLU "
-                          "layer outside the fused level-1/2 stages + the cosine contraction",
+                          "layer outside the fused level stages (correspondence heads, "
+                          "keypoint MLPs) + the cosine contraction",
                 "timing": "HIP events on the launch stream, " + (
                     "instrumented eager pipelined pass of the same steps after the timed "
                     "graph region" if args.executor == "graph" else "inside the timed region"),
@@ -279,7 +293,10 @@ def main():
                              "gflop_per_pair": round(l1_flops / args.steps / B / 1e9, 3)},
                 "group_l2": {"avg_launch_us": round(l2_ms / max(n_l2, 1) * 1e3, 2),
                              "tflops": round(l2_flops / max(l2_ms, 1e-9) / 1e9, 3),
-                             "gflop_per_pair": round(l2_flops / args.steps / B / 1e9, 3)}}
+                             "gflop_per_pair": round(l2_flops / args.steps / B / 1e9, 3)},
+                "group_l3": {"avg_launch_us": round(l3_ms / max(n_l3, 1) * 1e3, 2),
+                             "tflops": round(l3_flops / max(l3_ms, 1e-9) / 1e9, 3),
+                             "gflop_per_pair": round(l3_flops / args.steps / B / 1e9, 3)}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

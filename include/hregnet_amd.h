@@ -209,6 +209,15 @@ int hreg_group_l2(const float *table, const float *geom, const float *knn_xyz,
                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                   float *desc, void *stream);
 
+/* Fused level-3 grouping stage: C_in = 4 + 128, convs 132->128->128->256,
+ * mlp 768->128->256, nsample = 16 (two groups per 32-row tile, G even);
+ * feats [*][128] (the level-2 attentive features) -> kp [G][3],
+ * att_feat [G][256], desc [G][256]. */
+int hreg_group_l3_table_floats(void);
+int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
+                  const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
+                  float *desc, void *stream);
+
 /* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */
 int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,

@@ -63,11 +63,12 @@ _SIGS = {
     "hreg_transform_points": [_vp, _vp, _vp, _i, _i, _vp, _vp],
     "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
 }
 
 EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_group_l1_table_floats",
-                          "hreg_group_l2_table_floats")
+                          "hreg_group_l2_table_floats", "hreg_group_l3_table_floats")
 
 _lib = None
 
@@ -87,7 +88,8 @@ def load(require_gpu: bool = True):
             fn.restype = ctypes.c_int
         L.hreg_version.restype = ctypes.c_char_p
         L.hreg_version.argtypes = []
-        for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats"):
+        for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
+                     "hreg_group_l3_table_floats"):
             getattr(L, name).restype = ctypes.c_int
             getattr(L, name).argtypes = []
         _lib = L

@@ -169,3 +169,18 @@ __device__ __forceinline__ float half_bcast(float v, int h) {
     const float hi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
     return h ? hi : lo;
 }
+
+// Sum / max over each 16-lane DPP row, result in every lane of the row.
+__device__ __forceinline__ float row_sum16(float v) {
+    v = fadd_rn(v, dpp_all<0xb1>(v));
+    v = fadd_rn(v, dpp_all<0x4e>(v));
+    v = fadd_rn(v, dpp_all<0x141>(v));
+    return fadd_rn(v, dpp_all<0x140>(v));
+}
+__device__ __forceinline__ float row_max16_nonneg(float f) {
+    int v = __float_as_int(f);
+    v = max(v, dpp_all_i<0xb1>(v));
+    v = max(v, dpp_all_i<0x4e>(v));
+    v = max(v, dpp_all_i<0x141>(v));
+    return __int_as_float(max(v, dpp_all_i<0x140>(v)));
+}

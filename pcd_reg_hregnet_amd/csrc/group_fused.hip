@@ -1,7 +1,7 @@
-// group_l2.hip -- fused level-2 keypoint detector + descriptor for gfx950.
+// group_fused.hip -- fused level-2 / level-3 keypoint detector + descriptor for gfx950.
 //
-// One wave owns one keypoint group: its k = 32 neighbour rows = one 32-row MFMA
-// column tile.  Every layer of
+// One wave owns one 32-row MFMA column tile: one keypoint group of k = 32
+// neighbour rows (level 2) or two groups of k = 16 (level 3).  Every layer of
 //   KeypointDetector.convs [geom 4 + feat CF] -> C1 -> C1 -> C3  (layers.py:115-121, 150)
 //   attention: max_c -> softmax_k -> keypoint / attentive feature (layers.py:151-159)
 //   DescExtractor.convs   [geom 4 + feat CF] -> C1 -> C1 -> C3  (layers.py:183-189, 201)
@@ -12,9 +12,9 @@
 // row j holds channels [h*CF/2, (h+1)*CF/2) of its neighbour's feature row,
 // loaded as float4s, and feeds them as the B operand of k-steps 0..CF/2-1.
 //
-// At level 2 the folded weights are 258 KB -- more than the 160 KB of LDS -- so
-// the A fragments stream from global memory (the table is L2-resident: every
-// CU reads the same 258 KB).  fp32 MFMA needs 256 B of A per 64-cycle
+// The folded weights (258 KB at level 2, 1 MB at level 3) exceed the 160 KB of
+// LDS, so the A fragments stream from global memory (the table is L2-resident:
+// every CU reads the same table).  fp32 MFMA needs 256 B of A per 64-cycle
 // 32x32x2 op, i.e. 16 B/clk per CU at peak, well inside the L2->CU rate.
 //
 // The reference materialises [B, 68..384, 512, 32] tensors for this stage
@@ -23,7 +23,8 @@
 #include "common.h"
 
 // tools/l2_experiment.py builds variants: 1 = no epilogue / reductions (MFMA +
-// loads only), 2 = additionally no weight loads (MFMA issue structure only)
+// loads only), 2 = additionally no weight loads (MFMA issue structure only),
+// 3 = feature rows read without the kNN indirection (no dependent gather)
 #ifndef HREG_L2_EXP
 #define HREG_L2_EXP 0
 #endif
@@ -35,10 +36,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(1))) const float gfloat;
 
 constexpr int WAVES = 4;
-constexpr int KN = 32;  // neighbours per group (level 2)
 
-template <int CF, int C1, int C3, int CM1, int CM2>
+// KN_ neighbours per group (32: level 2, 16: level 3), CF gathered feature channels,
+// conv widths C1 / C3, mlp widths CM1 / CM2, WPS waves per SIMD (register budget)
+template <int KN_, int CF, int C1, int C3, int CM1, int CM2, int WPS_>
 struct Cfg {
+    static constexpr int KN = KN_, WPS = WPS_;
     static constexpr int TF = CF / 2;  // feature k-steps (one channel per lane half)
     static constexpr int T1 = C1 / 32, T3 = C3 / 32, TM1 = CM1 / 32, TM2 = CM2 / 32;
     // fragment table (floats): [co][k-step][lane] blocks, see engine.l2_table
@@ -59,7 +62,8 @@ struct Cfg {
                          E_M1 = E_E3 + 2 * C3, E_M2 = E_M1 + 2 * CM1, TABLE = E_M2 + 2 * CM2;
 };
 
-using L2 = Cfg<64, 64, 128, 64, 128>;
+using L2 = Cfg<32, 64, 64, 128, 64, 128, 2>;
+using L3 = Cfg<16, 128, 128, 256, 128, 256, 1>;
 
 __device__ __forceinline__ f32x16 zero16() {
     f32x16 z;
@@ -86,12 +90,34 @@ struct FragSeq {
     int base, stride;
 };
 
-__device__ __forceinline__ float ldfrag(const gfloat *__restrict__ wf, int f, int lane) {
-    return HREG_L2_EXP == 2 ? (float)(lane + f) : wf[f * 64 + lane];
-}
-
 template <int COUT_T>
-constexpr int win_for() { return COUT_T >= 4 ? 4 : 8; }
+constexpr int win_for() { return COUT_T >= 8 ? 2 : COUT_T >= 4 ? 4 : 8; }
+template <int NSTEP, int COUT_T>
+constexpr int first_win() { return NSTEP < win_for<COUT_T>() ? NSTEP : win_for<COUT_T>(); }
+
+// Fragments are stored in groups of GS = min(4, window) consecutive k-steps with
+// the steps innermost per lane ([step group][lane][GS], engine.l2_table), so one
+// global_load_dwordx4 (x2) brings a lane its A values for 4 (2) k-steps: 4x fewer
+// vector-memory instructions than one dword per MFMA.  Address: uniform fragment
+// base (SGPR pair) + the lane's byte offset.
+template <int GS>
+__device__ __forceinline__ void ldgroup(const gfloat *__restrict__ wf, int f0, int lane, float (&v)[GS]) {
+    if constexpr (HREG_L2_EXP == 2) {
+#pragma unroll
+        for (int i = 0; i < GS; ++i) v[i] = (float)(lane + f0 + i);
+    } else if constexpr (GS == 4) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const v4f gv4f;
+        const v4f t = *reinterpret_cast<const gv4f *>(wf + f0 * 64 + (unsigned)lane * 4);
+        v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+        static_assert(GS == 2, "group size");
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        typedef __attribute__((address_space(1))) const v2f gv2f;
+        const v2f t = *reinterpret_cast<const gv2f *>(wf + f0 * 64 + (unsigned)lane * 2);
+        v[0] = t[0]; v[1] = t[1];
+    }
+}
 
 // acc[co] += sum_{st < NSTEP} A(co, st) x bval(st) on v_mfma_f32_32x32x2_f32.
 // cin: this call's first window (loaded by the previous call); cout: receives the
@@ -100,8 +126,10 @@ template <int NSTEP, int COUT_T, int NCOUT, int NWIN, class BVal>
 __device__ __forceinline__ void mfma_pipe(const gfloat *__restrict__ wf, int lane, FragSeq f, BVal bval,
                                           f32x16 (&acc)[COUT_T], const float (&cin)[CARRY],
                                           FragSeq nf, float (&cout)[CARRY]) {
-    constexpr int WIN = NSTEP < win_for<COUT_T>() ? NSTEP : win_for<COUT_T>();
-    static_assert(NSTEP % WIN == 0 && WIN * COUT_T <= CARRY && NWIN * NCOUT <= CARRY, "window");
+    constexpr int WIN = first_win<NSTEP, COUT_T>();
+    constexpr int GS = WIN < 4 ? WIN : 4, NGS = NWIN < 4 ? NWIN : 4;
+    static_assert(NSTEP % WIN == 0 && WIN % GS == 0 && NWIN % NGS == 0, "window");
+    static_assert(WIN * COUT_T <= CARRY && NWIN * NCOUT <= CARRY, "carry");
     constexpr int NW = NSTEP / WIN;
     // two fragment buffers used alternately (window index is compile-time: no copies)
     float buf[2][WIN][COUT_T];
@@ -113,16 +141,24 @@ __device__ __forceinline__ void mfma_pipe(const gfloat *__restrict__ wf, int lan
     for (int w = 0; w < NW; ++w) {
         if (w + 1 < NW) {
 #pragma unroll
-            for (int s = 0; s < WIN; ++s)
+            for (int s0 = 0; s0 < WIN; s0 += GS)
 #pragma unroll
-                for (int co = 0; co < COUT_T; ++co)
-                    buf[(w + 1) & 1][s][co] = ldfrag(wf, f.base + co * f.stride + (w + 1) * WIN + s, lane);
+                for (int co = 0; co < COUT_T; ++co) {
+                    float v[GS];
+                    ldgroup<GS>(wf, f.base + co * f.stride + (w + 1) * WIN + s0, lane, v);
+#pragma unroll
+                    for (int i = 0; i < GS; ++i) buf[(w + 1) & 1][s0 + i][co] = v[i];
+                }
         } else {
 #pragma unroll
-            for (int s = 0; s < NWIN; ++s)
+            for (int s0 = 0; s0 < NWIN; s0 += NGS)
 #pragma unroll
-                for (int co = 0; co < NCOUT; ++co)
-                    cout[s * NCOUT + co] = ldfrag(wf, nf.base + co * nf.stride + s, lane);
+                for (int co = 0; co < NCOUT; ++co) {
+                    float v[NGS];
+                    ldgroup<NGS>(wf, nf.base + co * nf.stride + s0, lane, v);
+#pragma unroll
+                    for (int i = 0; i < NGS; ++i) cout[(s0 + i) * NCOUT + co] = v[i];
+                }
         }
 #pragma unroll
         for (int s = 0; s < WIN; ++s) {
@@ -134,9 +170,6 @@ __device__ __forceinline__ void mfma_pipe(const gfloat *__restrict__ wf, int lan
         __builtin_amdgcn_sched_barrier(0);
     }
 }
-
-template <int NSTEP, int COUT_T>
-constexpr int first_win() { return NSTEP < win_for<COUT_T>() ? NSTEP : win_for<COUT_T>(); }
 
 template <int COUT_T>
 __device__ __forceinline__ void epilogue(const float *ab, int lane, f32x16 (&acc)[COUT_T]) {
@@ -188,10 +221,10 @@ __device__ __forceinline__ void conv_stack(const gfloat *__restrict__ tb, const 
     epilogue<T3>(eb + e3, lane, out);
 }
 
-// one channel tile of a per-group result reduced over the rows (valid in lanes 31 /
-// 63): channels co*32 + 8r + 4h + {0..3} for registers q = 4r..4r+3 -> 4 float4 stores
-__device__ __forceinline__ void store_tile(float *out, int co, const f32x16 &v, int j, int h) {
-    if (j == 31) {
+// one channel tile of a per-group result reduced over the rows (valid in the writer
+// lanes): channels co*32 + 8r + 4h + {0..3} for registers q = 4r..4r+3 -> 4 float4 stores
+__device__ __forceinline__ void store_tile(float *out, int co, const f32x16 &v, bool writer, int h) {
+    if (writer) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             *reinterpret_cast<float4 *>(out + co * 32 + 8 * r + 4 * h) =
@@ -200,7 +233,7 @@ __device__ __forceinline__ void store_tile(float *out, int co, const f32x16 &v, 
 }
 
 template <class K>
-__global__ __launch_bounds__(256, 2) void group_l2_kernel(
+__global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
     float *__restrict__ att_feat, float *__restrict__ desc) {
@@ -215,6 +248,17 @@ __global__ __launch_bounds__(256, 2) void group_l2_kernel(
     const float *eb = ep - K::F_END;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int h = lane >> 5, j = lane & 31;
+    constexpr int KN = K::KN, GPT = 32 / KN;  // groups per 32-row tile
+    const int NT = G / GPT;
+    // per-group reductions over the KN rows of a tile: wave halves (KN = 32) or
+    // 16-lane DPP rows (KN = 16); *_b: result in every lane, *_w: in the writer lanes
+    const bool writer = KN == 32 ? j == 31 : (j & 15) == 15;
+    auto gsum_w = [&](float v) { return KN == 32 ? half_sum_hi(v) : row_sum16(v); };
+    auto gsum_b = [&](float v) { return KN == 32 ? half_bcast(half_sum_hi(v), h) : row_sum16(v); };
+    auto gmax_w = [&](float v) { return KN == 32 ? half_max_hi_nonneg(v) : row_max16_nonneg(v); };
+    auto gmax_b = [&](float v) {
+        return KN == 32 ? half_bcast(half_max_hi_nonneg(v), h) : row_max16_nonneg(v);
+    };
 
     // the group's call sequence (fragment blocks, see Cfg)
     const FragSeq det_g{K::F_DG / 64, 2}, desc_g{K::F_EG / 64, 2};
@@ -228,47 +272,53 @@ __global__ __launch_bounds__(256, 2) void group_l2_kernel(
     {
         const gfloat *tb = reinterpret_cast<const gfloat *>(reinterpret_cast<uint64_t>(table));
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int co = 0; co < T1; ++co) carry[s * T1 + co] = ldfrag(tb, det_g.base + co * 2 + s, lane);
+        for (int co = 0; co < T1; ++co) {
+            float v[2];
+            ldgroup<2>(tb, det_g.base + co * 2, lane, v);
+            carry[co] = v[0];
+            carry[T1 + co] = v[1];
+        }
     }
-    for (int g = blockIdx.x * WAVES + w; g < G; g += gridDim.x * WAVES) {
+    for (int t = blockIdx.x * WAVES + w; t < NT; t += gridDim.x * WAVES) {
+        const int g = t * GPT + (KN == 32 ? 0 : j >> 4);  // this lane's group
         // the weight fragments are loop-invariant: an opaque per-group copy of the
         // table pointer keeps the compiler from hoisting all 1032 fragment loads
         // out of the group loop (and spilling them)
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
-        const size_t row = (size_t)g * KN + j;
+        const size_t row = (size_t)t * 32 + j;
         const float2 gin = *reinterpret_cast<const float2 *>(geom + row * 4 + 2 * h);
-        const float *fr = feats + (size_t)gidx[row] * CF + h * K::TF;
-        float4 fin[K::TF / 4];
-#pragma unroll
-        for (int i = 0; i < K::TF / 4; ++i) fin[i] = *reinterpret_cast<const float4 *>(fr + 4 * i);
+        const float *fr = feats + (HREG_L2_EXP == 3 ? row : (size_t)gidx[row]) * CF + h * K::TF;
         float ca[CARRY], cb[CARRY];
 
         // ---- detector convs -> emb [C3][32 rows]
         f32x16 emb[T3];
-        conv_stack<K, T1, 2>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1, K::E_D2, K::E_D3,
-                             lane, gin, fin, emb, carry, desc_g, ca);
+        {
+            float4 fin[K::TF / 4];
+#pragma unroll
+            for (int i = 0; i < K::TF / 4; ++i) fin[i] = *reinterpret_cast<const float4 *>(fr + 4 * i);
+            conv_stack<K, TM1, WM1>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1, K::E_D2,
+                                    K::E_D3, lane, gin, fin, emb, carry, m1em, ca);
+        }
 
-        // ---- attention: x1 = max_c emb, a = softmax over the 32 rows (emb >= 0 after
-        // ReLU: maxima on the integer bit patterns)
+        // ---- attention: x1 = max_c emb, a = softmax over the group's rows (emb >= 0
+        // after ReLU: maxima on the integer bit patterns)
         int mi = __float_as_int(emb[0][0]);
 #pragma unroll
         for (int co = 0; co < T3; ++co)
 #pragma unroll
             for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(emb[co][q]));
         const float x1 = __int_as_float(max(mi, __shfl_xor(mi, 32)));
-        const float mx = half_bcast(half_max_hi_nonneg(x1), h);
+        const float mx = gmax_b(x1);
         const float e = expf(fsub_rn(x1, mx));
-        const float a = e / half_bcast(half_sum_hi(e), h);
+        const float a = e / gsum_b(e);
 
         const float *p = knn_xyz + row * 3;
-        const float kx = half_sum_hi(fmul_rn(a, p[0]));
-        const float ky = half_sum_hi(fmul_rn(a, p[1]));
-        const float kz = half_sum_hi(fmul_rn(a, p[2]));
-        if (lane == 31) {
+        const float kx = gsum_w(fmul_rn(a, p[0]));
+        const float ky = gsum_w(fmul_rn(a, p[1]));
+        const float kz = gsum_w(fmul_rn(a, p[2]));
+        if (writer && h == 0) {
             kp[(size_t)g * 3 + 0] = kx;
             kp[(size_t)g * 3 + 1] = ky;
             kp[(size_t)g * 3 + 2] = kz;
@@ -278,39 +328,49 @@ __global__ __launch_bounds__(256, 2) void group_l2_kernel(
             f32x16 v;
 #pragma unroll
             for (int q = 0; q < 16; ++q)
-                v[q] = HREG_L2_EXP ? emb[co][q] : half_sum_hi(fmul_rn(emb[co][q], a));
-            store_tile(att_feat + (size_t)g * C3, co, v, j, h);
+                v[q] = HREG_L2_EXP ? emb[co][q] : gsum_w(fmul_rn(emb[co][q], a));
+            store_tile(att_feat + (size_t)g * C3, co, v, writer, h);
         }
 
-        // ---- descriptor convs -> x1d [C3][32]
-        f32x16 x1d[T3];
-        conv_stack<K, TM1, WM1>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1, K::E_E2,
-                                K::E_E3, lane, gin, fin, x1d, ca, m1x2, cb);
-
-        // ---- mlp1: cat[x2 = k-max of x1d (repeated over rows), x1d, emb * a] -> CM1
+        // ---- mlp1 = W [x2 (k-max of x1d, repeated) | x1d | emb * a] -> CM1: the
+        // emb * a part first, so emb is dead before the descriptor convs run
         f32x16 y1[TM1];
         zero_tiles(y1);
+        mfma_pipe<T3 * 16, TM1, T1, 2>(
+            tb, lane, m1em, [&](int st) { return fmul_rn(emb[st >> 4][st & 15], a); }, y1, ca, desc_g, cb);
+
+        // ---- descriptor convs -> x1d [C3][32]; the gathered rows are re-read (L2 hits)
+        // rather than kept live across the detector
+        f32x16 x1d[T3];
+        {
+            uint64_t fra = reinterpret_cast<uint64_t>(fr);
+            asm volatile("" : "+v"(fra));
+            const float *fr2 = reinterpret_cast<const float *>(fra);
+            float4 fin[K::TF / 4];
+#pragma unroll
+            for (int i = 0; i < K::TF / 4; ++i) fin[i] = *reinterpret_cast<const float4 *>(fr2 + 4 * i);
+            conv_stack<K, TM1, WM1>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1, K::E_E2,
+                                    K::E_E3, lane, gin, fin, x1d, cb, m1x2, ca);
+        }
+
 #pragma unroll
         for (int ct = 0; ct < T3; ++ct) {
             f32x16 x2[1];
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                x2[0][q] = HREG_L2_EXP ? x1d[ct][q] : half_bcast(half_max_hi_nonneg(x1d[ct][q]), h);
+            for (int q = 0; q < 16; ++q) x2[0][q] = HREG_L2_EXP ? x1d[ct][q] : gmax_b(x1d[ct][q]);
             const FragSeq cur{m1x2.base + ct * 16, m1x2.stride};
             const FragSeq nxt = ct + 1 < T3 ? FragSeq{m1x2.base + (ct + 1) * 16, m1x2.stride} : m1x1;
-            // ct even: cb -> ca, odd: ca -> cb
+            // ct even: ca -> cb, odd: cb -> ca
             if (ct & 1)
-                mfma_pipe<16, TM1, TM1, WM1>(tb, lane, cur, [&](int st) { return x2[0][st]; }, y1, ca,
-                                             nxt, cb);
-            else
                 mfma_pipe<16, TM1, TM1, WM1>(tb, lane, cur, [&](int st) { return x2[0][st]; }, y1, cb,
                                              nxt, ca);
+            else
+                mfma_pipe<16, TM1, TM1, WM1>(tb, lane, cur, [&](int st) { return x2[0][st]; }, y1, ca,
+                                             nxt, cb);
         }
         static_assert(T3 % 2 == 0, "carry parity");
-        mfma_pipe<T3 * 16, TM1, TM1, WM1>(tb, lane, m1x1, [&](int st) { return x1d[st >> 4][st & 15]; },
-                                          y1, cb, m1em, ca);
-        mfma_pipe<T3 * 16, TM1, TM2, WM2>(
-            tb, lane, m1em, [&](int st) { return fmul_rn(emb[st >> 4][st & 15], a); }, y1, ca, m2, cb);
+        mfma_pipe<T3 * 16, TM1, TM2, WM2>(tb, lane, m1x1, [&](int st) { return x1d[st >> 4][st & 15]; },
+                                          y1, ca, m2, cb);
         epilogue<TM1>(eb + K::E_M1, lane, y1);
 
         // ---- mlp2: CM1 -> CM2, then max over the rows; prefetches the next group's
@@ -324,28 +384,45 @@ __global__ __launch_bounds__(256, 2) void group_l2_kernel(
         for (int co = 0; co < TM2; ++co) {
             f32x16 v;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = HREG_L2_EXP ? y2[co][q] : half_max_hi_nonneg(y2[co][q]);
-            store_tile(desc + (size_t)g * CM2, co, v, j, h);
+            for (int q = 0; q < 16; ++q) v[q] = HREG_L2_EXP ? y2[co][q] : gmax_w(y2[co][q]);
+            store_tile(desc + (size_t)g * CM2, co, v, writer, h);
         }
     }
+}
+
+template <class K>
+int launch_group(const float *table, const float *geom, const float *knn_xyz, const int32_t *gidx,
+                 const float *feats, int G, float *kp, float *att_feat, float *desc, void *stream) {
+    if (!table || !geom || !knn_xyz || !gidx || !feats || !kp || !att_feat || !desc || G < 0)
+        return HREG_ERR_INVALID;
+    if ((reinterpret_cast<uintptr_t>(feats) & 15) || (reinterpret_cast<uintptr_t>(geom) & 7) ||
+        (reinterpret_cast<uintptr_t>(att_feat) & 15) || (reinterpret_cast<uintptr_t>(desc) & 15))
+        return HREG_ERR_INVALID;
+    if (G % (32 / K::KN)) return HREG_ERR_INVALID;  // whole 32-row tiles
+    if (!G) return HREG_OK;
+    const int NT = G / (32 / K::KN);
+    int grid = (NT + WAVES - 1) / WAVES;
+    const int cap = 256 * K::WPS * 4 / WAVES * 2;  // two rounds of resident blocks
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(group_fused_kernel<K>, dim3(grid), dim3(256), 0, as_stream(stream), table,
+                       geom, knn_xyz, gidx, feats, G, kp, att_feat, desc);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
 }
 
 }  // namespace
 
 extern "C" int hreg_group_l2_table_floats(void) { return L2::TABLE; }
+extern "C" int hreg_group_l3_table_floats(void) { return L3::TABLE; }
 
 extern "C" int hreg_group_l2(const float *table, const float *geom, const float *knn_xyz,
                              const int32_t *gidx, const float *feats, int G, float *kp,
                              float *att_feat, float *desc, void *stream) {
-    if (!table || !geom || !knn_xyz || !gidx || !feats || !kp || !att_feat || !desc || G < 0)
-        return HREG_ERR_INVALID;
-    if ((reinterpret_cast<uintptr_t>(feats) & 15) || (reinterpret_cast<uintptr_t>(geom) & 7))
-        return HREG_ERR_INVALID;
-    if (!G) return HREG_OK;
-    int grid = (G + WAVES - 1) / WAVES;
-    if (grid > 2048) grid = 2048;
-    hipLaunchKernelGGL(group_l2_kernel<L2>, dim3(grid), dim3(256), 0, as_stream(stream), table,
-                       geom, knn_xyz, gidx, feats, G, kp, att_feat, desc);
-    HREG_CHECK_LAUNCH();
-    return HREG_OK;
+    return launch_group<L2>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, stream);
+}
+
+extern "C" int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
+                             const int32_t *gidx, const float *feats, int G, float *kp,
+                             float *att_feat, float *desc, void *stream) {
+    return launch_group<L3>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, stream);
 }

@@ -48,7 +48,9 @@ __device__ __forceinline__ f32x16 zero16() {
 
 __device__ __forceinline__ int chan(int co, int q, int h) { return co * 32 + (q & 3) + 8 * (q >> 2) + 4 * h; }
 
-// acc[co][jt] += W-fragments x in[ct][jt]  (in: accumulator-layout activations)
+// acc[co][jt] += W-fragments x in[ct][jt]  (in: accumulator-layout activations).
+// Fragments are stored with 4 consecutive k-steps innermost per lane
+// ([co][ct][q/4][lane][4], engine.l1_table): one ds_read_b128 per 4 MFMA k-steps.
 template <int CIN_T, int COUT_T, int JT, int JT_IN>
 __device__ __forceinline__ void mfma_accum(const float *__restrict__ wf, int lane,
                                            const f32x16 (&in)[CIN_T][JT_IN],
@@ -56,20 +58,28 @@ __device__ __forceinline__ void mfma_accum(const float *__restrict__ wf, int lan
 #pragma unroll
     for (int ct = 0; ct < CIN_T; ++ct)
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
+        for (int q4 = 0; q4 < 4; ++q4) {
+            float4 a[COUT_T];
 #pragma unroll
-            for (int co = 0; co < COUT_T; ++co) {
-                const float a = wf[((co * CIN_T + ct) * 16 + q) * 64 + lane];
+            for (int co = 0; co < COUT_T; ++co)
+                a[co] = *reinterpret_cast<const float4 *>(wf + (((co * CIN_T + ct) * 4 + q4) * 64 + lane) * 4);
 #pragma unroll
-                for (int jt = 0; jt < JT; ++jt) {
-                    float b = in[ct][JT_IN == 1 ? 0 : jt][q];
-                    if (scale) b = fmul_rn(b, scale[jt]);
-                    acc[co][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[co][jt], 0, 0, 0);
+            for (int i = 0; i < 4; ++i) {
+                const int q = q4 * 4 + i;
+#pragma unroll
+                for (int co = 0; co < COUT_T; ++co) {
+#pragma unroll
+                    for (int jt = 0; jt < JT; ++jt) {
+                        float b = in[ct][JT_IN == 1 ? 0 : jt][q];
+                        if (scale) b = fmul_rn(b, scale[jt]);
+                        acc[co][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32((&a[co].x)[i], b, acc[co][jt], 0, 0, 0);
+                    }
                 }
-                // bound the scheduler's look-ahead (LDS fragment loads, scaled B
-                // values) to 4 k-steps so the live set stays in the register file
-                if ((q & 3) == 3 && co == COUT_T - 1) __builtin_amdgcn_sched_barrier(0);
             }
+            // bound the scheduler's look-ahead (LDS fragment loads, scaled B values) to
+            // 4 k-steps so the live set stays in the register file
+            __builtin_amdgcn_sched_barrier(0);
+        }
 }
 
 template <int COUT_T, int JT>
@@ -95,12 +105,12 @@ __device__ __forceinline__ void conv_geom(const float *__restrict__ wf, const fl
                                           int lane, const float2 (&g)[JT], f32x16 (&acc)[1][JT]) {
 #pragma unroll
     for (int jt = 0; jt < JT; ++jt) acc[0][jt] = zero16();
+    const float2 a = *reinterpret_cast<const float2 *>(wf + lane * 2);  // [lane][2 k-steps]
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        const float a = wf[s * 64 + lane];
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt)
-            acc[0][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s == 0 ? g[jt].x : g[jt].y,
+            acc[0][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(s == 0 ? a.x : a.y, s == 0 ? g[jt].x : g[jt].y,
                                                                acc[0][jt], 0, 0, 0);
     }
     epilogue<1, JT>(ab, lane, acc);

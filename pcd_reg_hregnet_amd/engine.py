@@ -35,7 +35,8 @@ LEVELS = (
 )
 K_HEAD = 8  # CoarseReg/FineReg k (models.py:71-73)
 FUSED_L1 = True  # level 1 through the fused group_l1 kernel (False: layer-by-layer GEMMs)
-FUSED_L2 = True  # level 2 through the fused group_l2 kernel
+FUSED_L2 = True  # level 2 through the fused group_fused kernel (k = 32)
+FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
 
 
 @dataclass
@@ -129,8 +130,9 @@ class PreparedWeights:
             self.fine[name] = (_stack(sd, name + ".convs_1", 3, _perm_fine(C)), _mlp_head(sd, name))
         self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
         self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
+        self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
-                     "coarse_head", "fine", "l1_table", "l2_table"):
+                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
 
@@ -172,21 +174,53 @@ def frag_input(W: torch.Tensor) -> torch.Tensor:
     return geom.reshape(-1), feat.reshape(-1)
 
 
+def _win(cout_tiles: int, nstep: int) -> int:
+    """k-steps per prefetch window of a group_fused.hip call (first_win / win_for)."""
+    w = 2 if cout_tiles >= 8 else 4 if cout_tiles >= 4 else 8
+    return min(w, nstep)
+
+
+def _grouped(frag: torch.Tensor, cout_tiles: int, nstep: int) -> torch.Tensor:
+    """[co][step][lane] fragments -> [co][step group][lane][GS]: GS = min(4, window)
+    consecutive k-steps innermost per lane, so the kernel fetches them with one
+    global_load_dwordx4 (x2)."""
+    gs = min(4, _win(cout_tiles, nstep))
+    f = frag.reshape(cout_tiles, nstep // gs, gs, 64)
+    return f.transpose(-1, -2).reshape(-1)
+
+
 def l2_table(det, desc, mlp) -> torch.Tensor:
-    """Weight/epilogue table of the fused level-2 kernel (layout: group_l2.hip Cfg)."""
-    parts = [*frag_input(det[0].W), frag_layer(det[1].W), frag_layer(det[2].W),
-             *frag_input(desc[0].W), frag_layer(desc[1].W), frag_layer(desc[2].W),
-             frag_layer(mlp[0].W), frag_layer(mlp[1].W)]
+    """Weight/epilogue table of the fused level-2/3 kernel (layout: group_fused.hip Cfg)."""
+    T1, T3 = det[0].W.shape[0] // 32, det[2].W.shape[0] // 32
+    TM1, TM2 = mlp[0].W.shape[0] // 32, mlp[1].W.shape[0] // 32
+    TF = (det[0].W.shape[1] - 4) // 2
+    parts = []
+    for stack in (det, desc):
+        g, f = frag_input(stack[0].W)
+        parts += [_grouped(g, T1, 2), _grouped(f, T1, TF),
+                  _grouped(frag_layer(stack[1].W), T1, T1 * 16),
+                  _grouped(frag_layer(stack[2].W), T3, T1 * 16)]
+    parts += [_grouped(frag_layer(mlp[0].W), TM1, 3 * T3 * 16),
+              _grouped(frag_layer(mlp[1].W), TM2, TM1 * 16)]
     for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
 
 
+def _group4(frag: torch.Tensor, gs: int) -> torch.Tensor:
+    """[blocks][steps][lane] -> [blocks][steps/gs][lane][gs] (gs k-steps innermost)."""
+    f = frag.reshape(-1, gs, 64)
+    return f.transpose(-1, -2).reshape(-1)
+
+
 def l1_table(det, desc, mlp) -> torch.Tensor:
-    """Weight/epilogue table of the fused level-1 kernel (layout: group_l1.hip F_*/E_*)."""
-    parts = [frag_geom(det[0].W), frag_layer(det[1].W), frag_layer(det[2].W),
-             frag_geom(desc[0].W), frag_layer(desc[1].W), frag_layer(desc[2].W),
-             frag_layer(mlp[0].W), frag_layer(mlp[1].W)]
+    """Weight/epilogue table of the fused level-1 kernel (layout: group_l1.hip F_*/E_*;
+    fragments with 2 (first layer) or 4 consecutive k-steps innermost per lane)."""
+    parts = [_group4(frag_geom(det[0].W), 2), _group4(frag_layer(det[1].W), 4),
+             _group4(frag_layer(det[2].W), 4),
+             _group4(frag_geom(desc[0].W), 2), _group4(frag_layer(desc[1].W), 4),
+             _group4(frag_layer(desc[2].W), 4),
+             _group4(frag_layer(mlp[0].W), 4), _group4(frag_layer(mlp[1].W), 4)]
     for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
@@ -408,12 +442,13 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         sig, wnext = head_out(s, s.shape[1], nb, M, w3, b3, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)
         return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
-    if lvl == 1 and FUSED_L2:
+    if (lvl == 1 and FUSED_L2) or (lvl == 2 and FUSED_L3):
         dev = xyz.device
         kp = _empty(G, 3, device=dev)
-        att_feat = _empty(G, LEVELS[1][3][-1], device=dev)
-        desc = _empty(G, LEVELS[1][5], device=dev)
-        call("hreg_group_l2", P.l2_table, geom, kx, gidx, feats, G, kp, att_feat, desc, _stream())
+        att_feat = _empty(G, LEVELS[lvl][3][-1], device=dev)
+        desc = _empty(G, LEVELS[lvl][5], device=dev)
+        name, table = ("hreg_group_l2", P.l2_table) if lvl == 1 else ("hreg_group_l3", P.l3_table)
+        call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, _stream())
         m1, m2, w3, b3 = P.det_head[lvl]
         s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)
         s = gemm([_seg(s, 0, s.shape[1])], m2, G)

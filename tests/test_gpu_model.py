@@ -180,7 +180,7 @@ def test_graph_lanes_match_eager(net):
                 assert torch.equal(out["src_feats"]["desc_3"], ref["src_feats"]["desc_3"])
 
 
-@pytest.mark.parametrize("lvl", [0, 1])
+@pytest.mark.parametrize("lvl", [0, 1, 2])
 def test_fused_level_matches_layerwise(net, lvl):
     """The fused level kernels (group_l1 / group_l2: activations in MFMA accumulators)
     against the layer-by-layer GEMM path on the same grouping; fp32 summation order
@@ -196,7 +196,7 @@ def test_fused_level_matches_layerwise(net, lvl):
             kp, _, att, _, w, _ = engine.keypoint_level(P, level, xyz, feats, w)
             xyz, feats = kp, att
         grouped = engine.grouping(xyz, lvl, w)
-        flag = "FUSED_L1" if lvl == 0 else "FUSED_L2"
+        flag = ("FUSED_L1", "FUSED_L2", "FUSED_L3")[lvl]
         outs = []
         for fused in (True, False):
             old = getattr(engine, flag)

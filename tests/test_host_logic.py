@@ -181,3 +181,10 @@ def test_l2_table_size_matches_kernel(P):
     from pcd_reg_hregnet_amd import _lib
     L = _lib.load(require_gpu=False)
     assert prep.l2_table.numel() == L.hreg_group_l2_table_floats()
+
+
+def test_l3_table_size_matches_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.l3_table.numel() == L.hreg_group_l3_table_floats()

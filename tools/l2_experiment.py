@@ -16,7 +16,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 from tools.op_bench import timeit  # noqa: E402
 
-SRC = os.path.join(REPO, "pcd_reg_hregnet_amd", "csrc", "group_l2.hip")
+SRC = os.path.join(REPO, "pcd_reg_hregnet_amd", "csrc", "group_fused.hip")
 
 
 def build(exp):
@@ -33,7 +33,7 @@ def main():
     b = 16
     G = b * 512
     res = {}
-    for exp in (0, 1, 2):
+    for exp in (0, 1, 2, 3):
         L = ctypes.CDLL(build(exp))
         L.hreg_group_l2_table_floats.restype = ctypes.c_int
         nt = L.hreg_group_l2_table_floats()
@@ -41,7 +41,7 @@ def main():
         geom = torch.from_numpy(rng.normal(size=(G * 32, 4)).astype(np.float32)).cuda()
         kx = torch.from_numpy(rng.normal(size=(G * 32, 3)).astype(np.float32)).cuda()
         gidx = torch.from_numpy(rng.integers(0, b * 1024, G * 32).astype(np.int32)).cuda()
-        feats = torch.from_numpy(rng.normal(size=(b * 1024, 64)).astype(np.float32)).cuda()
+        feats = torch.from_numpy(rng.normal(size=(G * 32, 64)).astype(np.float32)).cuda()
         kp = torch.empty(G, 3, device="cuda")
         att = torch.empty(G, 128, device="cuda")
         desc = torch.empty(G, 128, device="cuda")
