@@ -41,6 +41,7 @@
 #ifndef HREGNET_AMD_H
 #define HREGNET_AMD_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -186,6 +187,17 @@ int hreg_weighted_svd(const float *src, const float *corres, const float *w, int
 /* out[b][i] = R[b] xyz[b][i] + t[b], xyz/out [nb][n][3] */
 int hreg_transform_points(const float *xyz, const float *R, const float *t, int nb, int n,
                           float *out, void *stream);
+
+/* Spatial index for exact culled kNN grouping (n <= 16384 points per cloud):
+ * hreg_spatial_index sorts each cloud of p [nb][n][3] by Morton code and records
+ * the bounding box of every 64 sorted points into ws (16-byte aligned,
+ * hreg_spatial_index_bytes(nb, n) bytes); hreg_knn_group_indexed is
+ * hreg_knn_group over that index -- bit-identical results, visiting only the
+ * point blocks whose box lower bound does not exceed the running K-th distance. */
+size_t hreg_spatial_index_bytes(int nb, int n);
+int hreg_spatial_index(const float *p, int nb, int n, void *ws, void *stream);
+int hreg_knn_group_indexed(const float *q, const float *p, const void *ws, int nb, int m, int n,
+                           int k, int32_t *gidx, float *geom, float *knn_xyz, void *stream);
 
 /* Fused level-1 grouping stage (KeypointDetector.convs/mlp + attention + DescExtractor
  * convs + k-max + mlp, layers.py:115-130 and 183-198, with C=64, nsample=32):

@@ -51,6 +51,8 @@ _SIGS = {
     "hreg_knn_points": [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_knn_gather": [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
     "hreg_knn_group": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "hreg_spatial_index": [_vp, _i, _i, _vp, _vp],
+    "hreg_knn_group_indexed": [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "hreg_gemm": [ctypes.POINTER(Gemm), _vp],
     "hreg_attend": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp],
     "hreg_group_max": [_vp, _i, _i, _i, _i, _vp, _i, _vp],
@@ -67,7 +69,7 @@ _SIGS = {
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
 }
 
-EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_group_l1_table_floats",
+EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_group_l1_table_floats",
                           "hreg_group_l2_table_floats", "hreg_group_l3_table_floats")
 
 _lib = None
@@ -88,6 +90,8 @@ def load(require_gpu: bool = True):
             fn.restype = ctypes.c_int
         L.hreg_version.restype = ctypes.c_char_p
         L.hreg_version.argtypes = []
+        L.hreg_spatial_index_bytes.restype = ctypes.c_size_t
+        L.hreg_spatial_index_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
                      "hreg_group_l3_table_floats"):
             getattr(L, name).restype = ctypes.c_int

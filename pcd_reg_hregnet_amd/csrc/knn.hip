@@ -255,6 +255,233 @@ __global__ __launch_bounds__(256) void knnd_kernel(const float *__restrict__ q,
     }
 }
 
+// ---- spatially indexed kNN grouping (xyz, n <= 16384) --------------------
+// hreg_spatial_index orders each cloud's points by a 12-bit Morton cell (one
+// workgroup per cloud, counting sort in LDS) and records the bounding box of
+// every run of 64 ordered points.  A query then scans only the
+// 64-point blocks whose box lower bound does not exceed its current K-th
+// distance: exact, because the bound is computed with the same fp32 operation
+// order as the point distances and fl() is monotone (for p in the box,
+// |fl(q - p)| >= |fl(q - clamp(q, lo, hi))| per axis), and because every point
+// with d <= tau is still offered, so ties order by index as in the full scan.
+#ifndef HREG_SI_EXP
+#define HREG_SI_EXP 0  // tools/si_experiment.py: 1 no sort, 2 no boxes, 3 bbox + keys only
+#endif
+constexpr int SI_THREADS = 1024;
+constexpr int SI_MAXN = 16384;
+
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits -> every third bit
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t quant10(float x, float lo, float sc) {
+    const float t = (x - lo) * sc;
+    return t <= 0.f ? 0u : (t >= 1023.f ? 1023u : (uint32_t)t);
+}
+
+__device__ __forceinline__ float box_lb(float qx, float qy, float qz, float4 lo, float4 hi) {
+    const float cx = fminf(fmaxf(qx, lo.x), hi.x);
+    const float cy = fminf(fmaxf(qy, lo.y), hi.y);
+    const float cz = fminf(fmaxf(qz, lo.z), hi.z);
+    return sqdist3(qx, qy, qz, cx, cy, cz);
+}
+
+constexpr int SI_CELLS = 4096;  // 12-bit Morton prefix: a 16 x 16 x 16 grid
+
+__global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *__restrict__ p, int n,
+                                                                   float4 *__restrict__ spts,
+                                                                   float4 *__restrict__ boxes) {
+    // counting sort of the points by the top 12 bits of their Morton code (the order
+    // inside a cell is whatever the LDS atomics give: it only shapes the boxes, the
+    // kNN result does not depend on it)
+    __shared__ uint32_t cnt[SI_CELLS];
+    __shared__ int sidx[SI_MAXN];
+    __shared__ float red[6][SI_THREADS / 64];
+    __shared__ uint32_t wsum[SI_THREADS / 64];
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float *P = p + (size_t)c * n * 3;
+    for (int i = tid; i < SI_CELLS; i += SI_THREADS) cnt[i] = 0;
+    // cloud bounding box
+    float mn[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+    float mx[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+    for (int i = tid; i < n; i += SI_THREADS)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            mn[d] = fminf(mn[d], P[i * 3 + d]);
+            mx[d] = fmaxf(mx[d], P[i * 3 + d]);
+        }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        mn[d] = -wave_max_f32(-mn[d]);
+        mx[d] = wave_max_f32(mx[d]);
+        if (lane == 0) { red[d][w] = mn[d]; red[3 + d][w] = mx[d]; }
+    }
+    __syncthreads();
+    float lo[3], sc[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        float a = red[d][0], b = red[3 + d][0];
+        for (int i = 1; i < SI_THREADS / 64; ++i) { a = fminf(a, red[d][i]); b = fmaxf(b, red[3 + d][i]); }
+        lo[d] = a;
+        sc[d] = b > a ? 1023.99f / (b - a) : 0.f;
+    }
+    auto cell_of = [&](int i) {
+        const uint32_t code = spread10(quant10(P[i * 3], lo[0], sc[0])) |
+                              (spread10(quant10(P[i * 3 + 1], lo[1], sc[1])) << 1) |
+                              (spread10(quant10(P[i * 3 + 2], lo[2], sc[2])) << 2);
+        return code >> 18;
+    };
+    for (int i = tid; i < n; i += SI_THREADS) atomicAdd(&cnt[cell_of(i)], 1u);
+    __syncthreads();
+    // exclusive prefix over the 4096 cells: 4 per thread, wave scans, wave totals
+    constexpr int PER = SI_CELLS / SI_THREADS;
+    uint32_t v[PER], tsum = 0;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) { v[e] = cnt[tid * PER + e]; tsum += v[e]; }
+    uint32_t incl = tsum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int i = 0; i < w; ++i) wbase += wsum[i];
+    uint32_t run = wbase + incl - tsum;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) { cnt[tid * PER + e] = run; run += v[e]; }
+    __syncthreads();
+    for (int i = tid; i < n; i += SI_THREADS) sidx[atomicAdd(&cnt[cell_of(i)], 1u)] = i;
+    __syncthreads();
+    int np = 64;
+    while (np < n) np <<= 1;
+    float4 *S = spts + (size_t)c * np;
+    for (int i = tid; i < n; i += SI_THREADS) {
+        const int id = sidx[i];
+        S[i] = make_float4(P[id * 3], P[id * 3 + 1], P[id * 3 + 2], __int_as_float(id));
+    }
+    const int nblk = (HREG_SI_EXP & 2) ? 0 : (n + 63) / 64;
+    float4 *B = boxes + (size_t)c * (np / 64) * 2;
+    for (int b = w; b < nblk; b += SI_THREADS / 64) {
+        const int i = b * 64 + lane;
+        float v3[3], u3[3];
+        if (i < n) {
+            const int id = sidx[i];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) v3[d] = u3[d] = P[id * 3 + d];
+        } else {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { v3[d] = __builtin_huge_valf(); u3[d] = -__builtin_huge_valf(); }
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) { v3[d] = -wave_max_f32(-v3[d]); u3[d] = wave_max_f32(u3[d]); }
+        if (lane == 0) {
+            B[b * 2] = make_float4(v3[0], v3[1], v3[2], 0.f);
+            B[b * 2 + 1] = make_float4(u3[0], u3[1], u3[2], 0.f);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    // DPP row minima, then the four row results
+    v = min(v, (uint32_t)dpp_all_i<0xb1>((int)v));
+    v = min(v, (uint32_t)dpp_all_i<0x4e>((int)v));
+    v = min(v, (uint32_t)dpp_all_i<0x141>((int)v));
+    v = min(v, (uint32_t)dpp_all_i<0x140>((int)v));
+    const uint32_t a = min((uint32_t)__builtin_amdgcn_readlane((int)v, 0),
+                           (uint32_t)__builtin_amdgcn_readlane((int)v, 16));
+    const uint32_t c = min((uint32_t)__builtin_amdgcn_readlane((int)v, 32),
+                           (uint32_t)__builtin_amdgcn_readlane((int)v, 48));
+    return min(a, c);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void knn_group_indexed_kernel(
+    const float *__restrict__ q, const float *__restrict__ p, const float4 *__restrict__ spts,
+    const float4 *__restrict__ boxes, int nb, int m, int n, int k, int32_t *__restrict__ gidx,
+    float *__restrict__ geom, float *__restrict__ knn_xyz) {
+    constexpr int NBL = SI_MAXN / 64 / 64;  // blocks per lane (<= 256 blocks)
+    __shared__ uint64_t sbuf[WAVES][128];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int qi = blockIdx.x * WAVES + w;
+    if (qi >= nb * m) return;
+    const int cloud = qi / m;
+    int np = 64;
+    while (np < n) np <<= 1;
+    const int nblk = (n + 63) / 64;
+    const float4 *S = spts + (size_t)cloud * np;
+    const float4 *B = boxes + (size_t)cloud * (np / 64) * 2;
+    const float *P = p + (size_t)cloud * n * 3;
+    const float qx = q[(size_t)qi * 3], qy = q[(size_t)qi * 3 + 1], qz = q[(size_t)qi * 3 + 2];
+
+    // lower bounds of this lane's blocks (bit patterns: lb >= 0 orders as uint32)
+    uint32_t lb[NBL];
+#pragma unroll
+    for (int t = 0; t < NBL; ++t) {
+        const int b = t * 64 + lane;
+        lb[t] = b < nblk ? __float_as_uint(box_lb(qx, qy, qz, B[b * 2], B[b * 2 + 1])) : 0xffffffffu;
+    }
+
+    WaveList L;
+    L.key = KEY_INF; L.tau = KEY_INF; L.cnt = 0;
+    // best-first: visit blocks in increasing lower bound until the smallest remaining
+    // bound exceeds the K-th distance so far.  The visiting order only needs to be
+    // approximate (bound bits truncated to make room for the block id), the stop
+    // test is exact: stop when even the truncated bound exceeds tau; a block whose
+    // exact bound exceeds tau is skipped, not visited.
+    for (;;) {
+        uint32_t kmin = 0xffffffffu;
+#pragma unroll
+        for (int t = 0; t < NBL; ++t) {
+            const uint32_t kk = lb[t] == 0xffffffffu ? 0xffffffffu
+                                                     : ((lb[t] & 0xffffff00u) | (uint32_t)(t * 64 + lane));
+            kmin = kk < kmin ? kk : kmin;
+        }
+        kmin = wave_min_u32(kmin);
+        if (kmin == 0xffffffffu) break;
+        const uint32_t tau_bits = (uint32_t)(L.tau >> 32);  // >= 0x7f800000 while unset
+        if ((kmin & 0xffffff00u) > tau_bits) break;
+        const int b = (int)(kmin & 0xffu);
+        const uint32_t lbb = __builtin_amdgcn_readlane(lb[b >> 6], b & 63);
+#pragma unroll
+        for (int t = 0; t < NBL; ++t)
+            if ((b >> 6) == t && lane == (b & 63)) lb[t] = 0xffffffffu;
+        if (lbb > tau_bits) continue;
+        const int i = b * 64 + lane;
+        uint64_t key = KEY_INF;
+        if (i < n) {
+            const float4 v = S[i];
+            const float d = sqdist3(qx, qy, qz, v.x, v.y, v.z);
+            key = ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)__float_as_int(v.w);
+        }
+        offer<K>(L, sbuf[w], key, lane);
+        if (L.tau == KEY_INF && L.cnt > 0) flush64<K>(L, sbuf[w], lane);  // first tau early
+    }
+    if (L.cnt > 0) flush64<K>(L, sbuf[w], lane);
+
+    if (lane < k) {
+        const size_t r = (size_t)qi * k + lane;
+        const bool valid = L.key != KEY_INF;
+        const int id = valid ? (int)(uint32_t)(L.key & 0xffffffffu) : 0;
+        const float px = P[id * 3], py = P[id * 3 + 1], pz = P[id * 3 + 2];
+        const float rx = fsub_rn(px, qx), ry = fsub_rn(py, qy), rz = fsub_rn(pz, qz);
+        const float d2 = fadd_rn(fadd_rn(fmul_rn(rx, rx), fmul_rn(ry, ry)), fmul_rn(rz, rz));
+        gidx[r] = cloud * n + id;
+        *reinterpret_cast<float4 *>(geom + r * 4) = make_float4(rx, ry, rz, sqrtf(d2));
+        if (knn_xyz) {
+            knn_xyz[r * 3 + 0] = px;
+            knn_xyz[r * 3 + 1] = py;
+            knn_xyz[r * 3 + 2] = pz;
+        }
+    }
+}
+
 template <int K>
 int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim, int k,
                float *dists, int64_t *idx64, int32_t *idx32, float *nn, hipStream_t st) {
@@ -317,6 +544,56 @@ extern "C" int hreg_knn_gather(const float *x, const int64_t *idx, int b, int n,
     if (total == 0) return HREG_OK;
     hipLaunchKernelGGL(knn_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        as_stream(stream), x, idx, n, c, m, k, total, out);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+static size_t spatial_index_np(int n) {
+    size_t np = 64;
+    while (np < (size_t)n) np <<= 1;
+    return np;
+}
+
+extern "C" size_t hreg_spatial_index_bytes(int nb, int n) {
+    if (nb <= 0 || n <= 0 || n > SI_MAXN) return 0;
+    const size_t np = spatial_index_np(n);
+    return (size_t)nb * (np * sizeof(float4) + (np / 64) * 2 * sizeof(float4));
+}
+
+extern "C" int hreg_spatial_index(const float *p, int nb, int n, void *ws, void *stream) {
+    if (!p || !ws || nb < 0 || n <= 0) return HREG_ERR_INVALID;
+    if (n > SI_MAXN) return HREG_ERR_UNSUPPORTED;
+    if ((reinterpret_cast<uintptr_t>(ws) & 15)) return HREG_ERR_INVALID;
+    if (nb == 0) return HREG_OK;
+    const size_t np = spatial_index_np(n);
+    float4 *spts = static_cast<float4 *>(ws);
+    float4 *boxes = spts + (size_t)nb * np;
+    hipLaunchKernelGGL(spatial_index_kernel, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream), p, n,
+                       spts, boxes);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_knn_group_indexed(const float *q, const float *p, const void *ws, int nb, int m,
+                                      int n, int k, int32_t *gidx, float *geom, float *knn_xyz,
+                                      void *stream) {
+    if (!q || !p || !ws || !gidx || !geom || nb < 0 || m < 0 || n <= 0 || k <= 0)
+        return HREG_ERR_INVALID;
+    if (k > 64 || n > SI_MAXN) return HREG_ERR_UNSUPPORTED;
+    if (nb == 0 || m == 0) return HREG_OK;
+    const size_t np = spatial_index_np(n);
+    const float4 *spts = static_cast<const float4 *>(ws);
+    const float4 *boxes = spts + (size_t)nb * np;
+    hipStream_t st = as_stream(stream);
+    dim3 grid((nb * m + WAVES - 1) / WAVES);
+#define HREG_KGI(KK)                                                                             \
+    hipLaunchKernelGGL((knn_group_indexed_kernel<KK>), grid, dim3(256), 0, st, q, p, spts, boxes, \
+                       nb, m, n, k, gidx, geom, knn_xyz)
+    if (k <= 8) HREG_KGI(8);
+    else if (k <= 16) HREG_KGI(16);
+    else if (k <= 32) HREG_KGI(32);
+    else HREG_KGI(64);
+#undef HREG_KGI
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

@@ -376,6 +376,28 @@ def knn_group(q, p, k, out=None):
     return gidx, geom, kx
 
 
+def spatial_index_bytes(nb: int, n: int) -> int:
+    return _lib.load(require_gpu=False).hreg_spatial_index_bytes(nb, n)
+
+
+def knn_group_indexed(q, p, k, ws, out=None):
+    """knn_group through a per-cloud Morton spatial index built into ws (n <= 16384):
+    bit-identical to knn_group, visiting only the point blocks that can hold a neighbour."""
+    nb, m, _ = q.shape
+    n = p.shape[1]
+    dev = q.device
+    R = nb * m * k
+    if out is None:
+        gidx = _empty(R, dtype=torch.int32, device=dev)
+        geom = _empty(R, 4, device=dev)
+        kx = _empty(R, 3, device=dev)
+    else:
+        gidx, geom, kx = out
+    call("hreg_spatial_index", p, nb, n, ws, _stream())
+    call("hreg_knn_group_indexed", q, p, ws, nb, m, n, k, gidx, geom, kx, _stream())
+    return gidx, geom, kx
+
+
 def knn_idx32(p1, p2, k):
     b, n1, d = p1.shape
     n2 = p2.shape[1]
@@ -386,14 +408,24 @@ def knn_idx32(p1, p2, k):
 
 # ------------------------------------------------------------------ stages
 
-def grouping(xyz, lvl: int, weights=None, out=None):
+SPATIAL_KNN_MIN = 4096  # clouds at least this large group through the spatial index
+
+
+def grouping(xyz, lvl: int, weights=None, out=None, ws=None):
     """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz).
-    out: optional preallocated tensors of the same tuple."""
+    out: optional preallocated tensors of the same tuple; ws: spatial-index workspace
+    (uint8, spatial_index_bytes) for large clouds."""
     M, k = LEVELS[lvl][:2]
     nb, n, _ = xyz.shape
     idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
                        out=None if out is None else out[:2])
-    gidx, geom, kx = knn_group(sampled, xyz, k, out=None if out is None else out[2:])
+    kout = None if out is None else out[2:5]
+    if SPATIAL_KNN_MIN <= n <= 16384:
+        if ws is None:
+            ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
+        gidx, geom, kx = knn_group_indexed(sampled, xyz, k, ws, out=kout)
+    else:
+        gidx, geom, kx = knn_group(sampled, xyz, k, out=kout)
     return idx, sampled, gidx, geom, kx
 
 
@@ -402,17 +434,18 @@ def alloc_stage1(B: int, N: int, device):
     nb = 2 * B
     M, k = LEVELS[0][:2]
     R = nb * M * k
+    ws = _empty(max(spatial_index_bytes(nb, N), 16), dtype=torch.uint8, device=device)
     return (_empty(nb, N, 3, device=device),
             (_empty(nb, M, dtype=torch.int32, device=device), _empty(nb, M, 3, device=device),
              _empty(R, dtype=torch.int32, device=device), _empty(R, 4, device=device),
-             _empty(R, 3, device=device)))
+             _empty(R, 3, device=device), ws))
 
 
 def stage1_into(bufs, src, dst):
     """cat(src, dst) + level-1 FPS + knn_group into preallocated buffers."""
     pts, g = bufs
     torch.cat([src, dst], 0, out=pts)
-    grouping(pts, 0, out=g)
+    grouping(pts, 0, out=g, ws=g[5])
 
 
 def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=None):
@@ -429,7 +462,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
     R = G * k
     if grouped is None:
         grouped = grouping(xyz, lvl, weights)
-    idx, sampled, gidx, geom, kx = grouped
+    idx, sampled, gidx, geom, kx = grouped[:5]
     if lvl == 0 and FUSED_L1:
         dev = xyz.device
         kp = _empty(G, 3, device=dev)

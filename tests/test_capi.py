@@ -14,7 +14,7 @@ def _declared():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
-    for m in re.finditer(r"(?:int|const char \*)\s*(hreg_\w+)\s*\(([^;]*?)\)\s*;", text, flags=re.S):
+    for m in re.finditer(r"(?:int|size_t|const char \*)\s*(hreg_\w+)\s*\(([^;]*?)\)\s*;", text, flags=re.S):
         params = [p.strip() for p in m.group(2).split(",") if p.strip() and p.strip() != "void"]
         decls[m.group(1)] = len(params)
     return decls

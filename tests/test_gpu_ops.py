@@ -268,3 +268,33 @@ def test_transform_points():
     out = engine.transform(dev(x), dev(R), dev(t)).cpu().numpy()
     np.testing.assert_allclose(out, np.einsum("bij,bnj->bni", R, x) + t[:, None], rtol=1e-5,
                                atol=1e-5)
+
+
+@pytest.mark.parametrize("case", ["lidar", "cube", "dups", "ragged"])
+@pytest.mark.parametrize("K", [8, 32, 64])
+def test_knn_group_indexed_matches_bruteforce(case, K):
+    """The Morton-indexed, box-culled kNN grouping is bit-identical to the full scan
+    (indices, relative coordinates, distances), ties included."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    rng = np.random.default_rng(7)
+    if case == "lidar":
+        p = synthetic.lidar_batch(2, 16384, seed0=3)[1]
+    elif case == "cube":
+        p = synthetic.cube_batch(2, 8192, seed=5)[0]
+    elif case == "dups":  # heavy exact duplicates and a lattice: many equal distances
+        base = rng.integers(-20, 20, (2, 1500, 3)).astype(np.float32)
+        p = base[:, rng.integers(0, 1500, 6000)]
+    else:  # n not a multiple of 64
+        p = rng.uniform(-40, 40, (3, 5001, 3)).astype(np.float32)
+    nb, n, _ = p.shape
+    m = 300
+    q = np.concatenate([p[:, rng.integers(0, n, m - 40)],
+                        rng.uniform(-50, 50, (nb, 40, 3)).astype(np.float32)], 1)
+    P = torch.from_numpy(np.ascontiguousarray(p)).cuda()
+    Q = torch.from_numpy(np.ascontiguousarray(q)).cuda()
+    ws = torch.empty(engine.spatial_index_bytes(nb, n), dtype=torch.uint8, device="cuda")
+    a = engine.knn_group_indexed(Q, P, K, ws)
+    b = engine.knn_group(Q, P, K)
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

@@ -49,6 +49,16 @@ def main():
         p = torch.from_numpy(rng.uniform(-40, 40, (a.b, 16384, 3)).astype(np.float32)).cuda()
         q = p[:, :1024].contiguous()
         res["knn_group_l1_ms"] = timeit(lambda: engine.knn_group(q, p, 64))
+        ws = torch.empty(engine.spatial_index_bytes(a.b, 16384), dtype=torch.uint8, device="cuda")
+        res["knn_group_l1_indexed_ms"] = timeit(lambda: engine.knn_group_indexed(q, p, 64, ws))
+        res["spatial_index_ms"] = timeit(lambda: _lib.call("hreg_spatial_index", p, a.b, 16384, ws,
+                                                           _lib.stream_handle()))
+        from pcd_reg_hregnet_amd import synthetic
+        pl = torch.from_numpy(synthetic.lidar_batch(a.b // 2, 16384, seed0=0)[1]).cuda()
+        pl = torch.cat([pl, pl], 0).contiguous()
+        ql = pl[:, ::16].contiguous()
+        res["knn_group_l1_lidar_ms"] = timeit(lambda: engine.knn_group(ql, pl, 64))
+        res["knn_group_l1_lidar_indexed_ms"] = timeit(lambda: engine.knn_group_indexed(ql, pl, 64, ws))
         d = torch.from_numpy(rng.normal(size=(a.b // 2, 256, 256)).astype(np.float32)).cuda()
         res["knn_desc_ms"] = timeit(lambda: engine.knn_idx32(d, d, 8))
     if a.what in ("l2", "all"):
