@@ -134,16 +134,15 @@ __device__ __forceinline__ void conv_stack(const float *tb, int f1, int f2, int 
     epilogue<2, 2>(tb + e3, lane, out);
 }
 
-// sum / max over the 32 rows of a half-wave (lanes l and l^m, m < 32)
-__device__ __forceinline__ float half_sum(float v) {
+// one channel tile of a per-group result reduced over the rows (valid in lanes 31 /
+// 63): channels co*32 + 8r + 4h + {0..3} for registers q = 4r..4r+3 -> 4 float4 stores
+__device__ __forceinline__ void store_tile(float *out, int co, const f32x16 &v, int j, int h) {
+    if (j == 31) {
 #pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) v = fadd_rn(v, __shfl_xor(v, m));
-    return v;
-}
-__device__ __forceinline__ float half_max(float v) {
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
-    return v;
+        for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<float4 *>(out + co * 32 + 8 * r + 4 * h) =
+                make_float4(v[4 * r], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+    }
 }
 
 __global__ __launch_bounds__(256, 2) void group_l1_kernel(
@@ -166,20 +165,21 @@ __global__ __launch_bounds__(256, 2) void group_l1_kernel(
         f32x16 emb[2][2];
         conv_stack(tb, F_DC1, F_DC2, F_DC3, E_DC1, E_DC2, E_DC3, lane, gin, emb);
 
-        // ---- attention: x1 = max_c emb, a = softmax over the 64 rows
+        // ---- attention: x1 = max_c emb, a = softmax over the 64 rows (emb >= 0 after
+        // ReLU: maxima on the integer bit patterns; DPP half-wave reductions)
         float x1[2];
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
-            float m = emb[0][jt][0];
+            int mi = __float_as_int(emb[0][jt][0]);
 #pragma unroll
             for (int co = 0; co < 2; ++co)
 #pragma unroll
-                for (int q = 0; q < 16; ++q) m = fmaxf(m, emb[co][jt][q]);
-            x1[jt] = fmaxf(m, __shfl_xor(m, 32));
+                for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(emb[co][jt][q]));
+            x1[jt] = __int_as_float(max(mi, __shfl_xor(mi, 32)));
         }
-        const float mx = half_max(fmaxf(x1[0], x1[1]));
+        const float mx = half_bcast(half_max_hi_nonneg(fmaxf(x1[0], x1[1])), h);
         const float e0 = expf(fsub_rn(x1[0], mx)), e1 = expf(fsub_rn(x1[1], mx));
-        const float ssum = half_sum(fadd_rn(e0, e1));
+        const float ssum = half_bcast(half_sum_hi(fadd_rn(e0, e1)), h);
         const float a[2] = {e0 / ssum, e1 / ssum};
 
         // keypoint = sum_rows a * knn_xyz
@@ -191,21 +191,21 @@ __global__ __launch_bounds__(256, 2) void group_l1_kernel(
             ky = fadd_rn(ky, fmul_rn(a[jt], p[1]));
             kz = fadd_rn(kz, fmul_rn(a[jt], p[2]));
         }
-        kx = half_sum(kx); ky = half_sum(ky); kz = half_sum(kz);
-        if (lane == 0) {
+        kx = half_sum_hi(kx); ky = half_sum_hi(ky); kz = half_sum_hi(kz);
+        if (lane == 31) {
             kp[(size_t)g * 3 + 0] = kx;
             kp[(size_t)g * 3 + 1] = ky;
             kp[(size_t)g * 3 + 2] = kz;
         }
         // attentive feature [64 ch] = sum_rows emb * a
 #pragma unroll
-        for (int co = 0; co < 2; ++co)
+        for (int co = 0; co < 2; ++co) {
+            f32x16 v;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float v = half_sum(fadd_rn(fmul_rn(emb[co][0][q], a[0]),
-                                                 fmul_rn(emb[co][1][q], a[1])));
-                if (j == 0) att_feat[(size_t)g * 64 + chan(co, q, h)] = v;
-            }
+            for (int q = 0; q < 16; ++q)
+                v[q] = half_sum_hi(fadd_rn(fmul_rn(emb[co][0][q], a[0]), fmul_rn(emb[co][1][q], a[1])));
+            store_tile(att_feat + (size_t)g * 64, co, v, j, h);
+        }
 
         // ---- descriptor convs -> x1d [64][64]
         f32x16 x1d[2][2];
@@ -215,7 +215,8 @@ __global__ __launch_bounds__(256, 2) void group_l1_kernel(
 #pragma unroll
         for (int co = 0; co < 2; ++co)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) x2[co][0][q] = half_max(fmaxf(x1d[co][0][q], x1d[co][1][q]));
+            for (int q = 0; q < 16; ++q)
+                x2[co][0][q] = half_bcast(half_max_hi_nonneg(fmaxf(x1d[co][0][q], x1d[co][1][q])), h);
 
         // ---- mlp1: cat[x2 (64), x1d (64), emb * a (64)] -> 32
         f32x16 y1[1][2];
@@ -234,12 +235,12 @@ __global__ __launch_bounds__(256, 2) void group_l1_kernel(
         mfma_accum<1, 2, 2, 2>(tb + F_M2, lane, y1, y2);
         epilogue<2, 2>(tb + E_M2, lane, y2);
 #pragma unroll
-        for (int co = 0; co < 2; ++co)
+        for (int co = 0; co < 2; ++co) {
+            f32x16 v;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float v = half_max(fmaxf(y2[co][0][q], y2[co][1][q]));
-                if (j == 0) desc[(size_t)g * 64 + chan(co, q, h)] = v;
-            }
+            for (int q = 0; q < 16; ++q) v[q] = half_max_hi_nonneg(fmaxf(y2[co][0][q], y2[co][1][q]));
+            store_tile(desc + (size_t)g * 64, co, v, j, h);
+        }
     }
 }
 
