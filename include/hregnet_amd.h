@@ -230,6 +230,17 @@ int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                   float *desc, void *stream);
 
+/* Fused FineReg head (layers.py:433-451) for C = 64 (fine_corres_1) or 128
+ * (fine_corres_2): small [G*8][16] from hreg_pair_feats (ldf 16), src_desc [G][C]
+ * (keypoint i's own descriptor), dst_desc [*][C] gathered by gidx [G*8],
+ * knn_xyz [G*8][3] -> corres [G][3] (attention-weighted neighbour xyz) and
+ * att [G][N1] (attentive feature, N1 = 2C), convs_1 + attention in one kernel.
+ * table = hreg_fine_head_table_floats(C) floats (engine.fine_head_table). */
+int hreg_fine_head_table_floats(int C);
+int hreg_fine_head(const float *table, int C, const float *small, const float *src_desc,
+                   const float *dst_desc, const int32_t *gidx, const float *knn_xyz, int G,
+                   float *corres, float *att, void *stream);
+
 /* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */
 int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,

@@ -66,6 +66,8 @@ _SIGS = {
     "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_fine_head": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
+    "hreg_fine_head_table_floats": [_i],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
 }
 

@@ -1,0 +1,239 @@
+// group_head.hip -- fused FineReg correspondence head for gfx950.
+//
+// FineReg.forward (layers.py:433-454) per keypoint i of the source and its k = 8
+// nearest destination points n_ij: the feature row
+//   [p - q (3), |p - q| (1), q (3), p (3), w_src (1), w_dst (1), 0 (4) | f_src C | f_dst[n_ij] C]
+// (columns of convs_1 permuted to this order on the host, engine._perm_fine, and
+// zero-padded 12 -> 16) runs through convs_1 (3 x [1x1 Conv2d + BN + ReLU],
+// 2C+16 -> N1 -> N1 -> N1), then the attention of layers.py:446-451: a = softmax
+// over the 8 rows of max over channels, corres = sum_j a_j p_j, attentive feature
+// = sum_j a_j f_j (N1 channels) -- all in one kernel.  One wave owns a 32-row MFMA
+// tile = 4 keypoints; the activations stay in the MFMA accumulators (as in
+// group_fused.hip) and the reductions over a keypoint's 8 rows are 3 DPP steps.
+// The first layer's B operand streams from the three row sources (one window of
+// k-steps ahead, like the A fragments), so the 2C+16-wide rows are never held.
+#include "mfma_chain.h"
+
+namespace {
+
+using namespace hreg_chain;
+
+constexpr int WAVES = 4;
+constexpr int KH = 8;  // neighbours per keypoint (models.py:71-73)
+
+template <int C_, int N1_, int WPS_>
+struct HeadCfg {
+    static constexpr int C = C_, N1 = N1_, WPS = WPS_;
+    static constexpr int T1 = N1 / 32, TA = C / 2;  // conv tiles; k-steps per descriptor segment
+    // fragment table (floats), engine.fine_head_table
+    static constexpr int F_S = 0;                         // small features [T1][8][64]
+    static constexpr int F_A = F_S + T1 * 8 * 64;          // source descriptor [T1][TA][64]
+    static constexpr int F_B = F_A + T1 * TA * 64;         // destination descriptor [T1][TA][64]
+    static constexpr int F_2 = F_B + T1 * TA * 64;         // conv 2 [T1][T1][16][64]
+    static constexpr int F_3 = F_2 + T1 * T1 * 16 * 64;    // conv 3
+    static constexpr int F_END = F_3 + T1 * T1 * 16 * 64;
+    static constexpr int E_1 = F_END, E_2 = E_1 + 2 * N1, E_3 = E_2 + 2 * N1, TABLE = E_3 + 2 * N1;
+};
+
+using Fine1 = HeadCfg<64, 128, 2>;
+using Fine2 = HeadCfg<128, 256, 1>;
+
+// acc[co] += sum_st A(co, st) x rowp[st]: the B operand read from this lane's row
+// (GS-float vector loads) in the same one-window-ahead pipeline as the A fragments.
+template <int NSTEP, int COUT_T, int NCOUT, int NWIN>
+__device__ __forceinline__ void mfma_pipe_rows(const gfloat *__restrict__ wf, int lane, FragSeq f,
+                                               const float *__restrict__ rowp, f32x16 (&acc)[COUT_T],
+                                               const float (&cin)[CARRY], FragSeq nf,
+                                               float (&cout)[CARRY]) {
+    constexpr int WIN = first_win<NSTEP, COUT_T>();
+    constexpr int GS = WIN < 4 ? WIN : 4, NGS = NWIN < 4 ? NWIN : 4;
+    static_assert(NSTEP % WIN == 0 && WIN % GS == 0 && NWIN % NGS == 0, "window");
+    constexpr int NW = NSTEP / WIN;
+    float buf[2][WIN][COUT_T], bb[2][WIN];
+    auto load_b = [&](int slot, int s0w) {
+#pragma unroll
+        for (int s0 = 0; s0 < WIN; s0 += GS) {
+            if constexpr (GS == 4) {
+                const float4 t = *reinterpret_cast<const float4 *>(rowp + s0w + s0);
+                bb[slot][s0] = t.x; bb[slot][s0 + 1] = t.y; bb[slot][s0 + 2] = t.z; bb[slot][s0 + 3] = t.w;
+            } else {
+                const float2 t = *reinterpret_cast<const float2 *>(rowp + s0w + s0);
+                bb[slot][s0] = t.x; bb[slot][s0 + 1] = t.y;
+            }
+        }
+    };
+    load_b(0, 0);
+#pragma unroll
+    for (int s = 0; s < WIN; ++s)
+#pragma unroll
+        for (int co = 0; co < COUT_T; ++co) buf[0][s][co] = cin[s * COUT_T + co];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        if (w + 1 < NW) {
+            load_b((w + 1) & 1, (w + 1) * WIN);
+#pragma unroll
+            for (int s0 = 0; s0 < WIN; s0 += GS)
+#pragma unroll
+                for (int co = 0; co < COUT_T; ++co) {
+                    float v[GS];
+                    ldgroup<GS>(wf, f.base + co * f.stride + (w + 1) * WIN + s0, lane, v);
+#pragma unroll
+                    for (int i = 0; i < GS; ++i) buf[(w + 1) & 1][s0 + i][co] = v[i];
+                }
+        } else {
+#pragma unroll
+            for (int s0 = 0; s0 < NWIN; s0 += NGS)
+#pragma unroll
+                for (int co = 0; co < NCOUT; ++co) {
+                    float v[NGS];
+                    ldgroup<NGS>(wf, nf.base + co * nf.stride + s0, lane, v);
+#pragma unroll
+                    for (int i = 0; i < NGS; ++i) cout[(s0 + i) * NCOUT + co] = v[i];
+                }
+        }
+#pragma unroll
+        for (int s = 0; s < WIN; ++s)
+#pragma unroll
+            for (int co = 0; co < COUT_T; ++co)
+                acc[co] = __builtin_amdgcn_mfma_f32_32x32x2f32(buf[w & 1][s][co], bb[w & 1][s], acc[co], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// sum / max over the 8 rows of a keypoint (8-lane DPP groups), result in all 8 lanes
+__device__ __forceinline__ float grp8_sum(float v) {
+    v = fadd_rn(v, dpp_all<0xb1>(v));
+    v = fadd_rn(v, dpp_all<0x4e>(v));
+    return fadd_rn(v, dpp_all<0x141>(v));
+}
+__device__ __forceinline__ float grp8_max_nonneg(float f) {
+    int v = __float_as_int(f);
+    v = max(v, dpp_all_i<0xb1>(v));
+    v = max(v, dpp_all_i<0x4e>(v));
+    return __int_as_float(max(v, dpp_all_i<0x141>(v)));
+}
+
+template <class K>
+__global__ __launch_bounds__(256, K::WPS) void fine_head_kernel(
+    const float *__restrict__ table, const float *__restrict__ small, const float *__restrict__ src_desc,
+    const float *__restrict__ dst_desc, const int32_t *__restrict__ gidx,
+    const float *__restrict__ knn_xyz, int G, float *__restrict__ corres, float *__restrict__ att) {
+    constexpr int C = K::C, N1 = K::N1, T1 = K::T1, TA = K::TA;
+    constexpr int NE = K::TABLE - K::F_END;
+    __shared__ float ep[NE];
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
+    __syncthreads();
+    const float *eb = ep - K::F_END;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int h = lane >> 5, j = lane & 31;
+    const int NT = G * KH / 32;
+    constexpr int WT = win_for<T1>();
+    const FragSeq fs{K::F_S / 64, 8}, fa{K::F_A / 64, TA}, fb{K::F_B / 64, TA};
+    const FragSeq f2{K::F_2 / 64, T1 * 16}, f3{K::F_3 / 64, T1 * 16};
+
+    float carry[CARRY];
+    {
+        const gfloat *tb = reinterpret_cast<const gfloat *>(reinterpret_cast<uint64_t>(table));
+        constexpr int GS0 = first_win<8, T1>() < 4 ? first_win<8, T1>() : 4;
+#pragma unroll
+        for (int s0 = 0; s0 < first_win<8, T1>(); s0 += GS0)
+#pragma unroll
+            for (int co = 0; co < T1; ++co) {
+                float v[GS0];
+                ldgroup<GS0>(tb, fs.base + co * fs.stride + s0, lane, v);
+#pragma unroll
+                for (int i = 0; i < GS0; ++i) carry[(s0 + i) * T1 + co] = v[i];
+            }
+    }
+    for (int t = blockIdx.x * WAVES + w; t < NT; t += gridDim.x * WAVES) {
+        uint64_t tba = reinterpret_cast<uint64_t>(table);
+        asm volatile("" : "+s"(tba));
+        const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
+        const int row = t * 32 + j;
+        const int g = row / KH;
+        float c1[CARRY], c2[CARRY], c3[CARRY], c4[CARRY];
+
+        f32x16 h1[T1], h2[T1];
+        zero_tiles(h1);
+        mfma_pipe_rows<8, T1, T1, first_win<TA, T1>()>(tb, lane, fs, small + (size_t)row * 16 + h * 8,
+                                                       h1, carry, fa, c1);
+        mfma_pipe_rows<TA, T1, T1, first_win<TA, T1>()>(tb, lane, fa, src_desc + (size_t)g * C + h * TA,
+                                                        h1, c1, fb, c2);
+        mfma_pipe_rows<TA, T1, T1, WT>(tb, lane, fb, dst_desc + (size_t)gidx[row] * C + h * TA, h1, c2,
+                                       f2, c3);
+        epilogue<T1>(eb + K::E_1, lane, h1);
+        zero_tiles(h2);
+        mfma_pipe<T1 * 16, T1, T1, WT>(tb, lane, f2, [&](int st) { return h1[st >> 4][st & 15]; }, h2, c3,
+                                       f3, c4);
+        epilogue<T1>(eb + K::E_2, lane, h2);
+        f32x16 f[T1];
+        zero_tiles(f);
+        mfma_pipe<T1 * 16, T1, T1, first_win<8, T1>()>(
+            tb, lane, f3, [&](int st) { return h2[st >> 4][st & 15]; }, f, c4, fs, carry);
+        epilogue<T1>(eb + K::E_3, lane, f);
+
+        // attention over the keypoint's 8 rows (f >= 0 after ReLU)
+        int mi = __float_as_int(f[0][0]);
+#pragma unroll
+        for (int co = 0; co < T1; ++co)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(f[co][q]));
+        const float x1 = __int_as_float(max(mi, __shfl_xor(mi, 32)));
+        const float e = expf(fsub_rn(x1, grp8_max_nonneg(x1)));
+        const float a = e / grp8_sum(e);
+        const bool writer = (j & 7) == 7;
+        const float *p = knn_xyz + (size_t)row * 3;
+        const float cx = grp8_sum(fmul_rn(a, p[0]));
+        const float cy = grp8_sum(fmul_rn(a, p[1]));
+        const float cz = grp8_sum(fmul_rn(a, p[2]));
+        if (writer && h == 0) {
+            corres[(size_t)g * 3 + 0] = cx;
+            corres[(size_t)g * 3 + 1] = cy;
+            corres[(size_t)g * 3 + 2] = cz;
+        }
+#pragma unroll
+        for (int co = 0; co < T1; ++co) {
+            f32x16 v;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = grp8_sum(fmul_rn(f[co][q], a));
+            store_tile(att + (size_t)g * N1, co, v, writer, h);
+        }
+    }
+}
+
+template <class K>
+int launch_fine(const float *table, const float *small, const float *src_desc, const float *dst_desc,
+                const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                void *stream) {
+    if ((reinterpret_cast<uintptr_t>(small) & 15) || (reinterpret_cast<uintptr_t>(src_desc) & 15) ||
+        (reinterpret_cast<uintptr_t>(dst_desc) & 15) || (reinterpret_cast<uintptr_t>(att) & 15))
+        return HREG_ERR_INVALID;
+    if ((G * KH) % 32) return HREG_ERR_INVALID;  // whole 32-row tiles
+    const int NT = G * KH / 32;
+    int grid = (NT + WAVES - 1) / WAVES;
+    const int cap = 256 * K::WPS * 2;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(fine_head_kernel<K>, dim3(grid), dim3(256), 0, as_stream(stream), table, small,
+                       src_desc, dst_desc, gidx, knn_xyz, G, corres, att);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+}  // namespace
+
+extern "C" int hreg_fine_head_table_floats(int C) {
+    return C == 64 ? Fine1::TABLE : C == 128 ? Fine2::TABLE : 0;
+}
+
+extern "C" int hreg_fine_head(const float *table, int C, const float *small, const float *src_desc,
+                              const float *dst_desc, const int32_t *gidx, const float *knn_xyz,
+                              int G, float *corres, float *att, void *stream) {
+    if (!table || !small || !src_desc || !dst_desc || !gidx || !knn_xyz || !corres || !att || G < 0)
+        return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    if (C == 64)
+        return launch_fine<Fine1>(table, small, src_desc, dst_desc, gidx, knn_xyz, G, corres, att, stream);
+    if (C == 128)
+        return launch_fine<Fine2>(table, small, src_desc, dst_desc, gidx, knn_xyz, G, corres, att, stream);
+    return HREG_ERR_UNSUPPORTED;
+}

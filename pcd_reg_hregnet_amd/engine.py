@@ -37,6 +37,7 @@ K_HEAD = 8  # CoarseReg/FineReg k (models.py:71-73)
 FUSED_L1 = True  # level 1 through the fused group_l1 kernel (False: layer-by-layer GEMMs)
 FUSED_L2 = True  # level 2 through the fused group_fused kernel (k = 32)
 FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
+FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
 
 
 @dataclass
@@ -131,8 +132,10 @@ class PreparedWeights:
         self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
         self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
+        self.fine_table = {name: fine_head_table(self.fine[name][0], C)
+                           for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
-                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table"):
+                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "fine_table"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
 
@@ -187,6 +190,34 @@ def _grouped(frag: torch.Tensor, cout_tiles: int, nstep: int) -> torch.Tensor:
     gs = min(4, _win(cout_tiles, nstep))
     f = frag.reshape(cout_tiles, nstep // gs, gs, 64)
     return f.transpose(-1, -2).reshape(-1)
+
+
+def frag_segment(W: torch.Tensor, col0: int, width: int) -> torch.Tensor:
+    """A fragments of input columns [col0, col0 + width) streamed as B from a row:
+    k-step s, lane half h -> column col0 + h*width/2 + s; [co][width/2][lane]."""
+    Cout = W.shape[0]
+    co = torch.arange(Cout // 32).view(-1, 1, 1)
+    lane = torch.arange(64).view(1, 1, -1)
+    s = torch.arange(width // 2).view(1, -1, 1)
+    return W[co * 32 + (lane & 31), col0 + (lane >> 5) * (width // 2) + s].reshape(-1)
+
+
+def fine_head_table(convs, C: int) -> torch.Tensor:
+    """Weight/epilogue table of group_head.hip's FineReg kernel: convs_1 with the input
+    columns in the packed order [small 12, pad 4, f_src C, f_dst C] (_perm_fine + 4 zero
+    columns), fragments grouped like l2_table."""
+    W1 = convs[0].W
+    N1 = W1.shape[0]
+    T1 = N1 // 32
+    W1p = torch.cat([W1[:, :12], torch.zeros(N1, 4, dtype=W1.dtype), W1[:, 12:]], 1)
+    parts = [_grouped(frag_segment(W1p, 0, 16), T1, 8),
+             _grouped(frag_segment(W1p, 16, C), T1, C // 2),
+             _grouped(frag_segment(W1p, 16 + C, C), T1, C // 2),
+             _grouped(frag_layer(convs[1].W), T1, T1 * 16),
+             _grouped(frag_layer(convs[2].W), T1, T1 * 16)]
+    for lin in convs:
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
 
 
 def l2_table(det, desc, mlp) -> torch.Tensor:
@@ -595,6 +626,19 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
     convs, head = P.fine[name]
     kidx = knn_idx32(src_xyz, dst_xyz, k)
     R = B * N * k
+    if FUSED_FINE:
+        small = _empty(R, 16, device=dev)
+        kx = _empty(R, 3, device=dev)
+        gidx = _empty(R, dtype=torch.int32, device=dev)
+        call("hreg_pair_feats", src_xyz, dst_xyz, src_w, dst_w, kidx, B, N, N, k, None, None, small,
+             16, kx, gidx, _stream())
+        N1 = convs[0].W.shape[0]
+        corres = _empty(B * N, 3, device=dev)
+        att = _empty(B * N, N1, device=dev)
+        call("hreg_fine_head", P.fine_table[name], C, small, src_desc, dst_desc, gidx, kx, B * N,
+             corres, att, _stream())
+        w = _mlp_weights(att, head, B * N, B, N)
+        return corres.view(B, N, 3), w.view(B, N)
     small = _empty(R, 12, device=dev)
     kx = _empty(R, 3, device=dev)
     gidx = _empty(R, dtype=torch.int32, device=dev)

@@ -209,3 +209,31 @@ def test_fused_level_matches_layerwise(net, lvl):
     (kp_f, sig_f, att_f, desc_f, w_f, _), (kp_r, sig_r, att_r, desc_r, w_r, _) = outs
     for a, b in ((kp_f, kp_r), (sig_f, sig_r), (att_f, att_r), (desc_f, desc_r)):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("name,C,N", [("fine_corres_1", 64, 1024), ("fine_corres_2", 128, 512)])
+def test_fused_fine_head_matches_layerwise(net, name, C, N):
+    """group_head.hip (convs_1 + attention in one kernel) against the GEMM + attend path."""
+    from pcd_reg_hregnet_amd import engine
+    P = net.prepared(torch.device("cuda"))
+    g = torch.Generator().manual_seed(3)
+    B = 2
+    sx = (torch.rand(B, N, 3, generator=g) * 40 - 20).cuda()
+    dx = (sx.cpu() + torch.randn(B, N, 3, generator=g) * 0.3).cuda()
+    sd = torch.relu(torch.randn(B * N, C, generator=g)).cuda()
+    dd = torch.relu(torch.randn(B * N, C, generator=g)).cuda()
+    sw = torch.rand(B * N, generator=g).cuda()
+    dw = torch.rand(B * N, generator=g).cuda()
+    outs = []
+    with torch.no_grad():
+        for fused in (True, False):
+            old = engine.FUSED_FINE
+            engine.FUSED_FINE = fused
+            try:
+                outs.append(engine.fine_reg(P, name, B, sx, sd, dx, dd, sw, dw))
+            finally:
+                engine.FUSED_FINE = old
+    torch.cuda.synchronize()
+    (c_f, w_f), (c_r, w_r) = outs
+    torch.testing.assert_close(c_f, c_r, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)

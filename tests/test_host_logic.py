@@ -188,3 +188,11 @@ def test_l3_table_size_matches_kernel(P):
     from pcd_reg_hregnet_amd import _lib
     L = _lib.load(require_gpu=False)
     assert prep.l3_table.numel() == L.hreg_group_l3_table_floats()
+
+
+def test_fine_head_table_sizes_match_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.fine_table["fine_corres_1"].numel() == L.hreg_fine_head_table_floats(64)
+    assert prep.fine_table["fine_corres_2"].numel() == L.hreg_fine_head_table_floats(128)
