@@ -70,9 +70,9 @@ class MfmaTimer:
     events on the launch stream and counts its algorithmic FLOPs and bytes."""
 
     def __init__(self):
-        self.events = {"gemm": [], "l1": [], "l2": [], "l3": []}
-        self.flops = {"gemm": 0.0, "l1": 0.0, "l2": 0.0, "l3": 0.0}
-        self.bytes = {"gemm": 0.0, "l1": 0.0, "l2": 0.0, "l3": 0.0}
+        self.events = {"gemm": [], "l1": [], "l2": [], "l3": [], "fine": []}
+        self.flops = {"gemm": 0.0, "l1": 0.0, "l2": 0.0, "l3": 0.0, "fine": 0.0}
+        self.bytes = {"gemm": 0.0, "l1": 0.0, "l2": 0.0, "l3": 0.0, "fine": 0.0}
         self.enabled = False
 
     def _timed(self, kind, fn, flops, nbytes):
@@ -110,6 +110,12 @@ class MfmaTimer:
                 G = args[5]
                 return self._timed("l2", lambda: orig_call(name, *args), L2_FLOPS_PER_GROUP * G,
                                    L2_BYTES_PER_GROUP * G)
+            if name == "hreg_fine_head":
+                C, G = args[1], args[7]
+                N1 = 2 * C
+                fl = 2.0 * 8 * G * ((2 * C + 12) * N1 + 2 * N1 * N1)  # algorithmic (unpadded) MACs
+                nb = 4.0 * G * (8 * (16 + C + 1 + 3) + C + 3 + N1)
+                return self._timed("fine", lambda: orig_call(name, *args), fl, nb)
             if name == "hreg_group_l3":
                 G = args[5]
                 return self._timed("l3", lambda: orig_call(name, *args), L3_FLOPS_PER_GROUP * G,
@@ -262,6 +268,7 @@ def main():
     l1_ms, n_l1, l1_flops, _ = timer.result("l1")
     l2_ms, n_l2, l2_flops, _ = timer.result("l2")
     l3_ms, n_l3, l3_flops, _ = timer.result("l3")
+    fh_ms, n_fh, fh_flops, _ = timer.result("fine")
 
     elapsed = max_over_ranks(elapsed, device)
     value = job_throughput(B, args.steps, world, elapsed)
@@ -296,7 +303,10 @@ def main():
                              "gflop_per_pair": round(l2_flops / args.steps / B / 1e9, 3)},
                 "group_l3": {"avg_launch_us": round(l3_ms / max(n_l3, 1) * 1e3, 2),
                              "tflops": round(l3_flops / max(l3_ms, 1e-9) / 1e9, 3),
-                             "gflop_per_pair": round(l3_flops / args.steps / B / 1e9, 3)}}
+                             "gflop_per_pair": round(l3_flops / args.steps / B / 1e9, 3)},
+                "fine_head": {"avg_launch_us": round(fh_ms / max(n_fh, 1) * 1e3, 2),
+                              "tflops": round(fh_flops / max(fh_ms, 1e-9) / 1e9, 3),
+                              "gflop_per_pair": round(fh_flops / args.steps / B / 1e9, 3)}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

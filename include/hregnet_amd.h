@@ -241,6 +241,15 @@ int hreg_fine_head(const float *table, int C, const float *small, const float *s
                    const float *dst_desc, const int32_t *gidx, const float *knn_xyz, int G,
                    float *corres, float *att, void *stream);
 
+/* Fused CoarseReg neighbour branch (layers.py:315-337), C = 256: rows
+ * [desc[gidx] C | geom 4] (geom [G*8] float4 from hreg_knn_group) through convs_2
+ * (260 -> 256 x 3) and the attention over the 8 rows, applied to the gathered
+ * descriptors: out [G][C] = sum_j a_j desc[gidx_j].  table =
+ * hreg_nbr_head_table_floats() floats (engine.nbr_head_table). */
+int hreg_nbr_head_table_floats(void);
+int hreg_nbr_head(const float *table, const float *desc, const int32_t *gidx, const float *geom,
+                  int G, float *out, void *stream);
+
 /* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */
 int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,

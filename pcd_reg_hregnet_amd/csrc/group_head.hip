@@ -12,6 +12,10 @@
 // group_fused.hip) and the reductions over a keypoint's 8 rows are 3 DPP steps.
 // The first layer's B operand streams from the three row sources (one window of
 // k-steps ahead, like the A fragments), so the 2C+16-wide rows are never held.
+//
+// nbr_head_kernel is CoarseReg's neighbour branch (layers.py:315-337): rows
+// [desc[nbr_ij] C | p_ij - q_i, |p_ij - q_i|] through convs_2 (C+4 -> 256 -> 256 -> 256),
+// attention over the 8 xyz neighbours, output sum_j a_j desc[nbr_ij] (C channels).
 #include "mfma_chain.h"
 
 namespace {
@@ -201,6 +205,97 @@ __global__ __launch_bounds__(256, K::WPS) void fine_head_kernel(
     }
 }
 
+template <int C_>
+struct NbrCfg {
+    static constexpr int C = C_, N1 = 256, WPS = 1;
+    static constexpr int T1 = N1 / 32, TA = C / 2;
+    static constexpr int F_D = 0;                          // descriptor part [T1][TA][64]
+    static constexpr int F_G = F_D + T1 * TA * 64;          // geometry part [T1][2][64]
+    static constexpr int F_2 = F_G + T1 * 2 * 64;
+    static constexpr int F_3 = F_2 + T1 * T1 * 16 * 64;
+    static constexpr int F_END = F_3 + T1 * T1 * 16 * 64;
+    static constexpr int E_1 = F_END, E_2 = E_1 + 2 * N1, E_3 = E_2 + 2 * N1, TABLE = E_3 + 2 * N1;
+};
+using Nbr = NbrCfg<256>;
+
+template <class K>
+__global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
+    const float *__restrict__ table, const float *__restrict__ desc, const int32_t *__restrict__ gidx,
+    const float *__restrict__ geom, int G, float *__restrict__ out) {
+    constexpr int C = K::C, T1 = K::T1, TA = K::TA;
+    constexpr int NE = K::TABLE - K::F_END;
+    __shared__ float ep[NE];
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
+    __syncthreads();
+    const float *eb = ep - K::F_END;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int h = lane >> 5, j = lane & 31;
+    const int NT = G * KH / 32;
+    constexpr int WT = win_for<T1>();
+    const FragSeq fd{K::F_D / 64, TA}, fg{K::F_G / 64, 2};
+    const FragSeq f2{K::F_2 / 64, T1 * 16}, f3{K::F_3 / 64, T1 * 16};
+    constexpr int W0 = first_win<TA, T1>();
+
+    float carry[CARRY];
+    {
+        const gfloat *tb = reinterpret_cast<const gfloat *>(reinterpret_cast<uint64_t>(table));
+        constexpr int GS0 = W0 < 4 ? W0 : 4;
+#pragma unroll
+        for (int s0 = 0; s0 < W0; s0 += GS0)
+#pragma unroll
+            for (int co = 0; co < T1; ++co) {
+                float v[GS0];
+                ldgroup<GS0>(tb, fd.base + co * fd.stride + s0, lane, v);
+#pragma unroll
+                for (int i = 0; i < GS0; ++i) carry[(s0 + i) * T1 + co] = v[i];
+            }
+    }
+    for (int t = blockIdx.x * WAVES + w; t < NT; t += gridDim.x * WAVES) {
+        uint64_t tba = reinterpret_cast<uint64_t>(table);
+        asm volatile("" : "+s"(tba));
+        const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
+        const int row = t * 32 + j;
+        const int g = row / KH;
+        const float *drow = desc + (size_t)gidx[row] * C;
+        float c1[CARRY], c2[CARRY], c3[CARRY], c4[CARRY];
+
+        f32x16 h1[T1], h2[T1];
+        zero_tiles(h1);
+        mfma_pipe_rows<TA, T1, T1, 2>(tb, lane, fd, drow + h * TA, h1, carry, fg, c1);
+        mfma_pipe_rows<2, T1, T1, WT>(tb, lane, fg, geom + (size_t)row * 4 + h * 2, h1, c1, f2, c2);
+        epilogue<T1>(eb + K::E_1, lane, h1);
+        zero_tiles(h2);
+        mfma_pipe<T1 * 16, T1, T1, WT>(tb, lane, f2, [&](int st) { return h1[st >> 4][st & 15]; }, h2, c2,
+                                       f3, c3);
+        epilogue<T1>(eb + K::E_2, lane, h2);
+        f32x16 f[T1];
+        zero_tiles(f);
+        mfma_pipe<T1 * 16, T1, T1, W0>(tb, lane, f3, [&](int st) { return h2[st >> 4][st & 15]; }, f, c3,
+                                       fd, carry);
+        epilogue<T1>(eb + K::E_3, lane, f);
+        (void)c4;
+
+        // attention over the 8 rows (f >= 0 after ReLU), applied to the input descriptors
+        int mi = __float_as_int(f[0][0]);
+#pragma unroll
+        for (int co = 0; co < T1; ++co)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(f[co][q]));
+        const float x1 = __int_as_float(max(mi, __shfl_xor(mi, 32)));
+        const float e = expf(fsub_rn(x1, grp8_max_nonneg(x1)));
+        const float a = e / grp8_sum(e);
+        const bool writer = (j & 7) == 7;
+        // lane half h owns channels [h*C/2, (h+1)*C/2) of its row's descriptor
+#pragma unroll 4
+        for (int c4i = 0; c4i < TA / 4; ++c4i) {
+            const float4 v = *reinterpret_cast<const float4 *>(drow + h * TA + c4i * 4);
+            const float4 r = make_float4(grp8_sum(fmul_rn(v.x, a)), grp8_sum(fmul_rn(v.y, a)),
+                                         grp8_sum(fmul_rn(v.z, a)), grp8_sum(fmul_rn(v.w, a)));
+            if (writer) *reinterpret_cast<float4 *>(out + (size_t)g * C + h * TA + c4i * 4) = r;
+        }
+    }
+}
+
 template <class K>
 int launch_fine(const float *table, const float *small, const float *src_desc, const float *dst_desc,
                 const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
@@ -220,6 +315,25 @@ int launch_fine(const float *table, const float *small, const float *src_desc, c
 }
 
 }  // namespace
+
+extern "C" int hreg_nbr_head_table_floats(void) { return Nbr::TABLE; }
+
+extern "C" int hreg_nbr_head(const float *table, const float *desc, const int32_t *gidx,
+                             const float *geom, int G, float *out, void *stream) {
+    if (!table || !desc || !gidx || !geom || !out || G < 0) return HREG_ERR_INVALID;
+    if ((reinterpret_cast<uintptr_t>(desc) & 15) || (reinterpret_cast<uintptr_t>(geom) & 15) ||
+        (reinterpret_cast<uintptr_t>(out) & 15))
+        return HREG_ERR_INVALID;
+    if ((G * KH) % 32) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    const int NT = G * KH / 32;
+    int grid = (NT + WAVES - 1) / WAVES;
+    if (grid > 512) grid = 512;
+    hipLaunchKernelGGL(nbr_head_kernel<Nbr>, dim3(grid), dim3(256), 0, as_stream(stream), table, desc,
+                       gidx, geom, G, out);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
 
 extern "C" int hreg_fine_head_table_floats(int C) {
     return C == 64 ? Fine1::TABLE : C == 128 ? Fine2::TABLE : 0;

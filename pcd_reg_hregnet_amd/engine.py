@@ -38,6 +38,7 @@ FUSED_L1 = True  # level 1 through the fused group_l1 kernel (False: layer-by-la
 FUSED_L2 = True  # level 2 through the fused group_fused kernel (k = 32)
 FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
+FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
 
 
 @dataclass
@@ -134,8 +135,10 @@ class PreparedWeights:
         self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
                            for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
+        self.nbr_table = nbr_head_table(self.coarse_convs2, 256)
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
-                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "fine_table"):
+                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "fine_table",
+                     "nbr_table"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
 
@@ -213,6 +216,19 @@ def fine_head_table(convs, C: int) -> torch.Tensor:
     parts = [_grouped(frag_segment(W1p, 0, 16), T1, 8),
              _grouped(frag_segment(W1p, 16, C), T1, C // 2),
              _grouped(frag_segment(W1p, 16 + C, C), T1, C // 2),
+             _grouped(frag_layer(convs[1].W), T1, T1 * 16),
+             _grouped(frag_layer(convs[2].W), T1, T1 * 16)]
+    for lin in convs:
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def nbr_head_table(convs, C: int) -> torch.Tensor:
+    """Table of group_head.hip's CoarseReg neighbour-branch kernel: convs_2 over the
+    columns [desc C | geom 4] (the order engine.coarse_reg assembles)."""
+    T1 = convs[0].W.shape[0] // 32
+    W1 = convs[0].W
+    parts = [_grouped(frag_segment(W1, 0, C), T1, C // 2), _grouped(frag_segment(W1, C, 4), T1, 2),
              _grouped(frag_layer(convs[1].W), T1, T1 * 16),
              _grouped(frag_layer(convs[2].W), T1, T1 * 16)]
     for lin in convs:
@@ -592,11 +608,15 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     gself, geom_self, _ = knn_group(xyz3, xyz3, k)
     G2 = 2 * B * N1
     R2 = G2 * k
-    segs = [_seg(desc3, 0, C, gather=gself), _seg(geom_self, C, 4)]
-    h = gemm(segs, P.coarse_convs2[0], R2)
-    h = gemm([_seg(h, 0, h.shape[1])], P.coarse_convs2[1], R2)
-    h = gemm([_seg(h, 0, h.shape[1])], P.coarse_convs2[2], R2)
-    _, nbr, _ = attend(h, G2, k, vals=desc3, vgather=gself)
+    if FUSED_NBR and C == 256:
+        nbr = _empty(G2, C, device=dev)
+        call("hreg_nbr_head", P.nbr_table, desc3, gself, geom_self, G2, nbr, _stream())
+    else:
+        segs = [_seg(desc3, 0, C, gather=gself), _seg(geom_self, C, 4)]
+        h = gemm(segs, P.coarse_convs2[0], R2)
+        h = gemm([_seg(h, 0, h.shape[1])], P.coarse_convs2[1], R2)
+        h = gemm([_seg(h, 0, h.shape[1])], P.coarse_convs2[2], R2)
+        _, nbr, _ = attend(h, G2, k, vals=desc3, vgather=gself)
     nnorm = row_norms(nbr)
     cosine_gemm(nbr[:B * N1], nbr[B * N1:], nnorm[:B * N1], nnorm[B * N1:], B, N1, N1, C, S)
     sims_b = _empty(B * N1 * k, 2, device=dev)

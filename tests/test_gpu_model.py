@@ -237,3 +237,27 @@ def test_fused_fine_head_matches_layerwise(net, name, C, N):
     (c_f, w_f), (c_r, w_r) = outs
     torch.testing.assert_close(c_f, c_r, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)
+
+
+def test_fused_nbr_head_matches_layerwise(net):
+    """CoarseReg neighbour branch in one kernel (group_head.hip) vs GEMMs + attend."""
+    from pcd_reg_hregnet_amd import engine
+    P = net.prepared(torch.device("cuda"))
+    g = torch.Generator().manual_seed(5)
+    B, N1, C = 2, 256, 256
+    xyz3 = (torch.rand(2 * B, N1, 3, generator=g) * 40 - 20).cuda()
+    desc3 = torch.relu(torch.randn(2 * B * N1, C, generator=g)).cuda()
+    sig3 = (torch.rand(2 * B * N1, generator=g) + 0.1).cuda()
+    outs = []
+    with torch.no_grad():
+        for fused in (True, False):
+            old = engine.FUSED_NBR
+            engine.FUSED_NBR = fused
+            try:
+                outs.append(engine.coarse_reg(P, B, xyz3, desc3, sig3))
+            finally:
+                engine.FUSED_NBR = old
+    torch.cuda.synchronize()
+    (c_f, w_f), (c_r, w_r) = outs
+    torch.testing.assert_close(c_f, c_r, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)

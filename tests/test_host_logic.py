@@ -196,3 +196,10 @@ def test_fine_head_table_sizes_match_kernel(P):
     L = _lib.load(require_gpu=False)
     assert prep.fine_table["fine_corres_1"].numel() == L.hreg_fine_head_table_floats(64)
     assert prep.fine_table["fine_corres_2"].numel() == L.hreg_fine_head_table_floats(128)
+
+
+def test_nbr_head_table_size_matches_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.nbr_table.numel() == L.hreg_nbr_head_table_floats()
