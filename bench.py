@@ -65,14 +65,39 @@ L3_FLOPS_PER_GROUP = 2.0 * 16 * (2 * (132 * 128 + 128 * 128 + 128 * 256) + 768 *
 L3_BYTES_PER_GROUP = 4.0 * (16 * 4 + 16 * 3 + 16 + 16 * 128 + 3 + 256 + 256)
 
 
+def _fine_work(args):
+    C, G = args[1], args[7]
+    N1 = 2 * C  # algorithmic (unpadded) conv MACs, rows of 8 neighbours
+    return (2.0 * 8 * G * ((2 * C + 12) * N1 + 2 * N1 * N1),
+            4.0 * G * (8 * (16 + C + 1 + 3) + C + 3 + N1))
+
+
+def _nbr_work(args):
+    G = args[4]
+    return (2.0 * 8 * G * (260 * 256 + 2 * 256 * 256), 4.0 * G * (8 * (256 + 4 + 1) + 256))
+
+
+# C-ABI entry -> (timer kind, (flops, bytes) of one launch from its arguments)
+MFMA_ENTRIES = {
+    "hreg_group_l1": ("l1", lambda a: (L1_FLOPS_PER_GROUP * a[3], L1_BYTES_PER_GROUP * a[3])),
+    "hreg_group_l2": ("fused", lambda a: (L2_FLOPS_PER_GROUP * a[5], L2_BYTES_PER_GROUP * a[5])),
+    "hreg_group_l3": ("fused", lambda a: (L3_FLOPS_PER_GROUP * a[5], L3_BYTES_PER_GROUP * a[5])),
+    "hreg_fine_head": ("head", _fine_work),
+    "hreg_nbr_head": ("head", _nbr_work),
+}
+
+
 class MfmaTimer:
-    """Brackets every fp32-MFMA launch (gemm_nt_kernel, group_l1_kernel) with HIP
-    events on the launch stream and counts its algorithmic FLOPs and bytes."""
+    """Brackets every fp32-MFMA launch (gemm_nt_kernel, group_l1_kernel,
+    group_fused_kernel, fine/nbr head kernels) with HIP events on the launch stream
+    and counts its algorithmic FLOPs and bytes, per kernel kind."""
+
+    KINDS = ("gemm", "l1", "fused", "head")
 
     def __init__(self):
-        self.events = {"gemm": [], "l1": [], "l2": [], "l3": [], "fine": []}
-        self.flops = {"gemm": 0.0, "l1": 0.0, "l2": 0.0, "l3": 0.0, "fine": 0.0}
-        self.bytes = {"gemm": 0.0, "l1": 0.0, "l2": 0.0, "l3": 0.0, "fine": 0.0}
+        self.events = {k: [] for k in self.KINDS}
+        self.flops = dict.fromkeys(self.KINDS, 0.0)
+        self.bytes = dict.fromkeys(self.KINDS, 0.0)
         self.enabled = False
 
     def _timed(self, kind, fn, flops, nbytes):
@@ -102,24 +127,10 @@ class MfmaTimer:
                                nbytes)
 
         def call(name, *args):
-            if name == "hreg_group_l1":
-                G = args[3]
-                return self._timed("l1", lambda: orig_call(name, *args), L1_FLOPS_PER_GROUP * G,
-                                   L1_BYTES_PER_GROUP * G)
-            if name == "hreg_group_l2":
-                G = args[5]
-                return self._timed("l2", lambda: orig_call(name, *args), L2_FLOPS_PER_GROUP * G,
-                                   L2_BYTES_PER_GROUP * G)
-            if name == "hreg_fine_head":
-                C, G = args[1], args[7]
-                N1 = 2 * C
-                fl = 2.0 * 8 * G * ((2 * C + 12) * N1 + 2 * N1 * N1)  # algorithmic (unpadded) MACs
-                nb = 4.0 * G * (8 * (16 + C + 1 + 3) + C + 3 + N1)
-                return self._timed("fine", lambda: orig_call(name, *args), fl, nb)
-            if name == "hreg_group_l3":
-                G = args[5]
-                return self._timed("l3", lambda: orig_call(name, *args), L3_FLOPS_PER_GROUP * G,
-                                   L3_BYTES_PER_GROUP * G)
+            if name in MFMA_ENTRIES:
+                kind, work = MFMA_ENTRIES[name]
+                fl, nb = work(args)
+                return self._timed(kind, lambda: orig_call(name, *args), fl, nb)
             return orig_call(name, *args)
         _lib.gemm = gemm
         engine.call = call
@@ -264,24 +275,30 @@ def main():
             pipe.run([(src, dst)] * args.steps)
         torch.cuda.synchronize()
     timer.enabled = False
-    gemm_ms, n_gemm, gemm_flops, gemm_bytes = timer.result("gemm")
-    l1_ms, n_l1, l1_flops, _ = timer.result("l1")
-    l2_ms, n_l2, l2_flops, _ = timer.result("l2")
-    l3_ms, n_l3, l3_flops, _ = timer.result("l3")
-    fh_ms, n_fh, fh_flops, _ = timer.result("fine")
+    res = {k: timer.result(k) for k in MfmaTimer.KINDS}
 
     elapsed = max_over_ranks(elapsed, device)
     value = job_throughput(B, args.steps, world, elapsed)
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank == 0:
-        per_launch_s = gemm_ms / max(n_gemm, 1) / 1e3
-        per_launch_flops = gemm_flops / max(n_gemm, 1)
+        def kind_summary(k):
+            ms, n, fl, nb = res[k]
+            return {"launches_per_step": n // args.steps,
+                    "avg_launch_us": round(ms / max(n, 1) * 1e3, 2),
+                    "ms_per_step": round(ms / args.steps, 3),
+                    "tflops": round(fl / max(ms, 1e-9) / 1e9, 2),
+                    "gflop_per_pair": round(fl / args.steps / B / 1e9, 3)}
+        f_ms, f_n, f_fl, f_nb = res["fused"]
+        per_launch_s = f_ms / max(f_n, 1) / 1e3
+        per_launch_flops = f_fl / max(f_n, 1)
         achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
-        traffic, traffic_src = pmc_traffic("gemm_nt_kernel")
-        roof = {"kernel": "gemm_nt_kernel (all tile instantiations): every 1x1-conv/BN/ReLU "
-                          "layer outside the fused level stages (correspondence heads, "
-                          "keypoint MLPs) + the cosine contraction",
+        traffic, traffic_src = pmc_traffic("group_fused_kernel")
+        tot_ms = sum(r[0] for r in res.values())
+        tot_fl = sum(r[2] for r in res.values())
+        roof = {"kernel": "group_fused_kernel (level-2 and level-3 keypoint detector + "
+                          "descriptor: every conv/BN/ReLU layer, attention and k-max of the "
+                          "level in one launch)",
                 "timing": "HIP events on the launch stream, " + (
                     "instrumented eager pipelined pass of the same steps after the timed "
                     "graph region" if args.executor == "graph" else "inside the timed region"),
@@ -289,24 +306,16 @@ def main():
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
                 "traffic": None if traffic is None else round(traffic),
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": round(gemm_bytes / max(n_gemm, 1)),
+                "algorithmic_bytes_per_launch": round(f_nb / max(f_n, 1)),
                 "flop_per_launch": round(per_launch_flops),
-                "launches_per_step": n_gemm // args.steps,
+                "launches_per_step": f_n // args.steps,
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
-                "gemm_ms_per_step": round(gemm_ms / args.steps, 3),
-                "algorithmic_gflop_per_pair": round(gemm_flops / args.steps / B / 1e9, 3),
-                "group_l1": {"avg_launch_us": round(l1_ms / max(n_l1, 1) * 1e3, 2),
-                             "tflops": round(l1_flops / max(l1_ms, 1e-9) / 1e9, 3),
-                             "gflop_per_pair": round(l1_flops / args.steps / B / 1e9, 3)},
-                "group_l2": {"avg_launch_us": round(l2_ms / max(n_l2, 1) * 1e3, 2),
-                             "tflops": round(l2_flops / max(l2_ms, 1e-9) / 1e9, 3),
-                             "gflop_per_pair": round(l2_flops / args.steps / B / 1e9, 3)},
-                "group_l3": {"avg_launch_us": round(l3_ms / max(n_l3, 1) * 1e3, 2),
-                             "tflops": round(l3_flops / max(l3_ms, 1e-9) / 1e9, 3),
-                             "gflop_per_pair": round(l3_flops / args.steps / B / 1e9, 3)},
-                "fine_head": {"avg_launch_us": round(fh_ms / max(n_fh, 1) * 1e3, 2),
-                              "tflops": round(fh_flops / max(fh_ms, 1e-9) / 1e9, 3),
-                              "gflop_per_pair": round(fh_flops / args.steps / B / 1e9, 3)}}
+                "other_mfma_kernels": {"gemm_nt_kernel": kind_summary("gemm"),
+                                       "group_l1_kernel": kind_summary("l1"),
+                                       "fine_head_kernel + nbr_head_kernel": kind_summary("head")},
+                "all_mfma": {"ms_per_step": round(tot_ms / args.steps, 3),
+                             "gflop_per_pair": round(tot_fl / args.steps / B / 1e9, 3),
+                             "tflops": round(tot_fl / max(tot_ms, 1e-9) / 1e9, 2)}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

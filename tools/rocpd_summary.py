@@ -16,8 +16,9 @@ import sqlite3
 import sys
 from collections import defaultdict
 
-FAMILIES = ("gemm_nt_kernel", "group_l1_kernel", "fps_reg_kernel", "knn_group_kernel",
-            "attend_kernel", "group_max_kernel", "knnd_kernel")
+FAMILIES = ("gemm_nt_kernel", "group_l1_kernel", "group_fused_kernel", "fine_head_kernel",
+            "nbr_head_kernel", "fps_reg_kernel", "knn_group", "spatial_index_kernel",
+            "attend_kernel", "knnd_kernel")
 
 
 def short(name):
