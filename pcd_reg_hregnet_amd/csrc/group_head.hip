@@ -95,6 +95,7 @@ __device__ __forceinline__ void mfma_pipe_rows(const gfloat *__restrict__ wf, in
                     for (int i = 0; i < NGS; ++i) cout[(s0 + i) * NCOUT + co] = v[i];
                 }
         }
+        __builtin_amdgcn_sched_barrier(0);  // loads stay at the top of the window
 #pragma unroll
         for (int s = 0; s < WIN; ++s)
 #pragma unroll
