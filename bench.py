@@ -206,7 +206,7 @@ def main():
     ap.add_argument("--executor", choices=("graph", "pipeline", "serial"), default="graph",
                     help="graph: pipelined forward replayed as HIP graphs; pipeline: same "
                          "eagerly; serial: no cross-batch overlap")
-    ap.add_argument("--lanes", type=int, default=2,
+    ap.add_argument("--lanes", type=int, default=4,
                     help="graph executor: batches in flight at once, one stream each "
                          "(a step is still one forward over one batch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)

@@ -86,6 +86,21 @@ __device__ __forceinline__ void conv_stack(const gfloat *__restrict__ tb, const 
     epilogue<T3>(eb + e3, lane, out);
 }
 
+// gathered feature rows: HREG_ROWS_NT = 1 reads them non-temporally so the random
+// row traffic does not evict the weight table from L2 (experiment switch)
+#ifndef HREG_ROWS_NT
+#define HREG_ROWS_NT 0
+#endif
+__device__ __forceinline__ float4 ld_rows(const float *p) {
+    if constexpr (HREG_ROWS_NT) {
+        typedef float v4 __attribute__((ext_vector_type(4)));
+        const v4 t = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p));
+        return make_float4(t[0], t[1], t[2], t[3]);
+    } else {
+        return *reinterpret_cast<const float4 *>(p);
+    }
+}
+
 template <class K>
 __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
@@ -151,7 +166,7 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
         {
             float4 fin[K::TF / 4];
 #pragma unroll
-            for (int i = 0; i < K::TF / 4; ++i) fin[i] = *reinterpret_cast<const float4 *>(fr + 4 * i);
+            for (int i = 0; i < K::TF / 4; ++i) fin[i] = ld_rows(fr + 4 * i);
             conv_stack<K, TM1, WM1>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1, K::E_D2,
                                     K::E_D3, lane, gin, fin, emb, carry, m1em, ca);
         }
@@ -202,7 +217,7 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
             const float *fr2 = reinterpret_cast<const float *>(fra);
             float4 fin[K::TF / 4];
 #pragma unroll
-            for (int i = 0; i < K::TF / 4; ++i) fin[i] = *reinterpret_cast<const float4 *>(fr2 + 4 * i);
+            for (int i = 0; i < K::TF / 4; ++i) fin[i] = ld_rows(fr2 + 4 * i);
             conv_stack<K, TM1, WM1>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1, K::E_E2,
                                     K::E_E3, lane, gin, fin, x1d, cb, m1x2, ca);
         }

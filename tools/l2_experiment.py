@@ -21,9 +21,9 @@ SRC = os.path.join(REPO, "pcd_reg_hregnet_amd", "csrc", "group_fused.hip")
 
 def build(exp):
     out = f"/tmp/l2exp_{exp}.so"
+    flags = {"nt": ["-DHREG_ROWS_NT=1"]}.get(exp, [f"-DHREG_L2_EXP={exp}"])
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                           "-ffp-contract=off", "-shared", "-fPIC", f"-DHREG_L2_EXP={exp}", SRC,
-                           "-o", out])
+                           "-ffp-contract=off", "-shared", "-fPIC", *flags, SRC, "-o", out])
     return out
 
 
@@ -33,7 +33,7 @@ def main():
     b = 16
     G = b * 512
     res = {}
-    for exp in (0, 2):
+    for exp in (0, 5):
         L = ctypes.CDLL(build(exp))
         L.hreg_group_l2_table_floats.restype = ctypes.c_int
         nt = L.hreg_group_l2_table_floats()
