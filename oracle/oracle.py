@@ -317,8 +317,10 @@ def coarse_reg(sd, pre, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w, k=8)
     return corres, _sigmoid(w[:, 0]), kidx
 
 
-def fine_reg(sd, pre, src_xyz, src_feat, dst_xyz, dst_feat, src_w, dst_w, k=8):
-    """FineReg.forward, layers.py:433-454."""
+def fine_reg(sd, pre, src_xyz, src_feat, dst_xyz, dst_feat, src_w, dst_w, k=8,
+             return_att=False):
+    """FineReg.forward, layers.py:433-454 (return_att: also the attentive features
+    [B, 2C, M] that model_v2/layers.py:471-481 feeds to mlpx)."""
     _, kidx = knn(src_xyz, dst_xyz, k)
     knn_xyz = knn_gather(dst_xyz, kidx)
     sf = np.ascontiguousarray(src_feat.transpose(0, 2, 1))
@@ -337,6 +339,8 @@ def fine_reg(sd, pre, src_xyz, src_feat, dst_xyz, dst_feat, src_w, dst_w, k=8):
     att = np.sum(a[:, None] * f, axis=-1).astype(np.float32)
     w = _mlp(_mlp(att, sd, pre + ".mlp1"), sd, pre + ".mlp2")
     w = _mlp(w, sd, pre + ".mlp3", act=False)
+    if return_att:
+        return corres, _sigmoid(w[:, 0]), kidx, att
     return corres, _sigmoid(w[:, 0]), kidx
 
 
@@ -403,3 +407,34 @@ def hregnet_forward(sd, src, dst, use_weights=True):
     return dict(src_xyz_corres_3=c3, src_xyz_corres_2=c2, src_xyz_corres_1=c1,
                 src_dst_weights_3=w3, src_dst_weights_2=w2, src_dst_weights_1=w1,
                 rotation=[R3, R2, R1], translation=[t3, t2, t1], src_feats=sf, dst_feats=df)
+
+
+def model_v2_forward(sd, src, dst, perm_feats, perm_weights, use_weights=True):
+    """Model_V2.forward, models/model_v2/models.py:77-183 (eval mode): HRegNet with
+    FineReg2 (model_v2/layers.py:462-500), whose attentive features also pass through
+    mlpx (Conv1d 2C->C + BN + ReLU).  The "prime" copies are batch-shuffled by the two
+    torch.randperm(B) draws the reference makes (features first, then weights,
+    models.py:118-119); the caller passes them in."""
+    sf = feature_extraction(sd, src, use_weights)
+    df = feature_extraction(sd, dst, use_weights)
+    c3, w3, _ = coarse_reg(sd, "coarse_corres", sf["xyz_3"], sf["desc_3"], df["xyz_3"],
+                           df["desc_3"], sf["sigmas_3"], df["sigmas_3"])
+    R3, t3 = weighted_svd(sf["xyz_3"], c3, w3)
+    x2t = _transform(R3, t3, sf["xyz_2"])
+    c2, w2, _, att2 = fine_reg(sd, "fine_corres_2", x2t, sf["desc_2"], df["xyz_2"],
+                               df["desc_2"], sf["sigmas_2"], df["sigmas_2"], return_att=True)
+    f2 = _mlp(att2, sd, "fine_corres_2.mlpx")
+    R2_, t2_ = weighted_svd(x2t, c2, w2)
+    R2, t2 = _compose(R2_, t2_, R3, t3)
+    x1t = _transform(R2, t2, sf["xyz_1"])
+    c1, w1, _ = fine_reg(sd, "fine_corres_1", x1t, sf["desc_1"], df["xyz_1"], df["desc_1"],
+                         sf["sigmas_1"], df["sigmas_1"])
+    R1_, t1_ = weighted_svd(x1t, c1, w1)
+    R1, t1 = _compose(R1_, t1_, R2, t2)
+    return dict(src_xyz_corres_3=c3, src_xyz_corres_2=c2, src_xyz_corres_1=c1,
+                rotation=[R3, R2, R1], translation=[t3, t2, t1],
+                src_feats_desc_2=sf["desc_2"], src_feats_sigmas_2=sf["sigmas_2"],
+                src_xyz_2_trans=x2t, dst_xyz_2=df["xyz_2"],
+                src_dst_feats_2=f2, src_dst_feats_2_prime=f2[np.asarray(perm_feats)],
+                src_dst_weights_2=w2, src_dst_weights_2_prime=w2[np.asarray(perm_weights)],
+                src_feats=sf, dst_feats=df)

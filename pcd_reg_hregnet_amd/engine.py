@@ -130,6 +130,9 @@ class PreparedWeights:
         self.fine = {}
         for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64)):
             self.fine[name] = (_stack(sd, name + ".convs_1", 3, _perm_fine(C)), _mlp_head(sd, name))
+        # Model_V2's FineReg2.mlpx (model_v2/layers.py:457-459), when the state dict has it
+        self.mlpx = (_conv_bn(sd, "fine_corres_2.mlpx.0", "fine_corres_2.mlpx.1")
+                     if "fine_corres_2.mlpx.0.weight" in sd else None)
         self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
         self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
@@ -138,7 +141,7 @@ class PreparedWeights:
         self.nbr_table = nbr_head_table(self.coarse_convs2, 256)
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
                      "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "fine_table",
-                     "nbr_table"):
+                     "nbr_table", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
 
@@ -637,7 +640,8 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     return corres.view(B, N1, 3), w.view(B, N1)
 
 
-def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w):
+def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w,
+             return_att=False):
     """FineReg.forward (layers.py:433-454); xyz [B,N,3], desc [B*N,C], w [B*N]."""
     dev = src_xyz.device
     k = K_HEAD
@@ -658,6 +662,8 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
         call("hreg_fine_head", P.fine_table[name], C, small, src_desc, dst_desc, gidx, kx, B * N,
              corres, att, _stream())
         w = _mlp_weights(att, head, B * N, B, N)
+        if return_att:
+            return corres.view(B, N, 3), w.view(B, N), att
         return corres.view(B, N, 3), w.view(B, N)
     small = _empty(R, 12, device=dev)
     kx = _empty(R, 3, device=dev)
@@ -670,6 +676,8 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
     f = gemm([_seg(f, 0, f.shape[1])], convs[2], R)
     _, att, corres = attend(f, B * N, k, vals=f, xyz_rows=kx)
     w = _mlp_weights(att, head, B * N, B, N)
+    if return_att:
+        return corres.view(B, N, 3), w.view(B, N), att
     return corres.view(B, N, 3), w.view(B, N)
 
 
@@ -735,6 +743,62 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts
         "src_dst_weights_3": w3, "src_dst_weights_2": w2, "src_dst_weights_1": w1,
         "rotation": [R3, R2, R1], "translation": [t3, t2, t1],
         "src_feats": feats(0), "dst_feats": feats(1),
+        "_fps_idx": [fe[f"fps_idx_{i + 1}"] for i in range(3)],
+    }
+
+
+def model_v2_forward(P: PreparedWeights, src, dst, use_weights=True):
+    """Model_V2.forward (models/model_v2/models.py:77-183), eval mode: the HRegNet
+    forward with FineReg2 (model_v2/layers.py:426-500), whose attentive features also
+    go through mlpx (Conv1d 2C->C + BN + ReLU), and the batch-shuffled "prime"
+    copies drawn with torch.randperm on the default generator in the reference's
+    order (features first, then weights)."""
+    if P.mlpx is None:
+        raise RuntimeError("model_v2_forward: the state dict has no fine_corres_2.mlpx")
+    B, N, _ = src.shape
+    pts = torch.cat([src, dst], 0).contiguous()
+    fe = feature_extraction(P, pts, use_weights)
+    M = [lv[0] for lv in LEVELS]
+    xyz = [fe[f"xyz_{i + 1}"] for i in range(3)]
+    sig = [fe[f"sigmas_{i + 1}"] for i in range(3)]
+    desc = [fe[f"desc_{i + 1}"] for i in range(3)]
+
+    def split(t, rows):
+        return t[:B * rows], t[B * rows:]
+
+    c3, w3 = coarse_reg(P, B, xyz[2], desc[2], sig[2])
+    _, _, R3, t3 = weighted_svd(xyz[2][:B], c3, w3)
+    x2t = transform(xyz[1][:B], R3, t3)
+    sd2, dd2 = split(desc[1], M[1])
+    ss2, ds2 = split(sig[1], M[1])
+    c2, w2, att2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2,
+                            return_att=True)
+    f2 = gemm([_seg(att2, 0, att2.shape[1])], P.mlpx, B * M[1])
+    feats2 = f2.view(B, M[1], -1).transpose(1, 2)
+    feats2_prime = feats2[torch.randperm(B)]
+    w2_prime = w2[torch.randperm(B)]
+    _, _, R2, t2 = weighted_svd(x2t, c2, w2, prev=(R3, t3))
+    x1t = transform(xyz[0][:B], R2, t2)
+    sd1, dd1 = split(desc[0], M[0])
+    ss1, ds1 = split(sig[0], M[0])
+    c1, w1 = fine_reg(P, "fine_corres_1", B, x1t, sd1, xyz[0][B:], dd1, ss1, ds1)
+    _, _, R1, t1 = weighted_svd(x1t, c1, w1, prev=(R2, t2))
+
+    def feats(part):
+        sl = slice(0, B) if part == 0 else slice(B, 2 * B)
+        return {f"{key}_{i + 1}": val for i in range(3) for key, val in (
+            ("xyz", xyz[i][sl]), ("sigmas", sig[i].view(2 * B, M[i])[sl]),
+            ("desc", desc[i].view(2 * B, M[i], -1)[sl].transpose(1, 2)))}
+
+    sf, df = feats(0), feats(1)
+    return {
+        "src_xyz_corres_3": c3, "src_xyz_corres_2": c2, "src_xyz_corres_1": c1,
+        "rotation": [R3, R2, R1], "translation": [t3, t2, t1],
+        "src_feats_desc_2": sf["desc_2"], "src_feats_sigmas_2": sf["sigmas_2"],
+        "src_xyz_2_trans": x2t, "dst_xyz_2": df["xyz_2"],
+        "src_dst_feats_2": feats2, "src_dst_feats_2_prime": feats2_prime,
+        "src_dst_weights_2": w2, "src_dst_weights_2_prime": w2_prime,
+        "src_feats": sf, "dst_feats": df,
         "_fps_idx": [fe[f"fps_idx_{i + 1}"] for i in range(3)],
     }
 

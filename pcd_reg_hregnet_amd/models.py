@@ -95,6 +95,17 @@ class FineReg(_HIPOnly):
         self.mlp1, self.mlp2, self.mlp3 = _head(2 * C)
 
 
+FineReg1 = FineReg  # model_v2/layers.py:368-424 (same layout as FineReg)
+
+
+class FineReg2(FineReg):
+    """Parameter layout of model_v2/layers.py:426-460: FineReg + mlpx (Conv1d 2C->C+BN+ReLU)."""
+
+    def __init__(self, k, in_channels):
+        super().__init__(k, in_channels)
+        self.mlpx = nn.Sequential(*_conv_bn_relu(2 * in_channels, in_channels, 1, bias=True))
+
+
 class WeightedSVDHead(nn.Module):
     """layers.py:456-504 on the HIP library: (src, src_corres, weights) -> (R, t)."""
 
@@ -219,6 +230,44 @@ class HRegNet(nn.Module):
                                      dst_points.float().contiguous(),
                                      self.feature_extraction.use_weights)
         out.pop("_fps_idx", None)
+        for part in ("src_feats", "dst_feats"):
+            out[part] = {k: v.contiguous() for k, v in out[part].items()}
+        return out
+
+
+class Model_V2(nn.Module):
+    """models/model_v2/models.py:60-183 (inference): HRegNet with FineReg2 (mlpx
+    features + batch-shuffled "prime" copies for the MI loss)."""
+
+    def __init__(self, args):
+        super().__init__()
+        self.feature_extraction = HierFeatureExtraction(args)
+        if args.freeze_feats:
+            for p in self.parameters():
+                p.requires_grad = False
+        self.coarse_corres = CoarseReg(k=8, in_channels=256, use_sim=True, use_neighbor=True)
+        self.fine_corres_2 = FineReg2(k=8, in_channels=128)
+        self.fine_corres_1 = FineReg1(k=8, in_channels=64)
+        self.svd_head = WeightedSVDHead()
+        self._prep = _Prepared()
+
+    def prepared(self, device):
+        return self._prep.get(self, device)
+
+    def forward(self, src_points, dst_points):
+        if self.training:
+            raise NotImplementedError(
+                "train-mode forward (batch-statistics BN + backward kernels) is not implemented "
+                "on the HIP path yet; call .eval()")
+        if not self.feature_extraction.use_fps:
+            raise NotImplementedError("use_fps=False (random sampling) is not implemented")
+        P = self.prepared(src_points.device)
+        out = engine.model_v2_forward(P, src_points.float().contiguous(),
+                                      dst_points.float().contiguous(),
+                                      self.feature_extraction.use_weights)
+        out.pop("_fps_idx", None)
+        for key in ("src_feats_desc_2", "src_dst_feats_2", "src_dst_feats_2_prime"):
+            out[key] = out[key].contiguous()
         for part in ("src_feats", "dst_feats"):
             out[part] = {k: v.contiguous() for k, v in out[part].items()}
         return out

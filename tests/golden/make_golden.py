@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -244,8 +244,65 @@ def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict) -> di
     return out
 
 
+def model_v2_fixture(Model_V2, pu, src: np.ndarray, dst: np.ndarray, sd: dict, seed: int) -> dict:
+    """Reference Model_V2 forward (models/model_v2/models.py:77-183) in eval mode; the
+    randperm "prime" shuffles come from torch's default generator seeded with `seed`."""
+    net = Model_V2(_Args())
+    net.load_state_dict(sd)
+    net.eval()
+    pu.calls.clear()
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        r = net(torch.from_numpy(src), torch.from_numpy(dst))
+    out = {"src": src, "dst": dst, "perm_seed": np.array(seed)}
+    for i, (R, t) in enumerate(zip(r["rotation"], r["translation"])):
+        out[f"R{3 - i}"] = R.numpy()
+        out[f"t{3 - i}"] = t.numpy()
+    for key in ("src_xyz_corres_3", "src_xyz_corres_2", "src_xyz_corres_1", "src_feats_desc_2",
+                "src_feats_sigmas_2", "src_xyz_2_trans", "dst_xyz_2", "src_dst_feats_2",
+                "src_dst_feats_2_prime", "src_dst_weights_2", "src_dst_weights_2_prime"):
+        out[key] = r[key].numpy()
+    for lv in (1, 2, 3):
+        for part in ("src", "dst"):
+            f = r[f"{part}_feats"]
+            out[f"{part}_xyz_{lv}"] = f[f"xyz_{lv}"].numpy()
+            out[f"{part}_sigmas_{lv}"] = f[f"sigmas_{lv}"].numpy()
+            out[f"{part}_desc_{lv}"] = f[f"desc_{lv}"].numpy()
+    names = ["src_fps_1", "src_fps_2", "src_fps_3", "dst_fps_1", "dst_fps_2", "dst_fps_3"]
+    for name, (_, idx) in zip(names, pu.calls):
+        out[name] = idx.numpy()
+    return out
+
+
+def v2_fixtures(pu):
+    """Model_V2 (config 5 shape: 65536-point clouds) fixtures."""
+    import models.utils as mu  # reference helpers, re-exported by models/__init__.py
+    pkg = sys.modules["models"]
+    for name in ("furthest_point_sample", "weighted_furthest_point_sample", "gather_operation",
+                 "set_seed"):
+        setattr(pkg, name, getattr(mu, name))
+    tr = sys.modules["pytorch3d.transforms"]
+    for name in ("axis_angle_to_matrix", "rotation_6d_to_matrix"):
+        setattr(tr, name, lambda *a, **k: (_ for _ in ()).throw(NotImplementedError()))
+    from models.model_v2.models import Model_V2  # noqa: E402  (reference code)
+    from pcd_reg_hregnet_amd import synthetic, weights
+    template = Model_V2(_Args()).state_dict()
+    sd = weights.make_state_dict(template, seed=0, pretrained_feats=True)
+    s, d, _, _ = synthetic.lidar_batch(2, 4096, seed0=50)
+    np.savez_compressed(os.path.join(HERE, "model_v2_lidar_b2_n4096.npz"),
+                        **model_v2_fixture(Model_V2, pu, s, d, sd, seed=7))
+    print("model_v2 b2 n4096 fixture written", flush=True)
+    s, d, _, _ = synthetic.lidar_batch(1, 65536, seed0=60)
+    np.savez_compressed(os.path.join(HERE, "model_v2_lidar_b1_n65536.npz"),
+                        **model_v2_fixture(Model_V2, pu, s, d, sd, seed=8))
+    print("model_v2 b1 n65536 fixture written", flush=True)
+
+
 def main():
     pu = install_shims()
+    if "--v2-only" in sys.argv:
+        v2_fixtures(pu)
+        return
     from models.HRegNet.models import HRegNet  # noqa: E402  (reference code)
     from pcd_reg_hregnet_amd import synthetic, weights
 
@@ -271,6 +328,7 @@ def main():
     fx["R_gt"], fx["t_gt"] = Rg, tg
     np.savez_compressed(os.path.join(HERE, "hregnet_lidar_b2_n4096.npz"), **fx)
     print("lidar fixture written", flush=True)
+    v2_fixtures(pu)
 
 
 if __name__ == "__main__":

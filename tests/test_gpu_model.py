@@ -261,3 +261,58 @@ def test_fused_nbr_head_matches_layerwise(net):
     (c_f, w_f), (c_r, w_r) = outs
     torch.testing.assert_close(c_f, c_r, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)
+
+
+@pytest.fixture(scope="module")
+def net_v2():
+    from helpers import state_dict_v2_torch
+    from pcd_reg_hregnet_amd.models import Model_V2
+    m = Model_V2(Args())
+    m.load_state_dict(state_dict_v2_torch())
+    return m.cuda().eval()
+
+
+@pytest.mark.parametrize("fixture", ["model_v2_lidar_b2_n4096.npz",
+                                     "model_v2_lidar_b1_n65536.npz"])
+def test_model_v2_matches_reference_fixture(net_v2, fixture):
+    """Model_V2 against the reference's own run of the same
+    weights/inputs; torch's generator is seeded as the fixture run was, so the
+    randperm "prime" shuffles are the same draws.  The N=65536 case is config 5's
+    cloud size (level-1 FPS from HBM, brute-force level-1 grouping)."""
+    from test_oracle_golden import compare_v2
+    from pcd_reg_hregnet_amd import engine
+    g = load_npz(fixture)
+    B = g["src"].shape[0]
+    P = net_v2.prepared(torch.device("cuda"))
+    torch.manual_seed(int(g["perm_seed"]))
+    with torch.no_grad():
+        r = engine.model_v2_forward(P, torch.from_numpy(g["src"]).cuda(),
+                                    torch.from_numpy(g["dst"]).cuda())
+    torch.cuda.synchronize()
+
+    def cpu(x):
+        if isinstance(x, torch.Tensor):
+            return x.cpu().numpy()
+        if isinstance(x, list):
+            return [cpu(v) for v in x]
+        if isinstance(x, dict):
+            return {k: cpu(v) for k, v in x.items()}
+        return x
+    r = cpu(r)
+    np.testing.assert_array_equal(r["_fps_idx"][0][:B], g["src_fps_1"])
+    np.testing.assert_array_equal(r["_fps_idx"][0][B:], g["dst_fps_1"])
+    compare_v2(r, g)
+
+
+def test_model_v2_module_api(net_v2):
+    """Model_V2.forward returns the reference's dict (model_v2/models.py:170-183)."""
+    g = load_npz("model_v2_lidar_b2_n4096.npz")
+    torch.manual_seed(int(g["perm_seed"]))
+    with torch.no_grad():
+        r = net_v2(torch.from_numpy(g["src"]).cuda(), torch.from_numpy(g["dst"]).cuda())
+    assert "_fps_idx" not in r
+    assert tuple(r["src_dst_feats_2"].shape) == (2, 128, 512)
+    assert tuple(r["src_dst_weights_2_prime"].shape) == (2, 512)
+    assert tuple(r["src_xyz_2_trans"].shape) == (2, 512, 3)
+    np.testing.assert_allclose(r["rotation"][-1].cpu().numpy(), g["R1"], atol=1e-4)
+    np.testing.assert_allclose(r["translation"][-1].cpu().numpy(), g["t1"], atol=1e-4)

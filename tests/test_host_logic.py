@@ -32,6 +32,22 @@ def test_state_dict_keys_match_reference_checkpoint():
     assert n_params == 2467846  # SURVEY.md 5 (DDP all-reduce size)
 
 
+def test_model_v2_state_dict_layout():
+    """Model_V2 = HRegNet's parameters + fine_corres_2.mlpx (model_v2/layers.py:460-462:
+    Conv1d(256->128, bias) + BatchNorm1d(128)); the V2 fixture weights load strictly."""
+    from helpers import state_dict_v2_torch
+    from pcd_reg_hregnet_amd.models import HRegNet, Model_V2
+    v2 = Model_V2(Args())
+    extra = set(v2.state_dict()) - set(HRegNet(Args()).state_dict())
+    assert extra == {"fine_corres_2.mlpx.0.weight", "fine_corres_2.mlpx.0.bias",
+                     "fine_corres_2.mlpx.1.weight", "fine_corres_2.mlpx.1.bias",
+                     "fine_corres_2.mlpx.1.running_mean", "fine_corres_2.mlpx.1.running_var",
+                     "fine_corres_2.mlpx.1.num_batches_tracked"}
+    assert tuple(v2.state_dict()["fine_corres_2.mlpx.0.weight"].shape) == (128, 256, 1)
+    assert sum(p.numel() for p in v2.parameters()) == 2467846 + 256 * 128 + 128 + 2 * 128
+    v2.load_state_dict(state_dict_v2_torch())
+
+
 def test_weights_deterministic():
     a = state_dict_torch()
     b = state_dict_torch()

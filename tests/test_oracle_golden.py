@@ -8,7 +8,7 @@ within the stated tolerances.
 import numpy as np
 import pytest
 
-from helpers import load_npz, state_dict_numpy
+from helpers import load_npz, state_dict_numpy, state_dict_v2_torch, v2_perms
 from oracle import oracle
 
 OPS = load_npz("ops.npz")
@@ -93,3 +93,44 @@ def test_forward_matches_reference(sd, fixture):
     np.testing.assert_array_equal(r["src_feats"]["fps_idx_1"], g["src_fps_1"])
     np.testing.assert_array_equal(r["dst_feats"]["fps_idx_1"], g["dst_fps_1"])
     compare_forward(r, g)
+
+
+# Model_V2 outputs indexed by source keypoint: [B, M, ...] (channel-major ones transposed)
+V2_ROWS = {"src_xyz_corres_3": 1e-3, "src_xyz_corres_2": 1e-3, "src_xyz_corres_1": 1e-3,
+           "src_xyz_2_trans": 1e-3, "src_feats_sigmas_2": 1e-3, "src_feats_desc_2": 1e-3,
+           "src_dst_feats_2": 1e-3, "src_dst_feats_2_prime": 1e-3,
+           "src_dst_weights_2": 1e-3, "src_dst_weights_2_prime": 1e-3}
+V2_CHANNEL_MAJOR = ("src_feats_desc_2", "src_dst_feats_2", "src_dst_feats_2_prime")
+
+
+def compare_v2(r, g, max_flip_frac=0.01):
+    """Model_V2 parity (model_v2/models.py:170-183): the HRegNet contract of
+    compare_forward, plus every extra output row-wise within rtol 1e-3 / atol 1e-4 on
+    all but max_flip_frac of the rows (a WFPS near-tie flip upstream moves a few rows),
+    and the prime copies exactly the batch permutation of their originals."""
+    compare_forward(r, g, max_flip_frac=max_flip_frac)
+    for key, rtol in V2_ROWS.items():
+        a = np.asarray(r[key])
+        b = g[key]
+        assert a.shape == b.shape, (key, a.shape, b.shape)
+        if key in V2_CHANNEL_MAJOR:
+            a, b = a.transpose(0, 2, 1), b.transpose(0, 2, 1)
+        a = a.reshape(a.shape[0], a.shape[1], -1)
+        b = b.reshape(a.shape)
+        ok = np.all(np.abs(a - b) <= 1e-4 + rtol * np.abs(b), axis=-1)
+        assert 1.0 - ok.mean() <= max_flip_frac, (key, 1.0 - ok.mean())
+    a = np.asarray(r["dst_xyz_2"])
+    ok = np.abs(a - g["dst_xyz_2"]).max(-1) <= 1e-3 + 1e-3 * np.abs(g["dst_xyz_2"]).max(-1)
+    assert 1.0 - ok.mean() <= max_flip_frac
+
+
+@pytest.mark.parametrize("fixture", ["model_v2_lidar_b2_n4096.npz",
+                                     "model_v2_lidar_b1_n65536.npz"])
+def test_model_v2_matches_reference(fixture):
+    """oracle.model_v2_forward vs the reference Model_V2 run (make_golden.py)."""
+    g = load_npz(fixture)
+    sd = {k: v.numpy() for k, v in state_dict_v2_torch().items()}
+    pf, pw = v2_perms(g["perm_seed"], g["src"].shape[0])
+    r = oracle.model_v2_forward(sd, g["src"], g["dst"], pf, pw)
+    np.testing.assert_array_equal(r["src_feats"]["fps_idx_1"], g["src_fps_1"])
+    compare_v2(r, g)
