@@ -32,6 +32,8 @@ PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak BW (spec)
 POINTS = 16384
 PAIRS_PER_GPU = 8
+V2_POINTS = 65536      # config 5 (MANTruckScenes-shape): B=16 over 8 GPUs -> 2 pairs/GPU
+V2_PAIRS_PER_GPU = 2
 
 
 class _Args:
@@ -41,10 +43,10 @@ class _Args:
     freeze_feats = False
 
 
-def make_model(device):
+def make_model(device, model="hregnet"):
     from pcd_reg_hregnet_amd import weights
-    from pcd_reg_hregnet_amd.models import HRegNet
-    net = HRegNet(_Args())
+    from pcd_reg_hregnet_amd.models import HRegNet, Model_V2
+    net = (Model_V2 if model == "v2" else HRegNet)(_Args())
     net.load_state_dict(weights.make_state_dict(net.state_dict(), seed=0, pretrained_feats=True))
     return net.to(device).eval()
 
@@ -200,8 +202,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=PAIRS_PER_GPU, help="pairs per GPU")
-    ap.add_argument("--points", type=int, default=POINTS)
+    ap.add_argument("--model", choices=("hregnet", "v2"), default="hregnet",
+                    help="v2: Model_V2 at config 5 (2 x 65536-pt pairs per GPU, serial executor)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help=f"pairs per GPU (default {PAIRS_PER_GPU}; {V2_PAIRS_PER_GPU} for v2)")
+    ap.add_argument("--points", type=int, default=None,
+                    help=f"points per cloud (default {POINTS}; {V2_POINTS} for v2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--executor", choices=("graph", "pipeline", "serial"), default="graph",
                     help="graph: pipelined forward replayed as HIP graphs; pipeline: same "
@@ -213,6 +219,14 @@ def main():
     ap.add_argument("--layerwise", default="",
                     help="comma list of levels (1,2,3) to run layer by layer instead of fused")
     args = ap.parse_args()
+    v2 = args.model == "v2"
+    if args.batch is None:
+        args.batch = V2_PAIRS_PER_GPU if v2 else PAIRS_PER_GPU
+    if args.points is None:
+        args.points = V2_POINTS if v2 else POINTS
+    if v2:
+        # the randperm "prime" draws happen on the host each forward: no graph replay
+        args.executor, args.lanes = "serial", 1
     if args.executor == "graph" and args.steps % args.lanes:
         ap.error("--steps must be a multiple of --lanes")
 
@@ -228,7 +242,7 @@ def main():
     _lib.load()
     for lv in filter(None, args.layerwise.split(",")):
         setattr(engine, f"FUSED_L{int(lv)}", False)
-    net = make_model(device)
+    net = make_model(device, args.model)
     P = net.prepared(device)
     B = args.batch
     s, d, _, _ = shard_batch(rank, B, args.points)
@@ -246,6 +260,8 @@ def main():
 
     def run(n):
         with torch.no_grad():
+            if v2:
+                return [engine.model_v2_forward(P, src, dst) for _ in range(n)]
             if args.executor == "serial":
                 return [engine.hregnet_forward(P, src, dst) for _ in range(n)]
             if args.executor == "graph":
@@ -317,19 +333,22 @@ def main():
                              "gflop_per_pair": round(tot_fl / args.steps / B / 1e9, 3),
                              "tflops": round(tot_fl / max(tot_ms, 1e-9) / 1e9, 2)}}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not v2:
             try:
                 cpu = cpu_baseline(args.cpu_budget)
             except Exception as e:  # the baseline must never sink the GPU number
                 cpu = {"error": repr(e)}
         line = {
-            "metric": "point-cloud pairs/sec, HRegNet forward, 16384-pt pairs",
+            "metric": ("point-cloud pairs/sec, Model_V2 forward, 65536-pt pairs (config 5)" if v2
+                       else "point-cloud pairs/sec, HRegNet forward, 16384-pt pairs"),
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded KITTI-shape LiDAR pairs; nusc_feats + seeded heads)",
-            "config": {"workload": f"HRegNet forward (eval), batch={B} pairs/GPU, "
-                                   f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])",
+            "config": {"workload": (f"Model_V2 forward (eval), batch={B} pairs/GPU, 2x{args.points}"
+                                    "-pt LiDAR pairs (BASELINE configs[4])") if v2 else (
+                                   f"HRegNet forward (eval), batch={B} pairs/GPU, "
+                                   f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])"),
                        "executor": args.executor + ("" if args.executor == "serial" else
                                    " (level-1 FPS of step i+1 overlaps step i)") + (
                                    f", {args.lanes} batches in flight" if args.lanes > 1 and

@@ -37,6 +37,8 @@
  *   hreg_weighted_svd                     <- WeightedSVDHead.forward (layers.py:469-504) + T = T_ @ T_prev
  *                                            composition (models/HRegNet/models.py:100-127)
  *   hreg_transform_points                 <- R @ xyz^T + t (models/HRegNet/models.py:91-92,113-114)
+ *   hreg_transformation_loss              <- transformation_loss + calc_rot_rre_err + calc_tran_rte_err
+ *                                            (losses/losses.py:97-164; callers train/train_reg_v1.py:101,252)
  */
 #ifndef HREGNET_AMD_H
 #define HREGNET_AMD_H
@@ -57,9 +59,11 @@ enum {
 
 /* ---------------- point_utils_cuda boundary ---------------- */
 
-/* points [b,n,3] f32, temp [b,n] f32 (may be NULL for n <= 16384; receives the
- * final running-min distances), idx [b,m] int32 (out), sampled_xyz [b,m,3]
- * (optional out: gathered coordinates of idx). */
+/* points [b,n,3] f32, temp [b,n] f32 scratch (required for n > 16384, may be NULL
+ * below; for n <= 16384 it receives the final running-min distances, above its
+ * contents are unspecified -- it holds the workgroups' exchange slots; the
+ * reference's caller discards temp, models/utils.py:24-27), idx [b,m] int32 (out),
+ * sampled_xyz [b,m,3] (optional out: gathered coordinates of idx). */
 int hreg_furthest_point_sampling(int b, int n, int m, const float *points, float *temp,
                                  int32_t *idx, float *sampled_xyz, void *stream);
 
@@ -187,6 +191,16 @@ int hreg_weighted_svd(const float *src, const float *corres, const float *w, int
 /* out[b][i] = R[b] xyz[b][i] + t[b], xyz/out [nb][n][3] */
 int hreg_transform_points(const float *xyz, const float *R, const float *t, int nb, int n,
                           float *out, void *stream);
+
+/* transformation_loss (losses/losses.py:97-164) for one level of nb pairs, all device
+ * pointers: pred_R/gt_R [nb][3][3], pred_t/gt_t [nb][3].  Outputs (each may be NULL):
+ * scalars[3] = {alpha*loss_R + loss_t, loss_R, loss_t}; R_err[3] = batch-mean |Euler XYZ
+ * angles| of pred_R^T gt_R in degrees; T_err[3] = batch-mean |pred_t - gt_t|;
+ * geodesic[nb] (RRE, degrees); eucl[nb] (RTE).  Deterministic (fixed-order reduction).
+ * Forward only (no gradient). */
+int hreg_transformation_loss(const float *pred_R, const float *pred_t, const float *gt_R,
+                             const float *gt_t, int nb, float alpha, float *scalars, float *R_err,
+                             float *T_err, float *geodesic, float *eucl, void *stream);
 
 /* Spatial index for exact culled kNN grouping (n <= 16384 points per cloud):
  * hreg_spatial_index sorts each cloud of p [nb][n][3] by Morton code and records

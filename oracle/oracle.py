@@ -438,3 +438,24 @@ def model_v2_forward(sd, src, dst, perm_feats, perm_weights, use_weights=True):
                 src_dst_feats_2=f2, src_dst_feats_2_prime=f2[np.asarray(perm_feats)],
                 src_dst_weights_2=w2, src_dst_weights_2_prime=w2[np.asarray(perm_weights)],
                 src_feats=sf, dst_feats=df)
+
+
+def transformation_loss(pred_R, pred_t, gt_R, gt_t, alpha=1.0):
+    """transformation_loss, losses/losses.py:97-164, with pytorch3d 0.7.8's
+    matrix_to_euler_angles(E, "XYZ") restated as (atan2(-E12, E22), asin(E02),
+    atan2(-E01, E00)) (pytorch3d is absent: SURVEY.md 8c).  fp32 like the reference.
+    Returns (loss, loss_R, loss_t, R_err[3], geodesic_dist[B], T_err[3], eucl_dist[B])."""
+    f = np.float32
+    E = np.matmul(pred_R.transpose(0, 2, 1).astype(f), gt_R.astype(f))
+    resi = np.sqrt(np.sum((E - np.eye(3, dtype=f)) ** 2, axis=(1, 2)))
+    eul = np.stack([np.arctan2(-E[:, 1, 2], E[:, 2, 2]), np.arcsin(E[:, 0, 2]),
+                    np.arctan2(-E[:, 0, 1], E[:, 0, 0])], -1).astype(f)
+    R_err = np.mean(np.abs(np.rad2deg(eul)), axis=0)
+    cos = np.clip((np.trace(E, axis1=1, axis2=2) - f(1)) / f(2), -1.0, 1.0).astype(f)
+    geo = np.rad2deg(np.arccos(cos)).astype(f)
+    dt = (pred_t - gt_t).astype(f)
+    T_err = np.mean(np.abs(dt), axis=0)
+    eucl = np.sqrt(np.sum(dt * dt, axis=1)).astype(f)
+    loss_R = np.mean(resi).astype(f)
+    loss_t = np.mean(eucl).astype(f)
+    return (f(alpha) * loss_R + loss_t, loss_R, loss_t, R_err.astype(f), geo, T_err.astype(f), eucl)

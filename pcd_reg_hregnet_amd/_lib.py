@@ -63,6 +63,8 @@ _SIGS = {
                         _vp],
     "hreg_weighted_svd": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_transform_points": [_vp, _vp, _vp, _i, _i, _vp, _vp],
+    "hreg_transformation_loss": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
+                                 _vp],
     "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],

@@ -308,6 +308,153 @@ __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// Large clouds (16384 < n <= 64 * 64 * 32): one cloud spread over NP <= 64
+// single-wave workgroups ("participants"), every point still register-resident.
+// Participant p's lane l owns the S consecutive reference ranks
+// (p * 64 + l) * S + s, rank = rp * Q + i for point k = bitrev_L(rp) + i * bs
+// (the fps_mem_kernel order), so "max d2, then lowest participant, lane, slot"
+// is the reference winner.  Per iteration each participant publishes its
+// candidate as four 64-bit words {d2 | rank | tag, x | j, y | j, z | j} with
+// agent-scope relaxed atomic stores into a per-cloud, per-parity slot, then one
+// lane per participant polls those slots (agent-scope atomic loads) until every
+// word carries this iteration's tag: the data is its own flag, so there is no
+// counter, fence or L2 write-back on the critical path.  A participant cannot
+// reach iteration j + 2 (same parity slot) before every participant has
+// published j + 1, i.e. finished reading j.  The slots live in the caller's
+// temp buffer, zeroed by the launcher (tags 0 never match j >= 1).  Every
+// poll loop is bounded; on expiry the kernel flags the cloud's idx[0] = -1 and
+// every wave exits.
+struct SyncSlot {
+    uint64_t w[4];
+};
+constexpr int FPS_CL_MAXP = 64;
+constexpr uint32_t FPS_CL_POLLS = 1u << 22;
+
+__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int S, bool WEIGHTED>
+__global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict__ xyz,
+                                                         const float *__restrict__ wts,
+                                                         SyncSlot *__restrict__ slots,
+                                                         int32_t *__restrict__ idx_out,
+                                                         float *__restrict__ sampled_out, int b,
+                                                         int n, int m, int bs, int L, int Q, int NP,
+                                                         float inf) {
+    constexpr int S2 = S / 2;
+    static_assert(S % 2 == 0 && S <= 32, "slots");
+    const int p = blockIdx.x;  // participant
+    const int lane = threadIdx.x;
+    for (int cloud = blockIdx.y; cloud < b; cloud += gridDim.y) {
+        const float *P = xyz + (size_t)cloud * n * 3;
+        const float *W = WEIGHTED ? wts + (size_t)cloud * n : nullptr;
+        SyncSlot *sl = slots + (size_t)cloud * 2 * FPS_CL_MAXP;
+        f2 PX[S2], PY[S2], PZ[S2], PT[S2], PW[S2];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int rank = (p * 64 + lane) * S + s;
+            const int rp = rank / Q, i = rank - rp * Q;
+            const int k = (int)bitrev_bits((uint32_t)rp, L) + i * bs;
+            const bool ok = rp < bs && k < n;
+            const int kk = ok ? k : 0;
+            PX[s / 2][s % 2] = P[kk * 3 + 0];
+            PY[s / 2][s % 2] = P[kk * 3 + 1];
+            PZ[s / 2][s % 2] = P[kk * 3 + 2];
+            PW[s / 2][s % 2] = WEIGHTED ? W[kk] : 1.0f;
+            PT[s / 2][s % 2] = ok ? 1e10f : -__builtin_huge_valf();
+        }
+        float x1 = P[0], y1 = P[1], z1 = P[2];
+        if (p == 0 && lane == 0) {
+            idx_out[(size_t)cloud * m] = 0;
+            if (sampled_out) {
+                float *o = sampled_out + (size_t)cloud * m * 3;
+                o[0] = x1; o[1] = y1; o[2] = z1;
+            }
+        }
+        for (int j = 1; j < m; ++j) {
+            const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
+            float best = -1.0f;
+#pragma unroll
+            for (int s = 0; s < S2; ++s) {
+                const f2 dx = PX[s] - X1, dy = PY[s] - Y1, dz = PZ[s] - Z1;
+                f2 d = (dx * dx + dy * dy) + dz * dz;
+                if (WEIGHTED) d = PW[s] * d;
+                f2 t;
+                t.x = fmin_nc(d.x, PT[s].x, inf);
+                t.y = fmin_nc(d.y, PT[s].y, inf);
+                PT[s] = t;
+                best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
+            }
+            const float wmax = wave_max_uniform(best, inf);
+            uint32_t smask = 0;
+#pragma unroll
+            for (int s = 0; s < S; ++s) smask |= (PT[s / 2][s % 2] == wmax) ? (1u << s) : 0u;
+            const int myslot = smask ? (int)__builtin_ctz(smask) : 0;
+            const uint64_t hit = __ballot(best == wmax);
+            const int wl = (int)__builtin_ctzll(hit);
+            const int ws = __builtin_amdgcn_readlane(myslot, wl);
+            float wx = 0.f, wy = 0.f, wz = 0.f;
+            pick_slot<0, S>(ws, wl, PX, PY, PZ, wx, wy, wz);
+            const uint32_t rank = (uint32_t)((p * 64 + wl) * S + ws);
+            SyncSlot *cur = sl + (j & 1) * FPS_CL_MAXP;
+            const uint64_t tag = (uint64_t)(uint32_t)j << 32;
+            if (lane == 0) {
+                st_agent(&cur[p].w[1], tag | __float_as_uint(wx));
+                st_agent(&cur[p].w[2], tag | __float_as_uint(wy));
+                st_agent(&cur[p].w[3], tag | __float_as_uint(wz));
+                st_agent(&cur[p].w[0], ((uint64_t)__float_as_uint(wmax) << 32) |
+                                           ((uint64_t)rank << 10) | (uint64_t)(j & 1023));
+            }
+            // poll: lane q reads participant q's words until all carry tag j
+            uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+            bool fresh = lane >= NP;
+            uint32_t polls = 0;
+            while (true) {
+                if (!fresh) {
+                    w0 = ld_agent(&cur[lane].w[0]);
+                    w1 = ld_agent(&cur[lane].w[1]);
+                    w2 = ld_agent(&cur[lane].w[2]);
+                    w3 = ld_agent(&cur[lane].w[3]);
+                    fresh = (w0 & 1023u) == (uint64_t)(j & 1023) && (w1 >> 32) == (uint64_t)j &&
+                            (w2 >> 32) == (uint64_t)j && (w3 >> 32) == (uint64_t)j;
+                }
+                if (__all(fresh)) break;
+                if (++polls > FPS_CL_POLLS) {
+                    if (lane == 0) idx_out[(size_t)cloud * m] = -1;
+                    return;
+                }
+            }
+            const float cd = lane < NP ? __uint_as_float((uint32_t)(w0 >> 32)) : -__builtin_huge_valf();
+            const float gmax = wave_max_uniform(cd, inf);
+            const int gl = (int)__builtin_ctzll(__ballot(lane < NP && cd == gmax));
+            int old;
+            if (gmax > -1.0f) {
+                const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w0, gl) >> 10;
+                const uint32_t rp = r / (uint32_t)Q, i = r - rp * (uint32_t)Q;
+                old = (int)bitrev_bits(rp, L) + (int)i * bs;
+                x1 = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w1, gl));
+                y1 = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w2, gl));
+                z1 = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w3, gl));
+            } else {  // the reference keeps (best=-1, besti=0)
+                old = 0;
+                x1 = P[0]; y1 = P[1]; z1 = P[2];
+            }
+            if (p == 0 && lane == 0) {
+                idx_out[(size_t)cloud * m + j] = old;
+                if (sampled_out) {
+                    float *o = sampled_out + ((size_t)cloud * m + j) * 3;
+                    o[0] = x1; o[1] = y1; o[2] = z1;
+                }
+            }
+        }
+    }
+}
+
 template <bool WEIGHTED, bool STAMP = false>
 bool launch_reg(int T, int G, int QT, int b, int n, int m, int bs, int L, const float *xyz,
                 const float *w, float *temp, int32_t *idx, float *sampled, uint64_t *stamps,
@@ -367,8 +514,28 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
         HREG_CHECK_LAUNCH();
         return HREG_OK;
     }
-    // large clouds: temp through memory (caller's temp buffer is required)
+    // large clouds: the caller's temp buffer is required (sync slots / running minima)
     if (temp == nullptr) return HREG_ERR_INVALID;
+    const long ranks = (long)bs * Q;
+    int S = 0;
+    for (int s : {8, 16, 32})
+        if (ranks <= (long)FPS_CL_MAXP * 64 * s) { S = s; break; }
+    const size_t slot_bytes = (size_t)2 * FPS_CL_MAXP * sizeof(SyncSlot);
+    if (S && (size_t)n * sizeof(float) >= slot_bytes && getenv("HREG_FPS_MEM") == nullptr) {
+        const int NP = (int)((ranks + 64L * S - 1) / (64L * S));
+        const int clusters = b < 1024 / NP ? b : 1024 / NP;  // <= 1024 resident waves
+        SyncSlot *slots = reinterpret_cast<SyncSlot *>(temp);
+        if (hipMemsetAsync(slots, 0, (size_t)b * slot_bytes, st) != hipSuccess) return HREG_ERR_LAUNCH;
+        const dim3 grid(NP, clusters);
+#define HREG_FPS_CL(SS)                                                                         \
+    if (S == SS)                                                                                \
+        hipLaunchKernelGGL((fps_cluster_kernel<SS, WEIGHTED>), grid, dim3(64), 0, st, xyz, w,     \
+                           slots, idx, sampled, b, n, m, bs, L, Q, NP, __builtin_huge_valf());
+        HREG_FPS_CL(8) HREG_FPS_CL(16) HREG_FPS_CL(32)
+#undef HREG_FPS_CL
+        HREG_CHECK_LAUNCH();
+        return HREG_OK;
+    }
     hipLaunchKernelGGL((fps_mem_kernel<WEIGHTED>), dim3(b), dim3(1024), 0, st, xyz, w, temp, idx,
                        sampled, n, m, bs, L, Q);
     HREG_CHECK_LAUNCH();

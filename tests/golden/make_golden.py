@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py [--v2-only]   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only | --loss-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -298,10 +298,80 @@ def v2_fixtures(pu):
     print("model_v2 b1 n65536 fixture written", flush=True)
 
 
+def p3d_angle_from_tan(axis, other_axis, data, horizontal, tait_bryan):
+    """pytorch3d 0.7.8 transforms/rotation_conversions.py _angle_from_tan (restated:
+    pytorch3d is not installed here)."""
+    i1, i2 = {"X": (2, 1), "Y": (0, 2), "Z": (1, 0)}[axis]
+    if horizontal:
+        i2, i1 = i1, i2
+    even = (axis + other_axis) in ["XY", "YZ", "ZX"]
+    if horizontal == even:
+        return torch.atan2(data[..., i1], data[..., i2])
+    if tait_bryan:
+        return torch.atan2(-data[..., i2], data[..., i1])
+    return torch.atan2(data[..., i2], -data[..., i1])
+
+
+def p3d_matrix_to_euler_angles(matrix, convention):
+    """pytorch3d 0.7.8 matrix_to_euler_angles (restated; the loss's only pytorch3d call)."""
+    idx = {"X": 0, "Y": 1, "Z": 2}
+    i0, i2 = idx[convention[0]], idx[convention[2]]
+    tait_bryan = i0 != i2
+    if tait_bryan:
+        central = torch.asin(matrix[..., i0, i2] * (-1.0 if i0 - i2 in [-1, 2] else 1.0))
+    else:
+        central = torch.acos(matrix[..., i0, i0])
+    o = (p3d_angle_from_tan(convention[0], convention[1], matrix[..., i2], False, tait_bryan),
+         central,
+         p3d_angle_from_tan(convention[2], convention[1], matrix[..., i0, :], True, tait_bryan))
+    return torch.stack(o, -1)
+
+
+def loss_fixtures():
+    """Reference transformation_loss (losses/losses.py:97-164) on the HRegNet lidar fixture's
+    per-level (R, t) against its ground truth, and on seeded random rotations (small,
+    large, and exact-identity errors)."""
+    sys.modules["pytorch3d.transforms"].matrix_to_euler_angles = p3d_matrix_to_euler_angles
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_losses", os.path.join(REF, "losses/losses.py"))
+    L = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(L)
+    from pcd_reg_hregnet_amd import synthetic
+    fx = dict(np.load(os.path.join(HERE, "hregnet_lidar_b2_n4096.npz")))
+    cases = [(np.stack([fx["R3"], fx["R2"], fx["R1"]]), np.stack([fx["t3"], fx["t2"], fx["t1"]]),
+              np.repeat(fx["R_gt"][None], 3, 0), np.repeat(fx["t_gt"][None], 3, 0))]
+    rng = np.random.default_rng(77)
+    for B, deg in ((16, 2.0), (16, 60.0), (300, 20.0)):
+        gR = np.stack([synthetic.random_se3(rng, 180.0)[0] for _ in range(B)]).astype(np.float32)
+        dR = np.stack([synthetic.random_se3(rng, deg)[0] for _ in range(B)]).astype(np.float32)
+        pR = np.matmul(gR, dR).astype(np.float32)
+        if B == 16 and deg == 2.0:
+            pR[3] = gR[3]  # exact: geodesic at the acos(1) end
+        gt = rng.normal(0, 1, (B, 3)).astype(np.float32)
+        pt = (gt + rng.normal(0, 0.1, (B, 3))).astype(np.float32)
+        cases.append((pR[None], pt[None], gR[None], gt[None]))
+    out = {}
+    for c, (pR, pt, gR, gt) in enumerate(cases):
+        res = [L.transformation_loss(torch.from_numpy(pR[i]), torch.from_numpy(pt[i]),
+                                     torch.from_numpy(gR[i]), torch.from_numpy(gt[i]), alpha=1.5)
+               for i in range(pR.shape[0])]
+        out[f"c{c}_pred_R"], out[f"c{c}_pred_t"], out[f"c{c}_gt_R"], out[f"c{c}_gt_t"] = pR, pt, gR, gt
+        for k, name in enumerate(("loss", "loss_R", "loss_t", "R_err", "geodesic_dist", "T_err",
+                                  "eucl_dist")):
+            out[f"c{c}_{name}"] = np.stack([r[k].numpy() for r in res])
+    out["alpha"] = np.array(1.5, np.float32)
+    out["ncases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(HERE, "transformation_loss.npz"), **out)
+    print("transformation_loss.npz written", flush=True)
+
+
 def main():
     pu = install_shims()
     if "--v2-only" in sys.argv:
         v2_fixtures(pu)
+        return
+    if "--loss-only" in sys.argv:
+        loss_fixtures()
         return
     from models.HRegNet.models import HRegNet  # noqa: E402  (reference code)
     from pcd_reg_hregnet_amd import synthetic, weights
@@ -329,6 +399,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "hregnet_lidar_b2_n4096.npz"), **fx)
     print("lidar fixture written", flush=True)
     v2_fixtures(pu)
+    loss_fixtures()
 
 
 if __name__ == "__main__":

@@ -45,7 +45,9 @@ def test_fps_vs_reference_fixture(case):
 
 @pytest.mark.parametrize("n,m,weighted", [(16384, 1024, False), (1024, 512, True), (512, 256, True),
                                           (2048, 700, False), (20000, 64, False), (20000, 64, True),
-                                          (3, 5, False), (1, 4, False), (777, 300, True)])
+                                          (3, 5, False), (1, 4, False), (777, 300, True),
+                                          (65536, 1024, False), (40000, 300, True),
+                                          (131072, 64, False), (140000, 8, False)])
 def test_fps_vs_oracle(n, m, weighted):
     from pcd_reg_hregnet_amd import point_utils_cuda as pu
     rng = np.random.default_rng(n * 7 + m)
@@ -61,6 +63,30 @@ def test_fps_vs_oracle(n, m, weighted):
         pu.furthest_point_sampling_wrapper(B, n, m, dev(xyz), temp, idx)
     ref = oracle.fps(xyz, m, w)
     np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+
+
+def test_fps_cluster_many_clouds_and_mem_path():
+    """n > 16384 runs on the multi-workgroup kernel; more clouds than resident clusters
+    (1024 / 64 participants = 16) loop; HREG_FPS_MEM forces the single-workgroup
+    memory path, which must agree bit for bit."""
+    import os
+    from pcd_reg_hregnet_amd import point_utils_cuda as pu
+    rng = np.random.default_rng(11)
+    B, n, m = 20, 65536, 48
+    xyz = rng.uniform(-40, 40, (B, n, 3)).astype(np.float32)
+    xyz[:, ::3] = np.round(xyz[:, ::3])
+    x = dev(xyz)
+    a = torch.empty((B, m), dtype=torch.int32, device="cuda")
+    b = torch.empty((B, m), dtype=torch.int32, device="cuda")
+    pu.furthest_point_sampling_wrapper(B, n, m, x, torch.empty((B, n), device="cuda"), a)
+    os.environ["HREG_FPS_MEM"] = "1"
+    try:
+        pu.furthest_point_sampling_wrapper(B, n, m, x, torch.full((B, n), 1e10, device="cuda"), b)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["HREG_FPS_MEM"]
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    np.testing.assert_array_equal(a.cpu().numpy()[:2], oracle.fps(xyz[:2], m, None))
 
 
 def test_fps_zero_points_requested():
@@ -298,3 +324,40 @@ def test_knn_group_indexed_matches_bruteforce(case, K):
     torch.cuda.synchronize()
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("c", range(int(load_npz("transformation_loss.npz")["ncases"])))
+def test_transformation_loss_matches_reference(c):
+    """hreg_transformation_loss vs the reference losses.py:97-164 run (A16)."""
+    from test_oracle_golden import LOSS, check_loss
+    from pcd_reg_hregnet_amd import transformation_loss
+    for i in range(LOSS[f"c{c}_pred_R"].shape[0]):
+        args = [torch.from_numpy(LOSS[f"c{c}_{k}"][i]).cuda()
+                for k in ("pred_R", "pred_t", "gt_R", "gt_t")]
+        res = transformation_loss(*args, alpha=float(LOSS["alpha"]))
+        check_loss([r.cpu().numpy() for r in res], c, i)
+
+
+def test_transformation_loss_deterministic_and_checked():
+    from pcd_reg_hregnet_amd import calc_rot_rre_err, calc_tran_rte_err, transformation_loss
+    rng = np.random.default_rng(3)
+    B = 1000
+    pR = torch.from_numpy(rng.normal(size=(B, 3, 3)).astype(np.float32)).cuda()
+    gR = torch.from_numpy(rng.normal(size=(B, 3, 3)).astype(np.float32)).cuda()
+    pt = torch.from_numpy(rng.normal(size=(B, 3)).astype(np.float32)).cuda()
+    gt = torch.from_numpy(rng.normal(size=(B, 3)).astype(np.float32)).cuda()
+    # non-rotation inputs: asin of |E02| > 1 is NaN (as in the reference); NaN == NaN here
+    a = [r.cpu().numpy() for r in transformation_loss(pR, pt, gR, gt)]
+    b = [r.cpu().numpy() for r in transformation_loss(pR, pt, gR, gt)]
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    R_err, geo = calc_rot_rre_err(pR, gR)
+    np.testing.assert_array_equal(R_err.cpu().numpy(), a[3])
+    np.testing.assert_array_equal(geo.cpu().numpy(), a[4])
+    T_err, eucl = calc_tran_rte_err(pt, gt)
+    np.testing.assert_array_equal(T_err.cpu().numpy(), a[5])
+    np.testing.assert_array_equal(eucl.cpu().numpy(), a[6])
+    with pytest.raises(ValueError):
+        transformation_loss(pR.cpu(), pt, gR, gt)
+    with pytest.raises(ValueError):
+        transformation_loss(pR[:, :2], pt, gR, gt)
