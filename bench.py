@@ -224,9 +224,6 @@ def main():
         args.batch = V2_PAIRS_PER_GPU if v2 else PAIRS_PER_GPU
     if args.points is None:
         args.points = V2_POINTS if v2 else POINTS
-    if v2:
-        # the randperm "prime" draws happen on the host each forward: no graph replay
-        args.executor, args.lanes = "serial", 1
     if args.executor == "graph" and args.steps % args.lanes:
         ap.error("--steps must be a multiple of --lanes")
 
@@ -252,17 +249,17 @@ def main():
     timer = MfmaTimer()
     timer.install()
 
-    pipe = engine.Pipeline(P, device)
+    pipe = engine.Pipeline(P, device, v2=v2)
     gpipe = None
     if args.executor == "graph":
         with torch.no_grad():
-            gpipe = engine.GraphPipeline(P, src, dst, lanes=args.lanes)
+            gpipe = engine.GraphPipeline(P, src, dst, lanes=args.lanes, v2=v2)
 
     def run(n):
         with torch.no_grad():
-            if v2:
-                return [engine.model_v2_forward(P, src, dst) for _ in range(n)]
             if args.executor == "serial":
+                if v2:
+                    return [engine.model_v2_forward(P, src, dst) for _ in range(n)]
                 return [engine.hregnet_forward(P, src, dst) for _ in range(n)]
             if args.executor == "graph":
                 return gpipe.run(-(-n // args.lanes))

@@ -325,8 +325,20 @@ __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__
 // temp buffer, zeroed by the launcher (tags 0 never match j >= 1).  Every
 // poll loop is bounded; on expiry the kernel flags the cloud's idx[0] = -1 and
 // every wave exits.
+// tools/fps_experiment.py variants: HREG_FPS_EXP 1 = four lanes publish in one store
+// instruction, 2 = s_sleep between polls; HREG_FPS_S forces the slots per lane,
+// HREG_FPS_PAD the slot stride (16: one 128-byte line per participant)
+#ifndef HREG_FPS_EXP
+#define HREG_FPS_EXP 0
+#endif
+#ifndef HREG_FPS_S
+#define HREG_FPS_S 0
+#endif
+#ifndef HREG_FPS_PAD
+#define HREG_FPS_PAD 4
+#endif
 struct SyncSlot {
-    uint64_t w[4];
+    uint64_t w[HREG_FPS_PAD];  // HREG_FPS_PAD = 16: one 128-byte line per participant
 };
 constexpr int FPS_CL_MAXP = 64;
 constexpr uint32_t FPS_CL_POLLS = 1u << 22;
@@ -403,6 +415,19 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
             const uint32_t rank = (uint32_t)((p * 64 + wl) * S + ws);
             SyncSlot *cur = sl + (j & 1) * FPS_CL_MAXP;
             const uint64_t tag = (uint64_t)(uint32_t)j << 32;
+            // lane 0 publishes; the coordinates first, the key word last.  (Variant 1,
+            // lanes 0..3 storing one word each in a single instruction, lets the polls
+            // start before the stores are acknowledged and measured slower: 2.45 vs
+            // 1.71 ms for 4 x 65536 points.)
+#if HREG_FPS_EXP == 1
+            if (lane < 4) {
+                const float c = lane == 1 ? wx : lane == 2 ? wy : wz;
+                const uint64_t v = lane == 0 ? ((uint64_t)__float_as_uint(wmax) << 32) |
+                                                   ((uint64_t)rank << 10) | (uint64_t)(j & 1023)
+                                             : tag | __float_as_uint(c);
+                st_agent(&cur[p].w[lane], v);
+            }
+#else
             if (lane == 0) {
                 st_agent(&cur[p].w[1], tag | __float_as_uint(wx));
                 st_agent(&cur[p].w[2], tag | __float_as_uint(wy));
@@ -410,6 +435,7 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                 st_agent(&cur[p].w[0], ((uint64_t)__float_as_uint(wmax) << 32) |
                                            ((uint64_t)rank << 10) | (uint64_t)(j & 1023));
             }
+#endif
             // poll: lane q reads participant q's words until all carry tag j
             uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
             bool fresh = lane >= NP;
@@ -424,6 +450,9 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                             (w2 >> 32) == (uint64_t)j && (w3 >> 32) == (uint64_t)j;
                 }
                 if (__all(fresh)) break;
+#if HREG_FPS_EXP == 2
+                __builtin_amdgcn_s_sleep(1);
+#endif
                 if (++polls > FPS_CL_POLLS) {
                     if (lane == 0) idx_out[(size_t)cloud * m] = -1;
                     return;
@@ -519,11 +548,13 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
     const long ranks = (long)bs * Q;
     int S = 0;
     for (int s : {8, 16, 32})
-        if (ranks <= (long)FPS_CL_MAXP * 64 * s) { S = s; break; }
+        if (ranks <= (long)FPS_CL_MAXP * 64 * s && (!HREG_FPS_S || s >= HREG_FPS_S)) { S = s; break; }
     const size_t slot_bytes = (size_t)2 * FPS_CL_MAXP * sizeof(SyncSlot);
     if (S && (size_t)n * sizeof(float) >= slot_bytes && getenv("HREG_FPS_MEM") == nullptr) {
         const int NP = (int)((ranks + 64L * S - 1) / (64L * S));
-        const int clusters = b < 1024 / NP ? b : 1024 / NP;  // <= 1024 resident waves
+        // <= 256 spinning waves per launch: with a few launches in flight on other
+        // streams (GraphPipeline lanes) every launch still fits on the chip at once
+        const int clusters = b < 256 / NP ? b : 256 / NP;
         SyncSlot *slots = reinterpret_cast<SyncSlot *>(temp);
         if (hipMemsetAsync(slots, 0, (size_t)b * slot_bytes, st) != hipSuccess) return HREG_ERR_LAUNCH;
         const dim3 grid(NP, clusters);

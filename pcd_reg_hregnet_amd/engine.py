@@ -701,8 +701,13 @@ def transform(xyz, R, t):
     return out
 
 
-def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=None):
-    """HRegNet.forward (models/HRegNet/models.py:77-148), eval mode."""
+def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=None, v2=False):
+    """HRegNet.forward (models/HRegNet/models.py:77-148), eval mode.
+
+    v2: the Model_V2 variant (models/model_v2/models.py:77-183): fine_corres_2 is
+    FineReg2 (model_v2/layers.py:462-500), whose attentive features also pass
+    through mlpx (Conv1d 2C->C + BN + ReLU) -> "src_dst_feats_2" [B, C, M2]; the
+    batch-shuffled prime copies are added by model_v2_finish (host RNG)."""
     B, N, _ = src.shape
     if pts is None:
         pts = torch.cat([src, dst], 0).contiguous()
@@ -720,7 +725,14 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts
     x2t = transform(xyz[1][:B], R3, t3)
     sd2, dd2 = split(desc[1], M[1])
     ss2, ds2 = split(sig[1], M[1])
-    c2, w2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2)
+    if v2:
+        if P.mlpx is None:
+            raise RuntimeError("Model_V2 forward: the state dict has no fine_corres_2.mlpx")
+        c2, w2, att2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2,
+                                return_att=True)
+        f2 = gemm([_seg(att2, 0, att2.shape[1])], P.mlpx, B * M[1])
+    else:
+        c2, w2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2)
     _, _, R2, t2 = weighted_svd(x2t, c2, w2, prev=(R3, t3))
     x1t = transform(xyz[0][:B], R2, t2)
     sd1, dd1 = split(desc[0], M[0])
@@ -738,69 +750,45 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts
             d[f"desc_{i + 1}"] = desc[i].view(2 * B, m, -1)[sl].transpose(1, 2)
         return d
 
-    return {
+    out = {
         "src_xyz_corres_3": c3, "src_xyz_corres_2": c2, "src_xyz_corres_1": c1,
         "src_dst_weights_3": w3, "src_dst_weights_2": w2, "src_dst_weights_1": w1,
         "rotation": [R3, R2, R1], "translation": [t3, t2, t1],
         "src_feats": feats(0), "dst_feats": feats(1),
         "_fps_idx": [fe[f"fps_idx_{i + 1}"] for i in range(3)],
     }
+    if v2:
+        out["src_xyz_2_trans"] = x2t
+        out["src_dst_feats_2"] = f2.view(B, M[1], -1).transpose(1, 2)
+    return out
+
+
+def model_v2_finish(out):
+    """The Model_V2 result dict (models/model_v2/models.py:145-183) from
+    hregnet_forward(..., v2=True): the "prime" copies are batch shuffles drawn with
+    torch.randperm(B) on the default (host) generator, features first, then weights
+    (model_v2/layers.py:491-497), as the reference draws them."""
+    f2, w2 = out["src_dst_feats_2"], out["src_dst_weights_2"]
+    B = w2.shape[0]
+    pf = torch.randperm(B)
+    pw = torch.randperm(B)
+    sf, df = out["src_feats"], out["dst_feats"]
+    return {
+        "src_xyz_corres_3": out["src_xyz_corres_3"], "src_xyz_corres_2": out["src_xyz_corres_2"],
+        "src_xyz_corres_1": out["src_xyz_corres_1"],
+        "rotation": out["rotation"], "translation": out["translation"],
+        "src_feats_desc_2": sf["desc_2"], "src_feats_sigmas_2": sf["sigmas_2"],
+        "src_xyz_2_trans": out["src_xyz_2_trans"], "dst_xyz_2": df["xyz_2"],
+        "src_dst_feats_2": f2, "src_dst_feats_2_prime": f2[pf.to(f2.device)],
+        "src_dst_weights_2": w2, "src_dst_weights_2_prime": w2[pw.to(w2.device)],
+        "src_feats": sf, "dst_feats": df,
+        "_fps_idx": out["_fps_idx"],
+    }
 
 
 def model_v2_forward(P: PreparedWeights, src, dst, use_weights=True):
-    """Model_V2.forward (models/model_v2/models.py:77-183), eval mode: the HRegNet
-    forward with FineReg2 (model_v2/layers.py:426-500), whose attentive features also
-    go through mlpx (Conv1d 2C->C + BN + ReLU), and the batch-shuffled "prime"
-    copies drawn with torch.randperm on the default generator in the reference's
-    order (features first, then weights)."""
-    if P.mlpx is None:
-        raise RuntimeError("model_v2_forward: the state dict has no fine_corres_2.mlpx")
-    B, N, _ = src.shape
-    pts = torch.cat([src, dst], 0).contiguous()
-    fe = feature_extraction(P, pts, use_weights)
-    M = [lv[0] for lv in LEVELS]
-    xyz = [fe[f"xyz_{i + 1}"] for i in range(3)]
-    sig = [fe[f"sigmas_{i + 1}"] for i in range(3)]
-    desc = [fe[f"desc_{i + 1}"] for i in range(3)]
-
-    def split(t, rows):
-        return t[:B * rows], t[B * rows:]
-
-    c3, w3 = coarse_reg(P, B, xyz[2], desc[2], sig[2])
-    _, _, R3, t3 = weighted_svd(xyz[2][:B], c3, w3)
-    x2t = transform(xyz[1][:B], R3, t3)
-    sd2, dd2 = split(desc[1], M[1])
-    ss2, ds2 = split(sig[1], M[1])
-    c2, w2, att2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2,
-                            return_att=True)
-    f2 = gemm([_seg(att2, 0, att2.shape[1])], P.mlpx, B * M[1])
-    feats2 = f2.view(B, M[1], -1).transpose(1, 2)
-    feats2_prime = feats2[torch.randperm(B)]
-    w2_prime = w2[torch.randperm(B)]
-    _, _, R2, t2 = weighted_svd(x2t, c2, w2, prev=(R3, t3))
-    x1t = transform(xyz[0][:B], R2, t2)
-    sd1, dd1 = split(desc[0], M[0])
-    ss1, ds1 = split(sig[0], M[0])
-    c1, w1 = fine_reg(P, "fine_corres_1", B, x1t, sd1, xyz[0][B:], dd1, ss1, ds1)
-    _, _, R1, t1 = weighted_svd(x1t, c1, w1, prev=(R2, t2))
-
-    def feats(part):
-        sl = slice(0, B) if part == 0 else slice(B, 2 * B)
-        return {f"{key}_{i + 1}": val for i in range(3) for key, val in (
-            ("xyz", xyz[i][sl]), ("sigmas", sig[i].view(2 * B, M[i])[sl]),
-            ("desc", desc[i].view(2 * B, M[i], -1)[sl].transpose(1, 2)))}
-
-    sf, df = feats(0), feats(1)
-    return {
-        "src_xyz_corres_3": c3, "src_xyz_corres_2": c2, "src_xyz_corres_1": c1,
-        "rotation": [R3, R2, R1], "translation": [t3, t2, t1],
-        "src_feats_desc_2": sf["desc_2"], "src_feats_sigmas_2": sf["sigmas_2"],
-        "src_xyz_2_trans": x2t, "dst_xyz_2": df["xyz_2"],
-        "src_dst_feats_2": feats2, "src_dst_feats_2_prime": feats2_prime,
-        "src_dst_weights_2": w2, "src_dst_weights_2_prime": w2_prime,
-        "src_feats": sf, "dst_feats": df,
-        "_fps_idx": [fe[f"fps_idx_{i + 1}"] for i in range(3)],
-    }
+    """Model_V2.forward (models/model_v2/models.py:77-183), eval mode."""
+    return model_v2_finish(hregnet_forward(P, src, dst, use_weights, v2=True))
 
 
 class Pipeline:
@@ -813,8 +801,9 @@ class Pipeline:
     through the complete forward; results are identical to hregnet_forward.
     """
 
-    def __init__(self, P: PreparedWeights, device):
+    def __init__(self, P: PreparedWeights, device, v2: bool = False):
         self.P = P
+        self.v2 = v2
         self.side = torch.cuda.Stream(device=device)
 
     def _stage1(self, src, dst):
@@ -851,7 +840,8 @@ class Pipeline:
             pts.record_stream(main)
             for t in g:
                 t.record_stream(main)
-            outs.append(hregnet_forward(self.P, src, dst, use_weights, l1=g, pts=pts))
+            out = hregnet_forward(self.P, src, dst, use_weights, l1=g, pts=pts, v2=self.v2)
+            outs.append(model_v2_finish(out) if self.v2 else out)
         return outs
 
 
@@ -869,10 +859,14 @@ class GraphPipeline:
     rest of the forward from A}, g_BA symmetric; replaying them alternately
     overlaps batch i+1's level-1 FPS with batch i.  Every batch runs the
     complete forward; outputs are bitwise those of ``hregnet_forward``.
+    v2: the Model_V2 forward; the prime shuffles (host torch.randperm, as the
+    reference draws them) are gathered eagerly after each round's replay.
     """
 
-    def __init__(self, P: PreparedWeights, src, dst, use_weights=True, lanes: int = 1):
+    def __init__(self, P: PreparedWeights, src, dst, use_weights=True, lanes: int = 1,
+                 v2: bool = False):
         self.P = P
+        self.v2 = v2
         self.use_weights = use_weights
         self.lanes = lanes
         dev = src.device
@@ -941,7 +935,7 @@ class GraphPipeline:
     def _rest(self, ln, cur):
         pts, g = self.bufs[ln][cur]
         return hregnet_forward(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g,
-                               pts=pts)
+                               pts=pts, v2=self.v2)
 
     def load(self, src, dst, lane: int = 0):
         self.src[lane].copy_(src)
@@ -957,7 +951,12 @@ class GraphPipeline:
         cur = 0
         for i in range(steps - 1):
             self.g_step[cur].replay()
+            if self.v2:  # host-RNG prime shuffles of this round, after its replay
+                for o in self.outs[cur]:
+                    model_v2_finish(o)
             cur = 1 - cur
         self.g_last[cur].replay()
         out = self.outs_last[cur]
+        if self.v2:
+            out = [model_v2_finish(o) for o in out]
         return out[0] if self.lanes == 1 else out

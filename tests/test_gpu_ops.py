@@ -67,7 +67,7 @@ def test_fps_vs_oracle(n, m, weighted):
 
 def test_fps_cluster_many_clouds_and_mem_path():
     """n > 16384 runs on the multi-workgroup kernel; more clouds than resident clusters
-    (1024 / 64 participants = 16) loop; HREG_FPS_MEM forces the single-workgroup
+    (256 / 64 participants = 4) loop; HREG_FPS_MEM forces the single-workgroup
     memory path, which must agree bit for bit."""
     import os
     from pcd_reg_hregnet_amd import point_utils_cuda as pu

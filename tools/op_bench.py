@@ -1,6 +1,6 @@
 """Micro-benchmarks of single C-ABI ops on the GPU (HIP events, median of reps).
 
-usage: python tools/op_bench.py fps|wfps|knn|all [--b 16]
+usage: python tools/op_bench.py fps|fps64k|wfps|knn|l2|all [--b 16]
 """
 import argparse
 import os
@@ -40,6 +40,14 @@ def main():
     if a.what in ("fps", "all"):
         x = torch.from_numpy(rng.uniform(-40, 40, (a.b, 16384, 3)).astype(np.float32)).cuda()
         res["fps_l1_ms"] = timeit(lambda: engine.fps(x, 1024))
+    if a.what in ("fps64k", "all"):
+        # config 5 level 1: 2 pairs -> 4 clouds of 65536 points (multi-workgroup FPS)
+        for nb in (4, 16):
+            x = torch.from_numpy(rng.uniform(-40, 40, (nb, 65536, 3)).astype(np.float32)).cuda()
+            res[f"fps_65536_b{nb}_ms"] = timeit(lambda: engine.fps(x, 1024))
+        p = x[:4].contiguous()
+        q = p[:, :1024].contiguous()
+        res["knn_group_65536_b4_ms"] = timeit(lambda: engine.knn_group(q, p, 64))
     if a.what in ("wfps", "all"):
         for n, m in ((1024, 512), (512, 256)):
             x = torch.from_numpy(rng.uniform(-40, 40, (a.b, n, 3)).astype(np.float32)).cuda()
