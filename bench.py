@@ -84,6 +84,8 @@ MFMA_ENTRIES = {
     "hreg_group_l1": ("l1", lambda a: (L1_FLOPS_PER_GROUP * a[3], L1_BYTES_PER_GROUP * a[3])),
     "hreg_group_l2": ("fused", lambda a: (L2_FLOPS_PER_GROUP * a[5], L2_BYTES_PER_GROUP * a[5])),
     "hreg_group_l3": ("fused", lambda a: (L3_FLOPS_PER_GROUP * a[5], L3_BYTES_PER_GROUP * a[5])),
+    "hreg_group_split_l2": ("fused", lambda a: (L2_FLOPS_PER_GROUP * a[5], L2_BYTES_PER_GROUP * a[5])),
+    "hreg_group_split_l3": ("fused", lambda a: (L3_FLOPS_PER_GROUP * a[5], L3_BYTES_PER_GROUP * a[5])),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
 }
@@ -216,6 +218,9 @@ def main():
                     help="graph executor: batches in flight at once, one stream each "
                          "(a step is still one forward over one batch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--split", default=None,
+                    help="comma list of levels (2,3) on the channel-split group kernel "
+                         "(default: the engine's SPLIT_L2/SPLIT_L3)")
     ap.add_argument("--layerwise", default="",
                     help="comma list of levels (1,2,3) to run layer by layer instead of fused")
     args = ap.parse_args()
@@ -239,6 +244,11 @@ def main():
     _lib.load()
     for lv in filter(None, args.layerwise.split(",")):
         setattr(engine, f"FUSED_L{int(lv)}", False)
+    if args.split is not None:
+        on = {int(x) for x in filter(None, args.split.split(","))}
+        engine.SPLIT_L2, engine.SPLIT_L3 = 2 in on, 3 in on
+    fused_names = [("group_split_kernel" if s else "group_fused_kernel") + f" (level {lv})"
+                   for lv, s in ((2, engine.SPLIT_L2), (3, engine.SPLIT_L3))]
     net = make_model(device, args.model)
     P = net.prepared(device)
     B = args.batch
@@ -306,12 +316,12 @@ def main():
         per_launch_s = f_ms / max(f_n, 1) / 1e3
         per_launch_flops = f_fl / max(f_n, 1)
         achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
-        traffic, traffic_src = pmc_traffic("group_fused_kernel")
+        traffic, traffic_src = pmc_traffic(" + ".join(fused_names))
         tot_ms = sum(r[0] for r in res.values())
         tot_fl = sum(r[2] for r in res.values())
-        roof = {"kernel": "group_fused_kernel (level-2 and level-3 keypoint detector + "
-                          "descriptor: every conv/BN/ReLU layer, attention and k-max of the "
-                          "level in one launch)",
+        roof = {"kernel": " + ".join(fused_names) + " (keypoint detector + descriptor: "
+                          "every conv/BN/ReLU layer, attention and k-max of the level in one "
+                          "launch)",
                 "timing": "HIP events on the launch stream, " + (
                     "instrumented eager pipelined pass of the same steps after the timed "
                     "graph region" if args.executor == "graph" else "inside the timed region"),

@@ -244,6 +244,19 @@ int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                   float *desc, void *stream);
 
+/* The level-2 / level-3 stages above on the channel-split kernel (group_split.hip):
+ * same arguments and outputs, table = hreg_group_split_l{2,3}_table_floats() floats
+ * (engine.split_table: the same blocks, fragments grouped 4 k-steps per lane); geom
+ * must be 16-byte aligned. */
+int hreg_group_split_l2_table_floats(void);
+int hreg_group_split_l2(const float *table, const float *geom, const float *knn_xyz,
+                        const int32_t *gidx, const float *feats, int G, float *kp,
+                        float *att_feat, float *desc, void *stream);
+int hreg_group_split_l3_table_floats(void);
+int hreg_group_split_l3(const float *table, const float *geom, const float *knn_xyz,
+                        const int32_t *gidx, const float *feats, int G, float *kp,
+                        float *att_feat, float *desc, void *stream);
+
 /* Fused FineReg head (layers.py:433-451) for C = 64 (fine_corres_1) or 128
  * (fine_corres_2): small [G*8][16] from hreg_pair_feats (ldf 16), src_desc [G][C]
  * (keypoint i's own descriptor), dst_desc [*][C] gathered by gidx [G*8],

@@ -68,6 +68,8 @@ _SIGS = {
     "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_group_split_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_group_split_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_fine_head": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_fine_head_table_floats": [_i],
     "hreg_nbr_head": [_vp, _vp, _vp, _vp, _i, _vp, _vp],
@@ -76,7 +78,8 @@ _SIGS = {
 
 EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_group_l1_table_floats",
                           "hreg_group_l2_table_floats", "hreg_group_l3_table_floats",
-                          "hreg_nbr_head_table_floats")
+                          "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
+                          "hreg_group_split_l3_table_floats")
 
 _lib = None
 
@@ -99,7 +102,8 @@ def load(require_gpu: bool = True):
         L.hreg_spatial_index_bytes.restype = ctypes.c_size_t
         L.hreg_spatial_index_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
-                     "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats"):
+                     "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
+                     "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats"):
             getattr(L, name).restype = ctypes.c_int
             getattr(L, name).argtypes = []
         _lib = L

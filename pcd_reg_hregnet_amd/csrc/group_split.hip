@@ -1,0 +1,461 @@
+// group_split.hip -- level-2 / level-3 keypoint detector + descriptor, channel-split.
+//
+// Same computation and weight order as group_fused.hip (layers.py:115-121,150-159,
+// 183-208; see that file), different decomposition.  group_fused.hip keeps a whole
+// 32-row tile's activations in one wave's accumulators, which at level 3 needs all
+// 512 VGPRs (one wave per SIMD, spills): any wait of that wave idles the SIMD's
+// matrix core.  Here a workgroup of 4 waves owns RT row tiles; the waves of a row
+// tile split every layer's output channels CW ways (wave cw computes tiles
+// co = cw*P + i), the activations of a layer go through LDS (row-major, stride
+// LDSW = widest layer + 4 floats, written and read as float4 in the MFMA
+// accumulator's channel order), and the next layer streams its B operand from LDS
+// one window ahead, like the A fragments from the L2-resident table.  Per wave:
+// P <= 2 output tiles, ~130 VGPRs; two workgroups per CU (LDS 2 x ~70 KB), so one
+// workgroup's barriers / epilogues overlap the other's MFMAs.  A-fragment windows
+// hold 32 fragments (2 x the chained kernel's), hiding a longer L2 latency.
+//
+// Per 32-row tile (4 waves, 11 workgroup barriers):
+//   stage [geom 4 | gathered feature CF] rows -> A
+//   det conv1 A->B, conv2 B->A, conv3 A->emb (registers)
+//   attention: per-wave channel max -> LDS -> row max, softmax over the group,
+//              keypoint and attentive feature (each wave its channels)
+//   emb*a -> B; mlp1 (emb*a part) B -> y1 (registers, kept)
+//   stage again -> A; desc conv1 A->B, conv2 B->A, conv3 A->x1d
+//   x2 = k-max(x1d) -> X2 (one row per group), x1d -> B; mlp1 (x2, x1d parts) -> y1
+//   y1 -> A; mlp2 A -> y2, k-max -> descriptor
+#include "mfma_chain.h"
+
+namespace {
+
+using namespace hreg_chain;
+
+// KN neighbours per group, CF gathered feature channels, conv widths C1/C3, mlp
+// widths CM1/CM2; RT row tiles x CW channel-split waves = 4 waves per workgroup.
+// Table layout: group_fused.hip Cfg offsets, fragments grouped 4 k-steps
+// innermost per lane ([co][step/4][lane][4]; the 2-step geometry block: [co][lane][2]),
+// engine.split_table.
+template <int KN_, int CF_, int C1, int C3, int CM1, int CM2, int RT_, int CW_>
+struct SCfg {
+    static constexpr int KN = KN_, CF = CF_, RT = RT_, CW = CW_;
+    static constexpr int TF = CF / 2;
+    static constexpr int T1 = C1 / 32, T3 = C3 / 32, TM1 = CM1 / 32, TM2 = CM2 / 32;
+    static constexpr int P1 = T1 / CW, P3 = T3 / CW, PM1 = TM1 / CW, PM2 = TM2 / CW;
+    static_assert(P1 * CW == T1 && P3 * CW == T3 && PM1 * CW == TM1 && PM2 * CW == TM2, "split");
+    static_assert(RT * CW == 4, "4 waves");
+    static constexpr int F_DG = 0;
+    static constexpr int F_DF = F_DG + T1 * 2 * 64;
+    static constexpr int F_D2 = F_DF + T1 * TF * 64;
+    static constexpr int F_D3 = F_D2 + T1 * T1 * 16 * 64;
+    static constexpr int F_EG = F_D3 + T3 * T1 * 16 * 64;
+    static constexpr int F_EF = F_EG + T1 * 2 * 64;
+    static constexpr int F_E2 = F_EF + T1 * TF * 64;
+    static constexpr int F_E3 = F_E2 + T1 * T1 * 16 * 64;
+    static constexpr int F_M1 = F_E3 + T3 * T1 * 16 * 64;
+    static constexpr int F_M2 = F_M1 + TM1 * 3 * T3 * 16 * 64;
+    static constexpr int F_END = F_M2 + TM2 * TM1 * 16 * 64;
+    static constexpr int E_D1 = F_END, E_D2 = E_D1 + 2 * C1, E_D3 = E_D2 + 2 * C1,
+                         E_E1 = E_D3 + 2 * C3, E_E2 = E_E1 + 2 * C1, E_E3 = E_E2 + 2 * C1,
+                         E_M1 = E_E3 + 2 * C3, E_M2 = E_M1 + 2 * CM1, TABLE = E_M2 + 2 * CM2;
+    static constexpr int W0 = C3 > 4 + CF ? C3 : 4 + CF;
+    static constexpr int LDSW = (W0 > CM1 ? W0 : CM1) + 4;  // row stride (floats)
+    static constexpr int GPT = 32 / KN;                      // groups per row tile
+    static constexpr int X2W = C3 + 4;
+};
+
+using S2 = SCfg<32, 64, 64, 128, 64, 128, 2, 2>;
+using S3 = SCfg<16, 128, 128, 256, 128, 256, 1, 4>;
+
+// tools/split_experiment.py: 1 = no workgroup barriers, 2 = B operand not read from
+// LDS (timing experiments only: results are wrong)
+#ifndef HREG_SPLIT_EXP
+#define HREG_SPLIT_EXP 0
+#endif
+__device__ __forceinline__ void tile_sync() {
+    if constexpr (HREG_SPLIT_EXP != 1) __syncthreads();
+}
+
+constexpr int SCARRY = 32;
+constexpr int SWIN = 16;  // k-steps per window (P <= 2 tiles: <= 32 fragments in flight)
+
+// acc[P] += sum_{st < NSTEP} A(co0 + i, st) x B(st): A fragments from the table
+// (grouped 4 k-steps per lane; GS = 2 for a 2-step call), B from LDS through
+// bl(st0, v) (GS consecutive k-steps).  cin: this call's first window of A
+// fragments (loaded by the previous call); cout: the first window (NWIN steps x NP
+// tiles) of the next call nf.  The first B window is read at entry (it is the
+// output of the barrier just passed); later windows one window ahead.
+template <int NSTEP, int P, int NP, int NWIN, class BL>
+__device__ __forceinline__ void pipe_lds(const gfloat *__restrict__ wf, int lane, FragSeq f, BL bl,
+                                         f32x16 (&acc)[P], const float (&cin)[SCARRY], FragSeq nf,
+                                         float (&cout)[SCARRY]) {
+    constexpr int WIN = NSTEP < SWIN ? NSTEP : SWIN;
+    constexpr int GS = WIN < 4 ? WIN : 4, NGS = NWIN < 4 ? NWIN : 4;
+    static_assert(NSTEP % WIN == 0 && WIN % GS == 0 && NWIN % NGS == 0, "window");
+    static_assert(WIN * P <= SCARRY && NWIN * NP <= SCARRY, "carry");
+    constexpr int NW = NSTEP / WIN;
+    float abuf[2][WIN][P];
+    float bbuf[2][WIN];
+#pragma unroll
+    for (int s = 0; s < WIN; ++s)
+#pragma unroll
+        for (int co = 0; co < P; ++co) abuf[0][s][co] = cin[s * P + co];
+#pragma unroll
+    for (int s0 = 0; s0 < WIN; s0 += GS) {
+        float v[GS];
+        if constexpr (HREG_SPLIT_EXP == 2) {
+#pragma unroll
+            for (int i = 0; i < GS; ++i) {
+                float x = __int_as_float(lane);
+                asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
+                v[i] = x;
+            }
+        } else {
+            bl(s0, v);
+        }
+#pragma unroll
+        for (int i = 0; i < GS; ++i) bbuf[0][s0 + i] = v[i];
+    }
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        if (w + 1 < NW) {
+#pragma unroll
+            for (int s0 = 0; s0 < WIN; s0 += GS) {
+#pragma unroll
+                for (int co = 0; co < P; ++co) {
+                    float v[GS];
+                    ldgroup<GS>(wf, f.base + co * f.stride + (w + 1) * WIN + s0, lane, v);
+#pragma unroll
+                    for (int i = 0; i < GS; ++i) abuf[(w + 1) & 1][s0 + i][co] = v[i];
+                }
+                float v[GS];
+                if constexpr (HREG_SPLIT_EXP == 2) {
+#pragma unroll
+                    for (int i = 0; i < GS; ++i) {
+                        float x = __int_as_float(lane);
+                        asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
+                        v[i] = x;
+                    }
+                } else {
+                    bl((w + 1) * WIN + s0, v);
+                }
+#pragma unroll
+                for (int i = 0; i < GS; ++i) bbuf[(w + 1) & 1][s0 + i] = v[i];
+            }
+        } else {
+#pragma unroll
+            for (int s0 = 0; s0 < NWIN; s0 += NGS)
+#pragma unroll
+                for (int co = 0; co < NP; ++co) {
+                    float v[NGS];
+                    ldgroup<NGS>(wf, nf.base + co * nf.stride + s0, lane, v);
+#pragma unroll
+                    for (int i = 0; i < NGS; ++i) cout[(s0 + i) * NP + co] = v[i];
+                }
+        }
+#pragma unroll
+        for (int s = 0; s < WIN; ++s)
+#pragma unroll
+            for (int co = 0; co < P; ++co)
+                acc[co] = __builtin_amdgcn_mfma_f32_32x32x2f32(abuf[w & 1][s][co], bbuf[w & 1][s],
+                                                               acc[co], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int NSTEP>
+constexpr int swin() { return NSTEP < SWIN ? NSTEP : SWIN; }
+
+// BN/ReLU epilogue of output tiles co0 .. co0+P-1 of a C-channel layer
+template <int P, int C>
+__device__ __forceinline__ void epi(const float *ab, int co0, int h, f32x16 (&acc)[P]) {
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int c = chan(co0 + i, q, h);
+            acc[i][q] = fmaxf(fadd_rn(fmul_rn(acc[i][q], ab[c]), ab[C + c]), 0.f);
+        }
+}
+
+// tile co of an activation (channels chan(co, q, h), row j) into a row-major LDS buffer
+template <int LDSW>
+__device__ __forceinline__ void put_tile(float *buf, int co, int j, int h, const f32x16 &v) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<float4 *>(buf + j * LDSW + co * 32 + 8 * r + 4 * h) =
+            make_float4(v[4 * r], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+}
+
+// B loader for a chained layer input: k-step st = ct*16 + q <-> channel chan(ct, q, h)
+struct ChanB {
+    const float *row;  // buf + j * LDSW
+    int h;
+    __device__ __forceinline__ void operator()(int st0, float (&v)[4]) const {
+        const int ct = st0 >> 4, r = (st0 & 15) >> 2;
+        const float4 t = *reinterpret_cast<const float4 *>(row + ct * 32 + 8 * r + 4 * h);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    }
+};
+
+// stage [geom 4 | feats[gidx[row]] CF] of the tile's 32 rows into buf (the CW waves
+// of the row tile share the float4 loads)
+template <class K>
+__device__ __forceinline__ void stage_rows(float *buf, const float *__restrict__ geom,
+                                           const int32_t *__restrict__ gidx,
+                                           const float *__restrict__ feats, int t, int cw, int lane) {
+    constexpr int F4 = 1 + K::CF / 4;
+#pragma unroll
+    for (int i = cw * 64 + lane; i < 32 * F4; i += K::CW * 64) {
+        const int r = i / F4, c4 = i - r * F4;
+        const size_t row = (size_t)t * 32 + r;
+        const float *src = c4 == 0 ? geom + row * 4 : feats + (size_t)gidx[row] * K::CF + (c4 - 1) * 4;
+        *reinterpret_cast<float4 *>(buf + r * K::LDSW + c4 * 4) = *reinterpret_cast<const float4 *>(src);
+    }
+}
+
+// conv stack [geom | feat] -> C1 -> C1 -> C3 through the A/B buffers; result tiles
+// in out (epilogue applied).  Ends with out in registers; A / B free after the
+// caller's next barrier.
+template <class K, int NP, int NWN>
+__device__ __forceinline__ void conv_stack_split(const gfloat *__restrict__ tb, const float *eb, int fg,
+                                                 int ff, int f2, int f3, int e1, int e2, int e3,
+                                                 float *A, float *B, int cw, int lane,
+                                                 f32x16 (&out)[K::P3], const float (&cin)[SCARRY],
+                                                 FragSeq next, float (&cout)[SCARRY]) {
+    constexpr int T1 = K::T1, TF = K::TF, P1 = K::P1, P3 = K::P3, LDSW = K::LDSW;
+    const int h = lane >> 5, j = lane & 31;
+    const int c1 = cw * P1, c3 = cw * P3;
+    const FragSeq sg{fg / 64 + c1 * 2, 2}, sf{ff / 64 + c1 * TF, TF};
+    const FragSeq s2{f2 / 64 + c1 * T1 * 16, T1 * 16}, s3{f3 / 64 + c3 * T1 * 16, T1 * 16};
+    const float *arow = A + j * LDSW, *brow = B + j * LDSW;
+    float ca[SCARRY], cb[SCARRY];
+    f32x16 h1[P1];
+    zero_tiles(h1);
+    pipe_lds<2, P1, P1, swin<TF>()>(
+        tb, lane, sg,
+        [&](int st0, float (&v)[2]) {
+            const float2 t = *reinterpret_cast<const float2 *>(arow + 2 * h);
+            v[0] = t.x; v[1] = t.y;
+        },
+        h1, cin, sf, ca);
+    pipe_lds<TF, P1, P1, swin<T1 * 16>()>(
+        tb, lane, sf,
+        [&](int st0, float (&v)[4]) {
+            const float4 t = *reinterpret_cast<const float4 *>(arow + 4 + h * TF + st0);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        },
+        h1, ca, s2, cb);
+    epi<P1, K::T1 * 32>(eb + e1, c1, h, h1);
+#pragma unroll
+    for (int i = 0; i < P1; ++i) put_tile<LDSW>(B, c1 + i, j, h, h1[i]);
+    tile_sync();
+    f32x16 h2[P1];
+    zero_tiles(h2);
+    pipe_lds<T1 * 16, P1, P3, swin<T1 * 16>()>(tb, lane, s2, ChanB{brow, h}, h2, cb, s3, ca);
+    epi<P1, K::T1 * 32>(eb + e2, c1, h, h2);
+#pragma unroll
+    for (int i = 0; i < P1; ++i) put_tile<LDSW>(A, c1 + i, j, h, h2[i]);
+    tile_sync();
+    zero_tiles(out);
+    pipe_lds<T1 * 16, P3, NP, NWN>(tb, lane, s3, ChanB{arow, h}, out, ca, next, cout);
+    epi<P3, K::T3 * 32>(eb + e3, c3, h, out);
+}
+
+template <class K>
+__global__ __launch_bounds__(256, 2) void group_split_kernel(
+    const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
+    const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
+    float *__restrict__ att_feat, float *__restrict__ desc) {
+    constexpr int C3 = K::T3 * 32, CM2 = K::TM2 * 32, LDSW = K::LDSW, X2W = K::X2W;
+    constexpr int T3 = K::T3, TM1 = K::TM1, P3 = K::P3, PM1 = K::PM1, PM2 = K::PM2;
+    constexpr int NE = K::TABLE - K::F_END, KN = K::KN, GPT = K::GPT, RT = K::RT, CW = K::CW;
+    __shared__ float ep[NE];
+    __shared__ __attribute__((aligned(16))) float sA[RT][32 * LDSW];
+    __shared__ __attribute__((aligned(16))) float sB[RT][32 * LDSW];
+    __shared__ __attribute__((aligned(16))) float sX2[RT][GPT * X2W];
+    __shared__ int sMax[RT][CW][32];
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
+    const float *eb = ep - K::F_END;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int rt = w / CW, cw = w % CW;
+    const int h = lane >> 5, j = lane & 31;
+    const int NT = G / GPT;
+    float *A = sA[rt], *B = sB[rt], *X2 = sX2[rt];
+    const bool writer = KN == 32 ? j == 31 : (j & 15) == 15;
+    auto gsum_w = [&](float v) { return KN == 32 ? half_sum_hi(v) : row_sum16(v); };
+    auto gsum_b = [&](float v) { return KN == 32 ? half_bcast(half_sum_hi(v), h) : row_sum16(v); };
+    auto gmax_w = [&](float v) { return KN == 32 ? half_max_hi_nonneg(v) : row_max16_nonneg(v); };
+    auto gmax_b = [&](float v) {
+        return KN == 32 ? half_bcast(half_max_hi_nonneg(v), h) : row_max16_nonneg(v);
+    };
+    const int c3 = cw * P3, m1 = cw * PM1, m2 = cw * PM2;
+    constexpr int MS = 3 * T3 * 16;  // mlp1 fragment stride per output tile
+    const FragSeq det_g{K::F_DG / 64 + cw * K::P1 * 2, 2}, desc_g{K::F_EG / 64 + cw * K::P1 * 2, 2};
+    const FragSeq m1x2{K::F_M1 / 64 + m1 * MS, MS};
+    const FragSeq m1x1{K::F_M1 / 64 + m1 * MS + T3 * 16, MS};
+    const FragSeq m1em{K::F_M1 / 64 + m1 * MS + 2 * T3 * 16, MS};
+    const FragSeq fm2{K::F_M2 / 64 + m2 * TM1 * 16, TM1 * 16};
+
+    float carry[SCARRY];
+    {
+        const gfloat *tb = reinterpret_cast<const gfloat *>(reinterpret_cast<uint64_t>(table));
+#pragma unroll
+        for (int i = 0; i < K::P1; ++i) {
+            float v[2];
+            ldgroup<2>(tb, det_g.base + i * 2, lane, v);
+            carry[i] = v[0];
+            carry[K::P1 + i] = v[1];
+        }
+    }
+    for (int base = blockIdx.x * RT; base < NT; base += gridDim.x * RT) {
+        // every wave of the workgroup runs the same trip count (barriers): a row tile
+        // past the end recomputes the last tile (identical values, identical stores)
+        const int t = min(base + rt, NT - 1);
+        const int g = t * GPT + (KN == 32 ? 0 : j >> 4);
+        const size_t row = (size_t)t * 32 + j;
+        uint64_t tba = reinterpret_cast<uint64_t>(table);
+        asm volatile("" : "+s"(tba));
+        const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
+        float ca[SCARRY], cb[SCARRY];
+
+        tile_sync();  // previous tile's readers of A are done (and ep is loaded)
+        stage_rows<K>(A, geom, gidx, feats, t, cw, lane);
+        tile_sync();
+
+        // ---- detector -> emb (this wave's P3 tiles)
+        f32x16 emb[P3];
+        conv_stack_split<K, PM1, swin<T3 * 16>()>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1,
+                                                  K::E_D2, K::E_D3, A, B, cw, lane, emb, carry, m1em, ca);
+
+        // ---- attention: row max over all C3 channels (per-wave partial maxima through
+        // LDS; emb >= 0 after ReLU: integer max on the bit patterns), softmax over the group
+        int mi = __float_as_int(emb[0][0]);
+#pragma unroll
+        for (int i = 0; i < P3; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(emb[i][q]));
+        mi = max(mi, __shfl_xor(mi, 32));
+        if (h == 0) sMax[rt][cw][j] = mi;
+        tile_sync();
+        int xm = sMax[rt][0][j];
+#pragma unroll
+        for (int c = 1; c < CW; ++c) xm = max(xm, sMax[rt][c][j]);
+        const float x1 = __int_as_float(xm);
+        const float mx = gmax_b(x1);
+        const float e = expf(fsub_rn(x1, mx));
+        const float a = e / gsum_b(e);
+        if (cw == 0) {
+            const float *p = knn_xyz + row * 3;
+            const float kx = gsum_w(fmul_rn(a, p[0]));
+            const float ky = gsum_w(fmul_rn(a, p[1]));
+            const float kz = gsum_w(fmul_rn(a, p[2]));
+            if (writer && h == 0) {
+                kp[(size_t)g * 3 + 0] = kx;
+                kp[(size_t)g * 3 + 1] = ky;
+                kp[(size_t)g * 3 + 2] = kz;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < P3; ++i) {
+            f32x16 v, ea;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                ea[q] = fmul_rn(emb[i][q], a);
+                v[q] = gsum_w(ea[q]);
+            }
+            store_tile(att_feat + (size_t)g * C3, c3 + i, v, writer, h);
+            put_tile<LDSW>(B, c3 + i, j, h, ea);
+        }
+        tile_sync();
+
+        // ---- mlp1, emb*a part (y1 stays in registers through the descriptor stack)
+        f32x16 y1[PM1];
+        zero_tiles(y1);
+        pipe_lds<T3 * 16, PM1, K::P1, 2>(tb, lane, m1em, ChanB{B + j * LDSW, h}, y1, ca, desc_g,
+                                         cb);
+        stage_rows<K>(A, geom, gidx, feats, t, cw, lane);
+        tile_sync();
+
+        // ---- descriptor -> x1d
+        f32x16 x1d[P3];
+        conv_stack_split<K, PM1, swin<T3 * 16>()>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1,
+                                                  K::E_E2, K::E_E3, A, B, cw, lane, x1d, cb, m1x2, ca);
+        // x2 = k-max of x1d (one row per group) -> X2; x1d -> B
+#pragma unroll
+        for (int i = 0; i < P3; ++i) {
+            f32x16 v;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = gmax_w(x1d[i][q]);
+            if (writer) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    *reinterpret_cast<float4 *>(X2 + (KN == 32 ? 0 : j >> 4) * X2W + (c3 + i) * 32 +
+                                                8 * r + 4 * h) =
+                        make_float4(v[4 * r], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+            }
+            put_tile<LDSW>(B, c3 + i, j, h, x1d[i]);
+        }
+        tile_sync();
+
+        // ---- mlp1, x2 part (the group's row of X2 for every row) and x1d part
+        pipe_lds<T3 * 16, PM1, PM1, swin<T3 * 16>()>(
+            tb, lane, m1x2, ChanB{X2 + (KN == 32 ? 0 : j >> 4) * X2W, h}, y1, ca,
+            m1x1, cb);
+        pipe_lds<T3 * 16, PM1, PM2, swin<TM1 * 16>()>(tb, lane, m1x1, ChanB{B + j * LDSW, h}, y1,
+                                                      cb, fm2, ca);
+        epi<PM1, TM1 * 32>(eb + K::E_M1, m1, h, y1);
+#pragma unroll
+        for (int i = 0; i < PM1; ++i) put_tile<LDSW>(A, m1 + i, j, h, y1[i]);
+        tile_sync();
+
+        // ---- mlp2 + k-max -> descriptor; prefetches the next tile's first window
+        f32x16 y2[PM2];
+        zero_tiles(y2);
+        pipe_lds<TM1 * 16, PM2, K::P1, 2>(tb, lane, fm2, ChanB{A + j * LDSW, h}, y2, ca, det_g,
+                                          carry);
+        epi<PM2, CM2>(eb + K::E_M2, m2, h, y2);
+#pragma unroll
+        for (int i = 0; i < PM2; ++i) {
+            f32x16 v;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = gmax_w(y2[i][q]);
+            store_tile(desc + (size_t)g * CM2, m2 + i, v, writer, h);
+        }
+    }
+}
+
+template <class K>
+int launch_split(const float *table, const float *geom, const float *knn_xyz, const int32_t *gidx,
+                 const float *feats, int G, float *kp, float *att_feat, float *desc, void *stream) {
+    if (!table || !geom || !knn_xyz || !gidx || !feats || !kp || !att_feat || !desc || G < 0)
+        return HREG_ERR_INVALID;
+    if ((reinterpret_cast<uintptr_t>(feats) & 15) || (reinterpret_cast<uintptr_t>(geom) & 15) ||
+        (reinterpret_cast<uintptr_t>(att_feat) & 15) || (reinterpret_cast<uintptr_t>(desc) & 15))
+        return HREG_ERR_INVALID;
+    if (G % K::GPT) return HREG_ERR_INVALID;  // whole 32-row tiles
+    if (!G) return HREG_OK;
+    const int NT = G / K::GPT;
+    int grid = (NT + K::RT - 1) / K::RT;
+    const int cap = 256 * 2 * 2;  // two resident workgroups per CU, two rounds
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(group_split_kernel<K>, dim3(grid), dim3(256), 0, as_stream(stream), table, geom,
+                       knn_xyz, gidx, feats, G, kp, att_feat, desc);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+}  // namespace
+
+extern "C" int hreg_group_split_l2_table_floats(void) { return S2::TABLE; }
+extern "C" int hreg_group_split_l3_table_floats(void) { return S3::TABLE; }
+
+extern "C" int hreg_group_split_l2(const float *table, const float *geom, const float *knn_xyz,
+                                   const int32_t *gidx, const float *feats, int G, float *kp,
+                                   float *att_feat, float *desc, void *stream) {
+    return launch_split<S2>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, stream);
+}
+
+extern "C" int hreg_group_split_l3(const float *table, const float *geom, const float *knn_xyz,
+                                   const int32_t *gidx, const float *feats, int G, float *kp,
+                                   float *att_feat, float *desc, void *stream) {
+    return launch_split<S3>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, stream);
+}

@@ -56,8 +56,13 @@ constexpr int first_win() { return NSTEP < win_for<COUT_T>() ? NSTEP : win_for<C
 template <int GS>
 __device__ __forceinline__ void ldgroup(const gfloat *__restrict__ wf, int f0, int lane, float (&v)[GS]) {
     if constexpr (HREG_L2_EXP == 2) {
+        // opaque register values: no load, nothing the compiler can hoist or fold
 #pragma unroll
-        for (int i = 0; i < GS; ++i) v[i] = (float)(lane + f0 + i);
+        for (int i = 0; i < GS; ++i) {
+            float x = __int_as_float(lane);
+            asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
+            v[i] = x;
+        }
     } else if constexpr (GS == 4) {
         typedef float v4f __attribute__((ext_vector_type(4)));
         typedef __attribute__((address_space(1))) const v4f gv4f;

@@ -37,6 +37,10 @@ K_HEAD = 8  # CoarseReg/FineReg k (models.py:71-73)
 FUSED_L1 = True  # level 1 through the fused group_l1 kernel (False: layer-by-layer GEMMs)
 FUSED_L2 = True  # level 2 through the fused group_fused kernel (k = 32)
 FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
+# levels 2 / 3 on the channel-split kernel (group_split.hip) instead of the
+# accumulator-chained one (group_fused.hip); measured per level (tools/group_bench.py)
+SPLIT_L2 = False
+SPLIT_L3 = True
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
 FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
 
@@ -136,11 +140,14 @@ class PreparedWeights:
         self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
         self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
+        self.l2s_table = split_table(self.det[1], self.desc[1], self.desc_mlp[1])
+        self.l3s_table = split_table(self.det[2], self.desc[2], self.desc_mlp[2])
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
                            for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
         self.nbr_table = nbr_head_table(self.coarse_convs2, 256)
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
-                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "fine_table",
+                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2s_table",
+                     "l3s_table", "fine_table",
                      "nbr_table", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
@@ -252,6 +259,20 @@ def l2_table(det, desc, mlp) -> torch.Tensor:
                   _grouped(frag_layer(stack[2].W), T3, T1 * 16)]
     parts += [_grouped(frag_layer(mlp[0].W), TM1, 3 * T3 * 16),
               _grouped(frag_layer(mlp[1].W), TM2, TM1 * 16)]
+    for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def split_table(det, desc, mlp) -> torch.Tensor:
+    """Weight/epilogue table of group_split.hip: the l2_table blocks and epilogues, with
+    every block grouped 4 k-steps innermost per lane (the 2-step geometry block: 2)."""
+    parts = []
+    for stack in (det, desc):
+        g, f = frag_input(stack[0].W)
+        parts += [_group4(g, 2), _group4(f, 4), _group4(frag_layer(stack[1].W), 4),
+                  _group4(frag_layer(stack[2].W), 4)]
+    parts += [_group4(frag_layer(mlp[0].W), 4), _group4(frag_layer(mlp[1].W), 4)]
     for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
@@ -530,7 +551,12 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         kp = _empty(G, 3, device=dev)
         att_feat = _empty(G, LEVELS[lvl][3][-1], device=dev)
         desc = _empty(G, LEVELS[lvl][5], device=dev)
-        name, table = ("hreg_group_l2", P.l2_table) if lvl == 1 else ("hreg_group_l3", P.l3_table)
+        if (SPLIT_L2, SPLIT_L3)[lvl - 1]:
+            name, table = (("hreg_group_split_l2", P.l2s_table) if lvl == 1 else
+                           ("hreg_group_split_l3", P.l3s_table))
+        else:
+            name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
+                           ("hreg_group_l3", P.l3_table))
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, _stream())
         m1, m2, w3, b3 = P.det_head[lvl]
         s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)

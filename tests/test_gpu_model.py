@@ -180,11 +180,11 @@ def test_graph_lanes_match_eager(net):
                 assert torch.equal(out["src_feats"]["desc_3"], ref["src_feats"]["desc_3"])
 
 
-@pytest.mark.parametrize("lvl", [0, 1, 2])
-def test_fused_level_matches_layerwise(net, lvl):
-    """The fused level kernels (group_l1 / group_l2: activations in MFMA accumulators)
-    against the layer-by-layer GEMM path on the same grouping; fp32 summation order
-    differs, so within 1e-4."""
+@pytest.mark.parametrize("lvl,split", [(0, False), (1, False), (2, False), (1, True), (2, True)])
+def test_fused_level_matches_layerwise(net, lvl, split):
+    """The fused level kernels (group_l1 / group_fused: activations in MFMA accumulators;
+    group_split: channel-split through LDS) against the layer-by-layer GEMM path on the
+    same grouping; fp32 summation order differs, so within 1e-4."""
     from pcd_reg_hregnet_amd import engine, synthetic
     P = net.prepared(torch.device("cuda"))
     s, _, _, _ = synthetic.lidar_batch(2, 4096, seed0=60)
@@ -198,6 +198,9 @@ def test_fused_level_matches_layerwise(net, lvl):
         grouped = engine.grouping(xyz, lvl, w)
         flag = ("FUSED_L1", "FUSED_L2", "FUSED_L3")[lvl]
         outs = []
+        sflag = ("SPLIT_L2", "SPLIT_L3")[max(lvl, 1) - 1]
+        old_split = getattr(engine, sflag)
+        setattr(engine, sflag, split)
         for fused in (True, False):
             old = getattr(engine, flag)
             setattr(engine, flag, fused)
@@ -205,6 +208,7 @@ def test_fused_level_matches_layerwise(net, lvl):
                 outs.append(engine.keypoint_level(P, lvl, xyz, feats, w, grouped=grouped))
             finally:
                 setattr(engine, flag, old)
+                setattr(engine, sflag, old_split)
     torch.cuda.synchronize()
     (kp_f, sig_f, att_f, desc_f, w_f, _), (kp_r, sig_r, att_r, desc_r, w_r, _) = outs
     for a, b in ((kp_f, kp_r), (sig_f, sig_r), (att_f, att_r), (desc_f, desc_r)):

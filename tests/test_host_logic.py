@@ -206,6 +206,18 @@ def test_l3_table_size_matches_kernel(P):
     assert prep.l3_table.numel() == L.hreg_group_l3_table_floats()
 
 
+def test_split_tables_match_kernel(P):
+    """group_split.hip tables: same size as the chained kernel's, same fragments
+    regrouped 4 k-steps per lane (2 for the geometry block)."""
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.l2s_table.numel() == L.hreg_group_split_l2_table_floats()
+    assert prep.l3s_table.numel() == L.hreg_group_split_l3_table_floats()
+    for a, b in ((prep.l2_table, prep.l2s_table), (prep.l3_table, prep.l3s_table)):
+        assert torch.equal(torch.sort(a).values, torch.sort(b).values)
+
+
 def test_fine_head_table_sizes_match_kernel(P):
     _, prep = P
     from pcd_reg_hregnet_amd import _lib

@@ -3,6 +3,7 @@
 
   kernel stats:  python tools/rocpd_summary.py stats <run_results.db | kernel_stats.csv> <steps> [out.md]
   HBM traffic:   python tools/rocpd_summary.py traffic <fetch .db|csv> <write .db|csv> [out.md] [out.json]
+  MFMA use:      python tools/rocpd_summary.py mfma <counter_collection.csv> [out.md] [out.json]
 
 Traffic follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE come
 from separate --pmc passes (TCC slots 3 + 2 > 4), both in KiB; on gfx950
@@ -16,7 +17,8 @@ import sqlite3
 import sys
 from collections import defaultdict
 
-FAMILIES = ("gemm_nt_kernel", "group_l1_kernel", "group_fused_kernel", "fine_head_kernel",
+FAMILIES = ("gemm_nt_kernel", "group_l1_kernel", "group_fused_kernel", "group_split_kernel",
+            "fine_head_kernel",
             "nbr_head_kernel", "fps_reg_kernel", "knn_group", "spatial_index_kernel",
             "attend_kernel", "knnd_kernel")
 
@@ -102,8 +104,59 @@ def traffic(fetch_path, write_path, out=None, out_json=None):
                   open(out_json, "w"), indent=1)
 
 
+SIMD_NUM = 256 * 4
+XCD_NUM = 8  # the CSV's GRBM_GUI_ACTIVE is summed over the 8 XCDs; the derived formula
+#              takes reduce(GRBM_GUI_ACTIVE, max), i.e. one XCD's count
+PEAK_F32_TFLOPS = 157.3
+
+
+def mfma(path, out=None, out_json=None):
+    """Per-kernel MFMA counters of one --pmc pass (SQ_VALU_MFMA_BUSY_CYCLES,
+    SQ_INSTS_VALU_MFMA_MOPS_F32, GRBM_GUI_ACTIVE): MfmaUtil = busy / (GUI_ACTIVE of one
+    XCD x SIMDs) (rocprofv3's derived formula), FLOPs = MOPS_F32 x 512, TF/s over the
+    dispatch's own duration (counter passes serialise dispatches)."""
+    per = defaultdict(dict)  # (kernel, dispatch) -> counter -> value, plus duration
+    for r in csv.DictReader(open(path)):
+        key = (short(r["Kernel_Name"]), r["Dispatch_Id"])
+        per[key][r["Counter_Name"]] = float(r["Counter_Value"])
+        per[key]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    agg = defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0.0])
+    for (name, _), c in per.items():
+        if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
+            continue
+        a = agg[name]
+        a[0] += 1
+        a[1] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
+        a[2] += c["GRBM_GUI_ACTIVE"] / XCD_NUM * SIMD_NUM
+        a[3] += c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) * 512
+        a[4] += c["_ns"]
+    lines = ["| kernel | dispatches | MfmaUtil % | MFMA GFLOP/dispatch | TF/s (own duration) | "
+             "% of fp32 MFMA peak |", "|---|---|---|---|---|---|"]
+    res = {}
+    for name, (n, busy, active, flops, ns) in sorted(agg.items(), key=lambda kv: -kv[1][3]):
+        if flops <= 0:
+            continue
+        util = 100.0 * busy / active if active else 0.0
+        tf = flops / ns / 1e3 if ns else 0.0
+        res[name] = {"mfma_util_pct": round(util, 1), "gflop_per_dispatch": round(flops / n / 1e9, 3),
+                     "tflops": round(tf, 1)}
+        lines.append(f"| `{name[:80]}` | {n} | {util:.1f} | {flops / n / 1e9:.3f} | {tf:.1f} | "
+                     f"{100 * tf / PEAK_F32_TFLOPS:.1f} |")
+    text = "\n".join(lines)
+    print(text)
+    if out:
+        open(out, "w").write(text + "\n")
+    if out_json:
+        json.dump({"kernels": res, "source": path,
+                   "formula": "MfmaUtil = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs); "
+                              "FLOPs = SQ_INSTS_VALU_MFMA_MOPS_F32 * 512"}, open(out_json, "w"), indent=1)
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "stats":
+    if sys.argv[1] == "mfma":
+        mfma(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None,
+             sys.argv[4] if len(sys.argv) > 4 else None)
+    elif sys.argv[1] == "stats":
         stats(sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else None)
     else:
         traffic(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None,
