@@ -37,6 +37,8 @@
  *   hreg_weighted_svd                     <- WeightedSVDHead.forward (layers.py:469-504) + T = T_ @ T_prev
  *                                            composition (models/HRegNet/models.py:100-127)
  *   hreg_transform_points                 <- R @ xyz^T + t (models/HRegNet/models.py:91-92,113-114)
+ *   hreg_bn_* / hreg_gemm_tn / hreg_adam_step <- train-mode BatchNorm, conv weight gradients and
+ *                                            optim.Adam of the training step (train/train_reg_v0.py:241-296)
  *   hreg_transformation_loss              <- transformation_loss + calc_rot_rre_err + calc_tran_rte_err
  *                                            (losses/losses.py:97-164; callers train/train_reg_v1.py:101,252)
  */
@@ -201,6 +203,39 @@ int hreg_transform_points(const float *xyz, const float *R, const float *t, int 
 int hreg_transformation_loss(const float *pred_R, const float *pred_t, const float *gt_R,
                              const float *gt_t, int nb, float alpha, float *scalars, float *R_err,
                              float *T_err, float *geodesic, float *eucl, void *stream);
+
+/* ---------------- training-step building blocks (csrc/train.hip) ----------------
+ * Train-mode BatchNorm after a 1x1 conv (layers.py:115-130 etc. in .train(); the
+ * reference's train loop train/train_reg_v0.py:241-296), weight gradients and Adam
+ * (train_reg_v0.py:246).  Row-major [R][C] tensors; every reduction over rows is
+ * deterministic (split partials in ws, summed in a fixed order). */
+size_t hreg_col_reduce_ws_bytes(int R, int C);
+/* per channel of y [R][C]: mean, invstd = 1/sqrt(var_biased + eps), var_unbiased (may be NULL) */
+int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, float *mean, float *invstd,
+                  float *var_unbiased, void *stream);
+/* out = act(gamma * (y - mean) * invstd + beta), act = ReLU if relu (out may alias y) */
+int hreg_bn_apply(const float *y, int R, int C, const float *mean, const float *invstd,
+                  const float *gamma, const float *beta, int relu, float *out, void *stream);
+/* backward of hreg_bn_apply given dout (and out for the ReLU mask): dgamma, dbeta [C],
+ * dy [R][C] (the batch-statistics BN input gradient) */
+int hreg_bn_backward(const float *dout, const float *out, const float *y, int R, int C,
+                     const float *mean, const float *invstd, const float *gamma, int relu,
+                     void *ws, float *dy, float *dgamma, float *dbeta, void *stream);
+/* running = (1 - momentum) * running + momentum * batch (nn.BatchNorm's momentum 0.1) */
+int hreg_bn_running_update(const float *mean, const float *var_unbiased, int C, float momentum,
+                           float *running_mean, float *running_var, void *stream);
+/* out[c] = sum_r x[r][c] (conv bias gradients) */
+int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, void *stream);
+/* out[n][k] = beta * out[n][k] + sum_r A[r][n] * B[r][k] (dW = dY^T X), fp32 MFMA,
+ * ws = hreg_gemm_tn_ws_bytes(R, N, K) bytes */
+size_t hreg_gemm_tn_ws_bytes(int R, int N, int K);
+int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N, int K, float beta,
+                 void *ws, float *out, void *stream);
+/* out [C][R] = in [R][C]^T */
+int hreg_transpose(const float *in, int R, int C, float *out, void *stream);
+/* torch.optim.Adam step t (>= 1) over n floats, weight decay 0, amsgrad off */
+int hreg_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, size_t n,
+                   float lr, float beta1, float beta2, float eps, int step, void *stream);
 
 /* Spatial index for exact culled kNN grouping (n <= 16384 points per cloud):
  * hreg_spatial_index sorts each cloud of p [nb][n][3] by Morton code and records

@@ -74,9 +74,19 @@ _SIGS = {
     "hreg_fine_head_table_floats": [_i],
     "hreg_nbr_head": [_vp, _vp, _vp, _vp, _i, _vp, _vp],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
+    "hreg_bn_apply": [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp],
+    "hreg_bn_backward": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_bn_running_update": [_vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp],
+    "hreg_col_sum": [_vp, _i, _i, _vp, _vp, _vp],
+    "hreg_gemm_tn": [_vp, _i, _vp, _i, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp],
+    "hreg_transpose": [_vp, _i, _i, _vp, _vp],
+    "hreg_adam_step": [_vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_float, ctypes.c_float,
+                       ctypes.c_float, ctypes.c_float, _i, _vp],
 }
 
-EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_group_l1_table_floats",
+EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_reduce_ws_bytes",
+                          "hreg_gemm_tn_ws_bytes", "hreg_group_l1_table_floats",
                           "hreg_group_l2_table_floats", "hreg_group_l3_table_floats",
                           "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
                           "hreg_group_split_l3_table_floats")
@@ -101,6 +111,10 @@ def load(require_gpu: bool = True):
         L.hreg_version.argtypes = []
         L.hreg_spatial_index_bytes.restype = ctypes.c_size_t
         L.hreg_spatial_index_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.hreg_col_reduce_ws_bytes.restype = ctypes.c_size_t
+        L.hreg_col_reduce_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.hreg_gemm_tn_ws_bytes.restype = ctypes.c_size_t
+        L.hreg_gemm_tn_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
                      "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
                      "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats"):

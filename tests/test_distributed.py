@@ -59,3 +59,44 @@ def test_single_process_path_has_no_collective():
     s0 = bench.shard_batch(0, 1, 1024)[0]
     s1 = bench.shard_batch(1, 1, 1024)[0]
     assert not np.array_equal(s0, s1)
+
+
+def _bucket_worker(rank, world, port, q):
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pcd_reg_hregnet_amd.train import GradBucket
+    torch.manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(7)),
+              torch.nn.Parameter(torch.randn(2, 2), requires_grad=False)]
+    b = GradBucket(params)
+    b.attach()
+    # rank-dependent "backward": one grad written in place, one allocated separately
+    params[0].grad.add_(float(rank + 1))
+    params[1].grad = torch.full((7,), 10.0 * (rank + 1))
+    b.collect()
+    b.all_reduce_mean()
+    q.put((rank, params[0].grad.clone(), params[1].grad.clone(), b.flat.numel(),
+           params[0].grad.data_ptr() == b.flat.data_ptr()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_grad_bucket_all_reduce():
+    """The training step's gradient bucket (config 4): all trainable
+    gradients in one flat buffer, one all_reduce, averaged; .grad are views into it."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, g0, g1, n, view in res:
+        assert n == 22 and view  # 5x3 + 7 trainable floats
+        assert torch.equal(g0, torch.full((5, 3), 1.5))   # mean of 1 and 2
+        assert torch.equal(g1, torch.full((7,), 15.0))    # mean of 10 and 20
