@@ -151,7 +151,9 @@ def pmc_traffic(kernel: str):
     (profiles/r1_traffic.json, made by tools/rocpd_summary.py traffic)."""
     path = os.path.join(REPO, "profiles", "r1_traffic.json")
     try:
-        return json.load(open(path))["bytes_per_launch"][kernel], os.path.relpath(path, REPO)
+        per = json.load(open(path))["bytes_per_launch"]
+        names = kernel.split(" + ")  # one launch of each per step: mean over the family
+        return sum(per[n] for n in names) / len(names), os.path.relpath(path, REPO)
     except Exception:
         return None, None
 
