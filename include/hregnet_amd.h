@@ -39,6 +39,8 @@
  *   hreg_transform_points                 <- R @ xyz^T + t (models/HRegNet/models.py:91-92,113-114)
  *   hreg_bn_* / hreg_gemm_tn / hreg_adam_step <- train-mode BatchNorm, conv weight gradients and
  *                                            optim.Adam of the training step (train/train_reg_v0.py:241-296)
+ *   hreg_copy_rows ... hreg_transformation_loss_bwd <- forward/backward of the training graph
+ *                                            (train_reg_v0.py:241-296 over layers.py / models.py)
  *   hreg_transformation_loss              <- transformation_loss + calc_rot_rre_err + calc_tran_rte_err
  *                                            (losses/losses.py:97-164; callers train/train_reg_v1.py:101,252)
  */
@@ -236,6 +238,96 @@ int hreg_transpose(const float *in, int R, int C, float *out, void *stream);
 /* torch.optim.Adam step t (>= 1) over n floats, weight decay 0, amsgrad off */
 int hreg_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, size_t n,
                    float lr, float beta1, float beta2, float eps, int step, void *stream);
+
+/* ---------------- training graph ops (csrc/train_ops.hip) ----------------
+ * Forward/backward of every non-GEMM op of the HRegNet training step
+ * (train/train_reg_v0.py:241-296 through models/HRegNet/layers.py and models.py in
+ * .train()), wired into autograd by pcd_reg_hregnet_amd/train_graph.py.  Rows are
+ * point-major [rows][ld]; a group of k neighbours is k consecutive rows.  Backward
+ * sums run in a fixed order (no float atomics): same bits every run. */
+/* dst[r][c] (+)= src[r / row_div][c]  (torch.cat / repeat over k; accumulate != 0 adds) */
+int hreg_copy_rows(const float *src, int lds, int row_div, int R, int C, float *dst, int ldd,
+                   int accumulate, void *stream);
+/* out[g][c] (+)= sum_{j<k} x[g*k+j][c]  (backward of a repeat over k; attentive sums) */
+int hreg_group_sum(const float *x, int ldx, int G, int k, int C, float *out, int ldo,
+                   int accumulate, void *stream);
+/* out[m] = x[idx[m]]  (knn_gather layers.py:25,279,288,317,323,434,437; gather_operation
+ * models/utils.py:60-78 with global row indices) */
+int hreg_gather_rows(const float *x, int ldx, const int32_t *idx, int M, int C, float *out,
+                     int ldo, void *stream);
+/* out[b*m + j] = idx[b*m + j] + b*n (per-cloud indices -> global rows of the [nb*n] stack) */
+int hreg_index_offset(const int32_t *idx, int nb, int m, int n, int32_t *out, void *stream);
+/* inverse of an index (the scatter of a gather's backward): ws of hreg_csr_ws_bytes(M, n)
+ * bytes gets, per source row s < n, the ascending list of m with idx[m] == s */
+size_t hreg_csr_ws_bytes(int M, int n);
+int hreg_csr_build(const int32_t *idx, int M, int n, void *ws, void *stream);
+/* dx[s] (+)= sum_{m: idx[m] = s} dy[m] in ascending m (replaces the atomicAdd of
+ * gather_points_grad_kernel, furthest_point_sampling_gpu.cu:41-73) */
+int hreg_scatter_rows(const float *dy, int ldy, const void *ws, int M, int n, int C, float *dx,
+                      int ldx, int accumulate, void *stream);
+/* out[r] = [knn_xyz[r] - q[r/k], |knn_xyz[r] - q[r/k]|]  (layers.py:21-23, 284-285) */
+int hreg_geom_rows(const float *q, const float *knn_xyz, int G, int k, float *out, int ldo,
+                   void *stream);
+/* backward: dq [G][3] = -sum_k drela, dknn [G*k][3] = drela (+ dknn_extra); either may be NULL */
+int hreg_geom_rows_bwd(const float *geom, int ldg, const float *dgeom, int lddg,
+                       const float *dknn_extra, int G, int k, float *dq, float *dknn,
+                       void *stream);
+/* a = softmax_k(max_c logits) (amax = argmax channel), kp = sum_k a knn_xyz,
+ * vmap = vals * a, vsum = sum_k vmap  (layers.py:151-159, 340-343, 384-388, 447-450);
+ * k <= 64, every output optional */
+int hreg_attention_fwd(const float *logits, int ldl, int C, const float *vals, int ldv, int Cv,
+                       const float *knn_xyz, int G, int k, float *a, int32_t *amax, float *kp,
+                       float *vmap, int ldm, float *vsum, int lds, void *stream);
+/* backward of hreg_attention_fwd: dlogits (written, every element), dvals, dknn;
+ * same != 0: vals is logits, dlogits then holds both gradients */
+int hreg_attention_bwd(const float *logits, int ldl, int C, const float *vals, int ldv, int Cv,
+                       const float *knn_xyz, int G, int k, const float *a, const int32_t *amax,
+                       const float *dkp, const float *dvmap, int lddm, const float *dvsum,
+                       int ldds, int same, float *dlogits, int lddl, float *dvals, int lddv,
+                       float *dknn, void *stream);
+/* out[g][c] = max_j x[g*k+j][c], arg = first maximising j  (layers.py:202, 208) */
+int hreg_group_max_arg(const float *x, int ldx, int G, int k, int C, float *out, int ldo,
+                       int32_t *arg, void *stream);
+int hreg_group_max_bwd(const float *dout, int ldd, const int32_t *arg, int G, int k, int C,
+                       float *dx, int ldx, int accumulate, void *stream);
+/* backward of hreg_head_out's activation: dz [G] = dy * act'(x.w3 + b3), dx = dz w3^T */
+int hreg_head_out_bwd(const float *x, int ldx, int C, const float *w3, const float *b3,
+                      const float *dy, int mode, int G, float *dz, float *dx, int lddx,
+                      void *stream);
+/* row maxima (over N2) / column maxima (over N1) of S [nb][N1][N2] with first argmax */
+int hreg_sim_stats(const float *S, int nb, int N1, int N2, float *rmax, int32_t *rarg,
+                   float *cmax, int32_t *carg, void *stream);
+/* out[r] = [S[i][n] / (rmax_i + 1e-6), S[i][n] / (cmax_n + 1e-6)], n = kidx[r], r = (b,i,j)
+ * (src_dst_cos, dst_src_cos: layers.py:290-313, 345-362) */
+int hreg_sim_feats(const float *S, int nb, int N1, int N2, const int32_t *kidx, int k,
+                   const float *rmax, const float *cmax, float *out, int ldo, void *stream);
+/* backward through the gathers, the maxima and calc_cosine_similarity (layers.py:29-41)
+ * to the descriptors a [nb][N1][C], b [nb][N2][C]; ws = hreg_sim_feats_bwd_ws_bytes */
+size_t hreg_sim_feats_bwd_ws_bytes(int nb, int N1, int N2);
+int hreg_sim_feats_bwd(const float *S, const float *a, const float *b, const float *na,
+                       const float *nb_, int nb, int N1, int N2, int C, const int32_t *kidx,
+                       int k, const float *rmax, const int32_t *rarg, const float *cmax,
+                       const int32_t *carg, const float *dout, int ldd, void *ws, float *da,
+                       float *db, void *stream);
+/* WeightedSVDHead backward (layers.py:469-504; torch.svd + torch.det backward), fp64:
+ * dR [nb][3][3], dt [nb][3] -> dsrc, dcorres [nb][n][3], dw [nb][n] */
+int hreg_weighted_svd_bwd(const float *src, const float *corres, const float *w, int nb, int n,
+                          const float *dR, const float *dt, float *dsrc, float *dcorres,
+                          float *dw, void *stream);
+/* backward of hreg_transform_points: dxyz (may be NULL), dR, dt (sums over the points) */
+int hreg_transform_points_bwd(const float *xyz, const float *R, int nb, int n, const float *dy,
+                              float *dxyz, float *dR, float *dt, void *stream);
+/* (Ro, to) = (Ra Rb, Ra tb + ta): T = T_a @ T_b (models.py:100-110, 120-127) and backward */
+int hreg_compose_se3(int nb, const float *Ra, const float *ta, const float *Rb, const float *tb,
+                     float *Ro, float *to, void *stream);
+int hreg_compose_se3_bwd(int nb, const float *Ra, const float *Rb, const float *tb,
+                         const float *dRo, const float *dto, float *dRa, float *dta, float *dRb,
+                         float *dtb, void *stream);
+/* gradient of scale * dloss[0] * transformation_loss(...)[0] (losses.py:117-160) w.r.t.
+ * pred R, t (dloss: device scalar, the upstream gradient; NULL = 1) */
+int hreg_transformation_loss_bwd(const float *pred_R, const float *pred_t, const float *gt_R,
+                                 const float *gt_t, int nb, float alpha, float scale,
+                                 const float *dloss, float *dR, float *dt, void *stream);
 
 /* Spatial index for exact culled kNN grouping (n <= 16384 points per cloud):
  * hreg_spatial_index sorts each cloud of p [nb][n][3] by Morton code and records

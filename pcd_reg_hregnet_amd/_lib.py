@@ -83,10 +83,36 @@ _SIGS = {
     "hreg_transpose": [_vp, _i, _i, _vp, _vp],
     "hreg_adam_step": [_vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_float, ctypes.c_float,
                        ctypes.c_float, ctypes.c_float, _i, _vp],
+    "hreg_copy_rows": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp],
+    "hreg_group_sum": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp],
+    "hreg_gather_rows": [_vp, _i, _vp, _i, _i, _vp, _i, _vp],
+    "hreg_csr_build": [_vp, _i, _i, _vp, _vp],
+    "hreg_scatter_rows": [_vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp],
+    "hreg_geom_rows": [_vp, _vp, _i, _i, _vp, _i, _vp],
+    "hreg_geom_rows_bwd": [_vp, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp],
+    "hreg_attention_fwd": [_vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp,
+                           _i, _vp],
+    "hreg_attention_bwd": [_vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp,
+                           _i, _i, _vp, _i, _vp, _i, _vp, _vp],
+    "hreg_group_max_arg": [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp],
+    "hreg_group_max_bwd": [_vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp],
+    "hreg_head_out_bwd": [_vp, _i, _i, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _vp],
+    "hreg_sim_stats": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_sim_feats": [_vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _i, _vp],
+    "hreg_sim_feats_bwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp,
+                           _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_weighted_svd_bwd": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_transform_points_bwd": [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_compose_se3": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_compose_se3_bwd": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_transformation_loss_bwd": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, ctypes.c_float, _vp,
+                                     _vp, _vp, _vp],
+    "hreg_index_offset": [_vp, _i, _i, _i, _vp, _vp],
 }
 
 EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_reduce_ws_bytes",
-                          "hreg_gemm_tn_ws_bytes", "hreg_group_l1_table_floats",
+                          "hreg_gemm_tn_ws_bytes", "hreg_csr_ws_bytes",
+                          "hreg_sim_feats_bwd_ws_bytes", "hreg_group_l1_table_floats",
                           "hreg_group_l2_table_floats", "hreg_group_l3_table_floats",
                           "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
                           "hreg_group_split_l3_table_floats")
@@ -115,6 +141,10 @@ def load(require_gpu: bool = True):
         L.hreg_col_reduce_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         L.hreg_gemm_tn_ws_bytes.restype = ctypes.c_size_t
         L.hreg_gemm_tn_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.hreg_csr_ws_bytes.restype = ctypes.c_size_t
+        L.hreg_csr_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.hreg_sim_feats_bwd_ws_bytes.restype = ctypes.c_size_t
+        L.hreg_sim_feats_bwd_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
                      "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
                      "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats"):

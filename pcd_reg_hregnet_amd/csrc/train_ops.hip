@@ -1,0 +1,1228 @@
+// train_ops.hip -- forward/backward kernels of the HRegNet training step
+// (BASELINE configs[3]: train_reg_v0.py:241-296).
+//
+// The training graph keeps the reference's layer structure (train-mode BatchNorm
+// needs batch statistics between every conv, so the eval-mode fused kernels do not
+// apply) and runs every op of it here; pcd_reg_hregnet_amd/train_graph.py wires
+// them into torch.autograd.Function objects.  Layout: activations are point-major
+// rows [rows][channels]; the rows of a group of k neighbours are consecutive.
+//
+//   copy_rows / group_sum        cat / split, repeat over k and its backward
+//   gather_rows, csr + scatter   knn_gather / gather_operation (layers.py:20-26,
+//                                139-143) and their backward, deterministic: the
+//                                backward sums each source row's contributions in
+//                                ascending destination order (the reference's
+//                                gather_points_grad_kernel uses atomicAdd, .cu:41-73)
+//   geom_rows                    [knn_xyz - q, |knn_xyz - q|] (layers.py:21-23, 284-285)
+//   attention                    max over channels -> softmax over k -> attentive sums
+//                                (layers.py:151-159, 384-388, 447-450, 340-343)
+//   group_max_arg                torch.max over k (layers.py:202, 208) with its argmax
+//   head_out_bwd                 mlp3 + softplus(+0.001) / sigmoid backward
+//   sim_*                        max-normalised cosine similarity gathered at the
+//                                descriptor kNN (layers.py:290-313, 345-362), backward
+//                                through the row/column maxima and the norms
+//   weighted_svd_bwd             WeightedSVDHead (layers.py:469-504) backward, fp64,
+//                                torch.svd's backward formula + det() of the reflection fix
+//   transform / compose          R x + t (models.py:91-92, 113-114) and T_ @ T_prev
+//                                (models.py:100-110, 120-127)
+//   transformation_loss_bwd      losses.py:117-160 (alpha * mean |R^T R_gt - I|_F + mean |dt|)
+#include "common.h"
+#include "svd3.h"
+
+namespace {
+
+constexpr int TB = 256;
+
+inline unsigned g1d(size_t n) {
+    size_t b = (n + TB - 1) / TB;
+    if (b > (1u << 20)) b = (1u << 20);
+    return (unsigned)(b ? b : 1);
+}
+
+#define GRID_STRIDE(i, total) \
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (total); \
+         i += (size_t)gridDim.x * blockDim.x)
+
+// ------------------------------------------------------------ copies / sums
+__global__ void copy_rows_kernel(const float *__restrict__ src, int lds, int row_div, int R, int C,
+                                 float *__restrict__ dst, int ldd, int acc) {
+    GRID_STRIDE(i, (size_t)R * C) {
+        const int r = (int)(i / C), c = (int)(i % C);
+        const float v = src[(size_t)(r / row_div) * lds + c];
+        float *o = dst + (size_t)r * ldd + c;
+        *o = acc ? fadd_rn(*o, v) : v;
+    }
+}
+
+__global__ void group_sum_kernel(const float *__restrict__ x, int ldx, int G, int k, int C,
+                                 float *__restrict__ out, int ldo, int acc) {
+    GRID_STRIDE(i, (size_t)G * C) {
+        const int g = (int)(i / C), c = (int)(i % C);
+        const float *p = x + (size_t)g * k * ldx + c;
+        float s = 0.f;
+        for (int j = 0; j < k; ++j) s = fadd_rn(s, p[(size_t)j * ldx]);
+        float *o = out + (size_t)g * ldo + c;
+        *o = acc ? fadd_rn(*o, s) : s;
+    }
+}
+
+__global__ void gather_rows_kernel(const float *__restrict__ x, int ldx,
+                                   const int32_t *__restrict__ idx, int M, int C,
+                                   float *__restrict__ out, int ldo) {
+    GRID_STRIDE(i, (size_t)M * C) {
+        const int m = (int)(i / C), c = (int)(i % C);
+        out[(size_t)m * ldo + c] = x[(size_t)idx[m] * ldx + c];
+    }
+}
+
+// out[b*m + j] = idx[b*m + j] + b*n: per-cloud indices -> rows of the [nb*n] stack
+__global__ void index_offset_kernel(const int32_t *__restrict__ idx, int nb, int m, int n,
+                                    int32_t *__restrict__ out) {
+    GRID_STRIDE(i, (size_t)nb * m) out[i] = idx[i] + (int32_t)(i / m) * n;
+}
+
+// ---------------------------------------------------------- CSR of an index
+// ws: offsets [n+1] | entries [M] | cursor [n]  (int32)
+struct Csr {
+    int32_t *off, *ent, *cur;
+};
+__host__ __device__ inline Csr csr_view(void *ws, int M, int n) {
+    int32_t *p = (int32_t *)ws;
+    return Csr{p, p + (n + 1), p + (n + 1) + M};
+}
+
+__global__ void csr_count_kernel(const int32_t *__restrict__ idx, int M, int n,
+                                 int32_t *__restrict__ cur) {
+    GRID_STRIDE(i, (size_t)M) {
+        const int v = idx[i];
+        if (v >= 0 && v < n) atomicAdd(&cur[v], 1);
+    }
+}
+
+// exclusive scan of cur[0..n) -> off[0..n], single workgroup of 1024 threads
+__global__ __launch_bounds__(1024) void csr_scan_kernel(const int32_t *__restrict__ cnt, int n,
+                                                        int32_t *__restrict__ off) {
+    __shared__ int32_t part[1024];
+    const int t = threadIdx.x;
+    const int chunk = (n + 1023) / 1024;
+    const int a = min(n, t * chunk), b = min(n, a + chunk);
+    int32_t s = 0;
+    for (int i = a; i < b; ++i) s += cnt[i];
+    part[t] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int32_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int32_t run = part[t] - s;  // exclusive prefix of this chunk
+    for (int i = a; i < b; ++i) {
+        off[i] = run;
+        run += cnt[i];
+    }
+    if (t == 1023) off[n] = part[1023];
+}
+
+__global__ void csr_fill_kernel(const int32_t *__restrict__ idx, int M, int n,
+                                const int32_t *__restrict__ off, int32_t *__restrict__ cur,
+                                int32_t *__restrict__ ent) {
+    GRID_STRIDE(i, (size_t)M) {
+        const int v = idx[i];
+        if (v >= 0 && v < n) ent[off[v] + atomicAdd(&cur[v], 1)] = (int32_t)i;
+    }
+}
+
+// each segment sorted ascending: the scatter then sums in destination order
+__global__ void csr_sort_kernel(int n, const int32_t *__restrict__ off, int32_t *__restrict__ ent) {
+    GRID_STRIDE(s, (size_t)n) {
+        const int a = off[s], b = off[s + 1];
+        for (int i = a + 1; i < b; ++i) {
+            const int32_t v = ent[i];
+            int j = i - 1;
+            while (j >= a && ent[j] > v) {
+                ent[j + 1] = ent[j];
+                --j;
+            }
+            ent[j + 1] = v;
+        }
+    }
+}
+
+__global__ void scatter_rows_kernel(const float *__restrict__ dy, int ldy,
+                                    const int32_t *__restrict__ off,
+                                    const int32_t *__restrict__ ent, int n, int C,
+                                    float *__restrict__ dx, int ldx, int acc) {
+    GRID_STRIDE(i, (size_t)n * C) {
+        const int s = (int)(i / C), c = (int)(i % C);
+        float v = 0.f;
+        for (int e = off[s]; e < off[s + 1]; ++e) v = fadd_rn(v, dy[(size_t)ent[e] * ldy + c]);
+        float *o = dx + (size_t)s * ldx + c;
+        *o = acc ? fadd_rn(*o, v) : v;
+    }
+}
+
+// ------------------------------------------------------------- geometry rows
+__global__ void geom_rows_kernel(const float *__restrict__ q, const float *__restrict__ kx, int G,
+                                 int k, float *__restrict__ out, int ldo) {
+    GRID_STRIDE(r, (size_t)G * k) {
+        const size_t g = r / k;
+        const float dx = fsub_rn(kx[r * 3], q[g * 3]);
+        const float dy = fsub_rn(kx[r * 3 + 1], q[g * 3 + 1]);
+        const float dz = fsub_rn(kx[r * 3 + 2], q[g * 3 + 2]);
+        float *o = out + r * ldo;
+        o[0] = dx;
+        o[1] = dy;
+        o[2] = dz;
+        o[3] = sqrtf(fadd_rn(fadd_rn(fmul_rn(dx, dx), fmul_rn(dy, dy)), fmul_rn(dz, dz)));
+    }
+}
+
+// geom = [rela(3), dist(1)]: drela = dgeom[0:3] + ddist * rela / dist (0 at dist 0, as
+// torch.norm's backward); dkx = drela (+ dkx_extra); dq = -sum_k drela
+__global__ void geom_rows_bwd_kernel(const float *__restrict__ geom, int ldg,
+                                     const float *__restrict__ dgeom, int lddg,
+                                     const float *__restrict__ dkx_extra, int G, int k,
+                                     float *__restrict__ dq, float *__restrict__ dkx) {
+    GRID_STRIDE(g, (size_t)G) {
+        float sx = 0.f, sy = 0.f, sz = 0.f;
+        for (int j = 0; j < k; ++j) {
+            const size_t r = g * k + j;
+            const float *gr = geom + r * ldg;
+            const float *dg = dgeom + r * lddg;
+            float d0 = dg[0], d1 = dg[1], d2 = dg[2];
+            const float dist = gr[3];
+            if (dist > 0.f) {
+                const float f = dg[3] / dist;
+                d0 = fadd_rn(d0, fmul_rn(f, gr[0]));
+                d1 = fadd_rn(d1, fmul_rn(f, gr[1]));
+                d2 = fadd_rn(d2, fmul_rn(f, gr[2]));
+            }
+            if (dkx) {
+                float e0 = d0, e1 = d1, e2 = d2;
+                if (dkx_extra) {
+                    e0 = fadd_rn(e0, dkx_extra[r * 3]);
+                    e1 = fadd_rn(e1, dkx_extra[r * 3 + 1]);
+                    e2 = fadd_rn(e2, dkx_extra[r * 3 + 2]);
+                }
+                dkx[r * 3] = e0;
+                dkx[r * 3 + 1] = e1;
+                dkx[r * 3 + 2] = e2;
+            }
+            sx = fadd_rn(sx, d0);
+            sy = fadd_rn(sy, d1);
+            sz = fadd_rn(sz, d2);
+        }
+        if (dq) {
+            dq[g * 3] = -sx;
+            dq[g * 3 + 1] = -sy;
+            dq[g * 3 + 2] = -sz;
+        }
+    }
+}
+
+// ----------------------------------------------------------------- attention
+// One workgroup per group of k <= 64 rows.  x1 = max_c logits (first index),
+// a = softmax_k(x1), kp = sum a*kx, vmap = vals*a, vsum = sum_k vmap.
+__global__ __launch_bounds__(TB) void attention_fwd_kernel(
+    const float *__restrict__ logits, int ldl, int C, const float *__restrict__ vals, int ldv,
+    int Cv, const float *__restrict__ kx, int k, float *__restrict__ a_out,
+    int32_t *__restrict__ amax, float *__restrict__ kp, float *__restrict__ vmap, int ldm,
+    float *__restrict__ vsum, int lds) {
+    __shared__ float x1[64], aw[64];
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int j = w; j < k; j += TB / 64) {
+        const float *row = logits + ((size_t)g * k + j) * ldl;
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int c = lane; c < C; c += 64) {
+            const float v = row[c];
+            if (v > best) { best = v; bi = c; }
+        }
+        for (int m = 32; m >= 1; m >>= 1) {
+            const float ob = __shfl_xor(best, m);
+            const int oi = __shfl_xor(bi, m);
+            if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        }
+        if (lane == 0) {
+            x1[j] = best;
+            if (amax) amax[(size_t)g * k + j] = bi;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float m = -INFINITY;
+        for (int j = 0; j < k; ++j) m = fmaxf(m, x1[j]);
+        float s = 0.f;
+        for (int j = 0; j < k; ++j) {
+            aw[j] = expf(fsub_rn(x1[j], m));
+            s = fadd_rn(s, aw[j]);
+        }
+        for (int j = 0; j < k; ++j) aw[j] = aw[j] / s;
+    }
+    __syncthreads();
+    if (threadIdx.x < k && a_out) a_out[(size_t)g * k + threadIdx.x] = aw[threadIdx.x];
+    if (kp && threadIdx.x < 3) {
+        float s = 0.f;
+        for (int j = 0; j < k; ++j)
+            s = fadd_rn(s, fmul_rn(aw[j], kx[((size_t)g * k + j) * 3 + threadIdx.x]));
+        kp[(size_t)g * 3 + threadIdx.x] = s;
+    }
+    if (vals)
+        for (int c = threadIdx.x; c < Cv; c += TB) {
+            float s = 0.f;
+            for (int j = 0; j < k; ++j) {
+                const float v = fmul_rn(vals[((size_t)g * k + j) * ldv + c], aw[j]);
+                if (vmap) vmap[((size_t)g * k + j) * ldm + c] = v;
+                s = fadd_rn(s, v);
+            }
+            if (vsum) vsum[(size_t)g * lds + c] = s;
+        }
+}
+
+// dve = dvmap + dvsum[g]; dvals = a*dve; da = sum_c vals*dve + kx.dkp;
+// dx1 = a*(da - sum a da); dlogits = onehot(amax)*dx1 (+ dvals when vals == logits)
+__global__ __launch_bounds__(TB) void attention_bwd_kernel(
+    const float *__restrict__ logits, int ldl, int C, const float *__restrict__ vals, int ldv,
+    int Cv, const float *__restrict__ kx, int k, const float *__restrict__ a_in,
+    const int32_t *__restrict__ amax, const float *__restrict__ dkp,
+    const float *__restrict__ dvmap, int lddm, const float *__restrict__ dvsum, int ldds,
+    int same, float *__restrict__ dlogits, int lddl, float *__restrict__ dvals, int lddv,
+    float *__restrict__ dkx) {
+    __shared__ float aw[64], da[64], dx1[64];
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x < k) aw[threadIdx.x] = a_in[(size_t)g * k + threadIdx.x];
+    __syncthreads();
+    for (int j = w; j < k; j += TB / 64) {
+        const size_t r = (size_t)g * k + j;
+        float part = 0.f;
+        if (vals && (dvmap || dvsum))
+            for (int c = lane; c < Cv; c += 64) {
+                float d = 0.f;
+                if (dvmap) d = dvmap[r * lddm + c];
+                if (dvsum) d = fadd_rn(d, dvsum[(size_t)g * ldds + c]);
+                part = fadd_rn(part, fmul_rn(vals[r * ldv + c], d));
+                if (dvals && !same) dvals[r * lddv + c] = fmul_rn(aw[j], d);
+            }
+        part = wave_sum_f32(part);
+        if (lane == 0) {
+            float s = part;
+            if (dkp)
+                for (int d = 0; d < 3; ++d) s = fadd_rn(s, fmul_rn(kx[r * 3 + d], dkp[(size_t)g * 3 + d]));
+            da[j] = s;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int j = 0; j < k; ++j) s = fadd_rn(s, fmul_rn(aw[j], da[j]));
+        for (int j = 0; j < k; ++j) dx1[j] = fmul_rn(aw[j], fsub_rn(da[j], s));
+    }
+    __syncthreads();
+    if (dkx && dkp && threadIdx.x < 3 * k) {
+        const int j = threadIdx.x / 3, d = threadIdx.x % 3;
+        dkx[((size_t)g * k + j) * 3 + d] = fmul_rn(aw[j], dkp[(size_t)g * 3 + d]);
+    }
+    if (dlogits)
+        for (int j = w; j < k; j += TB / 64) {
+            const size_t r = (size_t)g * k + j;
+            const int am = amax[r];
+            for (int c = lane; c < C; c += 64) {
+                float v = c == am ? dx1[j] : 0.f;
+                if (same) {
+                    float d = 0.f;
+                    if (dvmap) d = dvmap[r * lddm + c];
+                    if (dvsum) d = fadd_rn(d, dvsum[(size_t)g * ldds + c]);
+                    v = fadd_rn(v, fmul_rn(aw[j], d));
+                }
+                dlogits[r * lddl + c] = v;
+            }
+        }
+}
+
+// --------------------------------------------------------------- group max
+__global__ void group_max_arg_kernel(const float *__restrict__ x, int ldx, int G, int k, int C,
+                                     float *__restrict__ out, int ldo, int32_t *__restrict__ arg) {
+    GRID_STRIDE(i, (size_t)G * C) {
+        const int g = (int)(i / C), c = (int)(i % C);
+        const float *p = x + (size_t)g * k * ldx + c;
+        float b = p[0];
+        int bi = 0;
+        for (int j = 1; j < k; ++j) {
+            const float v = p[(size_t)j * ldx];
+            if (v > b) { b = v; bi = j; }
+        }
+        out[(size_t)g * ldo + c] = b;
+        arg[i] = bi;
+    }
+}
+
+__global__ void group_max_bwd_kernel(const float *__restrict__ dout, int ldd,
+                                     const int32_t *__restrict__ arg, int G, int k, int C,
+                                     float *__restrict__ dx, int ldx, int acc) {
+    GRID_STRIDE(i, (size_t)G * C) {
+        const int g = (int)(i / C), c = (int)(i % C);
+        const int a = arg[i];
+        const float d = dout[(size_t)g * ldd + c];
+        float *p = dx + (size_t)g * k * ldx + c;
+        if (acc) {
+            p[(size_t)a * ldx] = fadd_rn(p[(size_t)a * ldx], d);
+        } else {
+            for (int j = 0; j < k; ++j) p[(size_t)j * ldx] = j == a ? d : 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------- head output bwd
+// y = softplus(z) + 0.001 (mode HREG_HEAD_SOFTPLUS) or sigmoid(z), z = x.w3 + b3:
+// dz = dy * act'(z) (torch softplus_backward: threshold 20), dx = dz * w3
+__global__ __launch_bounds__(TB) void head_out_bwd_kernel(const float *__restrict__ x, int ldx,
+                                                          int C, const float *__restrict__ w3,
+                                                          const float *__restrict__ b3,
+                                                          const float *__restrict__ dy, int mode,
+                                                          int G, float *__restrict__ dz,
+                                                          float *__restrict__ dx, int lddx) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = blockIdx.x * (TB / 64) + w;
+    if (g >= G) return;
+    const float *row = x + (size_t)g * ldx;
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s = fadd_rn(s, fmul_rn(row[c], w3[c]));
+    s = wave_sum_f32(s);
+    const float z = fadd_rn(s, b3[0]);
+    float d;
+    if (mode == HREG_HEAD_SOFTPLUS) {
+        if (z > 20.f) {
+            d = dy[g];
+        } else {
+            const float e = expf(z);
+            d = dy[g] * e / (e + 1.f);
+        }
+    } else {
+        const float y = 1.f / (1.f + expf(-z));
+        d = fmul_rn(dy[g], fmul_rn(y, fsub_rn(1.f, y)));
+    }
+    if (lane == 0) dz[g] = d;
+    for (int c = lane; c < C; c += 64) dx[(size_t)g * lddx + c] = fmul_rn(d, w3[c]);
+}
+
+// --------------------------------------------------------- cosine similarity
+// S [nb][N1][N2]: row maxima (over N2) and column maxima (over N1), first index
+__global__ void sim_stats_kernel(const float *__restrict__ S, int nb, int N1, int N2,
+                                 float *__restrict__ rmax, int32_t *__restrict__ rarg,
+                                 float *__restrict__ cmax, int32_t *__restrict__ carg) {
+    GRID_STRIDE(t, (size_t)nb * (N1 + N2)) {
+        const int b = (int)(t / (N1 + N2)), u = (int)(t % (N1 + N2));
+        const float *Sb = S + (size_t)b * N1 * N2;
+        if (u < N1) {
+            const float *row = Sb + (size_t)u * N2;
+            float m = row[0];
+            int a = 0;
+            for (int j = 1; j < N2; ++j)
+                if (row[j] > m) { m = row[j]; a = j; }
+            rmax[(size_t)b * N1 + u] = m;
+            rarg[(size_t)b * N1 + u] = a;
+        } else {
+            const int j = u - N1;
+            float m = Sb[j];
+            int a = 0;
+            for (int i = 1; i < N1; ++i)
+                if (Sb[(size_t)i * N2 + j] > m) { m = Sb[(size_t)i * N2 + j]; a = i; }
+            cmax[(size_t)b * N2 + j] = m;
+            carg[(size_t)b * N2 + j] = a;
+        }
+    }
+}
+
+// out[r][0] = S[i][n] / (rmax_i + 1e-6)   (src_dst_cos, layers.py:300-313)
+// out[r][1] = S[i][n] / (cmax_n + 1e-6)   (dst_src_cos, layers.py:296-307), n = kidx[b][i][j]
+__global__ void sim_feats_kernel(const float *__restrict__ S, int nb, int N1, int N2,
+                                 const int32_t *__restrict__ kidx, int k,
+                                 const float *__restrict__ rmax, const float *__restrict__ cmax,
+                                 float *__restrict__ out, int ldo) {
+    GRID_STRIDE(r, (size_t)nb * N1 * k) {
+        const size_t bi = r / k;
+        const int b = (int)(bi / N1);
+        const int n = kidx[r];
+        const float s = S[bi * N2 + n];
+        out[r * ldo] = s / fadd_rn(rmax[bi], 1e-6f);
+        out[r * ldo + 1] = s / fadd_rn(cmax[(size_t)b * N2 + n], 1e-6f);
+    }
+}
+
+// dS rows (dS zeroed before): the gathered entries and the row-max term
+__global__ void sim_bwd_rows_kernel(const float *__restrict__ S, int nb, int N1, int N2,
+                                    const int32_t *__restrict__ kidx, int k,
+                                    const float *__restrict__ rmax, const int32_t *__restrict__ rarg,
+                                    const float *__restrict__ cmax, const float *__restrict__ dout,
+                                    int ldd, float *__restrict__ dS) {
+    GRID_STRIDE(bi, (size_t)nb * N1) {
+        const int b = (int)(bi / N1);
+        const float rm = fadd_rn(rmax[bi], 1e-6f);
+        float drm = 0.f;
+        float *dr = dS + bi * N2;
+        for (int j = 0; j < k; ++j) {
+            const size_t r = bi * k + j;
+            const int n = kidx[r];
+            const float s = S[bi * N2 + n];
+            const float g1 = dout[r * ldd], g2 = dout[r * ldd + 1];
+            const float cm = fadd_rn(cmax[(size_t)b * N2 + n], 1e-6f);
+            dr[n] = fadd_rn(dr[n], fadd_rn(g1 / rm, g2 / cm));
+            drm = fsub_rn(drm, g1 * s / fmul_rn(rm, rm));
+        }
+        const int a = rarg[bi];
+        dr[a] = fadd_rn(dr[a], drm);
+    }
+}
+
+// column-max term: dcm_n = -sum_{(i,j): kidx = n} g2 S[i][n] / (cmax_n+1e-6)^2 -> dS[carg_n][n]
+__global__ void sim_bwd_cols_kernel(const float *__restrict__ S, int nb, int N1, int N2,
+                                    const int32_t *__restrict__ kidx, int k,
+                                    const float *__restrict__ cmax, const int32_t *__restrict__ carg,
+                                    const float *__restrict__ dout, int ldd, float *__restrict__ dS) {
+    GRID_STRIDE(bn, (size_t)nb * N2) {
+        const int b = (int)(bn / N2), n = (int)(bn % N2);
+        const float cm = fadd_rn(cmax[bn], 1e-6f);
+        const float cm2 = fmul_rn(cm, cm);
+        float dcm = 0.f;
+        const int32_t *ki = kidx + (size_t)b * N1 * k;
+        for (int e = 0; e < N1 * k; ++e)
+            if (ki[e] == n) {
+                const int i = e / k;
+                const float s = S[((size_t)b * N1 + i) * N2 + n];
+                dcm = fsub_rn(dcm, dout[((size_t)b * N1 * k + e) * ldd + 1] * s / cm2);
+            }
+        float *p = dS + ((size_t)b * N1 + carg[bn]) * N2 + n;
+        *p = fadd_rn(*p, dcm);
+    }
+}
+
+// cosine backward, S = P / (na nb^T + 1e-6): dP = dS / den;
+// dna_i = -sum_j dS_ij S_ij nb_j / den_ij, dnb_j = -sum_i dS_ij S_ij na_i / den_ij
+__global__ void sim_bwd_cos_kernel(const float *__restrict__ S, const float *__restrict__ dS, int nb,
+                                   int N1, int N2, const float *__restrict__ na,
+                                   const float *__restrict__ nbv, float *__restrict__ dP,
+                                   float *__restrict__ dna, float *__restrict__ dnb) {
+    GRID_STRIDE(t, (size_t)nb * (N1 + N2)) {
+        const int b = (int)(t / (N1 + N2)), u = (int)(t % (N1 + N2));
+        const float *Sb = S + (size_t)b * N1 * N2, *dSb = dS + (size_t)b * N1 * N2;
+        const float *a = na + (size_t)b * N1, *c = nbv + (size_t)b * N2;
+        if (u < N1) {
+            float acc = 0.f;
+            for (int j = 0; j < N2; ++j) {
+                const size_t e = (size_t)u * N2 + j;
+                const float den = fadd_rn(fmul_rn(a[u], c[j]), 1e-6f);
+                dP[(size_t)b * N1 * N2 + e] = dSb[e] / den;
+                acc = fsub_rn(acc, dSb[e] * Sb[e] / den * c[j]);
+            }
+            dna[(size_t)b * N1 + u] = acc;
+        } else {
+            const int j = u - N1;
+            float acc = 0.f;
+            for (int i = 0; i < N1; ++i) {
+                const size_t e = (size_t)i * N2 + j;
+                const float den = fadd_rn(fmul_rn(a[i], c[j]), 1e-6f);
+                acc = fsub_rn(acc, dSb[e] * Sb[e] / den * a[i]);
+            }
+            dnb[(size_t)b * N2 + j] = acc;
+        }
+    }
+}
+
+// out[b][i][c] = sum_j M[b][i][j] X[b][j][c] + (dn_i / n_i) Y[b][i][c]   (TRANS: M^T)
+// 64x64 output tile per 256-thread workgroup, 4x4 per thread, j staged through LDS.
+template <bool TRANS>
+__global__ __launch_bounds__(TB) void sim_bwd_mm_kernel(const float *__restrict__ M, int N1,
+                                                        int N2, const float *__restrict__ X,
+                                                        const float *__restrict__ Y,
+                                                        const float *__restrict__ dn,
+                                                        const float *__restrict__ nrm, int C,
+                                                        float *__restrict__ out) {
+    // rows of out: TRANS ? N2 : N1; reduction length: TRANS ? N1 : N2
+    const int Ro = TRANS ? N2 : N1, Kr = TRANS ? N1 : N2;
+    const int b = blockIdx.z;
+    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    __shared__ float Ms[16][65], Xs[16][65];
+    const int tr = threadIdx.x / 16, tc = threadIdx.x % 16;
+    float acc[4][4] = {};
+    const float *Mb = M + (size_t)b * N1 * N2;
+    const float *Xb = X + (size_t)b * Kr * C;
+    for (int j0 = 0; j0 < Kr; j0 += 16) {
+        for (int e = threadIdx.x; e < 16 * 64; e += TB) {
+            const int jj = e / 64, rr = e % 64;
+            const int j = j0 + jj, r = r0 + rr, c = c0 + rr;
+            float mv = 0.f;
+            if (j < Kr && r < Ro) mv = TRANS ? Mb[(size_t)j * N2 + r] : Mb[(size_t)r * N2 + j];
+            Ms[jj][rr] = mv;
+            Xs[jj][rr] = (j < Kr && c < C) ? Xb[(size_t)j * C + c] : 0.f;
+        }
+        __syncthreads();
+        for (int jj = 0; jj < 16; ++jj)
+            for (int p = 0; p < 4; ++p)
+                for (int q = 0; q < 4; ++q)
+                    acc[p][q] = fmaf(Ms[jj][tr * 4 + p], Xs[jj][tc * 4 + q], acc[p][q]);
+        __syncthreads();
+    }
+    for (int p = 0; p < 4; ++p) {
+        const int r = r0 + tr * 4 + p;
+        if (r >= Ro) continue;
+        const float nv = nrm[(size_t)b * Ro + r];
+        const float f = nv > 0.f ? dn[(size_t)b * Ro + r] / nv : 0.f;
+        for (int q = 0; q < 4; ++q) {
+            const int c = c0 + tc * 4 + q;
+            if (c >= C) continue;
+            out[((size_t)b * Ro + r) * C + c] =
+                fadd_rn(acc[p][q], fmul_rn(f, Y[((size_t)b * Ro + r) * C + c]));
+        }
+    }
+}
+
+// ------------------------------------------------------- weighted SVD backward
+// Forward (layers.py:469-504): sw = sum w + 1e-4; wn = w / sw; den = sum wn + 1e-4;
+// mu_s = sum wn s / den; mu_c likewise; H = sum wn (s-mu_s)(c-mu_c)^T = U S V^T;
+// d = det(V^T U^T); R = V diag(1,1,d) U^T; t = mu_c - R mu_s.
+__global__ __launch_bounds__(TB) void svd_bwd_kernel(const float *__restrict__ src,
+                                                     const float *__restrict__ cor,
+                                                     const float *__restrict__ w, int n,
+                                                     const float *__restrict__ dR_in,
+                                                     const float *__restrict__ dt_in,
+                                                     float *__restrict__ dsrc,
+                                                     float *__restrict__ dcor,
+                                                     float *__restrict__ dw) {
+    __shared__ double red[TB / 64][16];
+    __shared__ double sh[32];  // gH 9 | ms 3 | mc 3 | dPs 3 | dPc 3 | dden | sw | ok | red
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b = blockIdx.x;
+    const float *S = src + (size_t)b * n * 3, *Cc = cor + (size_t)b * n * 3, *W = w + (size_t)b * n;
+    auto block_sum = [&](double v[], int cnt) {
+        for (int q = 0; q < cnt; ++q) v[q] = wave_sum_f64(v[q]);
+        __syncthreads();
+        if (lane == 0)
+            for (int q = 0; q < cnt; ++q) red[wv][q] = v[q];
+        __syncthreads();
+        for (int q = 0; q < cnt; ++q) v[q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+        __syncthreads();
+    };
+    double v1[1] = {0.0};
+    for (int i = threadIdx.x; i < n; i += TB) v1[0] += (double)W[i];
+    block_sum(v1, 1);
+    const double sw = v1[0] + 1e-4;
+    double m[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int i = threadIdx.x; i < n; i += TB) {
+        const double wi = (double)W[i] / sw;
+        m[0] += wi;
+        for (int d = 0; d < 3; ++d) {
+            m[1 + d] += wi * (double)S[i * 3 + d];
+            m[4 + d] += wi * (double)Cc[i * 3 + d];
+        }
+    }
+    block_sum(m, 7);
+    const double den = m[0] + 1e-4;
+    const double ms[3] = {m[1] / den, m[2] / den, m[3] / den};
+    const double mc[3] = {m[4] / den, m[5] / den, m[6] / den};
+    double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = threadIdx.x; i < n; i += TB) {
+        const double wi = (double)W[i] / sw;
+        double a[3], c[3];
+        for (int d = 0; d < 3; ++d) {
+            a[d] = (double)S[i * 3 + d] - ms[d];
+            c[d] = (double)Cc[i * 3 + d] - mc[d];
+        }
+        for (int p = 0; p < 3; ++p)
+            for (int q = 0; q < 3; ++q) h[p * 3 + q] += a[p] * wi * c[q];
+    }
+    block_sum(h, 9);
+    if (threadIdx.x == 0) {
+        bool ok = true;
+        for (int q = 0; q < 9; ++q) ok = ok && isfinite(h[q]);
+        double H[3][3], u[3][3], v[3][3], sg[3];
+        for (int p = 0; p < 3; ++p)
+            for (int q = 0; q < 3; ++q) H[p][q] = h[p * 3 + q];
+        double gH[3][3] = {};
+        double dms[3] = {0, 0, 0}, dmc[3] = {0, 0, 0};
+        if (ok) {
+            const double d = svd3_usv(H, u, sg, v);
+            // U[:, i] = u[i], V[:, i] = v[i]
+            double U[3][3], V[3][3], R[3][3], dR[3][3];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) { U[i][j] = u[j][i]; V[i][j] = v[j][i]; }
+            const double D[3] = {1.0, 1.0, d};
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    double s = 0;
+                    for (int q = 0; q < 3; ++q) s += V[i][q] * D[q] * U[j][q];
+                    R[i][j] = s;
+                }
+            const float *dRb = dR_in + (size_t)b * 9, *dtb = dt_in + (size_t)b * 3;
+            // t = mu_c - R mu_s
+            for (int i = 0; i < 3; ++i) {
+                dmc[i] = (double)dtb[i];
+                for (int j = 0; j < 3; ++j) dR[i][j] = (double)dRb[i * 3 + j] - (double)dtb[i] * ms[j];
+            }
+            for (int j = 0; j < 3; ++j) {
+                double s = 0;
+                for (int i = 0; i < 3; ++i) s += R[i][j] * (double)dtb[i];
+                dms[j] = -s;
+            }
+            // R = V D U^T: gV = dR U D, gU = dR^T V D, gdet = (V^T dR U)[2][2]
+            double gV[3][3], gU[3][3], M[3][3];
+            double gdet = 0;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    double sv = 0, su = 0;
+                    for (int q = 0; q < 3; ++q) {
+                        sv += dR[i][q] * U[q][j];
+                        su += dR[q][i] * V[q][j];
+                    }
+                    gV[i][j] = sv * D[j];
+                    gU[i][j] = su * D[j];
+                }
+            for (int p = 0; p < 3; ++p)
+                for (int q = 0; q < 3; ++q) gdet += V[p][2] * dR[p][q] * U[q][2];
+            // d = det(M), M = V^T U^T orthogonal: gM = gdet * d * M^{-T} = gdet * d * M
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    double s = 0;
+                    for (int q = 0; q < 3; ++q) s += V[q][i] * U[j][q];
+                    M[i][j] = s;
+                }
+            double gM[3][3];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) gM[i][j] = gdet * d * M[i][j];
+            // dM = dV^T U^T + V^T dU^T: gV += U^T gM^T, gU += gM^T V^T
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    double a = 0, c = 0;
+                    for (int q = 0; q < 3; ++q) {
+                        a += U[q][i] * gM[j][q];
+                        c += gM[q][i] * V[j][q];
+                    }
+                    gV[i][j] += a;
+                    gU[i][j] += c;
+                }
+            // torch svd_backward (gS = 0): skew(X) = X - X^T,
+            // ret = (skew(U^T gU) * S_j + S_i * skew(V^T gV)) / (S_j^2 - S_i^2), gH = U ret V^T
+            double UgU[3][3], VgV[3][3];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    double a = 0, c = 0;
+                    for (int q = 0; q < 3; ++q) {
+                        a += U[q][i] * gU[q][j];
+                        c += V[q][i] * gV[q][j];
+                    }
+                    UgU[i][j] = a;
+                    VgV[i][j] = c;
+                }
+            double ret[3][3];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    if (i == j) { ret[i][j] = 0; continue; }
+                    const double ku = UgU[i][j] - UgU[j][i], kv = VgV[i][j] - VgV[j][i];
+                    const double E = sg[j] * sg[j] - sg[i] * sg[i];
+                    ret[i][j] = (ku * sg[j] + sg[i] * kv) / E;
+                }
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    double s = 0;
+                    for (int p = 0; p < 3; ++p)
+                        for (int q = 0; q < 3; ++q) s += U[i][p] * ret[p][q] * V[j][q];
+                    gH[i][j] = s;
+                }
+            for (int i = 0; i < 9; ++i) ok = ok && isfinite(gH[i / 3][i % 3]);
+        }
+        for (int i = 0; i < 9; ++i) sh[i] = ok ? gH[i / 3][i % 3] : 0.0;
+        for (int d = 0; d < 3; ++d) {
+            sh[9 + d] = ms[d];
+            sh[12 + d] = mc[d];
+            sh[15 + d] = ok ? dms[d] : 0.0;
+            sh[18 + d] = ok ? dmc[d] : 0.0;
+        }
+        sh[21] = ok ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    double gH[9];
+    for (int i = 0; i < 9; ++i) gH[i] = sh[i];
+    const bool ok = sh[21] != 0.0;
+    // pass A: sum of dsc, dcc (the means' share)
+    double acc6[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = threadIdx.x; i < n; i += TB) {
+        const double wi = (double)W[i] / sw;
+        double a[3], c[3];
+        for (int d = 0; d < 3; ++d) {
+            a[d] = (double)S[i * 3 + d] - ms[d];
+            c[d] = (double)Cc[i * 3 + d] - mc[d];
+        }
+        for (int p = 0; p < 3; ++p) {
+            double s1 = 0, s2 = 0;
+            for (int q = 0; q < 3; ++q) {
+                s1 += gH[p * 3 + q] * c[q];
+                s2 += gH[q * 3 + p] * a[q];
+            }
+            acc6[p] += wi * s1;
+            acc6[3 + p] += wi * s2;
+        }
+    }
+    block_sum(acc6, 6);
+    double dPs[3], dPc[3];
+    for (int d = 0; d < 3; ++d) {
+        dPs[d] = (sh[15 + d] - acc6[d]) / den;
+        dPc[d] = (sh[18 + d] - acc6[3 + d]) / den;
+    }
+    const double dden = -((ms[0] * dPs[0] + ms[1] * dPs[1] + ms[2] * dPs[2]) +
+                          (mc[0] * dPc[0] + mc[1] * dPc[1] + mc[2] * dPc[2]));
+    // pass B: ds, dc; dwn_i; reduce sum dwn_i w_i
+    double acc1[1] = {0.0};
+    for (int i = threadIdx.x; i < n; i += TB) {
+        const double wi = (double)W[i] / sw;
+        double a[3], c[3], s[3], cc[3];
+        for (int d = 0; d < 3; ++d) {
+            s[d] = (double)S[i * 3 + d];
+            cc[d] = (double)Cc[i * 3 + d];
+            a[d] = s[d] - ms[d];
+            c[d] = cc[d] - mc[d];
+        }
+        double dwn = dden;
+        for (int p = 0; p < 3; ++p) {
+            double s1 = 0, s2 = 0;
+            for (int q = 0; q < 3; ++q) {
+                s1 += gH[p * 3 + q] * c[q];
+                s2 += gH[q * 3 + p] * a[q];
+            }
+            dwn += a[p] * s1 + s[p] * dPs[p] + cc[p] * dPc[p];
+            dsrc[((size_t)b * n + i) * 3 + p] = ok ? (float)(wi * s1 + wi * dPs[p]) : 0.f;
+            dcor[((size_t)b * n + i) * 3 + p] = ok ? (float)(wi * s2 + wi * dPc[p]) : 0.f;
+        }
+        acc1[0] += dwn * (double)W[i];
+    }
+    block_sum(acc1, 1);
+    const double corr = acc1[0] / (sw * sw);
+    for (int i = threadIdx.x; i < n; i += TB) {
+        double a[3], c[3], s[3], cc[3];
+        for (int d = 0; d < 3; ++d) {
+            s[d] = (double)S[i * 3 + d];
+            cc[d] = (double)Cc[i * 3 + d];
+            a[d] = s[d] - ms[d];
+            c[d] = cc[d] - mc[d];
+        }
+        double dwn = dden;
+        for (int p = 0; p < 3; ++p) {
+            double s1 = 0;
+            for (int q = 0; q < 3; ++q) s1 += gH[p * 3 + q] * c[q];
+            dwn += a[p] * s1 + s[p] * dPs[p] + cc[p] * dPc[p];
+        }
+        dw[(size_t)b * n + i] = ok ? (float)(dwn / sw - corr) : 0.f;
+    }
+}
+
+// ------------------------------------------------------- transform / compose
+// y = R x + t per point: dx = R^T dy; dR = sum dy x^T; dt = sum dy (fp64, one block per pair)
+__global__ __launch_bounds__(TB) void transform_bwd_kernel(const float *__restrict__ xyz,
+                                                           const float *__restrict__ R, int n,
+                                                           const float *__restrict__ dy,
+                                                           float *__restrict__ dx,
+                                                           float *__restrict__ dR,
+                                                           float *__restrict__ dt) {
+    __shared__ double red[TB / 64][12];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b = blockIdx.x;
+    const float *Rb = R + (size_t)b * 9;
+    double acc[12] = {};
+    for (int i = threadIdx.x; i < n; i += TB) {
+        const size_t e = ((size_t)b * n + i) * 3;
+        const float g[3] = {dy[e], dy[e + 1], dy[e + 2]};
+        if (dx)
+            for (int j = 0; j < 3; ++j)
+                dx[e + j] = fadd_rn(fadd_rn(fmul_rn(Rb[j], g[0]), fmul_rn(Rb[3 + j], g[1])),
+                                    fmul_rn(Rb[6 + j], g[2]));
+        for (int p = 0; p < 3; ++p) {
+            for (int q = 0; q < 3; ++q) acc[p * 3 + q] += (double)g[p] * (double)xyz[e + q];
+            acc[9 + p] += (double)g[p];
+        }
+    }
+    for (int q = 0; q < 12; ++q) acc[q] = wave_sum_f64(acc[q]);
+    if (lane == 0)
+        for (int q = 0; q < 12; ++q) red[wv][q] = acc[q];
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        const int q = threadIdx.x;
+        const double v = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+        if (q < 9) {
+            if (dR) dR[(size_t)b * 9 + q] = (float)v;
+        } else if (dt) {
+            dt[(size_t)b * 3 + q - 9] = (float)v;
+        }
+    }
+}
+
+// Ro = Ra Rb, to = Ra tb + ta  (T = T_a @ T_b in homogeneous form)
+__global__ void compose_kernel(int nb, const float *__restrict__ Ra, const float *__restrict__ ta,
+                               const float *__restrict__ Rb, const float *__restrict__ tb,
+                               float *__restrict__ Ro, float *__restrict__ to) {
+    GRID_STRIDE(b, (size_t)nb) {
+        const float *A = Ra + b * 9, *B = Rb + b * 9;
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) {
+                float s = 0.f;
+                for (int q = 0; q < 3; ++q) s = fadd_rn(s, fmul_rn(A[i * 3 + q], B[q * 3 + j]));
+                Ro[b * 9 + i * 3 + j] = s;
+            }
+            float s = 0.f;
+            for (int q = 0; q < 3; ++q) s = fadd_rn(s, fmul_rn(A[i * 3 + q], tb[b * 3 + q]));
+            to[b * 3 + i] = fadd_rn(s, ta[b * 3 + i]);
+        }
+    }
+}
+
+// dRa = dRo Rb^T + dto tb^T; dta = dto; dRb = Ra^T dRo; dtb = Ra^T dto
+__global__ void compose_bwd_kernel(int nb, const float *__restrict__ Ra,
+                                   const float *__restrict__ Rb, const float *__restrict__ tb,
+                                   const float *__restrict__ dRo, const float *__restrict__ dto,
+                                   float *__restrict__ dRa, float *__restrict__ dta,
+                                   float *__restrict__ dRb, float *__restrict__ dtb) {
+    GRID_STRIDE(b, (size_t)nb) {
+        const float *A = Ra + b * 9, *B = Rb + b * 9, *G = dRo + b * 9, *g = dto + b * 3;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                float s = fmul_rn(g[i], tb[b * 3 + j]);
+                float u = 0.f;
+                for (int q = 0; q < 3; ++q) {
+                    s = fadd_rn(s, fmul_rn(G[i * 3 + q], B[j * 3 + q]));
+                    u = fadd_rn(u, fmul_rn(A[q * 3 + i], G[q * 3 + j]));
+                }
+                dRa[b * 9 + i * 3 + j] = s;
+                dRb[b * 9 + i * 3 + j] = u;
+            }
+        for (int i = 0; i < 3; ++i) {
+            dta[b * 3 + i] = g[i];
+            float u = 0.f;
+            for (int q = 0; q < 3; ++q) u = fadd_rn(u, fmul_rn(A[q * 3 + i], g[q]));
+            dtb[b * 3 + i] = u;
+        }
+    }
+}
+
+// --------------------------------------------------------- loss backward
+// L = scale * (alpha * mean_b |E_b - I|_F + mean_b |t_b - t_gt,b|), E = R^T R_gt
+__global__ void loss_bwd_kernel(const float *__restrict__ pR, const float *__restrict__ pt,
+                                const float *__restrict__ gR, const float *__restrict__ gt, int nb,
+                                float alpha, float scale, const float *__restrict__ dloss,
+                                float *__restrict__ dR, float *__restrict__ dt) {
+    if (dloss) scale *= dloss[0];
+    GRID_STRIDE(b, (size_t)nb) {
+        const float *R = pR + b * 9, *G = gR + b * 9;
+        float D[3][3];
+        float fro = 0.f;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                float s = 0.f;
+                for (int q = 0; q < 3; ++q) s = fadd_rn(s, fmul_rn(R[q * 3 + i], G[q * 3 + j]));
+                D[i][j] = fsub_rn(s, i == j ? 1.f : 0.f);
+                fro = fadd_rn(fro, fmul_rn(D[i][j], D[i][j]));
+            }
+        fro = sqrtf(fro);
+        const float fR = fro > 0.f ? alpha * scale / (float)nb / fro : 0.f;
+        // dE = fR * D; dR = G dE^T
+        for (int p = 0; p < 3; ++p)
+            for (int q = 0; q < 3; ++q) {
+                float s = 0.f;
+                for (int j = 0; j < 3; ++j) s = fadd_rn(s, fmul_rn(G[p * 3 + j], D[q][j]));
+                dR[b * 9 + p * 3 + q] = fmul_rn(fR, s);
+            }
+        float e[3], n2 = 0.f;
+        for (int q = 0; q < 3; ++q) {
+            e[q] = fsub_rn(pt[b * 3 + q], gt[b * 3 + q]);
+            n2 = fadd_rn(n2, fmul_rn(e[q], e[q]));
+        }
+        const float nr = sqrtf(n2);
+        const float ft = nr > 0.f ? scale / (float)nb / nr : 0.f;
+        for (int q = 0; q < 3; ++q) dt[b * 3 + q] = fmul_rn(ft, e[q]);
+    }
+}
+
+}  // namespace
+
+// ======================================================================= C ABI
+
+extern "C" int hreg_copy_rows(const float *src, int lds, int row_div, int R, int C, float *dst,
+                              int ldd, int accumulate, void *stream) {
+    if (!src || !dst || R < 0 || C < 0 || row_div < 1 || lds < C || ldd < C) return HREG_ERR_INVALID;
+    if (!R || !C) return HREG_OK;
+    hipLaunchKernelGGL(copy_rows_kernel, dim3(g1d((size_t)R * C)), dim3(TB), 0, as_stream(stream),
+                       src, lds, row_div, R, C, dst, ldd, accumulate);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_group_sum(const float *x, int ldx, int G, int k, int C, float *out, int ldo,
+                              int accumulate, void *stream) {
+    if (!x || !out || G < 0 || k < 1 || C < 0 || ldx < C || ldo < C) return HREG_ERR_INVALID;
+    if (!G || !C) return HREG_OK;
+    hipLaunchKernelGGL(group_sum_kernel, dim3(g1d((size_t)G * C)), dim3(TB), 0, as_stream(stream),
+                       x, ldx, G, k, C, out, ldo, accumulate);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_gather_rows(const float *x, int ldx, const int32_t *idx, int M, int C,
+                                float *out, int ldo, void *stream) {
+    if (!x || !idx || !out || M < 0 || C < 0 || ldx < C || ldo < C) return HREG_ERR_INVALID;
+    if (!M || !C) return HREG_OK;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(g1d((size_t)M * C)), dim3(TB), 0,
+                       as_stream(stream), x, ldx, idx, M, C, out, ldo);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_index_offset(const int32_t *idx, int nb, int m, int n, int32_t *out,
+                                 void *stream) {
+    if (!idx || !out || nb < 0 || m < 0 || n < 0) return HREG_ERR_INVALID;
+    if (!nb || !m) return HREG_OK;
+    hipLaunchKernelGGL(index_offset_kernel, dim3(g1d((size_t)nb * m)), dim3(TB), 0,
+                       as_stream(stream), idx, nb, m, n, out);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" size_t hreg_csr_ws_bytes(int M, int n) {
+    if (M < 0 || n < 0) return 0;
+    return ((size_t)(n + 1) + (size_t)M + (size_t)n) * sizeof(int32_t);
+}
+
+extern "C" int hreg_csr_build(const int32_t *idx, int M, int n, void *ws, void *stream) {
+    if (!idx || !ws || M < 0 || n < 1) return HREG_ERR_INVALID;
+    hipStream_t st = as_stream(stream);
+    Csr c = csr_view(ws, M, n);
+    if (hipMemsetAsync(c.cur, 0, (size_t)n * sizeof(int32_t), st) != hipSuccess) return HREG_ERR_LAUNCH;
+    if (M) {
+        hipLaunchKernelGGL(csr_count_kernel, dim3(g1d(M)), dim3(TB), 0, st, idx, M, n, c.cur);
+        HREG_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(csr_scan_kernel, dim3(1), dim3(1024), 0, st, c.cur, n, c.off);
+    HREG_CHECK_LAUNCH();
+    if (hipMemsetAsync(c.cur, 0, (size_t)n * sizeof(int32_t), st) != hipSuccess) return HREG_ERR_LAUNCH;
+    if (M) {
+        hipLaunchKernelGGL(csr_fill_kernel, dim3(g1d(M)), dim3(TB), 0, st, idx, M, n, c.off, c.cur,
+                           c.ent);
+        HREG_CHECK_LAUNCH();
+        hipLaunchKernelGGL(csr_sort_kernel, dim3(g1d(n)), dim3(TB), 0, st, n, c.off, c.ent);
+        HREG_CHECK_LAUNCH();
+    }
+    return HREG_OK;
+}
+
+extern "C" int hreg_scatter_rows(const float *dy, int ldy, const void *ws, int M, int n, int C,
+                                 float *dx, int ldx, int accumulate, void *stream) {
+    if (!dy || !ws || !dx || M < 0 || n < 1 || C < 0 || ldy < C || ldx < C) return HREG_ERR_INVALID;
+    if (!C) return HREG_OK;
+    Csr c = csr_view(const_cast<void *>(ws), M, n);
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3(g1d((size_t)n * C)), dim3(TB), 0,
+                       as_stream(stream), dy, ldy, c.off, c.ent, n, C, dx, ldx, accumulate);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_geom_rows(const float *q, const float *knn_xyz, int G, int k, float *out,
+                              int ldo, void *stream) {
+    if (!q || !knn_xyz || !out || G < 0 || k < 1 || ldo < 4) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    hipLaunchKernelGGL(geom_rows_kernel, dim3(g1d((size_t)G * k)), dim3(TB), 0, as_stream(stream),
+                       q, knn_xyz, G, k, out, ldo);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_geom_rows_bwd(const float *geom, int ldg, const float *dgeom, int lddg,
+                                  const float *dknn_extra, int G, int k, float *dq, float *dknn,
+                                  void *stream) {
+    if (!geom || !dgeom || G < 0 || k < 1 || ldg < 4 || lddg < 4) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    hipLaunchKernelGGL(geom_rows_bwd_kernel, dim3(g1d(G)), dim3(TB), 0, as_stream(stream), geom, ldg,
+                       dgeom, lddg, dknn_extra, G, k, dq, dknn);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_attention_fwd(const float *logits, int ldl, int C, const float *vals, int ldv,
+                                  int Cv, const float *knn_xyz, int G, int k, float *a,
+                                  int32_t *amax, float *kp, float *vmap, int ldm, float *vsum,
+                                  int lds, void *stream) {
+    if (!logits || G < 0 || k < 1 || k > 64 || C < 1 || ldl < C) return HREG_ERR_INVALID;
+    if (vals && (ldv < Cv || Cv < 1)) return HREG_ERR_INVALID;
+    if (kp && !knn_xyz) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    hipLaunchKernelGGL(attention_fwd_kernel, dim3(G), dim3(TB), 0, as_stream(stream), logits, ldl,
+                       C, vals, ldv, Cv, knn_xyz, k, a, amax, kp, vmap, ldm, vsum, lds);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_attention_bwd(const float *logits, int ldl, int C, const float *vals, int ldv,
+                                  int Cv, const float *knn_xyz, int G, int k, const float *a,
+                                  const int32_t *amax, const float *dkp, const float *dvmap,
+                                  int lddm, const float *dvsum, int ldds, int same,
+                                  float *dlogits, int lddl, float *dvals, int lddv, float *dknn,
+                                  void *stream) {
+    if (!logits || !a || !amax || G < 0 || k < 1 || k > 64 || C < 1) return HREG_ERR_INVALID;
+    if (dkp && !knn_xyz) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    hipLaunchKernelGGL(attention_bwd_kernel, dim3(G), dim3(TB), 0, as_stream(stream), logits, ldl,
+                       C, vals, ldv, Cv, knn_xyz, k, a, amax, dkp, dvmap, lddm, dvsum, ldds, same,
+                       dlogits, lddl, dvals, lddv, dknn);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_group_max_arg(const float *x, int ldx, int G, int k, int C, float *out,
+                                  int ldo, int32_t *arg, void *stream) {
+    if (!x || !out || !arg || G < 0 || k < 1 || C < 0 || ldx < C || ldo < C) return HREG_ERR_INVALID;
+    if (!G || !C) return HREG_OK;
+    hipLaunchKernelGGL(group_max_arg_kernel, dim3(g1d((size_t)G * C)), dim3(TB), 0,
+                       as_stream(stream), x, ldx, G, k, C, out, ldo, arg);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_group_max_bwd(const float *dout, int ldd, const int32_t *arg, int G, int k,
+                                  int C, float *dx, int ldx, int accumulate, void *stream) {
+    if (!dout || !arg || !dx || G < 0 || k < 1 || C < 0 || ldd < C || ldx < C) return HREG_ERR_INVALID;
+    if (!G || !C) return HREG_OK;
+    hipLaunchKernelGGL(group_max_bwd_kernel, dim3(g1d((size_t)G * C)), dim3(TB), 0,
+                       as_stream(stream), dout, ldd, arg, G, k, C, dx, ldx, accumulate);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_head_out_bwd(const float *x, int ldx, int C, const float *w3, const float *b3,
+                                 const float *dy, int mode, int G, float *dz, float *dx, int lddx,
+                                 void *stream) {
+    if (!x || !w3 || !b3 || !dy || !dz || !dx || G < 0 || C < 1 || ldx < C || lddx < C)
+        return HREG_ERR_INVALID;
+    if (mode != HREG_HEAD_SOFTPLUS && mode != HREG_HEAD_SIGMOID) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    hipLaunchKernelGGL(head_out_bwd_kernel, dim3((G + 3) / 4), dim3(TB), 0, as_stream(stream), x,
+                       ldx, C, w3, b3, dy, mode, G, dz, dx, lddx);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_sim_stats(const float *S, int nb, int N1, int N2, float *rmax, int32_t *rarg,
+                              float *cmax, int32_t *carg, void *stream) {
+    if (!S || !rmax || !rarg || !cmax || !carg || nb < 0 || N1 < 1 || N2 < 1) return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipLaunchKernelGGL(sim_stats_kernel, dim3(g1d((size_t)nb * (N1 + N2))), dim3(TB), 0,
+                       as_stream(stream), S, nb, N1, N2, rmax, rarg, cmax, carg);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_sim_feats(const float *S, int nb, int N1, int N2, const int32_t *kidx, int k,
+                              const float *rmax, const float *cmax, float *out, int ldo,
+                              void *stream) {
+    if (!S || !kidx || !rmax || !cmax || !out || nb < 0 || N1 < 1 || N2 < 1 || k < 1 || ldo < 2)
+        return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipLaunchKernelGGL(sim_feats_kernel, dim3(g1d((size_t)nb * N1 * k)), dim3(TB), 0,
+                       as_stream(stream), S, nb, N1, N2, kidx, k, rmax, cmax, out, ldo);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" size_t hreg_sim_feats_bwd_ws_bytes(int nb, int N1, int N2) {
+    return ((size_t)2 * nb * N1 * N2 + (size_t)nb * (N1 + N2)) * sizeof(float);
+}
+
+// a [nb][N1][C], b [nb][N2][C] (descriptors), na / nb_ their norms, S the cosine matrix;
+// dout [nb*N1*k][ldd] the gradient of the two sim_feats columns -> da, db (written)
+extern "C" int hreg_sim_feats_bwd(const float *S, const float *a, const float *b, const float *na,
+                                  const float *nb_, int nb, int N1, int N2, int C,
+                                  const int32_t *kidx, int k, const float *rmax,
+                                  const int32_t *rarg, const float *cmax, const int32_t *carg,
+                                  const float *dout, int ldd, void *ws, float *da, float *db,
+                                  void *stream) {
+    if (!S || !a || !b || !na || !nb_ || !kidx || !rmax || !rarg || !cmax || !carg || !dout ||
+        !ws || !da || !db || nb < 0 || N1 < 1 || N2 < 1 || C < 1 || k < 1 || ldd < 2)
+        return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipStream_t st = as_stream(stream);
+    float *dS = (float *)ws;
+    float *dP = dS + (size_t)nb * N1 * N2;
+    float *dna = dP + (size_t)nb * N1 * N2;
+    float *dnb = dna + (size_t)nb * N1;
+    if (hipMemsetAsync(dS, 0, (size_t)nb * N1 * N2 * sizeof(float), st) != hipSuccess)
+        return HREG_ERR_LAUNCH;
+    hipLaunchKernelGGL(sim_bwd_rows_kernel, dim3(g1d((size_t)nb * N1)), dim3(TB), 0, st, S, nb, N1,
+                       N2, kidx, k, rmax, rarg, cmax, dout, ldd, dS);
+    HREG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(sim_bwd_cols_kernel, dim3(g1d((size_t)nb * N2)), dim3(TB), 0, st, S, nb, N1,
+                       N2, kidx, k, cmax, carg, dout, ldd, dS);
+    HREG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(sim_bwd_cos_kernel, dim3(g1d((size_t)nb * (N1 + N2))), dim3(TB), 0, st, S,
+                       dS, nb, N1, N2, na, nb_, dP, dna, dnb);
+    HREG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(sim_bwd_mm_kernel<false>, dim3((C + 63) / 64, (N1 + 63) / 64, nb), dim3(TB),
+                       0, st, dP, N1, N2, b, a, dna, na, C, da);
+    HREG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(sim_bwd_mm_kernel<true>, dim3((C + 63) / 64, (N2 + 63) / 64, nb), dim3(TB),
+                       0, st, dP, N1, N2, a, b, dnb, nb_, C, db);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_weighted_svd_bwd(const float *src, const float *corres, const float *w, int nb,
+                                     int n, const float *dR, const float *dt, float *dsrc,
+                                     float *dcorres, float *dw, void *stream) {
+    if (!src || !corres || !w || !dR || !dt || !dsrc || !dcorres || !dw || nb < 0 || n < 1)
+        return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipLaunchKernelGGL(svd_bwd_kernel, dim3(nb), dim3(TB), 0, as_stream(stream), src, corres, w, n,
+                       dR, dt, dsrc, dcorres, dw);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_transform_points_bwd(const float *xyz, const float *R, int nb, int n,
+                                         const float *dy, float *dxyz, float *dR, float *dt,
+                                         void *stream) {
+    if (!xyz || !R || !dy || nb < 0 || n < 1) return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipLaunchKernelGGL(transform_bwd_kernel, dim3(nb), dim3(TB), 0, as_stream(stream), xyz, R, n, dy,
+                       dxyz, dR, dt);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_compose_se3(int nb, const float *Ra, const float *ta, const float *Rb,
+                                const float *tb, float *Ro, float *to, void *stream) {
+    if (!Ra || !ta || !Rb || !tb || !Ro || !to || nb < 0) return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipLaunchKernelGGL(compose_kernel, dim3(g1d(nb)), dim3(TB), 0, as_stream(stream), nb, Ra, ta, Rb,
+                       tb, Ro, to);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_compose_se3_bwd(int nb, const float *Ra, const float *Rb, const float *tb,
+                                    const float *dRo, const float *dto, float *dRa, float *dta,
+                                    float *dRb, float *dtb, void *stream) {
+    if (!Ra || !Rb || !tb || !dRo || !dto || !dRa || !dta || !dRb || !dtb || nb < 0)
+        return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipLaunchKernelGGL(compose_bwd_kernel, dim3(g1d(nb)), dim3(TB), 0, as_stream(stream), nb, Ra, Rb,
+                       tb, dRo, dto, dRa, dta, dRb, dtb);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_transformation_loss_bwd(const float *pred_R, const float *pred_t,
+                                            const float *gt_R, const float *gt_t, int nb,
+                                            float alpha, float scale, const float *dloss,
+                                            float *dR, float *dt, void *stream) {
+    if (!pred_R || !pred_t || !gt_R || !gt_t || !dR || !dt || nb < 0) return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipLaunchKernelGGL(loss_bwd_kernel, dim3(g1d(nb)), dim3(TB), 0, as_stream(stream), pred_R, pred_t,
+                       gt_R, gt_t, nb, alpha, scale, dloss, dR, dt);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}

@@ -9,8 +9,8 @@ keys as the reference (models/HRegNet/models.py:7-75, layers.py:89-504), so
 The parameters are plain nn.Conv/BatchNorm modules (they are the checkpoint
 format); the forward itself runs on the gfx950 HIP library through
 :mod:`pcd_reg_hregnet_amd.engine` -- BatchNorm in eval mode.  The training
-forward (batch-statistics BN + backward kernels) is SURVEY.md 8f row 1 and is
-not implemented yet: calling forward in train mode raises.
+forward (``HRegNet`` in .train()) runs pcd_reg_hregnet_amd.train_graph: train-mode
+BatchNorm and a backward made of HIP kernels.
 """
 from __future__ import annotations
 
@@ -219,9 +219,9 @@ class HRegNet(nn.Module):
 
     def forward(self, src_points, dst_points):
         if self.training:
-            raise NotImplementedError(
-                "train-mode forward (batch-statistics BN + backward kernels) is not implemented "
-                "on the HIP path yet; call .eval()")
+            # batch-statistics BN + backward kernels (train_graph.py, csrc/train_ops.hip)
+            from . import train_graph
+            return train_graph.hregnet_train_forward(self, src_points, dst_points)
         if not self.feature_extraction.use_fps:
             raise NotImplementedError("use_fps=False (random sampling) is not implemented")
         dev = src_points.device

@@ -1,0 +1,721 @@
+"""HRegNet training forward (train-mode BatchNorm) with its backward on the HIP library.
+
+The reference trains ``HRegNet`` (models/HRegNet/models.py:77-148 with every
+BatchNorm in .train(), train/train_reg_v0.py:241-296) through PyTorch autograd.
+Here the same graph is built from ``torch.autograd.Function`` objects whose forward
+and backward are C-ABI launches (csrc/train_ops.hip, csrc/train.hip, csrc/gemm.hip):
+torch keeps the autograd tape, allocates memory and adds the gradients of tensors
+used twice; every arithmetic op on the path runs in libhregnet_amd.so.
+
+Layer structure follows the reference exactly, because train-mode BN needs the
+batch statistics of every conv output before the next layer (the eval-mode fused
+kernels of engine.py fold BN and cannot be used): conv -> BN(batch stats) -> ReLU
+per layer (train.conv_bn_act), the reference's concatenations materialised as
+row blocks, and each knn_gather / gather_operation a differentiable row gather whose
+backward is a deterministic scatter (ascending destination order).
+
+As in the reference, feature_extraction runs separately on src and dst (BN
+statistics and running-stat updates per call, models.py:79-80) and so does the
+CoarseReg neighbour branch (convs_2 on src, then dst: layers.py:334-343).
+Index selections (FPS/WFPS, every kNN) are not differentiable (models/utils.py:33,
+57; pytorch3d's knn_points indices) and run on the eval kernels; an ``IndexHook``
+can record them or substitute given ones (parity tests pin the graph on the
+reference's own selections).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib, engine, train
+from ._lib import call
+
+_f32 = torch.float32
+
+
+def _stream():
+    return _lib.stream_handle()
+
+
+def _empty(*shape, dtype=_f32, device):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+# ------------------------------------------------------------------ index maps
+
+class IndexMap:
+    """A gather index (global rows of a [n][C] source) plus its inverse, built on
+    first use by a backward and shared by every gather through the same index."""
+
+    def __init__(self, idx: torch.Tensor, n: int):
+        assert idx.dtype == torch.int32 and idx.is_contiguous()
+        self.idx = idx
+        self.M = idx.numel()
+        self.n = int(n)
+        self._ws = None
+
+    def csr(self):
+        if self._ws is None:
+            nbytes = _lib.load().hreg_csr_ws_bytes(self.M, self.n)
+            self._ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.idx.device)
+            call("hreg_csr_build", self.idx, self.M, self.n, self._ws, _stream())
+        return self._ws
+
+
+def offset_index(local: torch.Tensor, n: int) -> torch.Tensor:
+    """[nb, m(, k)] per-cloud indices -> flat int32 global rows of the [nb*n] stack."""
+    local = local.to(torch.int32).contiguous()
+    nb = local.shape[0]
+    m = local.numel() // max(nb, 1)
+    out = torch.empty(local.numel(), dtype=torch.int32, device=local.device)
+    call("hreg_index_offset", local, nb, m, n, out, _stream())
+    return out
+
+
+class IndexHook:
+    """Records every index selection of a training forward (``record``) and/or
+    replaces it (``inject``: name -> per-cloud indices [nb, m(, k)], as the reference's
+    fps / knn_points calls return them)."""
+
+    def __init__(self, inject: dict | None = None):
+        self.inject = dict(inject or {})
+        self.record = {}
+
+    def __call__(self, name, local_fn, n, device):
+        if name in self.inject:
+            loc = torch.as_tensor(self.inject[name]).to(device=device, dtype=torch.int32)
+        else:
+            loc = local_fn()
+        self.record[name] = loc
+        return loc
+
+    def record_global(self, name, gidx, nb, n):
+        """record global rows as per-cloud indices [nb, m, ...] (test bookkeeping)"""
+        g = gidx.view(nb, -1).to(torch.int64)
+        off = torch.arange(nb, device=g.device, dtype=torch.int64)[:, None] * n
+        self.record[name] = (g - off).to(torch.int32)
+
+
+def _select(hook, name, local_fn, n, device):
+    """-> (local [nb, m(, k)] int32, IndexMap over global rows)."""
+    loc = hook(name, local_fn, n, device) if hook is not None else local_fn()
+    return loc, IndexMap(offset_index(loc, n), loc.shape[0] * n)
+
+
+# ------------------------------------------------------------ autograd functions
+
+class _GatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, imap: IndexMap):
+        n, C = x.shape
+        out = _empty(imap.M, C, device=x.device)
+        call("hreg_gather_rows", x, C, imap.idx, imap.M, C, out, C, _stream())
+        ctx.imap = imap
+        ctx.C = C
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        imap = ctx.imap
+        dout = dout.contiguous()
+        dx = _empty(imap.n, ctx.C, device=dout.device)
+        call("hreg_scatter_rows", dout, ctx.C, imap.csr(), imap.M, imap.n, ctx.C, dx, ctx.C, 0,
+             _stream())
+        return dx, None
+
+
+def gather_rows(x, imap: IndexMap):
+    """out[m] = x[idx[m]] (knn_gather / gather_operation), x [n][C]."""
+    return _GatherRows.apply(x.contiguous(), imap)
+
+
+class _GeomRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, kx, k):
+        G = q.shape[0]
+        out = _empty(G * k, 4, device=q.device)
+        call("hreg_geom_rows", q, kx, G, k, out, 4, _stream())
+        ctx.save_for_backward(out)
+        ctx.k = k
+        return out
+
+    @staticmethod
+    def backward(ctx, dgeom):
+        (geom,) = ctx.saved_tensors
+        k = ctx.k
+        G = geom.shape[0] // k
+        dgeom = dgeom.contiguous()
+        dq = _empty(G, 3, device=geom.device) if ctx.needs_input_grad[0] else None
+        dkx = _empty(G * k, 3, device=geom.device) if ctx.needs_input_grad[1] else None
+        call("hreg_geom_rows_bwd", geom, 4, dgeom, 4, None, G, k, dq, dkx, _stream())
+        return dq, dkx, None
+
+
+def geom_rows(q, kx, k):
+    """[knn_xyz - q, |knn_xyz - q|] per neighbour row (layers.py:21-23)."""
+    return _GeomRows.apply(q.contiguous(), kx.contiguous(), k)
+
+
+class _CatRows(torch.autograd.Function):
+    """torch.cat over channels of row blocks; an input with repeat k is one row per
+    group of k output rows (the reference's unsqueeze(2).repeat(1,1,k,1))."""
+
+    @staticmethod
+    def forward(ctx, reps, *xs):
+        R = None
+        for x, r in zip(xs, reps):
+            rows = x.shape[0] * r
+            assert R is None or rows == R, "row counts of the concatenated blocks differ"
+            R = rows
+        Ct = sum(x.shape[1] for x in xs)
+        out = _empty(R, Ct, device=xs[0].device)
+        c0 = 0
+        for x, r in zip(xs, reps):
+            C = x.shape[1]
+            call("hreg_copy_rows", x, C, r, R, C, out[:, c0:], Ct, 0, _stream())
+            c0 += C
+        ctx.reps = reps
+        ctx.widths = [x.shape[1] for x in xs]
+        ctx.R = R
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = dout.contiguous()
+        Ct = dout.shape[1]
+        grads = []
+        c0 = 0
+        for i, (C, r) in enumerate(zip(ctx.widths, ctx.reps)):
+            if not ctx.needs_input_grad[1 + i]:
+                grads.append(None)
+            elif r == 1:
+                g = _empty(ctx.R, C, device=dout.device)
+                call("hreg_copy_rows", dout[:, c0:], Ct, 1, ctx.R, C, g, C, 0, _stream())
+                grads.append(g)
+            else:
+                g = _empty(ctx.R // r, C, device=dout.device)
+                call("hreg_group_sum", dout[:, c0:], Ct, ctx.R // r, r, C, g, C, 0, _stream())
+                grads.append(g)
+            c0 += C
+        return (None, *grads)
+
+
+def cat_rows(*blocks):
+    """blocks: tensors [R][C] or (tensor [G][C], k) repeated over k consecutive rows."""
+    xs, reps = [], []
+    for b in blocks:
+        if isinstance(b, tuple):
+            xs.append(b[0].contiguous())
+            reps.append(int(b[1]))
+        else:
+            xs.append(b.contiguous())
+            reps.append(1)
+    return _CatRows.apply(tuple(reps), *xs)
+
+
+class _Attention(torch.autograd.Function):
+    """a = softmax_k(max_C logits); kp = sum_k a * knn_xyz; vmap = vals * a;
+    vsum = sum_k vmap (layers.py:151-159 / 340-343 / 384-388 / 447-450)."""
+
+    @staticmethod
+    def forward(ctx, logits, vals, kx, k, same, want_map, want_sum):
+        R, C = logits.shape
+        G = R // k
+        dev = logits.device
+        v = logits if same else vals
+        Cv = v.shape[1] if v is not None else 0
+        a = _empty(R, device=dev)
+        amax = _empty(R, dtype=torch.int32, device=dev)
+        kp = _empty(G, 3, device=dev) if kx is not None else None
+        vmap = _empty(R, Cv, device=dev) if (want_map and v is not None) else None
+        vsum = _empty(G, Cv, device=dev) if (want_sum and v is not None) else None
+        call("hreg_attention_fwd", logits, C, C, v, Cv, Cv, kx, G, k, a, amax, kp, vmap, Cv,
+             vsum, Cv, _stream())
+        ctx.save_for_backward(logits, vals, kx, a, amax)
+        ctx.k, ctx.same = k, same
+        ctx.set_materialize_grads(False)
+        return kp, vmap, vsum
+
+    @staticmethod
+    def backward(ctx, dkp, dvmap, dvsum):
+        logits, vals, kx, a, amax = ctx.saved_tensors
+        k, same = ctx.k, ctx.same
+        R, C = logits.shape
+        G = R // k
+        dev = logits.device
+        v = logits if same else vals
+        Cv = v.shape[1] if v is not None else 0
+        dkp = dkp.contiguous() if dkp is not None else None
+        dvmap = dvmap.contiguous() if dvmap is not None else None
+        dvsum = dvsum.contiguous() if dvsum is not None else None
+        dlogits = _empty(R, C, device=dev)
+        dvals = _empty(R, Cv, device=dev) if (not same and vals is not None and
+                                              ctx.needs_input_grad[1]) else None
+        dkx = _empty(R, 3, device=dev) if (kx is not None and dkp is not None and
+                                           ctx.needs_input_grad[2]) else None
+        if dvals is not None and dvmap is None and dvsum is None:
+            dvals.zero_()
+        call("hreg_attention_bwd", logits, C, C, v, Cv, Cv, kx, G, k, a, amax, dkp, dvmap, Cv,
+             dvsum, Cv, 1 if same else 0, dlogits, C, dvals, Cv, dkx, _stream())
+        return dlogits, dvals, dkx, None, None, None, None
+
+
+def attention(logits, k, vals=None, kx=None, want_map=False, want_sum=False):
+    """-> (kp [G][3] | None, vmap [R][Cv] | None, vsum [G][Cv] | None); vals=None means
+    the attention weights multiply the logits themselves."""
+    same = vals is None
+    return _Attention.apply(logits.contiguous(), None if same else vals.contiguous(),
+                            None if kx is None else kx.contiguous(), k, same, want_map,
+                            want_sum)
+
+
+class _GroupMax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        R, C = x.shape
+        G = R // k
+        out = _empty(G, C, device=x.device)
+        arg = _empty(G, C, dtype=torch.int32, device=x.device)
+        call("hreg_group_max_arg", x, C, G, k, C, out, C, arg, _stream())
+        ctx.save_for_backward(arg)
+        ctx.k, ctx.R = k, R
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (arg,) = ctx.saved_tensors
+        dout = dout.contiguous()
+        G, C = dout.shape
+        dx = _empty(ctx.R, C, device=dout.device)
+        call("hreg_group_max_bwd", dout, C, arg, G, ctx.k, C, dx, C, 0, _stream())
+        return dx, None
+
+
+def group_max(x, k):
+    """torch.max over each group of k rows (layers.py:202, 208)."""
+    return _GroupMax.apply(x.contiguous(), k)
+
+
+class _HeadOut(torch.autograd.Function):
+    """mlp3 (Conv1d C->1) + softplus + 0.001 (layers.py:161-163) or sigmoid
+    (layers.py:393-394, 451-452); optionally the next level's WFPS weights
+    (1/(sigma+1e-5))/mean (models.py:30-32) as a non-differentiable output."""
+
+    @staticmethod
+    def forward(ctx, x, w3, b3, mode, nclouds, rows, want_weights):
+        G, C = x.shape
+        out = _empty(G, device=x.device)
+        wout = _empty(G, device=x.device) if want_weights else None
+        call("hreg_head_out", x, C, C, nclouds, rows, w3, b3, mode, out, wout, _stream())
+        ctx.save_for_backward(x, w3, b3)
+        ctx.mode = mode
+        if wout is not None:
+            ctx.mark_non_differentiable(wout)
+        return out, wout
+
+    @staticmethod
+    def backward(ctx, dy, _dw):
+        x, w3, b3 = ctx.saved_tensors
+        G, C = x.shape
+        dev = x.device
+        dy = dy.contiguous()
+        dz = _empty(G, 1, device=dev)
+        dx = _empty(G, C, device=dev)
+        call("hreg_head_out_bwd", x, C, C, w3, b3, dy, ctx.mode, G, dz, dx, C, _stream())
+        dw = train.gemm_tn(dz, x).view(-1) if ctx.needs_input_grad[1] else None
+        db = train.col_sum(dz) if ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None, None
+
+
+def head_out(x, conv, mode, nclouds=1, rows=None, want_weights=False):
+    C = x.shape[1]
+    w3 = conv.weight.view(C)
+    return _HeadOut.apply(x.contiguous(), w3, conv.bias, mode, nclouds,
+                          rows if rows is not None else x.shape[0], want_weights)
+
+
+class _SimFeats(torch.autograd.Function):
+    """[src_dst_cos, dst_src_cos] gathered at the descriptor kNN (layers.py:290-313)."""
+
+    @staticmethod
+    def forward(ctx, a, b, kidx, nb, N1, N2):
+        C = a.shape[1]
+        dev = a.device
+        k = kidx.shape[-1]
+        na = _empty(nb * N1, device=dev)
+        nbv = _empty(nb * N2, device=dev)
+        call("hreg_row_norms", a, nb * N1, C, C, na, _stream())
+        call("hreg_row_norms", b, nb * N2, C, C, nbv, _stream())
+        S = _empty(nb, N1, N2, device=dev)
+        engine.cosine_gemm(a, b, na, nbv, nb, N1, N2, C, S)
+        rmax = _empty(nb * N1, device=dev)
+        rarg = _empty(nb * N1, dtype=torch.int32, device=dev)
+        cmax = _empty(nb * N2, device=dev)
+        carg = _empty(nb * N2, dtype=torch.int32, device=dev)
+        call("hreg_sim_stats", S, nb, N1, N2, rmax, rarg, cmax, carg, _stream())
+        out = _empty(nb * N1 * k, 2, device=dev)
+        call("hreg_sim_feats", S, nb, N1, N2, kidx, k, rmax, cmax, out, 2, _stream())
+        ctx.save_for_backward(a, b, kidx, na, nbv, S, rmax, rarg, cmax, carg)
+        ctx.dims = (nb, N1, N2, C, k)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        a, b, kidx, na, nbv, S, rmax, rarg, cmax, carg = ctx.saved_tensors
+        nb, N1, N2, C, k = ctx.dims
+        dev = a.device
+        ws = torch.empty(_lib.load().hreg_sim_feats_bwd_ws_bytes(nb, N1, N2), dtype=torch.uint8,
+                         device=dev)
+        da = _empty(nb * N1, C, device=dev)
+        db = _empty(nb * N2, C, device=dev)
+        call("hreg_sim_feats_bwd", S, a, b, na, nbv, nb, N1, N2, C, kidx, k, rmax, rarg, cmax,
+             carg, dout.contiguous(), 2, ws, da, db, _stream())
+        return da, db, None, None, None, None
+
+
+def sim_feats(a, b, kidx, nb, N1, N2):
+    return _SimFeats.apply(a.contiguous(), b.contiguous(), kidx.contiguous(), nb, N1, N2)
+
+
+class _WeightedSVD(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, corres, w):
+        B, n, _ = src.shape
+        _, _, R, t = engine.weighted_svd(src, corres, w)
+        ctx.save_for_backward(src, corres, w)
+        return R, t
+
+    @staticmethod
+    def backward(ctx, dR, dt):
+        src, corres, w = ctx.saved_tensors
+        B, n, _ = src.shape
+        dev = src.device
+        dR = torch.zeros(B, 3, 3, device=dev) if dR is None else dR.contiguous()
+        dt = torch.zeros(B, 3, device=dev) if dt is None else dt.contiguous()
+        ds = torch.empty_like(src)
+        dc = torch.empty_like(corres)
+        dw = torch.empty_like(w)
+        call("hreg_weighted_svd_bwd", src, corres, w, B, n, dR, dt, ds, dc, dw, _stream())
+        return ds, dc, dw
+
+
+def weighted_svd(src, corres, w):
+    """WeightedSVDHead (layers.py:469-504): (R [B,3,3], t [B,3])."""
+    return _WeightedSVD.apply(src.contiguous(), corres.contiguous(), w.contiguous())
+
+
+class _Transform(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xyz, R, t):
+        B, n, _ = xyz.shape
+        out = torch.empty_like(xyz)
+        call("hreg_transform_points", xyz, R, t, B, n, out, _stream())
+        ctx.save_for_backward(xyz, R)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        xyz, R = ctx.saved_tensors
+        B, n, _ = xyz.shape
+        dev = xyz.device
+        dx = torch.empty_like(xyz) if ctx.needs_input_grad[0] else None
+        dR = _empty(B, 3, 3, device=dev)
+        dt = _empty(B, 3, device=dev)
+        call("hreg_transform_points_bwd", xyz, R, B, n, dy.contiguous(), dx, dR, dt, _stream())
+        return dx, dR, dt
+
+
+def transform(xyz, R, t):
+    """R xyz^T + t (models.py:91-92, 113-114)."""
+    return _Transform.apply(xyz.contiguous(), R.contiguous(), t.contiguous())
+
+
+class _Compose(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Ra, ta, Rb, tb):
+        B = Ra.shape[0]
+        Ro = torch.empty_like(Ra)
+        to = torch.empty_like(ta)
+        call("hreg_compose_se3", B, Ra, ta, Rb, tb, Ro, to, _stream())
+        ctx.save_for_backward(Ra, Rb, tb)
+        return Ro, to
+
+    @staticmethod
+    def backward(ctx, dRo, dto):
+        Ra, Rb, tb = ctx.saved_tensors
+        B = Ra.shape[0]
+        dev = Ra.device
+        dRo = torch.zeros(B, 3, 3, device=dev) if dRo is None else dRo.contiguous()
+        dto = torch.zeros(B, 3, device=dev) if dto is None else dto.contiguous()
+        dRa, dRb = torch.empty_like(Ra), torch.empty_like(Rb)
+        dta, dtb = _empty(B, 3, device=dev), torch.empty_like(tb)
+        call("hreg_compose_se3_bwd", B, Ra, Rb, tb, dRo, dto, dRa, dta, dRb, dtb, _stream())
+        return dRa, dta, dRb, dtb
+
+
+def compose(Ra, ta, Rb, tb):
+    """T = T_a @ T_b (models.py:100-110): (Ra Rb, Ra tb + ta)."""
+    return _Compose.apply(Ra.contiguous(), ta.contiguous(), Rb.contiguous(), tb.contiguous())
+
+
+class _TransformationLoss(torch.autograd.Function):
+    """transformation_loss(...)[0] = alpha * mean |R^T R_gt - I|_F + mean |t - t_gt|
+    (losses/losses.py:117-160); also returns (loss_R, loss_t) without gradient."""
+
+    @staticmethod
+    def forward(ctx, R, t, gR, gt, alpha):
+        B = R.shape[0]
+        dev = R.device
+        scal = _empty(3, device=dev)
+        R_err = _empty(3, device=dev)
+        T_err = _empty(3, device=dev)
+        call("hreg_transformation_loss", R, t, gR, gt, B, float(alpha), scal, R_err, T_err, None,
+             None, _stream())
+        ctx.save_for_backward(R, t, gR, gt)
+        ctx.alpha = float(alpha)
+        parts = scal[1:].clone()
+        ctx.mark_non_differentiable(parts)
+        return scal[0].clone(), parts
+
+    @staticmethod
+    def backward(ctx, dloss, _dparts):
+        R, t, gR, gt = ctx.saved_tensors
+        B = R.shape[0]
+        dR = torch.empty_like(R)
+        dt = torch.empty_like(t)
+        call("hreg_transformation_loss_bwd", R, t, gR, gt, B, ctx.alpha, 1.0,
+             dloss.contiguous().view(1), dR, dt, _stream())
+        return dR, dt, None, None, None
+
+
+def transformation_loss(R, t, gR, gt, alpha=1.0):
+    """-> (loss, [loss_R, loss_t]) with loss differentiable in R and t."""
+    return _TransformationLoss.apply(R.contiguous(), t.contiguous(), gR.contiguous(),
+                                     gt.contiguous(), alpha)
+
+
+# ------------------------------------------------------------------ modules
+
+def conv_bn(x, conv, bn, relu=True):
+    """Conv(1x1) + train-mode BatchNorm (+ ReLU) over rows (num_batches_tracked += 1)."""
+    W = conv.weight.view(conv.out_channels, -1)
+    y = train.conv_bn_act(x, W, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                          relu, momentum=bn.momentum, eps=bn.eps)
+    if bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return y
+
+
+def seq_convs(x, seq):
+    """nn.Sequential of [Conv, BN, ReLU] * n."""
+    mods = list(seq)
+    for i in range(0, len(mods), 3):
+        x = conv_bn(x, mods[i], mods[i + 1], relu=True)
+    return x
+
+
+def _mlp_head(x, head_mods, mode, nclouds, rows, want_weights=False):
+    m1, m2, m3 = head_mods
+    s = conv_bn(x, m1[0], m1[1])
+    s = conv_bn(s, m2[0], m2[1])
+    return head_out(s, m3[0], mode, nclouds, rows, want_weights)
+
+
+def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src"):
+    """KeypointDetector.forward + DescExtractor.forward (layers.py:134-209), train mode.
+
+    xyz [nb,n,3] (requires grad above level 1), feats [nb*n][Cf] or None, weights [nb*n]
+    (WFPS, no gradient) or None.  -> keypoints [nb,M,3], sigmas [nb*M], att_feat
+    [nb*M][C], desc [nb*M][Cd], next weights [nb*M] (no gradient)."""
+    M, k = engine.LEVELS[lvl][:2]
+    nb, n, _ = xyz.shape
+    dev = xyz.device
+    G = nb * M
+    xyz_flat = xyz.reshape(nb * n, 3)
+    with torch.no_grad():
+        xd = xyz.detach().contiguous()
+        wd = None if weights is None else weights.detach().view(nb, n).contiguous()
+        grouped = []
+
+        def fps_local():
+            grouped.append(engine.grouping(xd, lvl, wd))  # FPS/WFPS + kNN grouping
+            return grouped[0][0]
+
+        fps_loc, fps_map = _select(hook, f"{part}_fps_{lvl + 1}", fps_local, n, dev)
+        knn_name = f"{part}_knn_{lvl + 1}"
+        if grouped and not (hook is not None and knn_name in hook.inject):
+            kmap = IndexMap(grouped[0][2].contiguous(), nb * n)  # global rows
+            if hook is not None:
+                hook.record_global(knn_name, kmap.idx, nb, n)
+        else:
+            q_sel = _empty(nb, M, 3, device=dev)
+            call("hreg_gather_rows", xd.view(nb * n, 3), 3, fps_map.idx, G, 3, q_sel, 3,
+                 _stream())
+            _, kmap = _select(hook, knn_name, lambda: engine.knn_idx32(q_sel, xd, k), n, dev)
+    # differentiable recomputation of the grouped rows (layers.py:19-27, 139-149)
+    q = gather_rows(xyz_flat, fps_map)                  # sampled_xyz [G][3]
+    kx = gather_rows(xyz_flat, kmap)                    # knn_xyz [R][3]
+    geom = geom_rows(q, kx, k)                          # [rela, dist]
+    if feats is not None:
+        grouped_rows = cat_rows(geom, gather_rows(feats, kmap))
+    else:
+        grouped_rows = geom
+    # detector (layers.py:150-165)
+    emb = seq_convs(grouped_rows, det.convs)
+    kp, att_map, att_feat = attention(emb, k, kx=kx, want_map=True, want_sum=True)
+    sig, wnext = _mlp_head(att_feat, (det.mlp1, det.mlp2, det.mlp3), _lib.HREG_HEAD_SOFTPLUS,
+                           nb, M, want_weights=True)
+    # descriptor (layers.py:200-209)
+    x1 = seq_convs(grouped_rows, desc.convs)
+    x2 = group_max(x1, k)
+    y = cat_rows((x2, k), x1, att_map)
+    y = conv_bn(y, desc.mlp1[0], desc.mlp1[1])
+    y = conv_bn(y, desc.mlp2[0], desc.mlp2[1])
+    d = group_max(y, k)
+    return kp.view(nb, M, 3), sig, att_feat, d, wnext, fps_loc
+
+
+def feature_extraction(fe, points, hook=None, part="src"):
+    """HierFeatureExtraction.forward (models.py:26-58) in train mode."""
+    dets = (fe.detector_1, fe.detector_2, fe.detector_3)
+    descs = (fe.desc_extractor_1, fe.desc_extractor_2, fe.desc_extractor_3)
+    out = {}
+    xyz, feats, w = points, None, None
+    for lvl in range(3):
+        kp, sig, att, d, wnext, fps_loc = keypoint_level(dets[lvl], descs[lvl], lvl, xyz, feats,
+                                                         w, hook, part)
+        M = engine.LEVELS[lvl][0]
+        nb = points.shape[0]
+        out[f"xyz_{lvl + 1}"] = kp
+        out[f"sigmas_{lvl + 1}"] = sig.view(nb, M)
+        out[f"desc_{lvl + 1}"] = d  # [nb*M][C] point-major
+        out[f"fps_idx_{lvl + 1}"] = fps_loc
+        xyz, feats = kp, att
+        w = wnext if fe.use_weights else None
+    return out
+
+
+def _knn_local(hook, name, p1, p2, k, dev):
+    loc = hook(name, lambda: engine.knn_idx32(p1, p2, k), p2.shape[1], dev) if hook is not None \
+        else engine.knn_idx32(p1, p2, k)
+    return loc
+
+
+def _nbr_desc(convs_2, xyz, desc, k, hook, name):
+    """Neighbour-aware descriptor of one cloud set (layers.py:315-343)."""
+    nb, N, _ = xyz.shape
+    dev = xyz.device
+    with torch.no_grad():
+        xd = xyz.detach().contiguous()
+        loc = _knn_local(hook, name, xd, xd, k, dev)
+        imap = IndexMap(offset_index(loc, N), nb * N)
+    xyz_flat = xyz.reshape(nb * N, 3)
+    kfeat = gather_rows(desc, imap)                        # src_nbr_knn_feats
+    kx = gather_rows(xyz_flat, imap)
+    rows = cat_rows(kfeat, geom_rows(xyz_flat, kx, k))     # [knn_feats, rela, dist]
+    h = seq_convs(rows, convs_2)
+    _, _, nbr = attention(h, k, vals=kfeat, want_sum=True)
+    return nbr
+
+
+def coarse_reg(m, s_xyz, s_desc, d_xyz, d_desc, s_w, d_w, hook=None):
+    """CoarseReg.forward (layers.py:273-396), train mode.  xyz [B,N,3], desc [B*N][C]
+    point-major, w [B*N] (the sigmas, models.py:84-85)."""
+    k = m.k
+    B, N1, _ = s_xyz.shape
+    N2 = d_xyz.shape[1]
+    C = s_desc.shape[1]
+    dev = s_xyz.device
+    with torch.no_grad():
+        kidx = _knn_local(hook, "coarse_desc_knn", s_desc.detach().view(B, N1, C),
+                          d_desc.detach().view(B, N2, C), k, dev)
+        kmap = IndexMap(offset_index(kidx, N2), B * N2)
+    s_flat = s_xyz.reshape(B * N1, 3)
+    kx = gather_rows(d_xyz.reshape(B * N2, 3), kmap)                # src_knn_xyz
+    geom = geom_rows(s_flat, kx, k)                                 # rela, dist
+    kdesc = gather_rows(d_desc, kmap)                               # src_knn_desc
+    kw = gather_rows(d_w.reshape(B * N2, 1), kmap)                  # src_knn_weights
+    sims_a = sim_feats(s_desc, d_desc, kidx, B, N1, N2)             # original similarity
+    nbr_s = _nbr_desc(m.convs_2, s_xyz, s_desc, k, hook, "coarse_nbr_src")
+    nbr_d = _nbr_desc(m.convs_2, d_xyz, d_desc, k, hook, "coarse_nbr_dst")
+    sims_b = sim_feats(nbr_s, nbr_d, kidx, B, N1, N2)               # neighbour-aware
+    feats = cat_rows(geom, (s_flat, k), kx, (s_desc, k), kdesc, (s_w.reshape(B * N1, 1), k), kw,
+                     sims_a, sims_b)
+    f = seq_convs(feats, m.convs_1)
+    corres, _, att = attention(f, k, kx=kx, want_sum=True)
+    w, _ = _mlp_head(att, (m.mlp1, m.mlp2, m.mlp3), _lib.HREG_HEAD_SIGMOID, 1, B * N1)
+    return corres.view(B, N1, 3), w.view(B, N1)
+
+
+def fine_reg(m, s_xyz, s_feat, d_xyz, d_feat, s_w, d_w, hook=None, name="fine"):
+    """FineReg.forward (layers.py:433-454), train mode."""
+    k = m.k
+    B, N1, _ = s_xyz.shape
+    N2 = d_xyz.shape[1]
+    dev = s_xyz.device
+    with torch.no_grad():
+        kidx = _knn_local(hook, name + "_knn", s_xyz.detach().contiguous(),
+                          d_xyz.detach().contiguous(), k, dev)
+        kmap = IndexMap(offset_index(kidx, N2), B * N2)
+    s_flat = s_xyz.reshape(B * N1, 3)
+    kx = gather_rows(d_xyz.reshape(B * N2, 3), kmap)
+    geom = geom_rows(s_flat, kx, k)
+    kf = gather_rows(d_feat, kmap)
+    kw = gather_rows(d_w.reshape(B * N2, 1), kmap)
+    feats = cat_rows(geom, (s_flat, k), kx, (s_feat, k), kf, (s_w.reshape(B * N1, 1), k), kw)
+    f = seq_convs(feats, m.convs_1)
+    corres, _, att = attention(f, k, kx=kx, want_sum=True)
+    w, _ = _mlp_head(att, (m.mlp1, m.mlp2, m.mlp3), _lib.HREG_HEAD_SIGMOID, 1, B * N1)
+    return corres.view(B, N1, 3), w.view(B, N1)
+
+
+def hregnet_train_forward(net, src, dst, hook=None):
+    """HRegNet.forward (models/HRegNet/models.py:77-148) in train mode -> the reference's
+    result dict; differentiable in every parameter that requires grad."""
+    fe = net.feature_extraction
+    if not fe.use_fps:
+        raise NotImplementedError("use_fps=False (random sampling) is not implemented")
+    src = src.float().contiguous()
+    dst = dst.float().contiguous()
+    B = src.shape[0]
+    sf = feature_extraction(fe, src, hook, "src")
+    df = feature_extraction(fe, dst, hook, "dst")
+    c3, w3 = coarse_reg(net.coarse_corres, sf["xyz_3"], sf["desc_3"], df["xyz_3"], df["desc_3"],
+                        sf["sigmas_3"], df["sigmas_3"], hook)
+    R3, t3 = weighted_svd(sf["xyz_3"], c3, w3)
+    x2t = transform(sf["xyz_2"], R3, t3)
+    c2, w2 = fine_reg(net.fine_corres_2, x2t, sf["desc_2"], df["xyz_2"], df["desc_2"],
+                      sf["sigmas_2"], df["sigmas_2"], hook, "fine2")
+    R2_, t2_ = weighted_svd(x2t, c2, w2)
+    R2, t2 = compose(R2_, t2_, R3, t3)
+    x1t = transform(sf["xyz_1"], R2, t2)
+    c1, w1 = fine_reg(net.fine_corres_1, x1t, sf["desc_1"], df["xyz_1"], df["desc_1"],
+                      sf["sigmas_1"], df["sigmas_1"], hook, "fine1")
+    R1_, t1_ = weighted_svd(x1t, c1, w1)
+    R1, t1 = compose(R1_, t1_, R2, t2)
+
+    def feats(f):
+        d = {}
+        for i, m in enumerate((1024, 512, 256)):
+            d[f"xyz_{i + 1}"] = f[f"xyz_{i + 1}"]
+            d[f"sigmas_{i + 1}"] = f[f"sigmas_{i + 1}"]
+            d[f"desc_{i + 1}"] = f[f"desc_{i + 1}"].view(B, m, -1).transpose(1, 2)
+        return d
+
+    return {
+        "src_xyz_corres_3": c3, "src_xyz_corres_2": c2, "src_xyz_corres_1": c1,
+        "src_dst_weights_3": w3, "src_dst_weights_2": w2, "src_dst_weights_1": w1,
+        "rotation": [R3, R2, R1], "translation": [t3, t2, t1],
+        "src_feats": feats(sf), "dst_feats": feats(df),
+    }
+
+
+def registration_loss(ret, gt_R, gt_t, alpha=1.0):
+    """train_reg_v0.py:280-294: l_trans = mean over the 3 levels of transformation_loss;
+    -> (loss, l_R, l_t) with loss differentiable."""
+    losses, lr, lt = [], [], []
+    for R, t in zip(ret["rotation"], ret["translation"]):
+        l, parts = transformation_loss(R, t, gt_R, gt_t, alpha)
+        losses.append(l)
+        lr.append(parts[0])
+        lt.append(parts[1])
+    return torch.stack(losses).sum() / 3.0, torch.stack(lr).sum() / 3.0, torch.stack(lt).sum() / 3.0

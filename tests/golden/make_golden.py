@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py [--v2-only | --loss-only]   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -92,7 +92,18 @@ def fps_literal(xyz: np.ndarray, m: int, w: np.ndarray | None = None) -> np.ndar
 class _PointUtils(types.ModuleType):
     calls: list
 
+    replay: list | None = None
+
+    def _replayed(self, kind, idx):
+        if self.replay is None:
+            return False
+        idx.copy_(self.replay.pop(0))
+        self.calls.append((kind, idx.clone()))
+        return True
+
     def furthest_point_sampling_wrapper(self, b, n, m, points, temp, idx):
+        if self._replayed("fps", idx):
+            return 1
         P = points.detach().cpu().numpy()
         for c in range(b):
             idx[c] = torch.from_numpy(fps_literal(P[c], m))
@@ -100,6 +111,8 @@ class _PointUtils(types.ModuleType):
         return 1
 
     def weighted_furthest_point_sampling_wrapper(self, b, n, m, points, weights, temp, idx):
+        if self._replayed("wfps", idx):
+            return 1
         P = points.detach().cpu().numpy()
         Wt = weights.detach().cpu().numpy()
         for c in range(b):
@@ -126,9 +139,18 @@ def knn_brute(p1: torch.Tensor, p2: torch.Tensor, K: int):
     return dist[:, :, :K].contiguous(), idx[:, :, :K].contiguous()
 
 
+KNN_CALLS = []
+KNN_REPLAY = None  # list of idx tensors to return instead of searching (fp64 replay)
+
+
 def knn_points(p1, p2, lengths1=None, lengths2=None, norm=2, K=1, version=-1, return_nn=False,
                return_sorted=True):
-    dist, idx = knn_brute(p1.detach().float(), p2.detach().float(), K)
+    if KNN_REPLAY is not None:
+        idx = KNN_REPLAY.pop(0)
+        dist = None
+    else:
+        dist, idx = knn_brute(p1.detach().float(), p2.detach().float(), K)
+    KNN_CALLS.append(idx.clone())
     nn = knn_gather(p2, idx) if return_nn else None
     return dist, idx, nn
 
@@ -365,8 +387,127 @@ def loss_fixtures():
     print("transformation_loss.npz written", flush=True)
 
 
+TRAIN_KNN_NAMES = ["src_knn_1", "src_knn_2", "src_knn_3", "dst_knn_1", "dst_knn_2", "dst_knn_3",
+                   "coarse_desc_knn", "coarse_nbr_src", "coarse_nbr_dst", "fine2_knn", "fine1_knn"]
+TRAIN_FPS_NAMES = ["src_fps_1", "src_fps_2", "src_fps_3", "dst_fps_1", "dst_fps_2", "dst_fps_3"]
+
+
+FEAT_KEYS = ["xyz_1", "xyz_2", "xyz_3", "sigmas_1", "sigmas_2", "sigmas_3", "desc_1", "desc_2",
+             "desc_3"]
+
+
+def _retain_feats(ret):
+    for part in ("src_feats", "dst_feats"):
+        for k in FEAT_KEYS:
+            ret[part][k].retain_grad()
+
+
+def _save_feat_grads(ret, out, suffix):
+    """gradients of the feature-extraction outputs (models.py:44-56): xyz / sigmas whole,
+    desc [B,C,M] as its norm plus the first 64 keypoints of each cloud (float32)"""
+    for part in ("src_feats", "dst_feats"):
+        for k in FEAT_KEYS:
+            g = ret[part][k].grad.detach()
+            key = f"fgrad_{part[:3]}_{k}{suffix}"
+            out["norm_" + key] = np.array(g.double().norm().item())
+            out[key] = (g[:, :, :64] if k.startswith("desc") else g).float().numpy()
+
+
+def train_fixtures(pu):
+    """One reference training step (train/train_reg_v0.py:264-294): HRegNet in .train()
+    (batch-statistics BN), l_trans = mean over the 3 levels of transformation_loss
+    (alpha 1), loss.backward().  Saved: inputs, every index selection in call order
+    (FPS/WFPS, the 11 knn_points calls), per-level R/t, the loss, each parameter's
+    gradient (norm, sum, first 256 entries) and every BN running stat after the step."""
+    sys.modules["pytorch3d.transforms"].matrix_to_euler_angles = p3d_matrix_to_euler_angles
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_losses", os.path.join(REF, "losses/losses.py"))
+    L = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(L)
+    from models.HRegNet.models import HRegNet  # noqa: E402  (reference code)
+    from pcd_reg_hregnet_amd import synthetic, weights
+    template = HRegNet(_Args()).state_dict()
+    sd = weights.make_state_dict(template, seed=0, pretrained_feats=True)
+    net = HRegNet(_Args())
+    net.load_state_dict(sd)
+    net.train()
+    s, d, Rg, tg = synthetic.lidar_batch(2, 2048, seed0=5)
+    pu.calls.clear()
+    KNN_CALLS.clear()
+    ret = net(torch.from_numpy(s), torch.from_numpy(d))
+    _retain_feats(ret)
+    gR, gt = torch.from_numpy(Rg), torch.from_numpy(tg)
+    l_trans = 0.0
+    for i in range(3):
+        l_, _, _, _, _, _, _ = L.transformation_loss(ret["rotation"][i], ret["translation"][i], gR,
+                                                    gt, 1.0)
+        l_trans = l_trans + l_
+    loss = l_trans / 3.0
+    loss.backward()
+    out = {"src": s, "dst": d, "R_gt": Rg, "t_gt": tg, "loss": loss.detach().numpy()}
+    for i, (R, t) in enumerate(zip(ret["rotation"], ret["translation"])):
+        out[f"R{3 - i}"] = R.detach().numpy()
+        out[f"t{3 - i}"] = t.detach().numpy()
+    for name, (_, idx) in zip(TRAIN_FPS_NAMES, pu.calls):
+        out["idx_" + name] = idx.numpy().astype(np.int32)
+    assert len(KNN_CALLS) == len(TRAIN_KNN_NAMES), len(KNN_CALLS)
+    for name, idx in zip(TRAIN_KNN_NAMES, KNN_CALLS):
+        out["idx_" + name] = idx.numpy().astype(np.int32)
+    names = []
+    for name, p in net.named_parameters():
+        g = p.grad.detach().reshape(-1).double()
+        names.append(name)
+        out["gnorm_" + name] = np.array(g.norm().item())
+        out["gsum_" + name] = np.array(g.sum().item())
+        out["ghead_" + name] = g[:256].float().numpy()
+    out["param_names"] = np.array(names)
+    _save_feat_grads(ret, out, "")
+    for name, b in net.named_buffers():
+        if name.endswith("running_mean") or name.endswith("running_var"):
+            out["buf_" + name] = b.detach().numpy()
+    # the same step in float64 on the same selections: the fp32 reference's own rounding
+    # error (|g32 - g64|) is the scale the tests hold our gradients to
+    global KNN_REPLAY
+    net64 = HRegNet(_Args())
+    net64.load_state_dict(sd)
+    net64 = net64.double().train()
+    pu.replay = [c[1].clone() for c in pu.calls]
+    KNN_REPLAY = [c.clone() for c in KNN_CALLS]
+    pu.calls.clear()
+    KNN_CALLS.clear()
+    torch_eye, torch_zeros = torch.eye, torch.zeros
+    torch.eye = lambda *a, **k: torch_eye(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+    torch.zeros = lambda *a, **k: torch_zeros(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+    try:
+        ret64 = net64(torch.from_numpy(s).double(), torch.from_numpy(d).double())
+        _retain_feats(ret64)
+        l64 = 0.0
+        for i in range(3):
+            l64 = l64 + L.transformation_loss(ret64["rotation"][i], ret64["translation"][i],
+                                              gR.double(), gt.double(), 1.0)[0]
+        (l64 / 3.0).backward()
+    finally:
+        torch.eye, torch.zeros = torch_eye, torch_zeros
+        pu.replay = None
+        KNN_REPLAY = None
+    out["loss64"] = (l64 / 3.0).detach().numpy()
+    _save_feat_grads(ret64, out, "_64")
+    for i, (R, t) in enumerate(zip(ret64["rotation"], ret64["translation"])):
+        out[f"R{3 - i}_64"] = R.detach().numpy()
+        out[f"t{3 - i}_64"] = t.detach().numpy()
+    for name, p in net64.named_parameters():
+        g = p.grad.detach().reshape(-1)
+        out["g64norm_" + name] = np.array(g.norm().item())
+        out["g64head_" + name] = g[:256].numpy()
+    np.savez_compressed(os.path.join(HERE, "train_step_b2_n2048.npz"), **out)
+    print("train_step_b2_n2048.npz written, loss", float(loss), flush=True)
+
+
 def main():
     pu = install_shims()
+    if "--train-only" in sys.argv:
+        train_fixtures(pu)
+        return
     if "--v2-only" in sys.argv:
         v2_fixtures(pu)
         return
@@ -400,6 +541,7 @@ def main():
     print("lidar fixture written", flush=True)
     v2_fixtures(pu)
     loss_fixtures()
+    train_fixtures(pu)
 
 
 if __name__ == "__main__":
