@@ -201,13 +201,128 @@ def job_throughput(pairs_per_rank: int, steps: int, world: int, elapsed_max: flo
     return pairs_per_rank * steps * world / elapsed_max
 
 
+class TrainGemmTimer:
+    """HIP events around every fp32-MFMA GEMM of the training step: the forward and
+    input-gradient GEMMs (hreg_gemm -> gemm_nt_kernel) and the weight-gradient GEMMs
+    (hreg_gemm_tn -> gemm_tn_kernel + split reduction), with their algorithmic FLOPs."""
+
+    def __init__(self):
+        self.ev = {"nt": [], "tn": []}
+        self.flops = {"nt": 0.0, "tn": 0.0}
+        self.enabled = False
+
+    def _timed(self, kind, fn, flops):
+        if not self.enabled:
+            return fn()
+        st = torch.cuda.current_stream()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        r = fn()
+        e1.record(st)
+        self.ev[kind].append((e0, e1))
+        self.flops[kind] += flops
+        return r
+
+    def install(self):
+        from pcd_reg_hregnet_amd import _lib
+        orig_gemm, orig_call = _lib.gemm, _lib.call
+
+        def gemm(g):
+            return self._timed("nt", lambda: orig_gemm(g), 2.0 * g.R * g.N * g.K * g.batch)
+
+        def call(name, *a):
+            if name == "hreg_gemm_tn":
+                return self._timed("tn", lambda: orig_call(name, *a), 2.0 * a[4] * a[5] * a[6])
+            return orig_call(name, *a)
+        _lib.gemm, _lib.call = gemm, call
+
+    def result(self, kind):
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in self.ev[kind])
+        return ms, len(self.ev[kind]), self.flops[kind]
+
+
+def bench_train(args, world, rank, device):
+    """BASELINE configs[3]: train_reg_v0 step, 8 pairs of 2 x 16384 points per rank
+    (batch 64 over 8 GPUs), DDP gradient averaging over RCCL (one bucket all-reduce)."""
+    from pcd_reg_hregnet_amd import trainer, weights
+    from pcd_reg_hregnet_amd.models import HRegNet
+    net = HRegNet(_Args())
+    net.load_state_dict(weights.make_state_dict(net.state_dict(), seed=0, pretrained_feats=True))
+    net = net.to(device)
+    tr = trainer.Trainer(net, lr=1e-3, alpha=1.0)
+    B = args.batch
+    s, d, Rg, tg = shard_batch(rank, B, args.points)
+    src, dst = torch.from_numpy(s).to(device), torch.from_numpy(d).to(device)
+    gR, gt = torch.from_numpy(Rg).to(device), torch.from_numpy(tg).to(device)
+    timer = TrainGemmTimer()
+    timer.install()
+    for _ in range(args.warmup):
+        tr.step(src, dst, gR, gt)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    losses = [tr.step(src, dst, gR, gt)[0] for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    elapsed = max_over_ranks(elapsed, device)
+    value = job_throughput(B, args.steps, world, elapsed)
+    if rank == 0:
+        nt_ms, nt_n, nt_fl = timer.result("nt")
+        tn_ms, tn_n, tn_fl = timer.result("tn")
+        ach = (nt_fl + tn_fl) / max(nt_ms + tn_ms, 1e-9) / 1e9
+        fam = {"gemm_nt_kernel (forward + input gradients)": {
+                   "launches_per_step": nt_n // args.steps,
+                   "ms_per_step": round(nt_ms / args.steps, 3),
+                   "tflops": round(nt_fl / max(nt_ms, 1e-9) / 1e9, 2)},
+               "gemm_tn_kernel + tn_reduce (weight gradients)": {
+                   "launches_per_step": tn_n // args.steps,
+                   "ms_per_step": round(tn_ms / args.steps, 3),
+                   "tflops": round(tn_fl / max(tn_ms, 1e-9) / 1e9, 2)}}
+        line = {
+            "metric": "point-cloud pairs/sec, HRegNet training step (train_reg_v0), "
+                      "16384-pt pairs",
+            "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded KITTI-shape LiDAR pairs with their ground-truth SE(3); "
+                    "nusc_feats + seeded heads)",
+            "config": {"workload": f"HRegNet train step (train-mode BN, 3-level "
+                                   f"transformation_loss, backward, Adam), batch={B} pairs/GPU, "
+                                   f"2x{args.points}-pt pairs (BASELINE configs[3])",
+                       "global_batch": B * world, "points": args.points,
+                       "parallelism": f"dp{world} (one 9.87 MB gradient all-reduce per step)"},
+            "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
+            "roofline": {"kernel": "fp32 MFMA GEMM family of the step (forward, input- and "
+                                   "weight-gradient GEMMs)",
+                         "timing": "HIP events on the launch stream inside the timed region",
+                         "bound": "mfma", "achieved": round(ach, 3),
+                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                         "gemm_ms_per_step": round((nt_ms + tn_ms) / args.steps, 3),
+                         "gflop_per_pair": round((nt_fl + tn_fl) / args.steps / B / 1e9, 3),
+                         "families": fam},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", choices=("hregnet", "v2"), default="hregnet",
-                    help="v2: Model_V2 at config 5 (2 x 65536-pt pairs per GPU, serial executor)")
+    ap.add_argument("--model", choices=("hregnet", "v2", "train"), default="hregnet",
+                    help="v2: Model_V2 at config 5 (2 x 65536-pt pairs per GPU); train: the "
+                         "train_reg_v0 step at config 4 (8 pairs per GPU, DDP)")
     ap.add_argument("--batch", type=int, default=None,
                     help=f"pairs per GPU (default {PAIRS_PER_GPU}; {V2_PAIRS_PER_GPU} for v2)")
     ap.add_argument("--points", type=int, default=None,
@@ -231,7 +346,7 @@ def main():
         args.batch = V2_PAIRS_PER_GPU if v2 else PAIRS_PER_GPU
     if args.points is None:
         args.points = V2_POINTS if v2 else POINTS
-    if args.executor == "graph" and args.steps % args.lanes:
+    if args.model != "train" and args.executor == "graph" and args.steps % args.lanes:
         ap.error("--steps must be a multiple of --lanes")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,6 +359,11 @@ def main():
 
     from pcd_reg_hregnet_amd import _lib, engine
     _lib.load()
+    if args.model == "train":
+        bench_train(args, world, rank, device)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     for lv in filter(None, args.layerwise.split(",")):
         setattr(engine, f"FUSED_L{int(lv)}", False)
     if args.split is not None:

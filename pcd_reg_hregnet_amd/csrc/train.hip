@@ -18,26 +18,32 @@
 
 namespace {
 
-constexpr int CR_THREADS = 256;  // 64 columns x 4 row lanes
+constexpr int CR_THREADS = 256;  // column lanes x row lanes (column width 16, 32 or 64)
+
+// column width of a col_reduce workgroup: the smallest of 16 / 32 / 64 covering C, so
+// that narrow activations (C = 32 at level 1) keep every lane busy
+inline int cr_width_log2(int C) { return C <= 16 ? 4 : (C <= 32 ? 5 : 6); }
 
 // per-column sums over rows [r0, r1): MODE 0: (y, y^2); MODE 1: (g, g*xhat) with
 // g = dout * [out > 0 if relu], xhat = (y - mean) * invstd; MODE 2: (x, 0).
-// double accumulators (the variance is E[y^2] - E[y]^2).
+// double accumulators (the variance is E[y^2] - E[y]^2); row lanes combined in order.
 template <int MODE>
 __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
     const float *__restrict__ x, const float *__restrict__ out, const float *__restrict__ y,
     const float *__restrict__ mean, const float *__restrict__ invstd, int relu, int R, int C,
-    int rows_per_split, double *__restrict__ partial) {
-    __shared__ double s0[4][64], s1[4][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int rl = threadIdx.x >> 6;
+    int rows_per_split, int cw_log2, double *__restrict__ partial) {
+    __shared__ double s0[CR_THREADS], s1[CR_THREADS];
+    const int cw = 1 << cw_log2, nrl = CR_THREADS >> cw_log2;
+    const int cl = threadIdx.x & (cw - 1), rl = threadIdx.x >> cw_log2;
+    const int c = blockIdx.x * cw + cl;
     const int r0 = blockIdx.y * rows_per_split;
     const int r1 = min(R, r0 + rows_per_split);
     double a = 0.0, b = 0.0;
     if (c < C) {
         float mu = 0.f, is = 0.f;
         if (MODE == 1) { mu = mean[c]; is = invstd[c]; }
-        for (int r = r0 + rl; r < r1; r += 4) {
+#pragma unroll 4
+        for (int r = r0 + rl; r < r1; r += nrl) {
             const size_t i = (size_t)r * C + c;
             if (MODE == 0) {
                 const double v = x[i];
@@ -54,29 +60,48 @@ __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
             }
         }
     }
-    s0[rl][threadIdx.x & 63] = a;
-    s1[rl][threadIdx.x & 63] = b;
+    s0[threadIdx.x] = a;
+    s1[threadIdx.x] = b;
     __syncthreads();
     if (rl == 0 && c < C) {
-        const int l = threadIdx.x;
-        const double ta = ((s0[0][l] + s0[1][l]) + s0[2][l]) + s0[3][l];
-        const double tb = ((s1[0][l] + s1[1][l]) + s1[2][l]) + s1[3][l];
+        double ta = 0.0, tb = 0.0;
+        for (int q = 0; q < nrl; ++q) {
+            ta += s0[q * cw + cl];
+            tb += s1[q * cw + cl];
+        }
         partial[((size_t)blockIdx.y * C + c) * 2 + 0] = ta;
         partial[((size_t)blockIdx.y * C + c) * 2 + 1] = tb;
     }
 }
 
-// column totals over the splits, in split order, then MODE's finalisation
+// column totals over the splits (8 columns x 32 split lanes per workgroup: lane l sums
+// splits l, l+32, ... in order, then the 32 lanes in order), then MODE's finalisation
+constexpr int FIN_COLS = 8, FIN_LANES = 32;
+
 template <int MODE>
-__global__ void col_finalize_kernel(const double *__restrict__ partial, int S, int R, int C,
-                                    float eps, float *__restrict__ o0, float *__restrict__ o1,
-                                    float *__restrict__ o2) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+__global__ __launch_bounds__(FIN_COLS * FIN_LANES) void col_finalize_kernel(
+    const double *__restrict__ partial, int S, int R, int C, float eps, float *__restrict__ o0,
+    float *__restrict__ o1, float *__restrict__ o2) {
+    __shared__ double s0[FIN_COLS * FIN_LANES], s1[FIN_COLS * FIN_LANES];
+    const int cl = threadIdx.x % FIN_COLS, sl = threadIdx.x / FIN_COLS;
+    const int c = blockIdx.x * FIN_COLS + cl;
     double a = 0.0, b = 0.0;
-    for (int s = 0; s < S; ++s) {
-        a += partial[((size_t)s * C + c) * 2 + 0];
-        b += partial[((size_t)s * C + c) * 2 + 1];
+    if (c < C) {
+#pragma unroll 4
+        for (int s = sl; s < S; s += FIN_LANES) {
+            a += partial[((size_t)s * C + c) * 2 + 0];
+            b += partial[((size_t)s * C + c) * 2 + 1];
+        }
+    }
+    s0[threadIdx.x] = a;
+    s1[threadIdx.x] = b;
+    __syncthreads();
+    if (sl != 0 || c >= C) return;
+    a = 0.0;
+    b = 0.0;
+    for (int q = 0; q < FIN_LANES; ++q) {
+        a += s0[q * FIN_COLS + cl];
+        b += s1[q * FIN_COLS + cl];
     }
     if (MODE == 0) {
         // mean, invstd (biased variance, used to normalise), unbiased variance (running stat)
@@ -136,68 +161,114 @@ __global__ void bn_running_kernel(const float *__restrict__ mean, const float *_
 }
 
 // ---------------------------------------------------------------- gemm_tn
-// out[n][k] = sum_r A[r][n] * B[r][k]: a 64 x 64 output tile per workgroup (4 waves,
-// one 32 x 32 v_mfma_f32_32x32x2_f32 tile each), rows in chunks of 32 staged in LDS
-// as loaded (row-major, coalesced), k-step s of a chunk = rows 2s, 2s+1 (lane half
-// h takes row 2s+h).  Split over rows: split z writes its partial tile to
-// ws[z][N][K]; tn_reduce_kernel sums the splits in order.
+// out[n][k] = sum_r A[r][n] * B[r][k] (weight gradients: tall, skinny operands, HBM-bound).
+// A workgroup owns a 64 x 64 output tile and a range of rows; each of its 4 waves keeps
+// the whole tile in 4 v_mfma_f32_32x32x2_f32 accumulators and takes every 4th block of
+// 16 rows, loading its operands straight from global memory: at k-step s lane (h, j)
+// needs A[r][n0 + j (+32)] and B[r][k0 + j (+32)] with r = 2s + h, so each half-wave
+// reads 128 contiguous bytes of a row and no LDS staging or barrier sits in the loop
+// (8 k-steps = 32 loads in flight per lane).  The waves' tiles are added in wave order
+// through LDS at the end; split z of the rows writes ws[z][N][K] and tn_reduce_kernel
+// sums the splits in order (same bits every run).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int TN_BR = 32, TN_LDS = 64 + 32;  // row stride padded: halves hit distinct banks
+constexpr int TN_ROWS = 64;  // rows per workgroup iteration (16 per wave)
 
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const float *__restrict__ A, int lda,
                                                       const float *__restrict__ Bm, int ldb, int R,
                                                       int N, int K, int rows_per_split,
                                                       float *__restrict__ ws) {
-    __shared__ float As[TN_BR][TN_LDS], Bs[TN_BR][TN_LDS];
+    __shared__ float red[3][64 * 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wm = w >> 1, wn = w & 1;
+    const int h = lane >> 5, j = lane & 31;
     const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
     const int r0 = blockIdx.z * rows_per_split;
     const int r1 = min(R, r0 + rows_per_split);
-    const int h = lane >> 5, j = lane & 31;
-    f32x16 acc;
+    const bool okn0 = n0 + j < N, okn1 = n0 + 32 + j < N;
+    const bool okk0 = k0 + j < K, okk1 = k0 + 32 + j < K;
+    f32x16 acc00, acc01, acc10, acc11;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-    for (int rc = r0; rc < r1; rc += TN_BR) {
-        // stage 32 rows x 64 columns of A and B (8 floats per thread each)
+    for (int q = 0; q < 16; ++q) acc00[q] = acc01[q] = acc10[q] = acc11[q] = 0.f;
+    for (int base = r0 + 16 * w; base < r1; base += TN_ROWS) {
+        float a0[8], a1[8], b0[8], b1[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int e = tid + i * 256;  // 0 .. 2047
-            const int rr = e >> 6, cc = e & 63;
-            const int r = rc + rr;
+        for (int s = 0; s < 8; ++s) {
+            const int r = base + 2 * s + h;
             const bool okr = r < r1;
-            As[rr][cc] = (okr && n0 + cc < N) ? A[(size_t)r * lda + n0 + cc] : 0.f;
-            Bs[rr][cc] = (okr && k0 + cc < K) ? Bm[(size_t)r * ldb + k0 + cc] : 0.f;
+            const float *pa = A + (size_t)r * lda + n0 + j;
+            const float *pb = Bm + (size_t)r * ldb + k0 + j;
+            a0[s] = (okr && okn0) ? pa[0] : 0.f;
+            a1[s] = (okr && okn1) ? pa[32] : 0.f;
+            b0[s] = (okr && okk0) ? pb[0] : 0.f;
+            b1[s] = (okr && okk1) ? pb[32] : 0.f;
         }
-        __syncthreads();
 #pragma unroll
-        for (int s = 0; s < TN_BR / 2; ++s) {
-            const float a = As[2 * s + h][wm * 32 + j];
-            const float b = Bs[2 * s + h][wn * 32 + j];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        for (int s = 0; s < 8; ++s) {
+            acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc00, 0, 0, 0);
+            acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc01, 0, 0, 0);
+            acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc10, 0, 0, 0);
+            acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc11, 0, 0, 0);
         }
-        __syncthreads();
     }
-    // acc[q]: row n = (q&3) + 8(q>>2) + 4h of the wave tile, column k = j
-    float *o = ws + (size_t)blockIdx.z * N * K;
-    const int k = k0 + wn * 32 + j;
-    if (k < K) {
+    // acc[q]: tile row n = (q&3) + 8(q>>2) + 4h, column k = j (per 32 x 32 quarter)
+    if (w > 0) {
+        float *o = red[w - 1];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const int n = n0 + wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-            if (n < N) o[(size_t)n * K + k] = acc[q];
+            const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
+            o[n * 64 + j] = acc00[q];
+            o[n * 64 + 32 + j] = acc01[q];
+            o[(n + 32) * 64 + j] = acc10[q];
+            o[(n + 32) * 64 + 32 + j] = acc11[q];
+        }
+    }
+    __syncthreads();
+    if (w != 0) return;
+    float *o = ws + (size_t)blockIdx.z * N * K;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
+#pragma unroll
+        for (int quarter = 0; quarter < 4; ++quarter) {
+            const int nn = n + 32 * (quarter >> 1), kk = j + 32 * (quarter & 1);
+            float v = quarter == 0 ? acc00[q] : quarter == 1 ? acc01[q] : quarter == 2 ? acc10[q] : acc11[q];
+            v = fadd_rn(v, red[0][nn * 64 + kk]);
+            v = fadd_rn(v, red[1][nn * 64 + kk]);
+            v = fadd_rn(v, red[2][nn * 64 + kk]);
+            if (n0 + nn < N && k0 + kk < K) o[(size_t)(n0 + nn) * K + k0 + kk] = v;
         }
     }
 }
 
-__global__ void tn_reduce_kernel(const float *__restrict__ ws, int S, size_t NK, float beta,
-                                 float *__restrict__ out) {
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < NK;
-         i += (size_t)gridDim.x * blockDim.x) {
-        float s = 0.f;
-        for (int z = 0; z < S; ++z) s = fadd_rn(s, ws[(size_t)z * NK + i]);
-        out[i] = beta != 0.f ? fadd_rn(fmul_rn(beta, out[i]), s) : s;
+// out[i] = beta * out[i] + sum_z ws[z][i], z in order.  With many splits a workgroup
+// takes 16 outputs x 16 split lanes (lane l sums z = l, l+16, ... in order, then the 16
+// lanes in order); with few, one thread per output.
+template <int LANES>
+__global__ __launch_bounds__(256) void tn_reduce_kernel(const float *__restrict__ ws, int S, size_t NK,
+                                                        float beta, float *__restrict__ out) {
+    if (LANES == 1) {
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < NK;
+             i += (size_t)gridDim.x * blockDim.x) {
+            float s = 0.f;
+            for (int z = 0; z < S; ++z) s = fadd_rn(s, ws[(size_t)z * NK + i]);
+            out[i] = beta != 0.f ? fadd_rn(fmul_rn(beta, out[i]), s) : s;
+        }
+        return;
     }
+    constexpr int OUTS = 256 / LANES;
+    __shared__ float part[256];
+    const int ol = threadIdx.x % OUTS, sl = threadIdx.x / OUTS;
+    const size_t i = (size_t)blockIdx.x * OUTS + ol;
+    float s = 0.f;
+    if (i < NK) {
+#pragma unroll 4
+        for (int z = sl; z < S; z += LANES) s = fadd_rn(s, ws[(size_t)z * NK + i]);
+    }
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (sl != 0 || i >= NK) return;
+    float t = 0.f;
+    for (int q = 0; q < LANES; ++q) t = fadd_rn(t, part[q * OUTS + ol]);
+    out[i] = beta != 0.f ? fadd_rn(fmul_rn(beta, out[i]), t) : t;
 }
 
 __global__ void transpose_kernel(const float *__restrict__ in, int R, int C, float *__restrict__ out) {
@@ -245,22 +316,27 @@ unsigned grid1d(size_t n) {
 
 }  // namespace
 
+static int cr_blocks(int C) {
+    const int cw = 1 << cr_width_log2(C);
+    return (C + cw - 1) / cw;
+}
+
 extern "C" size_t hreg_col_reduce_ws_bytes(int R, int C) {
     if (R <= 0 || C <= 0) return 0;
-    const int S = splits_for(R, (C + 63) / 64, 256);
+    const int S = splits_for(R, cr_blocks(C), 256);
     return (size_t)S * C * 2 * sizeof(double);
 }
 
 extern "C" int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, float *mean,
                              float *invstd, float *var_unbiased, void *stream) {
     if (!y || !ws || !mean || !invstd || R <= 0 || C <= 0) return HREG_ERR_INVALID;
-    const int cb = (C + 63) / 64, S = splits_for(R, cb, 256);
+    const int cb = cr_blocks(C), S = splits_for(R, cb, 256);
     const int rps = (R + S - 1) / S;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(col_reduce_kernel<0>, dim3(cb, S), dim3(CR_THREADS), 0, st, y, nullptr, nullptr,
-                       nullptr, nullptr, 0, R, C, rps, (double *)ws);
+                       nullptr, nullptr, 0, R, C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(col_finalize_kernel<0>, dim3((C + 255) / 256), dim3(256), 0, st,
+    hipLaunchKernelGGL(col_finalize_kernel<0>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
                        (const double *)ws, S, R, C, eps, mean, invstd, var_unbiased);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
@@ -284,13 +360,13 @@ extern "C" int hreg_bn_backward(const float *dout, const float *out, const float
     if (!dout || !y || !mean || !invstd || !gamma || !ws || !dy || !dgamma || !dbeta || R <= 0 ||
         C <= 0 || (relu && !out))
         return HREG_ERR_INVALID;
-    const int cb = (C + 63) / 64, S = splits_for(R, cb, 256);
+    const int cb = cr_blocks(C), S = splits_for(R, cb, 256);
     const int rps = (R + S - 1) / S;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(col_reduce_kernel<1>, dim3(cb, S), dim3(CR_THREADS), 0, st, dout, out, y, mean,
-                       invstd, relu, R, C, rps, (double *)ws);
+                       invstd, relu, R, C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(col_finalize_kernel<1>, dim3((C + 255) / 256), dim3(256), 0, st,
+    hipLaunchKernelGGL(col_finalize_kernel<1>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
                        (const double *)ws, S, R, C, 0.f, dgamma, dbeta, nullptr);
     HREG_CHECK_LAUNCH();
     const size_t total = (size_t)R * C;
@@ -312,13 +388,13 @@ extern "C" int hreg_bn_running_update(const float *mean, const float *var_unbias
 
 extern "C" int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, void *stream) {
     if (!x || !ws || !out || R <= 0 || C <= 0) return HREG_ERR_INVALID;
-    const int cb = (C + 63) / 64, S = splits_for(R, cb, 256);
+    const int cb = cr_blocks(C), S = splits_for(R, cb, 256);
     const int rps = (R + S - 1) / S;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(col_reduce_kernel<2>, dim3(cb, S), dim3(CR_THREADS), 0, st, x, nullptr, nullptr,
-                       nullptr, nullptr, 0, R, C, rps, (double *)ws);
+                       nullptr, nullptr, 0, R, C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(col_finalize_kernel<2>, dim3((C + 255) / 256), dim3(256), 0, st,
+    hipLaunchKernelGGL(col_finalize_kernel<2>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
                        (const double *)ws, S, R, C, 0.f, out, nullptr, nullptr);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
@@ -339,14 +415,18 @@ extern "C" int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, in
         return HREG_ERR_INVALID;
     const int S = tn_splits(R, N, K);
     int rps = (R + S - 1) / S;
-    rps = (rps + TN_BR - 1) / TN_BR * TN_BR;
+    rps = (rps + TN_ROWS - 1) / TN_ROWS * TN_ROWS;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(gemm_tn_kernel, dim3((N + 63) / 64, (K + 63) / 64, S), dim3(256), 0, st, A, lda,
                        B, ldb, R, N, K, rps, (float *)ws);
     HREG_CHECK_LAUNCH();
     const size_t NK = (size_t)N * K;
-    hipLaunchKernelGGL(tn_reduce_kernel, dim3(grid1d(NK)), dim3(256), 0, st, (const float *)ws, S, NK,
-                       beta, out);
+    if (S >= 16)
+        hipLaunchKernelGGL(tn_reduce_kernel<16>, dim3((unsigned)((NK + 15) / 16)), dim3(256), 0, st,
+                           (const float *)ws, S, NK, beta, out);
+    else
+        hipLaunchKernelGGL(tn_reduce_kernel<1>, dim3(grid1d(NK)), dim3(256), 0, st, (const float *)ws,
+                           S, NK, beta, out);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

@@ -1,0 +1,97 @@
+"""HRegNet training step (BASELINE configs[3]: train_reg_v0, batch sharded over ranks).
+
+One step of train/train_reg_v0.py:264-294 -- ``optimizer.zero_grad()``, the train-mode
+forward, l_trans = mean over the 3 levels of ``transformation_loss`` (alpha), backward,
+``optimizer.step()`` (Adam, train_reg_v0.py:249) -- restated for one process per GPU:
+
+* parameters and their gradients live in two flat fp32 buffers (2,467,846 floats for
+  HRegNet, SURVEY.md 8(e), each tensor 256-byte aligned); every ``p`` / ``p.grad`` is a
+  view into them, so the backward writes straight into the gradient bucket;
+* with ``torch.distributed`` initialised (RCCL over xGMI on the GPU box), the bucket is
+  averaged with ONE all_reduce per step (a 9.87 MB ring pass, not one collective per
+  tensor), which is DistributedDataParallel's gradient semantics; ranks start from
+  rank 0's parameters (one broadcast at construction);
+* Adam is one launch over the flat buffers (csrc/train.hip ``adam_kernel``, the same
+  arithmetic as torch.optim.Adam's foreach path);
+* BatchNorm statistics are per rank (the reference does not use SyncBN).
+
+``StepLR(step_size=10, gamma=0.5)`` (train_reg_v0.py:250) is per epoch: ``set_lr``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _lib, train_graph
+from .train import GradBucket, flat_offsets
+
+
+def _dist_world(group=None) -> int:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group)
+    return 1
+
+
+class FlatParams:
+    """Re-home every trainable parameter into one flat buffer (p.data becomes a view)."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        offs, n = flat_offsets(self.params)
+        self.flat = torch.zeros(n, dtype=torch.float32, device=self.params[0].device)
+        for p, off in zip(self.params, offs):
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+
+    def broadcast(self, src: int = 0, group=None):
+        if _dist_world(group) > 1:
+            dist.broadcast(self.flat, src=src, group=group)
+
+
+class FlatAdam:
+    """torch.optim.Adam over the flat parameter / gradient buffers: one launch per step."""
+
+    def __init__(self, flat_params: FlatParams, bucket: GradBucket, lr=1e-3,
+                 betas=(0.9, 0.999), eps=1e-8):
+        self.p = flat_params.flat
+        self.g = bucket.flat
+        assert self.p.numel() == self.g.numel()
+        self.m = torch.zeros_like(self.p)
+        self.v = torch.zeros_like(self.p)
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.step_count = 0
+
+    @torch.no_grad()
+    def step(self):
+        self.step_count += 1
+        _lib.call("hreg_adam_step", self.p, self.g, self.m, self.v, self.p.numel(),
+                  float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps),
+                  self.step_count, _lib.stream_handle())
+
+
+class Trainer:
+    """``step(src, dst, gt_R, gt_t)`` = one train_reg_v0 iteration on this rank's shard."""
+
+    def __init__(self, net, lr=1e-3, alpha=1.0, group=None):
+        self.net = net.train()
+        self.alpha = alpha
+        self.group = group
+        self.params = FlatParams(net.parameters())
+        self.params.broadcast(0, group)
+        self.bucket = GradBucket(self.params.params)
+        self.opt = FlatAdam(self.params, self.bucket, lr=lr)
+
+    def set_lr(self, lr: float):
+        self.opt.lr = lr
+
+    def step(self, src, dst, gt_R, gt_t):
+        """-> (loss, l_R, l_t) of this rank's shard (detached, on the device)."""
+        self.bucket.attach()                     # optimizer.zero_grad()
+        ret = self.net(src, dst)
+        loss, l_R, l_t = train_graph.registration_loss(ret, gt_R, gt_t, self.alpha)
+        loss.backward()
+        self.bucket.collect()
+        self.bucket.all_reduce_mean(self.group)  # DDP gradient averaging, one collective
+        self.opt.step()
+        return loss.detach(), l_R.detach(), l_t.detach()

@@ -76,8 +76,18 @@ def _bucket_worker(rank, world, port, q):
     params[1].grad = torch.full((7,), 10.0 * (rank + 1))
     b.collect()
     b.all_reduce_mean()
+    # the trainer's flat parameters: rank 0's values everywhere after the broadcast
+    from pcd_reg_hregnet_amd.trainer import FlatParams
+    mine = [torch.nn.Parameter(torch.full((5, 3), float(rank))),
+            torch.nn.Parameter(torch.full((7,), 3.0 + rank))]
+    fp = FlatParams(mine)
+    fp.broadcast(0)
+    synced = (torch.equal(mine[0].detach(), torch.zeros(5, 3)) and
+              torch.equal(mine[1].detach(), torch.full((7,), 3.0)) and
+              mine[1].data_ptr() == fp.flat.data_ptr() + 64 * 4)
     q.put((rank, params[0].grad.clone(), params[1].grad.clone(), b.flat.numel(),
-           params[0].grad.data_ptr() == b.flat.data_ptr()))
+           params[0].grad.data_ptr() == b.flat.data_ptr() and
+           params[1].grad.data_ptr() == b.flat.data_ptr() + 64 * 4, synced))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -96,7 +106,8 @@ def test_gloo_grad_bucket_all_reduce():
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for _, g0, g1, n, view in res:
-        assert n == 22 and view  # 5x3 + 7 trainable floats
+    for _, g0, g1, n, view, synced in res:
+        assert n == 128 and view  # 5x3 + 7 trainable floats, each padded to 64 (256 B)
+        assert synced
         assert torch.equal(g0, torch.full((5, 3), 1.5))   # mean of 1 and 2
         assert torch.equal(g1, torch.full((7,), 15.0))    # mean of 10 and 20
