@@ -258,15 +258,16 @@ def bench_train(args, world, rank, device):
     gR, gt = torch.from_numpy(Rg).to(device), torch.from_numpy(tg).to(device)
     timer = TrainGemmTimer()
     timer.install()
+    nxt = (src, dst)  # the next step's batch: its level-1 grouping overlaps this step
     for _ in range(args.warmup):
-        tr.step(src, dst, gR, gt)
+        tr.step(src, dst, gR, gt, next_batch=nxt)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     timer.enabled = True
     t0 = time.perf_counter()
-    losses = [tr.step(src, dst, gR, gt)[0] for _ in range(args.steps)]
+    losses = [tr.step(src, dst, gR, gt, next_batch=nxt)[0] for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

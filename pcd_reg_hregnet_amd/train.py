@@ -76,12 +76,24 @@ def col_sum(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+_CONST = {}
+
+
+def _const(value: float, n: int, device) -> torch.Tensor:
+    """Cached constant vectors (the unit scale / zero shift of a plain GEMM epilogue)."""
+    key = (value, n, str(device))
+    t = _CONST.get(key)
+    if t is None:
+        t = _CONST[key] = torch.full((n,), value, dtype=torch.float32, device=device)
+    return t
+
+
 def _plain_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None) -> torch.Tensor:
     """x [R][K] @ W[N][K]^T (+ shift) on hreg_gemm (no activation)."""
     R, K = x.shape
     N = W.shape[0]
-    ones = torch.ones(N, device=x.device)
-    sh = shift if shift is not None else torch.zeros(N, device=x.device)
+    ones = _const(1.0, N, x.device)
+    sh = shift if shift is not None else _const(0.0, N, x.device)
     lin = engine.Lin(W.contiguous(), ones, sh.contiguous(), relu=False)
     return engine.gemm([engine._seg(x, 0, K)], lin, R)
 

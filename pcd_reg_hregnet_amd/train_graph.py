@@ -76,8 +76,11 @@ class IndexHook:
     replaces it (``inject``: name -> per-cloud indices [nb, m(, k)], as the reference's
     fps / knn_points calls return them)."""
 
-    def __init__(self, inject: dict | None = None):
+    def __init__(self, inject: dict | None = None, prepared: dict | None = None):
         self.inject = dict(inject or {})
+        # name -> (local [nb, m] or None, global rows int32): selections already on the
+        # device (the trainer's prefetched level-1 grouping), used without a copy
+        self.prepared = dict(prepared or {})
         self.record = {}
 
     def __call__(self, name, local_fn, n, device):
@@ -95,8 +98,11 @@ class IndexHook:
         self.record[name] = (g - off).to(torch.int32)
 
 
-def _select(hook, name, local_fn, n, device):
+def _select(hook, name, local_fn, n, device, nb=None):
     """-> (local [nb, m(, k)] int32, IndexMap over global rows)."""
+    if hook is not None and name in hook.prepared:
+        loc, gidx = hook.prepared[name]
+        return loc, IndexMap(gidx, nb * n)
     loc = hook(name, local_fn, n, device) if hook is not None else local_fn()
     return loc, IndexMap(offset_index(loc, n), loc.shape[0] * n)
 
@@ -495,13 +501,27 @@ def transformation_loss(R, t, gR, gt, alpha=1.0):
 
 # ------------------------------------------------------------------ modules
 
+_BN_COUNTERS: list = []  # num_batches_tracked of every BN call of the current forward
+
+
+def _flush_bn_counters():
+    """num_batches_tracked += 1 per BN call, as one multi-tensor launch per forward (a
+    module called twice -- src and dst -- appears once, with its count)."""
+    if _BN_COUNTERS:
+        uniq = {}
+        for t in _BN_COUNTERS:
+            uniq.setdefault(id(t), [t, 0])[1] += 1
+        torch._foreach_add_([t for t, _ in uniq.values()], [c for _, c in uniq.values()])
+        _BN_COUNTERS.clear()
+
+
 def conv_bn(x, conv, bn, relu=True):
     """Conv(1x1) + train-mode BatchNorm (+ ReLU) over rows (num_batches_tracked += 1)."""
     W = conv.weight.view(conv.out_channels, -1)
     y = train.conv_bn_act(x, W, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                           relu, momentum=bn.momentum, eps=bn.eps)
     if bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+        _BN_COUNTERS.append(bn.num_batches_tracked)
     return y
 
 
@@ -540,9 +560,11 @@ def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src"):
             grouped.append(engine.grouping(xd, lvl, wd))  # FPS/WFPS + kNN grouping
             return grouped[0][0]
 
-        fps_loc, fps_map = _select(hook, f"{part}_fps_{lvl + 1}", fps_local, n, dev)
+        fps_loc, fps_map = _select(hook, f"{part}_fps_{lvl + 1}", fps_local, n, dev, nb)
         knn_name = f"{part}_knn_{lvl + 1}"
-        if grouped and not (hook is not None and knn_name in hook.inject):
+        if hook is not None and knn_name in hook.prepared:
+            _, kmap = _select(hook, knn_name, None, n, dev, nb)
+        elif grouped and not (hook is not None and knn_name in hook.inject):
             kmap = IndexMap(grouped[0][2].contiguous(), nb * n)  # global rows
             if hook is not None:
                 hook.record_global(knn_name, kmap.idx, nb, n)
@@ -677,6 +699,7 @@ def hregnet_train_forward(net, src, dst, hook=None):
     src = src.float().contiguous()
     dst = dst.float().contiguous()
     B = src.shape[0]
+    _BN_COUNTERS.clear()
     sf = feature_extraction(fe, src, hook, "src")
     df = feature_extraction(fe, dst, hook, "dst")
     c3, w3 = coarse_reg(net.coarse_corres, sf["xyz_3"], sf["desc_3"], df["xyz_3"], df["desc_3"],
@@ -692,6 +715,7 @@ def hregnet_train_forward(net, src, dst, hook=None):
                       sf["sigmas_1"], df["sigmas_1"], hook, "fine1")
     R1_, t1_ = weighted_svd(x1t, c1, w1)
     R1, t1 = compose(R1_, t1_, R2, t2)
+    _flush_bn_counters()
 
     def feats(f):
         d = {}
