@@ -43,6 +43,8 @@
  *                                            (train_reg_v0.py:241-296 over layers.py / models.py)
  *   hreg_transformation_loss              <- transformation_loss + calc_rot_rre_err + calc_tran_rte_err
  *                                            (losses/losses.py:97-164; callers train/train_reg_v1.py:101,252)
+ *   hreg_calib_metrics                    <- CalibEval.add_batch / geodesic_distance
+ *                                            (metrics/calibeval.py:72-113,197-214; caller test/test_v3.py:130-140)
  */
 #ifndef HREGNET_AMD_H
 #define HREGNET_AMD_H
@@ -205,6 +207,13 @@ int hreg_transform_points(const float *xyz, const float *R, const float *t, int 
 int hreg_transformation_loss(const float *pred_R, const float *pred_t, const float *gt_R,
                              const float *gt_t, int nb, float alpha, float *scalars, float *R_err,
                              float *T_err, float *geodesic, float *eucl, void *stream);
+
+/* CalibEval.add_batch (metrics/calibeval.py:72-113) for one layer's batch of nb pairs, all
+ * device pointers: pred_tf/gt_tf [nb][4][4] row-major.  per_pair [nb][12] = {Euler XYZ
+ * angles (deg) of E = pred_tf . gt_tf, E[:3,3], Euler XYZ (deg) of pred_tf, pred_tf[:3,3]};
+ * batch_geo[2] = {mean geodesic angle of E (deg), mean ||E[:3,3]||} (calibeval.py:197-214). */
+int hreg_calib_metrics(const float *pred_tf, const float *gt_tf, int nb, float *per_pair,
+                       float *batch_geo, void *stream);
 
 /* ---------------- training-step building blocks (csrc/train.hip) ----------------
  * Train-mode BatchNorm after a 1x1 conv (layers.py:115-130 etc. in .train(); the

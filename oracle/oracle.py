@@ -459,3 +459,23 @@ def transformation_loss(pred_R, pred_t, gt_R, gt_t, alpha=1.0):
     loss_R = np.mean(resi).astype(f)
     loss_t = np.mean(eucl).astype(f)
     return (f(alpha) * loss_R + loss_t, loss_R, loss_t, R_err.astype(f), geo, T_err.astype(f), eucl)
+
+
+def calib_metrics(pred_tf, gt_tf):
+    """CalibEval.add_batch's per-pair numbers (metrics/calibeval.py:72-113) and
+    geodesic_distance (:197-214), fp32 like the reference: E = pred_tf @ gt_tf;
+    per_pair [B][12] = {deg Euler XYZ of E[:3,:3], E[:3,3], deg Euler XYZ of
+    pred_tf[:3,:3], pred_tf[:3,3]}; batch_geo [2] = {mean deg acos((tr-1)/2), mean ||E[:3,3]||}."""
+    f = np.float32
+    P = np.asarray(pred_tf, f)
+    E = np.matmul(P, np.asarray(gt_tf, f)).astype(f)
+
+    def eul(M):
+        return np.rad2deg(np.stack([np.arctan2(-M[:, 1, 2], M[:, 2, 2]), np.arcsin(M[:, 0, 2]),
+                                    np.arctan2(-M[:, 0, 1], M[:, 0, 0])], -1)).astype(f)
+
+    per = np.concatenate([eul(E[:, :3, :3]), E[:, :3, 3], eul(P[:, :3, :3]), P[:, :3, 3]], 1)
+    cos = np.clip((np.trace(E[:, :3, :3], axis1=1, axis2=2) - f(1)) / f(2), -1.0, 1.0).astype(f)
+    theta = np.rad2deg(np.arccos(cos)).astype(f)
+    tn = np.sqrt(np.sum(E[:, :3, 3] ** 2, axis=1)).astype(f)
+    return per.astype(f), np.array([theta.mean(), tn.mean()], f)

@@ -108,6 +108,7 @@ _SIGS = {
     "hreg_transformation_loss_bwd": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, ctypes.c_float, _vp,
                                      _vp, _vp, _vp],
     "hreg_index_offset": [_vp, _i, _i, _i, _vp, _vp],
+    "hreg_calib_metrics": [_vp, _vp, _i, _vp, _vp, _vp],
 }
 
 EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_reduce_ws_bytes",

@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only]   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --metrics-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -503,8 +503,72 @@ def train_fixtures(pu):
     print("train_step_b2_n2048.npz written, loss", float(loss), flush=True)
 
 
+class _CalibConfig:
+    """the attributes CalibEval / MultiLayerCalibEval read (config.py DataConfig)"""
+    dataset = "man"
+
+    class dataset_config:
+        version = "_v2"
+        model = "HRegNet"
+        max_trans_error = 0.5
+        max_rot_error = 20
+        distribution = "uniform"
+
+
+def metrics_fixtures():
+    """The reference's MultiLayerCalibEval (metrics/calibeval.py:340-380) fed as
+    test/test_v3.py:130-140 feeds it: 3 levels x 4 batches of 3 pairs; gt_tf = igt (a
+    random SE(3) from the synthetic generator), pred_tf = its inverse perturbed by a
+    level-dependent small rotation/translation (batch 0, level 2 exactly inverse:
+    acos clamp at 1).  Saved: the inputs and results.json as the reference writes it."""
+    import importlib.util
+    import json
+    sys.modules["pytorch3d.transforms"].matrix_to_euler_angles = p3d_matrix_to_euler_angles
+    spec = importlib.util.spec_from_file_location("ref_calibeval",
+                                                  os.path.join(REF, "metrics/calibeval.py"))
+    M = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(M)
+    from pcd_reg_hregnet_amd import synthetic
+    rng = np.random.default_rng(77)
+    ev = M.MultiLayerCalibEval(config=_CalibConfig(), num_layers=3)
+    gts, preds = [], []
+    for b in range(4):
+        _, _, R, t = synthetic.lidar_batch(3, 64, seed0=100 + 3 * b)
+        igt = np.tile(np.eye(4, dtype=np.float32), (3, 1, 1))
+        igt[:, :3, :3] = R
+        igt[:, :3, 3] = t
+        inv = np.linalg.inv(igt.astype(np.float64))
+        lay = []
+        for layer in range(3):
+            scale = 0.0 if (b == 0 and layer == 2) else 0.05 / (layer + 1)
+            w = rng.normal(0, scale, (3, 3))
+            P = inv.copy()
+            for i in range(3):
+                K = np.array([[0, -w[i, 2], w[i, 1]], [w[i, 2], 0, -w[i, 0]], [-w[i, 1], w[i, 0], 0]])
+                th = np.linalg.norm(w[i])
+                Rd = np.eye(3) if th == 0 else (np.eye(3) + np.sin(th) / th * K +
+                                                (1 - np.cos(th)) / th ** 2 * K @ K)
+                P[i, :3, :3] = Rd @ P[i, :3, :3]
+                P[i, :3, 3] += rng.normal(0, scale, 3)
+            P = P.astype(np.float32)
+            lay.append(P)
+            ev.add_batch(layer=layer, gt_tf=torch.from_numpy(igt), pred_tf=torch.from_numpy(P))
+        gts.append(igt)
+        preds.append(np.stack(lay))
+    path = os.path.join(HERE, "_calib_results.json")
+    ev.save_all_results(path)
+    res = open(path).read()
+    os.remove(path)
+    np.savez_compressed(os.path.join(HERE, "calib_metrics.npz"), gt_tf=np.stack(gts),
+                        pred_tf=np.stack(preds), results_json=np.array(res))
+    print("calib_metrics.npz written", flush=True)
+
+
 def main():
     pu = install_shims()
+    if "--metrics-only" in sys.argv:
+        metrics_fixtures()
+        return
     if "--train-only" in sys.argv:
         train_fixtures(pu)
         return
