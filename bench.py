@@ -79,6 +79,11 @@ def _nbr_work(args):
     return (2.0 * 8 * G * (260 * 256 + 2 * 256 * 256), 4.0 * G * (8 * (256 + 4 + 1) + 256))
 
 
+def _mlp_work(args):
+    C, G = args[1], args[4] * args[5]
+    return 2.0 * G * (2 * C * C + C), 4.0 * G * (C + 1)
+
+
 # C-ABI entry -> (timer kind, (flops, bytes) of one launch from its arguments)
 MFMA_ENTRIES = {
     "hreg_group_l1": ("l1", lambda a: (L1_FLOPS_PER_GROUP * a[3], L1_BYTES_PER_GROUP * a[3])),
@@ -88,15 +93,16 @@ MFMA_ENTRIES = {
     "hreg_group_split_l3": ("fused", lambda a: (L3_FLOPS_PER_GROUP * a[5], L3_BYTES_PER_GROUP * a[5])),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
+    "hreg_mlp_head": ("mlp", _mlp_work),
 }
 
 
 class MfmaTimer:
     """Brackets every fp32-MFMA launch (gemm_nt_kernel, group_l1_kernel,
-    group_fused_kernel, fine/nbr head kernels) with HIP events on the launch stream
+    group_fused_kernel, fine/nbr/mlp head kernels) with HIP events on the launch stream
     and counts its algorithmic FLOPs and bytes, per kernel kind."""
 
-    KINDS = ("gemm", "l1", "fused", "head")
+    KINDS = ("gemm", "l1", "fused", "head", "mlp")
 
     def __init__(self):
         self.events = {k: [] for k in self.KINDS}
@@ -458,7 +464,8 @@ def main():
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
                 "other_mfma_kernels": {"gemm_nt_kernel": kind_summary("gemm"),
                                        "group_l1_kernel": kind_summary("l1"),
-                                       "fine_head_kernel + nbr_head_kernel": kind_summary("head")},
+                                       "fine_head_kernel + nbr_head_kernel": kind_summary("head"),
+                                       "mlp_head_kernel": kind_summary("mlp")},
                 "all_mfma": {"ms_per_step": round(tot_ms / args.steps, 3),
                              "gflop_per_pair": round(tot_fl / args.steps / B / 1e9, 3),
                              "tflops": round(tot_fl / max(tot_ms, 1e-9) / 1e9, 2)}}

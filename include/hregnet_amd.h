@@ -167,6 +167,21 @@ int hreg_head_out(const float *x, int C, int ldx, int nclouds, int rows_per_clou
                   const float *w3, const float *b3, int mode, float *out, float *weights_out,
                   void *stream);
 
+/* weights = (1/(sigma+1e-5)) / mean_cloud(1/(sigma+1e-5)) (models.py:30-32) over
+ * nclouds x rows_per_cloud sigmas. */
+int hreg_sigma_weights(const float *sigma, int nclouds, int rows_per_cloud, float *weights,
+                       void *stream);
+
+/* The whole mlp1 -> mlp2 -> mlp3 head of KeypointDetector (layers.py:124-132,161-163),
+ * CoarseReg (layers.py:262-268,389-394) and FineReg (layers.py:425-431,451-452) in one
+ * launch (mlp_head.hip): x [nclouds*rows_per_cloud][ldx] (first C columns, 16-byte
+ * aligned rows, C in {64,128,256,512}, rows a multiple of 32) -> out [rows] =
+ * softplus(z)+0.001 or sigmoid(z); weights_out as hreg_head_out.  table: engine.mlp_head_table
+ * (hreg_mlp_head_table_floats(C) floats; -1 for an unsupported C). */
+int hreg_mlp_head_table_floats(int C);
+int hreg_mlp_head(const float *table, int C, const float *x, int ldx, int nclouds,
+                  int rows_per_cloud, int mode, float *out, float *weights_out, void *stream);
+
 /* norms[r] = sqrt(sum_c x[r][c]^2), x [R][ldx] */
 int hreg_row_norms(const float *x, int R, int C, int ldx, float *norms, void *stream);
 

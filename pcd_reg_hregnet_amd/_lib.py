@@ -73,6 +73,9 @@ _SIGS = {
     "hreg_fine_head": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_fine_head_table_floats": [_i],
     "hreg_nbr_head": [_vp, _vp, _vp, _vp, _i, _vp, _vp],
+    "hreg_mlp_head": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
+    "hreg_mlp_head_table_floats": [_i],
+    "hreg_sigma_weights": [_vp, _i, _i, _vp, _vp],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_apply": [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp],

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
     for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
     __syncthreads();
     const float *eb = ep - K::F_END;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
     constexpr int KN = K::KN, GPT = 32 / KN;  // groups per 32-row tile
     const int NT = G / GPT;

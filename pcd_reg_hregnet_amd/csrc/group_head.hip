@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, K::WPS) void fine_head_kernel(
     for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
     __syncthreads();
     const float *eb = ep - K::F_END;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
     const int NT = G * KH / 32;
     constexpr int WT = win_for<T1>();
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
     for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
     __syncthreads();
     const float *eb = ep - K::F_END;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
     const int NT = G * KH / 32;
     constexpr int WT = win_for<T1>();

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void group_l1_kernel(
     for (int i = threadIdx.x; i < TABLE_FLOATS; i += blockDim.x) tb[i] = table[i];
     __syncthreads();
 
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
     for (int g = blockIdx.x * WAVES + w; g < G; g += gridDim.x * WAVES) {
         const size_t r0 = (size_t)g * KN;

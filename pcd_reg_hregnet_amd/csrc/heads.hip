@@ -428,6 +428,16 @@ extern "C" int hreg_head_out(const float *x, int C, int ldx, int nclouds, int ro
     return HREG_OK;
 }
 
+extern "C" int hreg_sigma_weights(const float *sigma, int nclouds, int rows_per_cloud, float *weights,
+                                  void *stream) {
+    if (!sigma || !weights || nclouds < 0 || rows_per_cloud <= 0) return HREG_ERR_INVALID;
+    if (!nclouds) return HREG_OK;
+    hipLaunchKernelGGL(sigma_weights_kernel, dim3(nclouds), dim3(256), 0, as_stream(stream), sigma,
+                       rows_per_cloud, weights);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
 extern "C" int hreg_row_norms(const float *x, int R, int C, int ldx, float *norms, void *stream) {
     if (!x || !norms || R < 0 || C <= 0 || ldx < C) return HREG_ERR_INVALID;
     if (!R) return HREG_OK;

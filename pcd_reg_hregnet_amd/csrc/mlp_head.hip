@@ -1,0 +1,179 @@
+// mlp_head.hip -- the per-keypoint MLP heads as one launch each.
+//
+// KeypointDetector (layers.py:124-132, 161-163), CoarseReg (layers.py:262-268,
+// 389-394) and FineReg (layers.py:425-431, 451-452) end in the same head over a
+// per-keypoint feature row x [C]:
+//   y1 = ReLU(BN(W1 x))  (mlp1: Conv1d C->C + BN + ReLU)
+//   y2 = ReLU(BN(W2 y1)) (mlp2)
+//   z  = w3 . y2 + b3    (mlp3: Conv1d C->1)
+//   out = softplus(z) + 0.001 (sigma) or sigmoid(z) (correspondence weight)
+// The layer-by-layer path runs this as two GEMM launches + hreg_head_out; with
+// only 2k-16k rows per launch those GEMMs are latency-bound (~20 TF).  Here one
+// workgroup owns a 32-row tile: the rows are staged into LDS, CW waves split each
+// layer's output channels (P <= 2 tiles of 32 per wave, split_chain.h), y1 goes
+// back through the same LDS buffer, y2 stays in registers and the mlp3 dot is
+// reduced lane half -> waves in a fixed order.  BN is folded (eval) into the
+// per-channel alpha/beta epilogue, as everywhere else (engine._bn_fold).
+#include "split_chain.h"
+
+namespace {
+
+using namespace hreg_chain;
+using namespace hreg_split;
+
+// Table: [mlp1 fragments][mlp2 fragments] (engine.mlp_head_table: frag_layer order,
+// 4 k-steps innermost per lane), then alpha1, beta1, alpha2, beta2 (C each), w3 (C),
+// b3 (1) padded to 4.
+template <int C_, int CW_, int RT_, int WMAX_ = SWIN>
+struct HCfg {
+    static constexpr int C = C_, CW = CW_, RT = RT_, WMAX = WMAX_;
+    static constexpr int T = C / 32, P = T / CW, NS = T * 16;
+    static_assert(P * CW == T && P >= 1 && P <= 2, "channel split");
+    static constexpr int F_M1 = 0, F_M2 = T * NS * 64, F_END = 2 * F_M2;
+    static constexpr int E_M1 = F_END, E_M2 = E_M1 + 2 * C, E_W3 = E_M2 + 2 * C, E_B3 = E_W3 + C;
+    static constexpr int TABLE = E_B3 + 4;
+    static constexpr int LDSW = C + 4;
+    static constexpr int THREADS = CW * RT * 64;
+};
+
+using H64 = HCfg<64, 2, 2>;
+using H128 = HCfg<128, 4, 1>;
+using H256 = HCfg<256, 4, 1>;
+using H512 = HCfg<512, 8, 1, 8>;  // 2 waves per SIMD: 128 VGPRs + AGPRs, short windows
+
+template <class K>
+__global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__restrict__ table,
+                                                              const float *__restrict__ x, int ldx,
+                                                              int G, int mode, float *__restrict__ out) {
+    constexpr int C = K::C, P = K::P, CW = K::CW, RT = K::RT, LDSW = K::LDSW, NS = K::NS;
+    constexpr int NE = K::TABLE - K::F_END, WIN = NS < K::WMAX ? NS : K::WMAX;
+    __shared__ float ep[NE];
+    __shared__ __attribute__((aligned(16))) float sA[RT][32 * LDSW];
+    __shared__ float sPart[RT][CW][32];
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
+    const float *eb = ep - K::F_END;
+    // the wave index is uniform: in SGPRs, every fragment address is an SGPR base plus
+    // the lane's offset (not a hoisted per-load 64-bit VGPR address)
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int rt = w / CW, cw = w % CW;
+    const int h = lane >> 5, j = lane & 31;
+    const int NT = G / 32;
+    float *A = sA[rt];
+    const int c0 = cw * P;
+    const FragSeq f1{K::F_M1 / 64 + c0 * NS, NS}, f2{K::F_M2 / 64 + c0 * NS, NS};
+
+    float carry[SCARRY];
+    {
+        const gfloat *tb = reinterpret_cast<const gfloat *>(reinterpret_cast<uint64_t>(table));
+#pragma unroll
+        for (int s0 = 0; s0 < WIN; s0 += 4)
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                float v[4];
+                ldgroup<4>(tb, f1.base + i * f1.stride + s0, lane, v);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) carry[(s0 + q) * P + i] = v[q];
+            }
+    }
+    for (int base = blockIdx.x * RT; base < NT; base += gridDim.x * RT) {
+        // every wave runs the same trip count (barriers): a row tile past the end
+        // recomputes the last tile (identical values, identical stores)
+        const int t = min(base + rt, NT - 1);
+        uint64_t tba = reinterpret_cast<uint64_t>(table);
+        asm volatile("" : "+s"(tba));
+        const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
+        float ca[SCARRY];
+
+        tile_sync();  // the previous tile's readers of A are done (and ep is loaded)
+        constexpr int F4 = C / 4;
+#pragma unroll
+        for (int i = cw * 64 + lane; i < 32 * F4; i += CW * 64) {
+            const int r = i / F4, c4 = i - r * F4;
+            *reinterpret_cast<float4 *>(A + r * LDSW + c4 * 4) =
+                *reinterpret_cast<const float4 *>(x + ((size_t)t * 32 + r) * ldx + c4 * 4);
+        }
+        tile_sync();
+
+        f32x16 y1[P];
+        zero_tiles(y1);
+        pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f1, ChanB{A + j * LDSW, h}, y1, carry, f2, ca);
+        epi<P, C>(eb + K::E_M1, c0, h, y1);
+        tile_sync();  // every wave has read x from A
+#pragma unroll
+        for (int i = 0; i < P; ++i) put_tile<LDSW>(A, c0 + i, j, h, y1[i]);
+        tile_sync();
+
+        f32x16 y2[P];
+        zero_tiles(y2);
+        pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f2, ChanB{A + j * LDSW, h}, y2, ca, f1, carry);
+        epi<P, C>(eb + K::E_M2, c0, h, y2);
+
+        // mlp3: this wave's channels, then the two lane halves, then the waves in order
+        float p = 0.f;
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) p = fadd_rn(p, fmul_rn(y2[i][q], eb[K::E_W3 + chan(c0 + i, q, h)]));
+        p = fadd_rn(p, __shfl_xor(p, 32));  // commutative: both halves hold the same bits
+        if (h == 0) sPart[rt][cw][j] = p;
+        tile_sync();
+        if (cw == 0 && h == 0) {
+            float z = sPart[rt][0][j];
+#pragma unroll
+            for (int c = 1; c < CW; ++c) z = fadd_rn(z, sPart[rt][c][j]);
+            z = fadd_rn(z, eb[K::E_B3]);
+            float o;
+            if (mode == HREG_HEAD_SOFTPLUS) {
+                const float sp = z > 20.f ? z : log1pf(expf(z));
+                o = fadd_rn(sp, 0.001f);
+            } else {
+                o = 1.0f / fadd_rn(1.0f, expf(-z));
+            }
+            out[(size_t)t * 32 + j] = o;
+        }
+    }
+}
+
+template <class K>
+int launch_head(const float *table, const float *x, int ldx, int G, int mode, float *out, void *stream) {
+    const int NT = G / 32;
+    int grid = (NT + K::RT - 1) / K::RT;
+    if (grid > 2048) grid = 2048;
+    hipLaunchKernelGGL(mlp_head_kernel<K>, dim3(grid), dim3(K::THREADS), 0, as_stream(stream), table, x,
+                       ldx, G, mode, out);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+}  // namespace
+
+extern "C" int hreg_mlp_head_table_floats(int C) {
+    switch (C) {
+        case 64: return H64::TABLE;
+        case 128: return H128::TABLE;
+        case 256: return H256::TABLE;
+        case 512: return H512::TABLE;
+        default: return -1;
+    }
+}
+
+extern "C" int hreg_mlp_head(const float *table, int C, const float *x, int ldx, int nclouds,
+                             int rows_per_cloud, int mode, float *out, float *weights_out, void *stream) {
+    if (!table || !x || !out || nclouds < 0 || rows_per_cloud <= 0 || ldx < C || (ldx & 3) ||
+        (mode != HREG_HEAD_SOFTPLUS && mode != HREG_HEAD_SIGMOID))
+        return HREG_ERR_INVALID;
+    if (reinterpret_cast<uintptr_t>(x) & 15) return HREG_ERR_INVALID;
+    const int G = nclouds * rows_per_cloud;
+    if (G % 32) return HREG_ERR_UNSUPPORTED;  // whole 32-row tiles
+    if (hreg_mlp_head_table_floats(C) < 0) return HREG_ERR_UNSUPPORTED;
+    if (!G) return HREG_OK;
+    int rc;
+    switch (C) {
+        case 64: rc = launch_head<H64>(table, x, ldx, G, mode, out, stream); break;
+        case 128: rc = launch_head<H128>(table, x, ldx, G, mode, out, stream); break;
+        case 256: rc = launch_head<H256>(table, x, ldx, G, mode, out, stream); break;
+        default: rc = launch_head<H512>(table, x, ldx, G, mode, out, stream); break;
+    }
+    if (rc != HREG_OK || !weights_out) return rc;
+    return hreg_sigma_weights(out, nclouds, rows_per_cloud, weights_out, stream);
+}

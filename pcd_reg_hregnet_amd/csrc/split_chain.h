@@ -1,0 +1,145 @@
+// split_chain.h -- building blocks of the channel-split kernels (group_split.hip,
+// mlp_head.hip): a row tile's activations live in LDS (row-major, natural channel
+// order); each wave computes P output tiles of a layer with
+// v_mfma_f32_32x32x2_f32, A fragments streamed from the L2-resident table one
+// window ahead, B streamed from LDS.
+#pragma once
+
+#include "mfma_chain.h"
+
+namespace hreg_split {
+
+using namespace hreg_chain;
+
+// tools/split_experiment.py: 1 = no workgroup barriers, 2 = B operand not read from
+// LDS (timing experiments only: results are wrong)
+#ifndef HREG_SPLIT_EXP
+#define HREG_SPLIT_EXP 0
+#endif
+__device__ __forceinline__ void tile_sync() {
+    if constexpr (HREG_SPLIT_EXP != 1) __syncthreads();
+}
+
+constexpr int SCARRY = 32;
+constexpr int SWIN = 16;  // k-steps per window (P <= 2 tiles: <= 32 fragments in flight)
+
+// acc[P] += sum_{st < NSTEP} A(co0 + i, st) x B(st): A fragments from the table
+// (grouped 4 k-steps per lane; GS = 2 for a 2-step call), B from LDS through
+// bl(st0, v) (GS consecutive k-steps).  cin: this call's first window of A
+// fragments (loaded by the previous call); cout: the first window (NWIN steps x NP
+// tiles) of the next call nf.  The first B window is read at entry (it is the
+// output of the barrier just passed); later windows one window ahead.
+template <int NSTEP, int P, int NP, int NWIN, int WMAX = SWIN, class BL>
+__device__ __forceinline__ void pipe_lds(const gfloat *__restrict__ wf, int lane, FragSeq f, BL bl,
+                                         f32x16 (&acc)[P], const float (&cin)[SCARRY], FragSeq nf,
+                                         float (&cout)[SCARRY]) {
+    constexpr int WIN = NSTEP < WMAX ? NSTEP : WMAX;
+    constexpr int GS = WIN < 4 ? WIN : 4, NGS = NWIN < 4 ? NWIN : 4;
+    static_assert(NSTEP % WIN == 0 && WIN % GS == 0 && NWIN % NGS == 0, "window");
+    static_assert(WIN * P <= SCARRY && NWIN * NP <= SCARRY, "carry");
+    constexpr int NW = NSTEP / WIN;
+    float abuf[2][WIN][P];
+    float bbuf[2][WIN];
+#pragma unroll
+    for (int s = 0; s < WIN; ++s)
+#pragma unroll
+        for (int co = 0; co < P; ++co) abuf[0][s][co] = cin[s * P + co];
+#pragma unroll
+    for (int s0 = 0; s0 < WIN; s0 += GS) {
+        float v[GS];
+        if constexpr (HREG_SPLIT_EXP == 2) {
+#pragma unroll
+            for (int i = 0; i < GS; ++i) {
+                float x = __int_as_float(lane);
+                asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
+                v[i] = x;
+            }
+        } else {
+            bl(s0, v);
+        }
+#pragma unroll
+        for (int i = 0; i < GS; ++i) bbuf[0][s0 + i] = v[i];
+    }
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        if (w + 1 < NW) {
+#pragma unroll
+            for (int s0 = 0; s0 < WIN; s0 += GS) {
+#pragma unroll
+                for (int co = 0; co < P; ++co) {
+                    float v[GS];
+                    ldgroup<GS>(wf, f.base + co * f.stride + (w + 1) * WIN + s0, lane, v);
+#pragma unroll
+                    for (int i = 0; i < GS; ++i) abuf[(w + 1) & 1][s0 + i][co] = v[i];
+                }
+                float v[GS];
+                if constexpr (HREG_SPLIT_EXP == 2) {
+#pragma unroll
+                    for (int i = 0; i < GS; ++i) {
+                        float x = __int_as_float(lane);
+                        asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
+                        v[i] = x;
+                    }
+                } else {
+                    bl((w + 1) * WIN + s0, v);
+                }
+#pragma unroll
+                for (int i = 0; i < GS; ++i) bbuf[(w + 1) & 1][s0 + i] = v[i];
+            }
+        } else {
+#pragma unroll
+            for (int s0 = 0; s0 < NWIN; s0 += NGS)
+#pragma unroll
+                for (int co = 0; co < NP; ++co) {
+                    float v[NGS];
+                    ldgroup<NGS>(wf, nf.base + co * nf.stride + s0, lane, v);
+#pragma unroll
+                    for (int i = 0; i < NGS; ++i) cout[(s0 + i) * NP + co] = v[i];
+                }
+        }
+#pragma unroll
+        for (int s = 0; s < WIN; ++s)
+#pragma unroll
+            for (int co = 0; co < P; ++co)
+                acc[co] = __builtin_amdgcn_mfma_f32_32x32x2f32(abuf[w & 1][s][co], bbuf[w & 1][s],
+                                                               acc[co], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int NSTEP>
+constexpr int swin() { return NSTEP < SWIN ? NSTEP : SWIN; }
+
+// BN/ReLU epilogue of output tiles co0 .. co0+P-1 of a C-channel layer
+template <int P, int C>
+__device__ __forceinline__ void epi(const float *ab, int co0, int h, f32x16 (&acc)[P]) {
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int c = chan(co0 + i, q, h);
+            acc[i][q] = fmaxf(fadd_rn(fmul_rn(acc[i][q], ab[c]), ab[C + c]), 0.f);
+        }
+}
+
+// tile co of an activation (channels chan(co, q, h), row j) into a row-major LDS buffer
+template <int LDSW>
+__device__ __forceinline__ void put_tile(float *buf, int co, int j, int h, const f32x16 &v) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<float4 *>(buf + j * LDSW + co * 32 + 8 * r + 4 * h) =
+            make_float4(v[4 * r], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+}
+
+// B loader for a chained layer input: k-step st = ct*16 + q <-> channel chan(ct, q, h)
+struct ChanB {
+    const float *row;  // buf + j * LDSW
+    int h;
+    __device__ __forceinline__ void operator()(int st0, float (&v)[4]) const {
+        const int ct = st0 >> 4, r = (st0 & 15) >> 2;
+        const float4 t = *reinterpret_cast<const float4 *>(row + ct * 32 + 8 * r + 4 * h);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    }
+};
+
+}  // namespace hreg_split

@@ -43,6 +43,7 @@ SPLIT_L2 = False
 SPLIT_L3 = True
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
 FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
+FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip)
 
 
 @dataclass
@@ -145,10 +146,14 @@ class PreparedWeights:
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
                            for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
         self.nbr_table = nbr_head_table(self.coarse_convs2, 256)
+        self.head_table = {("det", lvl): mlp_head_table(self.det_head[lvl]) for lvl in range(3)}
+        self.head_table["coarse"] = mlp_head_table(self.coarse_head)
+        for name in ("fine_corres_2", "fine_corres_1"):
+            self.head_table[name] = mlp_head_table(self.fine[name][1])
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
                      "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2s_table",
                      "l3s_table", "fine_table",
-                     "nbr_table", "mlpx"):
+                     "nbr_table", "head_table", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
 
@@ -243,6 +248,15 @@ def nbr_head_table(convs, C: int) -> torch.Tensor:
              _grouped(frag_layer(convs[2].W), T1, T1 * 16)]
     for lin in convs:
         parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def mlp_head_table(head) -> torch.Tensor:
+    """Table of mlp_head.hip (HCfg): mlp1 and mlp2 fragments (frag_layer, 4 k-steps
+    innermost per lane), alpha1, beta1, alpha2, beta2, w3, b3 (+3 pad)."""
+    m1, m2, w3, b3 = head
+    parts = [_group4(frag_layer(m1.W), 4), _group4(frag_layer(m2.W), 4), m1.alpha, m1.beta,
+             m2.alpha, m2.beta, w3, b3, torch.zeros(3)]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
 
 
@@ -540,10 +554,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         att_feat = _empty(G, LEVELS[0][3][-1], device=dev)
         desc = _empty(G, LEVELS[0][5], device=dev)
         call("hreg_group_l1", P.l1_table, geom, kx, G, kp, att_feat, desc, _stream())
-        m1, m2, w3, b3 = P.det_head[lvl]
-        s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)
-        s = gemm([_seg(s, 0, s.shape[1])], m2, G)
-        sig, wnext = head_out(s, s.shape[1], nb, M, w3, b3, _lib.HREG_HEAD_SOFTPLUS,
+        sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)
         return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
     if (lvl == 1 and FUSED_L2) or (lvl == 2 and FUSED_L3):
@@ -558,10 +569,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
             name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
                            ("hreg_group_l3", P.l3_table))
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, _stream())
-        m1, m2, w3, b3 = P.det_head[lvl]
-        s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)
-        s = gemm([_seg(s, 0, s.shape[1])], m2, G)
-        sig, wnext = head_out(s, s.shape[1], nb, M, w3, b3, _lib.HREG_HEAD_SOFTPLUS,
+        sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)
         return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
     segs = [_seg(geom, 0, 4)]
@@ -572,10 +580,8 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
     h = gemm([_seg(h, 0, h.shape[1])], P.det[lvl][1], R)
     emb = gemm([_seg(h, 0, h.shape[1])], P.det[lvl][2], R)
     attw, att_feat, kp = attend(emb, G, k, vals=emb, xyz_rows=kx, want_attw=True)
-    m1, m2, w3, b3 = P.det_head[lvl]
-    s = gemm([_seg(att_feat, 0, att_feat.shape[1])], m1, G)
-    s = gemm([_seg(s, 0, s.shape[1])], m2, G)
-    sig, wnext = head_out(s, s.shape[1], nb, M, w3, b3, _lib.HREG_HEAD_SOFTPLUS, want_weights=True)
+    sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
+                          want_weights=True)
     # descriptor (layers.py:200-209)
     x = gemm(segs, P.desc[lvl][0], R)
     x = gemm([_seg(x, 0, x.shape[1])], P.desc[lvl][1], R)
@@ -607,11 +613,36 @@ def feature_extraction(P: PreparedWeights, points, use_weights=True, l1=None):
     return out
 
 
-def _mlp_weights(x, head, G, nclouds, rows):
-    m1, m2, w3, b3 = head
-    s = gemm([_seg(x, 0, x.shape[1])], m1, G)
+def _head_layers(P: PreparedWeights, key):
+    if key == "coarse":
+        return P.coarse_head
+    if isinstance(key, tuple):
+        return P.det_head[key[1]]
+    return P.fine[key][1]
+
+
+def mlp_head(P: PreparedWeights, key, x, nclouds, rows, mode, want_weights=False):
+    """mlp1 -> mlp2 -> mlp3 + softplus(+0.001) / sigmoid over per-keypoint rows x
+    [nclouds*rows][C] (layers.py:124-132,161-163; 262-268,389-394; 425-431,451-452).
+    key: ("det", lvl), "coarse" or the FineReg name.  One mlp_head.hip launch, or
+    with FUSED_HEAD off two GEMMs + hreg_head_out.  Returns (out, weights or None)."""
+    C = x.shape[1]
+    if FUSED_HEAD and C in (64, 128, 256, 512) and (nclouds * rows) % 32 == 0:
+        dev = x.device
+        out = _empty(nclouds * rows, device=dev)
+        wout = _empty(nclouds * rows, device=dev) if want_weights else None
+        call("hreg_mlp_head", P.head_table[key], C, x, C, nclouds, rows, mode, out, wout,
+             _stream())
+        return out, wout
+    m1, m2, w3, b3 = _head_layers(P, key)
+    G = nclouds * rows
+    s = gemm([_seg(x, 0, C)], m1, G)
     s = gemm([_seg(s, 0, s.shape[1])], m2, G)
-    w, _ = head_out(s, s.shape[1], nclouds, rows, w3, b3, _lib.HREG_HEAD_SIGMOID)
+    return head_out(s, s.shape[1], nclouds, rows, w3, b3, mode, want_weights=want_weights)
+
+
+def _mlp_weights(P: PreparedWeights, key, x, nclouds, rows):
+    w, _ = mlp_head(P, key, x, nclouds, rows, _lib.HREG_HEAD_SIGMOID)
     return w
 
 
@@ -662,7 +693,7 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[1], R)
     f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[2], R)
     _, att, corres = attend(f, B * N1, k, vals=f, xyz_rows=kx)
-    w = _mlp_weights(att, P.coarse_head, B * N1, B, N1)
+    w = _mlp_weights(P, "coarse", att, B, N1)
     return corres.view(B, N1, 3), w.view(B, N1)
 
 
@@ -687,7 +718,7 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
         att = _empty(B * N, N1, device=dev)
         call("hreg_fine_head", P.fine_table[name], C, small, src_desc, dst_desc, gidx, kx, B * N,
              corres, att, _stream())
-        w = _mlp_weights(att, head, B * N, B, N)
+        w = _mlp_weights(P, name, att, B, N)
         if return_att:
             return corres.view(B, N, 3), w.view(B, N), att
         return corres.view(B, N, 3), w.view(B, N)
@@ -701,7 +732,7 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
     f = gemm([_seg(f, 0, f.shape[1])], convs[1], R)
     f = gemm([_seg(f, 0, f.shape[1])], convs[2], R)
     _, att, corres = attend(f, B * N, k, vals=f, xyz_rows=kx)
-    w = _mlp_weights(att, head, B * N, B, N)
+    w = _mlp_weights(P, name, att, B, N)
     if return_att:
         return corres.view(B, N, 3), w.view(B, N), att
     return corres.view(B, N, 3), w.view(B, N)

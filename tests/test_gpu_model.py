@@ -267,6 +267,52 @@ def test_fused_nbr_head_matches_layerwise(net):
     torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("key,C,rows,mode", [(("det", 0), 64, 1024, 0), (("det", 1), 128, 512, 0),
+                                           (("det", 2), 256, 256, 0), ("coarse", 512, 256, 1),
+                                           ("fine_corres_2", 256, 512, 1),
+                                           ("fine_corres_1", 128, 1024, 1)])
+def test_fused_mlp_head_matches_layerwise(net, key, C, rows, mode):
+    """mlp_head.hip (mlp1 -> mlp2 -> mlp3 + softplus/sigmoid in one launch) against two
+    GEMMs + hreg_head_out; fp32 summation order differs, so within 1e-4 (and the
+    per-cloud sigma -> weight normalisation, models.py:30-32)."""
+    from pcd_reg_hregnet_amd import _lib, engine
+    P = net.prepared(torch.device("cuda"))
+    g = torch.Generator().manual_seed(7)
+    nclouds = 3
+    x = torch.relu(torch.randn(nclouds * rows, C, generator=g)).cuda()
+    outs = []
+    with torch.no_grad():
+        for fused in (True, False):
+            old = engine.FUSED_HEAD
+            engine.FUSED_HEAD = fused
+            try:
+                outs.append(engine.mlp_head(P, key, x, nclouds, rows, mode, want_weights=mode == 0))
+            finally:
+                engine.FUSED_HEAD = old
+    torch.cuda.synchronize()
+    (o_f, w_f), (o_r, w_r) = outs
+    torch.testing.assert_close(o_f, o_r, rtol=1e-4, atol=1e-6)
+    if mode == _lib.HREG_HEAD_SOFTPLUS:
+        torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-6)
+    # one pair's rows give the same bits alone as inside the batch
+    with torch.no_grad():
+        one, _ = engine.mlp_head(P, key, x[rows:2 * rows].contiguous(), 1, rows, mode)
+    assert torch.equal(one, o_f[rows:2 * rows])
+
+
+def test_mlp_head_rejects_bad_shapes(net):
+    from pcd_reg_hregnet_amd import _lib
+    P = net.prepared(torch.device("cuda"))
+    x = torch.zeros(64, 96, device="cuda")
+    out = torch.empty(64, device="cuda")
+    with pytest.raises(RuntimeError, match="unsupported"):
+        _lib.call("hreg_mlp_head", P.head_table["coarse"], 96, x, 96, 1, 64, 0, out, None,
+                  _lib.stream_handle())
+    with pytest.raises(RuntimeError, match="unsupported"):
+        _lib.call("hreg_mlp_head", P.head_table["coarse"], 64, x, 96, 1, 48, 0, out, None,
+                  _lib.stream_handle())
+
+
 @pytest.fixture(scope="module")
 def net_v2():
     from helpers import state_dict_v2_torch
