@@ -182,6 +182,31 @@ int hreg_mlp_head_table_floats(int C);
 int hreg_mlp_head(const float *table, int C, const float *x, int ldx, int nclouds,
                   int rows_per_cloud, int mode, float *out, float *weights_out, void *stream);
 
+/* ---- data side in front of the path (perturb.hip) ----
+ * Twists x = (w, v) [n][6], SE(3) matrices g [n][16] row-major. */
+/* g = SE3.exp(x) (transform/rodrigues.py:526-553) */
+int hreg_se3_exp(const float *x, int n, float *g, void *stream);
+/* x = SE3.log(g) (transform/rodrigues.py:571-582 with SO3.log :330-370) */
+int hreg_se3_log(const float *g, int n, float *x, void *stream);
+#define HREG_TWIST_UNIFORM 0          /* dataset_transforms.py:96-98 */
+#define HREG_TWIST_GAUSSIAN 1         /* dataset_transforms.py:100-105 */
+#define HREG_TWIST_INVERSE_GAUSSIAN 2 /* dataset_transforms.py:107-122 */
+/* UniformTransformSE3.generate_transform (transform/dataset_transforms.py:79-126) from
+ * its random draws: samples [n][6] (w draw, t draw), amp_tran [n][2] (radians, metres)
+ * -> x [n][6] = SE3.log([SO3.exp(w) | t]) */
+int hreg_twists_from_samples(const float *samples, const float *amp_tran, int n, int distribution,
+                             float *x, void *stream);
+/* TruckScenesPerturbation.lidar_to_lidar (dataset/man_dataset.py:606-631) for nb
+ * clouds: out[b] = SE3.transform(exp(x[b]), pts[b]), pts/out [nb][n][3]; igt [nb][16]
+ * = exp(x[b]) and gt [nb][16] = igt^-1 (train/train_reg_v0.py:268-271), both optional. */
+int hreg_perturb_clouds(const float *pts, const float *x, int nb, int n, float *out, float *igt,
+                        float *gt, void *stream);
+/* PointCloudFilter.remove_points_by_range (dataset/dataset_utils.py:113-127) for nb
+ * clouds [nb][n][3] (+ intensity [nb][n], optional): the points with ||p|| < max_range,
+ * in order, packed at the front of out[b] / out_intensity[b]; counts [nb] int32. */
+int hreg_range_filter(const float *pts, const float *intensity, int nb, int n, float max_range,
+                      float *out, float *out_intensity, int32_t *counts, void *stream);
+
 /* norms[r] = sqrt(sum_c x[r][c]^2), x [R][ldx] */
 int hreg_row_norms(const float *x, int R, int C, int ldx, float *norms, void *stream);
 

@@ -479,3 +479,120 @@ def calib_metrics(pred_tf, gt_tf):
     theta = np.rad2deg(np.arccos(cos)).astype(f)
     tn = np.sqrt(np.sum(E[:, :3, 3] ** 2, axis=1)).astype(f)
     return per.astype(f), np.array([theta.mean(), tn.mean()], f)
+
+
+# ------------------------------------------- data side
+def _sinc(t, kind):
+    """sinc1/2/3 with the O(t^8) Taylor branches below 0.01 (transform/rodrigues.py:5-19,
+    100-114, 132-145), float32 elementwise."""
+    t = np.asarray(t, np.float32)
+    t2 = t * t
+    small = np.abs(t) < np.float32(0.01)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if kind == 1:
+            tay = 1 - t2 / 6 * (1 - t2 / 20 * (1 - t2 / 42))
+            reg = np.sin(t) / t
+        elif kind == 2:
+            tay = np.float32(0.5) * (1 - t2 / 12 * (1 - t2 / 30 * (1 - t2 / 56)))
+            reg = (1 - np.cos(t)) / t2
+        else:
+            tay = np.float32(1 / 6) * (1 - t2 / 20 * (1 - t2 / 42 * (1 - t2 / 72)))
+            reg = (t - np.sin(t)) / (t * t * t)
+    return np.where(small, tay, reg).astype(np.float32)
+
+
+def _skew(w):
+    z = np.zeros_like(w[:, 0])
+    return np.stack([np.stack([z, -w[:, 2], w[:, 1]], 1), np.stack([w[:, 2], z, -w[:, 0]], 1),
+                     np.stack([-w[:, 1], w[:, 0], z], 1)], 1)
+
+
+def se3_exp(x):
+    """SE3.exp (transform/rodrigues.py:526-553): x [n, 6] -> g [n, 4, 4], float32."""
+    x = np.asarray(x, np.float32).reshape(-1, 6)
+    w, v = x[:, :3], x[:, 3:]
+    t = np.sqrt((w * w).sum(1)).astype(np.float32)[:, None, None]
+    W = _skew(w)
+    S = W @ W
+    eye = np.eye(3, dtype=np.float32)
+    R = eye + _sinc(t, 1) * W + _sinc(t, 2) * S
+    V = eye + _sinc(t, 2) * W + _sinc(t, 3) * S
+    g = np.zeros((len(x), 4, 4), np.float32)
+    g[:, :3, :3] = R
+    g[:, :3, 3] = (V @ v[:, :, None])[:, :, 0]
+    g[:, 3, 3] = 1
+    return g
+
+
+def so3_log(R):
+    """SO3.log (transform/rodrigues.py:330-370), including the t = pi branch and the
+    NaN-angle case (neither mask: w = 0)."""
+    R = np.asarray(R, np.float32)
+    tr = (R[:, 0, 0] + R[:, 1, 1]) + R[:, 2, 2]
+    with np.errstate(invalid="ignore"):
+        t = np.arccos((tr - 1) / 2).astype(np.float32)
+    sc = _sinc(t, 1)
+    w = np.zeros((len(R), 3), np.float32)
+    for i in range(len(R)):
+        if abs(sc[i]) > 1e-7:
+            d = np.float32(2) * sc[i]
+            w[i] = [(R[i, 2, 1] - R[i, 1, 2]) / d, (R[i, 0, 2] - R[i, 2, 0]) / d,
+                    (R[i, 1, 0] - R[i, 0, 1]) / d]
+        elif abs(sc[i]) <= 1e-7:
+            t2 = t[i] * t[i]
+            A = (R[i] + np.eye(3, dtype=np.float32)) * t2 / 2
+            s3 = np.sign(A[0, 2]) or np.float32(1)
+            s23 = np.sign(A[1, 2]) or np.float32(1)
+            w[i] = [np.sqrt(A[0, 0]), np.sqrt(A[1, 1]) * (s23 * s3), np.sqrt(A[2, 2]) * s3]
+    return w
+
+
+def se3_log(g):
+    """SE3.log (transform/rodrigues.py:571-582, inv_vecs_Xg_ig :400-420)."""
+    g = np.asarray(g, np.float32).reshape(-1, 4, 4)
+    w = so3_log(g[:, :3, :3])
+    t = np.sqrt((w * w).sum(1)).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t2 = t * t
+        eta = np.where(t < 0.01, ((t2 / 40 + 1) * t2 / 42 + 1) * t2 / 720 + np.float32(1 / 12),
+                       (1 - (t / 2) / np.tan(t / 2)) / t2).astype(np.float32)
+    X = _skew(w)
+    H = np.eye(3, dtype=np.float32) - np.float32(0.5) * X + eta[:, None, None] * (X @ X)
+    v = (H @ g[:, :3, 3:])[:, :, 0]
+    return np.concatenate([w, v], 1).astype(np.float32)
+
+
+def twists_from_samples(samples, amp_tran, distribution="uniform"):
+    """UniformTransformSE3.generate_transform (transform/dataset_transforms.py:79-126)
+    from its draws: samples [n, 6] (w draw, t draw), amp_tran [n, 2] float32."""
+    s = np.asarray(samples, np.float32)
+    amp = np.asarray(amp_tran, np.float32)[:, :1]
+    tran = np.asarray(amp_tran, np.float32)[:, 1:]
+    if distribution == "uniform":
+        w = (2 * s[:, :3] - 1) * amp
+        t = (2 * s[:, 3:] - 1) * tran
+    else:
+        w = s[:, :3] / np.sqrt((s[:, :3] ** 2).sum(1, keepdims=True)) * amp
+        u = s[:, 3:] * tran if distribution == "gaussian" else s[:, 3:]
+        t = u / np.sqrt((u * u).sum(1, keepdims=True)) * tran
+    R = se3_exp(np.concatenate([w, np.zeros_like(w)], 1))
+    R[:, :3, 3] = t
+    return se3_log(R)
+
+
+def range_filter(points, intensity, max_range):
+    """PointCloudFilter.remove_points_by_range (dataset/dataset_utils.py:113-127)."""
+    p = np.asarray(points, np.float32)
+    rng = np.sqrt((p[:, 0] * p[:, 0] + p[:, 1] * p[:, 1]) + p[:, 2] * p[:, 2])
+    keep = rng < max_range
+    return p[keep], (None if intensity is None else np.asarray(intensity)[keep])
+
+
+def resample_indices(n, num_points):
+    """PointCloudResampler.__call__ (dataset/dataset_utils.py:189-223): the rows it keeps,
+    drawn from numpy's global RandomState exactly as the reference draws them."""
+    if num_points == -1:
+        return np.arange(n)
+    if n <= num_points:
+        return np.concatenate([np.arange(n), np.random.choice(n, num_points - n, replace=True)])
+    return np.random.choice(n, num_points, replace=False)

@@ -23,6 +23,9 @@ HREG_EPI_AFFINE = 0
 HREG_EPI_COSINE = 1
 HREG_HEAD_SOFTPLUS = 0
 HREG_HEAD_SIGMOID = 1
+HREG_TWIST_UNIFORM = 0
+HREG_TWIST_GAUSSIAN = 1
+HREG_TWIST_INVERSE_GAUSSIAN = 2
 MAX_SEGS = 4
 
 _vp = ctypes.c_void_p
@@ -76,6 +79,11 @@ _SIGS = {
     "hreg_mlp_head": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "hreg_mlp_head_table_floats": [_i],
     "hreg_sigma_weights": [_vp, _i, _i, _vp, _vp],
+    "hreg_se3_exp": [_vp, _i, _vp, _vp],
+    "hreg_se3_log": [_vp, _i, _vp, _vp],
+    "hreg_twists_from_samples": [_vp, _vp, _i, _i, _vp, _vp],
+    "hreg_perturb_clouds": [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp],
+    "hreg_range_filter": [_vp, _vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_apply": [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp],

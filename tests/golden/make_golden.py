@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --metrics-only]   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --metrics-only | --perturb-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -564,8 +564,116 @@ def metrics_fixtures():
     print("calib_metrics.npz written", flush=True)
 
 
+def perturb_fixtures():
+    """The data side in front of the path, from the reference's
+    own transform/rodrigues.py, transform/dataset_transforms.py and
+    dataset/dataset_utils.py (open3d, imported at its top but unused by the range
+    filter and the resampler, is stubbed): SE3 exp/log over small-angle, generic and
+    near-pi twists (+ exact pi rotations), UniformTransformSE3 draws per distribution
+    under torch.manual_seed, apply_transform, the L2L perturbation + the training
+    loop's torch.inverse(igt), the perturbation-file text, the range filter and the
+    resampler under np.random.seed."""
+    import importlib.util
+    pkg = types.ModuleType("transform")
+    pkg.__path__ = [os.path.join(REF, "transform")]
+    sys.modules["transform"] = pkg
+    from transform.rodrigues import SE3, SO3  # noqa: E402  (reference code)
+    from transform.dataset_transforms import UniformTransformSE3  # noqa: E402
+    sys.modules.setdefault("open3d", types.ModuleType("open3d"))
+    spec = importlib.util.spec_from_file_location("ref_dataset_utils",
+                                                  os.path.join(REF, "dataset/dataset_utils.py"))
+    DU = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(DU)
+    from pcd_reg_hregnet_amd import synthetic
+    se3, so3 = SE3(), SO3()
+    out = {}
+    rng = np.random.default_rng(2024)
+    axes = rng.normal(size=(96, 3))
+    axes /= np.linalg.norm(axes, axis=1, keepdims=True)
+    ang = np.concatenate([rng.uniform(1e-5, 9e-3, 16), rng.uniform(0.011, 0.5, 32),
+                          rng.uniform(0.5, 3.0, 32), np.pi - rng.uniform(1e-4, 1e-2, 15), [0.0]])
+    x = np.concatenate([axes * ang[:, None], rng.normal(0, 0.5, (96, 3))], 1).astype(np.float32)
+    xt = torch.from_numpy(x)
+    g = se3.exp(xt)
+    out["se3_x"] = x
+    out["se3_exp"] = g.numpy()
+    out["se3_log"] = se3.log(g).numpy()
+    # exact pi rotations: the sign-fixed branch of SO3.log (rodrigues.py:347-364)
+    pax = np.array([[1, 0, 0], [0, 1, 0], [0, 0, 1], [1, 1, 0], [0.6, -0.8, 0], [1, 2, -2]],
+                   np.float64)
+    pax /= np.linalg.norm(pax, axis=1, keepdims=True)
+    Rpi = np.stack([2 * np.outer(a, a) - np.eye(3) for a in pax]).astype(np.float32)
+    gpi = np.tile(np.eye(4, dtype=np.float32), (len(pax), 1, 1))
+    gpi[:, :3, :3] = Rpi
+    gpi[:, :3, 3] = rng.normal(0, 0.3, (len(pax), 3))
+    out["pi_g"] = gpi
+    out["pi_log"] = se3.log(torch.from_numpy(gpi)).numpy()
+    # UniformTransformSE3 draws (dataset_config: max_rot_error 20, max_trans_error 0.5)
+    for tag, dist, randomly, seed in (("uniform_rand", "uniform", True, 3),
+                                      ("uniform_fixed", "uniform", False, 4),
+                                      ("gaussian_rand", "gaussian", True, 5),
+                                      ("invgauss_rand", "inverse_gaussian", True, 6)):
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        T = UniformTransformSE3(max_deg=20, max_tran=0.5, distribution=dist, mag_randomly=randomly)
+        out[f"twists_{tag}"] = torch.cat([T.generate_transform() for _ in range(24)]).numpy()
+    # apply_transform of one cloud [1, 3, N] (a bare [3, N] fails in the reference's
+    # SE3.transform: rodrigues.py:589 broadcasts [1,3,3] against [3,N,1])
+    s, d, _, _ = synthetic.lidar_batch(4, 2048, seed0=300)
+    T = UniformTransformSE3(max_deg=20, max_tran=0.5, mag_randomly=True)
+    p0 = torch.from_numpy(d[0].T.copy())[None]
+    xa = torch.from_numpy(out["twists_uniform_rand"][:1])
+    out["apply_p0"] = p0.numpy()
+    out["apply_x"] = xa.numpy()
+    out["apply_out"] = T.apply_transform(p0, xa).numpy()
+    out["apply_gt"] = T.gt.numpy()
+    out["apply_igt"] = T.igt.numpy()
+    # L2L batch: man_dataset.py:617-625 per cloud + the loop's torch.inverse(igt)
+    xb = torch.from_numpy(out["twists_uniform_rand"][:4])
+    unc, igts = [], []
+    for b in range(4):
+        igt = se3.exp(xb[b:b + 1])
+        unc.append(se3.transform(igt, torch.from_numpy(d[b].T.copy())[None]).squeeze(0).T)
+        igts.append(igt.squeeze(0))
+    out["l2l_pcd"] = d
+    out["l2l_x"] = xb.numpy()
+    out["l2l_uncalibed"] = torch.stack(unc).numpy()
+    out["l2l_igt"] = torch.stack(igts).numpy()
+    out["l2l_gt"] = torch.inverse(torch.stack(igts)).numpy()
+    # perturbation file text (man_dataset.py:536-545), seed 7, 10 lines
+    torch.manual_seed(7)
+    T = UniformTransformSE3(max_deg=20, max_tran=0.5, distribution="uniform", mag_randomly=True)
+    arr = np.zeros([10, 6])
+    for i in range(10):
+        arr[i, :] = T.generate_transform().cpu().numpy()
+    path = os.path.join(HERE, "_perturb.txt")
+    np.savetxt(path, arr, delimiter=",")
+    out["perturb_file_text"] = np.array(open(path).read())
+    os.remove(path)
+    # range filter (max_range 80, dataset/config.json:16) and resampler
+    s2, d2, _, _ = synthetic.lidar_batch(1, 8192, seed0=310)
+    cloud = np.concatenate([s2[0], d2[0] * 2.2]).astype(np.float32)  # ranges across 80 m
+    inten = rng.uniform(0, 1, len(cloud)).astype(np.float32)
+    filt = DU.PointCloudFilter(voxel_size=0.01, concat="none", max_range=80)
+    fp, fi = filt.remove_points_by_range(cloud, inten)
+    out["filter_in"], out["filter_in_int"] = cloud, inten
+    out["filter_out"], out["filter_out_int"] = fp, fi
+    for tag, n_keep, seed in (("pad", 3000, 11), ("sub", 6000, 12)):
+        np.random.seed(seed)
+        rs = DU.PointCloudResampler(num_points=4096)
+        rp, ri = rs(fp[:n_keep], fi[:n_keep])
+        out[f"resample_{tag}_n"] = np.array(n_keep)
+        out[f"resample_{tag}_seed"] = np.array(seed)
+        out[f"resample_{tag}_out"], out[f"resample_{tag}_int"] = rp, ri
+    np.savez_compressed(os.path.join(HERE, "perturb.npz"), **out)
+    print("perturb.npz written", flush=True)
+
+
 def main():
     pu = install_shims()
+    if "--perturb-only" in sys.argv:
+        perturb_fixtures()
+        return
     if "--metrics-only" in sys.argv:
         metrics_fixtures()
         return

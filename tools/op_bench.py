@@ -85,6 +85,30 @@ def main():
                                                       kp, att, desc, _lib.stream_handle()))
         flops = 2.0 * 32 * (2 * (68 * 64 + 64 * 64 + 64 * 128) + 384 * 64 + 64 * 128) * G
         res["group_l2_tflops"] = flops / res["group_l2_ms"] / 1e9
+    if a.what in ("perturb", "all"):
+        # data side (perturb.hip): L2L perturbation of 64 clouds x 16384 points (HBM:
+        # 12 B in + 12 B out per point) and the range filter over 64 raw clouds of
+        # 65536 points (12 B in + <= 12 B out per point)
+        from pcd_reg_hregnet_amd import perturb
+        B, N = 64, 16384
+        pts = torch.from_numpy(rng.uniform(-60, 60, (B, N, 3)).astype(np.float32)).cuda()
+        x = torch.from_numpy(rng.normal(0, 0.2, (B, 6)).astype(np.float32)).cuda()
+        out = torch.empty_like(pts)
+        igt = torch.empty(B, 16, device="cuda")
+        gt = torch.empty(B, 16, device="cuda")
+        ms = timeit(lambda: _lib.call("hreg_perturb_clouds", pts, x, B, N, out, igt, gt,
+                                      _lib.stream_handle()), reps=20)
+        res["perturb_clouds_64x16384_us"] = ms * 1e3
+        res["perturb_clouds_GBps"] = B * N * 24 / ms / 1e6
+        N2 = 65536
+        raw = torch.from_numpy(rng.uniform(-100, 100, (B, N2, 3)).astype(np.float32)).cuda()
+        filt = perturb.PointCloudFilter(80.0)
+        ms = timeit(lambda: filt.remove_points_by_range(raw), reps=20)
+        kept = int(filt.remove_points_by_range(raw)[2].sum())
+        res["range_filter_64x65536_us"] = ms * 1e3
+        res["range_filter_GBps"] = (B * N2 * 12 + kept * 12) / ms / 1e6
+        T = perturb.UniformTransformSE3(20, 0.5, "uniform", True)
+        res["generate_transforms_64_us"] = timeit(lambda: T.generate_transforms(64), reps=20) * 1e3
     print({k: round(v, 4) for k, v in res.items()})
 
 
