@@ -207,6 +207,33 @@ int hreg_perturb_clouds(const float *pts, const float *x, int nb, int n, float *
 int hreg_range_filter(const float *pts, const float *intensity, int nb, int n, float max_range,
                       float *out, float *out_intensity, int32_t *counts, void *stream);
 
+/* ---- Model_V2 training losses (mi_loss.hip) ---- */
+#define HREG_REDUCE_NONE 0
+#define HREG_REDUCE_MEAN 1
+#define HREG_REDUCE_SUM 2
+/* ChamferDistanceLoss(scale, reduction) (losses/chamfer_loss.py:20-36) over the
+ * chamfer_distance extension's nearest squared distances: p0 [nb][n][3], p1 [nb][m][3]
+ * (divided by scale first) -> d01 [nb][n], d10 [nb][m] (+ argmin idx, optional),
+ * per_pair [nb] = (mean sqrt d01 + mean sqrt d10) / 2 (optional), out [1] = mean / sum
+ * of per_pair (reduction MEAN / SUM; NONE writes per_pair only). */
+int hreg_chamfer(const float *p0, const float *p1, int nb, int n, int m, float scale, int reduction,
+                 float *d01, float *d10, int32_t *idx01, int32_t *idx10, float *per_pair, float *out,
+                 void *stream);
+/* DeepMILoss Jensen-Shannon terms (losses/mi_loss_v2.py:56-64): out [3] = (0.5 (Em - Ej),
+ * Ej, Em) from the discriminator outputs t_joint, t_marg [n]; g_joint / g_marg
+ * (optional) = d out[0] / d t. */
+int hreg_js_loss(const float *t_joint, const float *t_marg, int n, float *out, float *g_joint,
+                 float *g_marg, void *stream);
+/* t[r] = act(h[r] . w + b) (the 1-output conv3 / l0 of the discriminators,
+ * mi_loss_v2.py:13,33); b optional, relu 0/1.  _bwd: dh = g' w^T, dw = g'^T h,
+ * db = sum g' with g' = g [t > 0] when relu (each output optional). */
+int hreg_rowdot(const float *h, int R, int C, const float *w, const float *b, int relu, float *t,
+                void *stream);
+int hreg_rowdot_bwd(const float *g, const float *t, int relu, const float *h, int R, int C,
+                    const float *w, float *dh, float *dw, float *db, void *stream);
+/* dx = dy [y > 0] */
+int hreg_relu_bwd(const float *dy, const float *y, size_t n, float *dx, void *stream);
+
 /* norms[r] = sqrt(sum_c x[r][c]^2), x [R][ldx] */
 int hreg_row_norms(const float *x, int R, int C, int ldx, float *norms, void *stream);
 

@@ -596,3 +596,47 @@ def resample_indices(n, num_points):
     if n <= num_points:
         return np.concatenate([np.arange(n), np.random.choice(n, num_points - n, replace=True)])
     return np.random.choice(n, num_points, replace=False)
+
+
+# ------------------------------------- Model_V2 training losses (8f rank 2)
+def chamfer_loss(template, source, scale=1.0, reduction="mean"):
+    """ChamferDistanceLoss (losses/chamfer_loss.py:10-36) with the chamfer_distance
+    extension's nearest squared distances restated (float32, (dx^2+dy^2)+dz^2)."""
+    a = np.asarray(template, np.float32) / np.float32(scale)
+    b = np.asarray(source, np.float32) / np.float32(scale)
+    d = a[:, :, None, :] - b[:, None, :, :]
+    dist = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+    c01 = np.sqrt(dist.min(2)).mean(-1)
+    c10 = np.sqrt(dist.min(1)).mean(-1)
+    per = ((c01 + c10) / 2).astype(np.float32)
+    return {"none": per, "mean": per.mean(0), "sum": per.sum(0)}[reduction]
+
+
+def _softplus(z):
+    return np.where(z > 20, z, np.log1p(np.exp(np.minimum(z, 20))))
+
+
+def deep_mi_loss(params, x_global, x_global_prime, x_local, x_local_prime, c_local, c_global):
+    """DeepMILoss(512, 128).forward (losses/mi_loss_v2.py:42-79): JS estimator of the
+    local ([B, C, N] point rows) and global ([B, C]) discriminators, called as d(c, x)."""
+    relu = lambda v: np.maximum(v, 0)  # noqa: E731
+
+    def local_d(c, x):
+        h = np.concatenate([c, x], 1).transpose(0, 2, 1)  # [B, N, 2C]
+        for k in ("conv1", "conv2", "conv3"):
+            h = relu(h @ params[f"local_d.{k}.weight"][:, :, 0].T)
+        return h[..., 0]
+
+    def global_d(c, x):
+        h = np.concatenate([c, x], 1)
+        for k in ("c1", "c2", "c3"):
+            h = relu(h @ params[f"global_d.{k}.weight"][:, :, 0].T)
+        return h @ params["global_d.l0.weight"].T + params["global_d.l0.bias"]
+
+    def js(d, c, x, xp):
+        Ej = -_softplus(-d(c, x)).mean()
+        Em = _softplus(d(c, xp)).mean()
+        return 0.5 * (Em - Ej)
+    loc = js(local_d, c_local, x_local, x_local_prime)
+    glo = js(global_d, c_global, x_global, x_global_prime)
+    return np.float32(loc + glo), np.float32(loc), np.float32(glo)

@@ -26,6 +26,9 @@ HREG_HEAD_SIGMOID = 1
 HREG_TWIST_UNIFORM = 0
 HREG_TWIST_GAUSSIAN = 1
 HREG_TWIST_INVERSE_GAUSSIAN = 2
+HREG_REDUCE_NONE = 0
+HREG_REDUCE_MEAN = 1
+HREG_REDUCE_SUM = 2
 MAX_SEGS = 4
 
 _vp = ctypes.c_void_p
@@ -84,6 +87,11 @@ _SIGS = {
     "hreg_twists_from_samples": [_vp, _vp, _i, _i, _vp, _vp],
     "hreg_perturb_clouds": [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp],
     "hreg_range_filter": [_vp, _vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp],
+    "hreg_chamfer": [_vp, _vp, _i, _i, _i, ctypes.c_float, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_js_loss": [_vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_rowdot": [_vp, _i, _i, _vp, _vp, _i, _vp, _vp],
+    "hreg_rowdot_bwd": [_vp, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_relu_bwd": [_vp, _vp, ctypes.c_size_t, _vp, _vp],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_apply": [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp],

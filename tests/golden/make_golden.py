@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --metrics-only | --perturb-only]   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --metrics-only | --perturb-only | --mi-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -669,8 +669,74 @@ def perturb_fixtures():
     print("perturb.npz written", flush=True)
 
 
+def mi_fixtures():
+    """Model_V2's training losses from the reference's own
+    losses/mi_loss_v2.py (DeepMILoss(512, 128) as train/train_reg_v6.py:253-255 builds
+    it, seeded weights, V2-shaped inputs: weights/sigmas [B, 512], feats/desc
+    [B, 128, 512]) -- loss and the gradients of every input and parameter -- and
+    losses/chamfer_loss.py (ChamferDistanceLoss(scale=50, 'mean'/'none')) over a
+    stand-in for the absent third-party chamfer_distance extension: brute-force
+    nearest squared distances (its published semantics; the library itself is
+    parity-unpinned)."""
+    import importlib.util
+
+    class _ChamferDistance(torch.nn.Module):
+        def forward(self, a, b):
+            d = ((a[:, :, None, :] - b[:, None, :, :]) ** 2).sum(-1)
+            d1, i1 = d.min(2)
+            d2, i2 = d.min(1)
+            return d1, d2, i1, i2
+    cd = types.ModuleType("chamfer_distance")
+    cd.ChamferDistance = _ChamferDistance
+    sys.modules["chamfer_distance"] = cd
+    mods = {}
+    for name in ("mi_loss_v2", "chamfer_loss"):
+        spec = importlib.util.spec_from_file_location("ref_" + name,
+                                                      os.path.join(REF, f"losses/{name}.py"))
+        mods[name] = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mods[name])
+    torch.manual_seed(21)
+    mi = mods["mi_loss_v2"].DeepMILoss(global_in_channels=512, local_in_channels=128)
+    B = 3
+    g = torch.Generator().manual_seed(22)
+    inp = {
+        "x_global": torch.rand(B, 512, generator=g),                       # weights_2 (sigmoid)
+        "x_global_prime": torch.rand(B, 512, generator=g),
+        "c_global": torch.rand(B, 512, generator=g) * 2 + 0.01,            # sigmas_2 (softplus)
+        "x_local": torch.relu(torch.randn(B, 128, 512, generator=g)),      # mlpx feats (ReLU)
+        "x_local_prime": torch.relu(torch.randn(B, 128, 512, generator=g)),
+        "c_local": torch.relu(torch.randn(B, 128, 512, generator=g)),      # desc_2 (k-max of ReLU)
+    }
+    leaves = {k: v.clone().requires_grad_(True) for k, v in inp.items()}
+    loss = mi(**leaves)
+    loss.backward()
+    out = {f"in_{k}": v.numpy() for k, v in inp.items()}
+    out.update({f"grad_{k}": v.grad.numpy() for k, v in leaves.items()})
+    out.update({f"param_{k}": v.detach().numpy() for k, v in mi.state_dict().items()})
+    out.update({f"pgrad_{k}": p.grad.numpy() for k, p in mi.named_parameters()})
+    out["loss"] = loss.detach().numpy()
+    with torch.no_grad():
+        out["loss_local"] = mi.compute_local_loss(inp["x_local"], inp["x_local_prime"],
+                                                  inp["c_local"]).numpy()
+        out["loss_global"] = mi.compute_global_loss(inp["x_global"], inp["x_global_prime"],
+                                                    inp["c_global"]).numpy()
+    from pcd_reg_hregnet_amd import synthetic
+    s, d, _, _ = synthetic.lidar_batch(3, 512, seed0=500)
+    a, b = torch.from_numpy(s), torch.from_numpy(d[:, :400].copy())
+    CL = mods["chamfer_loss"].ChamferDistanceLoss
+    out["chamfer_a"], out["chamfer_b"] = s, d[:, :400].copy()
+    out["chamfer_mean"] = CL(scale=50.0, reduction="mean")(a, b).numpy()
+    out["chamfer_none"] = CL(scale=50.0, reduction="none")(a, b).numpy()
+    out["chamfer_sum"] = CL(scale=50.0, reduction="sum")(a, b).numpy()
+    np.savez_compressed(os.path.join(HERE, "mi_chamfer.npz"), **out)
+    print("mi_chamfer.npz written", flush=True)
+
+
 def main():
     pu = install_shims()
+    if "--mi-only" in sys.argv:
+        mi_fixtures()
+        return
     if "--perturb-only" in sys.argv:
         perturb_fixtures()
         return
