@@ -294,11 +294,12 @@ int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, float *mean
 /* out = act(gamma * (y - mean) * invstd + beta), act = ReLU if relu (out may alias y) */
 int hreg_bn_apply(const float *y, int R, int C, const float *mean, const float *invstd,
                   const float *gamma, const float *beta, int relu, float *out, void *stream);
-/* backward of hreg_bn_apply given dout (and out for the ReLU mask): dgamma, dbeta [C],
- * dy [R][C] (the batch-statistics BN input gradient) */
+/* backward of hreg_bn_apply given dout: dgamma, dbeta [C], dy [R][C] (the
+ * batch-statistics BN input gradient).  ReLU mask: out > 0 when out is given, else
+ * recomputed bit-identically from y, gamma and beta (one fewer [R][C] stream). */
 int hreg_bn_backward(const float *dout, const float *out, const float *y, int R, int C,
-                     const float *mean, const float *invstd, const float *gamma, int relu,
-                     void *ws, float *dy, float *dgamma, float *dbeta, void *stream);
+                     const float *mean, const float *invstd, const float *gamma, const float *beta,
+                     int relu, void *ws, float *dy, float *dgamma, float *dbeta, void *stream);
 /* running = (1 - momentum) * running + momentum * batch (nn.BatchNorm's momentum 0.1) */
 int hreg_bn_running_update(const float *mean, const float *var_unbiased, int C, float momentum,
                            float *running_mean, float *running_var, void *stream);

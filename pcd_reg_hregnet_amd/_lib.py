@@ -95,7 +95,7 @@ _SIGS = {
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_apply": [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp],
-    "hreg_bn_backward": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_bn_backward": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_running_update": [_vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp],
     "hreg_col_sum": [_vp, _i, _i, _vp, _vp, _vp],
     "hreg_gemm_tn": [_vp, _i, _vp, _i, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp],

@@ -30,8 +30,9 @@ inline int cr_width_log2(int C) { return C <= 16 ? 4 : (C <= 32 ? 5 : 6); }
 template <int MODE>
 __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
     const float *__restrict__ x, const float *__restrict__ out, const float *__restrict__ y,
-    const float *__restrict__ mean, const float *__restrict__ invstd, int relu, int R, int C,
-    int rows_per_split, int cw_log2, double *__restrict__ partial) {
+    const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ gamma,
+    const float *__restrict__ beta, int relu, int R, int C, int rows_per_split, int cw_log2,
+    double *__restrict__ partial) {
     __shared__ double s0[CR_THREADS], s1[CR_THREADS];
     const int cw = 1 << cw_log2, nrl = CR_THREADS >> cw_log2;
     const int cl = threadIdx.x & (cw - 1), rl = threadIdx.x >> cw_log2;
@@ -40,8 +41,12 @@ __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
     const int r1 = min(R, r0 + rows_per_split);
     double a = 0.0, b = 0.0;
     if (c < C) {
-        float mu = 0.f, is = 0.f;
-        if (MODE == 1) { mu = mean[c]; is = invstd[c]; }
+        float mu = 0.f, is = 0.f, ga = 0.f, be = 0.f;
+        if (MODE == 1) {
+            mu = mean[c];
+            is = invstd[c];
+            if (relu && !out) { ga = gamma[c]; be = beta[c]; }
+        }
 #pragma unroll 4
         for (int r = r0 + rl; r < r1; r += nrl) {
             const size_t i = (size_t)r * C + c;
@@ -51,8 +56,13 @@ __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
                 b += v * v;
             } else if (MODE == 1) {
                 float g = x[i];
-                if (relu && !(out[i] > 0.f)) g = 0.f;
                 const float xh = fmul_rn(fsub_rn(y[i], mu), is);
+                if (relu) {
+                    // the forward's ReLU mask: out > 0, or recomputed bit-identically
+                    // from y as bn_apply computed out (no third stream to read)
+                    const bool on = out ? out[i] > 0.f : fadd_rn(fmul_rn(xh, ga), be) > 0.f;
+                    if (!on) g = 0.f;
+                }
                 a += (double)g;
                 b += (double)g * (double)xh;
             } else {
@@ -137,15 +147,16 @@ __global__ void bn_apply_kernel(const float *__restrict__ y, const float *__rest
 __global__ void bn_backward_kernel(const float *__restrict__ dout, const float *__restrict__ out,
                                    const float *__restrict__ y, const float *__restrict__ mean,
                                    const float *__restrict__ invstd, const float *__restrict__ gamma,
-                                   const float *__restrict__ dgamma, const float *__restrict__ dbeta,
-                                   int relu, size_t total, int R, int C, float *__restrict__ dy) {
+                                   const float *__restrict__ beta, const float *__restrict__ dgamma,
+                                   const float *__restrict__ dbeta, int relu, size_t total, int R, int C,
+                                   float *__restrict__ dy) {
     const float invR = 1.0f / (float)R;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (size_t)gridDim.x * blockDim.x) {
         const int c = (int)(i % C);
         float g = dout[i];
-        if (relu && !(out[i] > 0.f)) g = 0.f;
         const float xh = fmul_rn(fsub_rn(y[i], mean[c]), invstd[c]);
+        if (relu && !(out ? out[i] > 0.f : fadd_rn(fmul_rn(xh, gamma[c]), beta[c]) > 0.f)) g = 0.f;
         const float t = fsub_rn(fsub_rn(g, fmul_rn(dbeta[c], invR)), fmul_rn(xh, fmul_rn(dgamma[c], invR)));
         dy[i] = fmul_rn(fmul_rn(t, invstd[c]), gamma[c]);
     }
@@ -305,7 +316,9 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g, 
 
 int splits_for(int R, int col_blocks, int min_rows) {
     int S = 1;
-    while (col_blocks * S < 512 && R / (S * 2) >= min_rows && S < 1024) S *= 2;
+    // >= 2048 workgroups (8 per CU) when the rows allow: a streaming reduction needs
+    // several waves per SIMD in flight to reach HBM rate
+    while (col_blocks * S < 2048 && R / (S * 2) >= min_rows && S < 1024) S *= 2;
     return S;
 }
 
@@ -334,7 +347,7 @@ extern "C" int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, 
     const int rps = (R + S - 1) / S;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(col_reduce_kernel<0>, dim3(cb, S), dim3(CR_THREADS), 0, st, y, nullptr, nullptr,
-                       nullptr, nullptr, 0, R, C, rps, cr_width_log2(C), (double *)ws);
+                       nullptr, nullptr, nullptr, nullptr, 0, R, C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
     hipLaunchKernelGGL(col_finalize_kernel<0>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
                        (const double *)ws, S, R, C, eps, mean, invstd, var_unbiased);
@@ -355,23 +368,24 @@ extern "C" int hreg_bn_apply(const float *y, int R, int C, const float *mean, co
 }
 
 extern "C" int hreg_bn_backward(const float *dout, const float *out, const float *y, int R, int C,
-                                const float *mean, const float *invstd, const float *gamma, int relu,
-                                void *ws, float *dy, float *dgamma, float *dbeta, void *stream) {
+                                const float *mean, const float *invstd, const float *gamma,
+                                const float *beta, int relu, void *ws, float *dy, float *dgamma,
+                                float *dbeta, void *stream) {
     if (!dout || !y || !mean || !invstd || !gamma || !ws || !dy || !dgamma || !dbeta || R <= 0 ||
-        C <= 0 || (relu && !out))
+        C <= 0 || (relu && !out && !beta))
         return HREG_ERR_INVALID;
     const int cb = cr_blocks(C), S = splits_for(R, cb, 256);
     const int rps = (R + S - 1) / S;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(col_reduce_kernel<1>, dim3(cb, S), dim3(CR_THREADS), 0, st, dout, out, y, mean,
-                       invstd, relu, R, C, rps, cr_width_log2(C), (double *)ws);
+                       invstd, gamma, beta, relu, R, C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
     hipLaunchKernelGGL(col_finalize_kernel<1>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
                        (const double *)ws, S, R, C, 0.f, dgamma, dbeta, nullptr);
     HREG_CHECK_LAUNCH();
     const size_t total = (size_t)R * C;
     hipLaunchKernelGGL(bn_backward_kernel, dim3(grid1d(total)), dim3(256), 0, st, dout, out, y, mean,
-                       invstd, gamma, dgamma, dbeta, relu, total, R, C, dy);
+                       invstd, gamma, beta, dgamma, dbeta, relu, total, R, C, dy);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -392,7 +406,7 @@ extern "C" int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, 
     const int rps = (R + S - 1) / S;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(col_reduce_kernel<2>, dim3(cb, S), dim3(CR_THREADS), 0, st, x, nullptr, nullptr,
-                       nullptr, nullptr, 0, R, C, rps, cr_width_log2(C), (double *)ws);
+                       nullptr, nullptr, nullptr, nullptr, 0, R, C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
     hipLaunchKernelGGL(col_finalize_kernel<2>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
                        (const double *)ws, S, R, C, 0.f, out, nullptr, nullptr);

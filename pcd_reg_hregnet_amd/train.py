@@ -111,21 +111,22 @@ class _ConvBNAct(torch.autograd.Function):
         if running_mean is not None:
             _lib.call("hreg_bn_running_update", mean, var, C, float(momentum), running_mean,
                       running_var, _stream())
-        ctx.save_for_backward(x, W, y, out, mean, invstd, gamma)
+        ctx.save_for_backward(x, W, y, mean, invstd, gamma, beta)
         ctx.relu = relu
         ctx.has_bias = bias is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, W, y, out, mean, invstd, gamma = ctx.saved_tensors
+        x, W, y, mean, invstd, gamma, beta = ctx.saved_tensors
         dout = dout.contiguous()
         R, C = y.shape
         dev = y.device
         dy = torch.empty_like(y)
         dgamma = torch.empty(C, device=dev)
         dbeta = torch.empty(C, device=dev)
-        _lib.call("hreg_bn_backward", dout, out, y, R, C, mean, invstd, gamma,
+        # the ReLU mask is recomputed from y (bit-identical to bn_apply's): out is not read
+        _lib.call("hreg_bn_backward", dout, None, y, R, C, mean, invstd, gamma, beta,
                   1 if ctx.relu else 0, col_reduce_ws(R, C, dev), dy, dgamma, dbeta, _stream())
         dW = gemm_tn(dy, x) if ctx.needs_input_grad[1] else None
         dbias = col_sum(dy) if ctx.has_bias and ctx.needs_input_grad[2] else None
