@@ -14,7 +14,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhregnet_amd.so")
+# HREG_LIB: an alternative build of the same library (A/B timing experiments only)
+LIB_PATH = os.environ.get("HREG_LIB") or os.path.join(_HERE, "libhregnet_amd.so")
 
 HREG_OK = 0
 _ERRORS = {1: "invalid argument", 2: "kernel launch failed", 3: "unsupported shape"}

@@ -314,11 +314,13 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g, 
     }
 }
 
-int splits_for(int R, int col_blocks, int min_rows) {
+// row splits so that col_blocks x S reaches `target` workgroups (2048 = 8 per CU: a
+// streaming reduction needs several waves per SIMD in flight to reach HBM rate; for
+// the weight-gradient GEMM too, despite the extra N x K partials: A/B 235 vs 232
+// train pairs/s against a 512 target)
+int splits_for(int R, int col_blocks, int min_rows, int target = 2048) {
     int S = 1;
-    // >= 2048 workgroups (8 per CU) when the rows allow: a streaming reduction needs
-    // several waves per SIMD in flight to reach HBM rate
-    while (col_blocks * S < 2048 && R / (S * 2) >= min_rows && S < 1024) S *= 2;
+    while (col_blocks * S < target && R / (S * 2) >= min_rows && S < 1024) S *= 2;
     return S;
 }
 
