@@ -158,7 +158,9 @@ def pmc_traffic(kernel: str):
     path = os.path.join(REPO, "profiles", "r1_traffic.json")
     try:
         per = json.load(open(path))["bytes_per_launch"]
-        names = kernel.split(" + ")  # one launch of each per step: mean over the family
+        # "group_fused_kernel (level 2) + ..." -> the rocprof family names; one launch of
+        # each per step: mean over the family
+        names = [n.split(" (")[0] for n in kernel.split(" + ")]
         return sum(per[n] for n in names) / len(names), os.path.relpath(path, REPO)
     except Exception:
         return None, None

@@ -218,8 +218,23 @@ extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
         dim3 grid((g.R + 63) / 64, (g.N + 63) / 64, g.batch);
         hipLaunchKernelGGL((gemm_nt_kernel<64, 64, 2, 2, 32>), grid, dim3(256), 0, st, g);
     } else {
-        dim3 grid((g.R + 127) / 128, (g.N + 127) / 128, g.batch);
-        hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2, 16>), grid, dim3(256), 0, st, g);
+        // HREG_GEMM_BIG (A/B switch, tools/gemm_profile.py): 0 = 128x128 tiles, K in
+        // 16-deep chunks; 1 = 32-deep chunks (half the barriers and load round trips per
+        // MFMA); 2 = 128x256 tiles, 16-deep.  Same k-order in all three: bit-identical.
+        static const int big = [] {
+            const char *e = getenv("HREG_GEMM_BIG");
+            return e ? atoi(e) : 1;
+        }();
+        if (big == 2 && g.N >= 256) {
+            dim3 grid((g.R + 127) / 128, (g.N + 255) / 256, g.batch);
+            hipLaunchKernelGGL((gemm_nt_kernel<128, 256, 2, 2, 16>), grid, dim3(256), 0, st, g);
+        } else if (big >= 1) {
+            dim3 grid((g.R + 127) / 128, (g.N + 127) / 128, g.batch);
+            hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2, 32>), grid, dim3(256), 0, st, g);
+        } else {
+            dim3 grid((g.R + 127) / 128, (g.N + 127) / 128, g.batch);
+            hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2, 16>), grid, dim3(256), 0, st, g);
+        }
     }
     HREG_CHECK_LAUNCH();
     return HREG_OK;
