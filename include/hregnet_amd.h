@@ -143,6 +143,13 @@ typedef struct {
     float *out;              /* [R][ldo] */
     int ldo;
     int64_t out_batch_stride;
+    /* optional pre-epilogue addends (EPI_AFFINE): acc = (acc + add[0][row0][n]) + add[1][row1][n],
+     * row_i = add[i].gather ? add[i].gather[r] : r / add[i].row_div; k0/kc/rowscale unused.
+     * A 1x1 conv over a concatenation [x_r | u_{r/k} | v_{idx[r]}] is W_x x_r + (W_u u)_{r/k} +
+     * (W_v v)_{idx[r]}: the repeated / gathered parts are multiplied once per source row
+     * (CoarseReg convs_1, layers.py:364-384) and added here. */
+    hreg_seg_t add[2];
+    int nadd;
 } hreg_gemm_t;
 
 int hreg_gemm(const hreg_gemm_t *g, void *stream);

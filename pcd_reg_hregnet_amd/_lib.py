@@ -47,7 +47,8 @@ class Gemm(ctypes.Structure):
                 ("batch", _i), ("ldw", _i), ("w_batch_stride", _i64), ("W", _vp),
                 ("scale", _vp), ("shift", _vp), ("relu", _i), ("epi", _i), ("rnorm", _vp),
                 ("cnorm", _vp), ("rnorm_batch_stride", _i64), ("cnorm_batch_stride", _i64),
-                ("out", _vp), ("ldo", _i), ("out_batch_stride", _i64)]
+                ("out", _vp), ("ldo", _i), ("out_batch_stride", _i64),
+                ("add", Seg * 2), ("nadd", _i)]
 
 
 _SIGS = {

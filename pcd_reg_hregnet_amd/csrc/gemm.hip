@@ -52,7 +52,7 @@ __device__ __forceinline__ float4 load_w4(const hreg_gemm_t &g, int b, int n, in
     return *reinterpret_cast<const float4 *>(p);
 }
 
-template <int BM, int BN, int WM, int WN, int BK>
+template <int BM, int BN, int WM, int WN, int BK, bool ADD = false>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     static_assert(WM * WN == 4, "4 waves");
     static_assert(BK == 16 || BK == 32, "BK");
@@ -150,6 +150,28 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     }
 
     // epilogue: lane l, reg q -> row (q&3) + 8*(q>>2) + 4*h, col l&31
+    // addends first, in a pass with no stores in it, so the (gathered) loads of a
+    // lane's 16 * TM * TN outputs are all in flight together
+    // (own instantiation: the plain kernels keep their register budget)
+#pragma unroll
+    for (int a = 0; a < (ADD ? 2 : 0); ++a) {
+        if (a >= g.nadd) break;
+        const hreg_seg_t &ad = g.add[a];
+        const float *abase = ad.base + (size_t)b * ad.batch_stride;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int r = r0 + wr * WTM + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                const int rr = r < g.R ? r : g.R - 1;
+                const float *arow = abase + (size_t)(ad.gather ? ad.gather[rr] : rr / ad.row_div) * ad.ld;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n0 + wc * WTN + j * 32 + l32;
+                    acc[i][j][q] = fadd_rn(acc[i][j][q], arow[n < g.N ? n : g.N - 1]);
+                }
+            }
+    }
     float *out = g.out + (size_t)b * g.out_batch_stride;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -202,13 +224,22 @@ extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
     if (g.epi == HREG_EPI_COSINE && (!g.rnorm || !g.cnorm)) return HREG_ERR_INVALID;
     for (int s = 0; s < g.nseg; ++s)
         if (!seg_ok(g.seg[s])) return HREG_ERR_INVALID;
+    if (g.nadd < 0 || g.nadd > 2 || (g.nadd && g.epi != HREG_EPI_AFFINE)) return HREG_ERR_INVALID;
+    for (int a = 0; a < g.nadd; ++a) {
+        const hreg_seg_t &ad = g.add[a];
+        if (!ad.base || ad.ld < g.N || (!ad.gather && ad.row_div < 1)) return HREG_ERR_INVALID;
+    }
     if (g.R == 0) return HREG_OK;
     hipStream_t st = as_stream(stream);
     // tile choice: wide tiles (K in 16-deep chunks) for the big layers; 64x64 tiles
     // with 32-deep K chunks when a 128x128 grid would leave most of the 256 CUs idle
     // (the small mlp-head GEMMs: 2x fewer serial chunk round trips per block)
     const long tiles128 = (long)((g.R + 127) / 128) * ((g.N + 127) / 128) * g.batch;
-    if (g.N <= 32) {
+    if (g.nadd) {
+        // the addend GEMMs are short-K (memory-bound epilogue): small tiles, many blocks
+        dim3 grid((g.R + 63) / 64, (g.N + 63) / 64, g.batch);
+        hipLaunchKernelGGL((gemm_nt_kernel<64, 64, 2, 2, 32, true>), grid, dim3(256), 0, st, g);
+    } else if (g.N <= 32) {
         dim3 grid((g.R + 255) / 256, (g.N + 31) / 32, g.batch);
         hipLaunchKernelGGL((gemm_nt_kernel<256, 32, 4, 1, 16>), grid, dim3(256), 0, st, g);
     } else if (g.N <= 64) {

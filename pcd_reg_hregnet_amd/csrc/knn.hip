@@ -255,6 +255,60 @@ __global__ __launch_bounds__(256) void knnd_kernel(const float *__restrict__ q,
     }
 }
 
+// Descriptor-space kNN, one wave per query, no LDS staging and no barriers (dim % 4
+// == 0, 16-byte aligned rows): lane = database row of a 64-row chunk, the row read
+// straight from L2 as float4s, the query's dims wave-uniform (scalar loads).  The
+// CoarseReg desc kNN (layers.py:278: 256 queries x 256 rows x 256 dims per pair) as
+// 16-query blocks gave one block per 16 queries -- 128 blocks at B=8, each a chain
+// of 16 barrier-separated staging round trips; this is 2048 independent waves.
+// Same distance order (q - p, squared, added in d order) and the same offer/merge:
+// bit-identical lists.
+template <int K>
+__global__ __launch_bounds__(256) void knnd_wave_kernel(const float *__restrict__ q,
+                                                        const float *__restrict__ p, int nb, int n1,
+                                                        int n2, int dim, float *__restrict__ dists,
+                                                        int64_t *__restrict__ idx64,
+                                                        int32_t *__restrict__ idx32,
+                                                        float *__restrict__ nn, int k) {
+    __shared__ uint64_t sbuf[WAVES][128];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int qi = blockIdx.x * WAVES + w;
+    if (qi >= nb * n1) return;  // wave-uniform
+    const int cloud = qi / n1;
+    const float *P = p + (size_t)cloud * n2 * dim;
+    const float *Q = q + (size_t)qi * dim;
+    WaveList L;
+    L.key = KEY_INF; L.tau = KEY_INF; L.cnt = 0;
+    for (int base = 0; base < n2; base += 64) {
+        const int pi = base + lane;
+        const float *pr = P + (size_t)(pi < n2 ? pi : n2 - 1) * dim;
+        float acc = 0.f;
+#pragma unroll 4
+        for (int e = 0; e < dim; e += 4) {
+            const float4 pv = *reinterpret_cast<const float4 *>(pr + e);
+            const float4 qv = *reinterpret_cast<const float4 *>(Q + e);
+            float d;
+            d = fsub_rn(qv.x, pv.x); acc = fadd_rn(acc, fmul_rn(d, d));
+            d = fsub_rn(qv.y, pv.y); acc = fadd_rn(acc, fmul_rn(d, d));
+            d = fsub_rn(qv.z, pv.z); acc = fadd_rn(acc, fmul_rn(d, d));
+            d = fsub_rn(qv.w, pv.w); acc = fadd_rn(acc, fmul_rn(d, d));
+        }
+        const uint64_t key = pi < n2 ? (((uint64_t)__float_as_uint(acc) << 32) | (uint32_t)pi) : KEY_INF;
+        offer<K>(L, sbuf[w], key, lane);
+    }
+    if (L.cnt > 0) flush64<K>(L, sbuf[w], lane);
+    if (lane < k) {
+        const bool valid = L.key != KEY_INF;
+        const int id = valid ? (int)(uint32_t)(L.key & 0xffffffffu) : -1;
+        const size_t o = (size_t)qi * k + lane;
+        if (dists) dists[o] = valid ? __uint_as_float((uint32_t)(L.key >> 32)) : 0.f;
+        if (idx64) idx64[o] = id;
+        if (idx32) idx32[o] = id;
+        if (nn)
+            for (int e = 0; e < dim; ++e) nn[o * dim + e] = valid ? P[(size_t)id * dim + e] : 0.f;
+    }
+}
+
 // ---- spatially indexed kNN grouping (xyz, n <= 16384) --------------------
 // hreg_spatial_index orders each cloud's points by a 12-bit Morton cell (one
 // workgroup per cloud, counting sort in LDS) and records the bounding box of
@@ -482,6 +536,16 @@ __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
     }
 }
 
+// HREG_KNND (A/B switch): 1 (default) = knnd_wave_kernel where it applies, 0 = the
+// LDS-staged 16-query blocks everywhere
+inline int knnd_mode() {
+    static const int m = [] {
+        const char *e = getenv("HREG_KNND");
+        return e ? atoi(e) : 1;
+    }();
+    return m;
+}
+
 template <int K>
 int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim, int k,
                float *dists, int64_t *idx64, int32_t *idx32, float *nn, hipStream_t st) {
@@ -489,6 +553,10 @@ int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim,
     if (dim == 3) {
         hipLaunchKernelGGL((knn3_kernel<K>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
                            p2, b, n1, n2, dists, idx64, idx32, nn, k);
+    } else if (dim % 4 == 0 && !((reinterpret_cast<uintptr_t>(p1) | reinterpret_cast<uintptr_t>(p2)) & 15) &&
+               knnd_mode() == 1) {
+        hipLaunchKernelGGL((knnd_wave_kernel<K>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
+                           p2, b, n1, n2, dim, dists, idx64, idx32, nn, k);
     } else {
         constexpr int QB = WAVES * QPW;
         if (b > 1 && n1 % QB) {  // a block's queries must belong to one cloud

@@ -17,6 +17,7 @@ order-independent up to fp32 rounding).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -44,6 +45,9 @@ SPLIT_L3 = True
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
 FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
 FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip)
+# CoarseReg convs_1[0] as [small] GEMM + per-keypoint desc / knn_desc products added in the
+# epilogue (distributivity over the concatenation, layers.py:364-384; False: one 528-deep GEMM)
+COARSE_SPLIT = os.environ.get("HREG_COARSE_SPLIT", "1") != "0"
 
 
 @dataclass
@@ -130,6 +134,12 @@ class PreparedWeights:
                                   _conv_bn(sd, e + ".mlp2.0", e + ".mlp2.1")])
         C = 256
         self.coarse_convs1 = _stack(sd, "coarse_corres.convs_1", 3, _perm_coarse(C))
+        # convs_1[0] split by input block (COARSE_SPLIT): the 16 per-row columns, and
+        # [W_desc; W_knn_desc] stacked as one batch-2 weight for the per-keypoint products
+        c0 = self.coarse_convs1[0]
+        self.coarse_c1_small = Lin(c0.W[:, :16].contiguous(), c0.alpha, c0.beta, True)
+        self.coarse_c1_desc = Lin(torch.stack([c0.W[:, 16:16 + C], c0.W[:, 16 + C:]]).contiguous(),
+                                  torch.ones(c0.N), torch.zeros(c0.N), False)
         self.coarse_convs2 = _stack(sd, "coarse_corres.convs_2", 3)
         self.coarse_head = _mlp_head(sd, "coarse_corres")
         self.fine = {}
@@ -150,7 +160,8 @@ class PreparedWeights:
         self.head_table["coarse"] = mlp_head_table(self.coarse_head)
         for name in ("fine_corres_2", "fine_corres_1"):
             self.head_table[name] = mlp_head_table(self.fine[name][1])
-        for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_convs2",
+        for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
+                     "coarse_c1_desc", "coarse_convs2",
                      "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2s_table",
                      "l3s_table", "fine_table",
                      "nbr_table", "head_table", "mlpx"):
@@ -337,14 +348,18 @@ def _seg(base, k0, kc, ld=None, gather=None, rowscale=None, row_div=1, batch_str
     return s
 
 
-def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None):
-    """out[R][N] = act(alpha * (A @ W^T) + beta), A assembled from segs."""
+def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=()):
+    """out[R][N] = act(alpha * (A @ W^T + sum(adds)) + beta), A assembled from segs;
+    adds: up to 2 row sources (_seg with row_div or gather) of [*, N] addends."""
     if out is None:
         out = torch.empty((R, lin.N), device=lin.W.device, dtype=torch.float32)
     g = Gemm()
     for i, s in enumerate(segs):
         g.seg[i] = s
     g.nseg = len(segs)
+    for i, s in enumerate(adds):
+        g.add[i] = s
+    g.nadd = len(adds)
     g.R, g.N, g.K = R, lin.N, lin.K
     g.batch = 1
     g.ldw = lin.K
@@ -357,6 +372,29 @@ def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None):
     g.out = out.data_ptr()
     g.ldo = out.shape[-1]
     g.out_batch_stride = 0
+    _lib.gemm(g)
+    return out
+
+
+def _gemm_batched_desc(lin: Lin, desc3, rows: int, C: int, out):
+    """out[i] = desc3[i * rows : (i + 1) * rows] @ lin.W[i]^T for i in {0, 1} (one
+    launch, grid.z = 2); lin.W [2][N][C], identity epilogue."""
+    N = lin.W.shape[1]
+    g = Gemm()
+    g.seg[0] = _seg(desc3, 0, C, ld=C, batch_stride=rows * C)
+    g.nseg = 1
+    g.R, g.N, g.K = rows, N, C
+    g.batch = 2
+    g.ldw = C
+    g.w_batch_stride = N * C
+    g.W = lin.W.data_ptr()
+    g.scale = lin.alpha.data_ptr()
+    g.shift = lin.beta.data_ptr()
+    g.relu = 0
+    g.epi = _lib.HREG_EPI_AFFINE
+    g.out = out.data_ptr()
+    g.ldo = N
+    g.out_batch_stride = rows * N
     _lib.gemm(g)
     return out
 
@@ -688,8 +726,20 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     gidx = _empty(R, dtype=torch.int32, device=dev)
     call("hreg_pair_feats", s_xyz, d_xyz, s_sig, d_sig, kidx, B, N1, N1, k, sims_a, sims_b,
          small, 16, kx, gidx, _stream())
-    segs = [_seg(small, 0, 16), _seg(s_desc, 16, C, row_div=k), _seg(d_desc, 16 + C, C, gather=gidx)]
-    f = gemm(segs, P.coarse_convs1[0], R)
+    if COARSE_SPLIT:
+        # W [small | desc | knn_desc]: the desc block is the same for the k rows of a
+        # keypoint and the knn_desc block the same for every row gathering that dst
+        # keypoint, so both are multiplied once per keypoint (one batch-2 GEMM over
+        # desc3 = [src; dst]) and added in the layer's epilogue: 8.86 -> 1.34 GFLOP
+        # per step at B=8 for this layer
+        ud = _empty(2, B * N1, P.coarse_c1_desc.W.shape[1], device=dev)
+        _gemm_batched_desc(P.coarse_c1_desc, desc3, B * N1, C, ud)
+        f = gemm([_seg(small, 0, 16)], P.coarse_c1_small, R,
+                 adds=[_seg(ud[0], 0, 4, row_div=k), _seg(ud[1], 0, 4, gather=gidx)])
+    else:
+        segs = [_seg(small, 0, 16), _seg(s_desc, 16, C, row_div=k),
+                _seg(d_desc, 16 + C, C, gather=gidx)]
+        f = gemm(segs, P.coarse_convs1[0], R)
     f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[1], R)
     f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[2], R)
     _, att, corres = attend(f, B * N1, k, vals=f, xyz_rows=kx)

@@ -243,6 +243,57 @@ def test_fused_fine_head_matches_layerwise(net, name, C, N):
     torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("B", [1, 3])
+def test_coarse_split_matches_concat_gemm(net, B):
+    """CoarseReg convs_1[0] as the 16-column GEMM + per-keypoint desc / knn_desc products
+    added in the epilogue vs the one 528-deep GEMM over the concatenated rows
+    (layers.py:364-384).  Only the fp32 summation order differs: 1e-4 on corres/weights."""
+    from pcd_reg_hregnet_amd import engine
+    P = net.prepared(torch.device("cuda"))
+    g = torch.Generator().manual_seed(11 + B)
+    N1, C = 256, 256
+    xyz3 = (torch.rand(2 * B, N1, 3, generator=g) * 40 - 20).cuda()
+    desc3 = torch.relu(torch.randn(2 * B * N1, C, generator=g)).cuda()
+    sig3 = (torch.rand(2 * B * N1, generator=g) + 0.1).cuda()
+    outs = []
+    with torch.no_grad():
+        for split in (True, False):
+            old = engine.COARSE_SPLIT
+            engine.COARSE_SPLIT = split
+            try:
+                outs.append(engine.coarse_reg(P, B, xyz3, desc3, sig3))
+            finally:
+                engine.COARSE_SPLIT = old
+    torch.cuda.synchronize()
+    (c_f, w_f), (c_r, w_r) = outs
+    torch.testing.assert_close(c_f, c_r, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)
+
+
+def test_gemm_addends_vs_torch():
+    """hreg_gemm's pre-epilogue addends (row_div and gather row sources) vs torch fp32."""
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(7)
+    R, N, K, k = 4096, 512, 16, 8
+    A = rng.normal(size=(R, K)).astype(np.float32)
+    W = (rng.normal(size=(N, K)) / 4).astype(np.float32)
+    U = rng.normal(size=(R // k, N)).astype(np.float32)
+    V = rng.normal(size=(300, N)).astype(np.float32)
+    gi = rng.integers(0, 300, R).astype(np.int32)
+    al = rng.uniform(0.5, 1.5, N).astype(np.float32)
+    be = rng.normal(0, 0.1, N).astype(np.float32)
+    t = {n: torch.from_numpy(v).cuda() for n, v in
+         dict(A=A, W=W, U=U, V=V, gi=gi, al=al, be=be).items()}
+    lin = engine.Lin(t["W"], t["al"], t["be"], True)
+    out = engine.gemm([engine._seg(t["A"], 0, K)], lin, R,
+                      adds=[engine._seg(t["U"], 0, 4, row_div=k),
+                            engine._seg(t["V"], 0, 4, gather=t["gi"])]).cpu().numpy()
+    pre = (A.astype(np.float64) @ W.T.astype(np.float64) + U[np.arange(R) // k] + V[gi])
+    ref = np.maximum(pre * al + be, 0)
+    scale = (np.abs(A) @ np.abs(W).T + np.abs(U[np.arange(R) // k]) + np.abs(V[gi])) * al + np.abs(be)
+    assert np.all(np.abs(out - ref) <= 1e-5 * scale + 1e-6)
+
+
 def test_fused_nbr_head_matches_layerwise(net):
     """CoarseReg neighbour branch in one kernel (group_head.hip) vs GEMMs + attend."""
     from pcd_reg_hregnet_amd import engine

@@ -111,7 +111,8 @@ def test_knn_vs_reference_fixture(case):
 
 
 @pytest.mark.parametrize("n1,n2,dim,K", [(1024, 16384, 3, 64), (512, 1024, 3, 32), (256, 512, 3, 16),
-                                         (256, 256, 256, 8), (33, 70, 5, 8), (10, 5, 3, 8)])
+                                         (256, 256, 256, 8), (33, 70, 5, 8), (10, 5, 3, 8),
+                                         (37, 200, 64, 8), (100, 300, 128, 16), (3, 6, 8, 8)])
 def test_knn_vs_oracle(n1, n2, dim, K):
     from pcd_reg_hregnet_amd.knn import knn_points
     rng = np.random.default_rng(n1 + n2 + dim + K)
