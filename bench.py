@@ -69,14 +69,17 @@ L3_BYTES_PER_GROUP = 4.0 * (16 * 4 + 16 * 3 + 16 + 16 * 128 + 3 + 256 + 256)
 
 def _fine_work(args):
     C, G = args[1], args[7]
-    N1 = 2 * C  # algorithmic (unpadded) conv MACs, rows of 8 neighbours
-    return (2.0 * 8 * G * ((2 * C + 12) * N1 + 2 * N1 * N1),
+    N1 = 2 * C  # conv MACs per row of 8 neighbours (unpadded), executed: with precomputed
+    # descriptor products (engine.HEAD_PRE, args[10]) only the 12 small columns of convs_1[0]
+    kin = 12 if args[10] is not None else 2 * C + 12
+    return (2.0 * 8 * G * (kin * N1 + 2 * N1 * N1),
             4.0 * G * (8 * (16 + C + 1 + 3) + C + 3 + N1))
 
 
 def _nbr_work(args):
     G = args[4]
-    return (2.0 * 8 * G * (260 * 256 + 2 * 256 * 256), 4.0 * G * (8 * (256 + 4 + 1) + 256))
+    kin = 4 if args[6] is not None else 260  # HEAD_PRE: geometry columns only
+    return (2.0 * 8 * G * (kin * 256 + 2 * 256 * 256), 4.0 * G * (8 * (256 + 4 + 1) + 256))
 
 
 def _mlp_work(args):

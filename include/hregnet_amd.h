@@ -473,20 +473,25 @@ int hreg_group_split_l3(const float *table, const float *geom, const float *knn_
  * (keypoint i's own descriptor), dst_desc [*][C] gathered by gidx [G*8],
  * knn_xyz [G*8][3] -> corres [G][3] (attention-weighted neighbour xyz) and
  * att [G][N1] (attentive feature, N1 = 2C), convs_1 + attention in one kernel.
- * table = hreg_fine_head_table_floats(C) floats (engine.fine_head_table). */
+ * table = hreg_fine_head_table_floats(C) floats (engine.fine_head_table).
+ * pre_src [G][N1] = W_f src_desc, pre_dst [*][N1] = W_kf dst_desc (optional, both or
+ * neither): the first layer's descriptor blocks precomputed once per point, so the
+ * kernel multiplies only the 16 small columns per row (src_desc / dst_desc unread). */
 int hreg_fine_head_table_floats(int C);
 int hreg_fine_head(const float *table, int C, const float *small, const float *src_desc,
                    const float *dst_desc, const int32_t *gidx, const float *knn_xyz, int G,
-                   float *corres, float *att, void *stream);
+                   float *corres, float *att, const float *pre_src, const float *pre_dst,
+                   void *stream);
 
 /* Fused CoarseReg neighbour branch (layers.py:315-337), C = 256: rows
  * [desc[gidx] C | geom 4] (geom [G*8] float4 from hreg_knn_group) through convs_2
  * (260 -> 256 x 3) and the attention over the 8 rows, applied to the gathered
  * descriptors: out [G][C] = sum_j a_j desc[gidx_j].  table =
- * hreg_nbr_head_table_floats() floats (engine.nbr_head_table). */
+ * hreg_nbr_head_table_floats() floats (engine.nbr_head_table).  pre [*][256] = W_d desc
+ * (optional): the descriptor block of convs_2[0] precomputed once per point. */
 int hreg_nbr_head_table_floats(void);
 int hreg_nbr_head(const float *table, const float *desc, const int32_t *gidx, const float *geom,
-                  int G, float *out, void *stream);
+                  int G, float *out, const float *pre, void *stream);
 
 /* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */

@@ -118,11 +118,38 @@ __device__ __forceinline__ float grp8_max_nonneg(float f) {
     return __int_as_float(max(v, dpp_all_i<0x141>(v)));
 }
 
-template <class K>
+// PRE: the descriptor blocks of the first layer come precomputed per point --
+// pre_src[g] = W_f f_src[g], pre_dst[n] = W_kf f_dst[n] ([*][N1], hreg_gemm) -- and
+// initialise the accumulators (lane j, register q <- channel chan(co, q, h) of its
+// row's two sources); only the 16 small columns run on the MFMA here.  Same sum up to
+// fp32 order, 2C k-steps per row fewer (the reference repeats / gathers the
+// descriptors into every row first, layers.py:444-445).
+template <int N1, int T1>
+__device__ __forceinline__ void init_from_rows(f32x16 (&acc)[T1], const float *__restrict__ u,
+                                               const float *__restrict__ v, int h) {
+#pragma unroll
+    for (int co = 0; co < T1; ++co)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int c = co * 32 + 8 * r + 4 * h;
+            const float4 a = *reinterpret_cast<const float4 *>(u + c);
+            if (v) {
+                const float4 b = *reinterpret_cast<const float4 *>(v + c);
+                acc[co][4 * r] = fadd_rn(a.x, b.x); acc[co][4 * r + 1] = fadd_rn(a.y, b.y);
+                acc[co][4 * r + 2] = fadd_rn(a.z, b.z); acc[co][4 * r + 3] = fadd_rn(a.w, b.w);
+            } else {
+                acc[co][4 * r] = a.x; acc[co][4 * r + 1] = a.y;
+                acc[co][4 * r + 2] = a.z; acc[co][4 * r + 3] = a.w;
+            }
+        }
+}
+
+template <class K, bool PRE>
 __global__ __launch_bounds__(256, K::WPS) void fine_head_kernel(
     const float *__restrict__ table, const float *__restrict__ small, const float *__restrict__ src_desc,
     const float *__restrict__ dst_desc, const int32_t *__restrict__ gidx,
-    const float *__restrict__ knn_xyz, int G, float *__restrict__ corres, float *__restrict__ att) {
+    const float *__restrict__ knn_xyz, int G, float *__restrict__ corres, float *__restrict__ att,
+    const float *__restrict__ pre_src, const float *__restrict__ pre_dst) {
     constexpr int C = K::C, N1 = K::N1, T1 = K::T1, TA = K::TA;
     constexpr int NE = K::TABLE - K::F_END;
     __shared__ float ep[NE];
@@ -159,13 +186,19 @@ __global__ __launch_bounds__(256, K::WPS) void fine_head_kernel(
         float c1[CARRY], c2[CARRY], c3[CARRY], c4[CARRY];
 
         f32x16 h1[T1], h2[T1];
-        zero_tiles(h1);
-        mfma_pipe_rows<8, T1, T1, first_win<TA, T1>()>(tb, lane, fs, small + (size_t)row * 16 + h * 8,
-                                                       h1, carry, fa, c1);
-        mfma_pipe_rows<TA, T1, T1, first_win<TA, T1>()>(tb, lane, fa, src_desc + (size_t)g * C + h * TA,
-                                                        h1, c1, fb, c2);
-        mfma_pipe_rows<TA, T1, T1, WT>(tb, lane, fb, dst_desc + (size_t)gidx[row] * C + h * TA, h1, c2,
-                                       f2, c3);
+        if constexpr (PRE) {
+            init_from_rows<N1, T1>(h1, pre_src + (size_t)g * N1, pre_dst + (size_t)gidx[row] * N1, h);
+            mfma_pipe_rows<8, T1, T1, WT>(tb, lane, fs, small + (size_t)row * 16 + h * 8, h1, carry, f2, c3);
+            (void)c1; (void)c2;
+        } else {
+            zero_tiles(h1);
+            mfma_pipe_rows<8, T1, T1, first_win<TA, T1>()>(tb, lane, fs, small + (size_t)row * 16 + h * 8,
+                                                           h1, carry, fa, c1);
+            mfma_pipe_rows<TA, T1, T1, first_win<TA, T1>()>(tb, lane, fa, src_desc + (size_t)g * C + h * TA,
+                                                            h1, c1, fb, c2);
+            mfma_pipe_rows<TA, T1, T1, WT>(tb, lane, fb, dst_desc + (size_t)gidx[row] * C + h * TA, h1, c2,
+                                           f2, c3);
+        }
         epilogue<T1>(eb + K::E_1, lane, h1);
         zero_tiles(h2);
         mfma_pipe<T1 * 16, T1, T1, WT>(tb, lane, f2, [&](int st) { return h1[st >> 4][st & 15]; }, h2, c3,
@@ -219,10 +252,12 @@ struct NbrCfg {
 };
 using Nbr = NbrCfg<256>;
 
-template <class K>
+// PRE: pre[n] = W_d desc[n] ([*][256], hreg_gemm) initialises the accumulators from
+// the row's gathered neighbour; only the 4 geometry columns run on the MFMA here.
+template <class K, bool PRE>
 __global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
     const float *__restrict__ table, const float *__restrict__ desc, const int32_t *__restrict__ gidx,
-    const float *__restrict__ geom, int G, float *__restrict__ out) {
+    const float *__restrict__ geom, int G, float *__restrict__ out, const float *__restrict__ pre) {
     constexpr int C = K::C, T1 = K::T1, TA = K::TA;
     constexpr int NE = K::TABLE - K::F_END;
     __shared__ float ep[NE];
@@ -235,7 +270,8 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
     constexpr int WT = win_for<T1>();
     const FragSeq fd{K::F_D / 64, TA}, fg{K::F_G / 64, 2};
     const FragSeq f2{K::F_2 / 64, T1 * 16}, f3{K::F_3 / 64, T1 * 16};
-    constexpr int W0 = first_win<TA, T1>();
+    constexpr int W0 = PRE ? first_win<2, T1>() : first_win<TA, T1>();
+    const FragSeq f0 = PRE ? fg : fd;  // the first call of a tile
 
     float carry[CARRY];
     {
@@ -246,7 +282,7 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
 #pragma unroll
             for (int co = 0; co < T1; ++co) {
                 float v[GS0];
-                ldgroup<GS0>(tb, fd.base + co * fd.stride + s0, lane, v);
+                ldgroup<GS0>(tb, f0.base + co * f0.stride + s0, lane, v);
 #pragma unroll
                 for (int i = 0; i < GS0; ++i) carry[(s0 + i) * T1 + co] = v[i];
             }
@@ -261,9 +297,15 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
         float c1[CARRY], c2[CARRY], c3[CARRY], c4[CARRY];
 
         f32x16 h1[T1], h2[T1];
-        zero_tiles(h1);
-        mfma_pipe_rows<TA, T1, T1, 2>(tb, lane, fd, drow + h * TA, h1, carry, fg, c1);
-        mfma_pipe_rows<2, T1, T1, WT>(tb, lane, fg, geom + (size_t)row * 4 + h * 2, h1, c1, f2, c2);
+        if constexpr (PRE) {
+            init_from_rows<K::N1, T1>(h1, pre + (size_t)gidx[row] * K::N1, nullptr, h);
+            mfma_pipe_rows<2, T1, T1, WT>(tb, lane, fg, geom + (size_t)row * 4 + h * 2, h1, carry, f2, c2);
+            (void)c1;
+        } else {
+            zero_tiles(h1);
+            mfma_pipe_rows<TA, T1, T1, 2>(tb, lane, fd, drow + h * TA, h1, carry, fg, c1);
+            mfma_pipe_rows<2, T1, T1, WT>(tb, lane, fg, geom + (size_t)row * 4 + h * 2, h1, c1, f2, c2);
+        }
         epilogue<T1>(eb + K::E_1, lane, h1);
         zero_tiles(h2);
         mfma_pipe<T1 * 16, T1, T1, WT>(tb, lane, f2, [&](int st) { return h1[st >> 4][st & 15]; }, h2, c2,
@@ -272,7 +314,7 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
         f32x16 f[T1];
         zero_tiles(f);
         mfma_pipe<T1 * 16, T1, T1, W0>(tb, lane, f3, [&](int st) { return h2[st >> 4][st & 15]; }, f, c3,
-                                       fd, carry);
+                                       f0, carry);
         epilogue<T1>(eb + K::E_3, lane, f);
         (void)c4;
 
@@ -300,17 +342,23 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
 template <class K>
 int launch_fine(const float *table, const float *small, const float *src_desc, const float *dst_desc,
                 const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
-                void *stream) {
+                const float *pre_src, const float *pre_dst, void *stream) {
     if ((reinterpret_cast<uintptr_t>(small) & 15) || (reinterpret_cast<uintptr_t>(src_desc) & 15) ||
-        (reinterpret_cast<uintptr_t>(dst_desc) & 15) || (reinterpret_cast<uintptr_t>(att) & 15))
+        (reinterpret_cast<uintptr_t>(dst_desc) & 15) || (reinterpret_cast<uintptr_t>(att) & 15) ||
+        (reinterpret_cast<uintptr_t>(pre_src) & 15) || (reinterpret_cast<uintptr_t>(pre_dst) & 15))
         return HREG_ERR_INVALID;
+    if (!pre_src != !pre_dst) return HREG_ERR_INVALID;
     if ((G * KH) % 32) return HREG_ERR_INVALID;  // whole 32-row tiles
     const int NT = G * KH / 32;
     int grid = (NT + WAVES - 1) / WAVES;
     const int cap = 256 * K::WPS * 2;
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(fine_head_kernel<K>, dim3(grid), dim3(256), 0, as_stream(stream), table, small,
-                       src_desc, dst_desc, gidx, knn_xyz, G, corres, att);
+    if (pre_src)
+        hipLaunchKernelGGL((fine_head_kernel<K, true>), dim3(grid), dim3(256), 0, as_stream(stream), table,
+                           small, src_desc, dst_desc, gidx, knn_xyz, G, corres, att, pre_src, pre_dst);
+    else
+        hipLaunchKernelGGL((fine_head_kernel<K, false>), dim3(grid), dim3(256), 0, as_stream(stream), table,
+                           small, src_desc, dst_desc, gidx, knn_xyz, G, corres, att, pre_src, pre_dst);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -320,18 +368,22 @@ int launch_fine(const float *table, const float *small, const float *src_desc, c
 extern "C" int hreg_nbr_head_table_floats(void) { return Nbr::TABLE; }
 
 extern "C" int hreg_nbr_head(const float *table, const float *desc, const int32_t *gidx,
-                             const float *geom, int G, float *out, void *stream) {
+                             const float *geom, int G, float *out, const float *pre, void *stream) {
     if (!table || !desc || !gidx || !geom || !out || G < 0) return HREG_ERR_INVALID;
     if ((reinterpret_cast<uintptr_t>(desc) & 15) || (reinterpret_cast<uintptr_t>(geom) & 15) ||
-        (reinterpret_cast<uintptr_t>(out) & 15))
+        (reinterpret_cast<uintptr_t>(out) & 15) || (reinterpret_cast<uintptr_t>(pre) & 15))
         return HREG_ERR_INVALID;
     if ((G * KH) % 32) return HREG_ERR_INVALID;
     if (!G) return HREG_OK;
     const int NT = G * KH / 32;
     int grid = (NT + WAVES - 1) / WAVES;
     if (grid > 512) grid = 512;
-    hipLaunchKernelGGL(nbr_head_kernel<Nbr>, dim3(grid), dim3(256), 0, as_stream(stream), table, desc,
-                       gidx, geom, G, out);
+    if (pre)
+        hipLaunchKernelGGL((nbr_head_kernel<Nbr, true>), dim3(grid), dim3(256), 0, as_stream(stream), table,
+                           desc, gidx, geom, G, out, pre);
+    else
+        hipLaunchKernelGGL((nbr_head_kernel<Nbr, false>), dim3(grid), dim3(256), 0, as_stream(stream), table,
+                           desc, gidx, geom, G, out, pre);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -342,13 +394,16 @@ extern "C" int hreg_fine_head_table_floats(int C) {
 
 extern "C" int hreg_fine_head(const float *table, int C, const float *small, const float *src_desc,
                               const float *dst_desc, const int32_t *gidx, const float *knn_xyz,
-                              int G, float *corres, float *att, void *stream) {
+                              int G, float *corres, float *att, const float *pre_src,
+                              const float *pre_dst, void *stream) {
     if (!table || !small || !src_desc || !dst_desc || !gidx || !knn_xyz || !corres || !att || G < 0)
         return HREG_ERR_INVALID;
     if (!G) return HREG_OK;
     if (C == 64)
-        return launch_fine<Fine1>(table, small, src_desc, dst_desc, gidx, knn_xyz, G, corres, att, stream);
+        return launch_fine<Fine1>(table, small, src_desc, dst_desc, gidx, knn_xyz, G, corres, att, pre_src,
+                                  pre_dst, stream);
     if (C == 128)
-        return launch_fine<Fine2>(table, small, src_desc, dst_desc, gidx, knn_xyz, G, corres, att, stream);
+        return launch_fine<Fine2>(table, small, src_desc, dst_desc, gidx, knn_xyz, G, corres, att, pre_src,
+                                  pre_dst, stream);
     return HREG_ERR_UNSUPPORTED;
 }

@@ -48,6 +48,10 @@ FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip
 # CoarseReg convs_1[0] as [small] GEMM + per-keypoint desc / knn_desc products added in the
 # epilogue (distributivity over the concatenation, layers.py:364-384; False: one 528-deep GEMM)
 COARSE_SPLIT = os.environ.get("HREG_COARSE_SPLIT", "1") != "0"
+# the same for the fused FineReg heads (descriptor blocks of convs_1[0]) and the CoarseReg
+# neighbour branch (descriptor block of convs_2[0]): per-point products precomputed, the
+# fused kernels multiply only the small / geometry columns per row
+HEAD_PRE = os.environ.get("HREG_HEAD_PRE", "1") != "0"
 
 
 @dataclass
@@ -141,10 +145,18 @@ class PreparedWeights:
         self.coarse_c1_desc = Lin(torch.stack([c0.W[:, 16:16 + C], c0.W[:, 16 + C:]]).contiguous(),
                                   torch.ones(c0.N), torch.zeros(c0.N), False)
         self.coarse_convs2 = _stack(sd, "coarse_corres.convs_2", 3)
+        n0 = self.coarse_convs2[0]
+        self.nbr_pre = Lin(n0.W[:, :C].contiguous(), torch.ones(n0.N), torch.zeros(n0.N), False)
         self.coarse_head = _mlp_head(sd, "coarse_corres")
         self.fine = {}
         for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64)):
             self.fine[name] = (_stack(sd, name + ".convs_1", 3, _perm_fine(C)), _mlp_head(sd, name))
+        # [W_f; W_knn_f] of each FineReg convs_1[0] as one batch-2 weight (HEAD_PRE)
+        self.fine_pre = {}
+        for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64)):
+            f0 = self.fine[name][0][0]
+            self.fine_pre[name] = Lin(torch.stack([f0.W[:, 12:12 + C], f0.W[:, 12 + C:]]).contiguous(),
+                                      torch.ones(f0.N), torch.zeros(f0.N), False)
         # Model_V2's FineReg2.mlpx (model_v2/layers.py:457-459), when the state dict has it
         self.mlpx = (_conv_bn(sd, "fine_corres_2.mlpx.0", "fine_corres_2.mlpx.1")
                      if "fine_corres_2.mlpx.0.weight" in sd else None)
@@ -161,7 +173,7 @@ class PreparedWeights:
         for name in ("fine_corres_2", "fine_corres_1"):
             self.head_table[name] = mlp_head_table(self.fine[name][1])
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
-                     "coarse_c1_desc", "coarse_convs2",
+                     "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre",
                      "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2s_table",
                      "l3s_table", "fine_table",
                      "nbr_table", "head_table", "mlpx"):
@@ -376,10 +388,15 @@ def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=()):
     return out
 
 
-def _gemm_batched_desc(lin: Lin, desc3, rows: int, C: int, out):
-    """out[i] = desc3[i * rows : (i + 1) * rows] @ lin.W[i]^T for i in {0, 1} (one
-    launch, grid.z = 2); lin.W [2][N][C], identity epilogue."""
+def _gemm_batched_desc(lin: Lin, desc3, rows: int, C: int, out, x1=None):
+    """out[i] = x_i @ lin.W[i]^T for i in {0, 1}, x_0 = desc3[:rows], x_1 = desc3[rows:2 rows]
+    (or x1 when given and not contiguous after x_0: then two launches); one launch with
+    grid.z = 2 otherwise; lin.W [2][N][C], identity epilogue."""
     N = lin.W.shape[1]
+    if x1 is not None and x1.data_ptr() != desc3.data_ptr() + rows * C * 4:
+        for i, x in enumerate((desc3, x1)):
+            gemm([_seg(x, 0, C, ld=C)], Lin(lin.W[i], lin.alpha, lin.beta, False), rows, out=out[i])
+        return out
     g = Gemm()
     g.seg[0] = _seg(desc3, 0, C, ld=C, batch_stride=rows * C)
     g.nseg = 1
@@ -708,7 +725,8 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     R2 = G2 * k
     if FUSED_NBR and C == 256:
         nbr = _empty(G2, C, device=dev)
-        call("hreg_nbr_head", P.nbr_table, desc3, gself, geom_self, G2, nbr, _stream())
+        pre = gemm([_seg(desc3, 0, C)], P.nbr_pre, G2) if HEAD_PRE else None
+        call("hreg_nbr_head", P.nbr_table, desc3, gself, geom_self, G2, nbr, pre, _stream())
     else:
         segs = [_seg(desc3, 0, C, gather=gself), _seg(geom_self, C, 4)]
         h = gemm(segs, P.coarse_convs2[0], R2)
@@ -766,8 +784,12 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
         N1 = convs[0].W.shape[0]
         corres = _empty(B * N, 3, device=dev)
         att = _empty(B * N, N1, device=dev)
+        pre = [None, None]
+        if HEAD_PRE:
+            pre = _empty(2, B * N, N1, device=dev)
+            _gemm_batched_desc(P.fine_pre[name], src_desc, B * N, C, pre, x1=dst_desc)
         call("hreg_fine_head", P.fine_table[name], C, small, src_desc, dst_desc, gidx, kx, B * N,
-             corres, att, _stream())
+             corres, att, pre[0], pre[1], _stream())
         w = _mlp_weights(P, name, att, B, N)
         if return_att:
             return corres.view(B, N, 3), w.view(B, N), att

@@ -215,10 +215,13 @@ def test_fused_level_matches_layerwise(net, lvl, split):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("pre", [True, False])
 @pytest.mark.parametrize("name,C,N", [("fine_corres_1", 64, 1024), ("fine_corres_2", 128, 512)])
-def test_fused_fine_head_matches_layerwise(net, name, C, N):
-    """group_head.hip (convs_1 + attention in one kernel) against the GEMM + attend path."""
+def test_fused_fine_head_matches_layerwise(net, name, C, N, pre, monkeypatch):
+    """group_head.hip (convs_1 + attention in one kernel; pre: descriptor blocks of
+    convs_1[0] precomputed per point, engine.HEAD_PRE) against the GEMM + attend path."""
     from pcd_reg_hregnet_amd import engine
+    monkeypatch.setattr(engine, "HEAD_PRE", pre)
     P = net.prepared(torch.device("cuda"))
     g = torch.Generator().manual_seed(3)
     B = 2
@@ -294,9 +297,12 @@ def test_gemm_addends_vs_torch():
     assert np.all(np.abs(out - ref) <= 1e-5 * scale + 1e-6)
 
 
-def test_fused_nbr_head_matches_layerwise(net):
-    """CoarseReg neighbour branch in one kernel (group_head.hip) vs GEMMs + attend."""
+@pytest.mark.parametrize("pre", [True, False])
+def test_fused_nbr_head_matches_layerwise(net, pre, monkeypatch):
+    """CoarseReg neighbour branch in one kernel (group_head.hip; pre: descriptor block of
+    convs_2[0] precomputed per point) vs GEMMs + attend."""
     from pcd_reg_hregnet_amd import engine
+    monkeypatch.setattr(engine, "HEAD_PRE", pre)
     P = net.prepared(torch.device("cuda"))
     g = torch.Generator().manual_seed(5)
     B, N1, C = 2, 256, 256
