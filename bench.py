@@ -30,6 +30,9 @@ sys.path.insert(0, REPO)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak BW (spec)
+# 20.51 GFLOP/pair of 1x1 convs (conv hooks on the reference) + 2 x 0.034
+# GFLOP cosine-similarity contractions
+ALG_GFLOP_PER_PAIR = 20.579
 POINTS = 16384
 PAIRS_PER_GPU = 8
 V2_POINTS = 65536      # config 5 (MANTruckScenes-shape): B=16 over 8 GPUs -> 2 pairs/GPU
@@ -51,49 +54,78 @@ def make_model(device, model="hregnet"):
     return net.to(device).eval()
 
 
+# Work per launch, as (algorithmic FLOPs, algorithmic bytes, executed FLOPs).  The
+# algorithmic FLOPs are the reference's conv MACs x 2 (20.51 GFLOP/pair of
+# 1x1 convs); executed FLOPs are what the MFMAs run: with the precomputed first-layer
+# feature / descriptor blocks (engine.LEVEL_PRE, HEAD_PRE, COARSE_SPLIT) the products of
+# a gathered or repeated block are made once per source row instead of once per grouped
+# row, so fewer FLOPs execute than the reference's algorithm counts.
 # level-1 fused kernel: per group 64 rows x (det 4*32+32*32+32*64, desc same,
 # mlp1 192*32, mlp2 32*64) MACs = 64 * 14592 MAC (layers.py:115-121,183-198)
 L1_FLOPS_PER_GROUP = 2.0 * 64 * (2 * (4 * 32 + 32 * 32 + 32 * 64) + 192 * 32 + 32 * 64)
 # per group: geom 64 x float4 + knn_xyz 64 x 3 in, kp 3 + att_feat 64 + desc 64 out
 L1_BYTES_PER_GROUP = 4.0 * (64 * 4 + 64 * 3 + 3 + 64 + 64)
-# level-2 fused kernel: 32 rows x (det 68*64+64*64+64*128, desc same, mlp1 384*64,
-# mlp2 64*128) MACs; bytes: geom 32 x float4, knn_xyz 32 x 3, gidx 32, gathered
-# features 32 x 64, out kp 3 + att_feat 128 + desc 128
-L2_FLOPS_PER_GROUP = 2.0 * 32 * (2 * (68 * 64 + 64 * 64 + 64 * 128) + 384 * 64 + 64 * 128)
+
+
+def _level_flops(kn, cf, c1, c3, cm1, cm2, pre):
+    """Fused level 2/3 kernel per group: kn rows x (det (4+cf)*c1 + c1*c1 + c1*c3, desc
+    same, mlp1 3*c3*cm1, mlp2 cm1*cm2) MACs; pre: the cf-wide first-layer blocks precomputed."""
+    cin = 4 if pre else 4 + cf
+    return 2.0 * kn * (2 * (cin * c1 + c1 * c1 + c1 * c3) + 3 * c3 * cm1 + cm1 * cm2)
+
+
+L2_FLOPS_PER_GROUP = _level_flops(32, 64, 64, 128, 64, 128, False)
+L3_FLOPS_PER_GROUP = _level_flops(16, 128, 128, 256, 128, 256, False)
+# bytes: geom kn x float4, knn_xyz kn x 3, gidx kn, gathered features kn x cf, out kp 3 +
+# att_feat c3 + desc cm2
 L2_BYTES_PER_GROUP = 4.0 * (32 * 4 + 32 * 3 + 32 + 32 * 64 + 3 + 128 + 128)
-# level-3 fused kernel: 16 rows x (det 132*128+128*128+128*256, desc same, mlp1 768*128,
-# mlp2 128*256) MACs
-L3_FLOPS_PER_GROUP = 2.0 * 16 * (2 * (132 * 128 + 128 * 128 + 128 * 256) + 768 * 128 + 128 * 256)
 L3_BYTES_PER_GROUP = 4.0 * (16 * 4 + 16 * 3 + 16 + 16 * 128 + 3 + 256 + 256)
+
+
+def _level_work(lvl):
+    cfg = {2: (32, 64, 64, 128, 64, 128), 3: (16, 128, 128, 256, 128, 256)}[lvl]
+    nb = L2_BYTES_PER_GROUP if lvl == 2 else L3_BYTES_PER_GROUP
+
+    def work(a):
+        G = a[5]
+        return (_level_flops(*cfg, False) * G, nb * G, _level_flops(*cfg, a[9] is not None) * G)
+    return work
 
 
 def _fine_work(args):
     C, G = args[1], args[7]
-    N1 = 2 * C  # conv MACs per row of 8 neighbours (unpadded), executed: with precomputed
+    N1 = 2 * C  # conv MACs per row of 8 neighbours (unpadded); executed: with precomputed
     # descriptor products (engine.HEAD_PRE, args[10]) only the 12 small columns of convs_1[0]
-    kin = 12 if args[10] is not None else 2 * C + 12
-    return (2.0 * 8 * G * (kin * N1 + 2 * N1 * N1),
-            4.0 * G * (8 * (16 + C + 1 + 3) + C + 3 + N1))
+    kx = 12 if args[10] is not None else 2 * C + 12
+    return (2.0 * 8 * G * ((2 * C + 12) * N1 + 2 * N1 * N1),
+            4.0 * G * (8 * (16 + C + 1 + 3) + C + 3 + N1),
+            2.0 * 8 * G * (kx * N1 + 2 * N1 * N1))
 
 
 def _nbr_work(args):
     G = args[4]
-    kin = 4 if args[6] is not None else 260  # HEAD_PRE: geometry columns only
-    return (2.0 * 8 * G * (kin * 256 + 2 * 256 * 256), 4.0 * G * (8 * (256 + 4 + 1) + 256))
+    kx = 4 if args[6] is not None else 260  # HEAD_PRE: geometry columns only
+    return (2.0 * 8 * G * (260 * 256 + 2 * 256 * 256), 4.0 * G * (8 * (256 + 4 + 1) + 256),
+            2.0 * 8 * G * (kx * 256 + 2 * 256 * 256))
 
 
 def _mlp_work(args):
     C, G = args[1], args[4] * args[5]
-    return 2.0 * G * (2 * C * C + C), 4.0 * G * (C + 1)
+    f = 2.0 * G * (2 * C * C + C)
+    return f, 4.0 * G * (C + 1), f
 
 
-# C-ABI entry -> (timer kind, (flops, bytes) of one launch from its arguments)
+def _l1_work(a):
+    return L1_FLOPS_PER_GROUP * a[3], L1_BYTES_PER_GROUP * a[3], L1_FLOPS_PER_GROUP * a[3]
+
+
+# C-ABI entry -> (timer kind, work of one launch from its arguments)
 MFMA_ENTRIES = {
-    "hreg_group_l1": ("l1", lambda a: (L1_FLOPS_PER_GROUP * a[3], L1_BYTES_PER_GROUP * a[3])),
-    "hreg_group_l2": ("fused", lambda a: (L2_FLOPS_PER_GROUP * a[5], L2_BYTES_PER_GROUP * a[5])),
-    "hreg_group_l3": ("fused", lambda a: (L3_FLOPS_PER_GROUP * a[5], L3_BYTES_PER_GROUP * a[5])),
-    "hreg_group_split_l2": ("fused", lambda a: (L2_FLOPS_PER_GROUP * a[5], L2_BYTES_PER_GROUP * a[5])),
-    "hreg_group_split_l3": ("fused", lambda a: (L3_FLOPS_PER_GROUP * a[5], L3_BYTES_PER_GROUP * a[5])),
+    "hreg_group_l1": ("l1", _l1_work),
+    "hreg_group_l2": ("fused", _level_work(2)),
+    "hreg_group_l3": ("fused", _level_work(3)),
+    "hreg_group_split_l2": ("fused", _level_work(2)),
+    "hreg_group_split_l3": ("fused", _level_work(3)),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
     "hreg_mlp_head": ("mlp", _mlp_work),
@@ -110,10 +142,11 @@ class MfmaTimer:
     def __init__(self):
         self.events = {k: [] for k in self.KINDS}
         self.flops = dict.fromkeys(self.KINDS, 0.0)
+        self.xflops = dict.fromkeys(self.KINDS, 0.0)
         self.bytes = dict.fromkeys(self.KINDS, 0.0)
         self.enabled = False
 
-    def _timed(self, kind, fn, flops, nbytes):
+    def _timed(self, kind, fn, flops, nbytes, xflops=None):
         if not self.enabled:
             return fn()
         st = torch.cuda.current_stream()
@@ -124,6 +157,7 @@ class MfmaTimer:
         e1.record(st)
         self.events[kind].append((e0, e1))
         self.flops[kind] += flops
+        self.xflops[kind] += flops if xflops is None else xflops
         self.bytes[kind] += nbytes
         return r
 
@@ -142,8 +176,8 @@ class MfmaTimer:
         def call(name, *args):
             if name in MFMA_ENTRIES:
                 kind, work = MFMA_ENTRIES[name]
-                fl, nb = work(args)
-                return self._timed(kind, lambda: orig_call(name, *args), fl, nb)
+                fl, nb, xf = work(args)
+                return self._timed(kind, lambda: orig_call(name, *args), fl, nb, xf)
             return orig_call(name, *args)
         _lib.gemm = gemm
         engine.call = call
@@ -152,7 +186,7 @@ class MfmaTimer:
         torch.cuda.synchronize()
         ev = self.events[kind]
         ms = sum(a.elapsed_time(b) for a, b in ev)
-        return ms, len(ev), self.flops[kind], self.bytes[kind]
+        return ms, len(ev), self.flops[kind], self.bytes[kind], self.xflops[kind]
 
 
 def pmc_traffic(kernel: str):
@@ -440,19 +474,22 @@ def main():
 
     if rank == 0:
         def kind_summary(k):
-            ms, n, fl, nb = res[k]
+            ms, n, fl, nb, xf = res[k]
             return {"launches_per_step": n // args.steps,
                     "avg_launch_us": round(ms / max(n, 1) * 1e3, 2),
                     "ms_per_step": round(ms / args.steps, 3),
                     "tflops": round(fl / max(ms, 1e-9) / 1e9, 2),
-                    "gflop_per_pair": round(fl / args.steps / B / 1e9, 3)}
-        f_ms, f_n, f_fl, f_nb = res["fused"]
+                    "gflop_per_pair": round(fl / args.steps / B / 1e9, 3),
+                    "executed_tflops": round(xf / max(ms, 1e-9) / 1e9, 2),
+                    "executed_gflop_per_pair": round(xf / args.steps / B / 1e9, 3)}
+        f_ms, f_n, f_fl, f_nb, f_xf = res["fused"]
         per_launch_s = f_ms / max(f_n, 1) / 1e3
         per_launch_flops = f_fl / max(f_n, 1)
         achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
         traffic, traffic_src = pmc_traffic(" + ".join(fused_names))
         tot_ms = sum(r[0] for r in res.values())
-        tot_fl = sum(r[2] for r in res.values())
+        tot_xf = sum(r[4] for r in res.values())
+        alg_fl = ALG_GFLOP_PER_PAIR * 1e9 * B * args.steps
         roof = {"kernel": " + ".join(fused_names) + " (keypoint detector + descriptor: "
                           "every conv/BN/ReLU layer, attention and k-max of the level in one "
                           "launch)",
@@ -465,6 +502,8 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": round(f_nb / max(f_n, 1)),
                 "flop_per_launch": round(per_launch_flops),
+                "executed_flop_per_launch": round(f_xf / max(f_n, 1)),
+                "executed_tflops": round(f_xf / max(f_ms, 1e-9) / 1e9, 3),
                 "launches_per_step": f_n // args.steps,
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
                 "other_mfma_kernels": {"gemm_nt_kernel": kind_summary("gemm"),
@@ -472,8 +511,10 @@ def main():
                                        "fine_head_kernel + nbr_head_kernel": kind_summary("head"),
                                        "mlp_head_kernel": kind_summary("mlp")},
                 "all_mfma": {"ms_per_step": round(tot_ms / args.steps, 3),
-                             "gflop_per_pair": round(tot_fl / args.steps / B / 1e9, 3),
-                             "tflops": round(tot_fl / max(tot_ms, 1e-9) / 1e9, 2)}}
+                             "gflop_per_pair": ALG_GFLOP_PER_PAIR,
+                             "tflops": round(alg_fl / max(tot_ms, 1e-9) / 1e9, 2),
+                             "executed_gflop_per_pair": round(tot_xf / args.steps / B / 1e9, 3),
+                             "executed_tflops": round(tot_xf / max(tot_ms, 1e-9) / 1e9, 2)}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not v2:
             try:

@@ -440,11 +440,14 @@ int hreg_group_l1(const float *table, const float *geom, const float *knn_xyz, i
  * table = hreg_group_l2_table_floats() floats (engine.l2_table); geom [G][32] float4
  * and knn_xyz [G][32][3] from hreg_knn_group; gidx [G*32] rows of feats
  * [*][64] (the level-1 attentive features, 16-byte aligned) ->
- * kp [G][3], att_feat [G][128], desc [G][128]. */
+ * kp [G][3], att_feat [G][128], desc [G][128].  pre (optional, levels 2 and 3, both
+ * kernels): [*][2 * C1] = [W_det_f | W_desc_f] feats, the feature blocks of the two
+ * first layers precomputed once per feature row (same gidx): then only the 4 geometry
+ * columns of those layers run per grouped row. */
 int hreg_group_l2_table_floats(void);
 int hreg_group_l2(const float *table, const float *geom, const float *knn_xyz,
                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
-                  float *desc, void *stream);
+                  float *desc, const float *pre, void *stream);
 
 /* Fused level-3 grouping stage: C_in = 4 + 128, convs 132->128->128->256,
  * mlp 768->128->256, nsample = 16 (two groups per 32-row tile, G even);
@@ -453,7 +456,7 @@ int hreg_group_l2(const float *table, const float *geom, const float *knn_xyz,
 int hreg_group_l3_table_floats(void);
 int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
-                  float *desc, void *stream);
+                  float *desc, const float *pre, void *stream);
 
 /* The level-2 / level-3 stages above on the channel-split kernel (group_split.hip):
  * same arguments and outputs, table = hreg_group_split_l{2,3}_table_floats() floats
@@ -462,11 +465,11 @@ int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
 int hreg_group_split_l2_table_floats(void);
 int hreg_group_split_l2(const float *table, const float *geom, const float *knn_xyz,
                         const int32_t *gidx, const float *feats, int G, float *kp,
-                        float *att_feat, float *desc, void *stream);
+                        float *att_feat, float *desc, const float *pre, void *stream);
 int hreg_group_split_l3_table_floats(void);
 int hreg_group_split_l3(const float *table, const float *geom, const float *knn_xyz,
                         const int32_t *gidx, const float *feats, int G, float *kp,
-                        float *att_feat, float *desc, void *stream);
+                        float *att_feat, float *desc, const float *pre, void *stream);
 
 /* Fused FineReg head (layers.py:433-451) for C = 64 (fine_corres_1) or 128
  * (fine_corres_2): small [G*8][16] from hreg_pair_feats (ldf 16), src_desc [G][C]

@@ -74,10 +74,10 @@ _SIGS = {
     "hreg_transformation_loss": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
                                  _vp],
     "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
-    "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
-    "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
-    "hreg_group_split_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
-    "hreg_group_split_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group_split_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group_split_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head_table_floats": [_i],
     "hreg_nbr_head": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],

@@ -59,22 +59,33 @@ using L3 = Cfg<16, 128, 128, 256, 128, 256, 1>;
 // conv stack [geom 4 | gathered feature CF] -> C1 -> C1 -> C3 (+ BN/ReLU epilogues).
 // Offsets (in floats) of the stack's four fragment blocks and three epilogues;
 // NC/NWN/next describe the call that follows the stack (for its prefetch).
-template <class K, int NC, int NWN>
+// PRE: the feature part of the first layer comes precomputed per source point
+// (pre_row = W_f f of this row's neighbour, C1 channels, hreg_gemm over the feature
+// rows) and initialises the accumulators; only the 2 geometry k-steps run here.
+template <class K, int NC, int NWN, bool PRE>
 __device__ __forceinline__ void conv_stack(const gfloat *__restrict__ tb, const float *eb, int fg, int ff,
                                            int f2, int f3, int e1, int e2, int e3, int lane, float2 gin,
-                                           const float4 (&fin)[K::TF / 4], f32x16 (&out)[K::T3],
-                                           const float (&cin)[CARRY], FragSeq next,
+                                           const float4 (&fin)[K::TF / 4], const float *pre_row,
+                                           f32x16 (&out)[K::T3], const float (&cin)[CARRY], FragSeq next,
                                            float (&cout)[CARRY]) {
     constexpr int T1 = K::T1, T3 = K::T3, TF = K::TF;
     const FragSeq sg{fg / 64, 2}, sf{ff / 64, TF}, s2{f2 / 64, T1 * 16}, s3{f3 / 64, T1 * 16};
     f32x16 h1[T1], h2[T1];
     float c1[CARRY], c2[CARRY], c3[CARRY];
-    zero_tiles(h1);
-    // geom part: 2 k-steps (channel 2h + s); feature part: TF k-steps (channel h*TF + s)
-    mfma_pipe<2, T1, T1, first_win<TF, T1>()>(
-        tb, lane, sg, [&](int st) { return st == 0 ? gin.x : gin.y; }, h1, cin, sf, c1);
-    mfma_pipe<TF, T1, T1, first_win<T1 * 16, T1>()>(
-        tb, lane, sf, [&](int st) { return (&fin[st >> 2].x)[st & 3]; }, h1, c1, s2, c2);
+    const int h = lane >> 5;
+    if constexpr (PRE) {
+        load_tiles<T1>(h1, pre_row, h);
+        mfma_pipe<2, T1, T1, first_win<T1 * 16, T1>()>(
+            tb, lane, sg, [&](int st) { return st == 0 ? gin.x : gin.y; }, h1, cin, s2, c2);
+        (void)c1; (void)sf; (void)fin;
+    } else {
+        zero_tiles(h1);
+        // geom part: 2 k-steps (channel 2h + s); feature part: TF k-steps (channel h*TF + s)
+        mfma_pipe<2, T1, T1, first_win<TF, T1>()>(
+            tb, lane, sg, [&](int st) { return st == 0 ? gin.x : gin.y; }, h1, cin, sf, c1);
+        mfma_pipe<TF, T1, T1, first_win<T1 * 16, T1>()>(
+            tb, lane, sf, [&](int st) { return (&fin[st >> 2].x)[st & 3]; }, h1, c1, s2, c2);
+    }
     epilogue<T1>(eb + e1, lane, h1);
     zero_tiles(h2);
     mfma_pipe<T1 * 16, T1, T3, first_win<T1 * 16, T3>()>(
@@ -101,11 +112,11 @@ __device__ __forceinline__ float4 ld_rows(const float *p) {
     }
 }
 
-template <class K>
+template <class K, bool PRE>
 __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
-    float *__restrict__ att_feat, float *__restrict__ desc) {
+    float *__restrict__ att_feat, float *__restrict__ desc, const float *__restrict__ pre) {
     constexpr int CF = K::TF * 2, C3 = K::T3 * 32, CM2 = K::TM2 * 32;
     constexpr int T1 = K::T1, T3 = K::T3, TM1 = K::TM1, TM2 = K::TM2;
     constexpr int NE = K::TABLE - K::F_END;
@@ -158,17 +169,21 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
         const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
         const size_t row = (size_t)t * 32 + j;
         const float2 gin = *reinterpret_cast<const float2 *>(geom + row * 4 + 2 * h);
-        const float *fr = feats + (HREG_L2_EXP == 3 ? row : (size_t)gidx[row]) * CF + h * K::TF;
+        const size_t src = HREG_L2_EXP == 3 ? row : (size_t)gidx[row];
+        const float *fr = feats + src * CF + h * K::TF;
+        const float *pr = PRE ? pre + src * (2 * K::T1 * 32) : nullptr;  // [det C1 | desc C1]
         float ca[CARRY], cb[CARRY];
 
         // ---- detector convs -> emb [C3][32 rows]
         f32x16 emb[T3];
         {
             float4 fin[K::TF / 4];
+            if constexpr (!PRE) {
 #pragma unroll
-            for (int i = 0; i < K::TF / 4; ++i) fin[i] = ld_rows(fr + 4 * i);
-            conv_stack<K, TM1, WM1>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1, K::E_D2,
-                                    K::E_D3, lane, gin, fin, emb, carry, m1em, ca);
+                for (int i = 0; i < K::TF / 4; ++i) fin[i] = ld_rows(fr + 4 * i);
+            }
+            conv_stack<K, TM1, WM1, PRE>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1, K::E_D2,
+                                         K::E_D3, lane, gin, fin, pr, emb, carry, m1em, ca);
         }
 
         // ---- attention: x1 = max_c emb, a = softmax over the group's rows (emb >= 0
@@ -216,10 +231,13 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
             asm volatile("" : "+v"(fra));
             const float *fr2 = reinterpret_cast<const float *>(fra);
             float4 fin[K::TF / 4];
+            if constexpr (!PRE) {
 #pragma unroll
-            for (int i = 0; i < K::TF / 4; ++i) fin[i] = ld_rows(fr2 + 4 * i);
-            conv_stack<K, TM1, WM1>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1, K::E_E2,
-                                    K::E_E3, lane, gin, fin, x1d, cb, m1x2, ca);
+                for (int i = 0; i < K::TF / 4; ++i) fin[i] = ld_rows(fr2 + 4 * i);
+            }
+            conv_stack<K, TM1, WM1, PRE>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1, K::E_E2,
+                                         K::E_E3, lane, gin, fin, PRE ? pr + K::T1 * 32 : nullptr, x1d,
+                                         cb, m1x2, ca);
         }
 
 #pragma unroll
@@ -261,7 +279,9 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
 
 template <class K>
 int launch_group(const float *table, const float *geom, const float *knn_xyz, const int32_t *gidx,
-                 const float *feats, int G, float *kp, float *att_feat, float *desc, void *stream) {
+                 const float *feats, int G, float *kp, float *att_feat, float *desc, const float *pre,
+                 void *stream) {
+    if (reinterpret_cast<uintptr_t>(pre) & 15) return HREG_ERR_INVALID;
     if (!table || !geom || !knn_xyz || !gidx || !feats || !kp || !att_feat || !desc || G < 0)
         return HREG_ERR_INVALID;
     if ((reinterpret_cast<uintptr_t>(feats) & 15) || (reinterpret_cast<uintptr_t>(geom) & 7) ||
@@ -273,8 +293,12 @@ int launch_group(const float *table, const float *geom, const float *knn_xyz, co
     int grid = (NT + WAVES - 1) / WAVES;
     const int cap = 256 * K::WPS * 4 / WAVES * 2;  // two rounds of resident blocks
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(group_fused_kernel<K>, dim3(grid), dim3(256), 0, as_stream(stream), table,
-                       geom, knn_xyz, gidx, feats, G, kp, att_feat, desc);
+    if (pre)
+        hipLaunchKernelGGL((group_fused_kernel<K, true>), dim3(grid), dim3(256), 0, as_stream(stream), table,
+                           geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
+    else
+        hipLaunchKernelGGL((group_fused_kernel<K, false>), dim3(grid), dim3(256), 0, as_stream(stream), table,
+                           geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -286,12 +310,12 @@ extern "C" int hreg_group_l3_table_floats(void) { return L3::TABLE; }
 
 extern "C" int hreg_group_l2(const float *table, const float *geom, const float *knn_xyz,
                              const int32_t *gidx, const float *feats, int G, float *kp,
-                             float *att_feat, float *desc, void *stream) {
-    return launch_group<L2>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, stream);
+                             float *att_feat, float *desc, const float *pre, void *stream) {
+    return launch_group<L2>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre, stream);
 }
 
 extern "C" int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
                              const int32_t *gidx, const float *feats, int G, float *kp,
-                             float *att_feat, float *desc, void *stream) {
-    return launch_group<L3>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, stream);
+                             float *att_feat, float *desc, const float *pre, void *stream) {
+    return launch_group<L3>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre, stream);
 }

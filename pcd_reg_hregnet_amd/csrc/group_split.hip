@@ -68,11 +68,11 @@ using S3 = SCfg<16, 128, 128, 256, 128, 256, 1, 4>;
 
 // stage [geom 4 | feats[gidx[row]] CF] of the tile's 32 rows into buf (the CW waves
 // of the row tile share the float4 loads)
-template <class K>
+template <class K, bool PRE = false>
 __device__ __forceinline__ void stage_rows(float *buf, const float *__restrict__ geom,
                                            const int32_t *__restrict__ gidx,
                                            const float *__restrict__ feats, int t, int cw, int lane) {
-    constexpr int F4 = 1 + K::CF / 4;
+    constexpr int F4 = PRE ? 1 : 1 + K::CF / 4;  // PRE: the first layer reads geometry only
 #pragma unroll
     for (int i = cw * 64 + lane; i < 32 * F4; i += K::CW * 64) {
         const int r = i / F4, c4 = i - r * F4;
@@ -85,12 +85,16 @@ __device__ __forceinline__ void stage_rows(float *buf, const float *__restrict__
 // conv stack [geom | feat] -> C1 -> C1 -> C3 through the A/B buffers; result tiles
 // in out (epilogue applied).  Ends with out in registers; A / B free after the
 // caller's next barrier.
-template <class K, int NP, int NWN>
+// PRE: the first layer's feature part precomputed per source point (pre_row = W_f f of
+// the row's neighbour, C1 channels) initialises this wave's P1 tiles; only the 2
+// geometry k-steps run here.
+template <class K, int NP, int NWN, bool PRE = false>
 __device__ __forceinline__ void conv_stack_split(const gfloat *__restrict__ tb, const float *eb, int fg,
                                                  int ff, int f2, int f3, int e1, int e2, int e3,
                                                  float *A, float *B, int cw, int lane,
                                                  f32x16 (&out)[K::P3], const float (&cin)[SCARRY],
-                                                 FragSeq next, float (&cout)[SCARRY]) {
+                                                 FragSeq next, float (&cout)[SCARRY],
+                                                 const float *pre_row = nullptr) {
     constexpr int T1 = K::T1, TF = K::TF, P1 = K::P1, P3 = K::P3, LDSW = K::LDSW;
     const int h = lane >> 5, j = lane & 31;
     const int c1 = cw * P1, c3 = cw * P3;
@@ -99,21 +103,25 @@ __device__ __forceinline__ void conv_stack_split(const gfloat *__restrict__ tb, 
     const float *arow = A + j * LDSW, *brow = B + j * LDSW;
     float ca[SCARRY], cb[SCARRY];
     f32x16 h1[P1];
-    zero_tiles(h1);
-    pipe_lds<2, P1, P1, swin<TF>()>(
-        tb, lane, sg,
-        [&](int st0, float (&v)[2]) {
-            const float2 t = *reinterpret_cast<const float2 *>(arow + 2 * h);
-            v[0] = t.x; v[1] = t.y;
-        },
-        h1, cin, sf, ca);
-    pipe_lds<TF, P1, P1, swin<T1 * 16>()>(
-        tb, lane, sf,
-        [&](int st0, float (&v)[4]) {
-            const float4 t = *reinterpret_cast<const float4 *>(arow + 4 + h * TF + st0);
-            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-        },
-        h1, ca, s2, cb);
+    auto geom_b = [&](int st0, float (&v)[2]) {
+        const float2 t = *reinterpret_cast<const float2 *>(arow + 2 * h);
+        v[0] = t.x; v[1] = t.y;
+    };
+    if constexpr (PRE) {
+        load_tiles<P1>(h1, pre_row + c1 * 32, h);
+        pipe_lds<2, P1, P1, swin<T1 * 16>()>(tb, lane, sg, geom_b, h1, cin, s2, cb);
+        (void)sf;
+    } else {
+        zero_tiles(h1);
+        pipe_lds<2, P1, P1, swin<TF>()>(tb, lane, sg, geom_b, h1, cin, sf, ca);
+        pipe_lds<TF, P1, P1, swin<T1 * 16>()>(
+            tb, lane, sf,
+            [&](int st0, float (&v)[4]) {
+                const float4 t = *reinterpret_cast<const float4 *>(arow + 4 + h * TF + st0);
+                v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+            },
+            h1, ca, s2, cb);
+    }
     epi<P1, K::T1 * 32>(eb + e1, c1, h, h1);
 #pragma unroll
     for (int i = 0; i < P1; ++i) put_tile<LDSW>(B, c1 + i, j, h, h1[i]);
@@ -130,11 +138,11 @@ __device__ __forceinline__ void conv_stack_split(const gfloat *__restrict__ tb, 
     epi<P3, K::T3 * 32>(eb + e3, c3, h, out);
 }
 
-template <class K>
+template <class K, bool PRE>
 __global__ __launch_bounds__(256, 2) void group_split_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
-    float *__restrict__ att_feat, float *__restrict__ desc) {
+    float *__restrict__ att_feat, float *__restrict__ desc, const float *__restrict__ pre) {
     constexpr int C3 = K::T3 * 32, CM2 = K::TM2 * 32, LDSW = K::LDSW, X2W = K::X2W;
     constexpr int T3 = K::T3, TM1 = K::TM1, P3 = K::P3, PM1 = K::PM1, PM2 = K::PM2;
     constexpr int NE = K::TABLE - K::F_END, KN = K::KN, GPT = K::GPT, RT = K::RT, CW = K::CW;
@@ -187,14 +195,17 @@ __global__ __launch_bounds__(256, 2) void group_split_kernel(
         const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
         float ca[SCARRY], cb[SCARRY];
 
+        // PRE: this lane's row of the precomputed first-layer products [det C1 | desc C1]
+        const float *prow = PRE ? pre + (size_t)gidx[row] * (2 * K::T1 * 32) : nullptr;
         tile_sync();  // previous tile's readers of A are done (and ep is loaded)
-        stage_rows<K>(A, geom, gidx, feats, t, cw, lane);
+        stage_rows<K, PRE>(A, geom, gidx, feats, t, cw, lane);
         tile_sync();
 
         // ---- detector -> emb (this wave's P3 tiles)
         f32x16 emb[P3];
-        conv_stack_split<K, PM1, swin<T3 * 16>()>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3, K::E_D1,
-                                                  K::E_D2, K::E_D3, A, B, cw, lane, emb, carry, m1em, ca);
+        conv_stack_split<K, PM1, swin<T3 * 16>(), PRE>(tb, eb, K::F_DG, K::F_DF, K::F_D2, K::F_D3,
+                                                       K::E_D1, K::E_D2, K::E_D3, A, B, cw, lane, emb,
+                                                       carry, m1em, ca, prow);
 
         // ---- attention: row max over all C3 channels (per-wave partial maxima through
         // LDS; emb >= 0 after ReLU: integer max on the bit patterns), softmax over the group
@@ -242,13 +253,14 @@ __global__ __launch_bounds__(256, 2) void group_split_kernel(
         zero_tiles(y1);
         pipe_lds<T3 * 16, PM1, K::P1, 2>(tb, lane, m1em, ChanB{B + j * LDSW, h}, y1, ca, desc_g,
                                          cb);
-        stage_rows<K>(A, geom, gidx, feats, t, cw, lane);
+        stage_rows<K, PRE>(A, geom, gidx, feats, t, cw, lane);
         tile_sync();
 
         // ---- descriptor -> x1d
         f32x16 x1d[P3];
-        conv_stack_split<K, PM1, swin<T3 * 16>()>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3, K::E_E1,
-                                                  K::E_E2, K::E_E3, A, B, cw, lane, x1d, cb, m1x2, ca);
+        conv_stack_split<K, PM1, swin<T3 * 16>(), PRE>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3,
+                                                       K::E_E1, K::E_E2, K::E_E3, A, B, cw, lane, x1d,
+                                                       cb, m1x2, ca, PRE ? prow + K::T1 * 32 : nullptr);
         // x2 = k-max of x1d (one row per group) -> X2; x1d -> B
 #pragma unroll
         for (int i = 0; i < P3; ++i) {
@@ -295,7 +307,9 @@ __global__ __launch_bounds__(256, 2) void group_split_kernel(
 
 template <class K>
 int launch_split(const float *table, const float *geom, const float *knn_xyz, const int32_t *gidx,
-                 const float *feats, int G, float *kp, float *att_feat, float *desc, void *stream) {
+                 const float *feats, int G, float *kp, float *att_feat, float *desc, const float *pre,
+                 void *stream) {
+    if (reinterpret_cast<uintptr_t>(pre) & 15) return HREG_ERR_INVALID;
     if (!table || !geom || !knn_xyz || !gidx || !feats || !kp || !att_feat || !desc || G < 0)
         return HREG_ERR_INVALID;
     if ((reinterpret_cast<uintptr_t>(feats) & 15) || (reinterpret_cast<uintptr_t>(geom) & 15) ||
@@ -307,8 +321,12 @@ int launch_split(const float *table, const float *geom, const float *knn_xyz, co
     int grid = (NT + K::RT - 1) / K::RT;
     const int cap = 256 * 2 * 2;  // two resident workgroups per CU, two rounds
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(group_split_kernel<K>, dim3(grid), dim3(256), 0, as_stream(stream), table, geom,
-                       knn_xyz, gidx, feats, G, kp, att_feat, desc);
+    if (pre)
+        hipLaunchKernelGGL((group_split_kernel<K, true>), dim3(grid), dim3(256), 0, as_stream(stream), table,
+                           geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
+    else
+        hipLaunchKernelGGL((group_split_kernel<K, false>), dim3(grid), dim3(256), 0, as_stream(stream), table,
+                           geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -320,12 +338,12 @@ extern "C" int hreg_group_split_l3_table_floats(void) { return S3::TABLE; }
 
 extern "C" int hreg_group_split_l2(const float *table, const float *geom, const float *knn_xyz,
                                    const int32_t *gidx, const float *feats, int G, float *kp,
-                                   float *att_feat, float *desc, void *stream) {
-    return launch_split<S2>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, stream);
+                                   float *att_feat, float *desc, const float *pre, void *stream) {
+    return launch_split<S2>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre, stream);
 }
 
 extern "C" int hreg_group_split_l3(const float *table, const float *geom, const float *knn_xyz,
                                    const int32_t *gidx, const float *feats, int G, float *kp,
-                                   float *att_feat, float *desc, void *stream) {
-    return launch_split<S3>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, stream);
+                                   float *att_feat, float *desc, const float *pre, void *stream) {
+    return launch_split<S3>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre, stream);
 }

@@ -143,6 +143,21 @@ __device__ __forceinline__ void epilogue(const float *ab, int lane, f32x16 (&acc
         }
 }
 
+// accumulator tiles initialised from a per-row vector (this lane's row): register q of
+// tile co <- row[chan(co, q, h)] (4 float4 loads per tile).  Used for first-layer blocks
+// precomputed once per source point (W_f f_n, gathered by the row's neighbour index).
+template <int T>
+__device__ __forceinline__ void load_tiles(f32x16 (&acc)[T], const float *__restrict__ row, int h) {
+#pragma unroll
+    for (int co = 0; co < T; ++co)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float4 a = *reinterpret_cast<const float4 *>(row + co * 32 + 8 * r + 4 * h);
+            acc[co][4 * r] = a.x; acc[co][4 * r + 1] = a.y;
+            acc[co][4 * r + 2] = a.z; acc[co][4 * r + 3] = a.w;
+        }
+}
+
 template <int N>
 __device__ __forceinline__ void zero_tiles(f32x16 (&t)[N]) {
 #pragma unroll

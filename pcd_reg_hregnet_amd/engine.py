@@ -52,6 +52,10 @@ COARSE_SPLIT = os.environ.get("HREG_COARSE_SPLIT", "1") != "0"
 # neighbour branch (descriptor block of convs_2[0]): per-point products precomputed, the
 # fused kernels multiply only the small / geometry columns per row
 HEAD_PRE = os.environ.get("HREG_HEAD_PRE", "1") != "0"
+# levels 2 / 3: the feature blocks of the detector's and the descriptor's first conv,
+# W_f f per level-(l-1) feature row, precomputed once (one GEMM) instead of once per
+# grouped row (k = 32 / 16 rows gather each feature row)
+LEVEL_PRE = os.environ.get("HREG_LEVEL_PRE", "1") != "0"
 
 
 @dataclass
@@ -136,6 +140,11 @@ class PreparedWeights:
             self.desc.append(_stack(sd, e + ".convs", 3))
             self.desc_mlp.append([_conv_bn(sd, e + ".mlp1.0", e + ".mlp1.1"),
                                   _conv_bn(sd, e + ".mlp2.0", e + ".mlp2.1")])
+        # [W_det_f; W_desc_f] of the level's two first convs (columns 4: of [geom 4 | feat])
+        self.level_pre = [None] + [
+            Lin(torch.cat([self.det[lv][0].W[:, 4:], self.desc[lv][0].W[:, 4:]]).contiguous(),
+                torch.ones(2 * self.det[lv][0].N), torch.zeros(2 * self.det[lv][0].N), False)
+            for lv in (1, 2)]
         C = 256
         self.coarse_convs1 = _stack(sd, "coarse_corres.convs_1", 3, _perm_coarse(C))
         # convs_1[0] split by input block (COARSE_SPLIT): the 16 per-row columns, and
@@ -173,7 +182,7 @@ class PreparedWeights:
         for name in ("fine_corres_2", "fine_corres_1"):
             self.head_table[name] = mlp_head_table(self.fine[name][1])
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
-                     "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre",
+                     "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre",
                      "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2s_table",
                      "l3s_table", "fine_table",
                      "nbr_table", "head_table", "mlpx"):
@@ -623,7 +632,9 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         else:
             name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
                            ("hreg_group_l3", P.l3_table))
-        call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, _stream())
+        pre = (gemm([_seg(feats, 0, Cf)], P.level_pre[lvl], feats.shape[0]) if LEVEL_PRE
+               else None)
+        call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())
         sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)
         return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx

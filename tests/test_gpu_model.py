@@ -180,12 +180,16 @@ def test_graph_lanes_match_eager(net):
                 assert torch.equal(out["src_feats"]["desc_3"], ref["src_feats"]["desc_3"])
 
 
-@pytest.mark.parametrize("lvl,split", [(0, False), (1, False), (2, False), (1, True), (2, True)])
-def test_fused_level_matches_layerwise(net, lvl, split):
+@pytest.mark.parametrize("lvl,split,pre", [(0, False, False), (1, False, False), (2, False, False),
+                                           (1, True, False), (2, True, False), (1, False, True),
+                                           (2, False, True), (1, True, True), (2, True, True)])
+def test_fused_level_matches_layerwise(net, lvl, split, pre, monkeypatch):
     """The fused level kernels (group_l1 / group_fused: activations in MFMA accumulators;
-    group_split: channel-split through LDS) against the layer-by-layer GEMM path on the
-    same grouping; fp32 summation order differs, so within 1e-4."""
+    group_split: channel-split through LDS; pre: the first convs' feature blocks
+    precomputed per feature row, engine.LEVEL_PRE) against the layer-by-layer GEMM path on
+    the same grouping; fp32 summation order differs, so within 1e-4."""
     from pcd_reg_hregnet_amd import engine, synthetic
+    monkeypatch.setattr(engine, "LEVEL_PRE", pre)
     P = net.prepared(torch.device("cuda"))
     s, _, _, _ = synthetic.lidar_batch(2, 4096, seed0=60)
     pts = torch.from_numpy(s).cuda()
