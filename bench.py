@@ -84,11 +84,14 @@ L3_BYTES_PER_GROUP = 4.0 * (16 * 4 + 16 * 3 + 16 + 16 * 128 + 3 + 256 + 256)
 
 def _level_work(lvl):
     cfg = {2: (32, 64, 64, 128, 64, 128), 3: (16, 128, 128, 256, 128, 256)}[lvl]
+    kn, cf, c1 = cfg[:3]
     nb = L2_BYTES_PER_GROUP if lvl == 2 else L3_BYTES_PER_GROUP
 
     def work(a):
-        G = a[5]
-        return (_level_flops(*cfg, False) * G, nb * G, _level_flops(*cfg, a[9] is not None) * G)
+        G, pre = a[5], a[9] is not None
+        # pre: each row gathers its precomputed [det c1 | desc c1] row instead of the features
+        b = nb + (4.0 * kn * (2 * c1 - cf) if pre else 0.0)
+        return _level_flops(*cfg, False) * G, b * G, _level_flops(*cfg, pre) * G
     return work
 
 
