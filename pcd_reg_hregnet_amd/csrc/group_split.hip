@@ -53,7 +53,8 @@ struct SCfg {
     static constexpr int F_E3 = F_E2 + T1 * T1 * 16 * 64;
     static constexpr int F_M1 = F_E3 + T3 * T1 * 16 * 64;
     static constexpr int F_M2 = F_M1 + TM1 * 3 * T3 * 16 * 64;
-    static constexpr int F_END = F_M2 + TM2 * TM1 * 16 * 64;
+    static constexpr int F_X2 = F_M2 + TM2 * TM1 * 16 * 64;  // mlp1 x2 block, row-major [CM1][C3]
+    static constexpr int F_END = F_X2 + CM1 * C3;
     static constexpr int E_D1 = F_END, E_D2 = E_D1 + 2 * C1, E_D3 = E_D2 + 2 * C1,
                          E_E1 = E_D3 + 2 * C3, E_E2 = E_E1 + 2 * C1, E_E3 = E_E2 + 2 * C1,
                          E_M1 = E_E3 + 2 * C3, E_M2 = E_M1 + 2 * CM1, TABLE = E_M2 + 2 * CM2;
@@ -168,7 +169,6 @@ __global__ __launch_bounds__(256, 2) void group_split_kernel(
     const int c3 = cw * P3, m1 = cw * PM1, m2 = cw * PM2;
     constexpr int MS = 3 * T3 * 16;  // mlp1 fragment stride per output tile
     const FragSeq det_g{K::F_DG / 64 + cw * K::P1 * 2, 2}, desc_g{K::F_EG / 64 + cw * K::P1 * 2, 2};
-    const FragSeq m1x2{K::F_M1 / 64 + m1 * MS, MS};
     const FragSeq m1x1{K::F_M1 / 64 + m1 * MS + T3 * 16, MS};
     const FragSeq m1em{K::F_M1 / 64 + m1 * MS + 2 * T3 * 16, MS};
     const FragSeq fm2{K::F_M2 / 64 + m2 * TM1 * 16, TM1 * 16};
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256, 2) void group_split_kernel(
         f32x16 x1d[P3];
         conv_stack_split<K, PM1, swin<T3 * 16>(), PRE>(tb, eb, K::F_EG, K::F_EF, K::F_E2, K::F_E3,
                                                        K::E_E1, K::E_E2, K::E_E3, A, B, cw, lane, x1d,
-                                                       cb, m1x2, ca, PRE ? prow + K::T1 * 32 : nullptr);
+                                                       cb, m1x1, ca, PRE ? prow + K::T1 * 32 : nullptr);
         // x2 = k-max of x1d (one row per group) -> X2; x1d -> B
 #pragma unroll
         for (int i = 0; i < P3; ++i) {
@@ -278,12 +278,52 @@ __global__ __launch_bounds__(256, 2) void group_split_kernel(
         }
         tile_sync();
 
-        // ---- mlp1, x2 part (the group's row of X2 for every row) and x1d part
-        pipe_lds<T3 * 16, PM1, PM1, swin<T3 * 16>()>(
-            tb, lane, m1x2, ChanB{X2 + (KN == 32 ? 0 : j >> 4) * X2W, h}, y1, ca,
-            m1x1, cb);
+        // ---- mlp1, x2 part: x2 (the k-max row, layers.py:204-206) is the same for every
+        // row of a group, so W_x2 x2 is a matrix-vector product per group -- lane j of
+        // half h: output channel (m1 + i) * 32 + j over the half's C3 / 2 input channels
+        // (W_x2 rows from the L2-resident table, x2 from X2 as LDS broadcasts), halves
+        // summed, then moved into the accumulator layout -- instead of MFMAs over the
+        // group's 16 / 32 identical rows.  Then the x1d part.
+        {
+            constexpr int CH = C3 / 2;
+            float v[PM1][GPT];
+#pragma unroll
+            for (int i = 0; i < PM1; ++i) {
+#pragma unroll
+                for (int g2 = 0; g2 < GPT; ++g2) v[i][g2] = 0.f;
+                const float *wr = table + K::F_X2 + (size_t)((m1 + i) * 32 + j) * C3 + h * CH;
+#pragma unroll 8
+                for (int c4 = 0; c4 < CH / 4; ++c4) {
+                    const float4 wv = *reinterpret_cast<const float4 *>(wr + c4 * 4);
+#pragma unroll
+                    for (int g2 = 0; g2 < GPT; ++g2) {
+                        const float4 xv = *reinterpret_cast<const float4 *>(X2 + g2 * X2W + h * CH + c4 * 4);
+                        v[i][g2] = fmaf(wv.x, xv.x, v[i][g2]);
+                        v[i][g2] = fmaf(wv.y, xv.y, v[i][g2]);
+                        v[i][g2] = fmaf(wv.z, xv.z, v[i][g2]);
+                        v[i][g2] = fmaf(wv.w, xv.w, v[i][g2]);
+                    }
+                }
+#pragma unroll
+                for (int g2 = 0; g2 < GPT; ++g2)  // commutative: both halves get the same bits
+                    v[i][g2] = fadd_rn(v[i][g2], __shfl_xor(v[i][g2], 32));
+            }
+            const int mg = KN == 32 ? 0 : j >> 4;
+#pragma unroll
+            for (int i = 0; i < PM1; ++i)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int src = (q & 3) + 8 * (q >> 2) + 4 * h;  // lane holding chan(m1+i, q, h)
+                    float a = __shfl(v[i][0], src);
+                    if constexpr (GPT == 2) {
+                        const float b = __shfl(v[i][1], src);
+                        a = mg ? b : a;
+                    }
+                    y1[i][q] = fadd_rn(y1[i][q], a);
+                }
+        }
         pipe_lds<T3 * 16, PM1, PM2, swin<TM1 * 16>()>(tb, lane, m1x1, ChanB{B + j * LDSW, h}, y1,
-                                                      cb, fm2, ca);
+                                                      ca, fm2, cb);
         epi<PM1, TM1 * 32>(eb + K::E_M1, m1, h, y1);
 #pragma unroll
         for (int i = 0; i < PM1; ++i) put_tile<LDSW>(A, m1 + i, j, h, y1[i]);
@@ -292,7 +332,7 @@ __global__ __launch_bounds__(256, 2) void group_split_kernel(
         // ---- mlp2 + k-max -> descriptor; prefetches the next tile's first window
         f32x16 y2[PM2];
         zero_tiles(y2);
-        pipe_lds<TM1 * 16, PM2, K::P1, 2>(tb, lane, fm2, ChanB{A + j * LDSW, h}, y2, ca, det_g,
+        pipe_lds<TM1 * 16, PM2, K::P1, 2>(tb, lane, fm2, ChanB{A + j * LDSW, h}, y2, cb, det_g,
                                           carry);
         epi<PM2, CM2>(eb + K::E_M2, m2, h, y2);
 #pragma unroll

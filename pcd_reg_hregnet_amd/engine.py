@@ -319,6 +319,8 @@ def split_table(det, desc, mlp) -> torch.Tensor:
         parts += [_group4(g, 2), _group4(f, 4), _group4(frag_layer(stack[1].W), 4),
                   _group4(frag_layer(stack[2].W), 4)]
     parts += [_group4(frag_layer(mlp[0].W), 4), _group4(frag_layer(mlp[1].W), 4)]
+    # mlp1's x2 block row-major [CM1][C3] (group_split.hip: per-group matrix-vector product)
+    parts += [mlp[0].W[:, :det[2].W.shape[0]].contiguous()]
     for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()

@@ -207,15 +207,23 @@ def test_l3_table_size_matches_kernel(P):
 
 
 def test_split_tables_match_kernel(P):
-    """group_split.hip tables: same size as the chained kernel's, same fragments
-    regrouped 4 k-steps per lane (2 for the geometry block)."""
+    """group_split.hip tables: the chained kernel's fragments regrouped 4 k-steps per lane
+    (2 for the geometry block), plus mlp1's x2 block row-major [CM1][C3] (the per-group
+    matrix-vector product) before the epilogues."""
     _, prep = P
     from pcd_reg_hregnet_amd import _lib
     L = _lib.load(require_gpu=False)
     assert prep.l2s_table.numel() == L.hreg_group_split_l2_table_floats()
     assert prep.l3s_table.numel() == L.hreg_group_split_l3_table_floats()
-    for a, b in ((prep.l2_table, prep.l2s_table), (prep.l3_table, prep.l3s_table)):
-        assert torch.equal(torch.sort(a).values, torch.sort(b).values)
+    for a, b, lvl in ((prep.l2_table, prep.l2s_table, 1), (prep.l3_table, prep.l3s_table, 2)):
+        a, b = a.cpu(), b.cpu()
+        x2 = prep.desc_mlp[lvl][0].W[:, :prep.det[lvl][2].N].reshape(-1).cpu()
+        ne = sum(2 * lin.N for lin in (*prep.det[lvl], *prep.desc[lvl], *prep.desc_mlp[lvl]))
+        nf = b.numel() - x2.numel() - ne  # b = [fragments][x2 block][epilogues]
+        assert torch.equal(b[nf:nf + x2.numel()], x2)
+        bx = torch.cat([b[:nf], b[nf + x2.numel():]])
+        assert bx.numel() == a.numel()
+        assert torch.equal(torch.sort(a).values, torch.sort(bx).values)
 
 
 def test_fine_head_table_sizes_match_kernel(P):
