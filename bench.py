@@ -367,7 +367,7 @@ def bench_train(args, world, rank, device):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", choices=("hregnet", "v2", "train"), default="hregnet",
                     help="v2: Model_V2 at config 5 (2 x 65536-pt pairs per GPU); train: the "
@@ -380,9 +380,11 @@ def main():
     ap.add_argument("--executor", choices=("graph", "pipeline", "serial"), default="graph",
                     help="graph: pipelined forward replayed as HIP graphs; pipeline: same "
                          "eagerly; serial: no cross-batch overlap")
-    ap.add_argument("--lanes", type=int, default=4,
+    ap.add_argument("--lanes", type=int, default=None,
                     help="graph executor: batches in flight at once, one stream each "
-                         "(a step is still one forward over one batch)")
+                         "(a step is still one forward over one batch); default 8 (A/B: "
+                         "+3 %% over 4), 4 for v2 (its cluster FPS spins up to 256 waves "
+                         "per launch and needs every launch's participants co-resident)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--split", default=None,
                     help="comma list of levels (2,3) on the channel-split group kernel "
@@ -395,8 +397,19 @@ def main():
         args.batch = V2_PAIRS_PER_GPU if v2 else PAIRS_PER_GPU
     if args.points is None:
         args.points = V2_POINTS if v2 else POINTS
+    if args.lanes is None:
+        args.lanes = 4 if v2 else 8
     if args.model != "train" and args.executor == "graph" and args.steps % args.lanes:
-        ap.error("--steps must be a multiple of --lanes")
+        # a replay runs one batch per lane: time exactly --steps forwards with the most
+        # lanes <= --lanes that divide it, powers of two first (the streams share
+        # GPU_MAX_HW_QUEUES = 4 hardware queues: 5 or 6 lanes measured slower than 4;
+        # e.g. --steps 20 --lanes 8 -> 4 lanes)
+        cand = [d for d in range(1, args.lanes + 1) if args.steps % d == 0]
+        pow2 = [d for d in cand if d & (d - 1) == 0]
+        lanes = max(pow2) if max(pow2) >= 4 or max(pow2) == max(cand) else max(cand)
+        print(f"bench: --steps {args.steps} is not a multiple of --lanes {args.lanes}; "
+              f"using {lanes} lanes", file=sys.stderr)
+        args.lanes = lanes
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
