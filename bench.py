@@ -476,6 +476,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if gpipe is not None:
+        gpipe.check()  # device status of replayed multi-workgroup FPS (after the sync)
     if args.executor == "graph":
         timer.enabled = True
         with torch.no_grad():

@@ -63,6 +63,13 @@ enum {
     HREG_ERR_UNSUPPORTED = 3  /* shape outside what the kernels implement (e.g. K > 64) */
 };
 
+/* Sticky error bits that asynchronous kernels raise on the device (no host round trip
+ * at launch time); read (and optionally cleared) by hreg_device_status. */
+enum {
+    HREG_STATUS_FPS_TIMEOUT = 1  /* multi-workgroup FPS (n > 16384): a participant's
+                                    exchange poll expired; that cloud's idx holds zeros */
+};
+
 /* ---------------- point_utils_cuda boundary ---------------- */
 
 /* points [b,n,3] f32, temp [b,n] f32 scratch (required for n > 16384, may be NULL
@@ -500,6 +507,18 @@ int hreg_nbr_head(const float *table, const float *desc, const int32_t *gidx, co
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */
 int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,
                           int32_t *idx, uint64_t *stamps, void *stream);
+
+/* Reads the device status word (HREG_STATUS_* bits raised by kernels since the last
+ * clear) into *status after the device work issued so far; clear != 0 resets it.
+ * Synchronous (a device-to-host copy). */
+int hreg_device_status(int *status, int clear);
+
+/* Diagnostic: the multi-workgroup FPS kernel forced on any n with at most polls_max
+ * exchange polls per iteration, participant `stall` never publishing (-1: none) --
+ * the timeout path of hreg_furthest_point_sampling (tests/test_gpu_ops.py). */
+int hreg_debug_fps_cluster(int b, int n, int m, const float *points, float *temp,
+                           int32_t *idx, float *sampled_xyz, int stall, unsigned polls_max,
+                           void *stream);
 
 /* library build id (for the loaded-.so audit) */
 const char *hreg_version(void);

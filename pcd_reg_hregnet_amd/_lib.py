@@ -18,6 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HREG_LIB") or os.path.join(_HERE, "libhregnet_amd.so")
 
 HREG_OK = 0
+HREG_STATUS_FPS_TIMEOUT = 1
 _ERRORS = {1: "invalid argument", 2: "kernel launch failed", 3: "unsupported shape"}
 
 HREG_EPI_AFFINE = 0
@@ -95,6 +96,8 @@ _SIGS = {
     "hreg_rowdot_bwd": [_vp, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_relu_bwd": [_vp, _vp, ctypes.c_size_t, _vp, _vp],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_debug_fps_cluster": [_i, _i, _i, _vp, _vp, _vp, _vp, _i, ctypes.c_uint, _vp],
+    "hreg_device_status": [ctypes.POINTER(ctypes.c_int), _i],
     "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_apply": [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp],
     "hreg_bn_backward": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
@@ -201,6 +204,16 @@ def call(name: str, *args) -> None:
     rc = getattr(L, name)(*conv)
     if rc != HREG_OK:
         raise RuntimeError(f"{name} failed: {_ERRORS.get(rc, rc)} (code {rc})")
+
+
+def device_status(clear: bool = True) -> int:
+    """HREG_STATUS_* bits raised by kernels since the last clear (synchronous)."""
+    L = load()
+    v = ctypes.c_int(0)
+    rc = L.hreg_device_status(ctypes.byref(v), 1 if clear else 0)
+    if rc != HREG_OK:
+        raise RuntimeError(f"hreg_device_status failed: {_ERRORS.get(rc, rc)} (code {rc})")
+    return v.value
 
 
 def gemm(g: Gemm) -> None:

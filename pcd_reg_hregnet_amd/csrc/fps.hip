@@ -323,8 +323,11 @@ __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__
 // reach iteration j + 2 (same parity slot) before every participant has
 // published j + 1, i.e. finished reading j.  The slots live in the caller's
 // temp buffer, zeroed by the launcher (tags 0 never match j >= 1).  Every
-// poll loop is bounded; on expiry the kernel flags the cloud's idx[0] = -1 and
-// every wave exits.
+// poll loop is bounded; on expiry the wave sets HREG_STATUS_FPS_TIMEOUT in the
+// library's device status word (read and cleared by hreg_device_status, which the
+// host checks at its sync points), fills the cloud's remaining idx entries with
+// 0 and sampled rows with point 0 (valid indices for every consumer), and moves
+// on to its next cloud (every cloud has its own slots).
 // tools/fps_experiment.py variants: HREG_FPS_EXP 1 = four lanes publish in one store
 // instruction, 2 = s_sleep between polls; HREG_FPS_S forces the slots per lane,
 // HREG_FPS_PAD the slot stride (16: one 128-byte line per participant)
@@ -343,6 +346,13 @@ struct SyncSlot {
 constexpr int FPS_CL_MAXP = 64;
 constexpr uint32_t FPS_CL_POLLS = 1u << 22;
 
+}  // namespace
+
+// sticky error bits of asynchronous kernels (HREG_STATUS_*), hreg_device_status()
+__device__ int g_hreg_status = 0;
+
+namespace {
+
 __device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -357,7 +367,7 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                                                          int32_t *__restrict__ idx_out,
                                                          float *__restrict__ sampled_out, int b,
                                                          int n, int m, int bs, int L, int Q, int NP,
-                                                         float inf) {
+                                                         float inf, uint32_t polls_max, int stall) {
     constexpr int S2 = S / 2;
     static_assert(S % 2 == 0 && S <= 32, "slots");
     const int p = blockIdx.x;  // participant
@@ -388,7 +398,8 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                 o[0] = x1; o[1] = y1; o[2] = z1;
             }
         }
-        for (int j = 1; j < m; ++j) {
+        bool timed_out = false;
+        for (int j = 1; j < m && !timed_out; ++j) {
             const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
             float best = -1.0f;
 #pragma unroll
@@ -428,7 +439,7 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                 st_agent(&cur[p].w[lane], v);
             }
 #else
-            if (lane == 0) {
+            if (lane == 0 && p != stall) {  // stall: hreg_debug_fps_cluster's forced-stall test
                 st_agent(&cur[p].w[1], tag | __float_as_uint(wx));
                 st_agent(&cur[p].w[2], tag | __float_as_uint(wy));
                 st_agent(&cur[p].w[3], tag | __float_as_uint(wz));
@@ -453,10 +464,22 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
 #if HREG_FPS_EXP == 2
                 __builtin_amdgcn_s_sleep(1);
 #endif
-                if (++polls > FPS_CL_POLLS) {
-                    if (lane == 0) idx_out[(size_t)cloud * m] = -1;
-                    return;
+                if (++polls > polls_max) {
+                    timed_out = true;
+                    break;
                 }
+            }
+            if (timed_out) {
+                // the selection of this cloud is lost: flag it, leave valid indices behind
+                if (lane == 0) atomicOr(&g_hreg_status, HREG_STATUS_FPS_TIMEOUT);
+                for (int jj = j + lane; jj < m; jj += 64) {
+                    idx_out[(size_t)cloud * m + jj] = 0;
+                    if (sampled_out) {
+                        float *o = sampled_out + ((size_t)cloud * m + jj) * 3;
+                        o[0] = P[0]; o[1] = P[1]; o[2] = P[2];
+                    }
+                }
+                break;
             }
             const float cd = lane < NP ? __uint_as_float((uint32_t)(w0 >> 32)) : -__builtin_huge_valf();
             const float gmax = wave_max_uniform(cd, inf);
@@ -530,7 +553,8 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
 
 template <bool WEIGHTED>
 int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *temp, int32_t *idx,
-               float *sampled, hipStream_t st) {
+               float *sampled, hipStream_t st, uint32_t polls_max = FPS_CL_POLLS, int stall = -1,
+               bool force_cluster = false) {
     if (b < 0 || n <= 0 || xyz == nullptr || idx == nullptr) return HREG_ERR_INVALID;
     if (WEIGHTED && w == nullptr) return HREG_ERR_INVALID;
     if (b == 0 || m <= 0) return HREG_OK;  // .cu:92: if (m <= 0) return;
@@ -539,7 +563,8 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
     const int Q = (n + bs - 1) / bs;
     int T, G, QT;
     choose_geometry(n, WEIGHTED, T, G, QT);
-    if (launch_reg<WEIGHTED>(T, G, QT, b, n, m, bs, L, xyz, w, temp, idx, sampled, nullptr, st)) {
+    if (!force_cluster &&
+        launch_reg<WEIGHTED>(T, G, QT, b, n, m, bs, L, xyz, w, temp, idx, sampled, nullptr, st)) {
         HREG_CHECK_LAUNCH();
         return HREG_OK;
     }
@@ -561,12 +586,14 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
 #define HREG_FPS_CL(SS)                                                                         \
     if (S == SS)                                                                                \
         hipLaunchKernelGGL((fps_cluster_kernel<SS, WEIGHTED>), grid, dim3(64), 0, st, xyz, w,     \
-                           slots, idx, sampled, b, n, m, bs, L, Q, NP, __builtin_huge_valf());
+                           slots, idx, sampled, b, n, m, bs, L, Q, NP, __builtin_huge_valf(),   \
+                           polls_max, stall);
         HREG_FPS_CL(8) HREG_FPS_CL(16) HREG_FPS_CL(32)
 #undef HREG_FPS_CL
         HREG_CHECK_LAUNCH();
         return HREG_OK;
     }
+    if (force_cluster) return HREG_ERR_UNSUPPORTED;
     hipLaunchKernelGGL((fps_mem_kernel<WEIGHTED>), dim3(b), dim3(1024), 0, st, xyz, w, temp, idx,
                        sampled, n, m, bs, L, Q);
     HREG_CHECK_LAUNCH();
@@ -605,4 +632,24 @@ extern "C" int hreg_weighted_furthest_point_sampling(int b, int n, int m, const 
                                                      int32_t *idx, float *sampled_xyz,
                                                      void *stream) {
     return launch_fps<true>(b, n, m, points, weights, temp, idx, sampled_xyz, as_stream(stream));
+}
+
+extern "C" int hreg_device_status(int *status, int clear) {
+    if (!status) return HREG_ERR_INVALID;
+    if (hipMemcpyFromSymbol(status, HIP_SYMBOL(g_hreg_status), sizeof(int)) != hipSuccess)
+        return HREG_ERR_LAUNCH;
+    if (clear && *status) {
+        const int zero = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_hreg_status), &zero, sizeof(int)) != hipSuccess)
+            return HREG_ERR_LAUNCH;
+    }
+    return HREG_OK;
+}
+
+extern "C" int hreg_debug_fps_cluster(int b, int n, int m, const float *points, float *temp,
+                                      int32_t *idx, float *sampled_xyz, int stall,
+                                      unsigned polls_max, void *stream) {
+    if (polls_max == 0) return HREG_ERR_INVALID;
+    return launch_fps<false>(b, n, m, points, nullptr, temp, idx, sampled_xyz, as_stream(stream),
+                             polls_max, stall, true);
 }

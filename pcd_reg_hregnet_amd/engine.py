@@ -458,7 +458,30 @@ def _empty(*shape, dtype=torch.float32, device):
     return torch.empty(shape, dtype=dtype, device=device)
 
 
+# set when a multi-workgroup FPS (n > 16384) has been enqueued since the last
+# check_device_status(): only those kernels raise device status bits
+_status_pending = False
+
+
+def check_device_status(force: bool = False):
+    """Raise if a kernel flagged an error on the device since the last check (the
+    multi-workgroup FPS poll timeout, HREG_STATUS_FPS_TIMEOUT: its cloud's indices were
+    replaced by zeros).  Synchronous; called at the sync points the executors already
+    have (GraphPipeline.run, Pipeline.run, models.*.forward when such an FPS ran)."""
+    global _status_pending
+    if not (_status_pending or force):
+        return
+    _status_pending = False
+    st = _lib.device_status(clear=True)
+    if st & _lib.HREG_STATUS_FPS_TIMEOUT:
+        raise RuntimeError("multi-workgroup FPS: exchange poll timed out on the device; "
+                           "the affected clouds' FPS indices are invalid (zeros)")
+    if st:
+        raise RuntimeError(f"device status {st:#x}")
+
+
 def fps(xyz, npoint, weights=None, out=None):
+    global _status_pending
     nb, n, _ = xyz.shape
     dev = xyz.device
     if out is None:
@@ -466,7 +489,10 @@ def fps(xyz, npoint, weights=None, out=None):
         sampled = _empty(nb, npoint, 3, device=dev)
     else:
         idx, sampled = out
-    temp = _empty(nb, n, device=dev) if n > 16384 else None
+    # temp: exchange slots of the multi-workgroup kernel, which also takes weighted
+    # clouds above 8192 points (their register geometry has no single-workgroup case)
+    temp = _empty(nb, n, device=dev) if n > 8192 else None
+    _status_pending |= n > 16384 or (weights is not None and n > 8192)
     if weights is None:
         call("hreg_furthest_point_sampling", nb, n, npoint, xyz, temp, idx, sampled, _stream())
     else:
@@ -984,6 +1010,7 @@ class Pipeline:
                 t.record_stream(main)
             out = hregnet_forward(self.P, src, dst, use_weights, l1=g, pts=pts, v2=self.v2)
             outs.append(model_v2_finish(out) if self.v2 else out)
+        check_device_status()  # syncs only when a multi-workgroup FPS ran
         return outs
 
 
@@ -1022,6 +1049,10 @@ class GraphPipeline:
         stage1_into(self.bufs[0][0], self.src[0], self.dst[0])
         self._rest(0, 0)
         torch.cuda.synchronize()
+        # the captured graphs contain multi-workgroup FPS launches (n > 16384): their
+        # device status is checked by check() after replays
+        self.status_check = _status_pending
+        check_device_status()
         self.pool = torch.cuda.graph_pool_handle()
         self.g_first = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_first, pool=self.pool):
@@ -1082,6 +1113,14 @@ class GraphPipeline:
     def load(self, src, dst, lane: int = 0):
         self.src[lane].copy_(src)
         self.dst[lane].copy_(dst)
+
+    def check(self):
+        """Raise if a replayed multi-workgroup FPS flagged a poll timeout (synchronous
+        when the graphs hold such launches; call it where the caller syncs anyway)."""
+        global _status_pending
+        _status_pending = False
+        if self.status_check:
+            check_device_status(force=True)
 
     def run(self, steps: int):
         """Runs `steps` rounds; a round is one complete forward of every lane's static

@@ -2,8 +2,11 @@
 
 transformation_loss keeps the reference's signature and 7-tuple result
 (losses/losses.py:97-134); the per-pair work and the batch means run in one
-kernel (csrc/losses.hip, hreg_transformation_loss).  Forward only: the
-training backward is SURVEY.md 8(f) rank 1, not built yet.
+kernel (csrc/losses.hip, hreg_transformation_loss).  As in the reference, loss,
+loss_R and loss_t are differentiable in pred_R / pred_t when those require grad
+(backward: hreg_transformation_loss_bwd through train_graph.transformation_loss);
+the error metrics (R_err, geodesic_dist, T_err, eucl_dist) are returned without
+gradient (the reference's trainers only log them).
 """
 from __future__ import annotations
 
@@ -38,6 +41,16 @@ def transformation_loss(pred_R, pred_t, gt_R, gt_t, alpha=1.0):
     eucl = torch.empty(B, device=dev)
     _lib.call("hreg_transformation_loss", pR, pt, gR, gt, B, float(alpha), scalars, R_err, T_err,
               geo, eucl, _lib.stream_handle())
+    if torch.is_grad_enabled() and (pred_R.requires_grad or pred_t.requires_grad):
+        from . import train_graph
+        R, t = pred_R.float().contiguous(), pred_t.float().contiguous()
+        loss, _ = train_graph.transformation_loss(R, t, gR, gt, alpha)
+        # loss_R / loss_t: the alpha = 1 loss with the other input detached carries
+        # exactly the gradient of that part; its value is replaced by the part's
+        lR = train_graph.transformation_loss(R, t.detach(), gR, gt, 1.0)[0]
+        lt = train_graph.transformation_loss(R.detach(), t, gR, gt, 1.0)[0]
+        return (loss, lR - lR.detach() + scalars[1], lt - lt.detach() + scalars[2], R_err, geo,
+                T_err, eucl)
     return scalars[0], scalars[1], scalars[2], R_err, geo, T_err, eucl
 
 

@@ -229,6 +229,7 @@ class HRegNet(nn.Module):
         out = engine.hregnet_forward(P, src_points.float().contiguous(),
                                      dst_points.float().contiguous(),
                                      self.feature_extraction.use_weights)
+        engine.check_device_status()  # syncs only when a multi-workgroup FPS ran (N > 16384)
         out.pop("_fps_idx", None)
         for part in ("src_feats", "dst_feats"):
             out[part] = {k: v.contiguous() for k, v in out[part].items()}
@@ -265,6 +266,7 @@ class Model_V2(nn.Module):
         out = engine.model_v2_forward(P, src_points.float().contiguous(),
                                       dst_points.float().contiguous(),
                                       self.feature_extraction.use_weights)
+        engine.check_device_status()  # syncs only when a multi-workgroup FPS ran (N > 16384)
         out.pop("_fps_idx", None)
         for key in ("src_feats_desc_2", "src_dst_feats_2", "src_dst_feats_2_prime"):
             out[key] = out[key].contiguous()

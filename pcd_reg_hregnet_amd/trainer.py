@@ -19,6 +19,8 @@ forward, l_trans = mean over the 3 levels of ``transformation_loss`` (alpha), ba
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.distributed as dist
 
@@ -74,7 +76,15 @@ class Level1Prefetch:
     """Level-1 FPS + kNN grouping of a batch (input-only, weight-independent: the same
     selections whenever they are computed) for src and dst in one launch set, on a side
     stream.  The trainer starts it for batch i+1 before running step i, so the level-1
-    FPS (one workgroup per cloud, ~1.8 ms at N = 16384) runs beside step i's kernels."""
+    FPS (one workgroup per cloud, ~1.8 ms at N = 16384) runs beside step i's kernels.
+
+    A prefetch belongs to the exact tensor objects it was started on, at their version
+    counters of that moment: ``take`` matches on weak references to src / dst (a freed
+    tensor whose address the caching allocator hands out again is a different object)
+    and on ``Tensor._version`` (a static buffer refilled in place with ``copy_`` bumps
+    it), so a step never runs on selections computed from other contents.  Writes that
+    bypass autograd's version counter (a raw-pointer kernel filling the buffer) are not
+    seen: pass a fresh tensor, or call ``discard()``, after such a write."""
 
     def __init__(self, device):
         self.stream = torch.cuda.Stream(device=device)
@@ -103,15 +113,33 @@ class Level1Prefetch:
             for t in (loc, g):
                 if t is not None:
                     t.record_stream(main)  # consumed on the main stream
-        self.key = (src.data_ptr(), dst.data_ptr(), tuple(src.shape))
+        self.key = self._key(src, dst)
         self.prepared = prepared
 
+    @staticmethod
+    def _key(src, dst):
+        return (weakref.ref(src), weakref.ref(dst), src._version, dst._version,
+                src.data_ptr(), dst.data_ptr(), tuple(src.shape))
+
+    def matches(self, src, dst) -> bool:
+        if self.key is None:
+            return False
+        rs, rd, vs, vd, ps, pd, shape = self.key
+        return (rs() is src and rd() is dst and src._version == vs and dst._version == vd
+                and (src.data_ptr(), dst.data_ptr(), tuple(src.shape)) == (ps, pd, shape))
+
+    def discard(self):
+        self.key, self.prepared = None, None
+
     def take(self, src, dst):
-        """The prefetched selections if they belong to (src, dst), else None."""
-        if self.key != (src.data_ptr(), dst.data_ptr(), tuple(src.shape)):
+        """The prefetched selections if they belong to (src, dst) as they were when the
+        prefetch started, else None (and the stale prefetch is dropped)."""
+        if not self.matches(src, dst):
+            self.discard()
             return None
         torch.cuda.current_stream().wait_event(self.event)
-        prepared, self.key, self.prepared = self.prepared, None, None
+        prepared = self.prepared
+        self.discard()
         return prepared
 
 

@@ -362,3 +362,78 @@ def test_transformation_loss_deterministic_and_checked():
         transformation_loss(pR.cpu(), pt, gR, gt)
     with pytest.raises(ValueError):
         transformation_loss(pR[:, :2], pt, gR, gt)
+
+
+def test_transformation_loss_differentiable_like_reference():
+    """transformation_loss is differentiable in pred_R / pred_t, as the
+    reference (losses.py:117-134): loss, loss_R and loss_t gradients against the
+    reference formula in float64 torch autograd; values equal the forward-only call."""
+    from pcd_reg_hregnet_amd import transformation_loss
+    rng = np.random.default_rng(4)
+    B, alpha = 6, 0.7
+    R0 = torch.from_numpy(rng.normal(size=(B, 3, 3)).astype(np.float32))
+    gR = torch.from_numpy(rng.normal(size=(B, 3, 3)).astype(np.float32)).cuda()
+    t0 = torch.from_numpy(rng.normal(size=(B, 3)).astype(np.float32))
+    gt = torch.from_numpy(rng.normal(size=(B, 3)).astype(np.float32)).cuda()
+    plain = transformation_loss(R0.cuda(), t0.cuda(), gR, gt, alpha)
+    for which in range(3):
+        R = R0.cuda().requires_grad_(True)
+        t = t0.cuda().requires_grad_(True)
+        res = transformation_loss(R, t, gR, gt, alpha)
+        torch.testing.assert_close(res[which].detach(), plain[which], rtol=1e-6, atol=1e-7)
+        res[which].backward()
+        R64 = R0.double().requires_grad_(True)
+        t64 = t0.double().requires_grad_(True)
+        eye = torch.eye(3, dtype=torch.float64).expand(B, 3, 3)
+        lR = torch.norm(R64.transpose(2, 1) @ gR.cpu().double() - eye, dim=(1, 2)).mean()
+        lt = torch.norm(t64 - gt.cpu().double(), dim=1).mean()
+        (alpha * lR + lt, lR, lt)[which].backward()
+        for ours, ref, x in ((R.grad, R64.grad, R64), (t.grad, t64.grad, t64)):
+            got = torch.zeros_like(x) if ours is None else ours.cpu().double()
+            want = torch.zeros_like(x) if ref is None else ref
+            torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+
+
+def test_fps_cluster_timeout_flags_and_leaves_valid_indices():
+    """when the multi-workgroup FPS exchange times out (here forced: one
+    participant never publishes, 2000 polls), the device status word reports it, the
+    engine raises at its next check, and every idx entry is a valid index (0 fill)."""
+    from pcd_reg_hregnet_amd import _lib as L, engine
+    assert L.device_status(clear=True) == 0
+    rng = np.random.default_rng(5)
+    B, n, m = 2, 4096, 64
+    x = dev(rng.uniform(-40, 40, (B, n, 3)).astype(np.float32))
+    idx = torch.full((B, m), -7, dtype=torch.int32, device="cuda")
+    smp = torch.empty((B, m, 3), device="cuda")
+    temp = torch.empty((B, n), device="cuda")
+    # no stall: the forced cluster kernel agrees with the oracle and raises nothing
+    L.call("hreg_debug_fps_cluster", B, n, m, x, temp, idx, smp, -1, 1 << 22, L.stream_handle())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idx.cpu().numpy(), oracle.fps(x.cpu().numpy(), m, None))
+    assert L.device_status(clear=True) == 0
+    idx.fill_(-7)
+    L.call("hreg_debug_fps_cluster", B, n, m, x, temp, idx, smp, 3, 2000, L.stream_handle())
+    torch.cuda.synchronize()
+    got = idx.cpu().numpy()
+    assert ((got >= 0) & (got < n)).all()
+    assert (got[:, 1:] == 0).all()  # the exchange never completes: every later entry is 0
+    np.testing.assert_array_equal(smp.cpu().numpy()[:, 1:], np.repeat(x.cpu().numpy()[:, :1], m - 1, 1))
+    engine._status_pending = True
+    with pytest.raises(RuntimeError, match="timed out"):
+        engine.check_device_status()
+    assert L.device_status(clear=True) == 0  # the check cleared it
+
+
+def test_engine_fps_weighted_mid_size():
+    """weighted FPS for 8192 < n <= 16384 (no single-workgroup register case)
+    through engine.fps / grouping(weights=...) matches the oracle."""
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(9)
+    B, m = 2, 256
+    for n in (12000, 16384):
+        xyz = rng.uniform(-40, 40, (B, n, 3)).astype(np.float32)
+        w = rng.uniform(0.1, 2.0, (B, n)).astype(np.float32)
+        idx, _ = engine.fps(dev(xyz), m, weights=dev(w))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(idx.cpu().numpy(), oracle.fps(xyz, m, w))
+    engine.check_device_status()

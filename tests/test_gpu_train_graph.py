@@ -625,6 +625,35 @@ def test_sim_feats_full_size_vs_float64(tg):
         assert e_ours <= max(4 * e_32, 1e-6 * scale)
 
 
+def test_trainer_prefetch_static_buffers_refilled():
+    """inputs refilled in place between steps (a static-buffer loader) must
+    not reuse the prefetch made from the previous contents: steps with next_batch =
+    the same (refilled) buffers equal steps without any prefetch."""
+    from pcd_reg_hregnet_amd import synthetic, trainer
+    data = []
+    for seed in (11, 23, 37):
+        s, d, Rg, tg_ = synthetic.lidar_batch(2, 2048, seed0=seed)
+        data.append(tuple(torch.from_numpy(x).to(DEV) for x in (s, d, Rg, tg_)))
+
+    def run(prefetch):
+        net = _train_net()
+        tr = trainer.Trainer(net, lr=1e-4)
+        src, dst = torch.empty_like(data[0][0]), torch.empty_like(data[0][1])
+        losses = []
+        for s, d, Rg, tg_ in data:
+            src.copy_(s)
+            dst.copy_(d)
+            nxt = (src, dst) if prefetch else None  # prefetched from the current contents
+            losses.append(float(tr.step(src, dst, Rg, tg_, next_batch=nxt)[0]))
+        torch.cuda.synchronize()
+        return losses, tr.params.flat.clone()
+
+    l1, p1 = run(True)
+    l2, p2 = run(False)
+    assert l1 == l2
+    assert torch.equal(p1, p2)
+
+
 def test_trainer_step_prefetch_bitwise():
     """trainer.Trainer (flat parameters, one-launch Adam, level-1 grouping of the next
     batch prefetched on a side stream): two steps with the prefetch are bitwise equal to

@@ -239,3 +239,29 @@ def test_nbr_head_table_size_matches_kernel(P):
     from pcd_reg_hregnet_amd import _lib
     L = _lib.load(require_gpu=False)
     assert prep.nbr_table.numel() == L.hreg_nbr_head_table_floats()
+
+
+def test_level1_prefetch_key_identity_and_version():
+    """a level-1 prefetch must not be reused when the same buffers hold new
+    data (copy_ into a static input) or when a new tensor reuses a freed address."""
+    from pcd_reg_hregnet_amd.trainer import Level1Prefetch
+    pf = Level1Prefetch.__new__(Level1Prefetch)
+    pf.key = pf.prepared = None
+    s, d = torch.zeros(2, 8, 3), torch.zeros(2, 8, 3)
+    pf.key = Level1Prefetch._key(s, d)
+    assert pf.matches(s, d)
+    assert not pf.matches(d, s)
+    assert not pf.matches(s.clone(), d)          # another object, same contents
+    assert not pf.matches(s.view(2, 8, 3), d)    # an alias is another object too
+    s.copy_(torch.ones_like(s))                  # static buffer refilled in place
+    assert not pf.matches(s, d)
+    pf.key = Level1Prefetch._key(s, d)
+    d[0, 0, 0] = 5.0
+    assert not pf.matches(s, d)
+    # a dead tensor never matches, whatever lives at its address now
+    a, b = torch.zeros(4, 8, 3), torch.zeros(4, 8, 3)
+    pf.key = Level1Prefetch._key(a, b)
+    del a
+    assert pf.key[0]() is None
+    pf.discard()
+    assert pf.key is None and not pf.matches(s, d)
