@@ -129,6 +129,8 @@ MFMA_ENTRIES = {
     "hreg_group_l3": ("fused", _level_work(3)),
     "hreg_group_split_l2": ("fused", _level_work(2)),
     "hreg_group_split_l3": ("fused", _level_work(3)),
+    "hreg_group6_l2": ("fused", _level_work(2)),
+    "hreg_group6_l3": ("fused", _level_work(3)),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
     "hreg_mlp_head": ("mlp", _mlp_work),
@@ -147,9 +149,10 @@ class MfmaTimer:
         self.flops = dict.fromkeys(self.KINDS, 0.0)
         self.xflops = dict.fromkeys(self.KINDS, 0.0)
         self.bytes = dict.fromkeys(self.KINDS, 0.0)
+        self.by_entry = {}  # C-ABI entry -> [(e0, e1)], algorithmic FLOPs
         self.enabled = False
 
-    def _timed(self, kind, fn, flops, nbytes, xflops=None):
+    def _timed(self, kind, fn, flops, nbytes, xflops=None, entry=None):
         if not self.enabled:
             return fn()
         st = torch.cuda.current_stream()
@@ -159,6 +162,10 @@ class MfmaTimer:
         r = fn()
         e1.record(st)
         self.events[kind].append((e0, e1))
+        if entry is not None:
+            ev, fl = self.by_entry.get(entry, ([], 0.0))
+            ev.append((e0, e1))
+            self.by_entry[entry] = (ev, fl + flops)
         self.flops[kind] += flops
         self.xflops[kind] += flops if xflops is None else xflops
         self.bytes[kind] += nbytes
@@ -180,7 +187,7 @@ class MfmaTimer:
             if name in MFMA_ENTRIES:
                 kind, work = MFMA_ENTRIES[name]
                 fl, nb, xf = work(args)
-                return self._timed(kind, lambda: orig_call(name, *args), fl, nb, xf)
+                return self._timed(kind, lambda: orig_call(name, *args), fl, nb, xf, entry=name)
             return orig_call(name, *args)
         _lib.gemm = gemm
         engine.call = call
@@ -190,6 +197,17 @@ class MfmaTimer:
         ev = self.events[kind]
         ms = sum(a.elapsed_time(b) for a, b in ev)
         return ms, len(ev), self.flops[kind], self.bytes[kind], self.xflops[kind]
+
+    def entries(self, steps):
+        """per C-ABI entry: launches per step, mean launch duration, algorithmic TFLOP/s"""
+        torch.cuda.synchronize()
+        out = {}
+        for name, (ev, fl) in sorted(self.by_entry.items()):
+            ms = sum(a.elapsed_time(b) for a, b in ev)
+            out[name] = {"launches_per_step": len(ev) // max(steps, 1),
+                         "avg_launch_us": round(ms / max(len(ev), 1) * 1e3, 2),
+                         "tflops": round(fl / max(ms, 1e-9) / 1e9, 2)}
+        return out
 
 
 def pmc_traffic(kernel: str):
@@ -528,6 +546,7 @@ def main():
                                        "group_l1_kernel": kind_summary("l1"),
                                        "fine_head_kernel + nbr_head_kernel": kind_summary("head"),
                                        "mlp_head_kernel": kind_summary("mlp")},
+                "per_entry": timer.entries(args.steps),
                 "all_mfma": {"ms_per_step": round(tot_ms / args.steps, 3),
                              "gflop_per_pair": ALG_GFLOP_PER_PAIR,
                              "tflops": round(alg_fl / max(tot_ms, 1e-9) / 1e9, 2),

@@ -465,6 +465,19 @@ int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                   float *desc, const float *pre, void *stream);
 
+/* The level-2 / level-3 stages above with fp32-accurate products on the bf16 matrix
+ * cores (bf16x6 split, group_fused6.hip): same arguments and outputs, table =
+ * hreg_group6_l{2,3}_table_floats() floats (engine.l2_table6: bf16 piece fragments of
+ * the same blocks, then the f32 epilogues), 16-byte aligned. */
+int hreg_group6_l2_table_floats(void);
+int hreg_group6_l2(const float *table, const float *geom, const float *knn_xyz,
+                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
+                   float *desc, const float *pre, void *stream);
+int hreg_group6_l3_table_floats(void);
+int hreg_group6_l3(const float *table, const float *geom, const float *knn_xyz,
+                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
+                   float *desc, const float *pre, void *stream);
+
 /* The level-2 / level-3 stages above on the channel-split kernel (group_split.hip):
  * same arguments and outputs, table = hreg_group_split_l{2,3}_table_floats() floats
  * (engine.split_table: the same blocks, fragments grouped 4 k-steps per lane); geom

@@ -78,6 +78,8 @@ _SIGS = {
     "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group6_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group6_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head_table_floats": [_i],
@@ -140,7 +142,8 @@ EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_
                           "hreg_sim_feats_bwd_ws_bytes", "hreg_group_l1_table_floats",
                           "hreg_group_l2_table_floats", "hreg_group_l3_table_floats",
                           "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
-                          "hreg_group_split_l3_table_floats")
+                          "hreg_group_split_l3_table_floats", "hreg_group6_l2_table_floats",
+                          "hreg_group6_l3_table_floats")
 
 _lib = None
 
@@ -172,7 +175,8 @@ def load(require_gpu: bool = True):
         L.hreg_sim_feats_bwd_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
                      "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
-                     "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats"):
+                     "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats",
+                     "hreg_group6_l2_table_floats", "hreg_group6_l3_table_floats"):
             getattr(L, name).restype = ctypes.c_int
             getattr(L, name).argtypes = []
         _lib = L

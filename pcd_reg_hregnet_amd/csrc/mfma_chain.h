@@ -175,4 +175,134 @@ __device__ __forceinline__ void store_tile(float *out, int co, const f32x16 &v, 
     }
 }
 
+// ------------------------------------------------------------------------
+// fp32-accurate products on the bf16 matrix cores ("bf16x6").  Every fp32 value is
+// split exactly into three bf16 pieces, x = hi + mid + lo (truncation split: hi =
+// the top 8 significant bits, mid the next 8 of x - hi, lo the remaining <= 8 bits;
+// exact for normal fp32), and a product a*b is accumulated as the six piece
+// products down to 2^-16 relative (a_h b_h, a_h b_m, a_m b_h, a_h b_l, a_m b_m,
+// a_l b_h; the dropped ones are <= 2^-24 relative), smallest first, in fp32 on
+// v_mfma_f32_32x32x16_bf16.  Measured (profiles/r2_split_mfma_micro.txt): the same
+// error vs fp64 as the f32-input MFMA (max 1.3e-7..1.8e-7 of sum|a b| at K = 32..512)
+// at 2.0-2.2x its throughput in an accumulator-chained layer stack (6 x 32 cycles
+// per 16-deep k-chunk instead of 8 x 64).
+//
+// Operand layout: v_mfma_f32_32x32x16_bf16 lane l holds A[l % 32][8 (l / 32) + i]
+// and B[8 (l / 32) + i][l % 32], i = 0..7, and its accumulator is laid out as the
+// f32 32x32x2 one.  A 16-deep chunk c therefore holds exactly the f32 k-steps
+// 8c .. 8c + 7 of each lane: bval(st) of the f32 pipes is reused unchanged, and
+// the weight pieces of chunk c are the lane's f32 fragments 8c .. 8c + 7
+// (engine.frag6), 3 x 16 bytes per lane.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+
+// 8 fp32 values (one lane's chunk of B) -> hi / mid / lo packed bf16x8
+__device__ __forceinline__ void split8(const float (&x)[8], u32x4 (&o)[3]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t hb[2], mb[2], lb[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float v = x[2 * i + j];
+            const uint32_t xb = __float_as_uint(v);
+            const float r = fsub_rn(v, __uint_as_float(xb & 0xffff0000u));
+            const uint32_t rb = __float_as_uint(r);
+            hb[j] = xb;
+            mb[j] = rb;
+            lb[j] = __float_as_uint(fsub_rn(r, __uint_as_float(rb & 0xffff0000u)));
+        }
+        o[0][i] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+        o[1][i] = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
+        o[2][i] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+    }
+}
+
+__device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// c += A x B for one 16-deep chunk as the six piece products, smallest first
+__device__ __forceinline__ f32x16 mma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+    c = mfma16(a[0], b[2], c);
+    c = mfma16(a[1], b[1], c);
+    c = mfma16(a[2], b[0], c);
+    c = mfma16(a[0], b[1], c);
+    c = mfma16(a[1], b[0], c);
+    return mfma16(a[0], b[0], c);
+}
+
+constexpr int CARRY6 = 8;  // output tiles of a call's first chunk carried between calls
+
+// weight pieces of chunk fragment f (units of 3 x 64 lanes x 16 B)
+__device__ __forceinline__ void ld6(const gu32x4 *__restrict__ wt, int f, int lane, u32x4 (&o)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) o[p] = wt[(unsigned)(f * 3 + p) * 64u + (unsigned)lane];
+}
+
+// acc[co] += sum_{c < NCH} A(co, c) x B(c) with B(c) = split(bval(8c .. 8c+7)); chunk
+// fragment (co, c) = f.base + co * f.stride + c.  cin: this call's first chunk (all
+// COUT_T tiles), loaded by the previous call; cout: the first chunk of the next call
+// nf (NCOUT tiles).  Weight pieces stream one chunk ahead of their MFMAs.
+// ROLL (default for >= 4 output tiles): one buffer; tile co's next chunk is loaded right
+// after its 6 MFMAs issue (COUT_T - 1 tiles = 18+ MFMAs of lead), 12 VGPRs per tile
+// instead of 24 for the double buffer.
+template <int NCH, int COUT_T, int NCOUT, class BVal, bool ROLL = (COUT_T >= 4)>
+__device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int lane, FragSeq f, BVal bval,
+                                           f32x16 (&acc)[COUT_T], const u32x4 (&cin)[CARRY6][3],
+                                           FragSeq nf, u32x4 (&cout)[CARRY6][3]) {
+    static_assert(COUT_T <= CARRY6 && NCOUT <= CARRY6, "carry");
+    if constexpr (ROLL) {
+        u32x4 rb[COUT_T][3];
+#pragma unroll
+        for (int co = 0; co < COUT_T; ++co)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) rb[co][p] = cin[co][p];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            float x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = bval(8 * c + i);
+            u32x4 b[3];
+            split8(x, b);
+#pragma unroll
+            for (int co = 0; co < COUT_T; ++co) {
+                acc[co] = mma6(rb[co], b, acc[co]);
+                if (c + 1 < NCH)
+                    ld6(wt, f.base + co * f.stride + c + 1, lane, rb[co]);
+                else if (co < NCOUT)
+                    ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int co = COUT_T; co < NCOUT; ++co) ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
+        return;
+    }
+    u32x4 buf[2][COUT_T][3];
+#pragma unroll
+    for (int co = 0; co < COUT_T; ++co)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) buf[0][co][p] = cin[co][p];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) {
+#pragma unroll
+            for (int co = 0; co < COUT_T; ++co) ld6(wt, f.base + co * f.stride + c + 1, lane, buf[(c + 1) & 1][co]);
+        } else {
+#pragma unroll
+            for (int co = 0; co < NCOUT; ++co) ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
+        }
+        float x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = bval(8 * c + i);
+        u32x4 b[3];
+        split8(x, b);
+#pragma unroll
+        for (int co = 0; co < COUT_T; ++co) acc[co] = mma6(buf[c & 1][co], b, acc[co]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 }  // namespace hreg_chain

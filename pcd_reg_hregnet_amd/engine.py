@@ -42,6 +42,9 @@ FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
 # accumulator-chained one (group_fused.hip); measured per level (tools/group_bench.py)
 SPLIT_L2 = False
 SPLIT_L3 = True
+# the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
+# (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
+B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
 FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
 FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip)
@@ -172,6 +175,8 @@ class PreparedWeights:
         self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
         self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
+        self.l2_table6 = l2_table6(self.det[1], self.desc[1], self.desc_mlp[1])
+        self.l3_table6 = l2_table6(self.det[2], self.desc[2], self.desc_mlp[2])
         self.l2s_table = split_table(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l3s_table = split_table(self.det[2], self.desc[2], self.desc_mlp[2])
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
@@ -183,7 +188,8 @@ class PreparedWeights:
             self.head_table[name] = mlp_head_table(self.fine[name][1])
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
                      "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre",
-                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2s_table",
+                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2_table6",
+                     "l3_table6", "l2s_table",
                      "l3s_table", "fine_table",
                      "nbr_table", "head_table", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
@@ -305,6 +311,55 @@ def l2_table(det, desc, mlp) -> torch.Tensor:
                   _grouped(frag_layer(stack[2].W), T3, T1 * 16)]
     parts += [_grouped(frag_layer(mlp[0].W), TM1, 3 * T3 * 16),
               _grouped(frag_layer(mlp[1].W), TM2, TM1 * 16)]
+    for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def _bf16_pieces(x: torch.Tensor) -> torch.Tensor:
+    """Exact truncation split of fp32 x into hi + mid + lo bf16 values (mfma_chain.h
+    split8): -> int16 bit patterns [3, *x.shape]."""
+    x = x.float().contiguous()
+    mask = torch.tensor(-65536, dtype=torch.int32)  # 0xffff0000
+    xb = x.view(torch.int32)
+    r = x - (xb & mask).view(torch.float32)
+    rb = r.view(torch.int32)
+    lo = r - (rb & mask).view(torch.float32)
+    out = []
+    for v in (xb, rb, lo.view(torch.int32)):
+        u = (v >> 16) & 0xFFFF
+        out.append(torch.where(u >= 32768, u - 65536, u).to(torch.int16))
+    return torch.stack(out)
+
+
+def frag6(frag: torch.Tensor, cout_tiles: int, nstep: int) -> torch.Tensor:
+    """f32 A-fragments [co][k-step][lane] (nstep k-steps, zero-padded to a multiple of 8)
+    -> the bf16x6 table block [co][chunk][piece][lane][8] (as float32 words): chunk c of
+    a lane holds its f32 fragments of k-steps 8c .. 8c+7 (mfma_chain.h, bf16x6)."""
+    f = frag.reshape(cout_tiles, nstep, 64).float()
+    pad = (-nstep) % 8
+    if pad:
+        f = torch.cat([f, torch.zeros(cout_tiles, pad, 64)], 1)
+    nch = f.shape[1] // 8
+    f = f.reshape(cout_tiles, nch, 8, 64).transpose(2, 3)      # [co][chunk][lane][8]
+    p = _bf16_pieces(f).permute(1, 2, 0, 3, 4).contiguous()   # [co][chunk][piece][lane][8]
+    return p.view(torch.float32).reshape(-1)
+
+
+def l2_table6(det, desc, mlp) -> torch.Tensor:
+    """Table of group_fused6.hip (Cfg6): bf16x6 chunk fragments of every layer in
+    l2_table's block order (the 2-step geometry block zero-padded to one chunk), then the
+    f32 epilogues."""
+    T1, T3 = det[0].W.shape[0] // 32, det[2].W.shape[0] // 32
+    TM1, TM2 = mlp[0].W.shape[0] // 32, mlp[1].W.shape[0] // 32
+    TF = (det[0].W.shape[1] - 4) // 2
+    parts = []
+    for stack in (det, desc):
+        g, f = frag_input(stack[0].W)
+        parts += [frag6(g, T1, 2), frag6(f, T1, TF), frag6(frag_layer(stack[1].W), T1, T1 * 16),
+                  frag6(frag_layer(stack[2].W), T3, T1 * 16)]
+    parts += [frag6(frag_layer(mlp[0].W), TM1, 3 * T3 * 16),
+              frag6(frag_layer(mlp[1].W), TM2, TM1 * 16)]
     for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
@@ -654,7 +709,9 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         kp = _empty(G, 3, device=dev)
         att_feat = _empty(G, LEVELS[lvl][3][-1], device=dev)
         desc = _empty(G, LEVELS[lvl][5], device=dev)
-        if (SPLIT_L2, SPLIT_L3)[lvl - 1]:
+        if lvl == 1 and B6_L2 and not SPLIT_L2:
+            name, table = "hreg_group6_l2", P.l2_table6
+        elif (SPLIT_L2, SPLIT_L3)[lvl - 1]:
             name, table = (("hreg_group_split_l2", P.l2s_table) if lvl == 1 else
                            ("hreg_group_split_l3", P.l3s_table))
         else:
