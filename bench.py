@@ -105,6 +105,15 @@ def _fine_work(args):
             2.0 * 8 * G * (kx * N1 + 2 * N1 * N1))
 
 
+def _fine6_work(args):
+    """hreg_fine_head6 (table, C, small, gidx, knn_xyz, G, ...): precomputed blocks always"""
+    C, G = args[1], args[5]
+    N1 = 2 * C
+    return (2.0 * 8 * G * ((2 * C + 12) * N1 + 2 * N1 * N1),
+            4.0 * G * (8 * (16 + C + 1 + 3) + C + 3 + N1),
+            2.0 * 8 * G * (12 * N1 + 2 * N1 * N1))
+
+
 def _nbr_work(args):
     G = args[4]
     kx = 4 if args[6] is not None else 260  # HEAD_PRE: geometry columns only
@@ -133,6 +142,8 @@ MFMA_ENTRIES = {
     "hreg_group6_l3": ("fused", _level_work(3)),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
+    "hreg_fine_head6": ("head", _fine6_work),
+    "hreg_nbr_head6": ("head", _nbr_work),
     "hreg_mlp_head": ("mlp", _mlp_work),
 }
 

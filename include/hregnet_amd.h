@@ -516,6 +516,18 @@ int hreg_nbr_head_table_floats(void);
 int hreg_nbr_head(const float *table, const float *desc, const int32_t *gidx, const float *geom,
                   int G, float *out, const float *pre, void *stream);
 
+/* The two heads above with fp32-accurate products on the bf16 matrix cores (bf16x6,
+ * group_head.hip), precomputed-block form only (pre_src / pre_dst / pre required):
+ * same outputs.  table = hreg_head6_table_floats(N1) floats, N1 = 2C for FineReg and
+ * 256 for the neighbour branch (engine.head_table6: bf16 piece fragments of the narrow
+ * first block, conv 2 and conv 3, then the f32 epilogues), 16-byte aligned. */
+int hreg_head6_table_floats(int N1);
+int hreg_fine_head6(const float *table, int C, const float *small, const int32_t *gidx,
+                    const float *knn_xyz, int G, float *corres, float *att, const float *pre_src,
+                    const float *pre_dst, void *stream);
+int hreg_nbr_head6(const float *table, const float *desc, const int32_t *gidx, const float *geom,
+                   int G, float *out, const float *pre, void *stream);
+
 /* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */
 int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,

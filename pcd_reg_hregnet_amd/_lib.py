@@ -84,6 +84,9 @@ _SIGS = {
     "hreg_fine_head": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head_table_floats": [_i],
     "hreg_nbr_head": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
+    "hreg_fine_head6": [_vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_nbr_head6": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
+    "hreg_head6_table_floats": [_i],
     "hreg_mlp_head": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "hreg_mlp_head_table_floats": [_i],
     "hreg_sigma_weights": [_vp, _i, _i, _vp, _vp],

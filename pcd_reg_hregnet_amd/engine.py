@@ -45,6 +45,9 @@ SPLIT_L3 = True
 # the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
 # (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
 B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
+# the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
+# precomputed-block form, HEAD_PRE)
+B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
 FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
 FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip)
@@ -182,6 +185,9 @@ class PreparedWeights:
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
                            for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
         self.nbr_table = nbr_head_table(self.coarse_convs2, 256)
+        self.fine_table6 = {name: fine_head_table6(self.fine[name][0])
+                            for name in ("fine_corres_2", "fine_corres_1")}
+        self.nbr_table6 = nbr_head_table6(self.coarse_convs2, 256)
         self.head_table = {("det", lvl): mlp_head_table(self.det_head[lvl]) for lvl in range(3)}
         self.head_table["coarse"] = mlp_head_table(self.coarse_head)
         for name in ("fine_corres_2", "fine_corres_1"):
@@ -190,7 +196,7 @@ class PreparedWeights:
                      "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre",
                      "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2_table6",
                      "l3_table6", "l2s_table",
-                     "l3s_table", "fine_table",
+                     "l3s_table", "fine_table", "fine_table6", "nbr_table6",
                      "nbr_table", "head_table", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
@@ -287,6 +293,33 @@ def nbr_head_table(convs, C: int) -> torch.Tensor:
     for lin in convs:
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def _head_table6(first, T1: int, nfirst: int, convs) -> torch.Tensor:
+    """Table of group_head.hip's bf16x6 head kernels (Head6Cfg): the narrow first block
+    (nfirst f32 k-steps, zero-padded to one chunk), conv 2, conv 3 as bf16 piece chunk
+    fragments (frag6), then the three f32 epilogues."""
+    parts = [frag6(first, T1, nfirst), frag6(frag_layer(convs[1].W), T1, T1 * 16),
+             frag6(frag_layer(convs[2].W), T1, T1 * 16)]
+    for lin in convs:
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def fine_head_table6(convs) -> torch.Tensor:
+    """FineReg convs_1 for fine_head6_kernel: the 16 small columns [small 12, pad 4] of
+    convs_1[0] (its descriptor blocks are precomputed per point, HEAD_PRE)."""
+    W1 = convs[0].W
+    N1 = W1.shape[0]
+    W1p = torch.cat([W1[:, :12], torch.zeros(N1, 4, dtype=W1.dtype)], 1)
+    return _head_table6(frag_segment(W1p, 0, 16), N1 // 32, 8, convs)
+
+
+def nbr_head_table6(convs, C: int) -> torch.Tensor:
+    """CoarseReg convs_2 for nbr_head6_kernel: the 4 geometry columns of convs_2[0] (its
+    descriptor block is precomputed per point, HEAD_PRE)."""
+    W1 = convs[0].W
+    return _head_table6(frag_segment(W1, C, 4), W1.shape[0] // 32, 2, convs)
 
 
 def mlp_head_table(head) -> torch.Tensor:
@@ -822,7 +855,10 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     if FUSED_NBR and C == 256:
         nbr = _empty(G2, C, device=dev)
         pre = gemm([_seg(desc3, 0, C)], P.nbr_pre, G2) if HEAD_PRE else None
-        call("hreg_nbr_head", P.nbr_table, desc3, gself, geom_self, G2, nbr, pre, _stream())
+        if B6_HEADS and HEAD_PRE:
+            call("hreg_nbr_head6", P.nbr_table6, desc3, gself, geom_self, G2, nbr, pre, _stream())
+        else:
+            call("hreg_nbr_head", P.nbr_table, desc3, gself, geom_self, G2, nbr, pre, _stream())
     else:
         segs = [_seg(desc3, 0, C, gather=gself), _seg(geom_self, C, 4)]
         h = gemm(segs, P.coarse_convs2[0], R2)
@@ -884,8 +920,12 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
         if HEAD_PRE:
             pre = _empty(2, B * N, N1, device=dev)
             _gemm_batched_desc(P.fine_pre[name], src_desc, B * N, C, pre, x1=dst_desc)
-        call("hreg_fine_head", P.fine_table[name], C, small, src_desc, dst_desc, gidx, kx, B * N,
-             corres, att, pre[0], pre[1], _stream())
+        if B6_HEADS and HEAD_PRE:
+            call("hreg_fine_head6", P.fine_table6[name], C, small, gidx, kx, B * N, corres, att,
+                 pre[0], pre[1], _stream())
+        else:
+            call("hreg_fine_head", P.fine_table[name], C, small, src_desc, dst_desc, gidx, kx,
+                 B * N, corres, att, pre[0], pre[1], _stream())
         w = _mlp_weights(P, name, att, B, N)
         if return_att:
             return corres.view(B, N, 3), w.view(B, N), att

@@ -219,13 +219,15 @@ def test_fused_level_matches_layerwise(net, lvl, split, pre, monkeypatch):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("pre", [True, False])
+@pytest.mark.parametrize("pre,b6", [(True, True), (True, False), (False, False)])
 @pytest.mark.parametrize("name,C,N", [("fine_corres_1", 64, 1024), ("fine_corres_2", 128, 512)])
-def test_fused_fine_head_matches_layerwise(net, name, C, N, pre, monkeypatch):
+def test_fused_fine_head_matches_layerwise(net, name, C, N, pre, b6, monkeypatch):
     """group_head.hip (convs_1 + attention in one kernel; pre: descriptor blocks of
-    convs_1[0] precomputed per point, engine.HEAD_PRE) against the GEMM + attend path."""
+    convs_1[0] precomputed per point, engine.HEAD_PRE; b6: the bf16x6 kernel, products on
+    the bf16 matrix cores at fp32 accuracy) against the GEMM + attend path."""
     from pcd_reg_hregnet_amd import engine
     monkeypatch.setattr(engine, "HEAD_PRE", pre)
+    monkeypatch.setattr(engine, "B6_HEADS", b6)
     P = net.prepared(torch.device("cuda"))
     g = torch.Generator().manual_seed(3)
     B = 2
@@ -301,12 +303,13 @@ def test_gemm_addends_vs_torch():
     assert np.all(np.abs(out - ref) <= 1e-5 * scale + 1e-6)
 
 
-@pytest.mark.parametrize("pre", [True, False])
-def test_fused_nbr_head_matches_layerwise(net, pre, monkeypatch):
+@pytest.mark.parametrize("pre,b6", [(True, True), (True, False), (False, False)])
+def test_fused_nbr_head_matches_layerwise(net, pre, b6, monkeypatch):
     """CoarseReg neighbour branch in one kernel (group_head.hip; pre: descriptor block of
-    convs_2[0] precomputed per point) vs GEMMs + attend."""
+    convs_2[0] precomputed per point; b6: bf16x6 products) vs GEMMs + attend."""
     from pcd_reg_hregnet_amd import engine
     monkeypatch.setattr(engine, "HEAD_PRE", pre)
+    monkeypatch.setattr(engine, "B6_HEADS", b6)
     P = net.prepared(torch.device("cuda"))
     g = torch.Generator().manual_seed(5)
     B, N1, C = 2, 256, 256

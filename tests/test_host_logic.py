@@ -241,6 +241,21 @@ def test_nbr_head_table_size_matches_kernel(P):
     assert prep.nbr_table.numel() == L.hreg_nbr_head_table_floats()
 
 
+def test_head6_tables_match_kernel(P):
+    """bf16x6 head tables (engine.fine_head_table6 / nbr_head_table6): sizes match the
+    kernels' Head6Cfg, and the three bf16 pieces of every weight sum back to it exactly."""
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib, engine
+    L = _lib.load(require_gpu=False)
+    assert prep.fine_table6["fine_corres_1"].numel() == L.hreg_head6_table_floats(128)
+    assert prep.fine_table6["fine_corres_2"].numel() == L.hreg_head6_table_floats(256)
+    assert prep.nbr_table6.numel() == L.hreg_head6_table_floats(256)
+    W = prep.coarse_convs2[1].W.cpu()
+    pieces = engine._bf16_pieces(W).to(torch.int32) << 16
+    back = [p.view(torch.float32).double() for p in pieces]
+    assert torch.equal(back[0] + back[1] + back[2], W.double())
+
+
 def test_level1_prefetch_key_identity_and_version():
     """a level-1 prefetch must not be reused when the same buffers hold new
     data (copy_ into a static input) or when a new tensor reuses a freed address."""
