@@ -134,6 +134,7 @@ def _l1_work(a):
 # C-ABI entry -> (timer kind, work of one launch from its arguments)
 MFMA_ENTRIES = {
     "hreg_group_l1": ("l1", _l1_work),
+    "hreg_group_l1_6": ("l1", _l1_work),
     "hreg_group_l2": ("fused", _level_work(2)),
     "hreg_group_l3": ("fused", _level_work(3)),
     "hreg_group_split_l2": ("fused", _level_work(2)),

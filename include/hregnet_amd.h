@@ -465,6 +465,13 @@ int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
                   const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                   float *desc, const float *pre, void *stream);
 
+/* The level-1 stage (hreg_group_l1) with fp32-accurate products on the bf16 matrix cores
+ * (bf16x6 split, group_l1_6.hip): same arguments and outputs, table =
+ * hreg_group_l1_6_table_floats() floats (engine.l1_table6), 16-byte aligned. */
+int hreg_group_l1_6_table_floats(void);
+int hreg_group_l1_6(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
+                    float *att_feat, float *desc, void *stream);
+
 /* The level-2 / level-3 stages above with fp32-accurate products on the bf16 matrix
  * cores (bf16x6 split, group_fused6.hip): same arguments and outputs, table =
  * hreg_group6_l{2,3}_table_floats() floats (engine.l2_table6: bf16 piece fragments of

@@ -75,6 +75,7 @@ _SIGS = {
     "hreg_transformation_loss": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
                                  _vp],
     "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_group_l1_6": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
@@ -146,7 +147,7 @@ EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_
                           "hreg_group_l2_table_floats", "hreg_group_l3_table_floats",
                           "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
                           "hreg_group_split_l3_table_floats", "hreg_group6_l2_table_floats",
-                          "hreg_group6_l3_table_floats")
+                          "hreg_group6_l3_table_floats", "hreg_group_l1_6_table_floats")
 
 _lib = None
 
@@ -179,7 +180,8 @@ def load(require_gpu: bool = True):
         for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
                      "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
                      "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats",
-                     "hreg_group6_l2_table_floats", "hreg_group6_l3_table_floats"):
+                     "hreg_group6_l2_table_floats", "hreg_group6_l3_table_floats",
+                     "hreg_group_l1_6_table_floats"):
             getattr(L, name).restype = ctypes.c_int
             getattr(L, name).argtypes = []
         _lib = L

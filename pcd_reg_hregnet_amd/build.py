@@ -26,6 +26,16 @@ CFLAGS = [
 ]
 
 
+# Kernels running v_mfma_f32_32x32x16_bf16 (the bf16x6 split products) are compiled
+# without packed fp32 VALU ops (v_pk_mul_f32 / v_pk_add_f32): with them, group_l1_6 gave
+# nondeterministic wrong accumulator values whenever two waves shared a SIMD (two
+# workgroups per CU, or one 8-wave workgroup), and exact results with one wave per SIMD
+# or without the packed ops (tools/debug_l1_6.py).  The host-side
+# compile ignores the feature (a warning).
+NO_PACKED_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+FILE_FLAGS = {f: NO_PACKED_F32 for f in ("group_l1_6.hip", "group_fused6.hip", "group_head.hip")}
+
+
 def _needs(obj: str, deps: list[str]) -> bool:
     if not os.path.exists(obj):
         return True
@@ -34,7 +44,7 @@ def _needs(obj: str, deps: list[str]) -> bool:
 
 
 def _compile(src: str, obj: str) -> tuple[str, int, str]:
-    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
     p = subprocess.run(cmd, capture_output=True, text=True)
     return src, p.returncode, p.stdout + p.stderr
 
@@ -43,7 +53,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     os.makedirs(OBJDIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(
-        os.path.join(HERE, "..", "include", "*.h"))
+        os.path.join(HERE, "..", "include", "*.h")) + [os.path.abspath(__file__)]
     jobs = []
     objs = []
     for s in srcs:

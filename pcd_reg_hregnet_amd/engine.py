@@ -45,6 +45,7 @@ SPLIT_L3 = True
 # the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
 # (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
 B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
+B6_L1 = os.environ.get("HREG_B6_L1", "1") != "0"  # group_l1_6.hip for level 1
 # the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
 # precomputed-block form, HEAD_PRE)
 B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
@@ -176,6 +177,7 @@ class PreparedWeights:
         self.mlpx = (_conv_bn(sd, "fine_corres_2.mlpx.0", "fine_corres_2.mlpx.1")
                      if "fine_corres_2.mlpx.0.weight" in sd else None)
         self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
+        self.l1_table6 = l1_table6(self.det[0], self.desc[0], self.desc_mlp[0])
         self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
         self.l2_table6 = l2_table6(self.det[1], self.desc[1], self.desc_mlp[1])
@@ -194,7 +196,7 @@ class PreparedWeights:
             self.head_table[name] = mlp_head_table(self.fine[name][1])
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
                      "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre",
-                     "coarse_head", "fine", "l1_table", "l2_table", "l3_table", "l2_table6",
+                     "coarse_head", "fine", "l1_table", "l1_table6", "l2_table", "l3_table", "l2_table6",
                      "l3_table6", "l2s_table",
                      "l3s_table", "fine_table", "fine_table6", "nbr_table6",
                      "nbr_table", "head_table", "mlpx"):
@@ -428,6 +430,19 @@ def l1_table(det, desc, mlp) -> torch.Tensor:
              _group4(frag_geom(desc[0].W), 2), _group4(frag_layer(desc[1].W), 4),
              _group4(frag_layer(desc[2].W), 4),
              _group4(frag_layer(mlp[0].W), 4), _group4(frag_layer(mlp[1].W), 4)]
+    for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def l1_table6(det, desc, mlp) -> torch.Tensor:
+    """Table of group_l1_6.hip: l1_table's blocks as bf16 piece chunk fragments (frag6;
+    the 2-step geometry blocks zero-padded to one chunk), then the same f32 epilogues."""
+    parts = [frag6(frag_geom(det[0].W), 1, 2), frag6(frag_layer(det[1].W), 1, 16),
+             frag6(frag_layer(det[2].W), 2, 16),
+             frag6(frag_geom(desc[0].W), 1, 2), frag6(frag_layer(desc[1].W), 1, 16),
+             frag6(frag_layer(desc[2].W), 2, 16),
+             frag6(frag_layer(mlp[0].W), 1, 96), frag6(frag_layer(mlp[1].W), 2, 16)]
     for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
@@ -733,7 +748,10 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         kp = _empty(G, 3, device=dev)
         att_feat = _empty(G, LEVELS[0][3][-1], device=dev)
         desc = _empty(G, LEVELS[0][5], device=dev)
-        call("hreg_group_l1", P.l1_table, geom, kx, G, kp, att_feat, desc, _stream())
+        if B6_L1:
+            call("hreg_group_l1_6", P.l1_table6, geom, kx, G, kp, att_feat, desc, _stream())
+        else:
+            call("hreg_group_l1", P.l1_table, geom, kx, G, kp, att_feat, desc, _stream())
         sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)
         return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx

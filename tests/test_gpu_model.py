@@ -180,16 +180,21 @@ def test_graph_lanes_match_eager(net):
                 assert torch.equal(out["src_feats"]["desc_3"], ref["src_feats"]["desc_3"])
 
 
-@pytest.mark.parametrize("lvl,split,pre", [(0, False, False), (1, False, False), (2, False, False),
-                                           (1, True, False), (2, True, False), (1, False, True),
-                                           (2, False, True), (1, True, True), (2, True, True)])
-def test_fused_level_matches_layerwise(net, lvl, split, pre, monkeypatch):
+@pytest.mark.parametrize("lvl,split,pre,b6", [
+    (0, False, False, False), (1, False, False, False), (2, False, False, False),
+    (1, True, False, False), (2, True, False, False), (1, False, True, False),
+    (2, False, True, False), (1, True, True, False), (2, True, True, False),
+    (0, False, False, True), (1, False, False, True), (1, False, True, True)])
+def test_fused_level_matches_layerwise(net, lvl, split, pre, b6, monkeypatch):
     """The fused level kernels (group_l1 / group_fused: activations in MFMA accumulators;
     group_split: channel-split through LDS; pre: the first convs' feature blocks
-    precomputed per feature row, engine.LEVEL_PRE) against the layer-by-layer GEMM path on
-    the same grouping; fp32 summation order differs, so within 1e-4."""
+    precomputed per feature row, engine.LEVEL_PRE; b6: group_l1_6 / group_fused6, the
+    products on the bf16 matrix cores at fp32 accuracy) against the layer-by-layer GEMM
+    path on the same grouping; fp32 summation order differs, so within 1e-4."""
     from pcd_reg_hregnet_amd import engine, synthetic
     monkeypatch.setattr(engine, "LEVEL_PRE", pre)
+    monkeypatch.setattr(engine, "B6_L1", b6)
+    monkeypatch.setattr(engine, "B6_L2", b6)
     P = net.prepared(torch.device("cuda"))
     s, _, _, _ = synthetic.lidar_batch(2, 4096, seed0=60)
     pts = torch.from_numpy(s).cuda()
@@ -456,3 +461,34 @@ def test_model_v2_graph_pipeline_matches_eager(net_v2):
             assert torch.equal(o["rotation"][i], ref["rotation"][i])
             assert torch.equal(o["translation"][i], ref["translation"][i])
     np.testing.assert_allclose(outs[1]["rotation"][-1].cpu().numpy(), g["R1"], atol=1e-4)
+
+
+def test_b6_kernels_deterministic(net):
+    """The bf16x6 kernels (group_l1_6, group_fused6, fine_head6 / nbr_head6) give the same
+    bits run after run with two workgroups per CU (two waves per SIMD): the configuration
+    in which packed-fp32 VALU ops next to the bf16 MFMAs gave nondeterministic wrong values
+    (build.NO_PACKED_F32); and level 1 matches the fp32-MFMA kernel at 1e-4."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    s, d, _, _ = synthetic.lidar_batch(4, 8192, seed0=70)
+    src, dst = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    with torch.no_grad():
+        runs = [engine.hregnet_forward(P, src, dst) for _ in range(4)]
+        g = engine.grouping(src, 0, None)
+        old = engine.B6_L1
+        try:
+            engine.B6_L1 = False
+            ref = engine.keypoint_level(P, 0, src, None, None, grouped=g)
+            engine.B6_L1 = True
+            b6 = engine.keypoint_level(P, 0, src, None, None, grouped=g)
+        finally:
+            engine.B6_L1 = old
+    torch.cuda.synchronize()
+    for r in runs[1:]:
+        for key in ("desc_1", "desc_2", "desc_3", "xyz_1", "xyz_2", "xyz_3"):
+            assert torch.equal(r["src_feats"][key], runs[0]["src_feats"][key]), key
+        for i in range(3):
+            assert torch.equal(r["rotation"][i], runs[0]["rotation"][i])
+        assert torch.equal(r["src_dst_weights_1"], runs[0]["src_dst_weights_1"])
+    for a, b in zip(ref[:4], b6[:4]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)

@@ -241,6 +241,13 @@ def test_nbr_head_table_size_matches_kernel(P):
     assert prep.nbr_table.numel() == L.hreg_nbr_head_table_floats()
 
 
+def test_l1_table6_matches_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.l1_table6.numel() == L.hreg_group_l1_6_table_floats()
+
+
 def test_head6_tables_match_kernel(P):
     """bf16x6 head tables (engine.fine_head_table6 / nbr_head_table6): sizes match the
     kernels' Head6Cfg, and the three bf16 pieces of every weight sum back to it exactly."""
