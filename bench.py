@@ -140,6 +140,8 @@ MFMA_ENTRIES = {
     "hreg_group_split_l2": ("fused", _level_work(2)),
     "hreg_group_split_l3": ("fused", _level_work(3)),
     "hreg_group6_l2": ("fused", _level_work(2)),
+    "hreg_group_split6_l2": ("fused", _level_work(2)),
+    "hreg_group_split6_l3": ("fused", _level_work(3)),
     "hreg_group6_l3": ("fused", _level_work(3)),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
@@ -220,6 +222,15 @@ class MfmaTimer:
                          "avg_launch_us": round(ms / max(len(ev), 1) * 1e3, 2),
                          "tflops": round(fl / max(ms, 1e-9) / 1e9, 2)}
         return out
+
+
+def level_kernel(engine, lv: int) -> str:
+    """rocprof name of the fused level-2/3 kernel the engine's switches select."""
+    split = engine.SPLIT_L2 if lv == 2 else engine.SPLIT_L3
+    b6 = engine.B6_L2 if lv == 2 else engine.B6_L3
+    if split:
+        return "group_split6_kernel" if b6 else "group_split_kernel"
+    return "group_fused6_kernel" if (lv == 2 and b6) else "group_fused_kernel"
 
 
 def pmc_traffic(kernel: str):
@@ -461,8 +472,7 @@ def main():
     if args.split is not None:
         on = {int(x) for x in filter(None, args.split.split(","))}
         engine.SPLIT_L2, engine.SPLIT_L3 = 2 in on, 3 in on
-    fused_names = [("group_split_kernel" if s else "group_fused_kernel") + f" (level {lv})"
-                   for lv, s in ((2, engine.SPLIT_L2), (3, engine.SPLIT_L3))]
+    fused_names = [level_kernel(engine, lv) + f" (level {lv})" for lv in (2, 3)]
     net = make_model(device, args.model)
     P = net.prepared(device)
     B = args.batch

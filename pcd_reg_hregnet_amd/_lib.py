@@ -82,6 +82,8 @@ _SIGS = {
     "hreg_group6_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group6_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group_split6_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group_split6_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head_table_floats": [_i],
     "hreg_nbr_head": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
@@ -147,7 +149,8 @@ EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_
                           "hreg_group_l2_table_floats", "hreg_group_l3_table_floats",
                           "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
                           "hreg_group_split_l3_table_floats", "hreg_group6_l2_table_floats",
-                          "hreg_group6_l3_table_floats", "hreg_group_l1_6_table_floats")
+                          "hreg_group6_l3_table_floats", "hreg_group_l1_6_table_floats",
+                          "hreg_group_split6_l2_table_floats", "hreg_group_split6_l3_table_floats")
 
 _lib = None
 
@@ -181,7 +184,8 @@ def load(require_gpu: bool = True):
                      "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
                      "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats",
                      "hreg_group6_l2_table_floats", "hreg_group6_l3_table_floats",
-                     "hreg_group_l1_6_table_floats"):
+                     "hreg_group_l1_6_table_floats", "hreg_group_split6_l2_table_floats",
+                     "hreg_group_split6_l3_table_floats"):
             getattr(L, name).restype = ctypes.c_int
             getattr(L, name).argtypes = []
         _lib = L

@@ -236,9 +236,12 @@ __device__ __forceinline__ f32x16 mma6(const u32x4 (&a)[3], const u32x4 (&b)[3],
 constexpr int CARRY6 = 8;  // output tiles of a call's first chunk carried between calls
 
 // weight pieces of chunk fragment f (units of 3 x 64 lanes x 16 B)
+// (signed pointer arithmetic: a wave-uniform f stays an SGPR base, the lane a VGPR offset,
+// the piece an immediate -- no per-fragment VGPR address to hoist and spill)
 __device__ __forceinline__ void ld6(const gu32x4 *__restrict__ wt, int f, int lane, u32x4 (&o)[3]) {
+    const gu32x4 *fp = wt + f * 192;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) o[p] = wt[(unsigned)(f * 3 + p) * 64u + (unsigned)lane];
+    for (int p = 0; p < 3; ++p) o[p] = fp[p * 64 + lane];
 }
 
 // acc[co] += sum_{c < NCH} A(co, c) x B(c) with B(c) = split(bval(8c .. 8c+7)); chunk

@@ -110,6 +110,57 @@ __device__ __forceinline__ void pipe_lds(const gfloat *__restrict__ wf, int lane
 template <int NSTEP>
 constexpr int swin() { return NSTEP < SWIN ? NSTEP : SWIN; }
 
+// The same on the bf16 matrix cores at fp32 accuracy (bf16x6, mfma_chain.h): acc[P] +=
+// sum_{c < NCH} A(co0 + i, c) x split(B(8c .. 8c+7)).  A: bf16 piece chunk fragments from
+// the table (fragment f.base + i * f.stride + c, one chunk ahead, double-buffered); B: 8
+// f32 k-steps per chunk read from LDS through bl(st0, v[4]) (two calls, one chunk ahead)
+// and split into pieces in registers.  cin: this call's first chunk (P tiles), loaded by
+// the previous call; cout: the first chunk of the next call nf (NP tiles).
+typedef u32x4 Carry6[CARRY6][3];
+
+template <int NCH, int P, int NP, class BL>
+__device__ __forceinline__ void pipe_lds6(const gu32x4 *__restrict__ wt, int lane, FragSeq f, BL bl,
+                                          f32x16 (&acc)[P], const Carry6 &cin, FragSeq nf, Carry6 &cout) {
+    static_assert(P <= CARRY6 && NP <= CARRY6, "carry");
+    u32x4 abuf[2][P][3];
+    float bb[2][8];
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) abuf[0][i][p] = cin[i][p];
+    {
+        float v[4];
+        bl(0, v);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bb[0][k] = v[k];
+        bl(4, v);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bb[0][4 + k] = v[k];
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) {
+#pragma unroll
+            for (int i = 0; i < P; ++i) ld6(wt, f.base + i * f.stride + c + 1, lane, abuf[(c + 1) & 1][i]);
+            float v[4];
+            bl(8 * (c + 1), v);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bb[(c + 1) & 1][k] = v[k];
+            bl(8 * (c + 1) + 4, v);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bb[(c + 1) & 1][4 + k] = v[k];
+        } else {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) ld6(wt, nf.base + i * nf.stride, lane, cout[i]);
+        }
+        u32x4 b[3];
+        split8(bb[c & 1], b);
+#pragma unroll
+        for (int i = 0; i < P; ++i) acc[i] = mma6(abuf[c & 1][i], b, acc[i]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // BN/ReLU epilogue of output tiles co0 .. co0+P-1 of a C-channel layer
 template <int P, int C>
 __device__ __forceinline__ void epi(const float *ab, int co0, int h, f32x16 (&acc)[P]) {

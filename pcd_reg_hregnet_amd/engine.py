@@ -46,6 +46,9 @@ SPLIT_L3 = True
 # (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
 B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
 B6_L1 = os.environ.get("HREG_B6_L1", "1") != "0"  # group_l1_6.hip for level 1
+# level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
+# (group_split6.hip)
+B6_L3 = os.environ.get("HREG_B6_L3", "1") != "0"
 # the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
 # precomputed-block form, HEAD_PRE)
 B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
@@ -183,6 +186,8 @@ class PreparedWeights:
         self.l2_table6 = l2_table6(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l3_table6 = l2_table6(self.det[2], self.desc[2], self.desc_mlp[2])
         self.l2s_table = split_table(self.det[1], self.desc[1], self.desc_mlp[1])
+        self.l2s_table6 = split_table6(self.det[1], self.desc[1], self.desc_mlp[1])
+        self.l3s_table6 = split_table6(self.det[2], self.desc[2], self.desc_mlp[2])
         self.l3s_table = split_table(self.det[2], self.desc[2], self.desc_mlp[2])
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
                            for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
@@ -197,7 +202,7 @@ class PreparedWeights:
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
                      "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre",
                      "coarse_head", "fine", "l1_table", "l1_table6", "l2_table", "l3_table", "l2_table6",
-                     "l3_table6", "l2s_table",
+                     "l3_table6", "l2s_table", "l2s_table6", "l3s_table6",
                      "l3s_table", "fine_table", "fine_table6", "nbr_table6",
                      "nbr_table", "head_table", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
@@ -414,6 +419,16 @@ def split_table(det, desc, mlp) -> torch.Tensor:
     for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]):
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def split_table6(det, desc, mlp) -> torch.Tensor:
+    """Table of group_split6.hip (SCfg6): l2_table6's bf16 piece chunk fragments, then
+    mlp1's x2 block f32 row-major [CM1][C3] (the per-group matrix-vector product), then the
+    f32 epilogues."""
+    t6 = l2_table6(det, desc, mlp)
+    ne = sum(2 * lin.N for lin in (det[0], det[1], det[2], desc[0], desc[1], desc[2], mlp[0], mlp[1]))
+    x2 = mlp[0].W[:, :det[2].W.shape[0]].contiguous().reshape(-1).float()
+    return torch.cat([t6[:t6.numel() - ne], x2, t6[t6.numel() - ne:]]).contiguous()
 
 
 def _group4(frag: torch.Tensor, gs: int) -> torch.Tensor:
@@ -760,9 +775,13 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         kp = _empty(G, 3, device=dev)
         att_feat = _empty(G, LEVELS[lvl][3][-1], device=dev)
         desc = _empty(G, LEVELS[lvl][5], device=dev)
+        split = (SPLIT_L2, SPLIT_L3)[lvl - 1]
         if lvl == 1 and B6_L2 and not SPLIT_L2:
             name, table = "hreg_group6_l2", P.l2_table6
-        elif (SPLIT_L2, SPLIT_L3)[lvl - 1]:
+        elif split and (B6_L2, B6_L3)[lvl - 1]:
+            name, table = (("hreg_group_split6_l2", P.l2s_table6) if lvl == 1 else
+                           ("hreg_group_split6_l3", P.l3s_table6))
+        elif split:
             name, table = (("hreg_group_split_l2", P.l2s_table) if lvl == 1 else
                            ("hreg_group_split_l3", P.l3s_table))
         else:

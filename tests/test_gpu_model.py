@@ -184,7 +184,8 @@ def test_graph_lanes_match_eager(net):
     (0, False, False, False), (1, False, False, False), (2, False, False, False),
     (1, True, False, False), (2, True, False, False), (1, False, True, False),
     (2, False, True, False), (1, True, True, False), (2, True, True, False),
-    (0, False, False, True), (1, False, False, True), (1, False, True, True)])
+    (0, False, False, True), (1, False, False, True), (1, False, True, True),
+    (1, True, False, True), (2, True, False, True), (1, True, True, True), (2, True, True, True)])
 def test_fused_level_matches_layerwise(net, lvl, split, pre, b6, monkeypatch):
     """The fused level kernels (group_l1 / group_fused: activations in MFMA accumulators;
     group_split: channel-split through LDS; pre: the first convs' feature blocks
@@ -195,6 +196,7 @@ def test_fused_level_matches_layerwise(net, lvl, split, pre, b6, monkeypatch):
     monkeypatch.setattr(engine, "LEVEL_PRE", pre)
     monkeypatch.setattr(engine, "B6_L1", b6)
     monkeypatch.setattr(engine, "B6_L2", b6)
+    monkeypatch.setattr(engine, "B6_L3", b6)
     P = net.prepared(torch.device("cuda"))
     s, _, _, _ = synthetic.lidar_batch(2, 4096, seed0=60)
     pts = torch.from_numpy(s).cuda()

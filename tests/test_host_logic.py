@@ -241,6 +241,14 @@ def test_nbr_head_table_size_matches_kernel(P):
     assert prep.nbr_table.numel() == L.hreg_nbr_head_table_floats()
 
 
+def test_split_tables6_match_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.l2s_table6.numel() == L.hreg_group_split6_l2_table_floats()
+    assert prep.l3s_table6.numel() == L.hreg_group_split6_l3_table_floats()
+
+
 def test_l1_table6_matches_kernel(P):
     _, prep = P
     from pcd_reg_hregnet_amd import _lib
