@@ -29,6 +29,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
+# fp32-accurate products on the bf16 matrix cores (bf16x6, mfma_chain.h): 6 bf16 MFMAs of
+# the same shape per fp32 product, so the fp32-equivalent peak is the bf16 dense peak / 6
+PEAK_B6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak BW (spec)
 # 20.51 GFLOP/pair of 1x1 convs (conv hooks on the reference) + 2 x 0.034
 # GFLOP cosine-similarity contractions
@@ -133,16 +137,16 @@ def _l1_work(a):
 
 # C-ABI entry -> (timer kind, work of one launch from its arguments)
 MFMA_ENTRIES = {
-    "hreg_group_l1": ("l1", _l1_work),
-    "hreg_group_l1_6": ("l1", _l1_work),
-    "hreg_group_l2": ("fused", _level_work(2)),
-    "hreg_group_l3": ("fused", _level_work(3)),
-    "hreg_group_split_l2": ("fused", _level_work(2)),
-    "hreg_group_split_l3": ("fused", _level_work(3)),
-    "hreg_group6_l2": ("fused", _level_work(2)),
-    "hreg_group_split6_l2": ("fused", _level_work(2)),
-    "hreg_group_split6_l3": ("fused", _level_work(3)),
-    "hreg_group6_l3": ("fused", _level_work(3)),
+    "hreg_group_l1": ("level", _l1_work),
+    "hreg_group_l1_6": ("level", _l1_work),
+    "hreg_group_l2": ("level", _level_work(2)),
+    "hreg_group_l3": ("level", _level_work(3)),
+    "hreg_group_split_l2": ("level", _level_work(2)),
+    "hreg_group_split_l3": ("level", _level_work(3)),
+    "hreg_group6_l2": ("level", _level_work(2)),
+    "hreg_group_split6_l2": ("level", _level_work(2)),
+    "hreg_group_split6_l3": ("level", _level_work(3)),
+    "hreg_group6_l3": ("level", _level_work(3)),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
     "hreg_fine_head6": ("head", _fine6_work),
@@ -152,11 +156,11 @@ MFMA_ENTRIES = {
 
 
 class MfmaTimer:
-    """Brackets every fp32-MFMA launch (gemm_nt_kernel, group_l1_kernel,
-    group_fused_kernel, fine/nbr/mlp head kernels) with HIP events on the launch stream
-    and counts its algorithmic FLOPs and bytes, per kernel kind."""
+    """Brackets every MFMA launch (gemm_nt_kernel, the fused level kernels, fine/nbr/mlp
+    head kernels) with HIP events on the launch stream and counts its algorithmic FLOPs and
+    bytes, per kernel kind and per C-ABI entry."""
 
-    KINDS = ("gemm", "l1", "fused", "head", "mlp")
+    KINDS = ("gemm", "level", "head", "mlp")
 
     def __init__(self):
         self.events = {k: [] for k in self.KINDS}
@@ -187,15 +191,17 @@ class MfmaTimer:
 
     def install(self):
         from pcd_reg_hregnet_amd import _lib, engine
-        orig_gemm = _lib.gemm
+        orig_gemm, orig_gemm6 = _lib.gemm, _lib.gemm6
         orig_call = engine.call
 
-        def gemm(g):
-            # algorithmic bytes: the A operand as presented (R x K, gathered rows
-            # counted once per use), W and the output, fp32
-            nbytes = 4.0 * g.batch * (g.R * g.K + g.N * g.K + g.R * g.N)
-            return self._timed("gemm", lambda: orig_gemm(g), 2.0 * g.R * g.N * g.K * g.batch,
-                               nbytes)
+        def gemm_of(fn, entry):
+            def gemm(g):
+                # algorithmic bytes: the A operand as presented (R x K, gathered rows
+                # counted once per use), W and the output, fp32
+                nbytes = 4.0 * g.batch * (g.R * g.K + g.N * g.K + g.R * g.N)
+                return self._timed("gemm", lambda: fn(g), 2.0 * g.R * g.N * g.K * g.batch,
+                                   nbytes, entry=entry)
+            return gemm
 
         def call(name, *args):
             if name in MFMA_ENTRIES:
@@ -203,7 +209,8 @@ class MfmaTimer:
                 fl, nb, xf = work(args)
                 return self._timed(kind, lambda: orig_call(name, *args), fl, nb, xf, entry=name)
             return orig_call(name, *args)
-        _lib.gemm = gemm
+        _lib.gemm = gemm_of(orig_gemm, "hreg_gemm")
+        _lib.gemm6 = gemm_of(orig_gemm6, "hreg_gemm6")
         engine.call = call
 
     def result(self, kind):
@@ -213,19 +220,30 @@ class MfmaTimer:
         return ms, len(ev), self.flops[kind], self.bytes[kind], self.xflops[kind]
 
     def entries(self, steps):
-        """per C-ABI entry: launches per step, mean launch duration, algorithmic TFLOP/s"""
+        """per C-ABI entry: launches per step, mean launch duration, algorithmic TFLOP/s,
+        the entry's MFMA peak (bf16x6 entries end in 6)"""
         torch.cuda.synchronize()
         out = {}
         for name, (ev, fl) in sorted(self.by_entry.items()):
             ms = sum(a.elapsed_time(b) for a, b in ev)
             out[name] = {"launches_per_step": len(ev) // max(steps, 1),
                          "avg_launch_us": round(ms / max(len(ev), 1) * 1e3, 2),
-                         "tflops": round(fl / max(ms, 1e-9) / 1e9, 2)}
+                         "tflops": round(fl / max(ms, 1e-9) / 1e9, 2),
+                         "peak": entry_peak(name), "_ms": ms, "_flops": fl}
         return out
 
 
+def entry_peak(name: str) -> float:
+    """MFMA peak (fp32-equivalent TFLOP/s) of a C-ABI entry's kernel: bf16x6 kernels
+    (hreg_group_l1_6, hreg_group6_*, hreg_group_split6_*, hreg_*_head6) run on the bf16
+    matrix cores, the others on v_mfma_f32_32x32x2_f32."""
+    return PEAK_B6_TFLOPS if name.endswith("6") or "6_" in name else PEAK_FP32_MFMA_TFLOPS
+
+
 def level_kernel(engine, lv: int) -> str:
-    """rocprof name of the fused level-2/3 kernel the engine's switches select."""
+    """rocprof name of the fused level kernel the engine's switches select."""
+    if lv == 1:
+        return "group_l1_6_kernel" if engine.B6_L1 else "group_l1_kernel"
     split = engine.SPLIT_L2 if lv == 2 else engine.SPLIT_L3
     b6 = engine.B6_L2 if lv == 2 else engine.B6_L3
     if split:
@@ -235,16 +253,18 @@ def level_kernel(engine, lv: int) -> str:
 
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/r1_traffic.json, made by tools/rocpd_summary.py traffic)."""
-    path = os.path.join(REPO, "profiles", "r1_traffic.json")
-    try:
-        per = json.load(open(path))["bytes_per_launch"]
-        # "group_fused_kernel (level 2) + ..." -> the rocprof family names; one launch of
-        # each per step: mean over the family
-        names = [n.split(" (")[0] for n in kernel.split(" + ")]
-        return sum(per[n] for n in names) / len(names), os.path.relpath(path, REPO)
-    except Exception:
-        return None, None
+    (profiles/r*_traffic.json, made by tools/rocpd_summary.py traffic; the latest round
+    that measured every kernel of the family)."""
+    names = [n.split(" (")[0] for n in kernel.split(" + ")]
+    for rnd in ("r2", "r1"):
+        path = os.path.join(REPO, "profiles", f"{rnd}_traffic.json")
+        try:
+            per = json.load(open(path))["bytes_per_launch"]
+            # one launch of each per step: mean over the family
+            return sum(per[n] for n in names) / len(names), os.path.relpath(path, REPO)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def cpu_baseline(budget_s: float = 12.0):
@@ -472,7 +492,7 @@ def main():
     if args.split is not None:
         on = {int(x) for x in filter(None, args.split.split(","))}
         engine.SPLIT_L2, engine.SPLIT_L3 = 2 in on, 3 in on
-    fused_names = [level_kernel(engine, lv) + f" (level {lv})" for lv in (2, 3)]
+    level_names = [level_kernel(engine, lv) + f" (level {lv})" for lv in (1, 2, 3)]
     net = make_model(device, args.model)
     P = net.prepared(device)
     B = args.batch
@@ -540,22 +560,35 @@ def main():
                     "gflop_per_pair": round(fl / args.steps / B / 1e9, 3),
                     "executed_tflops": round(xf / max(ms, 1e-9) / 1e9, 2),
                     "executed_gflop_per_pair": round(xf / args.steps / B / 1e9, 3)}
-        f_ms, f_n, f_fl, f_nb, f_xf = res["fused"]
+        # roofline kernel family: the three fused level kernels (keypoint detector +
+        # descriptor, levels 1-3), the largest MFMA family of the step
+        f_ms, f_n, f_fl, f_nb, f_xf = res["level"]
         per_launch_s = f_ms / max(f_n, 1) / 1e3
         per_launch_flops = f_fl / max(f_n, 1)
         achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(" + ".join(fused_names))
+        ent = timer.entries(args.steps)
+        lev = {n: e for n, e in ent.items() if n in MFMA_ENTRIES and MFMA_ENTRIES[n][0] == "level"}
+        # the family's peak: its FLOPs over the time they need at each kernel's own peak
+        t_peak = sum(e["_flops"] / (e["peak"] * 1e12) for e in lev.values())
+        peak = sum(e["_flops"] for e in lev.values()) / t_peak / 1e12 if t_peak else PEAK_B6_TFLOPS
+        traffic, traffic_src = pmc_traffic(" + ".join(level_names))
         tot_ms = sum(r[0] for r in res.values())
         tot_xf = sum(r[4] for r in res.values())
         alg_fl = ALG_GFLOP_PER_PAIR * 1e9 * B * args.steps
-        roof = {"kernel": " + ".join(fused_names) + " (keypoint detector + descriptor: "
-                          "every conv/BN/ReLU layer, attention and k-max of the level in one "
-                          "launch)",
+        per_entry = {n: {k: v for k, v in e.items() if not k.startswith("_")} for n, e in ent.items()}
+        roof = {"kernel": " + ".join(level_names) + " (keypoint detector + descriptor of "
+                          "levels 1-3: every conv/BN/ReLU layer, attention and k-max of a "
+                          "level in one launch)",
                 "timing": "HIP events on the launch stream, " + (
                     "instrumented eager pipelined pass of the same steps after the timed "
                     "graph region" if args.executor == "graph" else "inside the timed region"),
-                "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                "bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1),
+                "unit": "TFLOP/s",
+                "peak_basis": "fp32-accurate products: bf16x6 kernels at the bf16 dense MFMA "
+                              f"peak / 6 = {PEAK_B6_TFLOPS:.1f}, fp32-MFMA kernels at "
+                              f"{PEAK_FP32_MFMA_TFLOPS} (MI355X_MICROARCH.md); FLOP-weighted "
+                              "over the family",
+                "frac": round(achieved / peak, 4),
                 "traffic": None if traffic is None else round(traffic),
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": round(f_nb / max(f_n, 1)),
@@ -565,10 +598,9 @@ def main():
                 "launches_per_step": f_n // args.steps,
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
                 "other_mfma_kernels": {"gemm_nt_kernel": kind_summary("gemm"),
-                                       "group_l1_kernel": kind_summary("l1"),
-                                       "fine_head_kernel + nbr_head_kernel": kind_summary("head"),
+                                       "fine/nbr head kernels": kind_summary("head"),
                                        "mlp_head_kernel": kind_summary("mlp")},
-                "per_entry": timer.entries(args.steps),
+                "per_entry": per_entry,
                 "all_mfma": {"ms_per_step": round(tot_ms / args.steps, 3),
                              "gflop_per_pair": ALG_GFLOP_PER_PAIR,
                              "tflops": round(alg_fl / max(tot_ms, 1e-9) / 1e9, 2),
@@ -586,6 +618,11 @@ def main():
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "precision": "fp32 throughout; the fused level and head kernels take their fp32 "
+                         "products on the bf16 matrix cores as 3-piece exact splits (bf16x6, "
+                         "6 MFMAs per product, fp32 accumulate: error vs fp64 equal to the "
+                         "fp32 MFMA's, profiles/r2_split_mfma_micro.txt); parity tests at the "
+                         "fp32 bars",
             "data": "synthetic (seeded KITTI-shape LiDAR pairs; nusc_feats + seeded heads)",
             "config": {"workload": (f"Model_V2 forward (eval), batch={B} pairs/GPU, 2x{args.points}"
                                     "-pt LiDAR pairs (BASELINE configs[4])") if v2 else (

@@ -161,6 +161,12 @@ typedef struct {
 
 int hreg_gemm(const hreg_gemm_t *g, void *stream);
 
+/* hreg_gemm with fp32-accurate products on the bf16 matrix cores (bf16x6: A and W split
+ * exactly into three bf16 pieces while staged into LDS, 6 v_mfma_f32_32x32x16_bf16 per
+ * 16-deep k sub-chunk; gemm.hip gemm6_kernel).  Same arguments; addends (nadd > 0) are
+ * not supported (HREG_ERR_UNSUPPORTED).  Accumulation order independent of R / batch. */
+int hreg_gemm6(const hreg_gemm_t *g, void *stream);
+
 /* Attentive pooling over groups of k rows (layers.py:150-159 and siblings).
  * logits_src [G*k][C] : a = softmax_k(max_c logits_src[r][c])  -> attw [G*k] (optional)
  * values: att[g][c] = sum_j a[g,j] * V[row(g,j)][c], V = vals (row = g*k+j) or

@@ -63,6 +63,7 @@ _SIGS = {
     "hreg_spatial_index": [_vp, _i, _i, _vp, _vp],
     "hreg_knn_group_indexed": [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "hreg_gemm": [ctypes.POINTER(Gemm), _vp],
+    "hreg_gemm6": [ctypes.POINTER(Gemm), _vp],
     "hreg_attend": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp],
     "hreg_group_max": [_vp, _i, _i, _i, _i, _vp, _i, _vp],
     "hreg_head_out": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp],
@@ -234,3 +235,11 @@ def gemm(g: Gemm) -> None:
     rc = L.hreg_gemm(ctypes.byref(g), stream_handle())
     if rc != HREG_OK:
         raise RuntimeError(f"hreg_gemm failed: {_ERRORS.get(rc, rc)} (code {rc})")
+
+
+def gemm6(g: Gemm) -> None:
+    """hreg_gemm6: the same GEMM with bf16x6 products on the bf16 matrix cores."""
+    L = load()
+    rc = L.hreg_gemm6(ctypes.byref(g), stream_handle())
+    if rc != HREG_OK:
+        raise RuntimeError(f"hreg_gemm6 failed: {_ERRORS.get(rc, rc)} (code {rc})")

@@ -205,6 +205,170 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     }
 }
 
+// ------------------------------------------------------------------------
+// The same GEMM with fp32-accurate products on the bf16 matrix cores (bf16x6,
+// mfma_chain.h): every A and W value is split exactly into three bf16 pieces while it is
+// staged into LDS (once per workgroup), and each 16-deep k sub-chunk of a 32x32 output
+// tile is 6 v_mfma_f32_32x32x16_bf16 (a_h w_l, a_m w_m, a_l w_h, a_h w_m, a_m w_h, a_h w_h)
+// instead of 8 v_mfma_f32_32x32x2_f32.  128 x 128 tiles, 4 waves of 64 x 64, K in 32-deep
+// chunks: the next chunk is loaded into registers during this chunk's MFMAs, split and
+// stored after a barrier (one LDS buffer of pieces, 60 KB: two workgroups per CU).  LDS
+// rows of pieces are 32 bf16 + 8 pad (80 B: the 8-row groups of a ds_read_b128 hit
+// distinct 16-byte bank quads).  Lane half h takes k = sub*16 + 8h + i of a sub-chunk,
+// so the accumulation order of an output does not depend on R or the batch.
+typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
+
+constexpr int G6_BM = 128, G6_BN = 128, G6_BK = 32, G6_LDR = G6_BK + 8;  // LDS row, in bf16
+
+// x -> (hi, mid, lo) bf16 bit patterns: exact truncation split (mfma_chain.h split8)
+__device__ __forceinline__ void split1(float v, uint32_t &hb, uint32_t &mb, uint32_t &lb) {
+    const uint32_t xb = __float_as_uint(v);
+    const float r = fsub_rn(v, __uint_as_float(xb & 0xffff0000u));
+    const uint32_t rb = __float_as_uint(r);
+    hb = xb >> 16;
+    mb = rb >> 16;
+    lb = __float_as_uint(fsub_rn(r, __uint_as_float(rb & 0xffff0000u))) >> 16;
+}
+
+// float4 of row `row`, k = k0..k0+3 -> three 8-byte piece stores
+__device__ __forceinline__ void store_pieces(uint16_t *buf, int row, int k0, float4 v) {
+    uint32_t h[4], m[4], l[4];
+    split1(v.x, h[0], m[0], l[0]);
+    split1(v.y, h[1], m[1], l[1]);
+    split1(v.z, h[2], m[2], l[2]);
+    split1(v.w, h[3], m[3], l[3]);
+    constexpr int PS = 128 * G6_LDR;  // piece stride (bf16)
+    uint16_t *p = buf + row * G6_LDR + k0;
+    *reinterpret_cast<uint2 *>(p) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    *reinterpret_cast<uint2 *>(p + PS) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+    *reinterpret_cast<uint2 *>(p + 2 * PS) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+}
+
+__device__ __forceinline__ f32x16 mfma_b16(u32x4g a, u32x4g b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8g, a), __builtin_bit_cast(bf16x8g, b),
+                                                   c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256, 2) void gemm6_kernel(const hreg_gemm_t g) {
+    constexpr int BM = G6_BM, BN = G6_BN, BK = G6_BK, LDR = G6_LDR, PS = 128 * LDR;
+    constexpr int F4 = BK / 4, A_LD = BM * F4 / 256, B_LD = BN * F4 / 256;
+    constexpr int TM = 2, TN = 2;  // 32x32 tiles per wave (64 x 64)
+    __shared__ __attribute__((aligned(16))) uint16_t As[3 * PS];
+    __shared__ __attribute__((aligned(16))) uint16_t Ws[3 * PS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int b = blockIdx.z, r0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const int nchunks = (g.K + BK - 1) / BK;
+    const int h = lane >> 5, l32 = lane & 31;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+    float4 ra[A_LD], rb[B_LD];
+    auto gload = [&](int c) {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+            const int e = tid + i * 256;
+            ra[i] = load_a4(g, b, r0 + e / F4, c * BK + (e % F4) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) {
+            const int e = tid + i * 256;
+            rb[i] = load_w4(g, b, n0 + e / F4, c * BK + (e % F4) * 4);
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+            const int e = tid + i * 256;
+            store_pieces(As, e / F4, (e % F4) * 4, ra[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) {
+            const int e = tid + i * 256;
+            store_pieces(Ws, e / F4, (e % F4) * 4, rb[i]);
+        }
+    };
+
+    gload(0);
+    lstore();
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+        if (c + 1 < nchunks) gload(c + 1);
+#pragma unroll
+        for (int sub = 0; sub < BK / 16; ++sub) {
+            const int koff = sub * 16 + h * 8;
+            u32x4g fa[TM][3], fw[TN][3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    fa[i][p] = *reinterpret_cast<const u32x4g *>(&As[p * PS + (wr * 64 + i * 32 + l32) * LDR + koff]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    fw[j][p] = *reinterpret_cast<const u32x4g *>(&Ws[p * PS + (wc * 64 + j * 32 + l32) * LDR + koff]);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    f32x16 c6 = acc[i][j];
+                    c6 = mfma_b16(fa[i][0], fw[j][2], c6);
+                    c6 = mfma_b16(fa[i][1], fw[j][1], c6);
+                    c6 = mfma_b16(fa[i][2], fw[j][0], c6);
+                    c6 = mfma_b16(fa[i][0], fw[j][1], c6);
+                    c6 = mfma_b16(fa[i][1], fw[j][0], c6);
+                    acc[i][j] = mfma_b16(fa[i][0], fw[j][0], c6);
+                }
+        }
+        __syncthreads();  // every wave has read this chunk's pieces
+        if (c + 1 < nchunks) {
+            lstore();
+            __syncthreads();
+        }
+    }
+
+    // epilogue (gemm_nt_kernel's): lane l, reg q -> row (q&3) + 8*(q>>2) + 4*h, col l&31
+    float *out = g.out + (size_t)b * g.out_batch_stride;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wc * 64 + j * 32 + l32;
+        if (n >= g.N) continue;
+        float sc = 1.f, sh = 0.f, cn = 1.f;
+        if (g.epi == HREG_EPI_AFFINE) {
+            if (g.scale) sc = g.scale[n];
+            if (g.shift) sh = g.shift[n];
+        } else {
+            cn = g.cnorm[(size_t)b * g.cnorm_batch_stride + n];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int r = r0 + wr * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (r < g.R) {
+                    float y = acc[i][j][q];
+                    if (g.epi == HREG_EPI_AFFINE) {
+                        y = fadd_rn(fmul_rn(y, sc), sh);
+                        if (g.relu) y = fmaxf(y, 0.f);
+                    } else {
+                        const float rn = g.rnorm[(size_t)b * g.rnorm_batch_stride + r];
+                        y = y / fadd_rn(fmul_rn(rn, cn), 1e-6f);
+                    }
+                    out[(size_t)r * g.ldo + n] = y;
+                }
+            }
+        }
+    }
+}
+
 bool seg_ok(const hreg_seg_t &s) {
     if (!s.base || s.ld <= 0 || (s.ld & 3) || (s.k0 & 3) || (s.kc & 3) || s.kc <= 0) return false;
     if (!s.gather && s.row_div < 1) return false;
@@ -212,11 +376,7 @@ bool seg_ok(const hreg_seg_t &s) {
     return true;
 }
 
-}  // namespace
-
-extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
-    if (!gp) return HREG_ERR_INVALID;
-    const hreg_gemm_t &g = *gp;
+int gemm_check(const hreg_gemm_t &g) {
     if (g.R < 0 || g.N <= 0 || g.K <= 0 || g.batch < 1 || !g.W || !g.out) return HREG_ERR_INVALID;
     if (g.nseg < 1 || g.nseg > HREG_MAX_SEGS) return HREG_ERR_INVALID;
     if ((g.ldw & 3) || g.ldw < g.K || (reinterpret_cast<uintptr_t>(g.W) & 15)) return HREG_ERR_INVALID;
@@ -229,6 +389,27 @@ extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
         const hreg_seg_t &ad = g.add[a];
         if (!ad.base || ad.ld < g.N || (!ad.gather && ad.row_div < 1)) return HREG_ERR_INVALID;
     }
+    return HREG_OK;
+}
+
+}  // namespace
+
+extern "C" int hreg_gemm6(const hreg_gemm_t *gp, void *stream) {
+    if (!gp) return HREG_ERR_INVALID;
+    const hreg_gemm_t &g = *gp;
+    if (const int rc = gemm_check(g)) return rc;
+    if (g.nadd) return HREG_ERR_UNSUPPORTED;  // addends: hreg_gemm
+    if (g.R == 0) return HREG_OK;
+    dim3 grid((g.R + G6_BM - 1) / G6_BM, (g.N + G6_BN - 1) / G6_BN, g.batch);
+    hipLaunchKernelGGL(gemm6_kernel, grid, dim3(256), 0, as_stream(stream), g);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
+    if (!gp) return HREG_ERR_INVALID;
+    const hreg_gemm_t &g = *gp;
+    if (const int rc = gemm_check(g)) return rc;
     if (g.R == 0) return HREG_OK;
     hipStream_t st = as_stream(stream);
     // tile choice: wide tiles (K in 16-deep chunks) for the big layers; 64x64 tiles

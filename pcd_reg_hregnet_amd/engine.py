@@ -49,6 +49,9 @@ B6_L1 = os.environ.get("HREG_B6_L1", "1") != "0"  # group_l1_6.hip for level 1
 # level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
 # (group_split6.hip)
 B6_L3 = os.environ.get("HREG_B6_L3", "1") != "0"
+# the big plain GEMMs (CoarseReg convs_1 layers 2-3, 512 -> 512 over B*256*8 rows) on
+# hreg_gemm6 (bf16x6 products)
+B6_GEMM = os.environ.get("HREG_B6_GEMM", "1") != "0"
 # the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
 # precomputed-block form, HEAD_PRE)
 B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
@@ -489,9 +492,10 @@ def _seg(base, k0, kc, ld=None, gather=None, rowscale=None, row_div=1, batch_str
     return s
 
 
-def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=()):
+def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=(), b6=False):
     """out[R][N] = act(alpha * (A @ W^T + sum(adds)) + beta), A assembled from segs;
-    adds: up to 2 row sources (_seg with row_div or gather) of [*, N] addends."""
+    adds: up to 2 row sources (_seg with row_div or gather) of [*, N] addends;
+    b6: on hreg_gemm6 (bf16x6 products) when B6_GEMM (no addends)."""
     if out is None:
         out = torch.empty((R, lin.N), device=lin.W.device, dtype=torch.float32)
     g = Gemm()
@@ -513,7 +517,10 @@ def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=()):
     g.out = out.data_ptr()
     g.ldo = out.shape[-1]
     g.out_batch_stride = 0
-    _lib.gemm(g)
+    if b6 and B6_GEMM and not adds:
+        _lib.gemm6(g)
+    else:
+        _lib.gemm(g)
     return out
 
 
@@ -927,8 +934,8 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
         segs = [_seg(small, 0, 16), _seg(s_desc, 16, C, row_div=k),
                 _seg(d_desc, 16 + C, C, gather=gidx)]
         f = gemm(segs, P.coarse_convs1[0], R)
-    f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[1], R)
-    f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[2], R)
+    f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[1], R, b6=True)
+    f = gemm([_seg(f, 0, f.shape[1])], P.coarse_convs1[2], R, b6=True)
     _, att, corres = attend(f, B * N1, k, vals=f, xyz_rows=kx)
     w = _mlp_weights(P, "coarse", att, B, N1)
     return corres.view(B, N1, 3), w.view(B, N1)

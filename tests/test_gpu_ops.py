@@ -177,10 +177,14 @@ def test_knn_gather_and_grad():
     (3000, 128, [(128, "div"), (128, "plain"), (256, "scale")]),
     (2048, 512, [(16, "plain"), (256, "div"), (256, "gather")]),
     (777, 96, [(12, "plain"), (64, "gather")]),
+    (16384, 512, [(512, "plain")]),
+    (1000, 200, [(36, "plain"), (100, "gather")]),
 ])
-def test_gemm_segments_vs_torch_fp32(R, N, segs):
-    """fp32 MFMA GEMM with gathered/repeated/scaled segments vs torch fp32 on CPU.
-    Tolerance: 1e-5 relative to sum|a*w| (fp32 accumulation-order differences)."""
+@pytest.mark.parametrize("b6", [False, True])
+def test_gemm_segments_vs_torch_fp32(R, N, segs, b6):
+    """fp32 MFMA GEMM (b6: hreg_gemm6, bf16x6 products on the bf16 matrix cores) with
+    gathered/repeated/scaled segments vs torch fp32 on CPU.  Tolerance: 1e-5 relative to
+    sum|a*w| (fp32 accumulation-order differences) for both."""
     from pcd_reg_hregnet_amd import engine
     rng = np.random.default_rng(R + N)
     K = sum(c for c, _ in segs)
@@ -216,7 +220,7 @@ def test_gemm_segments_vs_torch_fp32(R, N, segs):
             dsegs.append(engine._seg(t, k0, c, rowscale=ts))
         k0 += c
     A = np.concatenate(parts, 1)
-    out = engine.gemm(dsegs, lin, R).cpu().numpy()
+    out = engine.gemm(dsegs, lin, R, b6=b6).cpu().numpy()
     ref = torch.from_numpy(A) @ torch.from_numpy(W).T
     ref = torch.relu(ref * torch.from_numpy(alpha) + torch.from_numpy(beta)).numpy()
     scale = (np.abs(A) @ np.abs(W).T) * alpha + np.abs(beta)
