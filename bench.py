@@ -152,6 +152,7 @@ MFMA_ENTRIES = {
     "hreg_fine_head6": ("head", _fine6_work),
     "hreg_nbr_head6": ("head", _nbr_work),
     "hreg_mlp_head": ("mlp", _mlp_work),
+    "hreg_mlp_head6": ("mlp", _mlp_work),
 }
 
 

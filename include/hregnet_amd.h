@@ -202,6 +202,13 @@ int hreg_mlp_head_table_floats(int C);
 int hreg_mlp_head(const float *table, int C, const float *x, int ldx, int nclouds,
                   int rows_per_cloud, int mode, float *out, float *weights_out, void *stream);
 
+/* hreg_mlp_head with fp32-accurate products on the bf16 matrix cores (bf16x6,
+ * mlp_head.hip): same arguments and outputs, table = hreg_mlp_head6_table_floats(C)
+ * floats (engine.mlp_head_table6), 16-byte aligned. */
+int hreg_mlp_head6_table_floats(int C);
+int hreg_mlp_head6(const float *table, int C, const float *x, int ldx, int nclouds,
+                   int rows_per_cloud, int mode, float *out, float *weights_out, void *stream);
+
 /* ---- data side in front of the path (perturb.hip) ----
  * Twists x = (w, v) [n][6], SE(3) matrices g [n][16] row-major. */
 /* g = SE3.exp(x) (transform/rodrigues.py:526-553) */

@@ -93,6 +93,8 @@ _SIGS = {
     "hreg_head6_table_floats": [_i],
     "hreg_mlp_head": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "hreg_mlp_head_table_floats": [_i],
+    "hreg_mlp_head6": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
+    "hreg_mlp_head6_table_floats": [_i],
     "hreg_sigma_weights": [_vp, _i, _i, _vp, _vp],
     "hreg_se3_exp": [_vp, _i, _vp, _vp],
     "hreg_se3_log": [_vp, _i, _vp, _vp],

@@ -12,7 +12,8 @@
 // workgroup owns a 32-row tile: the rows are staged into LDS, CW waves split each
 // layer's output channels (P <= 2 tiles of 32 per wave, split_chain.h), y1 goes
 // back through the same LDS buffer, y2 stays in registers and the mlp3 dot is
-// reduced lane half -> waves in a fixed order.  BN is folded (eval) into the
+// reduced lane half -> waves in a fixed order.  hreg_mlp_head6: the same with bf16x6
+// products (fp32-accurate, bf16 matrix cores).  BN is folded (eval) into the
 // per-channel alpha/beta epilogue, as everywhere else (engine._bn_fold).
 #include "split_chain.h"
 
@@ -30,8 +31,14 @@ struct HCfg {
     static constexpr int T = C / 32, P = T / CW, NS = T * 16;
     static_assert(P * CW == T && P >= 1 && P <= 2, "channel split");
     static constexpr int F_M1 = 0, F_M2 = T * NS * 64, F_END = 2 * F_M2;
-    static constexpr int E_M1 = F_END, E_M2 = E_M1 + 2 * C, E_W3 = E_M2 + 2 * C, E_B3 = E_W3 + C;
-    static constexpr int TABLE = E_B3 + 4;
+    // epilogue section (offsets from its start): alpha1, beta1, alpha2, beta2, w3, b3 (+3)
+    static constexpr int R_M1 = 0, R_M2 = 2 * C, R_W3 = 4 * C, R_B3 = 5 * C, NE = 5 * C + 4;
+    static constexpr int E_M1 = F_END + R_M1, E_M2 = F_END + R_M2, E_W3 = F_END + R_W3, E_B3 = F_END + R_B3;
+    static constexpr int TABLE = F_END + NE;
+    // bf16x6 table (engine.mlp_head_table6): mlp1, mlp2 as bf16 piece chunk fragments
+    // [tile][chunk] (units of 3 pieces x 64 lanes x 16 B), then the same epilogue section
+    static constexpr int NCH = 2 * T, G_M1 = 0, G_M2 = T * NCH;
+    static constexpr int F_END6 = 2 * T * NCH * 3 * 64 * 4, TABLE6 = F_END6 + NE;
     static constexpr int LDSW = C + 4;
     static constexpr int THREADS = CW * RT * 64;
 };
@@ -41,17 +48,20 @@ using H128 = HCfg<128, 4, 1>;
 using H256 = HCfg<256, 4, 1>;
 using H512 = HCfg<512, 8, 1, 8>;  // 2 waves per SIMD: 128 VGPRs + AGPRs, short windows
 
-template <class K>
+// B6: the two layers on the bf16 matrix cores at fp32 accuracy (bf16x6, split_chain.h
+// pipe_lds6: each wave splits the B chunks it reads from LDS into bf16 pieces)
+template <class K, bool B6>
 __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__restrict__ table,
                                                               const float *__restrict__ x, int ldx,
                                                               int G, int mode, float *__restrict__ out) {
     constexpr int C = K::C, P = K::P, CW = K::CW, RT = K::RT, LDSW = K::LDSW, NS = K::NS;
-    constexpr int NE = K::TABLE - K::F_END, WIN = NS < K::WMAX ? NS : K::WMAX;
+    constexpr int NE = K::NE, WIN = NS < K::WMAX ? NS : K::WMAX;
+    constexpr int FE = B6 ? K::F_END6 : K::F_END;
     __shared__ float ep[NE];
     __shared__ __attribute__((aligned(16))) float sA[RT][32 * LDSW];
     __shared__ float sPart[RT][CW][32];
-    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
-    const float *eb = ep - K::F_END;
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[FE + i];
+    const float *eb = ep;
     // the wave index is uniform: in SGPRs, every fragment address is an SGPR base plus
     // the lane's offset (not a hoisted per-load 64-bit VGPR address)
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -61,9 +71,15 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
     float *A = sA[rt];
     const int c0 = cw * P;
     const FragSeq f1{K::F_M1 / 64 + c0 * NS, NS}, f2{K::F_M2 / 64 + c0 * NS, NS};
+    const FragSeq g1{K::G_M1 + c0 * K::NCH, K::NCH}, g2{K::G_M2 + c0 * K::NCH, K::NCH};
 
     float carry[SCARRY];
-    {
+    Carry6 carry6;
+    if constexpr (B6) {
+        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table));
+#pragma unroll
+        for (int i = 0; i < P; ++i) ld6(wt, g1.base + i * g1.stride, lane, carry6[i]);
+    } else {
         const gfloat *tb = reinterpret_cast<const gfloat *>(reinterpret_cast<uint64_t>(table));
 #pragma unroll
         for (int s0 = 0; s0 < WIN; s0 += 4)
@@ -82,7 +98,9 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
+        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
         float ca[SCARRY];
+        Carry6 ca6;
 
         tile_sync();  // the previous tile's readers of A are done (and ep is loaded)
         constexpr int F4 = C / 4;
@@ -96,8 +114,11 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
 
         f32x16 y1[P];
         zero_tiles(y1);
-        pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f1, ChanB{A + j * LDSW, h}, y1, carry, f2, ca);
-        epi<P, C>(eb + K::E_M1, c0, h, y1);
+        if constexpr (B6)
+            pipe_lds6<K::NCH, P, P>(wt, lane, g1, ChanB{A + j * LDSW, h}, y1, carry6, g2, ca6);
+        else
+            pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f1, ChanB{A + j * LDSW, h}, y1, carry, f2, ca);
+        epi<P, C>(eb + K::R_M1, c0, h, y1);
         tile_sync();  // every wave has read x from A
 #pragma unroll
         for (int i = 0; i < P; ++i) put_tile<LDSW>(A, c0 + i, j, h, y1[i]);
@@ -105,15 +126,18 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
 
         f32x16 y2[P];
         zero_tiles(y2);
-        pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f2, ChanB{A + j * LDSW, h}, y2, ca, f1, carry);
-        epi<P, C>(eb + K::E_M2, c0, h, y2);
+        if constexpr (B6)
+            pipe_lds6<K::NCH, P, P>(wt, lane, g2, ChanB{A + j * LDSW, h}, y2, ca6, g1, carry6);
+        else
+            pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f2, ChanB{A + j * LDSW, h}, y2, ca, f1, carry);
+        epi<P, C>(eb + K::R_M2, c0, h, y2);
 
         // mlp3: this wave's channels, then the two lane halves, then the waves in order
         float p = 0.f;
 #pragma unroll
         for (int i = 0; i < P; ++i)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) p = fadd_rn(p, fmul_rn(y2[i][q], eb[K::E_W3 + chan(c0 + i, q, h)]));
+            for (int q = 0; q < 16; ++q) p = fadd_rn(p, fmul_rn(y2[i][q], eb[K::R_W3 + chan(c0 + i, q, h)]));
         p = fadd_rn(p, __shfl_xor(p, 32));  // commutative: both halves hold the same bits
         if (h == 0) sPart[rt][cw][j] = p;
         tile_sync();
@@ -121,7 +145,7 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
             float z = sPart[rt][0][j];
 #pragma unroll
             for (int c = 1; c < CW; ++c) z = fadd_rn(z, sPart[rt][c][j]);
-            z = fadd_rn(z, eb[K::E_B3]);
+            z = fadd_rn(z, eb[K::R_B3]);
             float o;
             if (mode == HREG_HEAD_SOFTPLUS) {
                 const float sp = z > 20.f ? z : log1pf(expf(z));
@@ -134,13 +158,14 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
     }
 }
 
-template <class K>
+template <class K, bool B6>
 int launch_head(const float *table, const float *x, int ldx, int G, int mode, float *out, void *stream) {
     const int NT = G / 32;
     int grid = (NT + K::RT - 1) / K::RT;
     if (grid > 2048) grid = 2048;
-    hipLaunchKernelGGL(mlp_head_kernel<K>, dim3(grid), dim3(K::THREADS), 0, as_stream(stream), table, x,
-                       ldx, G, mode, out);
+    if (B6 && (reinterpret_cast<uintptr_t>(table) & 15)) return HREG_ERR_INVALID;
+    hipLaunchKernelGGL((mlp_head_kernel<K, B6>), dim3(grid), dim3(K::THREADS), 0, as_stream(stream), table,
+                       x, ldx, G, mode, out);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -157,8 +182,19 @@ extern "C" int hreg_mlp_head_table_floats(int C) {
     }
 }
 
-extern "C" int hreg_mlp_head(const float *table, int C, const float *x, int ldx, int nclouds,
-                             int rows_per_cloud, int mode, float *out, float *weights_out, void *stream) {
+extern "C" int hreg_mlp_head6_table_floats(int C) {
+    switch (C) {
+        case 64: return H64::TABLE6;
+        case 128: return H128::TABLE6;
+        case 256: return H256::TABLE6;
+        case 512: return H512::TABLE6;
+        default: return -1;
+    }
+}
+
+template <bool B6>
+static int mlp_head_entry(const float *table, int C, const float *x, int ldx, int nclouds, int rows_per_cloud,
+                          int mode, float *out, float *weights_out, void *stream) {
     if (!table || !x || !out || nclouds < 0 || rows_per_cloud <= 0 || ldx < C || (ldx & 3) ||
         (mode != HREG_HEAD_SOFTPLUS && mode != HREG_HEAD_SIGMOID))
         return HREG_ERR_INVALID;
@@ -169,11 +205,21 @@ extern "C" int hreg_mlp_head(const float *table, int C, const float *x, int ldx,
     if (!G) return HREG_OK;
     int rc;
     switch (C) {
-        case 64: rc = launch_head<H64>(table, x, ldx, G, mode, out, stream); break;
-        case 128: rc = launch_head<H128>(table, x, ldx, G, mode, out, stream); break;
-        case 256: rc = launch_head<H256>(table, x, ldx, G, mode, out, stream); break;
-        default: rc = launch_head<H512>(table, x, ldx, G, mode, out, stream); break;
+        case 64: rc = launch_head<H64, B6>(table, x, ldx, G, mode, out, stream); break;
+        case 128: rc = launch_head<H128, B6>(table, x, ldx, G, mode, out, stream); break;
+        case 256: rc = launch_head<H256, B6>(table, x, ldx, G, mode, out, stream); break;
+        default: rc = launch_head<H512, B6>(table, x, ldx, G, mode, out, stream); break;
     }
     if (rc != HREG_OK || !weights_out) return rc;
     return hreg_sigma_weights(out, nclouds, rows_per_cloud, weights_out, stream);
+}
+
+extern "C" int hreg_mlp_head(const float *table, int C, const float *x, int ldx, int nclouds,
+                             int rows_per_cloud, int mode, float *out, float *weights_out, void *stream) {
+    return mlp_head_entry<false>(table, C, x, ldx, nclouds, rows_per_cloud, mode, out, weights_out, stream);
+}
+
+extern "C" int hreg_mlp_head6(const float *table, int C, const float *x, int ldx, int nclouds,
+                              int rows_per_cloud, int mode, float *out, float *weights_out, void *stream) {
+    return mlp_head_entry<true>(table, C, x, ldx, nclouds, rows_per_cloud, mode, out, weights_out, stream);
 }

@@ -52,6 +52,7 @@ B6_L3 = os.environ.get("HREG_B6_L3", "1") != "0"
 # the big plain GEMMs (CoarseReg convs_1 layers 2-3, 512 -> 512 over B*256*8 rows) on
 # hreg_gemm6 (bf16x6 products)
 B6_GEMM = os.environ.get("HREG_B6_GEMM", "1") != "0"
+B6_MLP = os.environ.get("HREG_B6_MLP", "1") != "0"  # mlp heads on hreg_mlp_head6
 # the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
 # precomputed-block form, HEAD_PRE)
 B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
@@ -202,12 +203,15 @@ class PreparedWeights:
         self.head_table["coarse"] = mlp_head_table(self.coarse_head)
         for name in ("fine_corres_2", "fine_corres_1"):
             self.head_table[name] = mlp_head_table(self.fine[name][1])
+        self.head_table6 = {k: mlp_head_table6(h) for k, h in (
+            [(("det", lvl), self.det_head[lvl]) for lvl in range(3)] + [("coarse", self.coarse_head)] +
+            [(n, self.fine[n][1]) for n in ("fine_corres_2", "fine_corres_1")])}
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
                      "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre",
                      "coarse_head", "fine", "l1_table", "l1_table6", "l2_table", "l3_table", "l2_table6",
                      "l3_table6", "l2s_table", "l2s_table6", "l3s_table6",
                      "l3s_table", "fine_table", "fine_table6", "nbr_table6",
-                     "nbr_table", "head_table", "mlpx"):
+                     "nbr_table", "head_table", "head_table6", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
 
@@ -338,6 +342,16 @@ def mlp_head_table(head) -> torch.Tensor:
     m1, m2, w3, b3 = head
     parts = [_group4(frag_layer(m1.W), 4), _group4(frag_layer(m2.W), 4), m1.alpha, m1.beta,
              m2.alpha, m2.beta, w3, b3, torch.zeros(3)]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def mlp_head_table6(head) -> torch.Tensor:
+    """Table of hreg_mlp_head6 (HCfg TABLE6): mlp1 and mlp2 as bf16 piece chunk fragments
+    (frag6), then mlp_head_table's epilogue section."""
+    m1, m2, w3, b3 = head
+    T = m1.W.shape[0] // 32
+    parts = [frag6(frag_layer(m1.W), T, T * 16), frag6(frag_layer(m2.W), T, T * 16), m1.alpha,
+             m1.beta, m2.alpha, m2.beta, w3, b3, torch.zeros(3)]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
 
 
@@ -859,8 +873,12 @@ def mlp_head(P: PreparedWeights, key, x, nclouds, rows, mode, want_weights=False
         dev = x.device
         out = _empty(nclouds * rows, device=dev)
         wout = _empty(nclouds * rows, device=dev) if want_weights else None
-        call("hreg_mlp_head", P.head_table[key], C, x, C, nclouds, rows, mode, out, wout,
-             _stream())
+        if B6_MLP:
+            call("hreg_mlp_head6", P.head_table6[key], C, x, C, nclouds, rows, mode, out, wout,
+                 _stream())
+        else:
+            call("hreg_mlp_head", P.head_table[key], C, x, C, nclouds, rows, mode, out, wout,
+                 _stream())
         return out, wout
     m1, m2, w3, b3 = _head_layers(P, key)
     G = nclouds * rows

@@ -343,11 +343,13 @@ def test_fused_nbr_head_matches_layerwise(net, pre, b6, monkeypatch):
                                            (("det", 2), 256, 256, 0), ("coarse", 512, 256, 1),
                                            ("fine_corres_2", 256, 512, 1),
                                            ("fine_corres_1", 128, 1024, 1)])
-def test_fused_mlp_head_matches_layerwise(net, key, C, rows, mode):
-    """mlp_head.hip (mlp1 -> mlp2 -> mlp3 + softplus/sigmoid in one launch) against two
-    GEMMs + hreg_head_out; fp32 summation order differs, so within 1e-4 (and the
-    per-cloud sigma -> weight normalisation, models.py:30-32)."""
+@pytest.mark.parametrize("b6", [False, True])
+def test_fused_mlp_head_matches_layerwise(net, key, C, rows, mode, b6, monkeypatch):
+    """mlp_head.hip (mlp1 -> mlp2 -> mlp3 + softplus/sigmoid in one launch; b6: bf16x6
+    products) against two GEMMs + hreg_head_out; fp32 summation order differs, so within
+    1e-4 (and the per-cloud sigma -> weight normalisation, models.py:30-32)."""
     from pcd_reg_hregnet_amd import _lib, engine
+    monkeypatch.setattr(engine, "B6_MLP", b6)
     P = net.prepared(torch.device("cuda"))
     g = torch.Generator().manual_seed(7)
     nclouds = 3

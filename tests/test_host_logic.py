@@ -249,6 +249,15 @@ def test_split_tables6_match_kernel(P):
     assert prep.l3s_table6.numel() == L.hreg_group_split6_l3_table_floats()
 
 
+def test_mlp_head_tables6_match_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    sizes = {C: L.hreg_mlp_head6_table_floats(C) for C in (64, 128, 256, 512)}
+    assert sorted(t.numel() for t in prep.head_table6.values()) == sorted(
+        [sizes[64], sizes[128], sizes[256], sizes[512], sizes[256], sizes[128]])
+
+
 def test_l1_table6_matches_kernel(P):
     _, prep = P
     from pcd_reg_hregnet_amd import _lib
