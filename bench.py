@@ -118,6 +118,14 @@ def _fine6_work(args):
             2.0 * 8 * G * (12 * N1 + 2 * N1 * N1))
 
 
+def _coarse6_work(args):
+    """hreg_coarse_head6 (table, small, ud0, ud1, gidx, knn_xyz, G, ...): convs_1 over 8 G
+    rows, 528 -> 512 -> 512 -> 512 (executed: the 16 small columns of the first layer)"""
+    G = args[6]
+    return (2.0 * 8 * G * (528 * 512 + 2 * 512 * 512), 4.0 * G * (8 * (16 + 512 + 3) + 512 + 512 + 3),
+            2.0 * 8 * G * (16 * 512 + 2 * 512 * 512))
+
+
 def _nbr_work(args):
     G = args[4]
     kx = 4 if args[6] is not None else 260  # HEAD_PRE: geometry columns only
@@ -151,6 +159,7 @@ MFMA_ENTRIES = {
     "hreg_nbr_head": ("head", _nbr_work),
     "hreg_fine_head6": ("head", _fine6_work),
     "hreg_nbr_head6": ("head", _nbr_work),
+    "hreg_coarse_head6": ("head", _coarse6_work),
     "hreg_mlp_head": ("mlp", _mlp_work),
     "hreg_mlp_head6": ("mlp", _mlp_work),
 }

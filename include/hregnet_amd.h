@@ -552,6 +552,17 @@ int hreg_nbr_head(const float *table, const float *desc, const int32_t *gidx, co
  * same outputs.  table = hreg_head6_table_floats(N1) floats, N1 = 2C for FineReg and
  * 256 for the neighbour branch (engine.head_table6: bf16 piece fragments of the narrow
  * first block, conv 2 and conv 3, then the f32 epilogues), 16-byte aligned. */
+/* CoarseReg convs_1 + attention in one launch (coarse6.hip, bf16x6 products;
+ * layers.py:364-390): G keypoints x 8 rows; small [G*8][16] packed small columns
+ * (hreg_pair_feats), ud0 [G][512] = W_desc desc_src (per keypoint), ud1 [*][512] = W_knn_desc
+ * desc_dst gathered by gidx [G*8], knn_xyz [G*8][3] -> corres [G][3], att [G][512] (the
+ * attentive feature).  table = hreg_coarse_head6_table_floats() floats
+ * (engine.coarse_head_table6), 16-byte aligned. */
+int hreg_coarse_head6_table_floats(void);
+int hreg_coarse_head6(const float *table, const float *small, const float *ud0, const float *ud1,
+                      const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                      void *stream);
+
 int hreg_head6_table_floats(int N1);
 int hreg_fine_head6(const float *table, int C, const float *small, const int32_t *gidx,
                     const float *knn_xyz, int G, float *corres, float *att, const float *pre_src,

@@ -91,6 +91,7 @@ _SIGS = {
     "hreg_fine_head6": [_vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_nbr_head6": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_head6_table_floats": [_i],
+    "hreg_coarse_head6": [_vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_mlp_head": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "hreg_mlp_head_table_floats": [_i],
     "hreg_mlp_head6": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
@@ -153,7 +154,8 @@ EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_
                           "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
                           "hreg_group_split_l3_table_floats", "hreg_group6_l2_table_floats",
                           "hreg_group6_l3_table_floats", "hreg_group_l1_6_table_floats",
-                          "hreg_group_split6_l2_table_floats", "hreg_group_split6_l3_table_floats")
+                          "hreg_group_split6_l2_table_floats", "hreg_group_split6_l3_table_floats",
+                          "hreg_coarse_head6_table_floats")
 
 _lib = None
 
@@ -188,7 +190,7 @@ def load(require_gpu: bool = True):
                      "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats",
                      "hreg_group6_l2_table_floats", "hreg_group6_l3_table_floats",
                      "hreg_group_l1_6_table_floats", "hreg_group_split6_l2_table_floats",
-                     "hreg_group_split6_l3_table_floats"):
+                     "hreg_group_split6_l3_table_floats", "hreg_coarse_head6_table_floats"):
             getattr(L, name).restype = ctypes.c_int
             getattr(L, name).argtypes = []
         _lib = L

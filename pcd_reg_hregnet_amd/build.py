@@ -34,7 +34,8 @@ CFLAGS = [
 # compile ignores the feature (a warning).
 NO_PACKED_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 FILE_FLAGS = {f: NO_PACKED_F32 for f in ("group_l1_6.hip", "group_fused6.hip", "group_head.hip",
-                                       "group_split6.hip", "gemm.hip", "mlp_head.hip")}
+                                       "group_split6.hip", "gemm.hip", "mlp_head.hip",
+                                       "coarse6.hip")}
 
 
 def _needs(obj: str, deps: list[str]) -> bool:

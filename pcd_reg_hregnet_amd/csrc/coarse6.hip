@@ -1,0 +1,157 @@
+// coarse6.hip -- CoarseReg correspondence features in one launch (layers.py:364-390):
+// convs_1 (3 x [1x1 Conv2d + BN + ReLU], 528 -> 512 -> 512 -> 512) over the rows of
+// every keypoint's 8 descriptor-space neighbours, then the attention of layers.py:384-390
+// (a = softmax over the 8 rows of max over channels; corres = sum_j a_j knn_xyz_j; the
+// attentive feature sum_j a_j f_j), with the products on the bf16 matrix cores at fp32
+// accuracy (bf16x6, mfma_chain.h).
+//
+// convs_1[0] runs in its split form (engine.COARSE_SPLIT): the desc / knn_desc blocks of
+// the 528-wide row are the same for the 8 rows of a keypoint / for every row gathering a
+// destination keypoint, so their products ud0[g] = W_d desc_src[g], ud1[n] = W_kd
+// desc_dst[n] are made once per keypoint (one batch-2 GEMM) and initialise the
+// accumulators; only the 16 small columns [dxyz, |d|, xyz, knn_xyz, w, knn_w, sims 4]
+// run here (one 16-deep chunk).
+//
+// Decomposition (split_chain.h, as mlp_head.hip): a workgroup of 8 waves owns a 32-row
+// tile (4 keypoints); each wave computes P = 2 output tiles (64 channels) of every layer;
+// a layer's output goes through one LDS buffer (32 x 512 f32, row-major) to the next
+// layer's B operand, which each wave splits into bf16 pieces as it reads it.  Weight
+// pieces stream from the L2-resident table (engine.coarse_head_table6) one chunk ahead.
+// The channel max of the attention is reduced per wave, then across the 8 waves through
+// LDS; the reductions over a keypoint's 8 rows are 3 DPP steps.
+#include "split_chain.h"
+
+namespace {
+
+using namespace hreg_chain;
+using namespace hreg_split;
+
+constexpr int C = 512, T = C / 32, CW = 8, P = T / CW, KH = 8, LDSW = C + 4;
+constexpr int NCH = T * 2;  // 16-deep chunks over 512 inputs
+// chunk-fragment table (units of 3 pieces x 64 lanes x 16 B), engine.coarse_head_table6
+constexpr int G_1 = 0;               // convs_1[0], the 16 small columns: [T][1]
+constexpr int G_2 = G_1 + T;         // convs_1[1]: [T][NCH]
+constexpr int G_3 = G_2 + T * NCH;   // convs_1[2]: [T][NCH]
+constexpr int G_END = G_3 + T * NCH;
+constexpr int F_END = G_END * 3 * 64 * 4;
+constexpr int NE = 6 * C;            // alpha, beta of the three layers
+constexpr int TABLE = F_END + NE;
+
+__global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
+    const float *__restrict__ table, const float *__restrict__ small, const float *__restrict__ ud0,
+    const float *__restrict__ ud1, const int32_t *__restrict__ gidx, const float *__restrict__ knn_xyz, int G,
+    float *__restrict__ corres, float *__restrict__ att) {
+    __shared__ float ep[NE];
+    __shared__ __attribute__((aligned(16))) float sA[32 * LDSW];
+    __shared__ int sMax[CW][32];
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[F_END + i];
+    __syncthreads();  // the first tile's layer-1 epilogue reads ep before any tile_sync
+    const int lane = threadIdx.x & 63, cw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, j = lane & 31;
+    const int NT = G * KH / 32;
+    const int c0 = cw * P;
+    const FragSeq g1{G_1 + c0, 1}, g2{G_2 + c0 * NCH, NCH}, g3{G_3 + c0 * NCH, NCH};
+    const bool writer = (j & 7) == 7;
+
+    Carry6 carry;
+    {
+        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table));
+#pragma unroll
+        for (int i = 0; i < P; ++i) ld6(wt, g1.base + i, lane, carry[i]);
+    }
+    for (int t = blockIdx.x; t < NT; t += gridDim.x) {
+        uint64_t tba = reinterpret_cast<uint64_t>(table);
+        asm volatile("" : "+s"(tba));
+        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
+        const int row = t * 32 + j, g = row / KH;
+        Carry6 ca, cb;
+
+        // ---- convs_1[0]: precomputed desc / knn_desc products + the 16 small columns
+        // (k-step s of lane half h <-> column 8h + s: one chunk)
+        f32x16 y[P];
+        init_from_rows<C, P>(y, ud0 + (size_t)g * C + c0 * 32, ud1 + (size_t)gidx[row] * C + c0 * 32, h);
+        {
+            const float4 s0 = *reinterpret_cast<const float4 *>(small + (size_t)row * 16 + h * 8);
+            const float4 s1 = *reinterpret_cast<const float4 *>(small + (size_t)row * 16 + h * 8 + 4);
+            const float sm[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            mfma_pipe6<1, P, P>(wt, lane, g1, [&](int st) { return sm[st]; }, y, carry, g2, ca);
+        }
+        epi<P, C>(ep, c0, h, y);
+        tile_sync();  // the previous tile's readers of sA are done
+#pragma unroll
+        for (int i = 0; i < P; ++i) put_tile<LDSW>(sA, c0 + i, j, h, y[i]);
+        tile_sync();
+
+        // ---- convs_1[1]
+        zero_tiles(y);
+        pipe_lds6<NCH, P, P>(wt, lane, g2, ChanB{sA + j * LDSW, h}, y, ca, g3, cb);
+        epi<P, C>(ep + 2 * C, c0, h, y);
+        tile_sync();  // every wave has read the layer input
+#pragma unroll
+        for (int i = 0; i < P; ++i) put_tile<LDSW>(sA, c0 + i, j, h, y[i]);
+        tile_sync();
+
+        // ---- convs_1[2]; prefetches the next tile's first chunk
+        zero_tiles(y);
+        pipe_lds6<NCH, P, P>(wt, lane, g3, ChanB{sA + j * LDSW, h}, y, cb, g1, carry);
+        epi<P, C>(ep + 4 * C, c0, h, y);
+
+        // ---- attention: row max over the 512 channels (ReLU outputs: integer max on the
+        // bit patterns; per wave, then across the waves through LDS), softmax over the 8 rows
+        int mi = __float_as_int(y[0][0]);
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(y[i][q]));
+        mi = max(mi, __shfl_xor(mi, 32));
+        if (h == 0) sMax[cw][j] = mi;
+        tile_sync();
+        int xm = sMax[0][j];
+#pragma unroll
+        for (int c = 1; c < CW; ++c) xm = max(xm, sMax[c][j]);
+        const float x1 = __int_as_float(xm);
+        const float e = expf(fsub_rn(x1, grp8_max_nonneg(x1)));
+        const float a = e / grp8_sum(e);
+        if (cw == 0) {
+            const float *p = knn_xyz + (size_t)row * 3;
+            const float cx = grp8_sum(fmul_rn(a, p[0]));
+            const float cy = grp8_sum(fmul_rn(a, p[1]));
+            const float cz = grp8_sum(fmul_rn(a, p[2]));
+            if (writer && h == 0) {
+                corres[(size_t)g * 3 + 0] = cx;
+                corres[(size_t)g * 3 + 1] = cy;
+                corres[(size_t)g * 3 + 2] = cz;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            f32x16 v;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = grp8_sum(fmul_rn(y[i][q], a));
+            store_tile(att + (size_t)g * C, c0 + i, v, writer, h);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int hreg_coarse_head6_table_floats(void) { return TABLE; }
+
+extern "C" int hreg_coarse_head6(const float *table, const float *small, const float *ud0, const float *ud1,
+                                 const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                                 void *stream) {
+    if (!table || !small || !ud0 || !ud1 || !gidx || !knn_xyz || !corres || !att || G < 0)
+        return HREG_ERR_INVALID;
+    if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(small) & 15) ||
+        (reinterpret_cast<uintptr_t>(ud0) & 15) || (reinterpret_cast<uintptr_t>(ud1) & 15) ||
+        (reinterpret_cast<uintptr_t>(att) & 15))
+        return HREG_ERR_INVALID;
+    if ((G * KH) % 32) return HREG_ERR_INVALID;  // whole 32-row tiles
+    if (!G) return HREG_OK;
+    const int NT = G * KH / 32;
+    int grid = NT < 1024 ? NT : 1024;  // two resident workgroups per CU, two rounds
+    hipLaunchKernelGGL(coarse_head6_kernel, dim3(grid), dim3(CW * 64), 0, as_stream(stream), table, small, ud0,
+                       ud1, gidx, knn_xyz, G, corres, att);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}

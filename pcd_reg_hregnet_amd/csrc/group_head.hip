@@ -105,44 +105,6 @@ __device__ __forceinline__ void mfma_pipe_rows(const gfloat *__restrict__ wf, in
     }
 }
 
-// sum / max over the 8 rows of a keypoint (8-lane DPP groups), result in all 8 lanes
-__device__ __forceinline__ float grp8_sum(float v) {
-    v = fadd_rn(v, dpp_all<0xb1>(v));
-    v = fadd_rn(v, dpp_all<0x4e>(v));
-    return fadd_rn(v, dpp_all<0x141>(v));
-}
-__device__ __forceinline__ float grp8_max_nonneg(float f) {
-    int v = __float_as_int(f);
-    v = max(v, dpp_all_i<0xb1>(v));
-    v = max(v, dpp_all_i<0x4e>(v));
-    return __int_as_float(max(v, dpp_all_i<0x141>(v)));
-}
-
-// PRE: the descriptor blocks of the first layer come precomputed per point --
-// pre_src[g] = W_f f_src[g], pre_dst[n] = W_kf f_dst[n] ([*][N1], hreg_gemm) -- and
-// initialise the accumulators (lane j, register q <- channel chan(co, q, h) of its
-// row's two sources); only the 16 small columns run on the MFMA here.  Same sum up to
-// fp32 order, 2C k-steps per row fewer (the reference repeats / gathers the
-// descriptors into every row first, layers.py:444-445).
-template <int N1, int T1>
-__device__ __forceinline__ void init_from_rows(f32x16 (&acc)[T1], const float *__restrict__ u,
-                                               const float *__restrict__ v, int h) {
-#pragma unroll
-    for (int co = 0; co < T1; ++co)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int c = co * 32 + 8 * r + 4 * h;
-            const float4 a = *reinterpret_cast<const float4 *>(u + c);
-            if (v) {
-                const float4 b = *reinterpret_cast<const float4 *>(v + c);
-                acc[co][4 * r] = fadd_rn(a.x, b.x); acc[co][4 * r + 1] = fadd_rn(a.y, b.y);
-                acc[co][4 * r + 2] = fadd_rn(a.z, b.z); acc[co][4 * r + 3] = fadd_rn(a.w, b.w);
-            } else {
-                acc[co][4 * r] = a.x; acc[co][4 * r + 1] = a.y;
-                acc[co][4 * r + 2] = a.z; acc[co][4 * r + 3] = a.w;
-            }
-        }
-}
 
 // FineReg attention over the keypoint's 8 rows (f >= 0 after ReLU, layers.py:446-451):
 // corres = sum_j a_j p_j, attentive feature sum_j a_j f_j

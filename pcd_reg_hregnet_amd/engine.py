@@ -53,6 +53,8 @@ B6_L3 = os.environ.get("HREG_B6_L3", "1") != "0"
 # hreg_gemm6 (bf16x6 products)
 B6_GEMM = os.environ.get("HREG_B6_GEMM", "1") != "0"
 B6_MLP = os.environ.get("HREG_B6_MLP", "1") != "0"  # mlp heads on hreg_mlp_head6
+# CoarseReg convs_1 (split first layer) + attention in one launch (coarse6.hip, bf16x6)
+FUSED_COARSE = os.environ.get("HREG_FUSED_COARSE", "1") != "0"
 # the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
 # precomputed-block form, HEAD_PRE)
 B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
@@ -199,6 +201,7 @@ class PreparedWeights:
         self.fine_table6 = {name: fine_head_table6(self.fine[name][0])
                             for name in ("fine_corres_2", "fine_corres_1")}
         self.nbr_table6 = nbr_head_table6(self.coarse_convs2, 256)
+        self.coarse_table6 = coarse_head_table6(self.coarse_c1_small, self.coarse_convs1)
         self.head_table = {("det", lvl): mlp_head_table(self.det_head[lvl]) for lvl in range(3)}
         self.head_table["coarse"] = mlp_head_table(self.coarse_head)
         for name in ("fine_corres_2", "fine_corres_1"):
@@ -210,7 +213,7 @@ class PreparedWeights:
                      "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre",
                      "coarse_head", "fine", "l1_table", "l1_table6", "l2_table", "l3_table", "l2_table6",
                      "l3_table6", "l2s_table", "l2s_table6", "l3s_table6",
-                     "l3s_table", "fine_table", "fine_table6", "nbr_table6",
+                     "l3s_table", "fine_table", "fine_table6", "nbr_table6", "coarse_table6",
                      "nbr_table", "head_table", "head_table6", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
 
@@ -316,6 +319,18 @@ def _head_table6(first, T1: int, nfirst: int, convs) -> torch.Tensor:
     parts = [frag6(first, T1, nfirst), frag6(frag_layer(convs[1].W), T1, T1 * 16),
              frag6(frag_layer(convs[2].W), T1, T1 * 16)]
     for lin in convs:
+        parts += [lin.alpha, lin.beta]
+    return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
+
+
+def coarse_head_table6(small: Lin, convs) -> torch.Tensor:
+    """Table of coarse6.hip: convs_1[0]'s 16 small columns (frag_segment: k-step s of lane
+    half h <-> column 8h + s, one chunk), convs_1[1], convs_1[2] as bf16 piece chunk
+    fragments, then alpha/beta of the three layers (convs_1[0]'s from the split Lin)."""
+    T = small.W.shape[0] // 32
+    parts = [frag6(frag_segment(small.W, 0, 16), T, 8), frag6(frag_layer(convs[1].W), T, T * 16),
+             frag6(frag_layer(convs[2].W), T, T * 16)]
+    for lin in (small, convs[1], convs[2]):
         parts += [lin.alpha, lin.beta]
     return torch.cat([p.reshape(-1).float() for p in parts]).contiguous()
 
@@ -946,6 +961,14 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
         # per step at B=8 for this layer
         ud = _empty(2, B * N1, P.coarse_c1_desc.W.shape[1], device=dev)
         _gemm_batched_desc(P.coarse_c1_desc, desc3, B * N1, C, ud)
+        if FUSED_COARSE and C == 256:
+            # convs_1 + attention in one launch (coarse6.hip)
+            corres = _empty(B * N1, 3, device=dev)
+            att = _empty(B * N1, ud.shape[2], device=dev)
+            call("hreg_coarse_head6", P.coarse_table6, small, ud[0], ud[1], gidx, kx, B * N1,
+                 corres, att, _stream())
+            w = _mlp_weights(P, "coarse", att, B, N1)
+            return corres.view(B, N1, 3), w.view(B, N1)
         f = gemm([_seg(small, 0, 16)], P.coarse_c1_small, R,
                  adds=[_seg(ud[0], 0, 4, row_div=k), _seg(ud[1], 0, 4, gather=gidx)])
     else:

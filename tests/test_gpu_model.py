@@ -259,13 +259,15 @@ def test_fused_fine_head_matches_layerwise(net, name, C, N, pre, b6, monkeypatch
     torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("B,b6", [(1, False), (3, False), (3, True)])
-def test_coarse_split_matches_concat_gemm(net, B, b6, monkeypatch):
+@pytest.mark.parametrize("B,b6,fused", [(1, False, False), (3, False, False), (3, True, False),
+                                         (1, True, True), (3, True, True)])
+def test_coarse_split_matches_concat_gemm(net, B, b6, fused, monkeypatch):
     """CoarseReg convs_1[0] as the 16-column GEMM + per-keypoint desc / knn_desc products
     added in the epilogue vs the one 528-deep GEMM over the concatenated rows
     (layers.py:364-384).  Only the fp32 summation order differs: 1e-4 on corres/weights."""
     from pcd_reg_hregnet_amd import engine
     monkeypatch.setattr(engine, "B6_GEMM", b6)
+    monkeypatch.setattr(engine, "FUSED_COARSE", fused)
     P = net.prepared(torch.device("cuda"))
     g = torch.Generator().manual_seed(11 + B)
     N1, C = 256, 256

@@ -258,6 +258,13 @@ def test_mlp_head_tables6_match_kernel(P):
         [sizes[64], sizes[128], sizes[256], sizes[512], sizes[256], sizes[128]])
 
 
+def test_coarse_table6_matches_kernel(P):
+    _, prep = P
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load(require_gpu=False)
+    assert prep.coarse_table6.numel() == L.hreg_coarse_head6_table_floats()
+
+
 def test_l1_table6_matches_kernel(P):
     _, prep = P
     from pcd_reg_hregnet_amd import _lib
