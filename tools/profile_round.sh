@@ -16,6 +16,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_eager -o run -- python3 bench.py --executor pipeline --no-cpu-baseline > $O/trace_eager.log 2>&1
 if [ "$2" = "pmc" ]; then
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --executor pipeline > $O/fetch.log 2>&1
-  timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 GRBM_GUI_ACTIVE --output-format csv -d $O/mfma -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --executor pipeline > $O/mfma.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE --output-format csv -d $O/mfma -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --executor pipeline > $O/mfma.log 2>&1
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --executor pipeline > $O/write.log 2>&1
 fi

@@ -112,15 +112,17 @@ PEAK_F32_TFLOPS = 157.3
 
 def mfma(path, out=None, out_json=None):
     """Per-kernel MFMA counters of one --pmc pass (SQ_VALU_MFMA_BUSY_CYCLES,
-    SQ_INSTS_VALU_MFMA_MOPS_F32, GRBM_GUI_ACTIVE): MfmaUtil = busy / (GUI_ACTIVE of one
-    XCD x SIMDs) (rocprofv3's derived formula), FLOPs = MOPS_F32 x 512, TF/s over the
-    dispatch's own duration (counter passes serialise dispatches)."""
+    SQ_INSTS_VALU_MFMA_MOPS_F32, SQ_INSTS_VALU_MFMA_MOPS_BF16, GRBM_GUI_ACTIVE): MfmaUtil =
+    busy / (GUI_ACTIVE of one XCD x SIMDs) (rocprofv3's derived formula), FLOPs = MOPS x
+    512 per dtype, TF/s over the dispatch's own duration (counter passes serialise
+    dispatches).  bf16 MFMA FLOPs of the bf16x6 kernels are 6 x their fp32-equivalent
+    FLOPs."""
     per = defaultdict(dict)  # (kernel, dispatch) -> counter -> value, plus duration
     for r in csv.DictReader(open(path)):
         key = (short(r["Kernel_Name"]), r["Dispatch_Id"])
         per[key][r["Counter_Name"]] = float(r["Counter_Value"])
         per[key]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
-    agg = defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0.0])
+    agg = defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0.0, 0.0])
     for (name, _), c in per.items():
         if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
             continue
@@ -130,18 +132,22 @@ def mfma(path, out=None, out_json=None):
         a[2] += c["GRBM_GUI_ACTIVE"] / XCD_NUM * SIMD_NUM
         a[3] += c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) * 512
         a[4] += c["_ns"]
-    lines = ["| kernel | dispatches | MfmaUtil % | MFMA GFLOP/dispatch | TF/s (own duration) | "
-             "% of fp32 MFMA peak |", "|---|---|---|---|---|---|"]
+        a[5] += c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512
+    lines = ["| kernel | dispatches | MfmaUtil % | f32 MFMA GFLOP/dispatch | f32 TF/s (% of 157.3) | "
+             "bf16 MFMA GFLOP/dispatch | bf16 TF/s (% of 2500) |", "|---|---|---|---|---|---|---|"]
     res = {}
-    for name, (n, busy, active, flops, ns) in sorted(agg.items(), key=lambda kv: -kv[1][3]):
-        if flops <= 0:
+    for name, (n, busy, active, flops, ns, bflops) in sorted(agg.items(), key=lambda kv: -(kv[1][3] + kv[1][5])):
+        if flops <= 0 and bflops <= 0:
             continue
         util = 100.0 * busy / active if active else 0.0
         tf = flops / ns / 1e3 if ns else 0.0
-        res[name] = {"mfma_util_pct": round(util, 1), "gflop_per_dispatch": round(flops / n / 1e9, 3),
-                     "tflops": round(tf, 1)}
-        lines.append(f"| `{name[:80]}` | {n} | {util:.1f} | {flops / n / 1e9:.3f} | {tf:.1f} | "
-                     f"{100 * tf / PEAK_F32_TFLOPS:.1f} |")
+        btf = bflops / ns / 1e3 if ns else 0.0
+        res[name] = {"mfma_util_pct": round(util, 1), "f32_gflop_per_dispatch": round(flops / n / 1e9, 3),
+                     "f32_tflops": round(tf, 1), "bf16_gflop_per_dispatch": round(bflops / n / 1e9, 3),
+                     "bf16_tflops": round(btf, 1)}
+        lines.append(f"| `{name[:80]}` | {n} | {util:.1f} | {flops / n / 1e9:.3f} | {tf:.1f} "
+                     f"({100 * tf / PEAK_F32_TFLOPS:.1f} %) | {bflops / n / 1e9:.3f} | {btf:.1f} "
+                     f"({100 * btf / 2500.0:.1f} %) |")
     text = "\n".join(lines)
     print(text)
     if out:
@@ -149,7 +155,7 @@ def mfma(path, out=None, out_json=None):
     if out_json:
         json.dump({"kernels": res, "source": path,
                    "formula": "MfmaUtil = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs); "
-                              "FLOPs = SQ_INSTS_VALU_MFMA_MOPS_F32 * 512"}, open(out_json, "w"), indent=1)
+                              "FLOPs = SQ_INSTS_VALU_MFMA_MOPS_{F32,BF16} * 512"}, open(out_json, "w"), indent=1)
 
 
 if __name__ == "__main__":
