@@ -446,6 +446,11 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                 st_agent(&cur[p].w[0], ((uint64_t)__float_as_uint(wmax) << 32) |
                                            ((uint64_t)rank << 10) | (uint64_t)(j & 1023));
             }
+            // wait for the store acknowledgement before polling: the r1 code got this wait
+            // by accident of scheduling, and without it (the timeout rework of r2 let the
+            // compiler drop it) a call took 3.0-3.9 instead of 1.7 ms for 4 x 65536 points
+            // (Model_V2 bench 774 -> 617 pairs/s, tools/v2_bisect.sh)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
             // poll: lane q reads participant q's words until all carry tag j
             uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
