@@ -159,6 +159,11 @@ EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_
 
 _lib = None
 
+# Timing analysis only (never in a correctness run): C-ABI entries named in HREG_SKIP are
+# not launched, so a bench run measures the step without them (their outputs stay
+# uninitialised).  tools/skip_sweep.sh.
+SKIP = frozenset(filter(None, os.environ.get("HREG_SKIP", "").split(",")))
+
 
 def load(require_gpu: bool = True):
     """Load the library (and check a GPU is visible unless require_gpu=False)."""
@@ -213,6 +218,8 @@ def stream_handle() -> int:
 
 def call(name: str, *args) -> None:
     L = load()
+    if name in SKIP:
+        return
     conv = []
     for a in args:
         if isinstance(a, torch.Tensor):
@@ -236,6 +243,8 @@ def device_status(clear: bool = True) -> int:
 
 def gemm(g: Gemm) -> None:
     L = load()
+    if "hreg_gemm" in SKIP:
+        return
     rc = L.hreg_gemm(ctypes.byref(g), stream_handle())
     if rc != HREG_OK:
         raise RuntimeError(f"hreg_gemm failed: {_ERRORS.get(rc, rc)} (code {rc})")

@@ -158,7 +158,29 @@ def mfma(path, out=None, out_json=None):
                               "FLOPs = SQ_INSTS_VALU_MFMA_MOPS_{F32,BF16} * 512"}, open(out_json, "w"), indent=1)
 
 
+def counters(path, out=None):
+    """Per-kernel mean of every counter of a --pmc pass (one line per kernel family)."""
+    per = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        name = short(r["Kernel_Name"])[:70]
+        per[name][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[name].add(r["Dispatch_Id"])
+    names = sorted({c for v in per.values() for c in v})
+    lines = ["| kernel | dispatches | " + " | ".join(names) + " |", "|---" * (len(names) + 2) + "|"]
+    for k, v in sorted(per.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0.0)):
+        n = len(disp[k])
+        lines.append(f"| `{k}` | {n} | " + " | ".join(f"{v[c] / n:.4g}" for c in names) + " |")
+    text = "\n".join(lines)
+    print(text)
+    if out:
+        open(out, "w").write(text + "\n")
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "counters":
+        counters(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+        sys.exit(0)
     if sys.argv[1] == "mfma":
         mfma(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None,
              sys.argv[4] if len(sys.argv) > 4 else None)
