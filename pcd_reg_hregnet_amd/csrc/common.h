@@ -136,14 +136,20 @@ __device__ __forceinline__ float dpp_mov(float v, float old) {
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
                                                       ROW_MASK, 0xf, false));
 }
-// full-mask DPP move (every lane written): lets the compiler fold it into v_add_f32_dpp
+// full-mask DPP move within a 16-lane row (quad_perm / row_mirror / row_half_mirror: every
+// lane has a valid source, so bound_ctrl and the old value never matter).  Written as
+// update_dpp(old = 0, bound_ctrl = 1) the compiler folds it into the consuming
+// v_add_f32_dpp / v_max_i32_dpp (one instruction per reduction step instead of a
+// v_mov_b32_dpp + the op: the row reductions were ~30 % of the fused kernels' VALU)
 template <int CTRL>
 __device__ __forceinline__ float dpp_all(float v) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+    static_assert(CTRL <= 0xff || CTRL == 0x140 || CTRL == 0x141, "in-row controls only");
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
 }
 template <int CTRL>
 __device__ __forceinline__ int dpp_all_i(int v) {
-    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+    static_assert(CTRL <= 0xff || CTRL == 0x140 || CTRL == 0x141, "in-row controls only");
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);
 }
 __device__ __forceinline__ float half_sum_hi(float v) {
     v = fadd_rn(v, dpp_all<0xb1>(v));
