@@ -76,25 +76,29 @@ __global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
             const float sm[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
             mfma_pipe6<1, P, P>(wt, lane, g1, [&](int st) { return sm[st]; }, y, carry, g2, ca);
         }
-        epi<P, C>(ep, c0, h, y);
+        // folded BN (engine._fold_bn: alpha in W_small and in the ud0 / ud1 weights): + beta, ReLU
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) y[i][q] = fmaxf(fadd_rn(y[i][q], ep[C + chan(c0 + i, q, h)]), 0.f);
         tile_sync();  // the previous tile's readers of sA are done
 #pragma unroll
         for (int i = 0; i < P; ++i) put_tile<LDSW>(sA, c0 + i, j, h, y[i]);
         tile_sync();
 
         // ---- convs_1[1]
-        zero_tiles(y);
+        beta_p<P, C>(ep + 2 * C, c0, h, y);
         pipe_lds6<NCH, P, P>(wt, lane, g2, ChanB{sA + j * LDSW, h}, y, ca, g3, cb);
-        epi<P, C>(ep + 2 * C, c0, h, y);
+        relu_tiles(y);
         tile_sync();  // every wave has read the layer input
 #pragma unroll
         for (int i = 0; i < P; ++i) put_tile<LDSW>(sA, c0 + i, j, h, y[i]);
         tile_sync();
 
         // ---- convs_1[2]; prefetches the next tile's first chunk
-        zero_tiles(y);
+        beta_p<P, C>(ep + 4 * C, c0, h, y);
         pipe_lds6<NCH, P, P>(wt, lane, g3, ChanB{sA + j * LDSW, h}, y, cb, g1, carry);
-        epi<P, C>(ep + 4 * C, c0, h, y);
+        relu_tiles(y);
 
         // ---- attention: row max over the 512 channels (ReLU outputs: integer max on the
         // bit patterns; per wave, then across the waves through LDS), softmax over the 8 rows

@@ -9,8 +9,9 @@
 // pieces in registers; the weights come pre-split from the table
 // (engine.l2_table6: [co][chunk][piece][lane] 16-byte pieces, L2-resident, streamed
 // one chunk ahead and across call boundaries as in group_fused.hip).  The 4-column
-// geometry block is one zero-padded chunk.  Epilogues, attention, k-max and the
-// stores are group_fused.hip's.
+// geometry block is one zero-padded chunk.  BN is folded (engine._fold_bn: alpha in the
+// weights, the accumulators start from beta, the epilogue is the ReLU).  Attention, k-max
+// and the stores are group_fused.hip's.
 #include "mfma_chain.h"
 
 namespace {
@@ -66,22 +67,22 @@ __device__ __forceinline__ void conv_stack6(const gu32x4 *__restrict__ wt, const
     // geometry chunk: f32 k-steps 0, 1 (channels 2h, 2h + 1), the rest zero
     auto geom = [&](int st) { return st == 0 ? gin.x : st == 1 ? gin.y : 0.f; };
     if constexpr (PRE) {
-        load_tiles<T1>(h1, pre_row, h);
+        load_tiles<T1>(h1, pre_row, h);  // engine.level_pre6: alpha-folded W_f f + beta
         mfma_pipe6<1, T1, T1>(wt, lane, sg, geom, h1, cin, s2, c2);
         (void)c1; (void)sf; (void)fin;
     } else {
-        zero_tiles(h1);
+        beta_tiles<T1>(eb + e1, lane, h1);
         mfma_pipe6<1, T1, T1>(wt, lane, sg, geom, h1, cin, sf, c1);
         mfma_pipe6<NF, T1, T1>(
             wt, lane, sf, [&](int st) { return (&fin[st >> 2].x)[st & 3]; }, h1, c1, s2, c2);
     }
-    epilogue<T1>(eb + e1, lane, h1);
-    zero_tiles(h2);
+    relu_tiles(h1);
+    beta_tiles<T1>(eb + e2, lane, h2);
     mfma_pipe6<N1, T1, T3>(wt, lane, s2, [&](int st) { return h1[st >> 4][st & 15]; }, h2, c2, s3, c3);
-    epilogue<T1>(eb + e2, lane, h2);
-    zero_tiles(out);
+    relu_tiles(h2);
+    beta_tiles<T3>(eb + e3, lane, out);
     mfma_pipe6<N1, T3, NC>(wt, lane, s3, [&](int st) { return h2[st >> 4][st & 15]; }, out, c3, next, cout);
-    epilogue<T3>(eb + e3, lane, out);
+    relu_tiles(out);
 }
 
 template <class K, bool PRE>
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused6_kernel(
 
         // ---- mlp1 = W [x2 | x1d | emb * a] -> CM1, the emb * a part first
         f32x16 y1[TM1];
-        zero_tiles(y1);
+        beta_tiles<TM1>(eb + K::E_M1, lane, y1);
         mfma_pipe6<N3, TM1, T1>(wt, lane, m1em, [&](int st) { return fmul_rn(emb[st >> 4][st & 15], a); }, y1,
                                 ca, desc_g, cb);
 
@@ -206,14 +207,14 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused6_kernel(
         }
         static_assert(T3 % 2 == 0, "carry parity");
         mfma_pipe6<N3, TM1, TM2>(wt, lane, m1x1, [&](int st) { return x1d[st >> 4][st & 15]; }, y1, ca, m2, cb);
-        epilogue<TM1>(eb + K::E_M1, lane, y1);
+        relu_tiles(y1);
 
         // ---- mlp2 + k-max -> descriptor; prefetches the next tile's first chunk
         f32x16 y2[TM2];
-        zero_tiles(y2);
+        beta_tiles<TM2>(eb + K::E_M2, lane, y2);
         mfma_pipe6<NM1, TM2, T1>(wt, lane, m2, [&](int st) { return y1[st >> 4][st & 15]; }, y2, cb, det_g,
                                  carry);
-        epilogue<TM2>(eb + K::E_M2, lane, y2);
+        relu_tiles(y2);
 #pragma unroll
         for (int co = 0; co < TM2; ++co) {
             f32x16 v;

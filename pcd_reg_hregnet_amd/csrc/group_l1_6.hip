@@ -15,6 +15,8 @@
 //    k-max row x2, which is the same for both tiles);
 //  * mlp1's emb*a block is accumulated right after the attention (then emb is dead
 //    through the descriptor stack), then the x2 and x1d blocks;
+//  * BN folded (engine._fold_bn): alpha in the weight pieces, the accumulators start from
+//    beta, the epilogue is the ReLU;
 //  * built without packed fp32 VALU ops (build.NO_PACKED_F32): with them this kernel gave
 //    nondeterministic wrong accumulator values whenever two waves shared a SIMD.
 #include "mfma_chain.h"
@@ -83,27 +85,39 @@ __device__ __forceinline__ void pipe6_jt(const gu32x4 *__restrict__ wt, int lane
     }
 }
 
-template <int COUT_T>
-__device__ __forceinline__ void epilogue_jt(const float *ab, int lane, f32x16 (&acc)[COUT_T][JT]) {
-    const int h = lane >> 5;
-    constexpr int C = COUT_T * 32;
-#pragma unroll
-    for (int co = 0; co < COUT_T; ++co)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int c = chan(co, q, h);
-            const float al = ab[c], be = ab[C + c];
-#pragma unroll
-            for (int jt = 0; jt < JT; ++jt) acc[co][jt][q] = fmaxf(fadd_rn(fmul_rn(acc[co][jt][q], al), be), 0.f);
-        }
-}
-
 template <int N>
 __device__ __forceinline__ void zero_jt(f32x16 (&t)[N][JT]) {
 #pragma unroll
     for (int i = 0; i < N; ++i)
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt) t[i][jt] = zero16();
+}
+
+// folded BN (mfma_chain.h beta_tiles): both row tiles start from the layer's beta; the
+// epilogue is the ReLU
+template <int COUT_T>
+__device__ __forceinline__ void beta_jt(const float *ab, int lane, f32x16 (&acc)[COUT_T][JT]) {
+#pragma unroll
+    for (int co = 0; co < COUT_T; ++co)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float4 b = *reinterpret_cast<const float4 *>(ab + COUT_T * 32 + co * 32 + 8 * r + 4 * (lane >> 5));
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt) {
+                acc[co][jt][4 * r] = b.x; acc[co][jt][4 * r + 1] = b.y;
+                acc[co][jt][4 * r + 2] = b.z; acc[co][jt][4 * r + 3] = b.w;
+            }
+        }
+}
+
+template <int N>
+__device__ __forceinline__ void relu_jt(f32x16 (&t)[N][JT]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t[i][jt][q] = fmaxf(t[i][jt][q], 0.f);
 }
 
 // conv stack 4 -> 32 -> 32 -> 64 (+ BN/ReLU); NC: output tiles of the call that follows
@@ -113,21 +127,21 @@ __device__ __forceinline__ void conv_stack6(const gu32x4 *__restrict__ wt, const
                                             f32x16 (&out)[2][JT], const Carry &cin, FragSeq next, Carry &cout) {
     f32x16 h1[1][JT], h2[1][JT];
     Carry c2, c3;
-    zero_jt(h1);
+    beta_jt<1>(eb + e1, lane, h1);
     // geometry chunk: f32 k-steps 0, 1 (channels 2h, 2h + 1), the rest zero
     pipe6_jt<1, 1, 1, false>(
         wt, lane, FragSeq{g1, 1},
         [&](int jt, int st) { return st == 0 ? gin[jt].x : st == 1 ? gin[jt].y : 0.f; }, h1, cin,
         FragSeq{g2, 2}, c2);
-    epilogue_jt<1>(eb + e1, lane, h1);
-    zero_jt(h2);
+    relu_jt(h1);
+    beta_jt<1>(eb + e2, lane, h2);
     pipe6_jt<2, 1, 2, false>(wt, lane, FragSeq{g2, 2}, [&](int jt, int st) { return h1[st >> 4][jt][st & 15]; },
                              h2, c2, FragSeq{g3, 2}, c3);
-    epilogue_jt<1>(eb + e2, lane, h2);
-    zero_jt(out);
+    relu_jt(h2);
+    beta_jt<2>(eb + e3, lane, out);
     pipe6_jt<2, 2, NC, false>(wt, lane, FragSeq{g3, 2}, [&](int jt, int st) { return h2[st >> 4][jt][st & 15]; },
                               out, c3, next, cout);
-    epilogue_jt<2>(eb + e3, lane, out);
+    relu_jt(out);
 }
 
 __device__ __forceinline__ void store_tile31(float *out, int co, const f32x16 &v, int j, int h) {
@@ -208,7 +222,7 @@ __global__ __launch_bounds__(256, 2) void group_l1_6_kernel(
 
         // ---- mlp1 = W [x2 | x1d | emb * a] -> 32, the emb * a block first
         f32x16 y1[1][JT];
-        zero_jt(y1);
+        beta_jt<1>(eb + E_M1, lane, y1);
         pipe6_jt<4, 1, 1, false>(wt, lane, m1em,
                                  [&](int jt, int st) { return fmul_rn(emb[st >> 4][jt][st & 15], a[jt]); }, y1, ca,
                                  FragSeq{G_EC1, 1}, cb);
@@ -226,14 +240,14 @@ __global__ __launch_bounds__(256, 2) void group_l1_6_kernel(
                                 cb);
         pipe6_jt<4, 1, 2, false>(wt, lane, m1x1, [&](int jt, int st) { return x1d[st >> 4][jt][st & 15]; }, y1,
                                  cb, m2, ca);
-        epilogue_jt<1>(eb + E_M1, lane, y1);
+        relu_jt(y1);
 
         // ---- mlp2: 32 -> 64, k-max -> descriptor; prefetches the next group's first chunk
         f32x16 y2[2][JT];
-        zero_jt(y2);
+        beta_jt<2>(eb + E_M2, lane, y2);
         pipe6_jt<2, 2, 1, false>(wt, lane, m2, [&](int jt, int st) { return y1[st >> 4][jt][st & 15]; }, y2, ca,
                                  FragSeq{G_DC1, 1}, carry);
-        epilogue_jt<2>(eb + E_M2, lane, y2);
+        relu_jt(y2);
 #pragma unroll
         for (int co = 0; co < 2; ++co) {
             f32x16 v;

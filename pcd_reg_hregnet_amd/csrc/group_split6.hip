@@ -7,7 +7,9 @@
 // group_split.hip, two workgroups per CU); each wave splits the B chunk it reads into its
 // bf16 pieces in registers.  Weight pieces stream from the L2-resident table
 // (engine.split_table6: group_fused6.hip's chunk fragments, then mlp1's x2 block f32
-// row-major for the per-group matrix-vector product, then the f32 epilogues).
+// row-major for the per-group matrix-vector product, then the f32 epilogues).  BN is
+// folded (engine._fold_bn): alpha in the weights, the accumulators start from beta, the
+// epilogue is the ReLU.
 #include "split_chain.h"
 
 namespace {
@@ -82,11 +84,11 @@ __device__ __forceinline__ void conv_stack_split6(const gu32x4 *__restrict__ wt,
         v[2] = 0.f; v[3] = 0.f;
     };
     if constexpr (PRE) {
-        load_tiles<P1>(h1, pre_row + c1 * 32, h);
+        load_tiles<P1>(h1, pre_row + c1 * 32, h);  // engine.level_pre6: alpha-folded W_f f + beta
         pipe_lds6<1, P1, P1>(wt, lane, sg, geom_b, h1, cin, s2, cb);
         (void)sf;
     } else {
-        zero_tiles(h1);
+        beta_p<P1, K::T1 * 32>(eb + e1, c1, h, h1);
         pipe_lds6<1, P1, P1>(wt, lane, sg, geom_b, h1, cin, sf, ca);
         pipe_lds6<NF, P1, P1>(
             wt, lane, sf,
@@ -96,20 +98,20 @@ __device__ __forceinline__ void conv_stack_split6(const gu32x4 *__restrict__ wt,
             },
             h1, ca, s2, cb);
     }
-    epi<P1, K::T1 * 32>(eb + e1, c1, h, h1);
+    relu_tiles(h1);
 #pragma unroll
     for (int i = 0; i < P1; ++i) put_tile<LDSW>(B, c1 + i, j, h, h1[i]);
     tile_sync();
     f32x16 h2[P1];
-    zero_tiles(h2);
+    beta_p<P1, K::T1 * 32>(eb + e2, c1, h, h2);
     pipe_lds6<N1, P1, P3>(wt, lane, s2, ChanB{brow, h}, h2, cb, s3, ca);
-    epi<P1, K::T1 * 32>(eb + e2, c1, h, h2);
+    relu_tiles(h2);
 #pragma unroll
     for (int i = 0; i < P1; ++i) put_tile<LDSW>(A, c1 + i, j, h, h2[i]);
     tile_sync();
-    zero_tiles(out);
+    beta_p<P3, K::T3 * 32>(eb + e3, c3, h, out);
     pipe_lds6<N1, P3, NP>(wt, lane, s3, ChanB{arow, h}, out, ca, next, cout);
-    epi<P3, K::T3 * 32>(eb + e3, c3, h, out);
+    relu_tiles(out);
 }
 
 template <class K, bool PRE>
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(256, 2) void group_split6_kernel(
 
         // ---- mlp1, emb*a part (y1 stays in registers through the descriptor stack)
         f32x16 y1[PM1];
-        zero_tiles(y1);
+        beta_p<PM1, TM1 * 32>(eb + K::E_M1, m1, h, y1);
         pipe_lds6<N3, PM1, K::P1>(wt, lane, m1em, ChanB{B + j * LDSW, h}, y1, ca, desc_g, cb);
         stage_rows6<K, PRE>(A, geom, gidx, feats, t, cw, lane);
         tile_sync();
@@ -280,16 +282,16 @@ __global__ __launch_bounds__(256, 2) void group_split6_kernel(
                 }
         }
         pipe_lds6<N3, PM1, PM2>(wt, lane, m1x1, ChanB{B + j * LDSW, h}, y1, ca, fm2, cb);
-        epi<PM1, TM1 * 32>(eb + K::E_M1, m1, h, y1);
+        relu_tiles(y1);
 #pragma unroll
         for (int i = 0; i < PM1; ++i) put_tile<LDSW>(A, m1 + i, j, h, y1[i]);
         tile_sync();
 
         // ---- mlp2 + k-max -> descriptor; prefetches the next tile's first chunk
         f32x16 y2[PM2];
-        zero_tiles(y2);
+        beta_p<PM2, CM2>(eb + K::E_M2, m2, h, y2);
         pipe_lds6<NM1, PM2, K::P1>(wt, lane, fm2, ChanB{A + j * LDSW, h}, y2, cb, det_g, carry);
-        epi<PM2, CM2>(eb + K::E_M2, m2, h, y2);
+        relu_tiles(y2);
 #pragma unroll
         for (int i = 0; i < PM2; ++i) {
             f32x16 v;

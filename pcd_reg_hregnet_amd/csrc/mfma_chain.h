@@ -158,6 +158,23 @@ __device__ __forceinline__ void load_tiles(f32x16 (&acc)[T], const float *__rest
         }
 }
 
+// Folded BN (the bf16x6 kernels): a layer's alpha is folded into its weight rows on the host
+// (engine._fold_bn), so an output tile starts from the per-channel beta -- read from the
+// [alpha C | beta C] epilogue section straight into the accumulators -- and the epilogue is
+// the ReLU alone (1 VALU per value instead of zeroing + multiply + add + max).
+template <int COUT_T>
+__device__ __forceinline__ void beta_tiles(const float *ab, int lane, f32x16 (&acc)[COUT_T]) {
+    load_tiles<COUT_T>(acc, ab + COUT_T * 32, lane >> 5);
+}
+
+template <int N>
+__device__ __forceinline__ void relu_tiles(f32x16 (&t)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t[i][q] = fmaxf(t[i][q], 0.f);
+}
+
 template <int N>
 __device__ __forceinline__ void zero_tiles(f32x16 (&t)[N]) {
 #pragma unroll

@@ -113,24 +113,36 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
         tile_sync();
 
         f32x16 y1[P];
-        zero_tiles(y1);
+        if constexpr (B6)
+            beta_p<P, C>(eb + K::R_M1, c0, h, y1);  // folded BN (engine._fold_bn)
+        else
+            zero_tiles(y1);
         if constexpr (B6)
             pipe_lds6<K::NCH, P, P>(wt, lane, g1, ChanB{A + j * LDSW, h}, y1, carry6, g2, ca6);
         else
             pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f1, ChanB{A + j * LDSW, h}, y1, carry, f2, ca);
-        epi<P, C>(eb + K::R_M1, c0, h, y1);
+        if constexpr (B6)
+            relu_tiles(y1);
+        else
+            epi<P, C>(eb + K::R_M1, c0, h, y1);
         tile_sync();  // every wave has read x from A
 #pragma unroll
         for (int i = 0; i < P; ++i) put_tile<LDSW>(A, c0 + i, j, h, y1[i]);
         tile_sync();
 
         f32x16 y2[P];
-        zero_tiles(y2);
+        if constexpr (B6)
+            beta_p<P, C>(eb + K::R_M2, c0, h, y2);
+        else
+            zero_tiles(y2);
         if constexpr (B6)
             pipe_lds6<K::NCH, P, P>(wt, lane, g2, ChanB{A + j * LDSW, h}, y2, ca6, g1, carry6);
         else
             pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f2, ChanB{A + j * LDSW, h}, y2, ca, f1, carry);
-        epi<P, C>(eb + K::R_M2, c0, h, y2);
+        if constexpr (B6)
+            relu_tiles(y2);
+        else
+            epi<P, C>(eb + K::R_M2, c0, h, y2);
 
         // mlp3: this wave's channels, then the two lane halves, then the waves in order
         float p = 0.f;

@@ -173,6 +173,13 @@ __device__ __forceinline__ void epi(const float *ab, int co0, int h, f32x16 (&ac
         }
 }
 
+// folded BN (mfma_chain.h beta_tiles): output tiles co0 .. co0+P-1 of a C-channel layer
+// start from the layer's beta ([alpha C | beta C] section)
+template <int P, int C>
+__device__ __forceinline__ void beta_p(const float *ab, int co0, int h, f32x16 (&acc)[P]) {
+    load_tiles<P>(acc, ab + C + co0 * 32, h);
+}
+
 // tile co of an activation (channels chan(co, q, h), row j) into a row-major LDS buffer
 template <int LDSW>
 __device__ __forceinline__ void put_tile(float *buf, int co, int j, int h, const f32x16 &v) {

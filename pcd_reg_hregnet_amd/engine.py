@@ -103,6 +103,19 @@ def _bn_fold(sd, pre, bias=None):
     return alpha.contiguous(), beta.contiguous()
 
 
+def _fold_bn(lin: Lin) -> Lin:
+    """The bf16x6 kernels' form of a conv + eval-BN layer: alpha folded into the weight
+    rows (W' = diag(alpha) W), the epilogue section [1 | beta]; the kernels start the
+    accumulators from beta and apply the ReLU alone.  Same function up to fp32 rounding
+    (alpha * sum w x vs sum (alpha w) x)."""
+    return Lin((lin.W * lin.alpha[:, None]).contiguous(), torch.ones_like(lin.alpha),
+               lin.beta.clone(), lin.relu)
+
+
+def _fold_all(lins):
+    return [_fold_bn(l) for l in lins]
+
+
 def _conv_bn(sd, conv, bn, perm=None):
     W = sd[conv + ".weight"].float()
     W = W.reshape(W.shape[0], -1)
@@ -161,6 +174,14 @@ class PreparedWeights:
             Lin(torch.cat([self.det[lv][0].W[:, 4:], self.desc[lv][0].W[:, 4:]]).contiguous(),
                 torch.ones(2 * self.det[lv][0].N), torch.zeros(2 * self.det[lv][0].N), False)
             for lv in (1, 2)]
+        # the same for the bf16x6 level kernels (folded BN): alpha-scaled rows and the two
+        # layers' beta in the epilogue, so a precomputed row is the whole accumulator start
+        self.level_pre6 = [None] + [
+            Lin(torch.cat([(self.det[lv][0].W[:, 4:] * self.det[lv][0].alpha[:, None]),
+                           (self.desc[lv][0].W[:, 4:] * self.desc[lv][0].alpha[:, None])]).contiguous(),
+                torch.ones(2 * self.det[lv][0].N),
+                torch.cat([self.det[lv][0].beta, self.desc[lv][0].beta]).contiguous(), False)
+            for lv in (1, 2)]
         C = 256
         self.coarse_convs1 = _stack(sd, "coarse_corres.convs_1", 3, _perm_coarse(C))
         # convs_1[0] split by input block (COARSE_SPLIT): the 16 per-row columns, and
@@ -169,6 +190,9 @@ class PreparedWeights:
         self.coarse_c1_small = Lin(c0.W[:, :16].contiguous(), c0.alpha, c0.beta, True)
         self.coarse_c1_desc = Lin(torch.stack([c0.W[:, 16:16 + C], c0.W[:, 16 + C:]]).contiguous(),
                                   torch.ones(c0.N), torch.zeros(c0.N), False)
+        # coarse6.hip (folded BN): alpha-scaled desc / knn_desc blocks
+        self.coarse_c1_desc6 = Lin((self.coarse_c1_desc.W * c0.alpha[None, :, None]).contiguous(),
+                                   torch.ones(c0.N), torch.zeros(c0.N), False)
         self.coarse_convs2 = _stack(sd, "coarse_corres.convs_2", 3)
         n0 = self.coarse_convs2[0]
         self.nbr_pre = Lin(n0.W[:, :C].contiguous(), torch.ones(n0.N), torch.zeros(n0.N), False)
@@ -186,14 +210,15 @@ class PreparedWeights:
         self.mlpx = (_conv_bn(sd, "fine_corres_2.mlpx.0", "fine_corres_2.mlpx.1")
                      if "fine_corres_2.mlpx.0.weight" in sd else None)
         self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
-        self.l1_table6 = l1_table6(self.det[0], self.desc[0], self.desc_mlp[0])
+        self.l1_table6 = l1_table6(_fold_all(self.det[0]), _fold_all(self.desc[0]),
+                                   _fold_all(self.desc_mlp[0]))
         self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
-        self.l2_table6 = l2_table6(self.det[1], self.desc[1], self.desc_mlp[1])
-        self.l3_table6 = l2_table6(self.det[2], self.desc[2], self.desc_mlp[2])
+        self.l2_table6 = l2_table6(*(_fold_all(x) for x in (self.det[1], self.desc[1], self.desc_mlp[1])))
+        self.l3_table6 = l2_table6(*(_fold_all(x) for x in (self.det[2], self.desc[2], self.desc_mlp[2])))
         self.l2s_table = split_table(self.det[1], self.desc[1], self.desc_mlp[1])
-        self.l2s_table6 = split_table6(self.det[1], self.desc[1], self.desc_mlp[1])
-        self.l3s_table6 = split_table6(self.det[2], self.desc[2], self.desc_mlp[2])
+        self.l2s_table6 = split_table6(*(_fold_all(x) for x in (self.det[1], self.desc[1], self.desc_mlp[1])))
+        self.l3s_table6 = split_table6(*(_fold_all(x) for x in (self.det[2], self.desc[2], self.desc_mlp[2])))
         self.l3s_table = split_table(self.det[2], self.desc[2], self.desc_mlp[2])
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
                            for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
@@ -201,7 +226,8 @@ class PreparedWeights:
         self.fine_table6 = {name: fine_head_table6(self.fine[name][0])
                             for name in ("fine_corres_2", "fine_corres_1")}
         self.nbr_table6 = nbr_head_table6(self.coarse_convs2, 256)
-        self.coarse_table6 = coarse_head_table6(self.coarse_c1_small, self.coarse_convs1)
+        self.coarse_table6 = coarse_head_table6(_fold_bn(self.coarse_c1_small),
+                                                _fold_all(self.coarse_convs1))
         self.head_table = {("det", lvl): mlp_head_table(self.det_head[lvl]) for lvl in range(3)}
         self.head_table["coarse"] = mlp_head_table(self.coarse_head)
         for name in ("fine_corres_2", "fine_corres_1"):
@@ -210,7 +236,7 @@ class PreparedWeights:
             [(("det", lvl), self.det_head[lvl]) for lvl in range(3)] + [("coarse", self.coarse_head)] +
             [(n, self.fine[n][1]) for n in ("fine_corres_2", "fine_corres_1")])}
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
-                     "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre",
+                     "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre", "level_pre6", "coarse_c1_desc6",
                      "coarse_head", "fine", "l1_table", "l1_table6", "l2_table", "l3_table", "l2_table6",
                      "l3_table6", "l2s_table", "l2s_table6", "l3s_table6",
                      "l3s_table", "fine_table", "fine_table6", "nbr_table6", "coarse_table6",
@@ -361,9 +387,10 @@ def mlp_head_table(head) -> torch.Tensor:
 
 
 def mlp_head_table6(head) -> torch.Tensor:
-    """Table of hreg_mlp_head6 (HCfg TABLE6): mlp1 and mlp2 as bf16 piece chunk fragments
-    (frag6), then mlp_head_table's epilogue section."""
+    """Table of hreg_mlp_head6 (HCfg TABLE6): mlp1 and mlp2 (folded BN, _fold_bn) as bf16
+    piece chunk fragments (frag6), then mlp_head_table's epilogue section."""
     m1, m2, w3, b3 = head
+    m1, m2 = _fold_bn(m1), _fold_bn(m2)
     T = m1.W.shape[0] // 32
     parts = [frag6(frag_layer(m1.W), T, T * 16), frag6(frag_layer(m2.W), T, T * 16), m1.alpha,
              m1.beta, m2.alpha, m2.beta, w3, b3, torch.zeros(3)]
@@ -823,8 +850,9 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         else:
             name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
                            ("hreg_group_l3", P.l3_table))
-        pre = (gemm([_seg(feats, 0, Cf)], P.level_pre[lvl], feats.shape[0]) if LEVEL_PRE
-               else None)
+        b6 = name in ("hreg_group6_l2", "hreg_group_split6_l2", "hreg_group_split6_l3")
+        pre = (gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl],
+                    feats.shape[0]) if LEVEL_PRE else None)
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())
         sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)
@@ -960,8 +988,9 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
         # desc3 = [src; dst]) and added in the layer's epilogue: 8.86 -> 1.34 GFLOP
         # per step at B=8 for this layer
         ud = _empty(2, B * N1, P.coarse_c1_desc.W.shape[1], device=dev)
-        _gemm_batched_desc(P.coarse_c1_desc, desc3, B * N1, C, ud)
-        if FUSED_COARSE and C == 256:
+        fused = FUSED_COARSE and C == 256
+        _gemm_batched_desc(P.coarse_c1_desc6 if fused else P.coarse_c1_desc, desc3, B * N1, C, ud)
+        if fused:
             # convs_1 + attention in one launch (coarse6.hip)
             corres = _empty(B * N1, 3, device=dev)
             att = _empty(B * N1, ud.shape[2], device=dev)
