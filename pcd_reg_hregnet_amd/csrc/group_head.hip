@@ -342,6 +342,9 @@ typedef u32x4 Carry6[CARRY6][3];
 
 // the three conv layers of a head tile: h1 holds the precomputed products; b0 gives the
 // first block's B values (f32 k-steps 0..7 of the lane); f receives the last layer
+// BN folded (engine._fold_bn): the precomputed products and the weight pieces carry alpha;
+// h1 starts from them (plus beta where the caller's rows do not hold it), layers 2 and 3
+// start from beta; every epilogue is the ReLU.
 template <class K, class B0>
 __device__ __forceinline__ void head_chain6(const gu32x4 *__restrict__ wt, const float *eb, int lane, B0 b0,
                                             f32x16 (&h1)[K::T1], f32x16 (&f)[K::T1], Carry6 &carry) {
@@ -349,14 +352,14 @@ __device__ __forceinline__ void head_chain6(const gu32x4 *__restrict__ wt, const
     const FragSeq fs{K::G_S, 1}, f2{K::G_2, NC}, f3{K::G_3, NC};
     Carry6 c2, c3;
     mfma_pipe6<1, T1, T1>(wt, lane, fs, b0, h1, carry, f2, c2);
-    epilogue<T1>(eb + K::E_1, lane, h1);
+    relu_tiles(h1);
     f32x16 h2[T1];
-    zero_tiles(h2);
+    beta_tiles<T1>(eb + K::E_2, lane, h2);
     mfma_pipe6<NC, T1, T1>(wt, lane, f2, [&](int st) { return h1[st >> 4][st & 15]; }, h2, c2, f3, c3);
-    epilogue<T1>(eb + K::E_2, lane, h2);
-    zero_tiles(f);
+    relu_tiles(h2);
+    beta_tiles<T1>(eb + K::E_3, lane, f);
     mfma_pipe6<NC, T1, T1>(wt, lane, f3, [&](int st) { return h2[st >> 4][st & 15]; }, f, c3, fs, carry);
-    epilogue<T1>(eb + K::E_3, lane, f);
+    relu_tiles(f);
 }
 
 template <class K>
@@ -391,6 +394,10 @@ __global__ __launch_bounds__(256, K::WPS) void fine_head6_kernel(
         const float sm[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
         f32x16 h1[T1], f[T1];
         init_from_rows<N1, T1>(h1, pre_src + (size_t)g * N1, pre_dst + (size_t)gidx[row] * N1, h);
+#pragma unroll
+        for (int co = 0; co < T1; ++co)  // + beta of convs_1[0] (the pre GEMM is batch-2)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) h1[co][q] = fadd_rn(h1[co][q], eb[K::E_1 + N1 + chan(co, q, h)]);
         head_chain6<K>(wt, eb, lane, [&](int st) { return sm[st]; }, h1, f, carry);
         fine_attend<T1>(f, lane, row, knn_xyz, corres, att);
     }
@@ -424,7 +431,7 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head6_kernel(
         // geometry k-steps 0, 1 (columns 2h, 2h + 1 of [dxyz, |d|]), the rest of the chunk zero
         const float2 gin = *reinterpret_cast<const float2 *>(geom + (size_t)row * 4 + h * 2);
         f32x16 h1[T1], f[T1];
-        init_from_rows<N1, T1>(h1, pre + src * N1, nullptr, h);
+        init_from_rows<N1, T1>(h1, pre + src * N1, nullptr, h);  // engine.nbr_pre6: alpha-folded + beta
         head_chain6<K>(wt, eb, lane, [&](int st) { return st == 0 ? gin.x : st == 1 ? gin.y : 0.f; }, h1, f,
                        carry);
         nbr_attend<T1, C>(f, lane, row, desc + src * C, out);

@@ -196,6 +196,9 @@ class PreparedWeights:
         self.coarse_convs2 = _stack(sd, "coarse_corres.convs_2", 3)
         n0 = self.coarse_convs2[0]
         self.nbr_pre = Lin(n0.W[:, :C].contiguous(), torch.ones(n0.N), torch.zeros(n0.N), False)
+        # nbr_head6_kernel (folded BN): alpha-scaled descriptor block, convs_2[0]'s beta
+        self.nbr_pre6 = Lin((n0.W[:, :C] * n0.alpha[:, None]).contiguous(), torch.ones(n0.N),
+                            n0.beta.clone(), False)
         self.coarse_head = _mlp_head(sd, "coarse_corres")
         self.fine = {}
         for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64)):
@@ -206,6 +209,10 @@ class PreparedWeights:
             f0 = self.fine[name][0][0]
             self.fine_pre[name] = Lin(torch.stack([f0.W[:, 12:12 + C], f0.W[:, 12 + C:]]).contiguous(),
                                       torch.ones(f0.N), torch.zeros(f0.N), False)
+        # fine_head6_kernel (folded BN): alpha-scaled descriptor blocks (its beta is added
+        # in the kernel: the batch-2 GEMM shares one epilogue)
+        self.fine_pre6 = {n: Lin((l.W * self.fine[n][0][0].alpha[None, :, None]).contiguous(), l.alpha,
+                                 l.beta, False) for n, l in self.fine_pre.items()}
         # Model_V2's FineReg2.mlpx (model_v2/layers.py:457-459), when the state dict has it
         self.mlpx = (_conv_bn(sd, "fine_corres_2.mlpx.0", "fine_corres_2.mlpx.1")
                      if "fine_corres_2.mlpx.0.weight" in sd else None)
@@ -223,9 +230,9 @@ class PreparedWeights:
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
                            for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
         self.nbr_table = nbr_head_table(self.coarse_convs2, 256)
-        self.fine_table6 = {name: fine_head_table6(self.fine[name][0])
+        self.fine_table6 = {name: fine_head_table6(_fold_all(self.fine[name][0]))
                             for name in ("fine_corres_2", "fine_corres_1")}
-        self.nbr_table6 = nbr_head_table6(self.coarse_convs2, 256)
+        self.nbr_table6 = nbr_head_table6(_fold_all(self.coarse_convs2), 256)
         self.coarse_table6 = coarse_head_table6(_fold_bn(self.coarse_c1_small),
                                                 _fold_all(self.coarse_convs1))
         self.head_table = {("det", lvl): mlp_head_table(self.det_head[lvl]) for lvl in range(3)}
@@ -236,7 +243,7 @@ class PreparedWeights:
             [(("det", lvl), self.det_head[lvl]) for lvl in range(3)] + [("coarse", self.coarse_head)] +
             [(n, self.fine[n][1]) for n in ("fine_corres_2", "fine_corres_1")])}
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
-                     "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "level_pre", "level_pre6", "coarse_c1_desc6",
+                     "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "fine_pre6", "nbr_pre6", "level_pre", "level_pre6", "coarse_c1_desc6",
                      "coarse_head", "fine", "l1_table", "l1_table6", "l2_table", "l3_table", "l2_table6",
                      "l3_table6", "l2s_table", "l2s_table6", "l3s_table6",
                      "l3s_table", "fine_table", "fine_table6", "nbr_table6", "coarse_table6",
@@ -959,8 +966,9 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     R2 = G2 * k
     if FUSED_NBR and C == 256:
         nbr = _empty(G2, C, device=dev)
-        pre = gemm([_seg(desc3, 0, C)], P.nbr_pre, G2) if HEAD_PRE else None
-        if B6_HEADS and HEAD_PRE:
+        b6 = B6_HEADS and HEAD_PRE
+        pre = gemm([_seg(desc3, 0, C)], P.nbr_pre6 if b6 else P.nbr_pre, G2) if HEAD_PRE else None
+        if b6:
             call("hreg_nbr_head6", P.nbr_table6, desc3, gself, geom_self, G2, nbr, pre, _stream())
         else:
             call("hreg_nbr_head", P.nbr_table, desc3, gself, geom_self, G2, nbr, pre, _stream())
@@ -1033,7 +1041,8 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
         pre = [None, None]
         if HEAD_PRE:
             pre = _empty(2, B * N, N1, device=dev)
-            _gemm_batched_desc(P.fine_pre[name], src_desc, B * N, C, pre, x1=dst_desc)
+            _gemm_batched_desc((P.fine_pre6 if B6_HEADS else P.fine_pre)[name], src_desc, B * N, C,
+                               pre, x1=dst_desc)
         if B6_HEADS and HEAD_PRE:
             call("hreg_fine_head6", P.fine_table6[name], C, small, gidx, kx, B * N, corres, att,
                  pre[0], pre[1], _stream())
