@@ -453,9 +453,10 @@ def main():
                          "eagerly; serial: no cross-batch overlap")
     ap.add_argument("--lanes", type=int, default=None,
                     help="graph executor: batches in flight at once, one stream each "
-                         "(a step is still one forward over one batch); default 8 (A/B: "
-                         "+3 %% over 4), 4 for v2 (its cluster FPS spins up to 256 waves "
-                         "per launch and needs every launch's participants co-resident)")
+                         "(a step is still one forward over one batch); default 8 (a "
+                         "--steps it does not divide: the most lanes that do, powers of two "
+                         "first), 4 for v2 (its cluster FPS spins up to 256 waves per "
+                         "launch and needs every launch's participants co-resident)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--split", default=None,
                     help="comma list of levels (2,3) on the channel-split group kernel "
@@ -473,15 +474,15 @@ def main():
     if args.model != "train" and args.executor == "graph" and args.steps % args.lanes:
         # a replay runs one batch per lane: time exactly --steps forwards with the most
         # lanes <= --lanes that divide it, powers of two first (the streams share
-        # GPU_MAX_HW_QUEUES = 4 hardware queues: 5 or 6 lanes measured slower than 4;
-        # e.g. --steps 20 --lanes 8 -> 4 lanes)
+        # GPU_MAX_HW_QUEUES = 4 hardware queues: 5 or 6 lanes measured slower than 4; a
+        # final partial round on some lanes, GraphPipeline.run_forwards, measured slower
+        # too: --steps 20 on 8 lanes 5179 vs 4 lanes 5293 pairs/s)
         cand = [d for d in range(1, args.lanes + 1) if args.steps % d == 0]
         pow2 = [d for d in cand if d & (d - 1) == 0]
         lanes = max(pow2) if max(pow2) >= 4 or max(pow2) == max(cand) else max(cand)
         print(f"bench: --steps {args.steps} is not a multiple of --lanes {args.lanes}; "
               f"using {lanes} lanes", file=sys.stderr)
         args.lanes = lanes
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -518,6 +519,8 @@ def main():
     if args.executor == "graph":
         with torch.no_grad():
             gpipe = engine.GraphPipeline(P, src, dst, lanes=args.lanes, v2=v2)
+            gpipe.prepare(args.warmup)
+            gpipe.prepare(args.steps)  # captured before the timed region
 
     def run(n):
         with torch.no_grad():
@@ -526,7 +529,7 @@ def main():
                     return [engine.model_v2_forward(P, src, dst) for _ in range(n)]
                 return [engine.hregnet_forward(P, src, dst) for _ in range(n)]
             if args.executor == "graph":
-                return gpipe.run(-(-n // args.lanes))
+                return gpipe.run_forwards(n)
             return pipe.run([(src, dst)] * n)
 
     run(args.warmup)

@@ -1293,19 +1293,22 @@ class GraphPipeline:
                 out = self._fork(lambda ln: self._rest(ln, cur))
             self.g_last.append(g)
             self.outs_last.append(out)
+        self._part = {}
         torch.cuda.synchronize()
 
-    def _fork(self, body, side=None):
-        """Inside a capture: body(lane) for every lane on its own stream (lane 0 on
-        the capturing stream) and side(lane) on the lane's side stream, all forked
-        from the capturing stream and joined back to it (one level of fork/join:
-        consecutive graph launches on one stream are ordered, so the side work of
-        this launch cannot overlap the previous launch's reads of its buffers).
+    def _fork(self, body, side=None, lanes=None, side_lanes=None):
+        """Inside a capture: body(lane) for every lane < lanes on its own stream (lane 0
+        on the capturing stream) and side(lane) for lane < side_lanes on the lane's side
+        stream, all forked from the capturing stream and joined back to it (one level of
+        fork/join: consecutive graph launches on one stream are ordered, so the side work
+        of this launch cannot overlap the previous launch's reads of its buffers).
         Returns the per-lane results of body."""
         main = torch.cuda.current_stream()
+        lanes = self.lanes if lanes is None else lanes
+        side_lanes = lanes if side_lanes is None else side_lanes
         jobs = []
-        for ln in range(self.lanes):
-            if side is not None:
+        for ln in range(lanes):
+            if side is not None and ln < side_lanes:
                 jobs.append((self.side[ln], side, ln))
             jobs.append((None if ln == 0 else self.lane_streams[ln], body, ln))
         for st, _, _ in jobs:
@@ -1341,6 +1344,78 @@ class GraphPipeline:
         _status_pending = False
         if self.status_check:
             check_device_status(force=True)
+
+    def _partial(self, r: int):
+        """Graphs for a final partial round of r < lanes forwards (captured on first use):
+        g_first_r = stage 1 of lanes < r; g_step_pr[cur] = the rest of every lane's batch
+        with stage 1 of the next batch on lanes < r only; g_last_r[cur] = the rest of lanes
+        < r."""
+        if r in self._part:
+            return self._part[r]
+        torch.cuda.synchronize()
+        first = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(first, pool=self.pool):
+            self._fork(lambda ln: stage1_into(self.bufs[ln][0], self.src[ln], self.dst[ln]), lanes=r)
+        steps, souts, lasts, louts = [], [], [], []
+        for cur in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                out = self._fork(
+                    lambda ln: self._rest(ln, cur),
+                    side=lambda ln: stage1_into(self.bufs[ln][1 - cur], self.src[ln], self.dst[ln]),
+                    side_lanes=r)
+            steps.append(g)
+            souts.append(out)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                out = self._fork(lambda ln: self._rest(ln, cur), lanes=r)
+            lasts.append(g)
+            louts.append(out)
+        torch.cuda.synchronize()
+        self._part[r] = (first, steps, souts, lasts, louts)
+        return self._part[r]
+
+    def prepare(self, n: int):
+        """Capture ahead what run_forwards(n) needs (the partial-round graphs)."""
+        if n % self.lanes:
+            self._partial(n % self.lanes)
+
+    def run_forwards(self, n: int):
+        """n forwards in all: full rounds of every lane, then (n % lanes) forwards on the
+        first lanes (a partial round: lanes < n % lanes run one forward more).  Returns
+        the last forward's output of every lane (views into graph-owned memory)."""
+        q, r = divmod(n, self.lanes)
+        if q == 0:
+            if r == 0:
+                return None
+            first, _, _, lasts, louts = self._partial(r)
+            first.replay()
+            lasts[0].replay()
+            out = louts[0]
+            out = [model_v2_finish(o) for o in out] if self.v2 else list(out)
+            return out + [None] * (self.lanes - r)
+        if r == 0:
+            return self.run(q) if self.lanes > 1 else [self.run(q)]
+        first, steps, souts, lasts, louts = self._partial(r)
+        self.g_first.replay()
+        cur = 0
+        for i in range(q - 1):
+            self.g_step[cur].replay()
+            if self.v2:
+                for o in self.outs[cur]:
+                    model_v2_finish(o)
+            cur = 1 - cur
+        steps[cur].replay()  # the last full round, stage 1 of lanes < r only
+        full = souts[cur]
+        if self.v2:
+            for o in full:
+                model_v2_finish(o)
+        cur = 1 - cur
+        lasts[cur].replay()
+        out = louts[cur]
+        if self.v2:
+            out = [model_v2_finish(o) for o in out]
+        return out + full[r:]
 
     def run(self, steps: int):
         """Runs `steps` rounds; a round is one complete forward of every lane's static

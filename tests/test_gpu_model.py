@@ -180,6 +180,31 @@ def test_graph_lanes_match_eager(net):
                 assert torch.equal(out["src_feats"]["desc_3"], ref["src_feats"]["desc_3"])
 
 
+def test_graph_partial_round_matches_eager(net):
+    """run_forwards(n) with n not a multiple of the lanes: full rounds, then a partial
+    round on the first lanes; every lane's last output is bitwise its eager forward."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    data = [synthetic.lidar_batch(2, 4096, seed0=sd)[:2] for sd in (52, 53, 54)]
+    dev = [(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()) for s, d in data]
+    with torch.no_grad():
+        gp = engine.GraphPipeline(P, dev[0][0], dev[0][1], lanes=3)
+        for ln in (1, 2):
+            gp.load(dev[ln][0], dev[ln][1], lane=ln)
+        refs = [engine.hregnet_forward(P, s, d) for s, d in dev]
+        for n in (2, 4, 7):
+            gp.prepare(n)
+            outs = gp.run_forwards(n)
+            torch.cuda.synchronize()
+            assert len(outs) == 3
+            for ln, out in enumerate(outs):
+                if out is None:
+                    continue
+                for i in range(3):
+                    assert torch.equal(out["rotation"][i], refs[ln]["rotation"][i]), (n, ln)
+                    assert torch.equal(out["translation"][i], refs[ln]["translation"][i]), (n, ln)
+
+
 @pytest.mark.parametrize("lvl,split,pre,b6", [
     (0, False, False, False), (1, False, False, False), (2, False, False, False),
     (1, True, False, False), (2, True, False, False), (1, False, True, False),
