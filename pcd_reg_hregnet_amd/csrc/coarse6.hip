@@ -80,7 +80,7 @@ __global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
 #pragma unroll
         for (int i = 0; i < P; ++i)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) y[i][q] = fmaxf(fadd_rn(y[i][q], ep[C + chan(c0 + i, q, h)]), 0.f);
+            for (int q = 0; q < 16; ++q) y[i][q] = relu_i(fadd_rn(y[i][q], ep[C + chan(c0 + i, q, h)]));
         tile_sync();  // the previous tile's readers of sA are done
 #pragma unroll
         for (int i = 0; i < P; ++i) put_tile<LDSW>(sA, c0 + i, j, h, y[i]);

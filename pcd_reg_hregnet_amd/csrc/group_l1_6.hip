@@ -117,7 +117,7 @@ __device__ __forceinline__ void relu_jt(f32x16 (&t)[N][JT]) {
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) t[i][jt][q] = fmaxf(t[i][jt][q], 0.f);
+            for (int q = 0; q < 16; ++q) t[i][jt][q] = relu_i(t[i][jt][q]);
 }
 
 // conv stack 4 -> 32 -> 32 -> 64 (+ BN/ReLU); NC: output tiles of the call that follows
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void group_l1_6_kernel(
                 for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(emb[co][jt][q]));
             x1[jt] = __int_as_float(max(mi, __shfl_xor(mi, 32)));
         }
-        const float mx = half_bcast(half_max_hi_nonneg(fmaxf(x1[0], x1[1])), h);
+        const float mx = half_bcast(half_max_hi_nonneg(max_nonneg(x1[0], x1[1])), h);
         const float e0 = expf(fsub_rn(x1[0], mx)), e1 = expf(fsub_rn(x1[1], mx));
         const float ssum = half_bcast(half_sum_hi(fadd_rn(e0, e1)), h);
         const float a[JT] = {e0 / ssum, e1 / ssum};
@@ -235,7 +235,8 @@ __global__ __launch_bounds__(256, 2) void group_l1_6_kernel(
 #pragma unroll
         for (int co = 0; co < 2; ++co)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) x2[co][q] = half_bcast(half_max_hi_nonneg(fmaxf(x1d[co][0][q], x1d[co][1][q])), h);
+            for (int q = 0; q < 16; ++q)
+                x2[co][q] = half_bcast(half_max_hi_nonneg(max_nonneg(x1d[co][0][q], x1d[co][1][q])), h);
         pipe6_jt<4, 1, 1, true>(wt, lane, m1x2, [&](int, int st) { return x2[st >> 4][st & 15]; }, y1, ca, m1x1,
                                 cb);
         pipe6_jt<4, 1, 2, false>(wt, lane, m1x1, [&](int jt, int st) { return x1d[st >> 4][jt][st & 15]; }, y1,
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(256, 2) void group_l1_6_kernel(
         for (int co = 0; co < 2; ++co) {
             f32x16 v;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = half_max_hi_nonneg(fmaxf(y2[co][0][q], y2[co][1][q]));
+            for (int q = 0; q < 16; ++q) v[q] = half_max_hi_nonneg(max_nonneg(y2[co][0][q], y2[co][1][q]));
             store_tile31(desc + (size_t)g * 64, co, v, j, h);
         }
     }

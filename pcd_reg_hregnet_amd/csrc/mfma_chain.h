@@ -167,12 +167,21 @@ __device__ __forceinline__ void beta_tiles(const float *ab, int lane, f32x16 (&a
     load_tiles<COUT_T>(acc, ab + COUT_T * 32, lane >> 5);
 }
 
+// ReLU on the bit patterns: max_i32(x, 0) keeps every non-negative float and maps every
+// negative one (and -0) to +0 -- one v_max_i32, where fmaxf(x, 0) on an MFMA result costs a
+// NaN-canonicalising v_max_f32 x, x first
+__device__ __forceinline__ float relu_i(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+// max of two non-negative floats (ReLU outputs) on the bit patterns
+__device__ __forceinline__ float max_nonneg(float a, float b) {
+    return __int_as_float(max(__float_as_int(a), __float_as_int(b)));
+}
+
 template <int N>
 __device__ __forceinline__ void relu_tiles(f32x16 (&t)[N]) {
 #pragma unroll
     for (int i = 0; i < N; ++i)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) t[i][q] = fmaxf(t[i][q], 0.f);
+        for (int q = 0; q < 16; ++q) t[i][q] = relu_i(t[i][q]);
 }
 
 template <int N>
