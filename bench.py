@@ -258,7 +258,7 @@ def level_kernel(engine, lv: int) -> str:
     b6 = engine.B6_L2 if lv == 2 else engine.B6_L3
     if split:
         return "group_split6_kernel" if b6 else "group_split_kernel"
-    return "group_fused6_kernel" if (lv == 2 and b6) else "group_fused_kernel"
+    return "group_fused6_kernel" if b6 else "group_fused_kernel"
 
 
 def pmc_traffic(kernel: str):

@@ -148,7 +148,10 @@ __device__ __forceinline__ void store_tile31(float *out, int co, const f32x16 &v
     store_tile(out, co, v, j == 31, h);
 }
 
-__global__ __launch_bounds__(256, 2) void group_l1_6_kernel(
+#ifndef HREG_L16_WPS
+#define HREG_L16_WPS 2  // waves per SIMD the register budget targets (A/B builds: 3)
+#endif
+__global__ __launch_bounds__(256, HREG_L16_WPS) void group_l1_6_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     int G, float *__restrict__ kp, float *__restrict__ att_feat, float *__restrict__ desc) {
     constexpr int NE = TABLE_FLOATS - F_END;

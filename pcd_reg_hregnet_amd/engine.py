@@ -40,8 +40,8 @@ FUSED_L2 = True  # level 2 through the fused group_fused kernel (k = 32)
 FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
 # levels 2 / 3 on the channel-split kernel (group_split.hip) instead of the
 # accumulator-chained one (group_fused.hip); measured per level (tools/group_bench.py)
-SPLIT_L2 = False
-SPLIT_L3 = True
+SPLIT_L2 = os.environ.get("HREG_SPLIT_L2", "0") != "0"
+SPLIT_L3 = os.environ.get("HREG_SPLIT_L3", "1") != "0"
 # the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
 # (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
 B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
@@ -848,6 +848,8 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         split = (SPLIT_L2, SPLIT_L3)[lvl - 1]
         if lvl == 1 and B6_L2 and not SPLIT_L2:
             name, table = "hreg_group6_l2", P.l2_table6
+        elif lvl == 2 and B6_L3 and not SPLIT_L3:
+            name, table = "hreg_group6_l3", P.l3_table6
         elif split and (B6_L2, B6_L3)[lvl - 1]:
             name, table = (("hreg_group_split6_l2", P.l2s_table6) if lvl == 1 else
                            ("hreg_group_split6_l3", P.l3s_table6))
@@ -857,7 +859,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         else:
             name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
                            ("hreg_group_l3", P.l3_table))
-        b6 = name in ("hreg_group6_l2", "hreg_group_split6_l2", "hreg_group_split6_l3")
+        b6 = name in ("hreg_group6_l2", "hreg_group6_l3", "hreg_group_split6_l2", "hreg_group_split6_l3")
         pre = (gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl],
                     feats.shape[0]) if LEVEL_PRE else None)
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())
