@@ -10,13 +10,16 @@
 // (engine.l2_table6: [co][chunk][piece][lane] 16-byte pieces, L2-resident, streamed
 // one chunk ahead and across call boundaries as in group_fused.hip).  The 4-column
 // geometry block is one zero-padded chunk.  BN is folded (engine._fold_bn: alpha in the
-// weights, the accumulators start from beta, the epilogue is the ReLU).  Attention, k-max
-// and the stores are group_fused.hip's.
+// weights, the accumulators start from beta, the epilogue is the ReLU).  Attention as in
+// group_fused.hip; the per-channel reductions over a group's rows (attentive feature, x2,
+// descriptor k-max) are butterflies over a tile's 16 values (rowred.h).
 #include "mfma_chain.h"
+#include "rowred.h"
 
 namespace {
 
 using namespace hreg_chain;
+using namespace hreg_rowred;
 
 constexpr int WAVES = 4;
 
@@ -104,7 +107,6 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused6_kernel(
     const bool writer = KN == 32 ? j == 31 : (j & 15) == 15;
     auto gsum_w = [&](float v) { return KN == 32 ? half_sum_hi(v) : row_sum16(v); };
     auto gsum_b = [&](float v) { return KN == 32 ? half_bcast(half_sum_hi(v), h) : row_sum16(v); };
-    auto gmax_w = [&](float v) { return KN == 32 ? half_max_hi_nonneg(v) : row_max16_nonneg(v); };
     auto gmax_b = [&](float v) {
         return KN == 32 ? half_bcast(half_max_hi_nonneg(v), h) : row_max16_nonneg(v);
     };
@@ -166,10 +168,10 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused6_kernel(
         }
 #pragma unroll
         for (int co = 0; co < T3; ++co) {
-            f32x16 v;
+            float v[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = gsum_w(fmul_rn(emb[co][q], a));
-            store_tile(att_feat + (size_t)g * C3, co, v, writer, h);
+            for (int q = 0; q < 16; ++q) v[q] = fmul_rn(emb[co][q], a);
+            reduce_store<KN, Sum>(att_feat + (size_t)g * C3, co, v, lane);
         }
 
         // ---- mlp1 = W [x2 | x1d | emb * a] -> CM1, the emb * a part first
@@ -195,9 +197,16 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused6_kernel(
 
 #pragma unroll
         for (int ct = 0; ct < T3; ++ct) {
-            f32x16 x2;
+            float x2[16];
+            if constexpr (KN == 32) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) x2[q] = gmax_b(x1d[ct][q]);
+                for (int q = 0; q < 16; ++q) x2[q] = x1d[ct][q];
+                bfly32<MaxNN>(x2, lane);
+                bcast32(x2, lane);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) x2[q] = row_max16_nonneg(x1d[ct][q]);
+            }
             const FragSeq cur{m1x2.base + ct * 2, m1x2.stride};
             const FragSeq nxt = ct + 1 < T3 ? FragSeq{m1x2.base + (ct + 1) * 2, m1x2.stride} : m1x1;
             if (ct & 1)
@@ -217,10 +226,10 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused6_kernel(
         relu_tiles(y2);
 #pragma unroll
         for (int co = 0; co < TM2; ++co) {
-            f32x16 v;
+            float v[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = gmax_w(y2[co][q]);
-            store_tile(desc + (size_t)g * CM2, co, v, writer, h);
+            for (int q = 0; q < 16; ++q) v[q] = y2[co][q];
+            reduce_store<KN, MaxNN>(desc + (size_t)g * CM2, co, v, lane);
         }
     }
 }

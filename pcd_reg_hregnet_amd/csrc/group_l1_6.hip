@@ -17,13 +17,18 @@
 //    through the descriptor stack), then the x2 and x1d blocks;
 //  * BN folded (engine._fold_bn): alpha in the weight pieces, the accumulators start from
 //    beta, the epilogue is the ReLU;
+//  * the per-channel reductions over the 64 rows (attentive feature, x2, descriptor k-max)
+//    combine the two row tiles in registers, then run as butterflies over a tile's 16
+//    values (rowred.h) and store from the reduced slots;
 //  * built without packed fp32 VALU ops (build.NO_PACKED_F32): with them this kernel gave
 //    nondeterministic wrong accumulator values whenever two waves shared a SIMD.
 #include "mfma_chain.h"
+#include "rowred.h"
 
 namespace {
 
 using namespace hreg_chain;
+using namespace hreg_rowred;
 
 constexpr int WAVES = 4;
 constexpr int KN = 64;  // neighbours per group (level 1)
@@ -144,10 +149,6 @@ __device__ __forceinline__ void conv_stack6(const gu32x4 *__restrict__ wt, const
     relu_jt(out);
 }
 
-__device__ __forceinline__ void store_tile31(float *out, int co, const f32x16 &v, int j, int h) {
-    store_tile(out, co, v, j == 31, h);
-}
-
 #ifndef HREG_L16_WPS
 #define HREG_L16_WPS 2  // waves per SIMD the register budget targets (A/B builds: 3)
 #endif
@@ -216,11 +217,10 @@ __global__ __launch_bounds__(256, HREG_L16_WPS) void group_l1_6_kernel(
         }
 #pragma unroll
         for (int co = 0; co < 2; ++co) {
-            f32x16 v;
+            float v[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                v[q] = half_sum_hi(fadd_rn(fmul_rn(emb[co][0][q], a[0]), fmul_rn(emb[co][1][q], a[1])));
-            store_tile31(att_feat + (size_t)g * 64, co, v, j, h);
+            for (int q = 0; q < 16; ++q) v[q] = fadd_rn(fmul_rn(emb[co][0][q], a[0]), fmul_rn(emb[co][1][q], a[1]));
+            reduce_store<32, Sum>(att_feat + (size_t)g * 64, co, v, lane);
         }
 
         // ---- mlp1 = W [x2 | x1d | emb * a] -> 32, the emb * a block first
@@ -234,12 +234,14 @@ __global__ __launch_bounds__(256, HREG_L16_WPS) void group_l1_6_kernel(
         f32x16 x1d[2][JT];
         conv_stack6<1>(wt, eb, G_EC1, G_EC2, G_EC3, E_EC1, E_EC2, E_EC3, lane, gin, x1d, cb, m1x2, ca);
         // x2 = max over the 64 rows (the repeat of layers.py:204: same for every row)
-        f32x16 x2[2];
+        float x2[2][16];
 #pragma unroll
-        for (int co = 0; co < 2; ++co)
+        for (int co = 0; co < 2; ++co) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                x2[co][q] = half_bcast(half_max_hi_nonneg(max_nonneg(x1d[co][0][q], x1d[co][1][q])), h);
+            for (int q = 0; q < 16; ++q) x2[co][q] = max_nonneg(x1d[co][0][q], x1d[co][1][q]);
+            bfly32<MaxNN>(x2[co], lane);
+            bcast32(x2[co], lane);
+        }
         pipe6_jt<4, 1, 1, true>(wt, lane, m1x2, [&](int, int st) { return x2[st >> 4][st & 15]; }, y1, ca, m1x1,
                                 cb);
         pipe6_jt<4, 1, 2, false>(wt, lane, m1x1, [&](int jt, int st) { return x1d[st >> 4][jt][st & 15]; }, y1,
@@ -254,10 +256,10 @@ __global__ __launch_bounds__(256, HREG_L16_WPS) void group_l1_6_kernel(
         relu_jt(y2);
 #pragma unroll
         for (int co = 0; co < 2; ++co) {
-            f32x16 v;
+            float v[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = half_max_hi_nonneg(max_nonneg(y2[co][0][q], y2[co][1][q]));
-            store_tile31(desc + (size_t)g * 64, co, v, j, h);
+            for (int q = 0; q < 16; ++q) v[q] = max_nonneg(y2[co][0][q], y2[co][1][q]);
+            reduce_store<32, MaxNN>(desc + (size_t)g * 64, co, v, lane);
         }
     }
 }
