@@ -152,6 +152,7 @@ MFMA_ENTRIES = {
     "hreg_group_split_l2": ("level", _level_work(2)),
     "hreg_group_split_l3": ("level", _level_work(3)),
     "hreg_group6_l2": ("level", _level_work(2)),
+    "hreg_group6x2_l2": ("level", _level_work(2)),
     "hreg_group_split6_l2": ("level", _level_work(2)),
     "hreg_group_split6_l3": ("level", _level_work(3)),
     "hreg_group6_l3": ("level", _level_work(3)),
@@ -258,6 +259,8 @@ def level_kernel(engine, lv: int) -> str:
     b6 = engine.B6_L2 if lv == 2 else engine.B6_L3
     if split:
         return "group_split6_kernel" if b6 else "group_split_kernel"
+    if b6 and lv == 2 and engine.PAIR_L2 and engine.LEVEL_PRE:
+        return "group_pair6_kernel"
     return "group_fused6_kernel" if b6 else "group_fused_kernel"
 
 

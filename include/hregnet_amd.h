@@ -493,6 +493,12 @@ int hreg_group6_l2_table_floats(void);
 int hreg_group6_l2(const float *table, const float *geom, const float *knn_xyz,
                    const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                    float *desc, const float *pre, void *stream);
+/* hreg_group6_l2 in its pair form: two 32-row groups per wave share every streamed
+ * weight chunk (half the L2 -> CU weight bytes per row); same table and arguments, pre
+ * required; bitwise-identical outputs. */
+int hreg_group6x2_l2(const float *table, const float *geom, const float *knn_xyz,
+                     const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
+                     float *desc, const float *pre, void *stream);
 /* The channel-split stages (hreg_group_split_l{2,3}) with fp32-accurate products on the
  * bf16 matrix cores (bf16x6, group_split6.hip): same arguments and outputs, table =
  * hreg_group_split6_l{2,3}_table_floats() floats (engine.split_table6), 16-byte aligned. */

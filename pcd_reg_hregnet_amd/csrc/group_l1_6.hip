@@ -22,17 +22,17 @@
 //    values (rowred.h) and store from the reduced slots;
 //  * built without packed fp32 VALU ops (build.NO_PACKED_F32): with them this kernel gave
 //    nondeterministic wrong accumulator values whenever two waves shared a SIMD.
-#include "mfma_chain.h"
+#include "mfma_jt.h"
 #include "rowred.h"
 
 namespace {
 
 using namespace hreg_chain;
+using namespace hreg_jt;
 using namespace hreg_rowred;
 
 constexpr int WAVES = 4;
-constexpr int KN = 64;  // neighbours per group (level 1)
-constexpr int JT = 2;   // 32-row tiles per group
+constexpr int KN = 64;  // neighbours per group (level 1) = JT 32-row tiles
 
 // chunk-fragment table (units of 3 pieces x 64 lanes x 16 B), engine.l1_table6
 constexpr int G_DC1 = 0;             // det conv1 (geom, 2 k-steps zero-padded): 1 co x 1 chunk
@@ -49,85 +49,9 @@ constexpr int E_DC1 = F_END, E_DC2 = E_DC1 + 64, E_DC3 = E_DC2 + 64, E_EC1 = E_D
               E_EC2 = E_EC1 + 64, E_EC3 = E_EC2 + 64, E_M1 = E_EC3 + 128, E_M2 = E_M1 + 64,
               TABLE_FLOATS = E_M2 + 128;
 
-typedef u32x4 Carry[CARRY6][3];
-
-// acc[co][jt] += sum_{c < NCH} A(co, c) x B_jt(c), B_jt(c) = split(bval(jt, 8c .. 8c+7));
-// the A pieces of a chunk are loaded once for both row tiles.  SAMEB: B does not depend
-// on jt (split once).  cin / cout as mfma_pipe6 (double-buffered: COUT_T <= 2 here).
-template <int NCH, int COUT_T, int NCOUT, bool SAMEB, class BVal>
-__device__ __forceinline__ void pipe6_jt(const gu32x4 *__restrict__ wt, int lane, FragSeq f, BVal bval,
-                                         f32x16 (&acc)[COUT_T][JT], const Carry &cin, FragSeq nf,
-                                         Carry &cout) {
-    static_assert(COUT_T <= CARRY6 && NCOUT <= CARRY6, "carry");
-    constexpr int NB = SAMEB ? 1 : JT;
-    u32x4 buf[2][COUT_T][3];
-#pragma unroll
-    for (int co = 0; co < COUT_T; ++co)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) buf[0][co][p] = cin[co][p];
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        if (c + 1 < NCH) {
-#pragma unroll
-            for (int co = 0; co < COUT_T; ++co) ld6(wt, f.base + co * f.stride + c + 1, lane, buf[(c + 1) & 1][co]);
-        } else {
-#pragma unroll
-            for (int co = 0; co < NCOUT; ++co) ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
-        }
-        u32x4 b[NB][3];
-#pragma unroll
-        for (int jb = 0; jb < NB; ++jb) {
-            float x[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = bval(jb, 8 * c + i);
-            split8(x, b[jb]);
-        }
-#pragma unroll
-        for (int co = 0; co < COUT_T; ++co)
-#pragma unroll
-            for (int jt = 0; jt < JT; ++jt) acc[co][jt] = mma6(buf[c & 1][co], b[SAMEB ? 0 : jt], acc[co][jt]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-template <int N>
-__device__ __forceinline__ void zero_jt(f32x16 (&t)[N][JT]) {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-        for (int jt = 0; jt < JT; ++jt) t[i][jt] = zero16();
-}
-
-// folded BN (mfma_chain.h beta_tiles): both row tiles start from the layer's beta; the
-// epilogue is the ReLU
-template <int COUT_T>
-__device__ __forceinline__ void beta_jt(const float *ab, int lane, f32x16 (&acc)[COUT_T][JT]) {
-#pragma unroll
-    for (int co = 0; co < COUT_T; ++co)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float4 b = *reinterpret_cast<const float4 *>(ab + COUT_T * 32 + co * 32 + 8 * r + 4 * (lane >> 5));
-#pragma unroll
-            for (int jt = 0; jt < JT; ++jt) {
-                acc[co][jt][4 * r] = b.x; acc[co][jt][4 * r + 1] = b.y;
-                acc[co][jt][4 * r + 2] = b.z; acc[co][jt][4 * r + 3] = b.w;
-            }
-        }
-}
-
-template <int N>
-__device__ __forceinline__ void relu_jt(f32x16 (&t)[N][JT]) {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-        for (int jt = 0; jt < JT; ++jt)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) t[i][jt][q] = relu_i(t[i][jt][q]);
-}
-
 // conv stack 4 -> 32 -> 32 -> 64 (+ BN/ReLU); NC: output tiles of the call that follows
-template <int NC>
-__device__ __forceinline__ void conv_stack6(const gu32x4 *__restrict__ wt, const float *eb, int g1, int g2, int g3,
+template <int NC, class WP>
+__device__ __forceinline__ void conv_stack6(WP wt, const float *eb, int g1, int g2, int g3,
                                             int e1, int e2, int e3, int lane, const float2 (&gin)[JT],
                                             f32x16 (&out)[2][JT], const Carry &cin, FragSeq next, Carry &cout) {
     f32x16 h1[1][JT], h2[1][JT];
@@ -163,17 +87,18 @@ __global__ __launch_bounds__(256, HREG_L16_WPS) void group_l1_6_kernel(
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
     const FragSeq m1x2{G_M1, 12}, m1x1{G_M1 + 4, 12}, m1em{G_M1 + 8, 12}, m2{G_M2, 2};
-
-    Carry carry;
-    {
-        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table));
-        ld6(wt, G_DC1, lane, carry[0]);
-    }
-    for (int g = blockIdx.x * WAVES + w; g < G; g += gridDim.x * WAVES) {
-        // opaque per-group table pointer: keeps the loop-invariant weight loads in the loop
+    // opaque per-group table pointer: keeps the loop-invariant weight loads in the loop
+    // (an LDS-resident copy of the table measured 1.5x slower: lgkmcnt-bound fragment reads)
+    auto table_ptr = [&]() {
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
-        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
+        return reinterpret_cast<const gu32x4 *>(tba);
+    };
+
+    Carry carry;
+    ld6(table_ptr(), G_DC1, lane, carry[0]);
+    for (int g = blockIdx.x * WAVES + w; g < G; g += gridDim.x * WAVES) {
+        const auto wt = table_ptr();
         const size_t r0 = (size_t)g * KN;
         float2 gin[JT];
 #pragma unroll

@@ -262,8 +262,22 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
+// tools/b6_experiment.py timing variants (results wrong): 2 = weight pieces not loaded
+// (ld6 leaves its registers as they are), 5 = B not split (the hi piece for all three)
+#ifndef HREG_B6_EXP
+#define HREG_B6_EXP 0
+#endif
+
 // 8 fp32 values (one lane's chunk of B) -> hi / mid / lo packed bf16x8
 __device__ __forceinline__ void split8(const float (&x)[8], u32x4 (&o)[3]) {
+    if constexpr (HREG_B6_EXP == 5) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            o[0][i] = __builtin_amdgcn_perm(__float_as_uint(x[2 * i + 1]), __float_as_uint(x[2 * i]), 0x07060302u);
+        o[1] = o[0];
+        o[2] = o[0];
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         uint32_t hb[2], mb[2], lb[2];
@@ -304,9 +318,41 @@ constexpr int CARRY6 = 8;  // output tiles of a call's first chunk carried betwe
 // (signed pointer arithmetic: a wave-uniform f stays an SGPR base, the lane a VGPR offset,
 // the piece an immediate -- no per-fragment VGPR address to hoist and spill)
 __device__ __forceinline__ void ld6(const gu32x4 *__restrict__ wt, int f, int lane, u32x4 (&o)[3]) {
+    if constexpr (HREG_B6_EXP == 2) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(o[p]));
+        return;
+    }
     const gu32x4 *fp = wt + f * 192;
 #pragma unroll
     for (int p = 0; p < 3; ++p) o[p] = fp[p * 64 + lane];
+}
+
+// Software-pipelined split (HREG_SWP, default on): chunk c + 1's B operand is split into its
+// pieces while chunk c's MFMAs run, the scheduler asked (sched_group_barrier) to place
+// about NVALU / NMFMA VALU instructions after each MFMA -- an MFMA holds the SIMD's vector
+// issue for 8 of its 32 cycles, so ~5 independent VALU per 32x32x16 MFMA issue in its
+// shadow instead of as a 44-instruction block between two MFMAs.
+#ifndef HREG_SWP
+#define HREG_SWP 1
+#endif
+
+template <int NMFMA, int NVALU>
+__device__ __forceinline__ void interleave_mfma_valu() {
+    constexpr int V = (NVALU + NMFMA - 1) / NMFMA;
+#pragma unroll
+    for (int k = 0; k < NMFMA; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, V, 0);  // then V VALU
+    }
+}
+
+template <class BVal>
+__device__ __forceinline__ void split_chunk(BVal bval, int c, u32x4 (&b)[3]) {
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = bval(8 * c + i);
+    split8(x, b);
 }
 
 // acc[co] += sum_{c < NCH} A(co, c) x B(c) with B(c) = split(bval(8c .. 8c+7)); chunk
@@ -327,21 +373,26 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
         for (int co = 0; co < COUT_T; ++co)
 #pragma unroll
             for (int p = 0; p < 3; ++p) rb[co][p] = cin[co][p];
+        u32x4 bs[2][3];
+        if constexpr (HREG_SWP) split_chunk(bval, 0, bs[0]);
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
-            float x[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = bval(8 * c + i);
-            u32x4 b[3];
-            split8(x, b);
+            if constexpr (!HREG_SWP) split_chunk(bval, c, bs[c & 1]);
 #pragma unroll
             for (int co = 0; co < COUT_T; ++co) {
-                acc[co] = mma6(rb[co], b, acc[co]);
+                acc[co] = mma6(rb[co], bs[c & 1], acc[co]);
                 if (c + 1 < NCH)
                     ld6(wt, f.base + co * f.stride + c + 1, lane, rb[co]);
                 else if (co < NCOUT)
                     ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
-                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (!HREG_SWP) __builtin_amdgcn_sched_barrier(0);
+            }
+            if constexpr (HREG_SWP) {
+                if (c + 1 < NCH) {
+                    split_chunk(bval, c + 1, bs[(c + 1) & 1]);
+                    interleave_mfma_valu<6 * COUT_T, 48>();
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
         }
 #pragma unroll
@@ -353,6 +404,8 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
     for (int co = 0; co < COUT_T; ++co)
 #pragma unroll
         for (int p = 0; p < 3; ++p) buf[0][co][p] = cin[co][p];
+    u32x4 bs[2][3];
+    if constexpr (HREG_SWP) split_chunk(bval, 0, bs[0]);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         if (c + 1 < NCH) {
@@ -362,14 +415,18 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
 #pragma unroll
             for (int co = 0; co < NCOUT; ++co) ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
         }
-        float x[8];
+        if constexpr (!HREG_SWP) split_chunk(bval, c, bs[c & 1]);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = bval(8 * c + i);
-        u32x4 b[3];
-        split8(x, b);
-#pragma unroll
-        for (int co = 0; co < COUT_T; ++co) acc[co] = mma6(buf[c & 1][co], b, acc[co]);
-        __builtin_amdgcn_sched_barrier(0);
+        for (int co = 0; co < COUT_T; ++co) acc[co] = mma6(buf[c & 1][co], bs[c & 1], acc[co]);
+        if constexpr (HREG_SWP) {
+            if (c + 1 < NCH) {
+                split_chunk(bval, c + 1, bs[(c + 1) & 1]);
+                interleave_mfma_valu<6 * COUT_T, 48>();
+            }
+        }
+        // HREG_SWP: no barrier after the last chunk -- the next call's ReLU + first split
+        // (which waits only for tile 0's result) may issue under this chunk's last MFMAs
+        if (!HREG_SWP || c + 1 < NCH) __builtin_amdgcn_sched_barrier(0);
     }
 }
 

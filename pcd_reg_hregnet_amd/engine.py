@@ -45,6 +45,10 @@ SPLIT_L3 = os.environ.get("HREG_SPLIT_L3", "1") != "0"
 # the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
 # (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
 B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
+# level 2 on the pair form of the bf16x6 kernel (two groups per wave: half the weight
+# bytes streamed per row, hreg_group6x2_l2).  Off: at one wave per SIMD it measured level
+# with the one-group kernel (183 vs 184 us; tools/b6_experiment.py: 180 vs 182 us)
+PAIR_L2 = os.environ.get("HREG_PAIR_L2", "0") != "0"
 B6_L1 = os.environ.get("HREG_B6_L1", "1") != "0"  # group_l1_6.hip for level 1
 # level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
 # (group_split6.hip)
@@ -847,7 +851,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         desc = _empty(G, LEVELS[lvl][5], device=dev)
         split = (SPLIT_L2, SPLIT_L3)[lvl - 1]
         if lvl == 1 and B6_L2 and not SPLIT_L2:
-            name, table = "hreg_group6_l2", P.l2_table6
+            name, table = ("hreg_group6x2_l2" if PAIR_L2 and LEVEL_PRE else "hreg_group6_l2"), P.l2_table6
         elif lvl == 2 and B6_L3 and not SPLIT_L3:
             name, table = "hreg_group6_l3", P.l3_table6
         elif split and (B6_L2, B6_L3)[lvl - 1]:
@@ -859,7 +863,8 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         else:
             name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
                            ("hreg_group_l3", P.l3_table))
-        b6 = name in ("hreg_group6_l2", "hreg_group6_l3", "hreg_group_split6_l2", "hreg_group_split6_l3")
+        b6 = name in ("hreg_group6_l2", "hreg_group6x2_l2", "hreg_group6_l3", "hreg_group_split6_l2",
+                      "hreg_group_split6_l3")
         pre = (gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl],
                     feats.shape[0]) if LEVEL_PRE else None)
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())

@@ -251,6 +251,37 @@ def test_fused_level_matches_layerwise(net, lvl, split, pre, b6, monkeypatch):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("G", [1, 5, 64, 1000])
+def test_pair_l2_matches_single(G):
+    """hreg_group6x2_l2 (two groups per wave sharing each streamed weight chunk) against
+    hreg_group6_l2 on random tables and rows: the same arithmetic per row, so bitwise equal,
+    odd G (the last pair recomputes its group) included."""
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(G)
+    nrows = 3 * G + 7
+
+    def t(x):
+        return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).cuda()
+
+    tb = t(rng.normal(0, 0.05, L.hreg_group6_l2_table_floats()))
+    geom, kx = t(rng.normal(size=(G * 32, 4))), t(rng.normal(size=(G * 32, 3)))
+    gidx = torch.from_numpy(rng.integers(0, nrows, G * 32).astype(np.int32)).cuda()
+    feats = t(np.abs(rng.normal(size=(nrows, 64))))
+    pre = t(rng.normal(size=(nrows, 128)))
+    outs = []
+    for name in ("hreg_group6_l2", "hreg_group6x2_l2"):
+        kp = torch.full((G, 3), float("nan"), device="cuda")
+        att = torch.full((G, 128), float("nan"), device="cuda")
+        desc = torch.full((G, 128), float("nan"), device="cuda")
+        _lib.call(name, tb, geom, kx, gidx, feats, G, kp, att, desc, pre, _lib.stream_handle())
+        outs.append((kp, att, desc))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert not torch.isnan(b).any()
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("pre,b6", [(True, True), (True, False), (False, False)])
 @pytest.mark.parametrize("name,C,N", [("fine_corres_1", 64, 1024), ("fine_corres_2", 128, 512)])
 def test_fused_fine_head_matches_layerwise(net, name, C, N, pre, b6, monkeypatch):

@@ -1,18 +1,22 @@
-"""Build an alternative libhregnet_amd (A/B and hazard experiments): one csrc file
-recompiled with extra -D flags, linked with the other in-tree objects.
-usage: python tools/build_variant.py OUT.so csrc_file.hip -DNAME=VALUE ...
+"""Build an alternative libhregnet_amd (A/B and hazard experiments): csrc files
+(comma-separated) recompiled with extra -D flags, linked with the other in-tree objects.
+usage: python tools/build_variant.py OUT.so csrc_file.hip[,other.hip] -DNAME=VALUE ...
 Select it at run time with HREG_LIB=OUT.so."""
 import glob, os, subprocess, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pcd_reg_hregnet_amd import build as b
 
-out, src, defs = sys.argv[1], sys.argv[2], sys.argv[3:]
+out, srcs, defs = sys.argv[1], sys.argv[2].split(","), sys.argv[3:]
 b.build()
-srcp = os.path.join(b.CSRC, src)
-obj = out + "." + src.replace(".hip", ".o")
-subprocess.check_call([b.HIPCC, *b.CFLAGS, *b.FILE_FLAGS.get(src, []), *defs, "-c", srcp, "-o", obj])
-objs = [o for o in sorted(glob.glob(os.path.join(b.OBJDIR, "*.o")))
-        if os.path.basename(o) != src.replace(".hip", ".o")] + [obj]
+new = []
+for src in srcs:
+    obj = out + "." + src.replace(".hip", ".o")
+    subprocess.check_call([b.HIPCC, *b.CFLAGS, *b.FILE_FLAGS.get(src, []), *defs, "-c",
+                           os.path.join(b.CSRC, src), "-o", obj])
+    new.append(obj)
+skip = {s.replace(".hip", ".o") for s in srcs}
+objs = [o for o in sorted(glob.glob(os.path.join(b.OBJDIR, "*.o"))) if os.path.basename(o) not in skip] + new
 subprocess.check_call([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", out, *objs])
-os.remove(obj)
+for obj in new:
+    os.remove(obj)
 print(out)
