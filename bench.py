@@ -248,7 +248,7 @@ def entry_peak(name: str) -> float:
     """MFMA peak (fp32-equivalent TFLOP/s) of a C-ABI entry's kernel: bf16x6 kernels
     (hreg_group_l1_6, hreg_group6_*, hreg_group_split6_*, hreg_*_head6) run on the bf16
     matrix cores, the others on v_mfma_f32_32x32x2_f32."""
-    return PEAK_B6_TFLOPS if name.endswith("6") or "6_" in name else PEAK_FP32_MFMA_TFLOPS
+    return PEAK_B6_TFLOPS if name.endswith("6") or "6_" in name or "6x2_" in name else PEAK_FP32_MFMA_TFLOPS
 
 
 def level_kernel(engine, lv: int) -> str:
