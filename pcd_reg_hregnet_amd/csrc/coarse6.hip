@@ -37,18 +37,29 @@ constexpr int F_END = G_END * 3 * 64 * 4;
 constexpr int NE = 6 * C;            // alpha, beta of the three layers
 constexpr int TABLE = F_END + NE;
 
+// HREG_COARSE_JT: 32-row tiles per workgroup.  2: every wave computes its P output tiles
+// for both row tiles, so each streamed weight chunk feeds twice the MFMAs (the one-tile
+// weight stream, 512 B of pieces per MFMA, keeps the CU's texture-data return unit ~82 %
+// busy) -- but the 64-row activation buffer (132 KB) leaves one workgroup per CU, and at
+// half the waves it measured slower (154 vs 134 us).  Default 1.
+#ifndef HREG_COARSE_JT
+#define HREG_COARSE_JT 1
+#endif
+constexpr int JT = HREG_COARSE_JT, RW = 32 * JT;  // row tiles / rows per workgroup
+
 __global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
     const float *__restrict__ table, const float *__restrict__ small, const float *__restrict__ ud0,
     const float *__restrict__ ud1, const int32_t *__restrict__ gidx, const float *__restrict__ knn_xyz, int G,
     float *__restrict__ corres, float *__restrict__ att) {
     __shared__ float ep[NE];
-    __shared__ __attribute__((aligned(16))) float sA[32 * LDSW];
-    __shared__ int sMax[CW][32];
+    __shared__ __attribute__((aligned(16))) float sA[RW * LDSW];
+    __shared__ int sMax[CW][RW];
     for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[F_END + i];
     __syncthreads();  // the first tile's layer-1 epilogue reads ep before any tile_sync
     const int lane = threadIdx.x & 63, cw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
-    const int NT = G * KH / 32;
+    const int NT = G * KH / 32;             // 32-row tiles
+    const int NW = (NT + JT - 1) / JT;      // workgroup steps (a last odd tile is recomputed)
     const int c0 = cw * P;
     const FragSeq g1{G_1 + c0, 1}, g2{G_2 + c0 * NCH, NCH}, g3{G_3 + c0 * NCH, NCH};
     const bool writer = (j & 7) == 7;
@@ -59,80 +70,124 @@ __global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
 #pragma unroll
         for (int i = 0; i < P; ++i) ld6(wt, g1.base + i, lane, carry[i]);
     }
-    for (int t = blockIdx.x; t < NT; t += gridDim.x) {
+    for (int tw = blockIdx.x; tw < NW; tw += gridDim.x) {
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
-        const int row = t * 32 + j, g = row / KH;
+        int row[JT], g[JT];
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) {
+            row[jt] = min(tw * JT + jt, NT - 1) * 32 + j;
+            g[jt] = row[jt] / KH;
+        }
         Carry6 ca, cb;
 
         // ---- convs_1[0]: precomputed desc / knn_desc products + the 16 small columns
         // (k-step s of lane half h <-> column 8h + s: one chunk)
-        f32x16 y[P];
-        init_from_rows<C, P>(y, ud0 + (size_t)g * C + c0 * 32, ud1 + (size_t)gidx[row] * C + c0 * 32, h);
-        {
-            const float4 s0 = *reinterpret_cast<const float4 *>(small + (size_t)row * 16 + h * 8);
-            const float4 s1 = *reinterpret_cast<const float4 *>(small + (size_t)row * 16 + h * 8 + 4);
-            const float sm[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-            mfma_pipe6<1, P, P>(wt, lane, g1, [&](int st) { return sm[st]; }, y, carry, g2, ca);
+        f32x16 y[P][JT];
+        float sm[JT][8];
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) {
+            f32x16 yt[P];
+            init_from_rows<C, P>(yt, ud0 + (size_t)g[jt] * C + c0 * 32, ud1 + (size_t)gidx[row[jt]] * C + c0 * 32,
+                                 h);
+#pragma unroll
+            for (int i = 0; i < P; ++i) y[i][jt] = yt[i];
+            const float4 s0 = *reinterpret_cast<const float4 *>(small + (size_t)row[jt] * 16 + h * 8);
+            const float4 s1 = *reinterpret_cast<const float4 *>(small + (size_t)row[jt] * 16 + h * 8 + 4);
+            sm[jt][0] = s0.x; sm[jt][1] = s0.y; sm[jt][2] = s0.z; sm[jt][3] = s0.w;
+            sm[jt][4] = s1.x; sm[jt][5] = s1.y; sm[jt][6] = s1.z; sm[jt][7] = s1.w;
         }
+        pipe_lds6_jt<1, P, P, JT>(wt, lane, g1, [&](int jt, int st0, float (&v)[4]) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = sm[jt][st0 + k];
+        }, y, carry, g2, ca);
         // folded BN (engine._fold_bn: alpha in W_small and in the ud0 / ud1 weights): + beta, ReLU
 #pragma unroll
         for (int i = 0; i < P; ++i)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) y[i][q] = relu_i(fadd_rn(y[i][q], ep[C + chan(c0 + i, q, h)]));
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    y[i][jt][q] = relu_i(fadd_rn(y[i][jt][q], ep[C + chan(c0 + i, q, h)]));
         tile_sync();  // the previous tile's readers of sA are done
 #pragma unroll
-        for (int i = 0; i < P; ++i) put_tile<LDSW>(sA, c0 + i, j, h, y[i]);
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int i = 0; i < P; ++i) put_tile<LDSW>(sA + jt * 32 * LDSW, c0 + i, j, h, y[i][jt]);
         tile_sync();
 
         // ---- convs_1[1]
-        beta_p<P, C>(ep + 2 * C, c0, h, y);
-        pipe_lds6<NCH, P, P>(wt, lane, g2, ChanB{sA + j * LDSW, h}, y, ca, g3, cb);
-        relu_tiles(y);
-        tile_sync();  // every wave has read the layer input
 #pragma unroll
-        for (int i = 0; i < P; ++i) put_tile<LDSW>(sA, c0 + i, j, h, y[i]);
-        tile_sync();
-
-        // ---- convs_1[2]; prefetches the next tile's first chunk
-        beta_p<P, C>(ep + 4 * C, c0, h, y);
-        pipe_lds6<NCH, P, P>(wt, lane, g3, ChanB{sA + j * LDSW, h}, y, cb, g1, carry);
-        relu_tiles(y);
-
-        // ---- attention: row max over the 512 channels (ReLU outputs: integer max on the
-        // bit patterns; per wave, then across the waves through LDS), softmax over the 8 rows
-        int mi = __float_as_int(y[0][0]);
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int i = 0; i < P; ++i) load_tiles<1>(*reinterpret_cast<f32x16(*)[1]>(&y[i][jt]), ep + 3 * C + (c0 + i) * 32, h);
+        pipe_lds6_jt<NCH, P, P, JT>(wt, lane, g2, ChanBJ<LDSW>{sA + j * LDSW, h}, y, ca, g3, cb);
 #pragma unroll
         for (int i = 0; i < P; ++i)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(y[i][q]));
-        mi = max(mi, __shfl_xor(mi, 32));
-        if (h == 0) sMax[cw][j] = mi;
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) y[i][jt][q] = relu_i(y[i][jt][q]);
+        tile_sync();  // every wave has read the layer input
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int i = 0; i < P; ++i) put_tile<LDSW>(sA + jt * 32 * LDSW, c0 + i, j, h, y[i][jt]);
         tile_sync();
-        int xm = sMax[0][j];
+
+        // ---- convs_1[2]; prefetches the next step's first chunk
 #pragma unroll
-        for (int c = 1; c < CW; ++c) xm = max(xm, sMax[c][j]);
-        const float x1 = __int_as_float(xm);
-        const float e = expf(fsub_rn(x1, grp8_max_nonneg(x1)));
-        const float a = e / grp8_sum(e);
-        if (cw == 0) {
-            const float *p = knn_xyz + (size_t)row * 3;
-            const float cx = grp8_sum(fmul_rn(a, p[0]));
-            const float cy = grp8_sum(fmul_rn(a, p[1]));
-            const float cz = grp8_sum(fmul_rn(a, p[2]));
-            if (writer && h == 0) {
-                corres[(size_t)g * 3 + 0] = cx;
-                corres[(size_t)g * 3 + 1] = cy;
-                corres[(size_t)g * 3 + 2] = cz;
-            }
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int i = 0; i < P; ++i) load_tiles<1>(*reinterpret_cast<f32x16(*)[1]>(&y[i][jt]), ep + 5 * C + (c0 + i) * 32, h);
+        pipe_lds6_jt<NCH, P, P, JT>(wt, lane, g3, ChanBJ<LDSW>{sA + j * LDSW, h}, y, cb, g1, carry);
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) y[i][jt][q] = relu_i(y[i][jt][q]);
+
+        // ---- attention: row max over the 512 channels (ReLU outputs: integer max on the
+        // bit patterns; per wave, then across the waves through LDS), softmax over the 8 rows
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) {
+            int mi = __float_as_int(y[0][jt][0]);
+#pragma unroll
+            for (int i = 0; i < P; ++i)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(y[i][jt][q]));
+            mi = max(mi, __shfl_xor(mi, 32));
+            if (h == 0) sMax[cw][jt * 32 + j] = mi;
         }
+        tile_sync();
 #pragma unroll
-        for (int i = 0; i < P; ++i) {
-            f32x16 v;
+        for (int jt = 0; jt < JT; ++jt) {
+            int xm = sMax[0][jt * 32 + j];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = grp8_sum(fmul_rn(y[i][q], a));
-            store_tile(att + (size_t)g * C, c0 + i, v, writer, h);
+            for (int c = 1; c < CW; ++c) xm = max(xm, sMax[c][jt * 32 + j]);
+            const float x1 = __int_as_float(xm);
+            const float e = expf(fsub_rn(x1, grp8_max_nonneg(x1)));
+            const float a = e / grp8_sum(e);
+            if (cw == 0) {
+                const float *p = knn_xyz + (size_t)row[jt] * 3;
+                const float cx = grp8_sum(fmul_rn(a, p[0]));
+                const float cy = grp8_sum(fmul_rn(a, p[1]));
+                const float cz = grp8_sum(fmul_rn(a, p[2]));
+                if (writer && h == 0) {
+                    corres[(size_t)g[jt] * 3 + 0] = cx;
+                    corres[(size_t)g[jt] * 3 + 1] = cy;
+                    corres[(size_t)g[jt] * 3 + 2] = cz;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                f32x16 v;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = grp8_sum(fmul_rn(y[i][jt][q], a));
+                store_tile(att + (size_t)g[jt] * C, c0 + i, v, writer, h);
+            }
         }
     }
 }
@@ -152,8 +207,9 @@ extern "C" int hreg_coarse_head6(const float *table, const float *small, const f
         return HREG_ERR_INVALID;
     if ((G * KH) % 32) return HREG_ERR_INVALID;  // whole 32-row tiles
     if (!G) return HREG_OK;
-    const int NT = G * KH / 32;
-    int grid = NT < 1024 ? NT : 1024;  // two resident workgroups per CU, two rounds
+    const int NW = (G * KH / 32 + JT - 1) / JT;
+    const int cap = JT == 1 ? 1024 : 512;  // two rounds of the resident workgroups (2 / 1 per CU)
+    const int grid = NW < cap ? NW : cap;
     hipLaunchKernelGGL(coarse_head6_kernel, dim3(grid), dim3(CW * 64), 0, as_stream(stream), table, small, ud0,
                        ud1, gidx, knn_xyz, G, corres, att);
     HREG_CHECK_LAUNCH();

@@ -48,6 +48,9 @@ __device__ __forceinline__ void pipe6_jt(WP wt, int lane, FragSeq f, BVal bval,
 #pragma unroll
             for (int co = 0; co < NCOUT; ++co) ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
         }
+#ifdef HREG_PIN_PREFETCH
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this chunk's MFMAs
+#endif
         if constexpr (!HREG_SWP) split_jt(c, b[c & 1]);
 #pragma unroll
         for (int co = 0; co < COUT_T; ++co)

@@ -161,6 +161,52 @@ __device__ __forceinline__ void pipe_lds6(const gu32x4 *__restrict__ wt, int lan
     }
 }
 
+// pipe_lds6 over JT row tiles: each chunk's weight pieces (P tiles) feed the MFMAs of
+// every row tile (JT x fewer weight bytes per MFMA); B of row tile jt through bl(jt, st0, v)
+template <int NCH, int P, int NP, int JT, class BL>
+__device__ __forceinline__ void pipe_lds6_jt(const gu32x4 *__restrict__ wt, int lane, FragSeq f, BL bl,
+                                             f32x16 (&acc)[P][JT], const Carry6 &cin, FragSeq nf, Carry6 &cout) {
+    static_assert(P <= CARRY6 && NP <= CARRY6, "carry");
+    u32x4 abuf[2][P][3];
+    float bb[2][JT][8];
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) abuf[0][i][p] = cin[i][p];
+    auto ldb = [&](int c, float (&d)[JT][8]) {
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) {
+            float v[4];
+            bl(jt, 8 * c, v);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[jt][k] = v[k];
+            bl(jt, 8 * c + 4, v);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[jt][4 + k] = v[k];
+        }
+    };
+    ldb(0, bb[0]);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) {
+#pragma unroll
+            for (int i = 0; i < P; ++i) ld6(wt, f.base + i * f.stride + c + 1, lane, abuf[(c + 1) & 1][i]);
+            ldb(c + 1, bb[(c + 1) & 1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) ld6(wt, nf.base + i * nf.stride, lane, cout[i]);
+        }
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) {
+            u32x4 b[3];
+            split8(bb[c & 1][jt], b);
+#pragma unroll
+            for (int i = 0; i < P; ++i) acc[i][jt] = mma6(abuf[c & 1][i], b, acc[i][jt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // BN/ReLU epilogue of output tiles co0 .. co0+P-1 of a C-channel layer
 template <int P, int C>
 __device__ __forceinline__ void epi(const float *ab, int co0, int h, f32x16 (&acc)[P]) {
@@ -188,6 +234,18 @@ __device__ __forceinline__ void put_tile(float *buf, int co, int j, int h, const
         *reinterpret_cast<float4 *>(buf + j * LDSW + co * 32 + 8 * r + 4 * h) =
             make_float4(v[4 * r], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
 }
+
+// ChanB over JT row tiles of 32 rows (row tile jt = rows 32 jt .. 32 jt + 31 of the buffer)
+template <int LDSW>
+struct ChanBJ {
+    const float *row;  // buf + j * LDSW
+    int h;
+    __device__ __forceinline__ void operator()(int jt, int st0, float (&v)[4]) const {
+        const int ct = st0 >> 4, r = (st0 & 15) >> 2;
+        const float4 t = *reinterpret_cast<const float4 *>(row + jt * 32 * LDSW + ct * 32 + 8 * r + 4 * h);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    }
+};
 
 // B loader for a chained layer input: k-step st = ct*16 + q <-> channel chan(ct, q, h)
 struct ChanB {

@@ -28,7 +28,8 @@ def build():
         objs = []
         for src in SRCS:
             obj = f"/tmp/b6exp_{v}_{src}.o"
-            subprocess.check_call([b.HIPCC, *b.CFLAGS, *b.FILE_FLAGS.get(src, []), f"-DHREG_B6_EXP={v}", "-c",
+            extra = os.environ.get("B6EXP_DEFS", "").split()  # e.g. -DHREG_L1_LDSW=1
+            subprocess.check_call([b.HIPCC, *b.CFLAGS, *b.FILE_FLAGS.get(src, []), f"-DHREG_B6_EXP={v}", *extra, "-c",
                                    os.path.join(b.CSRC, src), "-o", obj])
             objs.append(obj)
         subprocess.check_call([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", so_path(v), *objs])
