@@ -126,6 +126,17 @@ def _coarse6_work(args):
             2.0 * 8 * G * (16 * 512 + 2 * 512 * 512))
 
 
+def _corr6_work(args):
+    """hreg_corr_head6 (table, N1, small, ud0, ud1, gidx, knn_xyz, G, ...): FineReg convs_1
+    over 8 G rows, (2C + 12) -> N1 -> N1 -> N1 with C = N1 / 2 (executed: the 12 small
+    columns; N1 = 512 is CoarseReg's 528 -> 512 layers, 16 small columns)"""
+    N1, G = args[1], args[7]
+    kin = 528 if N1 == 512 else N1 + 12
+    ks = 16 if N1 == 512 else 12
+    return (2.0 * 8 * G * (kin * N1 + 2 * N1 * N1), 4.0 * G * (8 * (16 + N1 // 2 + 3) + N1 + 3 + N1),
+            2.0 * 8 * G * (ks * N1 + 2 * N1 * N1))
+
+
 def _nbr_work(args):
     G = args[4]
     kx = 4 if args[6] is not None else 260  # HEAD_PRE: geometry columns only
@@ -160,7 +171,9 @@ MFMA_ENTRIES = {
     "hreg_nbr_head": ("head", _nbr_work),
     "hreg_fine_head6": ("head", _fine6_work),
     "hreg_nbr_head6": ("head", _nbr_work),
+    "hreg_nbr_head6s": ("head", _nbr_work),
     "hreg_coarse_head6": ("head", _coarse6_work),
+    "hreg_corr_head6": ("head", _corr6_work),
     "hreg_mlp_head": ("mlp", _mlp_work),
     "hreg_mlp_head6": ("mlp", _mlp_work),
 }
@@ -248,7 +261,8 @@ def entry_peak(name: str) -> float:
     """MFMA peak (fp32-equivalent TFLOP/s) of a C-ABI entry's kernel: bf16x6 kernels
     (hreg_group_l1_6, hreg_group6_*, hreg_group_split6_*, hreg_*_head6) run on the bf16
     matrix cores, the others on v_mfma_f32_32x32x2_f32."""
-    return PEAK_B6_TFLOPS if name.endswith("6") or "6_" in name or "6x2_" in name else PEAK_FP32_MFMA_TFLOPS
+    b6 = name.endswith(("6", "6s")) or "6_" in name or "6x2_" in name
+    return PEAK_B6_TFLOPS if b6 else PEAK_FP32_MFMA_TFLOPS
 
 
 def level_kernel(engine, lv: int) -> str:

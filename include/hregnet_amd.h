@@ -558,6 +558,16 @@ int hreg_nbr_head(const float *table, const float *desc, const int32_t *gidx, co
  * same outputs.  table = hreg_head6_table_floats(N1) floats, N1 = 2C for FineReg and
  * 256 for the neighbour branch (engine.head_table6: bf16 piece fragments of the narrow
  * first block, conv 2 and conv 3, then the f32 epilogues), 16-byte aligned. */
+/* The correspondence-head kernel of hreg_coarse_head6 at conv width N1 in {128, 256, 512}
+ * (channel split over N1/64 waves, activations through LDS, coarse6.hip): FineReg convs_1 +
+ * attention with the precomputed descriptor blocks (ud0 = pre_src per keypoint, ud1 =
+ * pre_dst per destination point gathered by gidx) -- the arguments of hreg_fine_head6 in
+ * coarse6's order; table = hreg_corr_head6_table_floats(N1) floats (engine.fine_head_table6 /
+ * coarse_head_table6, the same layout); -1 for an unsupported N1. */
+int hreg_corr_head6_table_floats(int N1);
+int hreg_corr_head6(const float *table, int N1, const float *small, const float *ud0, const float *ud1,
+                    const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                    void *stream);
 /* CoarseReg convs_1 + attention in one launch (coarse6.hip, bf16x6 products;
  * layers.py:364-390): G keypoints x 8 rows; small [G*8][16] packed small columns
  * (hreg_pair_feats), ud0 [G][512] = W_desc desc_src (per keypoint), ud1 [*][512] = W_knn_desc
@@ -575,6 +585,10 @@ int hreg_fine_head6(const float *table, int C, const float *small, const int32_t
                     const float *pre_dst, void *stream);
 int hreg_nbr_head6(const float *table, const float *desc, const int32_t *gidx, const float *geom,
                    int G, float *out, const float *pre, void *stream);
+/* hreg_nbr_head6 on the channel-split correspondence kernel (coarse6.hip: four waves of
+ * 64 channels, activations through LDS): same arguments, table and outputs. */
+int hreg_nbr_head6s(const float *table, const float *desc, const int32_t *gidx, const float *geom,
+                    int G, float *out, const float *pre, void *stream);
 
 /* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */

@@ -91,8 +91,11 @@ _SIGS = {
     "hreg_nbr_head": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_fine_head6": [_vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_nbr_head6": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
+    "hreg_nbr_head6s": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_head6_table_floats": [_i],
+    "hreg_corr_head6_table_floats": [_i],
     "hreg_coarse_head6": [_vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
+    "hreg_corr_head6": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_mlp_head": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "hreg_mlp_head_table_floats": [_i],
     "hreg_mlp_head6": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],

@@ -26,16 +26,24 @@ namespace {
 using namespace hreg_chain;
 using namespace hreg_split;
 
-constexpr int C = 512, T = C / 32, CW = 8, P = T / CW, KH = 8, LDSW = C + 4;
-constexpr int NCH = T * 2;  // 16-deep chunks over 512 inputs
-// chunk-fragment table (units of 3 pieces x 64 lanes x 16 B), engine.coarse_head_table6
-constexpr int G_1 = 0;               // convs_1[0], the 16 small columns: [T][1]
-constexpr int G_2 = G_1 + T;         // convs_1[1]: [T][NCH]
-constexpr int G_3 = G_2 + T * NCH;   // convs_1[2]: [T][NCH]
-constexpr int G_END = G_3 + T * NCH;
-constexpr int F_END = G_END * 3 * 64 * 4;
-constexpr int NE = 6 * C;            // alpha, beta of the three layers
-constexpr int TABLE = F_END + NE;
+constexpr int KH = 8;
+
+// conv width C (= attention output channels): CoarseReg C = 512, FineReg N1 = 256 / 128.
+// CW waves of P = 2 output tiles each (P = 2: one B split feeds 12 MFMAs).
+template <int C_>
+struct CorrCfg {
+    static constexpr int C = C_, T = C / 32, P = 2, CW = T / P, LDSW = C + 4;
+    static constexpr int NCH = T * 2;  // 16-deep chunks over C inputs
+    // chunk-fragment table (units of 3 pieces x 64 lanes x 16 B), engine.coarse_head_table6
+    // (and engine.fine_head_table6: the same layout)
+    static constexpr int G_1 = 0;               // layer 0, the 16 small columns: [T][1]
+    static constexpr int G_2 = G_1 + T;         // layer 1: [T][NCH]
+    static constexpr int G_3 = G_2 + T * NCH;   // layer 2: [T][NCH]
+    static constexpr int G_END = G_3 + T * NCH;
+    static constexpr int F_END = G_END * 3 * 64 * 4;
+    static constexpr int NE = 6 * C;            // alpha, beta of the three layers
+    static constexpr int TABLE = F_END + NE;
+};
 
 // HREG_COARSE_JT: 32-row tiles per workgroup.  2: every wave computes its P output tiles
 // for both row tiles, so each streamed weight chunk feeds twice the MFMAs (the one-tile
@@ -47,10 +55,19 @@ constexpr int TABLE = F_END + NE;
 #endif
 constexpr int JT = HREG_COARSE_JT, RW = 32 * JT;  // row tiles / rows per workgroup
 
-__global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
+// NBR: CoarseReg's neighbour branch (layers.py:315-337, nbr_head6_kernel's job): rows
+// [desc[nbr] C | dxyz, |d|] through convs_2, the descriptor block precomputed per point
+// with its beta (ud1 = engine.nbr_pre6 rows gathered by gidx; no per-keypoint block), the
+// 4 geometry columns as k-steps 0, 1 of each lane half (small = geom [rows][4]); output
+// sum_j a_j desc[nbr_j] (knn_xyz = desc, att = out; no corres).
+template <class K, bool NBR>
+__global__ __launch_bounds__(K::CW * 64) void coarse_head6_kernel(
     const float *__restrict__ table, const float *__restrict__ small, const float *__restrict__ ud0,
     const float *__restrict__ ud1, const int32_t *__restrict__ gidx, const float *__restrict__ knn_xyz, int G,
     float *__restrict__ corres, float *__restrict__ att) {
+    constexpr int C = K::C, T = K::T, P = K::P, CW = K::CW, LDSW = K::LDSW, NCH = K::NCH;
+    constexpr int G_1 = K::G_1, G_2 = K::G_2, G_3 = K::G_3, F_END = K::F_END, NE = K::NE;
+    (void)T;
     __shared__ float ep[NE];
     __shared__ __attribute__((aligned(16))) float sA[RW * LDSW];
     __shared__ int sMax[CW][RW];
@@ -89,14 +106,22 @@ __global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt) {
             f32x16 yt[P];
-            init_from_rows<C, P>(yt, ud0 + (size_t)g[jt] * C + c0 * 32, ud1 + (size_t)gidx[row[jt]] * C + c0 * 32,
-                                 h);
+            if constexpr (NBR) {
+                init_from_rows<C, P>(yt, ud1 + (size_t)gidx[row[jt]] * C + c0 * 32, nullptr, h);
+                const float2 gin = *reinterpret_cast<const float2 *>(small + (size_t)row[jt] * 4 + h * 2);
+                sm[jt][0] = gin.x; sm[jt][1] = gin.y;
+#pragma unroll
+                for (int k = 2; k < 8; ++k) sm[jt][k] = 0.f;
+            } else {
+                init_from_rows<C, P>(yt, ud0 + (size_t)g[jt] * C + c0 * 32,
+                                     ud1 + (size_t)gidx[row[jt]] * C + c0 * 32, h);
+                const float4 s0 = *reinterpret_cast<const float4 *>(small + (size_t)row[jt] * 16 + h * 8);
+                const float4 s1 = *reinterpret_cast<const float4 *>(small + (size_t)row[jt] * 16 + h * 8 + 4);
+                sm[jt][0] = s0.x; sm[jt][1] = s0.y; sm[jt][2] = s0.z; sm[jt][3] = s0.w;
+                sm[jt][4] = s1.x; sm[jt][5] = s1.y; sm[jt][6] = s1.z; sm[jt][7] = s1.w;
+            }
 #pragma unroll
             for (int i = 0; i < P; ++i) y[i][jt] = yt[i];
-            const float4 s0 = *reinterpret_cast<const float4 *>(small + (size_t)row[jt] * 16 + h * 8);
-            const float4 s1 = *reinterpret_cast<const float4 *>(small + (size_t)row[jt] * 16 + h * 8 + 4);
-            sm[jt][0] = s0.x; sm[jt][1] = s0.y; sm[jt][2] = s0.z; sm[jt][3] = s0.w;
-            sm[jt][4] = s1.x; sm[jt][5] = s1.y; sm[jt][6] = s1.z; sm[jt][7] = s1.w;
         }
         pipe_lds6_jt<1, P, P, JT>(wt, lane, g1, [&](int jt, int st0, float (&v)[4]) {
 #pragma unroll
@@ -109,7 +134,7 @@ __global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
             for (int jt = 0; jt < JT; ++jt)
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
-                    y[i][jt][q] = relu_i(fadd_rn(y[i][jt][q], ep[C + chan(c0 + i, q, h)]));
+                    y[i][jt][q] = relu_i(NBR ? y[i][jt][q] : fadd_rn(y[i][jt][q], ep[C + chan(c0 + i, q, h)]));
         tile_sync();  // the previous tile's readers of sA are done
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt)
@@ -170,7 +195,7 @@ __global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
             const float x1 = __int_as_float(xm);
             const float e = expf(fsub_rn(x1, grp8_max_nonneg(x1)));
             const float a = e / grp8_sum(e);
-            if (cw == 0) {
+            if (!NBR && cw == 0) {
                 const float *p = knn_xyz + (size_t)row[jt] * 3;
                 const float cx = grp8_sum(fmul_rn(a, p[0]));
                 const float cy = grp8_sum(fmul_rn(a, p[1]));
@@ -181,24 +206,53 @@ __global__ __launch_bounds__(CW * 64) void coarse_head6_kernel(
                     corres[(size_t)g[jt] * 3 + 2] = cz;
                 }
             }
+            if constexpr (NBR) {
+                // the attentive sum of the neighbours' descriptors (this wave's P channel tiles)
+                f32x16 dv[P];
+                init_from_rows<C, P>(dv, knn_xyz + (size_t)gidx[row[jt]] * C + c0 * 32, nullptr, h);
 #pragma unroll
-            for (int i = 0; i < P; ++i) {
-                f32x16 v;
+                for (int i = 0; i < P; ++i) {
+                    f32x16 v;
 #pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = grp8_sum(fmul_rn(y[i][jt][q], a));
-                store_tile(att + (size_t)g[jt] * C, c0 + i, v, writer, h);
+                    for (int q = 0; q < 16; ++q) v[q] = grp8_sum(fmul_rn(dv[i][q], a));
+                    store_tile(att + (size_t)g[jt] * C, c0 + i, v, writer, h);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < P; ++i) {
+                    f32x16 v;
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) v[q] = grp8_sum(fmul_rn(y[i][jt][q], a));
+                    store_tile(att + (size_t)g[jt] * C, c0 + i, v, writer, h);
+                }
             }
         }
     }
 }
 
+template <class K, bool NBR = false>
+int launch_corr6(const float *table, const float *small, const float *ud0, const float *ud1, const int32_t *gidx,
+                 const float *knn_xyz, int G, float *corres, float *att, void *stream) {
+    const int NW = (G * KH / 32 + JT - 1) / JT;
+    const int cap = 256 * (JT == 1 ? 4 : 2);  // a few rounds of the resident workgroups
+    const int grid = NW < cap ? NW : cap;
+    hipLaunchKernelGGL((coarse_head6_kernel<K, NBR>), dim3(grid), dim3(K::CW * 64), 0, as_stream(stream), table, small,
+                       ud0, ud1, gidx, knn_xyz, G, corres, att);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
 }  // namespace
 
-extern "C" int hreg_coarse_head6_table_floats(void) { return TABLE; }
+extern "C" int hreg_coarse_head6_table_floats(void) { return CorrCfg<512>::TABLE; }
 
-extern "C" int hreg_coarse_head6(const float *table, const float *small, const float *ud0, const float *ud1,
-                                 const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
-                                 void *stream) {
+extern "C" int hreg_corr_head6_table_floats(int N1) {
+    return N1 == 512 ? CorrCfg<512>::TABLE : N1 == 256 ? CorrCfg<256>::TABLE : N1 == 128 ? CorrCfg<128>::TABLE : -1;
+}
+
+extern "C" int hreg_corr_head6(const float *table, int N1, const float *small, const float *ud0, const float *ud1,
+                               const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                               void *stream) {
     if (!table || !small || !ud0 || !ud1 || !gidx || !knn_xyz || !corres || !att || G < 0)
         return HREG_ERR_INVALID;
     if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(small) & 15) ||
@@ -206,12 +260,30 @@ extern "C" int hreg_coarse_head6(const float *table, const float *small, const f
         (reinterpret_cast<uintptr_t>(att) & 15))
         return HREG_ERR_INVALID;
     if ((G * KH) % 32) return HREG_ERR_INVALID;  // whole 32-row tiles
+    if (N1 != 512 && N1 != 256 && N1 != 128) return HREG_ERR_UNSUPPORTED;
     if (!G) return HREG_OK;
-    const int NW = (G * KH / 32 + JT - 1) / JT;
-    const int cap = JT == 1 ? 1024 : 512;  // two rounds of the resident workgroups (2 / 1 per CU)
-    const int grid = NW < cap ? NW : cap;
-    hipLaunchKernelGGL(coarse_head6_kernel, dim3(grid), dim3(CW * 64), 0, as_stream(stream), table, small, ud0,
-                       ud1, gidx, knn_xyz, G, corres, att);
-    HREG_CHECK_LAUNCH();
-    return HREG_OK;
+    if (N1 == 512) return launch_corr6<CorrCfg<512>>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+    if (N1 == 256) return launch_corr6<CorrCfg<256>>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+    return launch_corr6<CorrCfg<128>>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+}
+
+extern "C" int hreg_coarse_head6(const float *table, const float *small, const float *ud0, const float *ud1,
+                                 const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                                 void *stream) {
+    return hreg_corr_head6(table, 512, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+}
+
+// hreg_nbr_head6 (group_head.hip) on the channel-split kernel: same arguments and table
+// (engine.nbr_head_table6 -- the layout of coarse_head_table6 at C = 256 with a 2-k-step
+// first block), bitwise-identical attention sums
+extern "C" int hreg_nbr_head6s(const float *table, const float *desc, const int32_t *gidx, const float *geom,
+                               int G, float *out, const float *pre, void *stream) {
+    if (!table || !desc || !gidx || !geom || !out || !pre || G < 0) return HREG_ERR_INVALID;
+    if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(desc) & 15) ||
+        (reinterpret_cast<uintptr_t>(geom) & 7) || (reinterpret_cast<uintptr_t>(out) & 15) ||
+        (reinterpret_cast<uintptr_t>(pre) & 15))
+        return HREG_ERR_INVALID;
+    if ((G * KH) % 32) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    return launch_corr6<CorrCfg<256>, true>(table, geom, nullptr, pre, gidx, desc, G, nullptr, out, stream);
 }

@@ -62,6 +62,11 @@ FUSED_COARSE = os.environ.get("HREG_FUSED_COARSE", "1") != "0"
 # the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
 # precomputed-block form, HEAD_PRE)
 B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
+# the FineReg heads on coarse6.hip's channel-split correspondence kernel (hreg_corr_head6:
+# N1/64 waves of two output tiles, activations through LDS, ~136 VGPRs) instead of the
+# register-chained fine_head6_kernel (one wave per SIMD at N1 = 256)
+SPLIT_FINE = os.environ.get("HREG_SPLIT_FINE", "1") != "0"
+SPLIT_NBR = os.environ.get("HREG_SPLIT_NBR", "1") != "0"  # the neighbour branch likewise
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
 FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
 FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip)
@@ -976,7 +981,8 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
         b6 = B6_HEADS and HEAD_PRE
         pre = gemm([_seg(desc3, 0, C)], P.nbr_pre6 if b6 else P.nbr_pre, G2) if HEAD_PRE else None
         if b6:
-            call("hreg_nbr_head6", P.nbr_table6, desc3, gself, geom_self, G2, nbr, pre, _stream())
+            call("hreg_nbr_head6s" if SPLIT_NBR else "hreg_nbr_head6", P.nbr_table6, desc3, gself, geom_self, G2,
+                 nbr, pre, _stream())
         else:
             call("hreg_nbr_head", P.nbr_table, desc3, gself, geom_self, G2, nbr, pre, _stream())
     else:
@@ -1050,7 +1056,10 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
             pre = _empty(2, B * N, N1, device=dev)
             _gemm_batched_desc((P.fine_pre6 if B6_HEADS else P.fine_pre)[name], src_desc, B * N, C,
                                pre, x1=dst_desc)
-        if B6_HEADS and HEAD_PRE:
+        if B6_HEADS and HEAD_PRE and SPLIT_FINE:
+            call("hreg_corr_head6", P.fine_table6[name], N1, small, pre[0], pre[1], gidx, kx, B * N,
+                 corres, att, _stream())
+        elif B6_HEADS and HEAD_PRE:
             call("hreg_fine_head6", P.fine_table6[name], C, small, gidx, kx, B * N, corres, att,
                  pre[0], pre[1], _stream())
         else:

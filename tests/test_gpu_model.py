@@ -282,15 +282,18 @@ def test_pair_l2_matches_single(G):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("pre,b6", [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("pre,b6,split", [(True, True, True), (True, True, False), (True, False, False),
+                                          (False, False, False)])
 @pytest.mark.parametrize("name,C,N", [("fine_corres_1", 64, 1024), ("fine_corres_2", 128, 512)])
-def test_fused_fine_head_matches_layerwise(net, name, C, N, pre, b6, monkeypatch):
+def test_fused_fine_head_matches_layerwise(net, name, C, N, pre, b6, split, monkeypatch):
     """group_head.hip (convs_1 + attention in one kernel; pre: descriptor blocks of
     convs_1[0] precomputed per point, engine.HEAD_PRE; b6: the bf16x6 kernel, products on
-    the bf16 matrix cores at fp32 accuracy) against the GEMM + attend path."""
+    the bf16 matrix cores at fp32 accuracy; split: coarse6.hip's channel-split kernel,
+    hreg_corr_head6) against the GEMM + attend path."""
     from pcd_reg_hregnet_amd import engine
     monkeypatch.setattr(engine, "HEAD_PRE", pre)
     monkeypatch.setattr(engine, "B6_HEADS", b6)
+    monkeypatch.setattr(engine, "SPLIT_FINE", split)
     P = net.prepared(torch.device("cuda"))
     g = torch.Generator().manual_seed(3)
     B = 2
@@ -369,13 +372,16 @@ def test_gemm_addends_vs_torch():
     assert np.all(np.abs(out - ref) <= 1e-5 * scale + 1e-6)
 
 
-@pytest.mark.parametrize("pre,b6", [(True, True), (True, False), (False, False)])
-def test_fused_nbr_head_matches_layerwise(net, pre, b6, monkeypatch):
+@pytest.mark.parametrize("pre,b6,split", [(True, True, True), (True, True, False), (True, False, False),
+                                          (False, False, False)])
+def test_fused_nbr_head_matches_layerwise(net, pre, b6, split, monkeypatch):
     """CoarseReg neighbour branch in one kernel (group_head.hip; pre: descriptor block of
-    convs_2[0] precomputed per point; b6: bf16x6 products) vs GEMMs + attend."""
+    convs_2[0] precomputed per point; b6: bf16x6 products; split: coarse6.hip's
+    channel-split kernel, hreg_nbr_head6s) vs GEMMs + attend."""
     from pcd_reg_hregnet_amd import engine
     monkeypatch.setattr(engine, "HEAD_PRE", pre)
     monkeypatch.setattr(engine, "B6_HEADS", b6)
+    monkeypatch.setattr(engine, "SPLIT_NBR", split)
     P = net.prepared(torch.device("cuda"))
     g = torch.Generator().manual_seed(5)
     B, N1, C = 2, 256, 256
@@ -395,6 +401,30 @@ def test_fused_nbr_head_matches_layerwise(net, pre, b6, monkeypatch):
     (c_f, w_f), (c_r, w_r) = outs
     torch.testing.assert_close(c_f, c_r, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(w_f, w_r, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("G", [4, 12, 1024])
+def test_nbr_head6_split_matches_chained(net, G):
+    """hreg_nbr_head6s (channel-split, coarse6.hip) against hreg_nbr_head6 (register-chained,
+    group_head.hip) on the prepared table and random rows: the same per-row arithmetic up
+    to the accumulation of the three layers (both bf16x6, same chunk order), so the
+    attention sums agree to fp32 rounding; 1e-5 relative."""
+    from pcd_reg_hregnet_amd import _lib
+    P = net.prepared(torch.device("cuda"))
+    rng = np.random.default_rng(G)
+    npts = G + 5
+    desc = torch.from_numpy(np.abs(rng.normal(size=(npts, 256))).astype(np.float32)).cuda()
+    pre = torch.from_numpy(rng.normal(size=(npts, 256)).astype(np.float32)).cuda()
+    geom = torch.from_numpy(rng.normal(size=(G * 8, 4)).astype(np.float32)).cuda()
+    gidx = torch.from_numpy(rng.integers(0, npts, G * 8).astype(np.int32)).cuda()
+    outs = []
+    for name in ("hreg_nbr_head6", "hreg_nbr_head6s"):
+        out = torch.full((G, 256), float("nan"), device="cuda")
+        _lib.call(name, P.nbr_table6, desc, gidx, geom, G, out, pre, _lib.stream_handle())
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[1]).any()
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("key,C,rows,mode", [(("det", 0), 64, 1024, 0), (("det", 1), 128, 512, 0),

@@ -280,6 +280,11 @@ def test_head6_tables_match_kernel(P):
     L = _lib.load(require_gpu=False)
     assert prep.fine_table6["fine_corres_1"].numel() == L.hreg_head6_table_floats(128)
     assert prep.fine_table6["fine_corres_2"].numel() == L.hreg_head6_table_floats(256)
+    # the channel-split correspondence kernel reads the same tables (hreg_corr_head6)
+    assert prep.fine_table6["fine_corres_1"].numel() == L.hreg_corr_head6_table_floats(128)
+    assert prep.fine_table6["fine_corres_2"].numel() == L.hreg_corr_head6_table_floats(256)
+    assert prep.coarse_table6.numel() == L.hreg_corr_head6_table_floats(512)
+    assert L.hreg_corr_head6_table_floats(64) == -1
     assert prep.nbr_table6.numel() == L.hreg_head6_table_floats(256)
     W = prep.coarse_convs2[1].W.cpu()
     pieces = engine._bf16_pieces(W).to(torch.int32) << 16
