@@ -61,11 +61,11 @@ __device__ __forceinline__ void stage_rows6(float *buf, const float *__restrict_
 
 // conv stack [geom | feat] -> C1 -> C1 -> C3 through the A/B buffers (group_split.hip
 // conv_stack_split); this wave's P3 output tiles in out (epilogue applied).
-template <class K, int NP, bool PRE>
+template <class K, int NP, bool PRE, bool ONE>
 __device__ __forceinline__ void conv_stack_split6(const gu32x4 *__restrict__ wt, const float *eb, int gg, int gf,
                                                   int g2, int g3, int e1, int e2, int e3, float *A, float *B,
                                                   int cw, int lane, f32x16 (&out)[K::P3], const Carry6 &cin,
-                                                  FragSeq next, Carry6 &cout, const float *pre_row) {
+                                                  FragSeq next, Carry6 &cout, const float *pre_row, float2 gin) {
     constexpr int TF = K::TF, P1 = K::P1, P3 = K::P3, LDSW = K::LDSW, N1 = K::N1, NF = K::NF;
     const int h = lane >> 5, j = lane & 31;
     const int c1 = cw * P1, c3 = cw * P3;
@@ -76,7 +76,7 @@ __device__ __forceinline__ void conv_stack_split6(const gu32x4 *__restrict__ wt,
     // geometry chunk: f32 k-steps 0, 1 (channels 2h, 2h + 1), the rest zero
     auto geom_b = [&](int st0, float (&v)[4]) {
         if (st0 == 0) {
-            const float2 t = *reinterpret_cast<const float2 *>(arow + 2 * h);
+            const float2 t = ONE ? gin : *reinterpret_cast<const float2 *>(arow + 2 * h);
             v[0] = t.x; v[1] = t.y;
         } else {
             v[0] = 0.f; v[1] = 0.f;
@@ -106,6 +106,7 @@ __device__ __forceinline__ void conv_stack_split6(const gu32x4 *__restrict__ wt,
     beta_p<P1, K::T1 * 32>(eb + e2, c1, h, h2);
     pipe_lds6<N1, P1, P3>(wt, lane, s2, ChanB{brow, h}, h2, cb, s3, ca);
     relu_tiles(h2);
+    if constexpr (ONE) tile_sync();  // one buffer: every wave has read layer 2's input
 #pragma unroll
     for (int i = 0; i < P1; ++i) put_tile<LDSW>(A, c1 + i, j, h, h2[i]);
     tile_sync();
@@ -114,8 +115,16 @@ __device__ __forceinline__ void conv_stack_split6(const gu32x4 *__restrict__ wt,
     relu_tiles(out);
 }
 
-template <class K, bool PRE>
-__global__ __launch_bounds__(256, 2) void group_split6_kernel(
+// HREG_SPLIT_1BUF (default, PRE form): one activation buffer instead of two -- the
+// geometry comes from registers, and a barrier before each write that replaces a layer's
+// input (4 more per tile) -- so the LDS footprint drops from 80 to 47 KB (level 3) and three
+// workgroups fit per CU (3 waves per SIMD at <= 168 VGPRs) instead of two.
+#ifndef HREG_SPLIT_1BUF
+#define HREG_SPLIT_1BUF 1
+#endif
+
+template <class K, bool PRE, bool ONE = (HREG_SPLIT_1BUF && PRE)>
+__global__ __launch_bounds__(256, ONE ? 3 : 2) void group_split6_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
     float *__restrict__ att_feat, float *__restrict__ desc, const float *__restrict__ pre) {
@@ -125,7 +134,7 @@ __global__ __launch_bounds__(256, 2) void group_split6_kernel(
     constexpr int NE = K::TABLE - K::F_END, KN = K::KN, GPT = K::GPT, RT = K::RT, CW = K::CW;
     __shared__ float ep[NE];
     __shared__ __attribute__((aligned(16))) float sA[RT][32 * LDSW];
-    __shared__ __attribute__((aligned(16))) float sB[RT][32 * LDSW];
+    __shared__ __attribute__((aligned(16))) float sB[ONE ? 1 : RT][ONE ? 4 : 32 * LDSW];
     __shared__ __attribute__((aligned(16))) float sX2[RT][GPT * X2W];
     __shared__ int sMax[RT][CW][32];
     for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
@@ -134,7 +143,7 @@ __global__ __launch_bounds__(256, 2) void group_split6_kernel(
     const int rt = w / CW, cw = w % CW;
     const int h = lane >> 5, j = lane & 31;
     const int NT = G / GPT;
-    float *A = sA[rt], *B = sB[rt], *X2 = sX2[rt];
+    float *A = sA[rt], *B = ONE ? sA[rt] : sB[rt], *X2 = sX2[rt];
     const bool writer = KN == 32 ? j == 31 : (j & 15) == 15;
     auto gsum_w = [&](float v) { return KN == 32 ? half_sum_hi(v) : row_sum16(v); };
     auto gsum_b = [&](float v) { return KN == 32 ? half_bcast(half_sum_hi(v), h) : row_sum16(v); };
@@ -166,14 +175,17 @@ __global__ __launch_bounds__(256, 2) void group_split6_kernel(
         Carry6 ca, cb;
 
         const float *prow = PRE ? pre + (size_t)gidx[row] * (2 * K::T1 * 32) : nullptr;
+        const float2 gin = ONE ? *reinterpret_cast<const float2 *>(geom + row * 4 + 2 * h) : make_float2(0.f, 0.f);
         tile_sync();  // previous tile's readers of A are done (and ep is loaded)
-        stage_rows6<K, PRE>(A, geom, gidx, feats, t, cw, lane);
-        tile_sync();
+        if constexpr (!ONE) {
+            stage_rows6<K, PRE>(A, geom, gidx, feats, t, cw, lane);
+            tile_sync();
+        }
 
         // ---- detector -> emb (this wave's P3 tiles)
         f32x16 emb[P3];
-        conv_stack_split6<K, PM1, PRE>(wt, eb, K::G_DG, K::G_DF, K::G_D2, K::G_D3, K::E_D1, K::E_D2, K::E_D3,
-                                       A, B, cw, lane, emb, carry, m1em, ca, prow);
+        conv_stack_split6<K, PM1, PRE, ONE>(wt, eb, K::G_DG, K::G_DF, K::G_D2, K::G_D3, K::E_D1, K::E_D2,
+                                            K::E_D3, A, B, cw, lane, emb, carry, m1em, ca, prow, gin);
 
         // ---- attention (group_split.hip): row max over all C3 channels through LDS,
         // softmax over the group, keypoint and attentive feature
@@ -220,13 +232,15 @@ __global__ __launch_bounds__(256, 2) void group_split6_kernel(
         f32x16 y1[PM1];
         beta_p<PM1, TM1 * 32>(eb + K::E_M1, m1, h, y1);
         pipe_lds6<N3, PM1, K::P1>(wt, lane, m1em, ChanB{B + j * LDSW, h}, y1, ca, desc_g, cb);
-        stage_rows6<K, PRE>(A, geom, gidx, feats, t, cw, lane);
-        tile_sync();
+        if constexpr (!ONE) stage_rows6<K, PRE>(A, geom, gidx, feats, t, cw, lane);
+        tile_sync();  // (one buffer: every wave has read emb * a)
 
         // ---- descriptor -> x1d
         f32x16 x1d[P3];
-        conv_stack_split6<K, PM1, PRE>(wt, eb, K::G_EG, K::G_EF, K::G_E2, K::G_E3, K::E_E1, K::E_E2, K::E_E3,
-                                       A, B, cw, lane, x1d, cb, m1x1, ca, PRE ? prow + K::T1 * 32 : nullptr);
+        conv_stack_split6<K, PM1, PRE, ONE>(wt, eb, K::G_EG, K::G_EF, K::G_E2, K::G_E3, K::E_E1, K::E_E2,
+                                            K::E_E3, A, B, cw, lane, x1d, cb, m1x1, ca,
+                                            PRE ? prow + K::T1 * 32 : nullptr, gin);
+        if constexpr (ONE) tile_sync();  // every wave has read layer 3's input
 #pragma unroll
         for (int i = 0; i < P3; ++i) {
             f32x16 v;
@@ -283,6 +297,7 @@ __global__ __launch_bounds__(256, 2) void group_split6_kernel(
         }
         pipe_lds6<N3, PM1, PM2>(wt, lane, m1x1, ChanB{B + j * LDSW, h}, y1, ca, fm2, cb);
         relu_tiles(y1);
+        if constexpr (ONE) tile_sync();  // every wave has read x1d
 #pragma unroll
         for (int i = 0; i < PM1; ++i) put_tile<LDSW>(A, m1 + i, j, h, y1[i]);
         tile_sync();
@@ -316,7 +331,7 @@ int launch_split6(const float *table, const float *geom, const float *knn_xyz, c
     if (!G) return HREG_OK;
     const int NT = G / K::GPT;
     int grid = (NT + K::RT - 1) / K::RT;
-    const int cap = 256 * 2 * 2;  // two resident workgroups per CU, two rounds
+    const int cap = 256 * (HREG_SPLIT_1BUF && pre ? 3 : 2) * 2;  // resident workgroups per CU, two rounds
     if (grid > cap) grid = cap;
     if (pre)
         hipLaunchKernelGGL((group_split6_kernel<K, true>), dim3(grid), dim3(256), 0, as_stream(stream), table,
