@@ -49,6 +49,9 @@ B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
 # bytes streamed per row, hreg_group6x2_l2).  Off: at one wave per SIMD it measured level
 # with the one-group kernel (183 vs 184 us; tools/b6_experiment.py: 180 vs 182 us)
 PAIR_L2 = os.environ.get("HREG_PAIR_L2", "0") != "0"
+# GraphPipeline: level-1 stage of all lanes as one batched launch per kernel (one side
+# stream) instead of one per lane
+BATCH_STAGE1 = os.environ.get("HREG_BATCH_STAGE1", "1") != "0"
 B6_L1 = os.environ.get("HREG_B6_L1", "1") != "0"  # group_l1_6.hip for level 1
 # level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
 # (group_split6.hip)
@@ -1276,13 +1279,30 @@ class GraphPipeline:
         self.lanes = lanes
         dev = src.device
         B, N, _ = src.shape
-        self.src = [src.clone() for _ in range(lanes)]
-        self.dst = [dst.clone() for _ in range(lanes)]
-        self.bufs = [[alloc_stage1(B, N, dev), alloc_stage1(B, N, dev)] for _ in range(lanes)]
+        self.B, self.N = B, N
+        # BATCH_STAGE1: stage 1 (level-1 FPS + spatial index + kNN) of every lane's next batch
+        # as ONE launch each over lanes x 2B clouds on one side stream; the lanes read
+        # cloud-slice views of it (the level-1 kernel reads geom / knn_xyz, not the global
+        # gidx: FUSED_L1 only)
+        self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1
+        if self.bs1:
+            self.src_all = src.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
+            self.dst_all = dst.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
+            self.src = [self.src_all[ln] for ln in range(lanes)]
+            self.dst = [self.dst_all[ln] for ln in range(lanes)]
+            self.bufs_all = [alloc_stage1(B * lanes, N, dev) for _ in (0, 1)]
+            self.bufs = [[self._lane_view(ab, ln) for ab in (0, 1)] for ln in range(lanes)]
+        else:
+            self.src = [src.clone() for _ in range(lanes)]
+            self.dst = [dst.clone() for _ in range(lanes)]
+            self.bufs = [[alloc_stage1(B, N, dev), alloc_stage1(B, N, dev)] for _ in range(lanes)]
         self.side = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
         self.lane_streams = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
         # eager warm-up: library, allocator and workspace shapes
-        stage1_into(self.bufs[0][0], self.src[0], self.dst[0])
+        if self.bs1:
+            self._stage1_all(0)
+        else:
+            stage1_into(self.bufs[0][0], self.src[0], self.dst[0])
         self._rest(0, 0)
         torch.cuda.synchronize()
         # the captured graphs contain multi-workgroup FPS launches (n > 16384): their
@@ -1292,14 +1312,12 @@ class GraphPipeline:
         self.pool = torch.cuda.graph_pool_handle()
         self.g_first = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_first, pool=self.pool):
-            self._fork(lambda ln: stage1_into(self.bufs[ln][0], self.src[ln], self.dst[ln]))
+            self._first_stage1()
         self.g_step, self.outs = [], []
         for cur in (0, 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.pool):
-                out = self._fork(
-                    lambda ln: self._rest(ln, cur),
-                    side=lambda ln: stage1_into(self.bufs[ln][1 - cur], self.src[ln], self.dst[ln]))
+                out = self._fork(lambda ln: self._rest(ln, cur), **self._side_kw(1 - cur))
             self.g_step.append(g)
             self.outs.append(out)
         self.g_last, self.outs_last = [], []
@@ -1312,7 +1330,39 @@ class GraphPipeline:
         self._part = {}
         torch.cuda.synchronize()
 
-    def _fork(self, body, side=None, lanes=None, side_lanes=None):
+    def _lane_view(self, ab: int, ln: int):
+        """Lane ln's stage-1 buffers as cloud-slice views of the batched set ab."""
+        pts, (idx, sampled, gidx, geom, kx, ws) = self.bufs_all[ab]
+        nb = 2 * self.B
+        M, k = LEVELS[0][:2]
+        R = nb * M * k
+        c, r = slice(ln * nb, (ln + 1) * nb), slice(ln * R, (ln + 1) * R)
+        return pts[c], (idx[c], sampled[c], gidx[r], geom[r], kx[r], ws)
+
+    def _stage1_all(self, ab: int):
+        """Stage 1 of every lane's static batch into buffer set ab: 2 copies + one FPS, one
+        spatial index and one kNN launch over lanes x 2B clouds."""
+        pts, g = self.bufs_all[ab]
+        v = pts.view(self.lanes, 2, self.B, self.N, 3)
+        v[:, 0].copy_(self.src_all)
+        v[:, 1].copy_(self.dst_all)
+        grouping(pts, 0, out=g, ws=g[5])
+
+    def _first_stage1(self, lanes=None):
+        if self.bs1:
+            self._stage1_all(0)
+        else:
+            self._fork(lambda ln: stage1_into(self.bufs[ln][0], self.src[ln], self.dst[ln]), lanes=lanes)
+
+    def _side_kw(self, ab: int, side_lanes=None):
+        """_fork keywords for the next batch's stage 1 into buffer set ab (batched: one job
+        for all lanes; per lane: lanes < side_lanes)."""
+        if self.bs1:
+            return {"side_all": lambda: self._stage1_all(ab)}
+        return {"side": lambda ln: stage1_into(self.bufs[ln][ab], self.src[ln], self.dst[ln]),
+                "side_lanes": side_lanes}
+
+    def _fork(self, body, side=None, lanes=None, side_lanes=None, side_all=None):
         """Inside a capture: body(lane) for every lane < lanes on its own stream (lane 0
         on the capturing stream) and side(lane) for lane < side_lanes on the lane's side
         stream, all forked from the capturing stream and joined back to it (one level of
@@ -1323,6 +1373,8 @@ class GraphPipeline:
         lanes = self.lanes if lanes is None else lanes
         side_lanes = lanes if side_lanes is None else side_lanes
         jobs = []
+        if side_all is not None:
+            jobs.append((self.side[0], lambda _ln: side_all(), -1))
         for ln in range(lanes):
             if side is not None and ln < side_lanes:
                 jobs.append((self.side[ln], side, ln))
@@ -1371,15 +1423,12 @@ class GraphPipeline:
         torch.cuda.synchronize()
         first = torch.cuda.CUDAGraph()
         with torch.cuda.graph(first, pool=self.pool):
-            self._fork(lambda ln: stage1_into(self.bufs[ln][0], self.src[ln], self.dst[ln]), lanes=r)
+            self._first_stage1(lanes=r)  # (batched: every lane's stage 1, the extra lanes unused)
         steps, souts, lasts, louts = [], [], [], []
         for cur in (0, 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.pool):
-                out = self._fork(
-                    lambda ln: self._rest(ln, cur),
-                    side=lambda ln: stage1_into(self.bufs[ln][1 - cur], self.src[ln], self.dst[ln]),
-                    side_lanes=r)
+                out = self._fork(lambda ln: self._rest(ln, cur), **self._side_kw(1 - cur, side_lanes=r))
             steps.append(g)
             souts.append(out)
             g = torch.cuda.CUDAGraph()
