@@ -39,6 +39,7 @@ PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak BW (spec)
 ALG_GFLOP_PER_PAIR = 20.579
 POINTS = 16384
 PAIRS_PER_GPU = 8
+LANES_MAX = 48         # graph executor: most batches in flight (memory: one forward's buffers each)
 V2_POINTS = 65536      # config 5 (MANTruckScenes-shape): B=16 over 8 GPUs -> 2 pairs/GPU
 V2_PAIRS_PER_GPU = 2
 
@@ -455,7 +456,7 @@ def bench_train(args, world, rank, device):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=24)
+    ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", choices=("hregnet", "v2", "train"), default="hregnet",
                     help="v2: Model_V2 at config 5 (2 x 65536-pt pairs per GPU); train: the "
@@ -470,10 +471,11 @@ def main():
                          "eagerly; serial: no cross-batch overlap")
     ap.add_argument("--lanes", type=int, default=None,
                     help="graph executor: batches in flight at once, one stream each "
-                         "(a step is still one forward over one batch); default 8 (a "
-                         "--steps it does not divide: the most lanes that do, powers of two "
-                         "first), 4 for v2 (its cluster FPS spins up to 256 waves per "
-                         "launch and needs every launch's participants co-resident)")
+                         "(a step is still one forward over one batch); default: --steps "
+                         "up to 48 (one round), else its largest divisor in [16, 48]; 4 "
+                         "for v2 (its cluster FPS spins up to 256 waves per launch and "
+                         "needs every launch's participants co-resident).  An explicit "
+                         "value that --steps does not divide: the most lanes that do")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--split", default=None,
                     help="comma list of levels (2,3) on the channel-split group kernel "
@@ -486,9 +488,23 @@ def main():
         args.batch = V2_PAIRS_PER_GPU if v2 else PAIRS_PER_GPU
     if args.points is None:
         args.points = V2_POINTS if v2 else POINTS
-    if args.lanes is None:
-        args.lanes = 4 if v2 else 8
-    if args.model != "train" and args.executor == "graph" and args.steps % args.lanes:
+    lanes_auto = args.lanes is None
+    if lanes_auto:
+        # one round when it fits: a replay boundary drains the pipeline and the round's
+        # level-1 stage runs once per round (batched over its lanes, GraphPipeline
+        # BATCH_STAGE1): lanes = --steps up to LANES_MAX, else the largest divisor of --steps
+        # in [16, LANES_MAX] (measured on one box: --steps 24 on 8 / 12 / 24 lanes 6122 /
+        # 6295 / 6432 pairs/s; --steps 48 on 16 / 24 / 48 lanes 6802 / 6697 / 6891), else
+        # LANES_MAX with a final partial round (GraphPipeline.run_forwards); v2: 4
+        if v2:
+            args.lanes = 4
+        elif args.steps <= LANES_MAX:
+            args.lanes = max(args.steps, 1)
+        else:
+            divs = [d for d in range(16, LANES_MAX + 1) if args.steps % d == 0]
+            args.lanes = max(divs) if divs else LANES_MAX
+    if (args.model != "train" and args.executor == "graph" and args.steps % args.lanes
+            and not lanes_auto):
         # a replay runs one batch per lane: time exactly --steps forwards with the most
         # lanes <= --lanes that divide it, powers of two first (the streams share
         # GPU_MAX_HW_QUEUES = 4 hardware queues: 5 or 6 lanes measured slower than 4; a
