@@ -52,6 +52,12 @@ __device__ __forceinline__ float4 load_w4(const hreg_gemm_t &g, int b, int n, in
     return *reinterpret_cast<const float4 *>(p);
 }
 
+// timing experiment (bench A/B only, results wrong): HREG_GEMM_EXP=1 skips the K loop
+// (loads + MFMAs), the epilogue writes the affine shift / zeros
+#ifndef HREG_GEMM_EXP
+#define HREG_GEMM_EXP 0
+#endif
+
 template <int BM, int BN, int WM, int WN, int BK, bool ADD = false>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     static_assert(WM * WN == 4, "4 waves");
@@ -73,7 +79,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     const int b = blockIdx.z;
     const int r0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
-    const int nchunks = (g.K + BK - 1) / BK;
+    const int nchunks = HREG_GEMM_EXP ? 0 : (g.K + BK - 1) / BK;
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -113,8 +119,10 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
         }
     };
 
-    gload(0);
-    lstore(0);
+    if (nchunks) {
+        gload(0);
+        lstore(0);
+    }
     __syncthreads();
 
     const int h = lane >> 5, l32 = lane & 31;
