@@ -1287,7 +1287,10 @@ class GraphPipeline:
         # as ONE launch each over lanes x 2B clouds on one side stream; the lanes read
         # cloud-slice views of it (the level-1 kernel reads geom / knn_xyz, not the global
         # gidx: FUSED_L1 only)
-        self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1
+        # (clouds above 16384 points -- Model_V2's config -- keep the per-lane stage: their
+        # multi-workgroup FPS spins every participant of a launch, and one batched launch
+        # measured slower: 803 vs 844 pairs/s)
+        self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1 and N <= 16384
         if self.bs1:
             self.src_all = src.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
             self.dst_all = dst.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
