@@ -30,9 +30,9 @@ constexpr int KH = 8;
 
 // conv width C (= attention output channels): CoarseReg C = 512, FineReg N1 = 256 / 128.
 // CW waves of P = 2 output tiles each (P = 2: one B split feeds 12 MFMAs).
-template <int C_>
+template <int C_, int P_ = 2>
 struct CorrCfg {
-    static constexpr int C = C_, T = C / 32, P = 2, CW = T / P, LDSW = C + 4;
+    static constexpr int C = C_, T = C / 32, P = P_, CW = T / P, LDSW = C + 4;
     static constexpr int NCH = T * 2;  // 16-deep chunks over C inputs
     // chunk-fragment table (units of 3 pieces x 64 lanes x 16 B), engine.coarse_head_table6
     // (and engine.fine_head_table6: the same layout)
@@ -244,10 +244,16 @@ int launch_corr6(const float *table, const float *small, const float *ud0, const
 
 }  // namespace
 
-extern "C" int hreg_coarse_head6_table_floats(void) { return CorrCfg<512>::TABLE; }
+// output tiles per wave of the CoarseReg (N1 = 512) instance (A/B builds: 1 = 16 waves)
+#ifndef HREG_CORR512_P
+#define HREG_CORR512_P 2
+#endif
+using Corr512 = CorrCfg<512, HREG_CORR512_P>;
+
+extern "C" int hreg_coarse_head6_table_floats(void) { return Corr512::TABLE; }
 
 extern "C" int hreg_corr_head6_table_floats(int N1) {
-    return N1 == 512 ? CorrCfg<512>::TABLE : N1 == 256 ? CorrCfg<256>::TABLE : N1 == 128 ? CorrCfg<128>::TABLE : -1;
+    return N1 == 512 ? Corr512::TABLE : N1 == 256 ? CorrCfg<256>::TABLE : N1 == 128 ? CorrCfg<128>::TABLE : -1;
 }
 
 extern "C" int hreg_corr_head6(const float *table, int N1, const float *small, const float *ud0, const float *ud1,
@@ -262,7 +268,7 @@ extern "C" int hreg_corr_head6(const float *table, int N1, const float *small, c
     if ((G * KH) % 32) return HREG_ERR_INVALID;  // whole 32-row tiles
     if (N1 != 512 && N1 != 256 && N1 != 128) return HREG_ERR_UNSUPPORTED;
     if (!G) return HREG_OK;
-    if (N1 == 512) return launch_corr6<CorrCfg<512>>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+    if (N1 == 512) return launch_corr6<Corr512>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
     if (N1 == 256) return launch_corr6<CorrCfg<256>>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
     return launch_corr6<CorrCfg<128>>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
 }

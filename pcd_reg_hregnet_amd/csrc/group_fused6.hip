@@ -56,8 +56,8 @@ using hreg_jt::Carry;
 // NC: output tiles of the call that follows (its first chunk is prefetched into cout).
 // PRE: the feature part of the first layer comes precomputed per source point and
 // initialises the accumulators (group_fused.hip).
-template <class K, int NC, bool PRE>
-__device__ __forceinline__ void conv_stack6(const gu32x4 *__restrict__ wt, const float *eb, int gg, int gf,
+template <class K, int NC, bool PRE, class WT>
+__device__ __forceinline__ void conv_stack6(WT &&wt, const float *eb, int gg, int gf,
                                             int g2, int g3, int e1, int e2, int e3, int lane, float2 gin,
                                             const float4 (&fin)[K::TF / 4], const float *pre_row,
                                             f32x16 (&out)[K::T3], const Carry &cin, FragSeq next,
@@ -88,8 +88,17 @@ __device__ __forceinline__ void conv_stack6(const gu32x4 *__restrict__ wt, const
     relu_tiles(out);
 }
 
-template <class K, bool PRE>
-__global__ __launch_bounds__(256, K::WPS) void group_fused6_kernel(
+// HREG_RING (level 2): the weight pieces through the workgroup-shared LDS stream
+// (mfma_chain.h Ring6) instead of one register stream per wave
+#ifndef HREG_RING
+#define HREG_RING 1
+#endif
+#ifndef HREG_RING_WPS
+#define HREG_RING_WPS 3  // waves per SIMD the ring kernel's register budget targets
+#endif
+
+template <class K, bool PRE, bool RING = false>
+__global__ __launch_bounds__(256, RING ? HREG_RING_WPS : K::WPS) void group_fused6_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
     float *__restrict__ att_feat, float *__restrict__ desc, const float *__restrict__ pre) {
@@ -116,17 +125,32 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused6_kernel(
     const FragSeq m2{K::G_M2, NM1};
 
     Carry carry;
-    {
+    constexpr int RT_TILES = T3 > TM2 ? (T3 > T1 ? T3 : T1) : (TM2 > T1 ? TM2 : T1);
+    __shared__ __attribute__((aligned(16))) u32x4 ring_lds[RING ? 2 * RT_TILES * 192 : 1];
+    Ring6<RT_TILES, WAVES> ring{reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table)),
+                                (lds_u32x4 *)ring_lds, 0, w};
+    if constexpr (RING) {
+        ring_fill<T1>(ring, 0, det_g, 0, lane);
+    } else {
         const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table));
 #pragma unroll
         for (int co = 0; co < T1; ++co) ld6(wt, det_g.base + co, lane, carry[co]);
     }
-    for (int t = blockIdx.x * WAVES + w; t < NT; t += gridDim.x * WAVES) {
+    // RING: every wave of the workgroup runs the same tiles count (a tile past the end
+    // recomputes the last one: identical values, identical stores)
+    const int tstride = gridDim.x * WAVES;
+    for (int t0 = blockIdx.x * WAVES + (RING ? 0 : w); t0 < NT; t0 += tstride) {
+        const int t = RING ? min(t0 + w, NT - 1) : t0;
         const int g = t * GPT + (KN == 32 ? 0 : j >> 4);  // this lane's group
         // opaque per-tile table pointer: keeps the loop-invariant weight loads in the loop
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
-        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
+        const gu32x4 *wtp = reinterpret_cast<const gu32x4 *>(tba);
+        ring.wt = wtp;  // (opaque per tile: the DMA addresses are not hoisted out of the loop)
+        auto &&wt = [&]() -> decltype(auto) {
+            if constexpr (RING) return (ring);
+            else return wtp;
+        }();
         const size_t row = (size_t)t * 32 + j;
         const float2 gin = *reinterpret_cast<const float2 *>(geom + row * 4 + 2 * h);
         const size_t src = (size_t)gidx[row];
@@ -249,9 +273,13 @@ int launch_group6(const float *table, const float *geom, const float *knn_xyz, c
     if (!G) return HREG_OK;
     const int NT = G / (32 / K::KN);
     int grid = (NT + WAVES - 1) / WAVES;
-    const int cap = 256 * K::WPS * 4 / WAVES * 2;  // two rounds of resident blocks
+    const int cap = 256 * (HREG_RING && K::KN == 32 ? HREG_RING_WPS : K::WPS) * 4 / WAVES * 2;  // two rounds
     if (grid > cap) grid = cap;
-    if (pre)
+    constexpr bool RING = HREG_RING && K::KN == 32;
+    if (RING && pre)
+        hipLaunchKernelGGL((group_fused6_kernel<K, true, RING>), dim3(grid), dim3(256), 0, as_stream(stream),
+                           table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
+    else if (pre)
         hipLaunchKernelGGL((group_fused6_kernel<K, true>), dim3(grid), dim3(256), 0, as_stream(stream), table,
                            geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
     else

@@ -430,4 +430,78 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
     }
 }
 
+// ------------------------------------------------------------------------
+// Workgroup-shared weight stream (group_fused6.hip, HREG_RING): the 4 waves of a workgroup
+// run the same chunk sequence on different row tiles, so each step's weight pieces are
+// brought into LDS ONCE per workgroup by LDS-DMA (global_load_lds_dwordx4, the 3 x NCO
+// pieces of a step spread over the waves) and every wave reads them with ds_read_b128 --
+// a quarter of the vector-memory return traffic of per-wave streams (the texture-data
+// return unit was ~87 % busy).  Two slots: the DMA of step s + 1 is issued right after the
+// barrier that opens step s (every wave's DMA of step s landed: vmcnt(0) before it; every
+// wave has finished reading step s - 1's slot).  Every wave must run the same steps.
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
+
+template <int SLOT_TILES, int NWAVES>
+struct Ring6 {
+    static constexpr int SLOT = SLOT_TILES * 192;  // u32x4 per slot
+    const gu32x4 *wt;   // the table (global)
+    lds_u32x4 *lds;     // 2 slots
+    int step, w;        // uniform: steps so far, this wave's index in the workgroup
+};
+
+template <int NCO, class R>
+__device__ __forceinline__ void ring_fill(R &ring, int slot, FragSeq f, int c, int lane) {
+    static_assert(NCO * 192 <= R::SLOT, "slot");
+    constexpr int NP = 3 * NCO;
+#pragma unroll
+    for (int i0 = 0; i0 < NP; i0 += 4) {
+        const int i = i0 + ring.w;  // piece i = co * 3 + p of this wave
+        if (i < NP) {
+            const int co = i / 3, p = i - 3 * co;
+            const gu32x4 *src = ring.wt + (f.base + co * f.stride + c) * 192 + p * 64 + lane;
+#if __HIP_DEVICE_COMPILE__  // (the gfx950 builtin does not exist in the host pass)
+            __builtin_amdgcn_global_load_lds(src, ring.lds + slot * R::SLOT + i * 64, 16, 0, 0);
+#else
+            (void)src;
+#endif
+        }
+    }
+}
+
+template <int NCH, int COUT_T, int NCOUT, class BVal, int ST, int NWV>
+__device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragSeq f, BVal bval,
+                                           f32x16 (&acc)[COUT_T], const u32x4 (&)[CARRY6][3], FragSeq nf,
+                                           u32x4 (&)[CARRY6][3]) {
+    static_assert(NWV == 4, "4 waves share the stream");
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of this step landed
+        __syncthreads();
+        const int cur = ring.step & 1;
+        if (c + 1 < NCH)
+            ring_fill<COUT_T>(ring, cur ^ 1, f, c + 1, lane);
+        else
+            ring_fill<NCOUT>(ring, cur ^ 1, nf, 0, lane);
+        u32x4 b[3];
+        split_chunk(bval, c, b);
+        const lds_cu32x4 *sp = ring.lds + cur * Ring6<ST, NWV>::SLOT + lane;
+        // tile co + 1's pieces are read while tile co's six MFMAs run (one tile of pieces
+        // in flight: 12 VGPRs, not the whole step's)
+        u32x4 a[2][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[0][p] = sp[p * 64];
+#pragma unroll
+        for (int co = 0; co < COUT_T; ++co) {
+            if (co + 1 < COUT_T) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) a[(co + 1) & 1][p] = sp[((co + 1) * 3 + p) * 64];
+            }
+            acc[co] = mma6(a[co & 1], b, acc[co]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        ++ring.step;
+    }
+}
+
 }  // namespace hreg_chain
