@@ -96,9 +96,20 @@ __device__ __forceinline__ void conv_stack6(WT &&wt, const float *eb, int gg, in
 #ifndef HREG_RING_WPS
 #define HREG_RING_WPS 3  // waves per SIMD the ring kernel's register budget targets
 #endif
+// level 3 on the ring (engine.SPLIT_L3 off selects it; A/B against the channel-split kernel)
+#ifndef HREG_RING_L3
+#define HREG_RING_L3 1
+#endif
+#ifndef HREG_RING_WPS_L3
+#define HREG_RING_WPS_L3 1
+#endif
+template <class K>
+constexpr bool ring_on() { return HREG_RING && (K::KN == 32 || HREG_RING_L3); }
+template <class K>
+constexpr int ring_wps() { return K::KN == 32 ? HREG_RING_WPS : HREG_RING_WPS_L3; }
 
 template <class K, bool PRE, bool RING = false>
-__global__ __launch_bounds__(256, RING ? HREG_RING_WPS : K::WPS) void group_fused6_kernel(
+__global__ __launch_bounds__(256, RING ? ring_wps<K>() : K::WPS) void group_fused6_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
     float *__restrict__ att_feat, float *__restrict__ desc, const float *__restrict__ pre) {
@@ -273,9 +284,9 @@ int launch_group6(const float *table, const float *geom, const float *knn_xyz, c
     if (!G) return HREG_OK;
     const int NT = G / (32 / K::KN);
     int grid = (NT + WAVES - 1) / WAVES;
-    const int cap = 256 * (HREG_RING && K::KN == 32 ? HREG_RING_WPS : K::WPS) * 4 / WAVES * 2;  // two rounds
+    const int cap = 256 * (ring_on<K>() ? ring_wps<K>() : K::WPS) * 4 / WAVES * 2;  // two rounds
     if (grid > cap) grid = cap;
-    constexpr bool RING = HREG_RING && K::KN == 32;
+    constexpr bool RING = ring_on<K>();
     if (RING && pre)
         hipLaunchKernelGGL((group_fused6_kernel<K, true, RING>), dim3(grid), dim3(256), 0, as_stream(stream),
                            table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
