@@ -249,11 +249,25 @@ int launch_corr6(const float *table, const float *small, const float *ud0, const
 #define HREG_CORR512_P 2
 #endif
 using Corr512 = CorrCfg<512, HREG_CORR512_P>;
+// the FineReg widths and the neighbour head: fewer output tiles per wave = more waves per
+// 32-row tile (their grids are a few hundred to a thousand tiles)
+#ifndef HREG_CORR256_P
+#define HREG_CORR256_P 2
+#endif
+#ifndef HREG_CORR128_P
+#define HREG_CORR128_P 2
+#endif
+#ifndef HREG_NBR_P
+#define HREG_NBR_P 2
+#endif
+using Corr256 = CorrCfg<256, HREG_CORR256_P>;
+using Corr128 = CorrCfg<128, HREG_CORR128_P>;
+using Nbr256 = CorrCfg<256, HREG_NBR_P>;
 
 extern "C" int hreg_coarse_head6_table_floats(void) { return Corr512::TABLE; }
 
 extern "C" int hreg_corr_head6_table_floats(int N1) {
-    return N1 == 512 ? Corr512::TABLE : N1 == 256 ? CorrCfg<256>::TABLE : N1 == 128 ? CorrCfg<128>::TABLE : -1;
+    return N1 == 512 ? Corr512::TABLE : N1 == 256 ? Corr256::TABLE : N1 == 128 ? Corr128::TABLE : -1;
 }
 
 extern "C" int hreg_corr_head6(const float *table, int N1, const float *small, const float *ud0, const float *ud1,
@@ -269,8 +283,8 @@ extern "C" int hreg_corr_head6(const float *table, int N1, const float *small, c
     if (N1 != 512 && N1 != 256 && N1 != 128) return HREG_ERR_UNSUPPORTED;
     if (!G) return HREG_OK;
     if (N1 == 512) return launch_corr6<Corr512>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
-    if (N1 == 256) return launch_corr6<CorrCfg<256>>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
-    return launch_corr6<CorrCfg<128>>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+    if (N1 == 256) return launch_corr6<Corr256>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+    return launch_corr6<Corr128>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
 }
 
 extern "C" int hreg_coarse_head6(const float *table, const float *small, const float *ud0, const float *ud1,
@@ -291,5 +305,5 @@ extern "C" int hreg_nbr_head6s(const float *table, const float *desc, const int3
         return HREG_ERR_INVALID;
     if ((G * KH) % 32) return HREG_ERR_INVALID;
     if (!G) return HREG_OK;
-    return launch_corr6<CorrCfg<256>, true>(table, geom, nullptr, pre, gidx, desc, G, nullptr, out, stream);
+    return launch_corr6<Nbr256, true>(table, geom, nullptr, pre, gidx, desc, G, nullptr, out, stream);
 }

@@ -442,6 +442,10 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 
+#ifndef HREG_RING_EXP
+#define HREG_RING_EXP 0
+#endif
+
 template <int SLOT_TILES, int NWAVES>
 struct Ring6 {
     static constexpr int SLOT = SLOT_TILES * 192;  // u32x4 per slot
@@ -476,8 +480,11 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
     static_assert(NWV == 4, "4 waves share the stream");
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of this step landed
-        __syncthreads();
+        // (HREG_RING_EXP timing experiments, results wrong: 1 = no wait and no barrier,
+        // 2 = no barrier)
+        if constexpr (HREG_RING_EXP != 1)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of this step landed
+        if constexpr (HREG_RING_EXP == 0) __syncthreads();
         const int cur = ring.step & 1;
         if (c + 1 < NCH)
             ring_fill<COUT_T>(ring, cur ^ 1, f, c + 1, lane);
