@@ -442,6 +442,10 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 
+// pieces of tile co + 1 read while tile co's MFMAs run (2) or right before them (1)
+#ifndef HREG_RING_ABUF
+#define HREG_RING_ABUF 2
+#endif
 #ifndef HREG_RING_EXP
 #define HREG_RING_EXP 0
 #endif
@@ -500,7 +504,11 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
         for (int p = 0; p < 3; ++p) a[0][p] = sp[p * 64];
 #pragma unroll
         for (int co = 0; co < COUT_T; ++co) {
-            if (co + 1 < COUT_T) {
+            if (HREG_RING_ABUF == 1 && co > 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) a[co & 1][p] = sp[(co * 3 + p) * 64];
+            }
+            if (HREG_RING_ABUF == 2 && co + 1 < COUT_T) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) a[(co + 1) & 1][p] = sp[((co + 1) * 3 + p) * 64];
             }
