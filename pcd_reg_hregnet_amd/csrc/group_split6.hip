@@ -61,8 +61,8 @@ __device__ __forceinline__ void stage_rows6(float *buf, const float *__restrict_
 
 // conv stack [geom | feat] -> C1 -> C1 -> C3 through the A/B buffers (group_split.hip
 // conv_stack_split); this wave's P3 output tiles in out (epilogue applied).
-template <class K, int NP, bool PRE, bool ONE>
-__device__ __forceinline__ void conv_stack_split6(const gu32x4 *__restrict__ wt, const float *eb, int gg, int gf,
+template <class K, int NP, bool PRE, bool ONE, class WT>
+__device__ __forceinline__ void conv_stack_split6(WT &&wt, const float *eb, int gg, int gf,
                                                   int g2, int g3, int e1, int e2, int e3, float *A, float *B,
                                                   int cw, int lane, f32x16 (&out)[K::P3], const Carry6 &cin,
                                                   FragSeq next, Carry6 &cout, const float *pre_row, float2 gin) {
@@ -123,22 +123,39 @@ __device__ __forceinline__ void conv_stack_split6(const gu32x4 *__restrict__ wt,
 #define HREG_SPLIT_1BUF 1
 #endif
 
-template <class K, bool PRE, bool ONE = (HREG_SPLIT_1BUF && PRE)>
-__global__ __launch_bounds__(256, ONE ? 3 : 2) void group_split6_kernel(
+// HREG_SPLIT_RING (level 3, PRE form): one workgroup of RING_RT row tiles x 4 channel
+// groups (12 waves, 3 per SIMD), the weight pieces through the channel-split LDS ring
+// (split_chain.h RingCW: the RING_RT waves of a channel group share every piece), the
+// epilogue constants read from the table in global memory; LDS 3 x 33 KB activations + 48 KB
+// ring + 8 KB = 153 KB, one workgroup per CU.  Measured slower (off): 249 vs 195 us in the
+// bench, 267 vs 190 standalone -- a step is only 6-12 MFMAs per wave between barriers that
+// span all 12 waves of the CU, with no second workgroup to fill the gaps.
+#ifndef HREG_SPLIT_RING
+#define HREG_SPLIT_RING 0
+#endif
+constexpr int RING_RT = 3;
+
+template <class K, bool PRE, bool ONE = (HREG_SPLIT_1BUF && PRE), bool RING = false>
+__global__ __launch_bounds__(RING ? RING_RT * 256 : 256, RING ? 1 : ONE ? 3 : 2) void group_split6_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
     float *__restrict__ att_feat, float *__restrict__ desc, const float *__restrict__ pre) {
     constexpr int C3 = K::T3 * 32, CM2 = K::TM2 * 32, LDSW = K::LDSW, X2W = K::X2W;
     constexpr int T3 = K::T3, TM1 = K::TM1, P3 = K::P3, PM1 = K::PM1, PM2 = K::PM2;
     constexpr int N3 = K::N3, NM1 = K::NM1;
-    constexpr int NE = K::TABLE - K::F_END, KN = K::KN, GPT = K::GPT, RT = K::RT, CW = K::CW;
-    __shared__ float ep[NE];
+    constexpr int NE = K::TABLE - K::F_END, KN = K::KN, GPT = K::GPT, CW = K::CW;
+    constexpr int RT = RING ? RING_RT : K::RT;
+    static_assert(!RING || (ONE && PRE), "ring: one-buffer PRE form");
+    __shared__ float ep[RING ? 1 : NE];
     __shared__ __attribute__((aligned(16))) float sA[RT][32 * LDSW];
     __shared__ __attribute__((aligned(16))) float sB[ONE ? 1 : RT][ONE ? 4 : 32 * LDSW];
     __shared__ __attribute__((aligned(16))) float sX2[RT][GPT * X2W];
     __shared__ int sMax[RT][CW][32];
-    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
-    const float *eb = ep - K::F_END;
+    constexpr int PMAX = K::P3 > K::PM2 ? (K::P3 > K::P1 ? K::P3 : K::P1) : (K::PM2 > K::PM1 ? K::PM2 : K::PM1);
+    __shared__ __attribute__((aligned(16))) u32x4 ring_lds[RING ? 2 * CW * PMAX * 192 : 1];
+    if constexpr (!RING)
+        for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
+    const float *eb = RING ? table : ep - K::F_END;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int rt = w / CW, cw = w % CW;
     const int h = lane >> 5, j = lane & 31;
@@ -158,7 +175,11 @@ __global__ __launch_bounds__(256, ONE ? 3 : 2) void group_split6_kernel(
     const FragSeq fm2{K::G_M2 + m2 * NM1, NM1};
 
     Carry6 carry;
-    {
+    RingCW<CW * PMAX, RT * CW, CW> ring{reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table)),
+                                       (lds_u32x4 *)ring_lds, 0, w, cw};
+    if constexpr (RING) {
+        ring_fill_cw<K::P1>(ring, 0, FragSeq{K::G_DG, 1}, K::P1, 0, lane);
+    } else {
         const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table));
 #pragma unroll
         for (int i = 0; i < K::P1; ++i) ld6(wt, det_g.base + i * det_g.stride, lane, carry[i]);
@@ -171,7 +192,12 @@ __global__ __launch_bounds__(256, ONE ? 3 : 2) void group_split6_kernel(
         const size_t row = (size_t)t * 32 + j;
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
-        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
+        const gu32x4 *wtp = reinterpret_cast<const gu32x4 *>(tba);
+        ring.wt = wtp;  // (opaque per tile: the DMA addresses are not hoisted out of the loop)
+        auto &&wt = [&]() -> decltype(auto) {
+            if constexpr (RING) return (ring);
+            else return wtp;
+        }();
         Carry6 ca, cb;
 
         const float *prow = PRE ? pre + (size_t)gidx[row] * (2 * K::T1 * 32) : nullptr;
@@ -330,6 +356,15 @@ int launch_split6(const float *table, const float *geom, const float *knn_xyz, c
     if (G % K::GPT) return HREG_ERR_INVALID;  // whole 32-row tiles
     if (!G) return HREG_OK;
     const int NT = G / K::GPT;
+    constexpr bool RING = HREG_SPLIT_RING && HREG_SPLIT_1BUF && K::KN == 16;  // level 3
+    if (RING && pre) {
+        int grid = (NT + RING_RT - 1) / RING_RT;
+        if (grid > 1024) grid = 1024;
+        hipLaunchKernelGGL((group_split6_kernel<K, true, true, RING>), dim3(grid), dim3(RING_RT * 256), 0,
+                           as_stream(stream), table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
+        HREG_CHECK_LAUNCH();
+        return HREG_OK;
+    }
     int grid = (NT + K::RT - 1) / K::RT;
     const int cap = 256 * (HREG_SPLIT_1BUF && pre ? 3 : 2) * 2;  // resident workgroups per CU, two rounds
     if (grid > cap) grid = cap;

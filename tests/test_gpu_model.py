@@ -251,11 +251,13 @@ def test_fused_level_matches_layerwise(net, lvl, split, pre, b6, monkeypatch):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("G", [1, 5, 64, 1000])
+@pytest.mark.parametrize("G", [1, 5, 64, 1000, 13001])
 def test_pair_l2_matches_single(G):
     """hreg_group6x2_l2 (two groups per wave sharing each streamed weight chunk) against
-    hreg_group6_l2 on random tables and rows: the same arithmetic per row, so bitwise equal,
-    odd G (the last pair recomputes its group) included."""
+    hreg_group6_l2 (the LDS weight ring: 4 waves of a workgroup on consecutive groups) on
+    random tables and rows: the same arithmetic per row, so bitwise equal; odd G (the last
+    pair recomputes its group), fewer groups than a workgroup's waves (1, 5) and more groups
+    than one pass of the capped grid (13001) included."""
     from pcd_reg_hregnet_amd import _lib
     L = _lib.load()
     rng = np.random.default_rng(G)
