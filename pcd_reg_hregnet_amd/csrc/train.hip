@@ -47,8 +47,35 @@ __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
             is = invstd[c];
             if (relu && !out) { ga = gamma[c]; be = beta[c]; }
         }
+        int r = r0 + rl;
+        if constexpr (MODE == 1) {
+            // eight rows' loads issued before their (in-order) accumulation: the loop body's
+            // two streams and the mask branch otherwise leave one load in flight per wave
+            const bool rec = relu && !out;
+            for (; r + 7 * nrl < r1; r += 8 * nrl) {
+                float gv[8], yv[8], ov[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const size_t i = (size_t)(r + u * nrl) * C + c;
+                    gv[u] = x[i];
+                    yv[u] = y[i];
+                    ov[u] = relu && out ? out[i] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    float g = gv[u];
+                    const float xh = fmul_rn(fsub_rn(yv[u], mu), is);
+                    if (relu) {
+                        const bool on = rec ? fadd_rn(fmul_rn(xh, ga), be) > 0.f : ov[u] > 0.f;
+                        if (!on) g = 0.f;
+                    }
+                    a += (double)g;
+                    b += (double)g * (double)xh;
+                }
+            }
+        }
 #pragma unroll 4
-        for (int r = r0 + rl; r < r1; r += nrl) {
+        for (; r < r1; r += nrl) {
             const size_t i = (size_t)r * C + c;
             if (MODE == 0) {
                 const double v = x[i];
@@ -126,6 +153,75 @@ __global__ __launch_bounds__(FIN_COLS * FIN_LANES) void col_finalize_kernel(
         o1[c] = (float)a;  // dbeta = sum g
     } else {
         o0[c] = (float)a;
+    }
+}
+
+// bn_apply / bn_backward on float4 groups of 4 channels (C % 4 == 0, C <= BN4_MAXC: every
+// layer of the path), 32-bit indexing, the per-channel parameters staged in LDS (one
+// ds_read_b128 per parameter and float4 instead of 4 scattered global loads); the
+// per-element arithmetic of the scalar kernels (same results)
+constexpr int BN4_MAXC = 512;
+
+template <int NP>
+__device__ __forceinline__ void stage_params(float4 (*sp)[BN4_MAXC / 4], const float *const (&src)[NP], int C4) {
+    for (int k = threadIdx.x; k < NP * C4; k += blockDim.x) {
+        const int a = k / C4, c4 = k - a * C4;
+        const float *p = src[a] + 4 * c4;
+        sp[a][c4] = make_float4(p[0], p[1], p[2], p[3]);
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void bn_apply4_kernel(const float4 *__restrict__ y, const float *__restrict__ mean,
+                                                        const float *__restrict__ invstd,
+                                                        const float *__restrict__ gamma,
+                                                        const float *__restrict__ beta, int relu, int total4,
+                                                        int C4, float4 *__restrict__ out) {
+    __shared__ float4 sp[4][BN4_MAXC / 4];
+    stage_params<4>(sp, {mean, invstd, gamma, beta}, C4);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+        const int c4 = i % C4;
+        const float4 yv = y[i], mu = sp[0][c4], is = sp[1][c4], ga = sp[2][c4], be = sp[3][c4];
+        const float *yp = &yv.x, *mp = &mu.x, *ip = &is.x, *gp = &ga.x, *bp = &be.x;
+        float o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float xh = fmul_rn(fsub_rn(yp[u], mp[u]), ip[u]);
+            float v = fadd_rn(fmul_rn(xh, gp[u]), bp[u]);
+            if (relu) v = fmaxf(v, 0.f);
+            o[u] = v;
+        }
+        out[i] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void bn_backward4_kernel(
+    const float4 *__restrict__ dout, const float4 *__restrict__ out, const float4 *__restrict__ y,
+    const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ gamma,
+    const float *__restrict__ beta, const float *__restrict__ dgamma, const float *__restrict__ dbeta, int relu,
+    int total4, int R, int C4, float4 *__restrict__ dy) {
+    __shared__ float4 sp[6][BN4_MAXC / 4];
+    const float *zero_beta = beta ? beta : mean;  // (beta is only read for the recomputed mask)
+    stage_params<6>(sp, {mean, invstd, gamma, zero_beta, dgamma, dbeta}, C4);
+    const float invR = 1.0f / (float)R;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+        const int c4 = i % C4;
+        const float4 gv4 = dout[i], yv4 = y[i];
+        const float4 ov4 = relu && out ? out[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 mu = sp[0][c4], is = sp[1][c4], ga = sp[2][c4], be = sp[3][c4], dg = sp[4][c4],
+                     db = sp[5][c4];
+        const float *gp = &gv4.x, *yp = &yv4.x, *op = &ov4.x, *mp = &mu.x, *ip = &is.x, *gap = &ga.x,
+                    *bp = &be.x, *dgp = &dg.x, *dbp = &db.x;
+        float o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float g = gp[u];
+            const float xh = fmul_rn(fsub_rn(yp[u], mp[u]), ip[u]);
+            if (relu && !(out ? op[u] > 0.f : fadd_rn(fmul_rn(xh, gap[u]), bp[u]) > 0.f)) g = 0.f;
+            const float t = fsub_rn(fsub_rn(g, fmul_rn(dbp[u], invR)), fmul_rn(xh, fmul_rn(dgp[u], invR)));
+            o[u] = fmul_rn(fmul_rn(t, ip[u]), gap[u]);
+        }
+        dy[i] = make_float4(o[0], o[1], o[2], o[3]);
     }
 }
 
@@ -318,9 +414,9 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g, 
 // streaming reduction needs several waves per SIMD in flight to reach HBM rate; for
 // the weight-gradient GEMM too, despite the extra N x K partials: A/B 235 vs 232
 // train pairs/s against a 512 target)
-int splits_for(int R, int col_blocks, int min_rows, int target = 2048) {
+int splits_for(int R, int col_blocks, int min_rows, int target = 2048, int cap = 1024) {
     int S = 1;
-    while (col_blocks * S < target && R / (S * 2) >= min_rows && S < 1024) S *= 2;
+    while (col_blocks * S < target && R / (S * 2) >= min_rows && S < cap) S *= 2;
     return S;
 }
 
@@ -336,9 +432,13 @@ static int cr_blocks(int C) {
     return (C + cw - 1) / cw;
 }
 
+// row splits of a col_reduce launch; the BN backward's two-stream reduction (MODE 1) takes
+// up to 4096 (a wave keeps only 16 loads in flight: more workgroups, not longer loops)
+static int cr_splits(int R, int C, bool bwd) { return splits_for(R, cr_blocks(C), 256, 2048, bwd ? 4096 : 1024); }
+
 extern "C" size_t hreg_col_reduce_ws_bytes(int R, int C) {
     if (R <= 0 || C <= 0) return 0;
-    const int S = splits_for(R, cr_blocks(C), 256);
+    const int S = cr_splits(R, C, true);  // (>= every mode's)
     return (size_t)S * C * 2 * sizeof(double);
 }
 
@@ -363,8 +463,14 @@ extern "C" int hreg_bn_apply(const float *y, int R, int C, const float *mean, co
     if (!y || !mean || !invstd || !gamma || !beta || !out || R < 0 || C <= 0) return HREG_ERR_INVALID;
     const size_t total = (size_t)R * C;
     if (!total) return HREG_OK;
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(grid1d(total)), dim3(256), 0, as_stream(stream), y, mean,
-                       invstd, gamma, beta, relu, total, C, out);
+    if (C % 4 == 0 && C <= BN4_MAXC && total / 4 < (size_t)INT32_MAX && !(reinterpret_cast<uintptr_t>(y) & 15) &&
+        !(reinterpret_cast<uintptr_t>(out) & 15))
+        hipLaunchKernelGGL(bn_apply4_kernel, dim3(grid1d(total / 4)), dim3(256), 0, as_stream(stream),
+                           reinterpret_cast<const float4 *>(y), mean, invstd, gamma, beta, relu, (int)(total / 4),
+                           C / 4, reinterpret_cast<float4 *>(out));
+    else
+        hipLaunchKernelGGL(bn_apply_kernel, dim3(grid1d(total)), dim3(256), 0, as_stream(stream), y, mean,
+                           invstd, gamma, beta, relu, total, C, out);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -376,7 +482,7 @@ extern "C" int hreg_bn_backward(const float *dout, const float *out, const float
     if (!dout || !y || !mean || !invstd || !gamma || !ws || !dy || !dgamma || !dbeta || R <= 0 ||
         C <= 0 || (relu && !out && !beta))
         return HREG_ERR_INVALID;
-    const int cb = cr_blocks(C), S = splits_for(R, cb, 256);
+    const int cb = cr_blocks(C), S = cr_splits(R, C, true);
     const int rps = (R + S - 1) / S;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(col_reduce_kernel<1>, dim3(cb, S), dim3(CR_THREADS), 0, st, dout, out, y, mean,
@@ -386,8 +492,16 @@ extern "C" int hreg_bn_backward(const float *dout, const float *out, const float
                        (const double *)ws, S, R, C, 0.f, dgamma, dbeta, nullptr);
     HREG_CHECK_LAUNCH();
     const size_t total = (size_t)R * C;
-    hipLaunchKernelGGL(bn_backward_kernel, dim3(grid1d(total)), dim3(256), 0, st, dout, out, y, mean,
-                       invstd, gamma, beta, dgamma, dbeta, relu, total, R, C, dy);
+    if (C % 4 == 0 && C <= BN4_MAXC && total / 4 < (size_t)INT32_MAX &&
+        !((reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(out) |
+           reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(dy)) & 15))
+        hipLaunchKernelGGL(bn_backward4_kernel, dim3(grid1d(total / 4)), dim3(256), 0, st,
+                           reinterpret_cast<const float4 *>(dout), reinterpret_cast<const float4 *>(out),
+                           reinterpret_cast<const float4 *>(y), mean, invstd, gamma, beta, dgamma, dbeta, relu,
+                           (int)(total / 4), R, C / 4, reinterpret_cast<float4 *>(dy));
+    else
+        hipLaunchKernelGGL(bn_backward_kernel, dim3(grid1d(total)), dim3(256), 0, st, dout, out, y, mean,
+                           invstd, gamma, beta, dgamma, dbeta, relu, total, R, C, dy);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
