@@ -27,7 +27,9 @@ inline int cr_width_log2(int C) { return C <= 16 ? 4 : (C <= 32 ? 5 : 6); }
 // per-column sums over rows [r0, r1): MODE 0: (y, y^2); MODE 1: (g, g*xhat) with
 // g = dout * [out > 0 if relu], xhat = (y - mean) * invstd; MODE 2: (x, 0).
 // double accumulators (the variance is E[y^2] - E[y]^2); row lanes combined in order.
-template <int MODE>
+// MK (MODE 1): the ReLU mask -- 0 none, 1 from out, 2 recomputed from y (compile-time, so
+// the batched loads carry no branches)
+template <int MODE, int MK = 0>
 __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
     const float *__restrict__ x, const float *__restrict__ out, const float *__restrict__ y,
     const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ gamma,
@@ -51,7 +53,6 @@ __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
         if constexpr (MODE == 1) {
             // eight rows' loads issued before their (in-order) accumulation: the loop body's
             // two streams and the mask branch otherwise leave one load in flight per wave
-            const bool rec = relu && !out;
             for (; r + 7 * nrl < r1; r += 8 * nrl) {
                 float gv[8], yv[8], ov[8];
 #pragma unroll
@@ -59,14 +60,14 @@ __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
                     const size_t i = (size_t)(r + u * nrl) * C + c;
                     gv[u] = x[i];
                     yv[u] = y[i];
-                    ov[u] = relu && out ? out[i] : 0.f;
+                    ov[u] = MK == 1 ? out[i] : 0.f;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     float g = gv[u];
                     const float xh = fmul_rn(fsub_rn(yv[u], mu), is);
-                    if (relu) {
-                        const bool on = rec ? fadd_rn(fmul_rn(xh, ga), be) > 0.f : ov[u] > 0.f;
+                    if (MK != 0) {
+                        const bool on = MK == 2 ? fadd_rn(fmul_rn(xh, ga), be) > 0.f : ov[u] > 0.f;
                         if (!on) g = 0.f;
                     }
                     a += (double)g;
@@ -485,8 +486,9 @@ extern "C" int hreg_bn_backward(const float *dout, const float *out, const float
     const int cb = cr_blocks(C), S = cr_splits(R, C, true);
     const int rps = (R + S - 1) / S;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(col_reduce_kernel<1>, dim3(cb, S), dim3(CR_THREADS), 0, st, dout, out, y, mean,
-                       invstd, gamma, beta, relu, R, C, rps, cr_width_log2(C), (double *)ws);
+    auto red = !relu ? col_reduce_kernel<1, 0> : out ? col_reduce_kernel<1, 1> : col_reduce_kernel<1, 2>;
+    hipLaunchKernelGGL(red, dim3(cb, S), dim3(CR_THREADS), 0, st, dout, out, y, mean, invstd, gamma, beta, relu, R,
+                       C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
     hipLaunchKernelGGL(col_finalize_kernel<1>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
                        (const double *)ws, S, R, C, 0.f, dgamma, dbeta, nullptr);
