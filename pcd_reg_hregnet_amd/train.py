@@ -19,6 +19,8 @@ arithmetic op runs in the HIP library, which must be present (no CPU fallback).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -26,6 +28,14 @@ from . import _lib, engine
 
 BN_MOMENTUM = 0.1  # nn.BatchNorm default
 BN_EPS = 1e-5
+# conv products (forward and input-gradient GEMMs) on hreg_gemm6: fp32-accurate bf16x6
+# products on the bf16 matrix cores (engine.B6_GEMM) instead of the f32 MFMA
+# for outputs at least TRAIN_B6_MIN_N wide (hreg_gemm6 has 128 x 128 tiles only: narrower
+# outputs stay on hreg_gemm's 256 x 32 / 256 x 64 tiles).  Off: the step gains 1-3 % (noise
+# level, tools/train_ab.sh) and the reference-gradient test's d/d dst_sigmas_3 error moves
+# to 1.16x its bar.
+TRAIN_B6 = os.environ.get("HREG_TRAIN_B6", "0") != "0"
+TRAIN_B6_MIN_N = int(os.environ.get("HREG_TRAIN_B6_MIN_N", "128"))
 
 
 def _stream():
@@ -95,7 +105,7 @@ def _plain_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None) ->
     ones = _const(1.0, N, x.device)
     sh = shift if shift is not None else _const(0.0, N, x.device)
     lin = engine.Lin(W.contiguous(), ones, sh.contiguous(), relu=False)
-    return engine.gemm([engine._seg(x, 0, K)], lin, R)
+    return engine.gemm([engine._seg(x, 0, K)], lin, R, b6=TRAIN_B6 and N >= TRAIN_B6_MIN_N)
 
 
 class _ConvBNAct(torch.autograd.Function):
