@@ -442,6 +442,10 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 
+// HREG_RING_SWP: chunk c + 1's B split in the shadow of tile 0's MFMAs of chunk c
+#ifndef HREG_RING_SWP
+#define HREG_RING_SWP 0
+#endif
 // pieces of tile co + 1 read while tile co's MFMAs run (2) or right before them (1)
 #ifndef HREG_RING_ABUF
 #define HREG_RING_ABUF 2
@@ -482,6 +486,8 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
                                            f32x16 (&acc)[COUT_T], const u32x4 (&)[CARRY6][3], FragSeq nf,
                                            u32x4 (&)[CARRY6][3]) {
     static_assert(NWV == 4, "4 waves share the stream");
+    u32x4 b[3], bn[3];
+    (void)bn;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         // (HREG_RING_EXP timing experiments, results wrong: 1 = no wait and no barrier,
@@ -494,8 +500,7 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
             ring_fill<COUT_T>(ring, cur ^ 1, f, c + 1, lane);
         else
             ring_fill<NCOUT>(ring, cur ^ 1, nf, 0, lane);
-        u32x4 b[3];
-        split_chunk(bval, c, b);
+        if (!HREG_RING_SWP || c == 0) split_chunk(bval, c, b);
         const lds_cu32x4 *sp = ring.lds + cur * Ring6<ST, NWV>::SLOT + lane;
         // tile co + 1's pieces are read while tile co's six MFMAs run (one tile of pieces
         // in flight: 12 VGPRs, not the whole step's)
@@ -513,7 +518,12 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
                 for (int p = 0; p < 3; ++p) a[(co + 1) & 1][p] = sp[((co + 1) * 3 + p) * 64];
             }
             acc[co] = mma6(a[co & 1], b, acc[co]);
+            if (HREG_RING_SWP && co == 0 && c + 1 < NCH) split_chunk(bval, c + 1, bn);  // under tile 0's MFMAs
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (HREG_RING_SWP) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) b[p] = bn[p];
         }
         ++ring.step;
     }
