@@ -159,6 +159,7 @@ def _l1_work(a):
 MFMA_ENTRIES = {
     "hreg_group_l1": ("level", _l1_work),
     "hreg_group_l1_6": ("level", _l1_work),
+    "hreg_group_l1_6g": ("level", _l1_work),
     "hreg_group_l2": ("level", _level_work(2)),
     "hreg_group_l3": ("level", _level_work(3)),
     "hreg_group_split_l2": ("level", _level_work(2)),

@@ -484,6 +484,11 @@ int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
 int hreg_group_l1_6_table_floats(void);
 int hreg_group_l1_6(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
                     float *att_feat, float *desc, void *stream);
+/* The same with the weight table streamed from global memory instead of resident in LDS
+ * (4-wave workgroups, no 92 KB LDS claim): for clouds whose FPS runs on the multi-workgroup
+ * cluster kernel alongside (engine.L1_LDS_MAX_N); bitwise-equal outputs. */
+int hreg_group_l1_6g(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
+                     float *att_feat, float *desc, void *stream);
 
 /* The level-2 / level-3 stages above with fp32-accurate products on the bf16 matrix
  * cores (bf16x6 split, group_fused6.hip): same arguments and outputs, table =

@@ -77,6 +77,7 @@ _SIGS = {
                                  _vp],
     "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l1_6": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_group_l1_6g": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],

@@ -23,12 +23,9 @@
 //  * built without packed fp32 VALU ops (build.NO_PACKED_F32): with them this kernel gave
 //    nondeterministic wrong accumulator values whenever two waves shared a SIMD.
 #include "mfma_chain.h"
-// HREG_L1_LDSW (below): weight table resident in LDS
-#ifndef HREG_L1_LDSW
-#define HREG_L1_LDSW 1
-#endif
-#if HREG_L1_LDSW
-#define HREG_PIN_PREFETCH 1
+// weight table resident in LDS (below: the LDSW kernel form, hreg_group_l1_6) or streamed
+// from global memory (hreg_group_l1_6g)
+#define HREG_PIN_PREFETCH 1  // (mfma_jt.h: applies to the LDS-table form only)
 namespace hreg_chain {
 __device__ __forceinline__ void ld6(const __attribute__((address_space(3))) u32x4 *wt, int f, int lane,
                                     u32x4 (&o)[3]) {
@@ -37,7 +34,6 @@ __device__ __forceinline__ void ld6(const __attribute__((address_space(3))) u32x
     for (int p = 0; p < 3; ++p) o[p] = fp[p * 64 + lane];
 }
 }  // namespace hreg_chain
-#endif
 #include "mfma_jt.h"
 #include "rowred.h"
 
@@ -92,48 +88,50 @@ __device__ __forceinline__ void conv_stack6(WP wt, const float *eb, int g1, int 
 #ifndef HREG_L16_WPS
 #define HREG_L16_WPS 2  // waves per SIMD the register budget targets (A/B builds: 3)
 #endif
-// HREG_L1_LDSW: the whole weight-piece table (90 KB) resident in LDS -- each 8-wave
+// LDSW (hreg_group_l1_6): the whole weight-piece table (90 KB) resident in LDS -- each 8-wave
 // workgroup copies it once and loops over 16+ groups; chunk fragments are ds_read_b128
 // (the per-wave weight streams through the vector-memory path keep the CU's texture-data
 // return unit ~70-87 % busy).  The epilogue constants then come through vector memory so
 // that the LDS counter tracks the fragment reads alone, and the prefetch is pinned ahead
 // of each chunk's MFMAs (mfma_jt.h HREG_PIN_PREFETCH).  Measured: 172.7 vs 175.2 us in the
-// bench, 328k vs 340k cycles standalone.
-constexpr int L1_WAVES = HREG_L1_LDSW ? 8 : WAVES;
+// bench, 328k vs 340k cycles standalone.  But the 92 KB of LDS leave no room beside a
+// co-running kernel that holds LDS on every CU -- Model_V2's cluster FPS (clouds > 16384
+// points) -- so that configuration runs the global-table form (LDSW false, 4-wave
+// workgroups): Model_V2 942 vs 856 pairs/s.
+template <bool LDSW>
+constexpr int l1_waves() { return LDSW ? 8 : WAVES; }
 typedef __attribute__((address_space(3))) const u32x4 lu32x4;
 
-__global__ __launch_bounds__(L1_WAVES * 64, HREG_L1_LDSW ? 1 : HREG_L16_WPS) void group_l1_6_kernel(
+template <bool LDSW>
+__global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : HREG_L16_WPS) void group_l1_6_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     int G, float *__restrict__ kp, float *__restrict__ att_feat, float *__restrict__ desc) {
-#if HREG_L1_LDSW
-    __shared__ u32x4 wl[G_END * 192];
-    for (int i = threadIdx.x; i < G_END * 192; i += blockDim.x) wl[i] = reinterpret_cast<const u32x4 *>(table)[i];
-    __syncthreads();
-    const float *eb = table;
-#else
+    constexpr int L1_WAVES = l1_waves<LDSW>();
     constexpr int NE = TABLE_FLOATS - F_END;
-    __shared__ float ep[NE];
-    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[F_END + i];
+    __shared__ u32x4 wl[LDSW ? G_END * 192 : 1];
+    __shared__ float ep[LDSW ? 1 : NE];
+    if constexpr (LDSW) {
+        for (int i = threadIdx.x; i < G_END * 192; i += blockDim.x) wl[i] = reinterpret_cast<const u32x4 *>(table)[i];
+    } else {
+        for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[F_END + i];
+    }
     __syncthreads();
-    const float *eb = ep - F_END;
-#endif
+    const float *eb = LDSW ? table : ep - F_END;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
     const FragSeq m1x2{G_M1, 12}, m1x1{G_M1 + 4, 12}, m1em{G_M1 + 8, 12}, m2{G_M2, 2};
     // opaque per-group table pointer: keeps the loop-invariant weight loads in the loop
-#if HREG_L1_LDSW
     auto table_ptr = [&]() {
-        uint32_t lb = (uint32_t)reinterpret_cast<uintptr_t>((const lu32x4 *)wl);
-        asm volatile("" : "+s"(lb));
-        return (const lu32x4 *)(uintptr_t)lb;
+        if constexpr (LDSW) {
+            uint32_t lb = (uint32_t)reinterpret_cast<uintptr_t>((const lu32x4 *)wl);
+            asm volatile("" : "+s"(lb));
+            return (const lu32x4 *)(uintptr_t)lb;
+        } else {
+            uint64_t tba = reinterpret_cast<uint64_t>(table);
+            asm volatile("" : "+s"(tba));
+            return reinterpret_cast<const gu32x4 *>(tba);
+        }
     };
-#else
-    auto table_ptr = [&]() {
-        uint64_t tba = reinterpret_cast<uint64_t>(table);
-        asm volatile("" : "+s"(tba));
-        return reinterpret_cast<const gu32x4 *>(tba);
-    };
-#endif
 
     Carry carry;
     ld6(table_ptr(), G_DC1, lane, carry[0]);
@@ -233,20 +231,32 @@ __global__ __launch_bounds__(L1_WAVES * 64, HREG_L1_LDSW ? 1 : HREG_L16_WPS) voi
 
 extern "C" int hreg_group_l1_6_table_floats(void) { return TABLE_FLOATS; }
 
-extern "C" int hreg_group_l1_6(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
-                               float *att_feat, float *desc, void *stream) {
+template <bool LDSW>
+static int launch_l1_6(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
+                       float *att_feat, float *desc, void *stream) {
     if (!table || !geom || !knn_xyz || !kp || !att_feat || !desc || G < 0) return HREG_ERR_INVALID;
     if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(geom) & 7) ||
         (reinterpret_cast<uintptr_t>(att_feat) & 15) || (reinterpret_cast<uintptr_t>(desc) & 15))
         return HREG_ERR_INVALID;
     if (!G) return HREG_OK;
+    constexpr int L1_WAVES = l1_waves<LDSW>();
     int grid = (G + L1_WAVES - 1) / L1_WAVES;
     // LDS table: workgroups of 8 waves x 2+ groups (the 90 KB copy amortised over 16 groups;
     // a fully persistent grid stalls behind CUs held by concurrent kernels)
-    const int cap = HREG_L1_LDSW ? 1024 : 2048;
+    const int cap = LDSW ? 1024 : 2048;
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(group_l1_6_kernel, dim3(grid), dim3(L1_WAVES * 64), 0, as_stream(stream), table, geom,
+    hipLaunchKernelGGL(group_l1_6_kernel<LDSW>, dim3(grid), dim3(L1_WAVES * 64), 0, as_stream(stream), table, geom,
                        knn_xyz, G, kp, att_feat, desc);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
+}
+
+extern "C" int hreg_group_l1_6(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
+                               float *att_feat, float *desc, void *stream) {
+    return launch_l1_6<true>(table, geom, knn_xyz, G, kp, att_feat, desc, stream);
+}
+
+extern "C" int hreg_group_l1_6g(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
+                                float *att_feat, float *desc, void *stream) {
+    return launch_l1_6<false>(table, geom, knn_xyz, G, kp, att_feat, desc, stream);
 }

@@ -17,6 +17,15 @@ typedef u32x4 Carry[CARRY6][3];
 // acc[co][jt] += sum_{c < NCH} A(co, c) x B_jt(c), B_jt(c) = split(bval(jt, 8c .. 8c+7));
 // the A pieces of a chunk are loaded once for both row tiles.  SAMEB: B does not depend
 // on jt (split once).  cin / cout as mfma_pipe6 (double-buffered: COUT_T <= 2 here).
+template <class T>
+struct is_lds_table {
+    static constexpr bool value = false;
+};
+template <>
+struct is_lds_table<const __attribute__((address_space(3))) u32x4 *> {
+    static constexpr bool value = true;
+};
+
 template <int NCH, int COUT_T, int NCOUT, bool SAMEB, class BVal, class WP>
 __device__ __forceinline__ void pipe6_jt(WP wt, int lane, FragSeq f, BVal bval,
                                          f32x16 (&acc)[COUT_T][JT], const Carry &cin, FragSeq nf,
@@ -49,7 +58,9 @@ __device__ __forceinline__ void pipe6_jt(WP wt, int lane, FragSeq f, BVal bval,
             for (int co = 0; co < NCOUT; ++co) ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
         }
 #ifdef HREG_PIN_PREFETCH
-        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this chunk's MFMAs
+        // keep the prefetch ahead of this chunk's MFMAs (LDS-resident tables: the compiler
+        // otherwise sinks each ds_read next to its MFMA)
+        if constexpr (is_lds_table<WP>::value) __builtin_amdgcn_sched_barrier(0);
 #endif
         if constexpr (!HREG_SWP) split_jt(c, b[c & 1]);
 #pragma unroll

@@ -71,6 +71,10 @@ B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
 # the FineReg heads on coarse6.hip's channel-split correspondence kernel (hreg_corr_head6:
 # N1/64 waves of two output tiles, activations through LDS, ~136 VGPRs) instead of the
 # register-chained fine_head6_kernel (one wave per SIMD at N1 = 256)
+# level 1 with its weight table resident in LDS (hreg_group_l1_6) for clouds up to this many
+# points; above, the cluster FPS co-runs on every CU and the 92 KB LDS claim would wait for
+# it, so the global-table form (hreg_group_l1_6g) runs: Model_V2 942 vs 856 pairs/s
+L1_LDS_MAX_N = int(os.environ.get("HREG_L1_LDS_MAX_N", "16384"))
 SPLIT_FINE = os.environ.get("HREG_SPLIT_FINE", "1") != "0"
 SPLIT_NBR = os.environ.get("HREG_SPLIT_NBR", "1") != "0"  # the neighbour branch likewise
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
@@ -849,7 +853,8 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         att_feat = _empty(G, LEVELS[0][3][-1], device=dev)
         desc = _empty(G, LEVELS[0][5], device=dev)
         if B6_L1:
-            call("hreg_group_l1_6", P.l1_table6, geom, kx, G, kp, att_feat, desc, _stream())
+            call("hreg_group_l1_6" if n <= L1_LDS_MAX_N else "hreg_group_l1_6g", P.l1_table6, geom, kx, G, kp,
+                 att_feat, desc, _stream())
         else:
             call("hreg_group_l1", P.l1_table, geom, kx, G, kp, att_feat, desc, _stream())
         sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,

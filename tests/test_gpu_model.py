@@ -284,6 +284,33 @@ def test_pair_l2_matches_single(G):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("G", [1, 7, 4099])
+def test_l1_global_table_matches_lds_table(G):
+    """hreg_group_l1_6g (weight table streamed from global memory, 4-wave workgroups) against
+    hreg_group_l1_6 (table resident in LDS, 8-wave workgroups) on random tables and rows: the
+    same arithmetic per group, so bitwise equal."""
+    from pcd_reg_hregnet_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(G + 11)
+
+    def t(x):
+        return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).cuda()
+
+    tb = t(rng.normal(0, 0.1, L.hreg_group_l1_6_table_floats()))
+    geom, kx = t(rng.normal(size=(G * 64, 4))), t(rng.normal(size=(G * 64, 3)))
+    outs = []
+    for name in ("hreg_group_l1_6", "hreg_group_l1_6g"):
+        kp = torch.full((G, 3), float("nan"), device="cuda")
+        att = torch.full((G, 64), float("nan"), device="cuda")
+        desc = torch.full((G, 64), float("nan"), device="cuda")
+        _lib.call(name, tb, geom, kx, G, kp, att, desc, _lib.stream_handle())
+        outs.append((kp, att, desc))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert not torch.isnan(b).any()
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("pre,b6,split", [(True, True, True), (True, True, False), (True, False, False),
                                           (False, False, False)])
 @pytest.mark.parametrize("name,C,N", [("fine_corres_1", 64, 1024), ("fine_corres_2", 128, 512)])
