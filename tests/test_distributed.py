@@ -85,7 +85,9 @@ def _bucket_worker(rank, world, port, q):
     synced = (torch.equal(mine[0].detach(), torch.zeros(5, 3)) and
               torch.equal(mine[1].detach(), torch.full((7,), 3.0)) and
               mine[1].data_ptr() == fp.flat.data_ptr() + 64 * 4)
-    q.put((rank, params[0].grad.clone(), params[1].grad.clone(), b.flat.numel(),
+    # numpy copies: a tensor on a multiprocessing queue travels as a shared-memory fd
+    # that the receiver can only open while this process is still alive
+    q.put((rank, params[0].grad.numpy().copy(), params[1].grad.numpy().copy(), b.flat.numel(),
            params[0].grad.data_ptr() == b.flat.data_ptr() and
            params[1].grad.data_ptr() == b.flat.data_ptr() + 64 * 4, synced))
     dist.barrier()
@@ -109,5 +111,5 @@ def test_gloo_grad_bucket_all_reduce():
     for _, g0, g1, n, view, synced in res:
         assert n == 128 and view  # 5x3 + 7 trainable floats, each padded to 64 (256 B)
         assert synced
-        assert torch.equal(g0, torch.full((5, 3), 1.5))   # mean of 1 and 2
-        assert torch.equal(g1, torch.full((7,), 15.0))    # mean of 10 and 20
+        assert torch.equal(torch.from_numpy(g0), torch.full((5, 3), 1.5))   # mean of 1 and 2
+        assert torch.equal(torch.from_numpy(g1), torch.full((7,), 15.0))    # mean of 10 and 20
