@@ -525,7 +525,8 @@ bool launch_reg(int T, int G, int QT, int b, int n, int m, int bs, int L, const 
     }
     HREG_FPS_CASE(1024, 1, 1) HREG_FPS_CASE(1024, 1, 2) HREG_FPS_CASE(1024, 1, 4)
     HREG_FPS_CASE(1024, 1, 8)
-    if constexpr (!WEIGHTED) { HREG_FPS_CASE(1024, 1, 16) }
+    // (512, 2, 16) unweighted only: the weighted form needs 32 more VGPRs and spills
+    if constexpr (!WEIGHTED) { HREG_FPS_CASE(1024, 1, 16) HREG_FPS_CASE(512, 2, 16) }
     HREG_FPS_CASE(512, 1, 1) HREG_FPS_CASE(512, 1, 2)
     HREG_FPS_CASE(256, 4, 1) HREG_FPS_CASE(256, 1, 1) HREG_FPS_CASE(256, 1, 2)
     HREG_FPS_CASE(128, 4, 1) HREG_FPS_CASE(128, 1, 1) HREG_FPS_CASE(128, 1, 2)
@@ -554,6 +555,13 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     else { T = 64; G = 1; }
     // per-slot registers (x, y, z, temp[, w]) must fit the VGPR budget
     if (T == 1024 && QT > (weighted ? 8 : 16)) { T = 512; G = 2; }
+    // n = 16384 (level 1): 8 waves x 32 slots rather than 16 waves x 16 -- the same VALU
+    // work per SIMD, half the per-wave reduction/winner overhead; both fill a CU's VGPRs
+    // (127 x 1024 vs 254 x 512).  768 clouds (the batched level-1 stage) 5.70 -> 5.19 ms,
+    // identical indices (tools/micro/fps_l1_geom.py); HREG_FPS_L1_1024 keeps 16 x 16.
+    if (!weighted && T == 1024 && QT == 16 && getenv("HREG_FPS_L1_1024") == nullptr) {
+        T = 512; G = 2;
+    }
 }
 
 template <bool WEIGHTED>
