@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void knnd_wave_kernel(const float *__restrict_
     }
 }
 
-// ---- spatially indexed kNN grouping (xyz, n <= 16384) --------------------
+// ---- spatially indexed kNN grouping (xyz, n <= 65536) --------------------
 // hreg_spatial_index orders each cloud's points by a 12-bit Morton cell (one
 // workgroup per cloud, counting sort in LDS) and records the bounding box of
 // every run of 64 ordered points.  A query then scans only the
@@ -322,7 +322,8 @@ __global__ __launch_bounds__(256) void knnd_wave_kernel(const float *__restrict_
 #define HREG_SI_EXP 0  // tools/si_experiment.py: 1 no sort, 2 no boxes, 3 bbox + keys only
 #endif
 constexpr int SI_THREADS = 1024;
-constexpr int SI_MAXN = 16384;
+constexpr int SI_LDSN = 16384;  // clouds up to this size sort through an LDS index list
+constexpr int SI_MAXN = 65536;  // larger ones (Model_V2's config 5) scatter straight to HBM
 
 __device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits -> every third bit
     v &= 0x3ffu;
@@ -347,14 +348,17 @@ __device__ __forceinline__ float box_lb(float qx, float qy, float qz, float4 lo,
 
 constexpr int SI_CELLS = 4096;  // 12-bit Morton prefix: a 16 x 16 x 16 grid
 
+template <bool BIG>
 __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *__restrict__ p, int n,
                                                                    float4 *__restrict__ spts,
                                                                    float4 *__restrict__ boxes) {
     // counting sort of the points by the top 12 bits of their Morton code (the order
     // inside a cell is whatever the LDS atomics give: it only shapes the boxes, the
-    // kNN result does not depend on it)
+    // kNN result does not depend on it).  BIG (n > SI_LDSN): the sorted rank list does
+    // not fit LDS, so points are scattered to their sorted slot in HBM directly and
+    // the boxes read them back (this workgroup's own stores; fenced at agent scope)
     __shared__ uint32_t cnt[SI_CELLS];
-    __shared__ int sidx[SI_MAXN];
+    __shared__ int sidx[BIG ? 1 : SI_LDSN];
     __shared__ float red[6][SI_THREADS / 64];
     __shared__ uint32_t wsum[SI_THREADS / 64];
     const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -411,14 +415,23 @@ __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *
 #pragma unroll
     for (int e = 0; e < PER; ++e) { cnt[tid * PER + e] = run; run += v[e]; }
     __syncthreads();
-    for (int i = tid; i < n; i += SI_THREADS) sidx[atomicAdd(&cnt[cell_of(i)], 1u)] = i;
-    __syncthreads();
     int np = 64;
     while (np < n) np <<= 1;
     float4 *S = spts + (size_t)c * np;
-    for (int i = tid; i < n; i += SI_THREADS) {
-        const int id = sidx[i];
-        S[i] = make_float4(P[id * 3], P[id * 3 + 1], P[id * 3 + 2], __int_as_float(id));
+    if constexpr (BIG) {
+        for (int i = tid; i < n; i += SI_THREADS)
+            S[atomicAdd(&cnt[cell_of(i)], 1u)] =
+                make_float4(P[i * 3], P[i * 3 + 1], P[i * 3 + 2], __int_as_float(i));
+        __threadfence();  // release: the scattered stores complete before the barrier
+        __syncthreads();
+        __threadfence();  // acquire: no stale L1 lines for the reads below
+    } else {
+        for (int i = tid; i < n; i += SI_THREADS) sidx[atomicAdd(&cnt[cell_of(i)], 1u)] = i;
+        __syncthreads();
+        for (int i = tid; i < n; i += SI_THREADS) {
+            const int id = sidx[i];
+            S[i] = make_float4(P[id * 3], P[id * 3 + 1], P[id * 3 + 2], __int_as_float(id));
+        }
     }
     const int nblk = (HREG_SI_EXP & 2) ? 0 : (n + 63) / 64;
     float4 *B = boxes + (size_t)c * (np / 64) * 2;
@@ -426,9 +439,14 @@ __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *
         const int i = b * 64 + lane;
         float v3[3], u3[3];
         if (i < n) {
-            const int id = sidx[i];
+            if constexpr (BIG) {
+                const float4 v = S[i];
+                v3[0] = u3[0] = v.x; v3[1] = u3[1] = v.y; v3[2] = u3[2] = v.z;
+            } else {
+                const int id = sidx[i];
 #pragma unroll
-            for (int d = 0; d < 3; ++d) v3[d] = u3[d] = P[id * 3 + d];
+                for (int d = 0; d < 3; ++d) v3[d] = u3[d] = P[id * 3 + d];
+            }
         } else {
 #pragma unroll
             for (int d = 0; d < 3; ++d) { v3[d] = __builtin_huge_valf(); u3[d] = -__builtin_huge_valf(); }
@@ -455,12 +473,14 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return min(a, c);
 }
 
-template <int K>
+// NBL point blocks of 64 per lane: 4 for n <= 16384, 16 for n <= 65536
+template <int K, int NBL>
 __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
     const float *__restrict__ q, const float *__restrict__ p, const float4 *__restrict__ spts,
     const float4 *__restrict__ boxes, int nb, int m, int n, int k, int32_t *__restrict__ gidx,
     float *__restrict__ geom, float *__restrict__ knn_xyz) {
-    constexpr int NBL = SI_MAXN / 64 / 64;  // blocks per lane (<= 256 blocks)
+    constexpr int IDB = NBL * 64 <= 256 ? 8 : 10;  // low key bits carrying the block id
+    constexpr uint32_t HI = ~((1u << IDB) - 1u);
     __shared__ uint64_t sbuf[WAVES][128];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int qi = blockIdx.x * WAVES + w;
@@ -494,14 +514,14 @@ __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
             const uint32_t kk = lb[t] == 0xffffffffu ? 0xffffffffu
-                                                     : ((lb[t] & 0xffffff00u) | (uint32_t)(t * 64 + lane));
+                                                     : ((lb[t] & HI) | (uint32_t)(t * 64 + lane));
             kmin = kk < kmin ? kk : kmin;
         }
         kmin = wave_min_u32(kmin);
         if (kmin == 0xffffffffu) break;
         const uint32_t tau_bits = (uint32_t)(L.tau >> 32);  // >= 0x7f800000 while unset
-        if ((kmin & 0xffffff00u) > tau_bits) break;
-        const int b = (int)(kmin & 0xffu);
+        if ((kmin & HI) > tau_bits) break;
+        const int b = (int)(kmin & ~HI);
         const uint32_t lbb = __builtin_amdgcn_readlane(lb[b >> 6], b & 63);
 #pragma unroll
         for (int t = 0; t < NBL; ++t)
@@ -636,8 +656,12 @@ extern "C" int hreg_spatial_index(const float *p, int nb, int n, void *ws, void 
     const size_t np = spatial_index_np(n);
     float4 *spts = static_cast<float4 *>(ws);
     float4 *boxes = spts + (size_t)nb * np;
-    hipLaunchKernelGGL(spatial_index_kernel, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream), p, n,
-                       spts, boxes);
+    if (n > SI_LDSN)
+        hipLaunchKernelGGL(spatial_index_kernel<true>, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream),
+                           p, n, spts, boxes);
+    else
+        hipLaunchKernelGGL(spatial_index_kernel<false>, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream),
+                           p, n, spts, boxes);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -654,13 +678,17 @@ extern "C" int hreg_knn_group_indexed(const float *q, const float *p, const void
     const float4 *boxes = spts + (size_t)nb * np;
     hipStream_t st = as_stream(stream);
     dim3 grid((nb * m + WAVES - 1) / WAVES);
-#define HREG_KGI(KK)                                                                             \
-    hipLaunchKernelGGL((knn_group_indexed_kernel<KK>), grid, dim3(256), 0, st, q, p, spts, boxes, \
-                       nb, m, n, k, gidx, geom, knn_xyz)
-    if (k <= 8) HREG_KGI(8);
-    else if (k <= 16) HREG_KGI(16);
-    else if (k <= 32) HREG_KGI(32);
-    else HREG_KGI(64);
+#define HREG_KGI(KK)                                                                              \
+    if (n > SI_LDSN)                                                                              \
+        hipLaunchKernelGGL((knn_group_indexed_kernel<KK, SI_MAXN / 4096>), grid, dim3(256), 0, st, q, \
+                           p, spts, boxes, nb, m, n, k, gidx, geom, knn_xyz);                      \
+    else                                                                                          \
+        hipLaunchKernelGGL((knn_group_indexed_kernel<KK, SI_LDSN / 4096>), grid, dim3(256), 0, st, q, \
+                           p, spts, boxes, nb, m, n, k, gidx, geom, knn_xyz)
+    if (k <= 8) { HREG_KGI(8); }
+    else if (k <= 16) { HREG_KGI(16); }
+    else if (k <= 32) { HREG_KGI(32); }
+    else { HREG_KGI(64); }
 #undef HREG_KGI
     HREG_CHECK_LAUNCH();
     return HREG_OK;

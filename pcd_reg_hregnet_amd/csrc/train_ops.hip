@@ -478,24 +478,39 @@ __global__ void sim_bwd_rows_kernel(const float *__restrict__ S, int nb, int N1,
 }
 
 // column-max term: dcm_n = -sum_{(i,j): kidx = n} g2 S[i][n] / (cmax_n+1e-6)^2 -> dS[carg_n][n]
-__global__ void sim_bwd_cols_kernel(const float *__restrict__ S, int nb, int N1, int N2,
-                                    const int32_t *__restrict__ kidx, int k,
-                                    const float *__restrict__ cmax, const int32_t *__restrict__ carg,
-                                    const float *__restrict__ dout, int ldd, float *__restrict__ dS) {
-    GRID_STRIDE(bn, (size_t)nb * N2) {
+// One wave per column (b, n): the N1*k index entries are scanned 64 per step (one
+// coalesced load + ballot) and the matches applied in ascending e, i.e. the same
+// sequential sum as a one-thread serial scan, at 1/64 of its dependent steps (one
+// thread per column scanned 2048 entries: 293 us at B = 8, r2 training profile).
+__global__ __launch_bounds__(TB) void sim_bwd_cols_kernel(
+    const float *__restrict__ S, int nb, int N1, int N2, const int32_t *__restrict__ kidx, int k,
+    const float *__restrict__ cmax, const int32_t *__restrict__ carg,
+    const float *__restrict__ dout, int ldd, float *__restrict__ dS) {
+    constexpr int WPB = TB / 64;
+    const int lane = threadIdx.x & 63;
+    const int E = N1 * k;
+    for (size_t bn = (size_t)blockIdx.x * WPB + threadIdx.x / 64; bn < (size_t)nb * N2;
+         bn += (size_t)gridDim.x * WPB) {
         const int b = (int)(bn / N2), n = (int)(bn % N2);
         const float cm = fadd_rn(cmax[bn], 1e-6f);
         const float cm2 = fmul_rn(cm, cm);
         float dcm = 0.f;
-        const int32_t *ki = kidx + (size_t)b * N1 * k;
-        for (int e = 0; e < N1 * k; ++e)
-            if (ki[e] == n) {
-                const int i = e / k;
+        const int32_t *ki = kidx + (size_t)b * E;
+        for (int e0 = 0; e0 < E; e0 += 64) {
+            const int e = e0 + lane;
+            uint64_t hit = __ballot(e < E && ki[e] == n);
+            while (hit) {  // wave-uniform: every lane computes the same terms
+                const int ee = e0 + (int)__builtin_ctzll(hit);
+                hit &= hit - 1;
+                const int i = ee / k;
                 const float s = S[((size_t)b * N1 + i) * N2 + n];
-                dcm = fsub_rn(dcm, dout[((size_t)b * N1 * k + e) * ldd + 1] * s / cm2);
+                dcm = fsub_rn(dcm, dout[((size_t)b * E + ee) * ldd + 1] * s / cm2);
             }
-        float *p = dS + ((size_t)b * N1 + carg[bn]) * N2 + n;
-        *p = fadd_rn(*p, dcm);
+        }
+        if (lane == 0) {
+            float *p = dS + ((size_t)b * N1 + carg[bn]) * N2 + n;
+            *p = fadd_rn(*p, dcm);
+        }
     }
 }
 
@@ -1155,7 +1170,7 @@ extern "C" int hreg_sim_feats_bwd(const float *S, const float *a, const float *b
     hipLaunchKernelGGL(sim_bwd_rows_kernel, dim3(g1d((size_t)nb * N1)), dim3(TB), 0, st, S, nb, N1,
                        N2, kidx, k, rmax, rarg, cmax, dout, ldd, dS);
     HREG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(sim_bwd_cols_kernel, dim3(g1d((size_t)nb * N2)), dim3(TB), 0, st, S, nb, N1,
+    hipLaunchKernelGGL(sim_bwd_cols_kernel, dim3(g1d((size_t)nb * N2 * 64)), dim3(TB), 0, st, S, nb, N1,
                        N2, kidx, k, cmax, carg, dout, ldd, dS);
     HREG_CHECK_LAUNCH();
     hipLaunchKernelGGL(sim_bwd_cos_kernel, dim3(g1d((size_t)nb * (N1 + N2))), dim3(TB), 0, st, S,

@@ -765,7 +765,7 @@ def spatial_index_bytes(nb: int, n: int) -> int:
 
 
 def knn_group_indexed(q, p, k, ws, out=None):
-    """knn_group through a per-cloud Morton spatial index built into ws (n <= 16384):
+    """knn_group through a per-cloud Morton spatial index built into ws (n <= 65536):
     bit-identical to knn_group, visiting only the point blocks that can hold a neighbour."""
     nb, m, _ = q.shape
     n = p.shape[1]
@@ -793,6 +793,7 @@ def knn_idx32(p1, p2, k):
 # ------------------------------------------------------------------ stages
 
 SPATIAL_KNN_MIN = 4096  # clouds at least this large group through the spatial index
+SPATIAL_KNN_MAX = int(os.environ.get("HREG_SPATIAL_KNN_MAX", "65536"))  # <= csrc/knn.hip SI_MAXN
 
 
 def grouping(xyz, lvl: int, weights=None, out=None, ws=None):
@@ -804,7 +805,7 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None):
     idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
                        out=None if out is None else out[:2])
     kout = None if out is None else out[2:5]
-    if SPATIAL_KNN_MIN <= n <= 16384:
+    if SPATIAL_KNN_MIN <= n <= SPATIAL_KNN_MAX:
         if ws is None:
             ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
         gidx, geom, kx = knn_group_indexed(sampled, xyz, k, ws, out=kout)

@@ -301,7 +301,7 @@ def test_transform_points():
                                atol=1e-5)
 
 
-@pytest.mark.parametrize("case", ["lidar", "cube", "dups", "ragged"])
+@pytest.mark.parametrize("case", ["lidar", "cube", "dups", "ragged", "lidar64k", "ragged64k"])
 @pytest.mark.parametrize("K", [8, 32, 64])
 def test_knn_group_indexed_matches_bruteforce(case, K):
     """The Morton-indexed, box-culled kNN grouping is bit-identical to the full scan
@@ -315,6 +315,10 @@ def test_knn_group_indexed_matches_bruteforce(case, K):
     elif case == "dups":  # heavy exact duplicates and a lattice: many equal distances
         base = rng.integers(-20, 20, (2, 1500, 3)).astype(np.float32)
         p = base[:, rng.integers(0, 1500, 6000)]
+    elif case == "lidar64k":  # Model_V2's config 5 (n > 16384: the HBM-scatter index)
+        p = synthetic.lidar_batch(1, 65536, seed0=4)[0]
+    elif case == "ragged64k":
+        p = rng.uniform(-40, 40, (2, 65536 - 37, 3)).astype(np.float32)
     else:  # n not a multiple of 64
         p = rng.uniform(-40, 40, (3, 5001, 3)).astype(np.float32)
     nb, n, _ = p.shape
