@@ -57,6 +57,31 @@ def test_gather_rows_and_deterministic_scatter(tg):
     assert torch.equal(g1[0], g3[0])
 
 
+def test_csr_segments_ascending(tg):
+    """hreg_csr_build: every destination's entries in ascending order (short segments in
+    registers, long ones by the wave's rank sort, > 512 by one lane's insertion sort)."""
+    from pcd_reg_hregnet_amd import _lib
+    g = torch.Generator().manual_seed(5)
+    n = 5000
+    idx = torch.randint(0, n, (60000,), generator=g, dtype=torch.int32)
+    for row, cnt in ((11, 17), (12, 64), (13, 65), (14, 300), (15, 512), (16, 513), (17, 1500)):
+        pos = torch.randperm(idx.numel(), generator=g)[:cnt]
+        idx[pos] = row
+    idx[torch.randperm(idx.numel(), generator=g)[:100]] = -1  # out-of-range entries skipped
+    M = idx.numel()
+    ws = tg.IndexMap(idx.to(DEV), n).csr()
+    torch.cuda.synchronize()
+    w = ws.view(torch.int32).cpu()
+    off, ent = w[:n + 1], w[n + 1:n + 1 + M]
+    valid = idx >= 0
+    order = torch.argsort(idx[valid].long() * M + torch.arange(M)[valid], stable=True)
+    expect = torch.arange(M, dtype=torch.int32)[valid][order]
+    assert int(off[n]) == int(valid.sum())
+    assert torch.equal(ent[:int(off[n])], expect)
+    counts = torch.bincount(idx[valid].long(), minlength=n)
+    assert torch.equal(off[1:] - off[:-1], counts.to(torch.int32))
+
+
 def test_geom_rows(tg):
     G, k = 40, 8
     q = _rand(G, 3, seed=3, scale=5)
