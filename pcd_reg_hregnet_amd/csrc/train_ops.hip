@@ -54,6 +54,26 @@ __global__ void copy_rows_kernel(const float *__restrict__ src, int lds, int row
     }
 }
 
+// float4 form (C, lds, ldd multiples of 4, 16-byte aligned rows, R * C / 4 < 2^31): four
+// channels per thread, 32-bit index arithmetic; the same per-element operations
+template <bool ACC>
+__global__ __launch_bounds__(TB) void copy_rows4_kernel(const float4 *__restrict__ src, int lds4,
+                                                        int row_div, int R, int C4,
+                                                        float4 *__restrict__ dst, int ldd4) {
+    const uint32_t total = (uint32_t)R * (uint32_t)C4;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const uint32_t r = i / (uint32_t)C4, c = i - r * (uint32_t)C4;
+        const float4 v = src[(size_t)(r / (uint32_t)row_div) * lds4 + c];
+        float4 *o = dst + (size_t)r * ldd4 + c;
+        if (ACC) {
+            const float4 a = *o;
+            *o = make_float4(fadd_rn(a.x, v.x), fadd_rn(a.y, v.y), fadd_rn(a.z, v.z), fadd_rn(a.w, v.w));
+        } else {
+            *o = v;
+        }
+    }
+}
+
 __global__ void group_sum_kernel(const float *__restrict__ x, int ldx, int G, int k, int C,
                                  float *__restrict__ out, int ldo, int acc) {
     GRID_STRIDE(i, (size_t)G * C) {
@@ -1022,8 +1042,23 @@ extern "C" int hreg_copy_rows(const float *src, int lds, int row_div, int R, int
                               int ldd, int accumulate, void *stream) {
     if (!src || !dst || R < 0 || C < 0 || row_div < 1 || lds < C || ldd < C) return HREG_ERR_INVALID;
     if (!R || !C) return HREG_OK;
-    hipLaunchKernelGGL(copy_rows_kernel, dim3(g1d((size_t)R * C)), dim3(TB), 0, as_stream(stream),
-                       src, lds, row_div, R, C, dst, ldd, accumulate);
+    const bool v4 = !(C & 3) && !(lds & 3) && !(ldd & 3) &&
+                    !((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) &&
+                    (size_t)R * C / 4 < (1u << 31);
+    if (v4) {
+        const dim3 g(g1d((size_t)R * C / 4));
+        if (accumulate)
+            hipLaunchKernelGGL(copy_rows4_kernel<true>, g, dim3(TB), 0, as_stream(stream),
+                               reinterpret_cast<const float4 *>(src), lds / 4, row_div, R, C / 4,
+                               reinterpret_cast<float4 *>(dst), ldd / 4);
+        else
+            hipLaunchKernelGGL(copy_rows4_kernel<false>, g, dim3(TB), 0, as_stream(stream),
+                               reinterpret_cast<const float4 *>(src), lds / 4, row_div, R, C / 4,
+                               reinterpret_cast<float4 *>(dst), ldd / 4);
+    } else {
+        hipLaunchKernelGGL(copy_rows_kernel, dim3(g1d((size_t)R * C)), dim3(TB), 0, as_stream(stream),
+                           src, lds, row_div, R, C, dst, ldd, accumulate);
+    }
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

@@ -99,11 +99,12 @@ def test_geom_rows(tg):
         _close(a, b, rtol=1e-5, atol=1e-5)
 
 
-def test_cat_rows_with_repeat(tg):
+@pytest.mark.parametrize("widths", [(3, 6, 2), (4, 8, 12)])  # 2nd: the float4 copy path
+def test_cat_rows_with_repeat(tg, widths):
     G, k = 10, 4
-    a = _rand(G * k, 3, seed=5)
-    b = _rand(G, 6, seed=6)
-    c = _rand(G * k, 2, seed=7)
+    a = _rand(G * k, widths[0], seed=5)
+    b = _rand(G, widths[1], seed=6)
+    c = _rand(G * k, widths[2], seed=7)
     o1, g1 = _grads(lambda a, b, c: tg.cat_rows(a, (b, k), c), [a, b, c])
     o2, g2 = _grads(lambda a, b, c: torch.cat([a, b.repeat_interleave(k, 0), c], 1), [a, b, c])
     _close(o1[0], o2[0], rtol=0, atol=0)
