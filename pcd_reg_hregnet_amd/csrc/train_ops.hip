@@ -227,6 +227,46 @@ __global__ __launch_bounds__(TB) void csr_sort_kernel(int n, const int32_t *__re
     }
 }
 
+// float4 forms of gather_rows / scatter_rows (same conditions as copy_rows4_kernel): four
+// channels per thread, 32-bit index arithmetic, the same per-element operations and order
+__global__ __launch_bounds__(TB) void gather_rows4_kernel(const float4 *__restrict__ x, int ldx4,
+                                                          const int32_t *__restrict__ idx, int M,
+                                                          int C4, float4 *__restrict__ out, int ldo4) {
+    const uint32_t total = (uint32_t)M * (uint32_t)C4;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const uint32_t m = i / (uint32_t)C4, c = i - m * (uint32_t)C4;
+        out[(size_t)m * ldo4 + c] = x[(size_t)idx[m] * ldx4 + c];
+    }
+}
+
+__global__ __launch_bounds__(TB) void scatter_rows4_kernel(const float4 *__restrict__ dy, int ldy4,
+                                                           const int32_t *__restrict__ off,
+                                                           const int32_t *__restrict__ ent, int n,
+                                                           int C4, float4 *__restrict__ dx, int ldx4,
+                                                           int acc) {
+    const uint32_t total = (uint32_t)n * (uint32_t)C4;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const uint32_t s = i / (uint32_t)C4, c = i - s * (uint32_t)C4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int e = off[s]; e < off[s + 1]; ++e) {
+            const float4 d = dy[(size_t)ent[e] * ldy4 + c];
+            v = make_float4(fadd_rn(v.x, d.x), fadd_rn(v.y, d.y), fadd_rn(v.z, d.z), fadd_rn(v.w, d.w));
+        }
+        float4 *o = dx + (size_t)s * ldx4 + c;
+        if (acc) {
+            const float4 a = *o;
+            v = make_float4(fadd_rn(a.x, v.x), fadd_rn(a.y, v.y), fadd_rn(a.z, v.z), fadd_rn(a.w, v.w));
+        }
+        *o = v;
+    }
+}
+
+inline bool rows_v4(int C, int ld0, int ld1, const void *p0, const void *p1, size_t rows) {
+    return !(C & 3) && !(ld0 & 3) && !(ld1 & 3) &&
+           !((reinterpret_cast<uintptr_t>(p0) | reinterpret_cast<uintptr_t>(p1)) & 15) &&
+           rows * (size_t)C / 4 < (1u << 31);
+}
+
 __global__ void scatter_rows_kernel(const float *__restrict__ dy, int ldy,
                                     const int32_t *__restrict__ off,
                                     const int32_t *__restrict__ ent, int n, int C,
@@ -1106,8 +1146,13 @@ extern "C" int hreg_gather_rows(const float *x, int ldx, const int32_t *idx, int
                                 float *out, int ldo, void *stream) {
     if (!x || !idx || !out || M < 0 || C < 0 || ldx < C || ldo < C) return HREG_ERR_INVALID;
     if (!M || !C) return HREG_OK;
-    hipLaunchKernelGGL(gather_rows_kernel, dim3(g1d((size_t)M * C)), dim3(TB), 0,
-                       as_stream(stream), x, ldx, idx, M, C, out, ldo);
+    if (rows_v4(C, ldx, ldo, x, out, (size_t)M))
+        hipLaunchKernelGGL(gather_rows4_kernel, dim3(g1d((size_t)M * C / 4)), dim3(TB), 0,
+                           as_stream(stream), reinterpret_cast<const float4 *>(x), ldx / 4, idx, M,
+                           C / 4, reinterpret_cast<float4 *>(out), ldo / 4);
+    else
+        hipLaunchKernelGGL(gather_rows_kernel, dim3(g1d((size_t)M * C)), dim3(TB), 0,
+                           as_stream(stream), x, ldx, idx, M, C, out, ldo);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -1154,8 +1199,13 @@ extern "C" int hreg_scatter_rows(const float *dy, int ldy, const void *ws, int M
     if (!dy || !ws || !dx || M < 0 || n < 1 || C < 0 || ldy < C || ldx < C) return HREG_ERR_INVALID;
     if (!C) return HREG_OK;
     Csr c = csr_view(const_cast<void *>(ws), M, n);
-    hipLaunchKernelGGL(scatter_rows_kernel, dim3(g1d((size_t)n * C)), dim3(TB), 0,
-                       as_stream(stream), dy, ldy, c.off, c.ent, n, C, dx, ldx, accumulate);
+    if (rows_v4(C, ldy, ldx, dy, dx, (size_t)n))
+        hipLaunchKernelGGL(scatter_rows4_kernel, dim3(g1d((size_t)n * C / 4)), dim3(TB), 0,
+                           as_stream(stream), reinterpret_cast<const float4 *>(dy), ldy / 4, c.off,
+                           c.ent, n, C / 4, reinterpret_cast<float4 *>(dx), ldx / 4, accumulate);
+    else
+        hipLaunchKernelGGL(scatter_rows_kernel, dim3(g1d((size_t)n * C)), dim3(TB), 0,
+                           as_stream(stream), dy, ldy, c.off, c.ent, n, C, dx, ldx, accumulate);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

@@ -40,8 +40,9 @@ def tg():
     return train_graph
 
 
-def test_gather_rows_and_deterministic_scatter(tg):
-    n, C, M = 300, 5, 2000
+@pytest.mark.parametrize("C", [5, 8])  # 8: the float4 gather / scatter kernels
+def test_gather_rows_and_deterministic_scatter(tg, C):
+    n, M = 300, 2000
     x = _rand(n, C, seed=1)
     g = torch.Generator().manual_seed(2)
     idx = torch.randint(0, n, (M,), generator=g, dtype=torch.int32)
