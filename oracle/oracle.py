@@ -204,7 +204,7 @@ def keypoint_detector(sd, pre, xyz, feats, weights, nsample, k):
     """KeypointDetector.forward, layers.py:134-165 (fps=True)."""
     idx = fps(xyz, nsample, weights)
     sampled = gather_points(np.ascontiguousarray(xyz.transpose(0, 2, 1)), idx).transpose(0, 2, 1)
-    grouped, knn_xyz, _ = knn_group(np.ascontiguousarray(sampled), xyz, feats, k)
+    grouped, knn_xyz, kidx = knn_group(np.ascontiguousarray(sampled), xyz, feats, k)
     emb = _conv_stack(grouped, sd, pre + ".convs", 3)
     x1 = np.max(emb, axis=1)
     a = _softmax(x1, -1)
@@ -214,7 +214,7 @@ def keypoint_detector(sd, pre, xyz, feats, weights, nsample, k):
     s = _mlp(_mlp(att_feat, sd, pre + ".mlp1"), sd, pre + ".mlp2")
     s = _mlp(s, sd, pre + ".mlp3", act=False)
     sigmas = (_softplus(s) + np.float32(0.001))[:, 0]
-    return keypoints, sigmas, att_feat, grouped, att_map, idx
+    return keypoints, sigmas, att_feat, grouped, att_map, idx, kidx
 
 
 def desc_extractor(sd, pre, grouped, att_map):
@@ -237,16 +237,17 @@ def _norm_weights(s):
 def feature_extraction(sd, points, use_weights=True):
     """HierFeatureExtraction.forward, models.py:26-58 (use_fps=True)."""
     p = "feature_extraction."
-    xyz1, s1, f1, g1, m1, i1 = keypoint_detector(sd, p + "detector_1", points, None, None, 1024, 64)
+    xyz1, s1, f1, g1, m1, i1, k1 = keypoint_detector(sd, p + "detector_1", points, None, None, 1024, 64)
     d1 = desc_extractor(sd, p + "desc_extractor_1", g1, m1)
     w1 = _norm_weights(s1) if use_weights else None
-    xyz2, s2, f2, g2, m2, i2 = keypoint_detector(sd, p + "detector_2", xyz1, f1, w1, 512, 32)
+    xyz2, s2, f2, g2, m2, i2, k2 = keypoint_detector(sd, p + "detector_2", xyz1, f1, w1, 512, 32)
     d2 = desc_extractor(sd, p + "desc_extractor_2", g2, m2)
     w2 = _norm_weights(s2) if use_weights else None
-    xyz3, s3, f3, g3, m3, i3 = keypoint_detector(sd, p + "detector_3", xyz2, f2, w2, 256, 16)
+    xyz3, s3, f3, g3, m3, i3, k3 = keypoint_detector(sd, p + "detector_3", xyz2, f2, w2, 256, 16)
     d3 = desc_extractor(sd, p + "desc_extractor_3", g3, m3)
     return dict(xyz_1=xyz1, xyz_2=xyz2, xyz_3=xyz3, sigmas_1=s1, sigmas_2=s2, sigmas_3=s3,
-                desc_1=d1, desc_2=d2, desc_3=d3, fps_idx_1=i1, fps_idx_2=i2, fps_idx_3=i3)
+                desc_1=d1, desc_2=d2, desc_3=d3, fps_idx_1=i1, fps_idx_2=i2, fps_idx_3=i3,
+                knn_idx_1=k1, knn_idx_2=k2, knn_idx_3=k3)
 
 
 def cosine_similarity_matrix(a, b):
@@ -275,8 +276,8 @@ def _sim_feats(src_d, dst_d, knn_idx):
     return src_dst, dst_src
 
 
-def _nbr_desc(sd, pre, xyz, desc, k):
-    """neighbour-aware descriptor, layers.py:316-337."""
+def _nbr_desc(sd, pre, xyz, desc, k, rec=None, name=None):
+    """neighbour-aware descriptor, layers.py:316-337 (rec[name] = its xyz kNN)."""
     _, idx = knn(xyz, xyz, k)
     knn_xyz = knn_gather(xyz, idx)
     feats = knn_gather(desc, idx)
@@ -285,11 +286,14 @@ def _nbr_desc(sd, pre, xyz, desc, k):
     f = np.concatenate([feats, rela, dist], axis=-1)
     w = _conv_stack(np.ascontiguousarray(f.transpose(0, 3, 1, 2)), sd, pre + ".convs_2", 3)
     w = _softmax(np.max(w, axis=1), -1)
+    if rec is not None:
+        rec[name] = idx
     return np.sum(feats * w[..., None], axis=2).astype(np.float32)
 
 
-def coarse_reg(sd, pre, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w, k=8):
-    """CoarseReg.forward, layers.py:273-396 (use_sim = use_neighbor = True)."""
+def coarse_reg(sd, pre, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w, k=8, rec=None):
+    """CoarseReg.forward, layers.py:273-396 (use_sim = use_neighbor = True); rec: the
+    neighbour branch's xyz kNN selections (coarse_nbr_src / coarse_nbr_dst)."""
     sdsc = np.ascontiguousarray(src_desc.transpose(0, 2, 1))
     ddsc = np.ascontiguousarray(dst_desc.transpose(0, 2, 1))
     _, kidx = knn(sdsc, ddsc, k)
@@ -302,8 +306,8 @@ def coarse_reg(sd, pre, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w, k=8)
     w_e = np.repeat(src_w[:, :, None, None], k, axis=2)
     knn_w = knn_gather(dst_w[..., None], kidx)
     sd_cos, ds_cos = _sim_feats(sdsc, ddsc, kidx)
-    snb = _nbr_desc(sd, pre, src_xyz, sdsc, k)
-    dnb = _nbr_desc(sd, pre, dst_xyz, ddsc, k)
+    snb = _nbr_desc(sd, pre, src_xyz, sdsc, k, rec, "coarse_nbr_src")
+    dnb = _nbr_desc(sd, pre, dst_xyz, ddsc, k, rec, "coarse_nbr_dst")
     sd_ncos, ds_ncos = _sim_feats(snb, dnb, kidx)
     feats = np.concatenate([rela, dist, xyz_e, knn_xyz, desc_e, knn_desc, w_e, knn_w,
                             sd_cos[..., None], ds_cos[..., None], sd_ncos[..., None],
@@ -391,22 +395,29 @@ def hregnet_forward(sd, src, dst, use_weights=True):
     """HRegNet.forward, models/HRegNet/models.py:77-148 (eval mode)."""
     sf = feature_extraction(sd, src, use_weights)
     df = feature_extraction(sd, dst, use_weights)
-    c3, w3, _ = coarse_reg(sd, "coarse_corres", sf["xyz_3"], sf["desc_3"], df["xyz_3"],
-                           df["desc_3"], sf["sigmas_3"], df["sigmas_3"])
+    rec = {}
+    c3, w3, kd = coarse_reg(sd, "coarse_corres", sf["xyz_3"], sf["desc_3"], df["xyz_3"],
+                            df["desc_3"], sf["sigmas_3"], df["sigmas_3"], rec=rec)
     R3, t3 = weighted_svd(sf["xyz_3"], c3, w3)
     x2t = _transform(R3, t3, sf["xyz_2"])
-    c2, w2, _ = fine_reg(sd, "fine_corres_2", x2t, sf["desc_2"], df["xyz_2"], df["desc_2"],
-                         sf["sigmas_2"], df["sigmas_2"])
+    c2, w2, k2 = fine_reg(sd, "fine_corres_2", x2t, sf["desc_2"], df["xyz_2"], df["desc_2"],
+                          sf["sigmas_2"], df["sigmas_2"])
     R2_, t2_ = weighted_svd(x2t, c2, w2)
     R2, t2 = _compose(R2_, t2_, R3, t3)
     x1t = _transform(R2, t2, sf["xyz_1"])
-    c1, w1, _ = fine_reg(sd, "fine_corres_1", x1t, sf["desc_1"], df["xyz_1"], df["desc_1"],
-                         sf["sigmas_1"], df["sigmas_1"])
+    c1, w1, k1 = fine_reg(sd, "fine_corres_1", x1t, sf["desc_1"], df["xyz_1"], df["desc_1"],
+                          sf["sigmas_1"], df["sigmas_1"])
     R1_, t1_ = weighted_svd(x1t, c1, w1)
     R1, t1 = _compose(R1_, t1_, R2, t2)
+    # every kNN selection, named as make_golden.py's knn_* fixture keys
+    knn_sel = {"coarse_desc_knn": kd, "fine2_knn": k2, "fine1_knn": k1, **rec}
+    for lv in (1, 2, 3):
+        knn_sel[f"src_knn_{lv}"] = sf[f"knn_idx_{lv}"]
+        knn_sel[f"dst_knn_{lv}"] = df[f"knn_idx_{lv}"]
     return dict(src_xyz_corres_3=c3, src_xyz_corres_2=c2, src_xyz_corres_1=c1,
                 src_dst_weights_3=w3, src_dst_weights_2=w2, src_dst_weights_1=w1,
-                rotation=[R3, R2, R1], translation=[t3, t2, t1], src_feats=sf, dst_feats=df)
+                rotation=[R3, R2, R1], translation=[t3, t2, t1], src_feats=sf, dst_feats=df,
+                knn_sel=knn_sel)
 
 
 def model_v2_forward(sd, src, dst, perm_feats, perm_weights, use_weights=True):
@@ -417,21 +428,26 @@ def model_v2_forward(sd, src, dst, perm_feats, perm_weights, use_weights=True):
     models.py:118-119); the caller passes them in."""
     sf = feature_extraction(sd, src, use_weights)
     df = feature_extraction(sd, dst, use_weights)
-    c3, w3, _ = coarse_reg(sd, "coarse_corres", sf["xyz_3"], sf["desc_3"], df["xyz_3"],
-                           df["desc_3"], sf["sigmas_3"], df["sigmas_3"])
+    rec = {}
+    c3, w3, kd = coarse_reg(sd, "coarse_corres", sf["xyz_3"], sf["desc_3"], df["xyz_3"],
+                            df["desc_3"], sf["sigmas_3"], df["sigmas_3"], rec=rec)
     R3, t3 = weighted_svd(sf["xyz_3"], c3, w3)
     x2t = _transform(R3, t3, sf["xyz_2"])
-    c2, w2, _, att2 = fine_reg(sd, "fine_corres_2", x2t, sf["desc_2"], df["xyz_2"],
-                               df["desc_2"], sf["sigmas_2"], df["sigmas_2"], return_att=True)
+    c2, w2, k2, att2 = fine_reg(sd, "fine_corres_2", x2t, sf["desc_2"], df["xyz_2"],
+                                df["desc_2"], sf["sigmas_2"], df["sigmas_2"], return_att=True)
     f2 = _mlp(att2, sd, "fine_corres_2.mlpx")
     R2_, t2_ = weighted_svd(x2t, c2, w2)
     R2, t2 = _compose(R2_, t2_, R3, t3)
     x1t = _transform(R2, t2, sf["xyz_1"])
-    c1, w1, _ = fine_reg(sd, "fine_corres_1", x1t, sf["desc_1"], df["xyz_1"], df["desc_1"],
-                         sf["sigmas_1"], df["sigmas_1"])
+    c1, w1, k1 = fine_reg(sd, "fine_corres_1", x1t, sf["desc_1"], df["xyz_1"], df["desc_1"],
+                          sf["sigmas_1"], df["sigmas_1"])
     R1_, t1_ = weighted_svd(x1t, c1, w1)
     R1, t1 = _compose(R1_, t1_, R2, t2)
-    return dict(src_xyz_corres_3=c3, src_xyz_corres_2=c2, src_xyz_corres_1=c1,
+    knn_sel = {"coarse_desc_knn": kd, "fine2_knn": k2, "fine1_knn": k1, **rec}
+    for lv in (1, 2, 3):
+        knn_sel[f"src_knn_{lv}"] = sf[f"knn_idx_{lv}"]
+        knn_sel[f"dst_knn_{lv}"] = df[f"knn_idx_{lv}"]
+    return dict(knn_sel=knn_sel, src_xyz_corres_3=c3, src_xyz_corres_2=c2, src_xyz_corres_1=c1,
                 rotation=[R3, R2, R1], translation=[t3, t2, t1],
                 src_feats_desc_2=sf["desc_2"], src_feats_sigmas_2=sf["sigmas_2"],
                 src_xyz_2_trans=x2t, dst_xyz_2=df["xyz_2"],

@@ -325,9 +325,11 @@ __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__
 // temp buffer, zeroed by the launcher (tags 0 never match j >= 1).  Every
 // poll loop is bounded; on expiry the wave sets HREG_STATUS_FPS_TIMEOUT in the
 // library's device status word (read and cleared by hreg_device_status, which the
-// host checks at its sync points), fills the cloud's remaining idx entries with
-// 0 and sampled rows with point 0 (valid indices for every consumer), and moves
-// on to its next cloud (every cloud has its own slots).
+// host checks at its sync points) and leaves the kernel.  Only participant 0 writes
+// idx / sampled, and the launcher zero-fills both first, so after a timeout every idx
+// entry of the launch is a valid index (0 or a real selection) and every sampled row
+// finite; their contents are otherwise undefined and the host raises.  Every other
+// participant then times out within one poll budget too, so the grid drains.
 // tools/fps_experiment.py variants: HREG_FPS_EXP 1 = four lanes publish in one store
 // instruction, 2 = s_sleep between polls; HREG_FPS_S forces the slots per lane,
 // HREG_FPS_PAD the slot stride (16: one 128-byte line per participant)
@@ -475,16 +477,10 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                 }
             }
             if (timed_out) {
-                // the selection of this cloud is lost: flag it, leave valid indices behind
+                // the launch's selections are lost: flag it and leave (idx / sampled hold
+                // the launcher's zero fill where participant 0 has not written)
                 if (lane == 0) atomicOr(&g_hreg_status, HREG_STATUS_FPS_TIMEOUT);
-                for (int jj = j + lane; jj < m; jj += 64) {
-                    idx_out[(size_t)cloud * m + jj] = 0;
-                    if (sampled_out) {
-                        float *o = sampled_out + ((size_t)cloud * m + jj) * 3;
-                        o[0] = P[0]; o[1] = P[1]; o[2] = P[2];
-                    }
-                }
-                break;
+                return;
             }
             const float cd = lane < NP ? __uint_as_float((uint32_t)(w0 >> 32)) : -__builtin_huge_valf();
             const float gmax = wave_max_uniform(cd, inf);
@@ -595,6 +591,10 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
         const int clusters = b < 256 / NP ? b : 256 / NP;
         SyncSlot *slots = reinterpret_cast<SyncSlot *>(temp);
         if (hipMemsetAsync(slots, 0, (size_t)b * slot_bytes, st) != hipSuccess) return HREG_ERR_LAUNCH;
+        // valid outputs even if the exchange times out (participant 0 writes; see above)
+        if (hipMemsetAsync(idx, 0, (size_t)b * m * sizeof(int32_t), st) != hipSuccess ||
+            (sampled && hipMemsetAsync(sampled, 0, (size_t)b * m * 3 * sizeof(float), st) != hipSuccess))
+            return HREG_ERR_LAUNCH;
         const dim3 grid(NP, clusters);
 #define HREG_FPS_CL(SS)                                                                         \
     if (S == SS)                                                                                \
@@ -647,15 +647,28 @@ extern "C" int hreg_weighted_furthest_point_sampling(int b, int n, int m, const 
     return launch_fps<true>(b, n, m, points, weights, temp, idx, sampled_xyz, as_stream(stream));
 }
 
+namespace {
+__device__ int g_hreg_status_taken = 0;
+// read-and-clear in one atomic step, so a bit raised by a kernel still running on
+// another stream is either returned now or kept for the next call, never lost
+__global__ void status_take_kernel() { g_hreg_status_taken = atomicExch(&g_hreg_status, 0); }
+}  // namespace
+
+// Synchronous: waits for every stream of the device first (the flagging kernels may run
+// on any non-blocking stream), then reads (and with clear, atomically takes)
+// the status word.
 extern "C" int hreg_device_status(int *status, int clear) {
     if (!status) return HREG_ERR_INVALID;
+    if (hipDeviceSynchronize() != hipSuccess) return HREG_ERR_LAUNCH;
+    if (clear) {
+        hipLaunchKernelGGL(status_take_kernel, dim3(1), dim3(1), 0, 0);
+        if (hipGetLastError() != hipSuccess) return HREG_ERR_LAUNCH;
+        if (hipMemcpyFromSymbol(status, HIP_SYMBOL(g_hreg_status_taken), sizeof(int)) != hipSuccess)
+            return HREG_ERR_LAUNCH;
+        return HREG_OK;
+    }
     if (hipMemcpyFromSymbol(status, HIP_SYMBOL(g_hreg_status), sizeof(int)) != hipSuccess)
         return HREG_ERR_LAUNCH;
-    if (clear && *status) {
-        const int zero = 0;
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_hreg_status), &zero, sizeof(int)) != hipSuccess)
-            return HREG_ERR_LAUNCH;
-    }
     return HREG_OK;
 }
 

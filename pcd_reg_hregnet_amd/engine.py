@@ -796,6 +796,22 @@ SPATIAL_KNN_MIN = 4096  # clouds at least this large group through the spatial i
 SPATIAL_KNN_MAX = int(os.environ.get("HREG_SPATIAL_KNN_MAX", "65536"))  # <= csrc/knn.hip SI_MAXN
 
 
+# Tests set this to a dict to receive every kNN selection of an eager forward as cloud-
+# local int64 [clouds, queries, k] tensors: "knn_1".."knn_3" (src and dst clouds stacked),
+# "coarse_desc_knn", "coarse_nbr" (src and dst stacked), "fine_corres_2_knn",
+# "fine_corres_1_knn".  None (the default) records nothing.
+INDEX_RECORD = None
+
+
+def _record_knn(name, idx, nclouds, n_db, k, global_rows):
+    if INDEX_RECORD is None:
+        return
+    i = idx.view(nclouds, -1, k).long()
+    if global_rows:
+        i = i - (torch.arange(nclouds, device=i.device) * n_db).view(-1, 1, 1)
+    INDEX_RECORD[name] = i.clone()
+
+
 def grouping(xyz, lvl: int, weights=None, out=None, ws=None):
     """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz).
     out: optional preallocated tensors of the same tuple; ws: spatial-index workspace
@@ -811,6 +827,7 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None):
         gidx, geom, kx = knn_group_indexed(sampled, xyz, k, ws, out=kout)
     else:
         gidx, geom, kx = knn_group(sampled, xyz, k, out=kout)
+    _record_knn(f"knn_{lvl + 1}", gidx, nb, n, k, True)
     return idx, sampled, gidx, geom, kx
 
 
@@ -977,6 +994,7 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     s_sig, d_sig = sig3[:B * N1], sig3[B * N1:]
     # desc-space kNN (layers.py:278)
     kidx = knn_idx32(s_desc.view(B, N1, C), d_desc.view(B, N1, C), k)
+    _record_knn("coarse_desc_knn", kidx, B, N1, k, False)
     # original similarity (layers.py:290-313)
     norms = row_norms(desc3)
     S = _empty(B, N1, N1, device=dev)
@@ -986,6 +1004,7 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_a, 2, _stream())
     # neighbour-aware descriptors for src and dst together (layers.py:315-337)
     gself, geom_self, _ = knn_group(xyz3, xyz3, k)
+    _record_knn("coarse_nbr", gself, 2 * B, N1, k, True)
     G2 = 2 * B * N1
     R2 = G2 * k
     if FUSED_NBR and C == 256:
@@ -1053,6 +1072,7 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
     C = src_desc.shape[1]
     convs, head = P.fine[name]
     kidx = knn_idx32(src_xyz, dst_xyz, k)
+    _record_knn(name + "_knn", kidx, B, dst_xyz.shape[1], k, False)
     R = B * N * k
     if FUSED_FINE:
         small = _empty(R, 16, device=dev)
@@ -1340,6 +1360,7 @@ class GraphPipeline:
             self.g_last.append(g)
             self.outs_last.append(out)
         self._part = {}
+        self.ready = None  # buffer set holding a streamed next-round stage 1 (run_forwards)
         torch.cuda.synchronize()
 
     def _lane_view(self, ab: int, ln: int):
@@ -1416,83 +1437,96 @@ class GraphPipeline:
     def load(self, src, dst, lane: int = 0):
         self.src[lane].copy_(src)
         self.dst[lane].copy_(dst)
+        self.ready = None  # a streamed stage 1 was made from the old contents
 
     def check(self):
         """Raise if a replayed multi-workgroup FPS flagged a poll timeout (synchronous
-        when the graphs hold such launches; call it where the caller syncs anyway)."""
-        global _status_pending
-        _status_pending = False
+        when the graphs hold such launches -- Model_V2's clouds above 16384 points -- and a
+        no-op otherwise).  run() and run_forwards() call it after their replays."""
         if self.status_check:
             check_device_status(force=True)
 
     def _partial(self, r: int):
-        """Graphs for a final partial round of r < lanes forwards (captured on first use):
-        g_first_r = stage 1 of lanes < r; g_step_pr[cur] = the rest of every lane's batch
-        with stage 1 of the next batch on lanes < r only; g_last_r[cur] = the rest of lanes
-        < r."""
+        """Graphs for a partial round of r < lanes forwards (captured on first use):
+        first = stage 1 of lanes < r; steps[cur] = the rest of every lane's batch with stage
+        1 of the next batch on lanes < r only; lasts[cur] = the rest of lanes < r; streaming
+        (batched stage 1 only): psteps[cur] = the rest of lanes < r with the next round's
+        batched stage 1 of every lane."""
         if r in self._part:
             return self._part[r]
         torch.cuda.synchronize()
-        first = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(first, pool=self.pool):
+        g = {"first": torch.cuda.CUDAGraph(), "steps": [], "souts": [], "lasts": [],
+             "louts": [], "psteps": [], "pouts": []}
+        with torch.cuda.graph(g["first"], pool=self.pool):
             self._first_stage1(lanes=r)  # (batched: every lane's stage 1, the extra lanes unused)
-        steps, souts, lasts, louts = [], [], [], []
         for cur in (0, 1):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
-                out = self._fork(lambda ln: self._rest(ln, cur), **self._side_kw(1 - cur, side_lanes=r))
-            steps.append(g)
-            souts.append(out)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
-                out = self._fork(lambda ln: self._rest(ln, cur), lanes=r)
-            lasts.append(g)
-            louts.append(out)
+            variants = [("steps", "souts", self._side_kw(1 - cur, side_lanes=r)),
+                        ("lasts", "louts", {"lanes": r})]
+            if self.bs1:
+                variants.append(("psteps", "pouts", {"lanes": r, **self._side_kw(1 - cur)}))
+            for gk, ok, kw in variants:
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr, pool=self.pool):
+                    out = self._fork(lambda ln: self._rest(ln, cur), **kw)
+                g[gk].append(gr)
+                g[ok].append(out)
         torch.cuda.synchronize()
-        self._part[r] = (first, steps, souts, lasts, louts)
-        return self._part[r]
+        self._part[r] = g
+        return g
 
     def prepare(self, n: int):
         """Capture ahead what run_forwards(n) needs (the partial-round graphs)."""
         if n % self.lanes:
             self._partial(n % self.lanes)
 
-    def run_forwards(self, n: int):
+    def _finish(self, outs):
+        """Per-lane outputs of one replay (Model_V2: the host-RNG prime shuffles of this
+        round, drawn after its replay as the reference draws them per forward)."""
+        return [model_v2_finish(o) for o in outs] if self.v2 else list(outs)
+
+    def run_forwards(self, n: int, stream: bool = False):
         """n forwards in all: full rounds of every lane, then (n % lanes) forwards on the
-        first lanes (a partial round: lanes < n % lanes run one forward more).  Returns
-        the last forward's output of every lane (views into graph-owned memory)."""
+        first lanes (a partial round: lanes < n % lanes run one forward more).  Returns the
+        last forward's output of every lane (views into graph-owned memory; None for a lane
+        that ran none).
+
+        stream=True (batched stage 1 only, clouds <= 16384 points): the executor as a
+        continuous stream -- the last replay also runs the NEXT round's stage 1 (level-1
+        FPS + spatial index + kNN of every lane's batch) beside its forwards, and the next
+        call starts from it instead of running stage 1 alone first.  Every call still runs
+        exactly one batched stage 1 per round; load() discards a streamed stage 1."""
+        if n <= 0:
+            return None
         q, r = divmod(n, self.lanes)
-        if q == 0:
-            if r == 0:
-                return None
-            first, _, _, lasts, louts = self._partial(r)
-            first.replay()
-            lasts[0].replay()
-            out = louts[0]
-            out = [model_v2_finish(o) for o in out] if self.v2 else list(out)
-            return out + [None] * (self.lanes - r)
-        if r == 0:
-            return self.run(q) if self.lanes > 1 else [self.run(q)]
-        first, steps, souts, lasts, louts = self._partial(r)
-        self.g_first.replay()
-        cur = 0
-        for i in range(q - 1):
-            self.g_step[cur].replay()
-            if self.v2:
-                for o in self.outs[cur]:
-                    model_v2_finish(o)
+        streaming = stream and self.bs1
+        part = self._partial(r) if r else None
+        if self.ready is not None:
+            cur = self.ready
+        else:
+            (self.g_first if q or part is None else part["first"]).replay()
+            cur = 0
+        self.ready = None
+        full = [None] * self.lanes
+        for i in range(q):
+            if i == q - 1 and r:      # stage 1 of the partial round's lanes next
+                g, o = part["steps"][cur], part["souts"][cur]
+            elif i == q - 1 and not streaming:
+                g, o = self.g_last[cur], self.outs_last[cur]
+            else:
+                g, o = self.g_step[cur], self.outs[cur]
+            g.replay()
+            full = self._finish(o)
             cur = 1 - cur
-        steps[cur].replay()  # the last full round, stage 1 of lanes < r only
-        full = souts[cur]
-        if self.v2:
-            for o in full:
-                model_v2_finish(o)
-        cur = 1 - cur
-        lasts[cur].replay()
-        out = louts[cur]
-        if self.v2:
-            out = [model_v2_finish(o) for o in out]
-        return out + full[r:]
+        if r:
+            g, o = (part["psteps"][cur], part["pouts"][cur]) if streaming else \
+                   (part["lasts"][cur], part["louts"][cur])
+            g.replay()
+            full = self._finish(o) + full[r:]
+            cur = 1 - cur
+        if streaming:
+            self.ready = cur
+        self.check()
+        return full
 
     def run(self, steps: int):
         """Runs `steps` rounds; a round is one complete forward of every lane's static
@@ -1500,16 +1534,5 @@ class GraphPipeline:
         per-lane dicts (views into graph-owned memory, valid until the next run)."""
         if steps <= 0:
             return None
-        self.g_first.replay()
-        cur = 0
-        for i in range(steps - 1):
-            self.g_step[cur].replay()
-            if self.v2:  # host-RNG prime shuffles of this round, after its replay
-                for o in self.outs[cur]:
-                    model_v2_finish(o)
-            cur = 1 - cur
-        self.g_last[cur].replay()
-        out = self.outs_last[cur]
-        if self.v2:
-            out = [model_v2_finish(o) for o in out]
+        out = self.run_forwards(steps * self.lanes)
         return out[0] if self.lanes == 1 else out

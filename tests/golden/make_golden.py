@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --metrics-only | --perturb-only | --mi-only]   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --traj-only [--traj-c4] | --forward-only | --metrics-only | --perturb-only | --mi-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -245,9 +245,14 @@ def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict) -> di
     net.load_state_dict(sd)
     net.eval()
     pu.calls.clear()
+    KNN_CALLS.clear()
     with torch.no_grad():
         r = net(torch.from_numpy(src), torch.from_numpy(dst))
     out = {"src": src, "dst": dst}
+    # the 11 knn_points selections in call order (same sites as the training step's)
+    assert len(KNN_CALLS) == len(TRAIN_KNN_NAMES), len(KNN_CALLS)
+    for name, idx in zip(TRAIN_KNN_NAMES, KNN_CALLS):
+        out["knn_" + name] = idx.numpy().astype(np.int32)
     for i, (R, t) in enumerate(zip(r["rotation"], r["translation"])):
         out[f"R{3 - i}"] = R.numpy()
         out[f"t{3 - i}"] = t.numpy()
@@ -263,7 +268,60 @@ def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict) -> di
     names = ["src_fps_1", "src_fps_2", "src_fps_3", "dst_fps_1", "dst_fps_2", "dst_fps_3"]
     for name, (_, idx) in zip(names, pu.calls):
         out[name] = idx.numpy()
+    # the same forward in float64 on the same selections: the fp32 reference's own distance
+    # from it is the scale a second fp32 implementation is held to (tests/parity.py)
+    r64 = _replay64(HRegNet, pu, sd, src, dst)
+    for i, (R, t) in enumerate(zip(r64["rotation"], r64["translation"])):
+        out[f"R{3 - i}_64"] = R.numpy()
+        out[f"t{3 - i}_64"] = t.numpy()
+    for lv in (1, 2, 3):
+        out[f"corres_{lv}_64"] = r64[f"src_xyz_corres_{lv}"].numpy()
+        out[f"weights_{lv}_64"] = r64[f"src_dst_weights_{lv}"].numpy()
+        for part in ("src", "dst"):
+            f = r64[f"{part}_feats"]
+            for q in ("xyz", "sigmas", "desc"):
+                out[f"{part}_{q}_{lv}_64"] = f[f"{q}_{lv}"].numpy()
     return out
+
+
+def _replay64(Model, pu, sd, src, dst, seed=None):
+    """The eval forward of `Model` in float64, every FPS / kNN selection replayed from the
+    fp32 run just made (pu.calls, KNN_CALLS)."""
+    global KNN_REPLAY
+    net = Model(_Args())
+    net.load_state_dict(sd)
+    net = net.double().eval()
+    pu.replay = [c[1].clone() for c in pu.calls]
+    KNN_REPLAY = [c.clone() for c in KNN_CALLS]
+    pu.calls.clear()
+    KNN_CALLS.clear()
+    torch_eye, torch_zeros = torch.eye, torch.zeros
+    torch.eye = lambda *a, **k: torch_eye(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+    torch.zeros = lambda *a, **k: torch_zeros(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+    try:
+        if seed is not None:
+            torch.manual_seed(seed)
+        with torch.no_grad():
+            return net(torch.from_numpy(src).double(), torch.from_numpy(dst).double())
+    finally:
+        torch.eye, torch.zeros = torch_eye, torch_zeros
+        pu.replay = None
+        KNN_REPLAY = None
+
+
+def forward_fixtures(HRegNet, pu, sd):
+    from pcd_reg_hregnet_amd import synthetic
+    # config 1 (BASELINE.json configs[0]): B=1, 2 x 16384 uniform cube, seed 1
+    src, dst = synthetic.cube_batch(1, 16384, seed=1)
+    np.savez_compressed(os.path.join(HERE, "hregnet_cube_b1_n16384.npz"),
+                        **model_fixture(HRegNet, pu, src, dst, sd))
+    print("cube fixture written", flush=True)
+    # LiDAR-shaped pairs, B=2, N=4096
+    s, d, Rg, tg = synthetic.lidar_batch(2, 4096, seed0=0)
+    fx = model_fixture(HRegNet, pu, s, d, sd)
+    fx["R_gt"], fx["t_gt"] = Rg, tg
+    np.savez_compressed(os.path.join(HERE, "hregnet_lidar_b2_n4096.npz"), **fx)
+    print("lidar fixture written", flush=True)
 
 
 def model_v2_fixture(Model_V2, pu, src: np.ndarray, dst: np.ndarray, sd: dict, seed: int) -> dict:
@@ -273,10 +331,14 @@ def model_v2_fixture(Model_V2, pu, src: np.ndarray, dst: np.ndarray, sd: dict, s
     net.load_state_dict(sd)
     net.eval()
     pu.calls.clear()
+    KNN_CALLS.clear()
     torch.manual_seed(seed)
     with torch.no_grad():
         r = net(torch.from_numpy(src), torch.from_numpy(dst))
     out = {"src": src, "dst": dst, "perm_seed": np.array(seed)}
+    assert len(KNN_CALLS) == len(TRAIN_KNN_NAMES), len(KNN_CALLS)
+    for name, idx in zip(TRAIN_KNN_NAMES, KNN_CALLS):
+        out["knn_" + name] = idx.numpy().astype(np.int32)
     for i, (R, t) in enumerate(zip(r["rotation"], r["translation"])):
         out[f"R{3 - i}"] = R.numpy()
         out[f"t{3 - i}"] = t.numpy()
@@ -293,6 +355,18 @@ def model_v2_fixture(Model_V2, pu, src: np.ndarray, dst: np.ndarray, sd: dict, s
     names = ["src_fps_1", "src_fps_2", "src_fps_3", "dst_fps_1", "dst_fps_2", "dst_fps_3"]
     for name, (_, idx) in zip(names, pu.calls):
         out[name] = idx.numpy()
+    r64 = _replay64(Model_V2, pu, sd, src, dst, seed=seed)
+    for i, (R, t) in enumerate(zip(r64["rotation"], r64["translation"])):
+        out[f"R{3 - i}_64"] = R.numpy()
+        out[f"t{3 - i}_64"] = t.numpy()
+    for key in ("src_xyz_corres_3", "src_xyz_corres_2", "src_xyz_corres_1", "src_xyz_2_trans",
+                "src_dst_feats_2", "src_dst_weights_2"):
+        out[key + "_64"] = r64[key].numpy()
+    for lv in (1, 2, 3):
+        for part in ("src", "dst"):
+            f = r64[f"{part}_feats"]
+            for q in ("xyz", "sigmas", "desc"):
+                out[f"{part}_{q}_{lv}_64"] = f[f"{q}_{lv}"].numpy()
     return out
 
 
@@ -501,6 +575,68 @@ def train_fixtures(pu):
         out["g64head_" + name] = g[:256].numpy()
     np.savez_compressed(os.path.join(HERE, "train_step_b2_n2048.npz"), **out)
     print("train_step_b2_n2048.npz written, loss", float(loss), flush=True)
+
+
+def _ref_adam_trajectory(HRegNet, L, sd, s, d, Rg, tg, steps, dtype):
+    """`steps` iterations of train_reg_v0.py:279-296 on one fixed batch: zero_grad, the
+    train-mode forward, l_trans = mean over the 3 levels of transformation_loss (alpha 1),
+    backward, optim.Adam(lr=1e-3) step (train_reg_v0.py:249).  -> per-step loss, l_R, l_t
+    (the loss of step i is evaluated before step i's update)."""
+    net = HRegNet(_Args())
+    net.load_state_dict(sd)
+    net = net.to(dtype).train()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    src, dst = torch.from_numpy(s).to(dtype), torch.from_numpy(d).to(dtype)
+    gR, gt = torch.from_numpy(Rg).to(dtype), torch.from_numpy(tg).to(dtype)
+    torch_eye, torch_zeros = torch.eye, torch.zeros
+    if dtype == torch.float64:
+        torch.eye = lambda *a, **k: torch_eye(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+        torch.zeros = lambda *a, **k: torch_zeros(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+    losses = []
+    try:
+        for _ in range(steps):
+            opt.zero_grad()
+            ret = net(src, dst)
+            lt = lr_ = lt_ = 0.0
+            for i in range(3):
+                l_, lR, ltr = L.transformation_loss(ret["rotation"][i], ret["translation"][i],
+                                                    gR, gt, 1.0)[:3]
+                lt, lr_, lt_ = lt + l_, lr_ + lR, lt_ + ltr
+            loss = lt / 3.0
+            loss.backward()
+            opt.step()
+            losses.append([float(loss), float(lr_ / 3.0), float(lt_ / 3.0)])
+            print(f"  {dtype} step {len(losses)}: loss {losses[-1][0]:.6f}", flush=True)
+    finally:
+        torch.eye, torch.zeros = torch_eye, torch_zeros
+    return np.array(losses, dtype=np.float64)
+
+
+def trajectory_fixtures(pu, B=2, N=2048, steps=6, seed0=5, name=None):
+    """Multi-step reference training trajectory: the reference HRegNet
+    trained with torch.optim.Adam on one fixed synthetic batch, in fp32 and in float64
+    (both with the shims' selections computed afresh every step).  The fp32-vs-float64
+    spread is the scale at which a second fp32 implementation can follow it."""
+    sys.modules["pytorch3d.transforms"].matrix_to_euler_angles = p3d_matrix_to_euler_angles
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_losses", os.path.join(REF, "losses/losses.py"))
+    L = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(L)
+    from models.HRegNet.models import HRegNet  # noqa: E402  (reference code)
+    from pcd_reg_hregnet_amd import synthetic, weights
+    sd = weights.make_state_dict(HRegNet(_Args()).state_dict(), seed=0, pretrained_feats=True)
+    s, d, Rg, tg = synthetic.lidar_batch(B, N, seed0=seed0)
+    out = {"R_gt": Rg, "t_gt": tg, "lr": np.array(1e-3), "B": np.array(B), "N": np.array(N),
+           "seed0": np.array(seed0), "input_sum": np.array(float(s.astype(np.float64).sum() +
+                                                                 d.astype(np.float64).sum()))}
+    if B * N <= 8192:  # small: the inputs themselves; config 4: regenerated from the seed
+        out.update(src=s, dst=d)
+    torch.set_num_threads(os.cpu_count())
+    out["loss32"] = _ref_adam_trajectory(HRegNet, L, sd, s, d, Rg, tg, steps, torch.float32)
+    out["loss64"] = _ref_adam_trajectory(HRegNet, L, sd, s, d, Rg, tg, steps, torch.float64)
+    name = name or f"train_traj_b{B}_n{N}.npz"
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print(name, "written:", out["loss32"][:, 0], out["loss64"][:, 0], flush=True)
 
 
 class _CalibConfig:
@@ -746,6 +882,14 @@ def main():
     if "--train-only" in sys.argv:
         train_fixtures(pu)
         return
+    if "--traj-only" in sys.argv:
+        # B=2 x 2048 pts, 6 steps (test fixture); config 4's shard shape (8 x 16384, the
+        # bench's rank-0 batch, seed0 0) with --traj-c4, 14 steps
+        if "--traj-c4" in sys.argv:
+            trajectory_fixtures(pu, B=8, N=16384, steps=14, seed0=0)
+        else:
+            trajectory_fixtures(pu)
+        return
     if "--v2-only" in sys.argv:
         v2_fixtures(pu)
         return
@@ -754,6 +898,10 @@ def main():
         return
     from models.HRegNet.models import HRegNet  # noqa: E402  (reference code)
     from pcd_reg_hregnet_amd import synthetic, weights
+    if "--forward-only" in sys.argv:  # the two HRegNet forward fixtures only
+        sd = weights.make_state_dict(HRegNet(_Args()).state_dict(), seed=0, pretrained_feats=True)
+        forward_fixtures(HRegNet, pu, sd)
+        return
 
     feats = torch.load(os.path.join(REF, "ckpt/pretrained/nusc_feats.pth"), map_location="cpu",
                        weights_only=True)
@@ -766,17 +914,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "ops.npz"), **ops_fixtures(rng))
     print("ops.npz written", flush=True)
 
-    # config 1 (BASELINE.json configs[0]): B=1, 2 x 16384 uniform cube, seed 1
-    src, dst = synthetic.cube_batch(1, 16384, seed=1)
-    np.savez_compressed(os.path.join(HERE, "hregnet_cube_b1_n16384.npz"),
-                        **model_fixture(HRegNet, pu, src, dst, sd))
-    print("cube fixture written", flush=True)
-    # LiDAR-shaped pairs, B=2, N=4096
-    s, d, Rg, tg = synthetic.lidar_batch(2, 4096, seed0=0)
-    fx = model_fixture(HRegNet, pu, s, d, sd)
-    fx["R_gt"], fx["t_gt"] = Rg, tg
-    np.savez_compressed(os.path.join(HERE, "hregnet_lidar_b2_n4096.npz"), **fx)
-    print("lidar fixture written", flush=True)
+    forward_fixtures(HRegNet, pu, sd)
     v2_fixtures(pu)
     loss_fixtures()
     train_fixtures(pu)

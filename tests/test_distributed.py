@@ -53,6 +53,37 @@ def test_gloo_sharded_bench_path(world):
     assert all(abs(r[4] - 2 * 10 * world / (0.5 + world - 1)) < 1e-9 for r in res)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launcher_starts_n_ranks(world):
+    """`python bench.py --gpus N` with no torchrun: the script starts
+    N rank processes itself, each initialises the process group with world size N, shards
+    its own pairs, and the elapsed time is the max over ranks."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(world),
+                        "--launch-check", "--backend", "gloo"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert sorted(x["rank"] for x in lines) == list(range(world))
+    assert all(x["world"] == world for x in lines)
+    assert len({x["shard_sum"] for x in lines}) == world         # disjoint shards
+    assert all(x["elapsed_max"] == 0.5 + world - 1 for x in lines)
+    assert all(abs(x["value"] - 10 * world / (0.5 + world - 1)) < 1e-9 for x in lines)
+
+
+def test_bench_rejects_world_mismatch():
+    """A rank whose WORLD_SIZE differs from --gpus exits non-zero instead of reporting."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--launch-check", "--backend", "gloo"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
+
+
 def test_single_process_path_has_no_collective():
     import bench
     assert bench.max_over_ranks(1.25, torch.device("cpu")) == 1.25

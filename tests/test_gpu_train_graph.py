@@ -630,10 +630,11 @@ def k_of(kidx):
     return kidx.shape[-1]
 
 
-def test_sim_feats_full_size_vs_float64(tg):
+@pytest.mark.parametrize("B", [2, 8])  # 8: config 4's pairs per rank
+def test_sim_feats_full_size_vs_float64(tg, B):
     """layers.py:290-313 at the CoarseReg size (N = 256, C = 256, k = 8): our gradient's
     distance from the float64 gradient is within a few times the fp32 torch one's."""
-    B, N, C, k = 2, 256, 256, 8
+    N, C, k = 256, 256, 8
     a = torch.relu(_rand(B * N, C, seed=60))
     b = torch.relu(_rand(B * N, C, seed=61))
     kidx = torch.stack([torch.randperm(N, generator=torch.Generator().manual_seed(70 + i))[:k]
@@ -717,3 +718,74 @@ def test_trainer_step_prefetch_bitwise():
     torch.cuda.synchronize()
     for sp, p in zip(shadow, params):
         torch.testing.assert_close(p.detach(), sp.detach(), rtol=2.4e-7, atol=1e-7)  # 1-2 ulp
+
+
+def _traj_run(fx, steps):
+    """Our trainer (flat Adam, lr from the fixture) on the fixture's fixed batch from the
+    fixture weights: the loss of every step (evaluated before its update)."""
+    from pcd_reg_hregnet_amd import synthetic, trainer
+    if "src" in fx:
+        s, d = fx["src"], fx["dst"]
+    else:  # config 4's shard: regenerated from the seed, checked against the stored sum
+        s, d, _, _ = synthetic.lidar_batch(int(fx["B"]), int(fx["N"]), seed0=int(fx["seed0"]))
+    tot = float(s.astype(np.float64).sum() + d.astype(np.float64).sum())
+    assert abs(tot - float(fx["input_sum"])) <= 1e-9 * max(abs(tot), 1.0)
+    tr = trainer.Trainer(_train_net(), lr=float(fx["lr"]), alpha=1.0)
+    src, dst = torch.from_numpy(s).to(DEV), torch.from_numpy(d).to(DEV)
+    gR, gt = torch.from_numpy(fx["R_gt"]).to(DEV), torch.from_numpy(fx["t_gt"]).to(DEV)
+    losses = [float(tr.step(src, dst, gR, gt)[0]) for _ in range(steps)]
+    assert torch.isfinite(tr.params.flat).all()
+    return np.array(losses), tr
+
+
+def _traj_table(ours, r32, r64):
+    print("\nstep  ours      ref fp32  ref fp64")
+    for i, row in enumerate(zip(ours, r32, r64)):
+        print("%4d  %.6f  %.6f  %.6f" % ((i + 1,) + row))
+
+
+def test_train_trajectory_tracks_reference_b2():
+    """a multi-step trajectory of the reference itself
+    (tests/golden/train_traj_b2_n2048.npz: the reference HRegNet + torch.optim.Adam lr 1e-3
+    on one fixed batch, fp32 and float64, selections recomputed every step).  Adam's first
+    update is sign-like (m / sqrt(v) = sign g), and every update moves WFPS / kNN
+    selections, so two correct implementations part ways after step 1: the reference's own
+    fp32 and float64 runs differ by 3.5 % at step 2 and 27 % at step 4.  Held here: step 1
+    at 1e-5; step 2 within 3x the reference's fp32-vs-float64 spread; every step inside a
+    factor-2 envelope of the two reference runs; and the same descent (the loss falls
+    > 5x over 6 steps, as both reference runs do)."""
+    fx = load_npz_golden("train_traj_b2_n2048.npz")
+    r32, r64 = fx["loss32"][:, 0], fx["loss64"][:, 0]
+    ours, _ = _traj_run(fx, len(r32))
+    _traj_table(ours, r32, r64)
+    assert abs(ours[0] - r32[0]) <= 1e-5 * r32[0]
+    assert abs(ours[1] - r64[1]) <= max(3 * abs(r32[1] - r64[1]), 1e-3 * r64[1])
+    lo, hi = np.minimum(r32, r64), np.maximum(r32, r64)
+    assert ((ours >= 0.5 * lo) & (ours <= 2.0 * hi)).all()
+    assert ours[-1] < ours[0] / 5 and r32[-1] < r32[0] / 5 and r64[-1] < r64[0] / 5
+
+
+def test_train_step_config4_shape():
+    """configs[3]'s per-rank shape (8 pairs x 2 x 16384 points, the bench's rank-0 shard),
+    against the reference's own 14-step trajectory on it (train_traj_b8_n16384.npz):
+    step-1 loss at 1e-4 (the forward's R/t bar), finite parameters throughout, bitwise
+    deterministic steps, and the reference's early descent (> 4x within 5 steps, the
+    first 5 steps inside a factor-2 envelope of its fp32 / float64 runs).  Later steps
+    are only printed: the reference's own fp32 and float64 runs both turn upward after
+    step 8 (to 3.7 and 5.2 at step 10 -- the rise the r2 bench's loss_first_last showed)
+    and part from each other there."""
+    fx = load_npz_golden("train_traj_b8_n16384.npz")
+    r32, r64 = fx["loss32"][:, 0], fx["loss64"][:, 0]
+    ours, _ = _traj_run(fx, len(r32))
+    _traj_table(ours, r32, r64)
+    assert abs(ours[0] - r32[0]) <= 1e-4 * r32[0]
+    assert ours[:5].min() < ours[0] / 4
+    lo, hi = np.minimum(r32, r64)[:5], np.maximum(r32, r64)[:5]
+    assert ((ours[:5] >= 0.5 * lo) & (ours[:5] <= 2.0 * hi)).all()
+    again, _ = _traj_run(fx, 2)
+    assert np.array_equal(again, ours[:2])
+
+
+def load_npz_golden(name):
+    from helpers import load_npz
+    return load_npz(name)
