@@ -30,12 +30,23 @@ CFLAGS = [
 # without packed fp32 VALU ops (v_pk_mul_f32 / v_pk_add_f32): with them, group_l1_6 gave
 # nondeterministic wrong accumulator values whenever two waves shared a SIMD (two
 # workgroups per CU, or one 8-wave workgroup), and exact results with one wave per SIMD
-# or without the packed ops (tools/debug_l1_6.py).  The host-side
-# compile ignores the feature (a warning).
+# or without the packed ops (tools/debug_l1_6.py; the instruction
+# pairings suspected so far are ruled out by tools/micro/pk_hazard.hip).  The flag is
+# derived, not listed: every source that uses the bf16x6 headers or names the bf16 MFMA
+# gets it, and tests/test_isa.py fails if any built kernel still mixes the two.  The
+# host-side compile ignores the feature (a warning).
 NO_PACKED_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
-FILE_FLAGS = {f: NO_PACKED_F32 for f in ("group_l1_6.hip", "group_fused6.hip", "group_head.hip",
-                                       "group_split6.hip", "gemm.hip", "mlp_head.hip",
-                                       "coarse6.hip")}
+B6_MARKERS = ("mfma_chain.h", "split_chain.h", "mfma_jt.h", "mfma_f32_32x32x16_bf16")
+
+
+def uses_bf16_mfma(path: str) -> bool:
+    with open(path) as f:
+        text = f.read()
+    return any(m in text for m in B6_MARKERS)
+
+
+def file_flags(path: str) -> list[str]:
+    return NO_PACKED_F32 if uses_bf16_mfma(path) else []
 
 
 def _needs(obj: str, deps: list[str]) -> bool:
@@ -46,7 +57,7 @@ def _needs(obj: str, deps: list[str]) -> bool:
 
 
 def _compile(src: str, obj: str) -> tuple[str, int, str]:
-    cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *file_flags(src), "-c", src, "-o", obj]
     p = subprocess.run(cmd, capture_output=True, text=True)
     return src, p.returncode, p.stdout + p.stderr
 

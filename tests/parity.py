@@ -17,8 +17,9 @@ So the contract is:
   the rows NOT downstream of a selection mismatch, normalised (max |a - b| / max |b| over
   the tensor): against the reference's float64 replay on its own selections (fixtures
   made by make_golden.py carry one) within max(FEAT_TOL = 1e-5, SPREAD x the fp32
-  reference's own distance from it) -- the reference itself is up to 4.8e-5 from float64
-  at level 3 -- and against a plain fp32 result (the CPU oracle) within PAIR_TOL;
+  reference's own distance from float64, pooled per quantity over the committed fixtures
+  -- up to 4.8e-5 at level 3), and against a plain fp32 result (the CPU oracle) within
+  twice that;
 * R / t within RT_TOL absolute everywhere (north_star: 1e-4).
 
 Inputs are dicts in the fixture layout of tests/golden/make_golden.py (as_layout converts
@@ -35,11 +36,8 @@ KNN_TIE = 1e-5
 FEAT_TOL = 1e-5   # A6-A13 outputs at <= 1e-5 relative
 SPREAD = 4.0      # ... or SPREAD x the fp32 reference's own distance from float64 (as the
 #                   training-gradient bars, test_gpu_train_graph.py)
-# Against a second fp32 result with no float64 twin (the CPU oracle at B = 8 / 32): 3 x the
-# largest fp32-reference-vs-float64 spread of the committed fixtures at that level (level
-# 3 -- nine conv layers and two maxima deep -- 4.8e-5 on sigma, 1.4e-5 on keypoints), at
-# least FEAT_TOL.  "heads": correspondences / weights (largest spread 2.2e-6).
-PAIR_TOL = {1: 1e-5, 2: 3e-5, 3: 1.5e-4, "heads": 1e-5}
+SPREAD_FIXTURES = ("hregnet_lidar_b2_n4096.npz", "hregnet_cube_b1_n16384.npz",
+                   "model_v2_lidar_b2_n4096.npz", "model_v2_lidar_b1_n65536.npz")
 RT_TOL = 1e-4
 KP_TOL = 1e-3     # "the same point" when matching selections across implementations
 
@@ -92,6 +90,44 @@ def as_layout(r, B):
             if ours in rec:
                 g["knn_" + name] = rec[ours]
     return g
+
+
+_SPREADS = None
+
+
+def spread_table():
+    """quantity ("xyz_3", "sigmas_2", "desc_1", "corres_3", "weights_2", ...) -> the largest
+    normalised distance of the fp32 reference from its own float64 replay over the
+    committed fixtures and both clouds.  Pooled over fixtures because a single tensor's
+    distance is partly luck: on hregnet_lidar_b2_n4096 the reference's dst desc_3 sits
+    6.7e-6 from float64 while the CPU oracle (numpy fp32) is 1.8e-5 and the layer-wise fp32
+    GEMM path 1.5e-5 from it at the same, ill-conditioned element (tools/parity_probe.py)."""
+    global _SPREADS
+    if _SPREADS is None:
+        from helpers import load_npz
+        t = {}
+        for name in SPREAD_FIXTURES:
+            g = load_npz(name)
+            for k in g:
+                if not k.endswith("_64"):
+                    continue
+                base = k[:-3]
+                q = base.replace("src_xyz_corres_", "corres_").replace("src_dst_weights_", "weights_")
+                q = q[4:] if q.startswith(("src_", "dst_")) else q
+                if q.startswith(("R", "t")) or base not in g or not q[-1].isdigit():
+                    continue
+                a, b = g[base], g[k]
+                if q.startswith("desc_"):
+                    a, b = a.transpose(0, 2, 1), b.transpose(0, 2, 1)
+                t[q] = max(t.get(q, 0.0), nerr(a, b))
+        _SPREADS = t
+    return _SPREADS
+
+
+def feat_bar(q):
+    """bar for a quantity against float64: max(FEAT_TOL, SPREAD x the pooled reference
+    spread); against a second fp32 result (no float64 twin), twice that"""
+    return max(FEAT_TOL, SPREAD * spread_table().get(q, 0.0))
 
 
 def _take(x, idx):
@@ -174,22 +210,22 @@ def evaluate(ours, ref):
     ours = {"src": ref["src"], "dst": ref["dst"], **ours}  # the same input clouds
     aff = {}  # (part, level) -> [B,M] bool: downstream of a selection mismatch
 
-    def cont(key, label, ok, lv, channel_major=False):
+    def cont(key, label, ok, channel_major=False):
         """a continuous output on the rows `ok`: against the float64 replay when the
-        reference has one (bar max(FEAT_TOL, SPREAD x the fp32 reference's own error)),
-        else against the fp32 reference (bar PAIR_TOL)"""
+        reference has one (bar feat_bar), else against the fp32 result (bar 2 x feat_bar:
+        each of two fp32 results within feat_bar of the exact values)"""
         x, y = ours[key], ref[key]
         y64 = ref.get(key + "_64")
         if channel_major:
             x, y = x.transpose(0, 2, 1), y.transpose(0, 2, 1)
             y64 = None if y64 is None else y64.transpose(0, 2, 1)
+        q = key[4:] if key.startswith(("src_", "dst_")) else key
         st[label + "_vs_ref32"] = nerr(x[ok], y[ok])
         if y64 is not None:
-            e, spread = nerr(x[ok], y64[ok]), nerr(y[ok], y64[ok])
-            bar = max(FEAT_TOL, SPREAD * spread)
-            st[label + "_vs_f64"], st[label + "_ref32_vs_f64"] = e, spread
+            e, bar = nerr(x[ok], y64[ok]), feat_bar(q)
+            st[label + "_vs_f64"], st[label + "_ref32_vs_f64"] = e, nerr(y[ok], y64[ok])
         else:
-            e, bar = st[label + "_vs_ref32"], PAIR_TOL[lv]
+            e, bar = st[label + "_vs_ref32"], 2 * feat_bar(q)
         st[label + "_bar"] = bar
         if e > bar:
             bad.append(f"{label}: {e:.2e} > bar {bar:.2e} on rows with identical selections")
@@ -250,7 +286,7 @@ def evaluate(ours, ref):
             ok = ~a
             st[f"{pre}_rows_compared"] = f"{int(ok.sum())}/{B * M}"
             for q in ("xyz", "sigmas", "desc"):
-                cont(f"{part}_{q}_{lv}", f"{pre}_{q}", ok, lv, q == "desc")
+                cont(f"{part}_{q}_{lv}", f"{pre}_{q}", ok, q == "desc")
     # CoarseReg (level 3): desc kNN src -> dst, neighbour branch xyz self-kNN on both clouds
     nbr = {}
     for part in PARTS:
@@ -265,7 +301,7 @@ def evaluate(ours, ref):
         ok = ~a
         for q in ("corres", "weights"):
             if f"{q}_{lv}" in ref:
-                cont(f"{q}_{lv}", f"{q}_{lv}", ok, "heads")
+                cont(f"{q}_{lv}", f"{q}_{lv}", ok)
         st[f"heads_L{lv}_rows_compared"] = f"{int(ok.sum())}/{ok.size}"
         st[f"_affected_heads_{lv}"] = a
         for q in ("R", "t"):

@@ -101,13 +101,14 @@ def compare_v2(r, g, title=""):
     ref["weights_2"] = g["src_dst_weights_2"]
     st, bad = parity.evaluate(ours, ref)
     ok = ~st.pop("_affected_heads_2")
-    for key in ("src_xyz_2_trans", "src_dst_feats_2", "src_dst_weights_2"):
-        a, b = np.asarray(r[key]), g[key]
+    for key, q in (("src_xyz_2_trans", "xyz_2"), ("src_dst_feats_2", "dst_feats_2"),
+                   ("src_dst_weights_2", "weights_2")):
+        a, b = np.asarray(r[key]), g[key + "_64"]
         if key == "src_dst_feats_2":
             a, b = a.transpose(0, 2, 1), b.transpose(0, 2, 1)
-        st[key] = parity.nerr(a[ok], b[ok])
-        if st[key] > parity.FEAT_TOL:
-            bad.append(f"{key}: {st[key]:.2e}")
+        st[key + "_vs_f64"] = e = parity.nerr(a[ok], b[ok])
+        if e > parity.feat_bar(q):
+            bad.append(f"{key}: {e:.2e} > bar {parity.feat_bar(q):.2e}")
     parity.report(st, title)
     assert not bad, "\n".join(bad)
     a = np.asarray(r["dst_xyz_2"])
