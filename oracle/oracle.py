@@ -200,9 +200,10 @@ def knn_group(xyz1, xyz2, feats2, k):
     return np.ascontiguousarray(g.transpose(0, 3, 1, 2)), knn_xyz, idx
 
 
-def keypoint_detector(sd, pre, xyz, feats, weights, nsample, k):
-    """KeypointDetector.forward, layers.py:134-165 (fps=True)."""
-    idx = fps(xyz, nsample, weights)
+def keypoint_detector(sd, pre, xyz, feats, weights, nsample, k, sample=None):
+    """KeypointDetector.forward, layers.py:134-165 (fps=True; sample: the random-sampling
+    indices [B, nsample] of fps=False, layers.py:144-147)."""
+    idx = fps(xyz, nsample, weights) if sample is None else np.asarray(sample, np.int32)
     sampled = gather_points(np.ascontiguousarray(xyz.transpose(0, 2, 1)), idx).transpose(0, 2, 1)
     grouped, knn_xyz, kidx = knn_group(np.ascontiguousarray(sampled), xyz, feats, k)
     emb = _conv_stack(grouped, sd, pre + ".convs", 3)
@@ -234,16 +235,19 @@ def _norm_weights(s):
     return (w / np.mean(w, axis=1, keepdims=True)).astype(np.float32)
 
 
-def feature_extraction(sd, points, use_weights=True):
-    """HierFeatureExtraction.forward, models.py:26-58 (use_fps=True)."""
+def feature_extraction(sd, points, use_weights=True, samples=None):
+    """HierFeatureExtraction.forward, models.py:26-58 (use_fps=True; samples: the three
+    levels' random-sampling indices of use_fps=False)."""
     p = "feature_extraction."
-    xyz1, s1, f1, g1, m1, i1, k1 = keypoint_detector(sd, p + "detector_1", points, None, None, 1024, 64)
+    smp = samples if samples is not None else (None, None, None)
+    xyz1, s1, f1, g1, m1, i1, k1 = keypoint_detector(sd, p + "detector_1", points, None, None, 1024, 64,
+                                                     smp[0])
     d1 = desc_extractor(sd, p + "desc_extractor_1", g1, m1)
     w1 = _norm_weights(s1) if use_weights else None
-    xyz2, s2, f2, g2, m2, i2, k2 = keypoint_detector(sd, p + "detector_2", xyz1, f1, w1, 512, 32)
+    xyz2, s2, f2, g2, m2, i2, k2 = keypoint_detector(sd, p + "detector_2", xyz1, f1, w1, 512, 32, smp[1])
     d2 = desc_extractor(sd, p + "desc_extractor_2", g2, m2)
     w2 = _norm_weights(s2) if use_weights else None
-    xyz3, s3, f3, g3, m3, i3, k3 = keypoint_detector(sd, p + "detector_3", xyz2, f2, w2, 256, 16)
+    xyz3, s3, f3, g3, m3, i3, k3 = keypoint_detector(sd, p + "detector_3", xyz2, f2, w2, 256, 16, smp[2])
     d3 = desc_extractor(sd, p + "desc_extractor_3", g3, m3)
     return dict(xyz_1=xyz1, xyz_2=xyz2, xyz_3=xyz3, sigmas_1=s1, sigmas_2=s2, sigmas_3=s3,
                 desc_1=d1, desc_2=d2, desc_3=d3, fps_idx_1=i1, fps_idx_2=i2, fps_idx_3=i3,
@@ -391,10 +395,11 @@ def _transform(R, t, xyz):
     return (np.einsum("bij,bnj->bni", R, xyz) + t[:, None, :]).astype(np.float32)
 
 
-def hregnet_forward(sd, src, dst, use_weights=True):
-    """HRegNet.forward, models/HRegNet/models.py:77-148 (eval mode)."""
-    sf = feature_extraction(sd, src, use_weights)
-    df = feature_extraction(sd, dst, use_weights)
+def hregnet_forward(sd, src, dst, use_weights=True, samples=None):
+    """HRegNet.forward, models/HRegNet/models.py:77-148 (eval mode); samples: (src levels
+    1-3, dst levels 1-3) random-sampling indices for use_fps=False."""
+    sf = feature_extraction(sd, src, use_weights, None if samples is None else samples[:3])
+    df = feature_extraction(sd, dst, use_weights, None if samples is None else samples[3:])
     rec = {}
     c3, w3, kd = coarse_reg(sd, "coarse_corres", sf["xyz_3"], sf["desc_3"], df["xyz_3"],
                             df["desc_3"], sf["sigmas_3"], df["sigmas_3"], rec=rec)

@@ -812,14 +812,50 @@ def _record_knn(name, idx, nclouds, n_db, k, global_rows):
     INDEX_RECORD[name] = i.clone()
 
 
-def grouping(xyz, lvl: int, weights=None, out=None, ws=None):
+def random_samples(parts: int, clouds_per_part: int, lvl_sizes, device):
+    """use_fps=False (layers.py:144-147): every level draws torch.randperm(N)[:nsample] on
+    the host generator, ONE draw for the whole batch of a cloud set, in the reference's
+    call order (src levels 1-3, then dst levels 1-3: models.py:79-80, 26-58).  -> per level
+    the local indices [parts * clouds_per_part, M] int32 on the device (each part's rows
+    share its draw)."""
+    draws = [[torch.randperm(n)[:LEVELS[lvl][0]] for lvl, n in enumerate(lvl_sizes)]
+             for _ in range(parts)]  # part-major: the reference's call order
+    out = []
+    for lvl in range(len(lvl_sizes)):
+        rows = [d[lvl].to(torch.int32).expand(clouds_per_part, -1) for d in draws]
+        out.append(torch.cat(rows, 0).contiguous().to(device, non_blocking=False))
+    return out
+
+
+def random_sample_level(lvl: int, n: int, clouds: int, device):
+    """one level's draw (layers.py:146) for `clouds` clouds -> [clouds, M] int32"""
+    return torch.randperm(n)[:LEVELS[lvl][0]].to(torch.int32).expand(clouds, -1).contiguous().to(device)
+
+
+def gather_xyz(xyz, idx):
+    """xyz [nb,n,3], local idx [nb,m] int32 -> xyz[c, idx[c]] [nb,m,3] (hreg_index_offset +
+    hreg_gather_rows)"""
+    nb, n, _ = xyz.shape
+    m = idx.shape[1]
+    g = _empty(nb * m, dtype=torch.int32, device=xyz.device)
+    call("hreg_index_offset", idx, nb, m, n, g, _stream())
+    out = _empty(nb, m, 3, device=xyz.device)
+    call("hreg_gather_rows", xyz, 3, g, nb * m, 3, out, 3, _stream())
+    return out
+
+
+def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None):
     """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz).
     out: optional preallocated tensors of the same tuple; ws: spatial-index workspace
-    (uint8, spatial_index_bytes) for large clouds."""
+    (uint8, spatial_index_bytes) for large clouds; sample: the level's random-sampling
+    indices instead of FPS (use_fps=False, random_samples)."""
     M, k = LEVELS[lvl][:2]
     nb, n, _ = xyz.shape
-    idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
-                       out=None if out is None else out[:2])
+    if sample is not None:
+        idx, sampled = sample, gather_xyz(xyz, sample)
+    else:
+        idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
+                           out=None if out is None else out[:2])
     kout = None if out is None else out[2:5]
     if SPATIAL_KNN_MIN <= n <= SPATIAL_KNN_MAX:
         if ws is None:
@@ -850,7 +886,7 @@ def stage1_into(bufs, src, dst):
     grouping(pts, 0, out=g, ws=g[5])
 
 
-def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=None):
+def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=None, sample=None):
     """KeypointDetector (layers.py:134-165) + DescExtractor (layers.py:200-209) for one level.
 
     xyz [nb,n,3]; feats [nb*n, Cf] point-major or None; weights [nb*n] or None;
@@ -863,7 +899,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
     G = nb * M
     R = G * k
     if grouped is None:
-        grouped = grouping(xyz, lvl, weights)
+        grouped = grouping(xyz, lvl, weights, sample=sample)
     idx, sampled, gidx, geom, kx = grouped[:5]
     if lvl == 0 and FUSED_L1:
         dev = xyz.device
@@ -929,14 +965,16 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
     return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
 
 
-def feature_extraction(P: PreparedWeights, points, use_weights=True, l1=None):
+def feature_extraction(P: PreparedWeights, points, use_weights=True, l1=None, samples=None):
     """HierFeatureExtraction.forward (models.py:26-58) over nb clouds at once.
-    l1: level-1 grouping computed ahead (see Pipeline)."""
+    l1: level-1 grouping computed ahead (see Pipeline); samples: per-level random-sampling
+    indices (use_fps=False, random_samples), else FPS / WFPS."""
     out = {}
     xyz, feats, w = points, None, None
     for lvl in range(3):
         kp, sig, att, desc, wnext, idx = keypoint_level(P, lvl, xyz, feats, w,
-                                                        l1 if lvl == 0 else None)
+                                                        l1 if lvl == 0 else None,
+                                                        None if samples is None else samples[lvl])
         out[f"xyz_{lvl + 1}"] = kp
         out[f"sigmas_{lvl + 1}"] = sig
         out[f"desc_{lvl + 1}"] = desc
@@ -1137,7 +1175,13 @@ def transform(xyz, R, t):
     return out
 
 
-def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=None, v2=False):
+def level_input_sizes(N: int):
+    """points entering each level's sampling: the cloud, then the previous level's keypoints"""
+    return (N, LEVELS[0][0], LEVELS[1][0])
+
+
+def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=None, v2=False,
+                    use_fps=True):
     """HRegNet.forward (models/HRegNet/models.py:77-148), eval mode.
 
     v2: the Model_V2 variant (models/model_v2/models.py:77-183): fine_corres_2 is
@@ -1147,7 +1191,12 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts
     B, N, _ = src.shape
     if pts is None:
         pts = torch.cat([src, dst], 0).contiguous()
-    fe = feature_extraction(P, pts, use_weights, l1)
+    samples = None
+    if not use_fps:
+        if l1 is not None:
+            raise ValueError("use_fps=False draws its level-1 sample in the forward (no l1)")
+        samples = random_samples(2, B, level_input_sizes(N), src.device)
+    fe = feature_extraction(P, pts, use_weights, l1, samples)
 
     def split(t, rows):
         return t[:B * rows], t[B * rows:]
@@ -1222,9 +1271,9 @@ def model_v2_finish(out):
     }
 
 
-def model_v2_forward(P: PreparedWeights, src, dst, use_weights=True):
+def model_v2_forward(P: PreparedWeights, src, dst, use_weights=True, use_fps=True):
     """Model_V2.forward (models/model_v2/models.py:77-183), eval mode."""
-    return model_v2_finish(hregnet_forward(P, src, dst, use_weights, v2=True))
+    return model_v2_finish(hregnet_forward(P, src, dst, use_weights, v2=True, use_fps=use_fps))
 
 
 class Pipeline:

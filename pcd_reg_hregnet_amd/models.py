@@ -156,10 +156,11 @@ class HierFeatureExtraction(nn.Module):
     def forward(self, points):
         if self.training:
             raise NotImplementedError("train-mode forward is not implemented on the HIP path yet")
-        if not self.use_fps:
-            raise NotImplementedError("use_fps=False (random sampling) is not implemented")
         P = self._prep.get(_Prefixed(self), points.device)
-        out = engine.feature_extraction(P, points.float().contiguous(), self.use_weights)
+        samples = None if self.use_fps else engine.random_samples(
+            1, points.shape[0], engine.level_input_sizes(points.shape[1]), points.device)
+        out = engine.feature_extraction(P, points.float().contiguous(), self.use_weights,
+                                        samples=samples)
         B = points.shape[0]
         res = {}
         for i, m in enumerate((1024, 512, 256)):
@@ -222,13 +223,12 @@ class HRegNet(nn.Module):
             # batch-statistics BN + backward kernels (train_graph.py, csrc/train_ops.hip)
             from . import train_graph
             return train_graph.hregnet_train_forward(self, src_points, dst_points)
-        if not self.feature_extraction.use_fps:
-            raise NotImplementedError("use_fps=False (random sampling) is not implemented")
         dev = src_points.device
         P = self.prepared(dev)
         out = engine.hregnet_forward(P, src_points.float().contiguous(),
                                      dst_points.float().contiguous(),
-                                     self.feature_extraction.use_weights)
+                                     self.feature_extraction.use_weights,
+                                     use_fps=self.feature_extraction.use_fps)
         engine.check_device_status()  # syncs only when a multi-workgroup FPS ran (N > 16384)
         out.pop("_fps_idx", None)
         for part in ("src_feats", "dst_feats"):
@@ -260,12 +260,11 @@ class Model_V2(nn.Module):
             raise NotImplementedError(
                 "train-mode forward (batch-statistics BN + backward kernels) is not implemented "
                 "on the HIP path yet; call .eval()")
-        if not self.feature_extraction.use_fps:
-            raise NotImplementedError("use_fps=False (random sampling) is not implemented")
         P = self.prepared(src_points.device)
         out = engine.model_v2_forward(P, src_points.float().contiguous(),
                                       dst_points.float().contiguous(),
-                                      self.feature_extraction.use_weights)
+                                      self.feature_extraction.use_weights,
+                                      use_fps=self.feature_extraction.use_fps)
         engine.check_device_status()  # syncs only when a multi-workgroup FPS ran (N > 16384)
         out.pop("_fps_idx", None)
         for key in ("src_feats_desc_2", "src_dst_feats_2", "src_dst_feats_2_prime"):

@@ -540,7 +540,7 @@ def _mlp_head(x, head_mods, mode, nclouds, rows, want_weights=False):
     return head_out(s, m3[0], mode, nclouds, rows, want_weights)
 
 
-def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src"):
+def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src", use_fps=True):
     """KeypointDetector.forward + DescExtractor.forward (layers.py:134-209), train mode.
 
     xyz [nb,n,3] (requires grad above level 1), feats [nb*n][Cf] or None, weights [nb*n]
@@ -557,6 +557,8 @@ def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src"):
         grouped = []
 
         def fps_local():
+            if not use_fps:  # layers.py:144-147: one host randperm draw for the batch
+                return engine.random_sample_level(lvl, n, nb, dev)
             grouped.append(engine.grouping(xd, lvl, wd))  # FPS/WFPS + kNN grouping
             return grouped[0][0]
 
@@ -604,7 +606,7 @@ def feature_extraction(fe, points, hook=None, part="src"):
     xyz, feats, w = points, None, None
     for lvl in range(3):
         kp, sig, att, d, wnext, fps_loc = keypoint_level(dets[lvl], descs[lvl], lvl, xyz, feats,
-                                                         w, hook, part)
+                                                         w, hook, part, fe.use_fps)
         M = engine.LEVELS[lvl][0]
         nb = points.shape[0]
         out[f"xyz_{lvl + 1}"] = kp
@@ -694,8 +696,6 @@ def hregnet_train_forward(net, src, dst, hook=None):
     """HRegNet.forward (models/HRegNet/models.py:77-148) in train mode -> the reference's
     result dict; differentiable in every parameter that requires grad."""
     fe = net.feature_extraction
-    if not fe.use_fps:
-        raise NotImplementedError("use_fps=False (random sampling) is not implemented")
     src = src.float().contiguous()
     dst = dst.float().contiguous()
     B = src.shape[0]

@@ -163,7 +163,9 @@ class Trainer:
     def step(self, src, dst, gt_R, gt_t, next_batch=None):
         """-> (loss, l_R, l_t) of this rank's shard (detached, on the device)."""
         prepared = self.prefetch.take(src, dst)
-        if next_batch is not None:
+        # FPS only: with use_fps=False the level-1 sample is a host RNG draw made in the
+        # forward, in the reference's order
+        if next_batch is not None and self.net.feature_extraction.use_fps:
             self.prefetch.start(*next_batch)
         self.bucket.attach()                     # optimizer.zero_grad()
         hook = train_graph.IndexHook(prepared=prepared) if prepared else None

@@ -240,15 +240,43 @@ class _Args:
     freeze_feats = False
 
 
-def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict) -> dict:
-    net = HRegNet(_Args())
+class _ArgsRandSample(_Args):
+    use_fps = False  # layers.py:144-147 (train_reg_v0.py:52's default: --use_fps is store_true)
+
+
+def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict, args=_Args,
+                  seed=None) -> dict:
+    """The reference's eval forward; with args.use_fps False the random samples are the
+    torch.randperm draws after torch.manual_seed(seed), saved as the *_fps_* selections."""
+    net = HRegNet(args())
     net.load_state_dict(sd)
     net.eval()
     pu.calls.clear()
     KNN_CALLS.clear()
-    with torch.no_grad():
-        r = net(torch.from_numpy(src), torch.from_numpy(dst))
+    draws = []
+    randperm = torch.randperm
+
+    def logged(*a, **k):
+        r = randperm(*a, **k)
+        draws.append(r.clone())
+        return r
+    if seed is not None:
+        torch.manual_seed(seed)
+    torch.randperm = logged
+    try:
+        with torch.no_grad():
+            r = net(torch.from_numpy(src), torch.from_numpy(dst))
+    finally:
+        torch.randperm = randperm
     out = {"src": src, "dst": dst}
+    if seed is not None:
+        out["perm_seed"] = np.array(seed)
+    if not args.use_fps:  # the samples as per-cloud selections (the whole batch shares a draw)
+        assert len(draws) == 6, len(draws)
+        B = src.shape[0]
+        names = ["src_fps_1", "src_fps_2", "src_fps_3", "dst_fps_1", "dst_fps_2", "dst_fps_3"]
+        for name, d, m in zip(names, draws, (1024, 512, 256) * 2):
+            out[name] = np.broadcast_to(d[:m].numpy().astype(np.int32), (B, m)).copy()
     # the 11 knn_points selections in call order (same sites as the training step's)
     assert len(KNN_CALLS) == len(TRAIN_KNN_NAMES), len(KNN_CALLS)
     for name, idx in zip(TRAIN_KNN_NAMES, KNN_CALLS):
@@ -270,7 +298,7 @@ def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict) -> di
         out[name] = idx.numpy()
     # the same forward in float64 on the same selections: the fp32 reference's own distance
     # from it is the scale a second fp32 implementation is held to (tests/parity.py)
-    r64 = _replay64(HRegNet, pu, sd, src, dst)
+    r64 = _replay64(HRegNet, pu, sd, src, dst, seed=seed, args=args)
     for i, (R, t) in enumerate(zip(r64["rotation"], r64["translation"])):
         out[f"R{3 - i}_64"] = R.numpy()
         out[f"t{3 - i}_64"] = t.numpy()
@@ -284,11 +312,11 @@ def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict) -> di
     return out
 
 
-def _replay64(Model, pu, sd, src, dst, seed=None):
+def _replay64(Model, pu, sd, src, dst, seed=None, args=None):
     """The eval forward of `Model` in float64, every FPS / kNN selection replayed from the
-    fp32 run just made (pu.calls, KNN_CALLS)."""
+    fp32 run just made (pu.calls, KNN_CALLS; random samples: the same seed)."""
     global KNN_REPLAY
-    net = Model(_Args())
+    net = Model((args or _Args)())
     net.load_state_dict(sd)
     net = net.double().eval()
     pu.replay = [c[1].clone() for c in pu.calls]
@@ -322,6 +350,10 @@ def forward_fixtures(HRegNet, pu, sd):
     fx["R_gt"], fx["t_gt"] = Rg, tg
     np.savez_compressed(os.path.join(HERE, "hregnet_lidar_b2_n4096.npz"), **fx)
     print("lidar fixture written", flush=True)
+    # use_fps=False: random sampling on the seeded host generator (layers.py:144-147)
+    fx = model_fixture(HRegNet, pu, s, d, sd, args=_ArgsRandSample, seed=11)
+    np.savez_compressed(os.path.join(HERE, "hregnet_randsample_b2_n4096.npz"), **fx)
+    print("random-sampling fixture written", flush=True)
 
 
 def model_v2_fixture(Model_V2, pu, src: np.ndarray, dst: np.ndarray, sd: dict, seed: int) -> dict:

@@ -60,6 +60,52 @@ def test_forward_matches_reference_fixture(net, fixture):
     compare_forward(r, g, title="GPU vs " + fixture)
 
 
+def test_random_sampling_forward_matches_reference(net):
+    """use_fps=False (layers.py:144-147; the default of the reference's training scripts):
+    the samples are torch.randperm draws on the host generator in the reference's order,
+    so after the fixture's seed engine.hregnet_forward(use_fps=False) selects the
+    reference's points and matches its forward under the parity contract; the module API
+    (HRegNet with args.use_fps False) draws the same and returns the same bits."""
+    from pcd_reg_hregnet_amd import engine
+    from pcd_reg_hregnet_amd.models import HRegNet
+    g = load_npz("hregnet_randsample_b2_n4096.npz")
+    B = g["src"].shape[0]
+    P = net.prepared(torch.device("cuda"))
+    src, dst = torch.from_numpy(g["src"]).cuda(), torch.from_numpy(g["dst"]).cuda()
+    torch.manual_seed(int(g["perm_seed"]))
+    engine.INDEX_RECORD = {}
+    try:
+        with torch.no_grad():
+            r = engine.hregnet_forward(P, src, dst, use_fps=False)
+        torch.cuda.synchronize()
+        rec = engine.INDEX_RECORD
+    finally:
+        engine.INDEX_RECORD = None
+    cpu = {"rotation": [x.cpu().numpy() for x in r["rotation"]],
+           "translation": [x.cpu().numpy() for x in r["translation"]],
+           "_fps_idx": [x.cpu().numpy() for x in r["_fps_idx"]],
+           "_knn": {k: v.cpu().numpy() for k, v in rec.items()}}
+    for k in r:
+        if k.startswith(("src_xyz_corres", "src_dst_weights")):
+            cpu[k] = r[k].cpu().numpy()
+    for part in ("src_feats", "dst_feats"):
+        cpu[part] = {k: v.cpu().numpy() for k, v in r[part].items()}
+    for lv in (1, 2, 3):
+        np.testing.assert_array_equal(cpu["_fps_idx"][lv - 1][:B], g[f"src_fps_{lv}"])
+        np.testing.assert_array_equal(cpu["_fps_idx"][lv - 1][B:], g[f"dst_fps_{lv}"])
+    compare_forward(cpu, g, title="GPU vs hregnet_randsample_b2_n4096.npz")
+
+    class NoFps(Args):
+        use_fps = False
+    m = HRegNet(NoFps())
+    m.load_state_dict(net.state_dict())
+    m = m.cuda().eval()
+    torch.manual_seed(int(g["perm_seed"]))
+    with torch.no_grad():
+        r2 = m(src, dst)
+    assert torch.equal(r2["rotation"][-1], r["rotation"][-1])
+
+
 def test_module_forward_api(net):
     """HRegNet.forward returns the reference's dict and shapes (models.py:129-148)."""
     g = load_npz("hregnet_lidar_b2_n4096.npz")

@@ -789,3 +789,44 @@ def test_train_step_config4_shape():
 def load_npz_golden(name):
     from helpers import load_npz
     return load_npz(name)
+
+
+def test_train_step_random_sampling():
+    """use_fps=False in train mode (train_reg_v0.py's default): each level's sample is the
+    reference's torch.randperm draw, in the reference's order (src levels 1-3, then dst),
+    the step runs with finite parameters, and two runs from the same seed are bitwise
+    equal."""
+    from pcd_reg_hregnet_amd import synthetic, train_graph, trainer
+    from helpers import Args, state_dict_torch
+    from pcd_reg_hregnet_amd.models import HRegNet
+
+    class NoFps(Args):
+        use_fps = False
+    s, d, Rg, tg_ = synthetic.lidar_batch(2, 2048, seed0=21)
+    s, d = torch.from_numpy(s).to(DEV), torch.from_numpy(d).to(DEV)
+    Rg, tg_ = torch.from_numpy(Rg).to(DEV), torch.from_numpy(tg_).to(DEV)
+
+    def run():
+        net = HRegNet(NoFps())
+        net.load_state_dict(state_dict_torch())
+        tr = trainer.Trainer(net.to(DEV), lr=1e-3)
+        torch.manual_seed(3)
+        hook = train_graph.IndexHook()
+        ret = train_graph.hregnet_train_forward(tr.net, s, d, hook)
+        torch.manual_seed(3)
+        losses = [float(tr.step(s, d, Rg, tg_, next_batch=(s, d))[0]) for _ in range(2)]
+        torch.cuda.synchronize()
+        assert torch.isfinite(tr.params.flat).all()
+        return hook.record, losses, tr.params.flat.clone(), ret
+
+    rec, l1, p1, _ = run()
+    torch.manual_seed(3)
+    want = [torch.randperm(n)[:m] for n, m in ((2048, 1024), (1024, 512), (512, 256)) * 2]
+    names = ["src_fps_1", "src_fps_2", "src_fps_3", "dst_fps_1", "dst_fps_2", "dst_fps_3"]
+    for name, w in zip(names, want):
+        got = rec[name].cpu()
+        assert got.shape == (2, w.numel())
+        assert torch.equal(got[0].long(), w) and torch.equal(got[1].long(), w), name
+    _, l2, p2, _ = run()
+    assert l1 == l2 and torch.equal(p1, p2)
+    assert all(np.isfinite(l1))

@@ -79,6 +79,30 @@ def test_forward_matches_reference(sd, fixture):
     compare_forward(r, g, title="oracle vs " + fixture)
 
 
+def test_random_sampling_forward_matches_reference(sd):
+    """use_fps=False (layers.py:144-147): the oracle fed the reference's own random samples
+    (hregnet_randsample_b2_n4096.npz) against the reference's forward."""
+    g = load_npz("hregnet_randsample_b2_n4096.npz")
+    samples = [g[f"{p}_fps_{lv}"] for p in ("src", "dst") for lv in (1, 2, 3)]
+    r = oracle.hregnet_forward(sd, g["src"], g["dst"], samples=samples)
+    compare_forward(r, g, title="oracle vs hregnet_randsample_b2_n4096.npz")
+
+
+def test_random_sample_draws_match_reference():
+    """engine.random_samples draws torch.randperm(N)[:M] per level on the host generator
+    in the reference's order (src levels 1-3, then dst), one draw per cloud set: after the
+    fixture's seed it reproduces the reference's samples exactly (no GPU needed)."""
+    import torch
+    from pcd_reg_hregnet_amd import engine
+    g = load_npz("hregnet_randsample_b2_n4096.npz")
+    B, N = g["src"].shape[:2]
+    torch.manual_seed(int(g["perm_seed"]))
+    got = engine.random_samples(2, B, engine.level_input_sizes(N), "cpu")
+    for lv in (1, 2, 3):
+        want = np.concatenate([g[f"src_fps_{lv}"], g[f"dst_fps_{lv}"]], 0)
+        np.testing.assert_array_equal(got[lv - 1].numpy(), want)
+
+
 # Model_V2 outputs indexed by source keypoint: [B, M, ...] (channel-major ones transposed)
 V2_ROWS = {"src_xyz_corres_3": 1e-3, "src_xyz_corres_2": 1e-3, "src_xyz_corres_1": 1e-3,
            "src_xyz_2_trans": 1e-3, "src_feats_sigmas_2": 1e-3, "src_feats_desc_2": 1e-3,
