@@ -45,6 +45,8 @@
  *                                            (losses/losses.py:97-164; callers train/train_reg_v1.py:101,252)
  *   hreg_calib_metrics                    <- CalibEval.add_batch / geodesic_distance
  *                                            (metrics/calibeval.py:72-113,197-214; caller test/test_v3.py:130-140)
+ *   hreg_icp_init / _iterate / _result    <- open3d.pipelines.registration.registration_icp, point-to-point
+ *                                            (test/test_v4.py:140-158; third-party, not vendored)
  */
 #ifndef HREGNET_AMD_H
 #define HREGNET_AMD_H
@@ -308,6 +310,24 @@ int hreg_transformation_loss(const float *pred_R, const float *pred_t, const flo
  * batch_geo[2] = {mean geodesic angle of E (deg), mean ||E[:3,3]||} (calibeval.py:197-214). */
 int hreg_calib_metrics(const float *pred_tf, const float *gt_tf, int nb, float *per_pair,
                        float *batch_geo, void *stream);
+
+/* ---------------- point-to-point ICP refinement (csrc/icp.hip) ----------------
+ * open3d registration_icp(source, target, max_correspondence_distance, init,
+ * TransformationEstimationPointToPoint(), ICPConvergenceCriteria(relative_fitness,
+ * relative_rmse, max_iteration)) as test/test_v4.py:140-158 calls it after the network,
+ * for nb independent pairs.  source [nb][n_src][3], target [nb][n_dst][3] fp32, n <= 65536;
+ * T0 [nb][4][4] fp32 row-major (null: identity).  ws: hreg_icp_ws_bytes, 256-byte aligned,
+ * owned by the caller for the whole run.  hreg_icp_iterate enqueues `iters` iterations (pairs
+ * already converged skip them); the caller polls hreg_icp_result's done flags between calls.
+ * Results: T [nb][4][4], fitness = matches / n_src, inlier_rmse, iterations = updates applied. */
+size_t hreg_icp_ws_bytes(int nb, int n_src, int n_dst);
+int hreg_icp_init(const float *src, const float *dst, int nb, int n_src, int n_dst, const float *T0,
+                  void *ws, void *stream);
+int hreg_icp_iterate(const float *dst, int nb, int n_src, int n_dst, float max_corr_dist,
+                     double rel_fitness, double rel_rmse, int max_iteration, int iters, void *ws,
+                     void *stream);
+int hreg_icp_result(const void *ws, int nb, int n_src, int n_dst, float *T_out, float *fitness,
+                    float *inlier_rmse, int32_t *iterations, int32_t *done, void *stream);
 
 /* ---------------- training-step building blocks (csrc/train.hip) ----------------
  * Train-mode BatchNorm after a 1x1 conv (layers.py:115-130 etc. in .train(); the

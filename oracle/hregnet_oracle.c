@@ -20,6 +20,11 @@
  *     returned ascending.  Tie order in pytorch3d is an unstable torch.sort,
  *     so the canonical order here is (dist, idx) ascending -- "parity
  *     unpinned" against pytorch3d itself.
+ *   - the nearest-neighbour-within-radius search of open3d's registration_icp
+ *     (third-party open3d, not vendored; caller test/test_v4.py:144-158): the
+ *     nearest target point with dist^2 < r^2 strictly (dist in the order above),
+ *     ties to the lowest index -- the choice of the GPU kernel (csrc/icp.hip);
+ *     parity unpinned against open3d's kd-tree.
  *
  * Float policy: compiled with -ffp-contract=off, so every a*a+b*b is two
  * roundings, matching the non-contracted CPU/PyTorch reference path.
@@ -187,4 +192,22 @@ int oracle_num_threads(void) {
 #else
     return 1;
 #endif
+}
+
+/* open3d registration_icp correspondence search, brute force: out[i] = argmin_j d2(q_i, p_j)
+ * over d2 < r2 (ties: lowest j), -1 when none; OpenMP over queries. */
+int oracle_nn_radius(const float *q, int nq, const float *p, int np, float r2, int32_t *out) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < nq; ++i) {
+        const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+        float best = INFINITY;
+        int bid = -1;
+        for (int j = 0; j < np; ++j) {
+            const float dx = qx - p[3 * j], dy = qy - p[3 * j + 1], dz = qz - p[3 * j + 2];
+            const float d = (dx * dx + dy * dy) + dz * dz;
+            if (d < best) { best = d; bid = j; }
+        }
+        out[i] = best < r2 ? bid : -1;
+    }
+    return 0;
 }

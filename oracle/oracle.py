@@ -49,6 +49,8 @@ def lib():
         L.oracle_gather_points_grad.argtypes = [f32p, i32p, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, ctypes.c_int, f32p]
         L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_nn_radius.argtypes = [f32p, ctypes.c_int, f32p, ctypes.c_int, ctypes.c_float, i32p]
+        L.oracle_nn_radius.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -661,3 +663,66 @@ def deep_mi_loss(params, x_global, x_global_prime, x_local, x_local_prime, c_loc
     loc = js(local_d, c_local, x_local, x_local_prime)
     glo = js(global_d, c_global, x_global, x_global_prime)
     return np.float32(loc + glo), np.float32(loc), np.float32(glo)
+
+
+def nn_radius(q, p, r):
+    """nearest p for each q strictly within r (fp32 distances, ties to the lowest index),
+    -1 when none (open3d's hybrid search as registration_icp uses it)"""
+    q = np.ascontiguousarray(q, np.float32)
+    p = np.ascontiguousarray(p, np.float32)
+    out = np.empty(q.shape[0], np.int32)
+    lib().oracle_nn_radius(_fp(q), q.shape[0], _fp(p), p.shape[0], np.float32(r) * np.float32(r),
+                           _ip(out))
+    return out
+
+
+def _xform64(T, s):
+    """p = R s + t in float64, the operation order of csrc/icp.hip xform"""
+    s = s.astype(np.float64)
+    return np.stack([((T[a, 0] * s[:, 0] + T[a, 1] * s[:, 1]) + T[a, 2] * s[:, 2]) + T[a, 3]
+                     for a in range(3)], 1)
+
+
+def registration_icp(src, dst, max_corr, init=None, rel_fitness=1e-6, rel_rmse=1e-6,
+                     max_iteration=30):
+    """open3d.pipelines.registration.registration_icp with
+    TransformationEstimationPointToPoint (test/test_v4.py:144-158), one pair; open3d is
+    not vendored -- its published loop: result_0 = correspondences(T_0); for i <
+    max_iteration: T_{i+1} = Kabsch(result_i) T_i, result_{i+1} = correspondences(T_{i+1}),
+    stop when fitness and inlier_rmse both move less than the relative criteria.
+    Correspondences: nn_radius on the fp32-rounded transformed source (fp64 pose), fitness =
+    matches / n_src, inlier_rmse = sqrt(mean d^2) in fp64.  -> (T [4,4] fp64, fitness,
+    inlier_rmse, updates applied)."""
+    T = np.eye(4) if init is None else np.asarray(init, np.float64).copy()
+
+    def corr(T):
+        p64 = _xform64(T, src)
+        j = nn_radius(p64.astype(np.float32), dst, max_corr)
+        ok = j >= 0
+        P, Q = p64[ok], dst[j[ok]].astype(np.float64)
+        n = int(ok.sum())
+        fit = n / src.shape[0]
+        rmse = float(np.sqrt(((P - Q) ** 2).sum() / n)) if n else 0.0
+        return P, Q, fit, rmse
+
+    P, Q, fit, rmse = corr(T)
+    it = 0
+    for it in range(1, max_iteration + 1):
+        upd = np.eye(4)
+        if P.shape[0]:  # Kabsch (Eigen::umeyama without scaling)
+            mp, mq = P.mean(0), Q.mean(0)
+            H = (P - mp).T @ (Q - mq)
+            U, _, Vt = np.linalg.svd(H)
+            V = Vt.T
+            D = np.diag([1.0, 1.0, np.sign(np.linalg.det(V @ U.T)) or 1.0])
+            R = V @ D @ U.T
+            upd[:3, :3], upd[:3, 3] = R, mq - R @ mp
+        T = upd @ T
+        P, Q, fit2, rmse2 = corr(T)
+        conv = abs(fit2 - fit) < rel_fitness and abs(rmse2 - rmse) < rel_rmse
+        fit, rmse = fit2, rmse2
+        if conv:
+            break
+    else:
+        it = max_iteration
+    return T, fit, rmse, it

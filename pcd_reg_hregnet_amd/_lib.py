@@ -150,6 +150,10 @@ _SIGS = {
                                      _vp, _vp, _vp],
     "hreg_index_offset": [_vp, _i, _i, _i, _vp, _vp],
     "hreg_calib_metrics": [_vp, _vp, _i, _vp, _vp, _vp],
+    "hreg_icp_init": [_vp, _vp, _i, _i, _i, _vp, _vp, _vp],
+    "hreg_icp_iterate": [_vp, _i, _i, _i, ctypes.c_float, ctypes.c_double, ctypes.c_double, _i, _i,
+                         _vp, _vp],
+    "hreg_icp_result": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 
 EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_reduce_ws_bytes",
@@ -160,7 +164,7 @@ EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_
                           "hreg_group_split_l3_table_floats", "hreg_group6_l2_table_floats",
                           "hreg_group6_l3_table_floats", "hreg_group_l1_6_table_floats",
                           "hreg_group_split6_l2_table_floats", "hreg_group_split6_l3_table_floats",
-                          "hreg_coarse_head6_table_floats")
+                          "hreg_coarse_head6_table_floats", "hreg_icp_ws_bytes")
 
 _lib = None
 
@@ -195,6 +199,8 @@ def load(require_gpu: bool = True):
         L.hreg_csr_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         L.hreg_sim_feats_bwd_ws_bytes.restype = ctypes.c_size_t
         L.hreg_sim_feats_bwd_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.hreg_icp_ws_bytes.restype = ctypes.c_size_t
+        L.hreg_icp_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
                      "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
                      "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats",
