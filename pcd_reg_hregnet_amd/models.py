@@ -257,9 +257,9 @@ class Model_V2(nn.Module):
 
     def forward(self, src_points, dst_points):
         if self.training:
-            raise NotImplementedError(
-                "train-mode forward (batch-statistics BN + backward kernels) is not implemented "
-                "on the HIP path yet; call .eval()")
+            # batch-statistics BN + backward kernels (train_graph.py, csrc/train_ops.hip)
+            from . import train_graph
+            return train_graph.hregnet_train_forward(self, src_points, dst_points, v2=True)
         P = self.prepared(src_points.device)
         out = engine.model_v2_forward(P, src_points.float().contiguous(),
                                       dst_points.float().contiguous(),

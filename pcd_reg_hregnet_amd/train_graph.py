@@ -670,8 +670,9 @@ def coarse_reg(m, s_xyz, s_desc, d_xyz, d_desc, s_w, d_w, hook=None):
     return corres.view(B, N1, 3), w.view(B, N1)
 
 
-def fine_reg(m, s_xyz, s_feat, d_xyz, d_feat, s_w, d_w, hook=None, name="fine"):
-    """FineReg.forward (layers.py:433-454), train mode."""
+def fine_reg(m, s_xyz, s_feat, d_xyz, d_feat, s_w, d_w, hook=None, name="fine", return_att=False):
+    """FineReg.forward (layers.py:433-454), train mode (return_att: also the attentive
+    features [B*N1][2C] that FineReg2 feeds to mlpx, model_v2/layers.py:484-490)."""
     k = m.k
     B, N1, _ = s_xyz.shape
     N2 = d_xyz.shape[1]
@@ -689,12 +690,27 @@ def fine_reg(m, s_xyz, s_feat, d_xyz, d_feat, s_w, d_w, hook=None, name="fine"):
     f = seq_convs(feats, m.convs_1)
     corres, _, att = attention(f, k, kx=kx, want_sum=True)
     w, _ = _mlp_head(att, (m.mlp1, m.mlp2, m.mlp3), _lib.HREG_HEAD_SIGMOID, 1, B * N1)
+    if return_att:
+        return corres.view(B, N1, 3), w.view(B, N1), att
     return corres.view(B, N1, 3), w.view(B, N1)
 
 
-def hregnet_train_forward(net, src, dst, hook=None):
+def batch_shuffle(x, perm):
+    """x[perm] along the batch dimension (FineReg2's prime copies, model_v2/layers.py:492,
+    497) as a row gather over [B][rest] with the deterministic scatter backward."""
+    B = x.shape[0]
+    rows = x.reshape(B, -1)
+    imap = IndexMap(perm.to(device=x.device, dtype=torch.int32).contiguous(), B)
+    return gather_rows(rows, imap).view_as(x)
+
+
+def hregnet_train_forward(net, src, dst, hook=None, v2=False):
     """HRegNet.forward (models/HRegNet/models.py:77-148) in train mode -> the reference's
-    result dict; differentiable in every parameter that requires grad."""
+    result dict; differentiable in every parameter that requires grad.  v2: Model_V2's
+    forward (model_v2/models.py:77-183): fine_corres_2 is FineReg2, whose attentive
+    features also pass mlpx (Conv1d + train-mode BN + ReLU) and whose prime copies are
+    batch shuffles by two host torch.randperm(B) draws, features first
+    (model_v2/layers.py:484-497); returns Model_V2's dict."""
     fe = net.feature_extraction
     src = src.float().contiguous()
     dst = dst.float().contiguous()
@@ -706,8 +722,19 @@ def hregnet_train_forward(net, src, dst, hook=None):
                         sf["sigmas_3"], df["sigmas_3"], hook)
     R3, t3 = weighted_svd(sf["xyz_3"], c3, w3)
     x2t = transform(sf["xyz_2"], R3, t3)
-    c2, w2 = fine_reg(net.fine_corres_2, x2t, sf["desc_2"], df["xyz_2"], df["desc_2"],
-                      sf["sigmas_2"], df["sigmas_2"], hook, "fine2")
+    if v2:
+        m2 = net.fine_corres_2
+        c2, w2, att2 = fine_reg(m2, x2t, sf["desc_2"], df["xyz_2"], df["desc_2"],
+                                sf["sigmas_2"], df["sigmas_2"], hook, "fine2", return_att=True)
+        N2 = c2.shape[1]
+        f2 = conv_bn(att2, m2.mlpx[0], m2.mlpx[1], relu=True)       # [B*N2][C]
+        feats2 = f2.view(B, N2, -1).transpose(1, 2)                   # [B, C, N2]
+        pf, pw = torch.randperm(B), torch.randperm(B)                 # features first
+        feats2_prime = batch_shuffle(f2.view(B, N2, -1), pf).transpose(1, 2)
+        w2_prime = batch_shuffle(w2, pw)
+    else:
+        c2, w2 = fine_reg(net.fine_corres_2, x2t, sf["desc_2"], df["xyz_2"], df["desc_2"],
+                          sf["sigmas_2"], df["sigmas_2"], hook, "fine2")
     R2_, t2_ = weighted_svd(x2t, c2, w2)
     R2, t2 = compose(R2_, t2_, R3, t3)
     x1t = transform(sf["xyz_1"], R2, t2)
@@ -725,6 +752,17 @@ def hregnet_train_forward(net, src, dst, hook=None):
             d[f"desc_{i + 1}"] = f[f"desc_{i + 1}"].view(B, m, -1).transpose(1, 2)
         return d
 
+    if v2:  # model_v2/models.py:143-181
+        sfd, dfd = feats(sf), feats(df)
+        return {
+            "src_xyz_corres_3": c3, "src_xyz_corres_2": c2, "src_xyz_corres_1": c1,
+            "rotation": [R3, R2, R1], "translation": [t3, t2, t1],
+            "src_feats_desc_2": sfd["desc_2"], "src_feats_sigmas_2": sfd["sigmas_2"],
+            "src_xyz_2_trans": x2t, "dst_xyz_2": dfd["xyz_2"],
+            "src_dst_feats_2": feats2, "src_dst_feats_2_prime": feats2_prime,
+            "src_dst_weights_2": w2, "src_dst_weights_2_prime": w2_prime,
+            "src_feats": sfd, "dst_feats": dfd,
+        }
     return {
         "src_xyz_corres_3": c3, "src_xyz_corres_2": c2, "src_xyz_corres_1": c1,
         "src_dst_weights_3": w3, "src_dst_weights_2": w2, "src_dst_weights_1": w1,

@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --traj-only [--traj-c4] | --forward-only | --metrics-only | --perturb-only | --mi-only]   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --traj-only [--traj-c4] | --forward-only | --v2-train-only | --metrics-only | --perturb-only | --mi-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -402,8 +402,8 @@ def model_v2_fixture(Model_V2, pu, src: np.ndarray, dst: np.ndarray, sd: dict, s
     return out
 
 
-def v2_fixtures(pu):
-    """Model_V2 (config 5 shape: 65536-point clouds) fixtures."""
+def v2_fixtures_setup():
+    """what importing models/model_v2 needs (it takes the helpers from the models package)"""
     import models.utils as mu  # reference helpers, re-exported by models/__init__.py
     pkg = sys.modules["models"]
     for name in ("furthest_point_sample", "weighted_furthest_point_sample", "gather_operation",
@@ -412,6 +412,11 @@ def v2_fixtures(pu):
     tr = sys.modules["pytorch3d.transforms"]
     for name in ("axis_angle_to_matrix", "rotation_6d_to_matrix"):
         setattr(tr, name, lambda *a, **k: (_ for _ in ()).throw(NotImplementedError()))
+
+
+def v2_fixtures(pu):
+    """Model_V2 (config 5 shape: 65536-point clouds) fixtures."""
+    v2_fixtures_setup()
     from models.model_v2.models import Model_V2  # noqa: E402  (reference code)
     from pcd_reg_hregnet_amd import synthetic, weights
     template = Model_V2(_Args()).state_dict()
@@ -671,6 +676,101 @@ def trajectory_fixtures(pu, B=2, N=2048, steps=6, seed0=5, name=None):
     print(name, "written:", out["loss32"][:, 0], out["loss64"][:, 0], flush=True)
 
 
+def v2_train_fixtures(pu):
+    """One Model_V2 training step as train/train_reg_v6.py:310-350 takes it: Model_V2 in
+    .train() (batch-statistics BN), DeepMILoss(512, 128) (.train()), js_loss = mi(x_global =
+    weights_2, x_global_prime, x_local = mlpx features, x_local_prime, c_local = desc_2,
+    c_global = sigmas_2) and loss = normalized_c_loss * beta + js_loss * gamma, where the
+    Chamfer term is a Python float (c_loss.item()) and so carries no gradient: the gradient
+    is js_loss's.  (The script unpacks `ret_dict, corres_dict = net(...)` and reads
+    x_global from corres_dict, but model_v2/models.py:183 returns ret_dict alone, whose
+    src_dst_weights_2 is the same tensor.)  Saved: inputs, the FPS / kNN selections, the
+    two prime draws' seed, js_loss, every parameter gradient (norm, leading entries) of the
+    net and the MI loss, and the same step replayed in float64 on the same selections."""
+    import importlib.util
+    global KNN_REPLAY
+    v2_fixtures_setup()
+    from models.model_v2.models import Model_V2  # noqa: E402  (reference code)
+    from pcd_reg_hregnet_amd import synthetic, weights
+    spec = importlib.util.spec_from_file_location("ref_mi_loss_v2", os.path.join(REF, "losses/mi_loss_v2.py"))
+    M = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(M)
+    sd = weights.make_state_dict(Model_V2(_Args()).state_dict(), seed=0, pretrained_feats=True)
+    torch.manual_seed(21)
+    mi = M.DeepMILoss(global_in_channels=512, local_in_channels=128)
+    mi_sd = {k: v.clone() for k, v in mi.state_dict().items()}
+    s, d, _, _ = synthetic.lidar_batch(2, 2048, seed0=5)
+    perm_seed = 13
+    out = {"src": s, "dst": d, "perm_seed": np.array(perm_seed)}
+    out.update({"mi_" + k: v.numpy() for k, v in mi_sd.items()})
+
+    def step(dtype, replay):
+        global KNN_REPLAY
+        net = Model_V2(_Args())
+        net.load_state_dict(sd)
+        net = net.to(dtype).train()
+        m = M.DeepMILoss(global_in_channels=512, local_in_channels=128)
+        m.load_state_dict(mi_sd)
+        m = m.to(dtype).train()
+        if replay is not None:
+            pu.replay = [c.clone() for c in replay[0]]
+            KNN_REPLAY = [c.clone() for c in replay[1]]
+        pu.calls.clear()
+        KNN_CALLS.clear()
+        torch_eye, torch_zeros = torch.eye, torch.zeros
+        if dtype == torch.float64:
+            torch.eye = lambda *a, **k: torch_eye(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+            torch.zeros = lambda *a, **k: torch_zeros(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+        try:
+            torch.manual_seed(perm_seed)
+            ret = net(torch.from_numpy(s).to(dtype), torch.from_numpy(d).to(dtype))
+            js = m(x_global=ret["src_dst_weights_2"], x_global_prime=ret["src_dst_weights_2_prime"],
+                   x_local=ret["src_dst_feats_2"], x_local_prime=ret["src_dst_feats_2_prime"],
+                   c_local=ret["src_feats"]["desc_2"], c_global=ret["src_feats"]["sigmas_2"])
+            js.backward()
+        finally:
+            torch.eye, torch.zeros = torch_eye, torch_zeros
+            pu.replay = None
+            KNN_REPLAY = None
+        return net, m, js, ret
+
+    net, m, js, ret = step(torch.float32, None)
+    sel = ([c[1].clone() for c in pu.calls], [c.clone() for c in KNN_CALLS])
+    for name, (_, idx) in zip(TRAIN_FPS_NAMES, pu.calls):
+        out["idx_" + name] = idx.numpy().astype(np.int32)
+    assert len(KNN_CALLS) == len(TRAIN_KNN_NAMES), len(KNN_CALLS)
+    for name, idx in zip(TRAIN_KNN_NAMES, KNN_CALLS):
+        out["idx_" + name] = idx.numpy().astype(np.int32)
+    out["js"] = js.detach().numpy()
+    out["R1"] = ret["rotation"][-1].detach().numpy()
+    out["feats_2"] = ret["src_dst_feats_2"].detach().numpy()
+    out["weights_2"] = ret["src_dst_weights_2"].detach().numpy()
+    names, nograd = [], []
+    for prefix, mod in (("net.", net), ("mi.", m)):
+        for name, p in mod.named_parameters():
+            if p.grad is None:  # outside js_loss's graph (fine_corres_1, ...)
+                nograd.append(prefix + name)
+                continue
+            g = p.grad.detach().reshape(-1).double()
+            names.append(prefix + name)
+            out["gnorm_" + prefix + name] = np.array(g.norm().item())
+            out["ghead_" + prefix + name] = g[:256].float().numpy()
+    out["param_names"] = np.array(names)
+    out["nograd_names"] = np.array(nograd)
+    net64, m64, js64, ret64 = step(torch.float64, sel)
+    out["js_64"] = js64.detach().numpy()
+    out["feats_2_64"] = ret64["src_dst_feats_2"].detach().numpy()
+    for prefix, mod in (("net.", net64), ("mi.", m64)):
+        for name, p in mod.named_parameters():
+            if p.grad is None:
+                continue
+            g = p.grad.detach().reshape(-1)
+            out["g64norm_" + prefix + name] = np.array(g.norm().item())
+            out["g64head_" + prefix + name] = g[:256].numpy()
+    np.savez_compressed(os.path.join(HERE, "v2_train_step_b2_n2048.npz"), **out)
+    print("v2_train_step_b2_n2048.npz written, js", float(js), float(js64), flush=True)
+
+
 class _CalibConfig:
     """the attributes CalibEval / MultiLayerCalibEval read (config.py DataConfig)"""
     dataset = "man"
@@ -921,6 +1021,9 @@ def main():
             trajectory_fixtures(pu, B=8, N=16384, steps=14, seed0=0)
         else:
             trajectory_fixtures(pu)
+        return
+    if "--v2-train-only" in sys.argv:
+        v2_train_fixtures(pu)
         return
     if "--v2-only" in sys.argv:
         v2_fixtures(pu)

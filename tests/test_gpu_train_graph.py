@@ -830,3 +830,65 @@ def test_train_step_random_sampling():
     _, l2, p2, _ = run()
     assert l1 == l2 and torch.equal(p1, p2)
     assert all(np.isfinite(l1))
+
+
+def test_model_v2_train_step_matches_reference():
+    """Model_V2 in train mode (model_v2/models.py:77-183: FineReg2's mlpx features and the
+    randperm prime copies) + DeepMILoss's js_loss backward (train/train_reg_v6.py:324-350,
+    whose loss gradient is js_loss's: the Chamfer term enters as a Python float) against
+    the reference's own step on the same selections (tests/golden/v2_train_step_b2_n2048.npz,
+    make_golden.py v2_train_fixtures), with the bars of the HRegNet step above: every
+    parameter gradient within max(4 x the fp32 reference's own distance from its float64
+    replay, 1e-3), FLIP_BAR below near-tie maxima, rounding-noise gradients (conv biases
+    before a train-mode BN) absolutely small, and no gradient where the reference has none."""
+    from helpers import load_npz, state_dict_v2_torch, Args
+    from pcd_reg_hregnet_amd import mi_losses, train_graph
+    from pcd_reg_hregnet_amd.models import Model_V2
+    fx = load_npz("v2_train_step_b2_n2048.npz")
+    net = Model_V2(Args())
+    net.load_state_dict(state_dict_v2_torch())
+    net = net.to(DEV).train()
+    mi = mi_losses.DeepMILoss(global_in_channels=512, local_in_channels=128)
+    mi.load_state_dict({k[3:]: torch.from_numpy(fx[k]) for k in fx if k.startswith("mi_")})
+    mi = mi.to(DEV).train()
+    hook = train_graph.IndexHook({k[4:]: fx[k] for k in fx if k.startswith("idx_")})
+    torch.manual_seed(int(fx["perm_seed"]))
+    ret = train_graph.hregnet_train_forward(net, torch.from_numpy(fx["src"]).to(DEV),
+                                            torch.from_numpy(fx["dst"]).to(DEV), hook, v2=True)
+    js = mi(x_global=ret["src_dst_weights_2"], x_global_prime=ret["src_dst_weights_2_prime"],
+            x_local=ret["src_dst_feats_2"], x_local_prime=ret["src_dst_feats_2_prime"],
+            c_local=ret["src_feats"]["desc_2"], c_global=ret["src_feats"]["sigmas_2"])
+    js.backward()
+    torch.cuda.synchronize()
+    print("\njs ours %.7f ref32 %.7f ref64 %.7f" % (float(js), float(fx["js"]), float(fx["js_64"])))
+    assert abs(float(js) - float(fx["js_64"])) <= max(4 * abs(float(fx["js"]) - float(fx["js_64"])),
+                                                      1e-5 * abs(float(fx["js_64"])))
+    f = ret["src_dst_feats_2"].detach().double().cpu().numpy()
+    e = np.abs(f - fx["feats_2_64"]).max() / np.abs(fx["feats_2_64"]).max()
+    assert e <= 1e-4, e
+    np.testing.assert_allclose(ret["rotation"][-1].detach().cpu().numpy(), fx["R1"], atol=1e-4)
+    params = {"net." + n: p for n, p in net.named_parameters()}
+    params.update({"mi." + n: p for n, p in mi.named_parameters()})
+    for name in fx["nograd_names"]:
+        g = params[str(name)].grad
+        assert g is None or float(g.abs().max()) == 0.0, name
+    gmax = max(float(fx["g64norm_" + n]) for n in fx["param_names"])
+    items = []
+    for name in fx["param_names"]:
+        name = str(name)
+        g = params[name].grad.detach().reshape(-1).double().cpu().numpy()
+        n64, n32 = float(fx["g64norm_" + name]), float(fx["gnorm_" + name])
+        h64, h32 = fx["g64head_" + name], fx["ghead_" + name].astype(np.float64)
+        if n64 < 1e-6 * gmax:  # rounding noise (conv bias before a train-mode BN)
+            assert np.linalg.norm(g) < 1e-5 * gmax, name
+            continue
+        hs = max(np.abs(h64).max(), 1e-30)
+        ours = max(abs(np.linalg.norm(g) - n64) / n64, np.abs(g[:h64.size] - h64).max() / hs)
+        ref = max(abs(n32 - n64) / n64, np.abs(h32 - h64).max() / hs)
+        flip_prone = ".feature_extraction." in name or ".convs_2." in name
+        items.append((name, ours, ref, FLIP_BAR if flip_prone else 1e-3))
+    rows = _bar_rows(items)
+    print("ratio to bar, ours vs fp64, fp32 ref vs fp64, gradient:")
+    for r in sorted(rows, key=lambda r: r[3]):
+        print("  %.3f  %.2e  %.2e  %s" % r)
+    assert max(rows)[0] <= 1.0, max(rows)
