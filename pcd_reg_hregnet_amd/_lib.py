@@ -168,10 +168,6 @@ EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_
 
 _lib = None
 
-# Timing analysis only (never in a correctness run): C-ABI entries named in HREG_SKIP are
-# not launched, so a bench run measures the step without them (their outputs stay
-# uninitialised).  tools/skip_sweep.sh.
-SKIP = frozenset(filter(None, os.environ.get("HREG_SKIP", "").split(",")))
 
 
 def load(require_gpu: bool = True):
@@ -229,8 +225,6 @@ def stream_handle() -> int:
 
 def call(name: str, *args) -> None:
     L = load()
-    if name in SKIP:
-        return
     conv = []
     for a in args:
         if isinstance(a, torch.Tensor):
@@ -254,8 +248,6 @@ def device_status(clear: bool = True) -> int:
 
 def gemm(g: Gemm) -> None:
     L = load()
-    if "hreg_gemm" in SKIP:
-        return
     rc = L.hreg_gemm(ctypes.byref(g), stream_handle())
     if rc != HREG_OK:
         raise RuntimeError(f"hreg_gemm failed: {_ERRORS.get(rc, rc)} (code {rc})")

@@ -330,20 +330,11 @@ __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__
 // entry of the launch is a valid index (0 or a real selection) and every sampled row
 // finite; their contents are otherwise undefined and the host raises.  Every other
 // participant then times out within one poll budget too, so the grid drains.
-// tools/fps_experiment.py variants: HREG_FPS_EXP 1 = four lanes publish in one store
-// instruction, 2 = s_sleep between polls; HREG_FPS_S forces the slots per lane,
-// HREG_FPS_PAD the slot stride (16: one 128-byte line per participant)
-#ifndef HREG_FPS_EXP
-#define HREG_FPS_EXP 0
-#endif
-#ifndef HREG_FPS_S
-#define HREG_FPS_S 0
-#endif
-#ifndef HREG_FPS_PAD
-#define HREG_FPS_PAD 4
-#endif
+// (measured alternatives, r2: four lanes publishing in one store instruction 2.45 vs
+// 1.71 ms for 4 x 65536 points; a 128-byte slot stride and s_sleep between polls no
+// faster)
 struct SyncSlot {
-    uint64_t w[HREG_FPS_PAD];  // HREG_FPS_PAD = 16: one 128-byte line per participant
+    uint64_t w[4];
 };
 constexpr int FPS_CL_MAXP = 64;
 constexpr uint32_t FPS_CL_POLLS = 1u << 22;
@@ -428,19 +419,9 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
             const uint32_t rank = (uint32_t)((p * 64 + wl) * S + ws);
             SyncSlot *cur = sl + (j & 1) * FPS_CL_MAXP;
             const uint64_t tag = (uint64_t)(uint32_t)j << 32;
-            // lane 0 publishes; the coordinates first, the key word last.  (Variant 1,
-            // lanes 0..3 storing one word each in a single instruction, lets the polls
-            // start before the stores are acknowledged and measured slower: 2.45 vs
-            // 1.71 ms for 4 x 65536 points.)
-#if HREG_FPS_EXP == 1
-            if (lane < 4) {
-                const float c = lane == 1 ? wx : lane == 2 ? wy : wz;
-                const uint64_t v = lane == 0 ? ((uint64_t)__float_as_uint(wmax) << 32) |
-                                                   ((uint64_t)rank << 10) | (uint64_t)(j & 1023)
-                                             : tag | __float_as_uint(c);
-                st_agent(&cur[p].w[lane], v);
-            }
-#else
+            // lane 0 publishes; the coordinates first, the key word last (lanes 0..3
+            // storing one word each in a single instruction let the polls start before the
+            // stores are acknowledged and measured slower)
             if (lane == 0 && p != stall) {  // stall: hreg_debug_fps_cluster's forced-stall test
                 st_agent(&cur[p].w[1], tag | __float_as_uint(wx));
                 st_agent(&cur[p].w[2], tag | __float_as_uint(wy));
@@ -453,7 +434,6 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
             // compiler drop it) a call took 3.0-3.9 instead of 1.7 ms for 4 x 65536 points
             // (Model_V2 bench 774 -> 617 pairs/s, tools/v2_bisect.sh)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
             // poll: lane q reads participant q's words until all carry tag j
             uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
             bool fresh = lane >= NP;
@@ -468,9 +448,6 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                             (w2 >> 32) == (uint64_t)j && (w3 >> 32) == (uint64_t)j;
                 }
                 if (__all(fresh)) break;
-#if HREG_FPS_EXP == 2
-                __builtin_amdgcn_s_sleep(1);
-#endif
                 if (++polls > polls_max) {
                     timed_out = true;
                     break;
@@ -554,8 +531,8 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     // n = 16384 (level 1): 8 waves x 32 slots rather than 16 waves x 16 -- the same VALU
     // work per SIMD, half the per-wave reduction/winner overhead; both fill a CU's VGPRs
     // (127 x 1024 vs 254 x 512).  768 clouds (the batched level-1 stage) 5.70 -> 5.19 ms,
-    // identical indices (tools/micro/fps_l1_geom.py); HREG_FPS_L1_1024 keeps 16 x 16.
-    if (!weighted && T == 1024 && QT == 16 && getenv("HREG_FPS_L1_1024") == nullptr) {
+    // identical indices (tools/micro/fps_l1_geom.py).
+    if (!weighted && T == 1024 && QT == 16) {
         T = 512; G = 2;
     }
 }
@@ -582,9 +559,9 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
     const long ranks = (long)bs * Q;
     int S = 0;
     for (int s : {8, 16, 32})
-        if (ranks <= (long)FPS_CL_MAXP * 64 * s && (!HREG_FPS_S || s >= HREG_FPS_S)) { S = s; break; }
+        if (ranks <= (long)FPS_CL_MAXP * 64 * s) { S = s; break; }
     const size_t slot_bytes = (size_t)2 * FPS_CL_MAXP * sizeof(SyncSlot);
-    if (S && (size_t)n * sizeof(float) >= slot_bytes && getenv("HREG_FPS_MEM") == nullptr) {
+    if (S && (size_t)n * sizeof(float) >= slot_bytes) {
         const int NP = (int)((ranks + 64L * S - 1) / (64L * S));
         // <= 256 spinning waves per launch: with a few launches in flight on other
         // streams (GraphPipeline lanes) every launch still fits on the chip at once

@@ -52,11 +52,6 @@ __device__ __forceinline__ float4 load_w4(const hreg_gemm_t &g, int b, int n, in
     return *reinterpret_cast<const float4 *>(p);
 }
 
-// timing experiment (bench A/B only, results wrong): HREG_GEMM_EXP=1 skips the K loop
-// (loads + MFMAs), the epilogue writes the affine shift / zeros
-#ifndef HREG_GEMM_EXP
-#define HREG_GEMM_EXP 0
-#endif
 
 template <int BM, int BN, int WM, int WN, int BK, bool ADD = false>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
@@ -79,7 +74,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     const int b = blockIdx.z;
     const int r0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
-    const int nchunks = HREG_GEMM_EXP ? 0 : (g.K + BK - 1) / BK;
+    const int nchunks = (g.K + BK - 1) / BK;
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -438,23 +433,11 @@ extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
         dim3 grid((g.R + 63) / 64, (g.N + 63) / 64, g.batch);
         hipLaunchKernelGGL((gemm_nt_kernel<64, 64, 2, 2, 32>), grid, dim3(256), 0, st, g);
     } else {
-        // HREG_GEMM_BIG (A/B switch, tools/gemm_profile.py): 0 = 128x128 tiles, K in
-        // 16-deep chunks; 1 = 32-deep chunks (half the barriers and load round trips per
-        // MFMA); 2 = 128x256 tiles, 16-deep.  Same k-order in all three: bit-identical.
-        static const int big = [] {
-            const char *e = getenv("HREG_GEMM_BIG");
-            return e ? atoi(e) : 1;
-        }();
-        if (big == 2 && g.N >= 256) {
-            dim3 grid((g.R + 127) / 128, (g.N + 255) / 256, g.batch);
-            hipLaunchKernelGGL((gemm_nt_kernel<128, 256, 2, 2, 16>), grid, dim3(256), 0, st, g);
-        } else if (big >= 1) {
-            dim3 grid((g.R + 127) / 128, (g.N + 127) / 128, g.batch);
-            hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2, 32>), grid, dim3(256), 0, st, g);
-        } else {
-            dim3 grid((g.R + 127) / 128, (g.N + 127) / 128, g.batch);
-            hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2, 16>), grid, dim3(256), 0, st, g);
-        }
+        // 128 x 128 tiles, K in 32-deep chunks (measured r1 against 16-deep chunks and
+        // 128 x 256 tiles, tools/gemm_profile.py: half the barriers and load round trips per
+        // MFMA; the same k-order in all three, bit-identical)
+        dim3 grid((g.R + 127) / 128, (g.N + 127) / 128, g.batch);
+        hipLaunchKernelGGL((gemm_nt_kernel<128, 128, 2, 2, 32>), grid, dim3(256), 0, st, g);
     }
     HREG_CHECK_LAUNCH();
     return HREG_OK;

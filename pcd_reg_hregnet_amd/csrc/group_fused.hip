@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
         const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
         const size_t row = (size_t)t * 32 + j;
         const float2 gin = *reinterpret_cast<const float2 *>(geom + row * 4 + 2 * h);
-        const size_t src = HREG_L2_EXP == 3 ? row : (size_t)gidx[row];
+        const size_t src = (size_t)gidx[row];
         const float *fr = feats + src * CF + h * K::TF;
         const float *pr = PRE ? pre + src * (2 * K::T1 * 32) : nullptr;  // [det C1 | desc C1]
         float ca[CARRY], cb[CARRY];
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
             f32x16 v;
 #pragma unroll
             for (int q = 0; q < 16; ++q)
-                v[q] = HREG_L2_EXP ? emb[co][q] : gsum_w(fmul_rn(emb[co][q], a));
+                v[q] = gsum_w(fmul_rn(emb[co][q], a));
             store_tile(att_feat + (size_t)g * C3, co, v, writer, h);
         }
 
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
         for (int ct = 0; ct < T3; ++ct) {
             f32x16 x2[1];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) x2[0][q] = HREG_L2_EXP ? x1d[ct][q] : gmax_b(x1d[ct][q]);
+            for (int q = 0; q < 16; ++q) x2[0][q] = gmax_b(x1d[ct][q]);
             const FragSeq cur{m1x2.base + ct * 16, m1x2.stride};
             const FragSeq nxt = ct + 1 < T3 ? FragSeq{m1x2.base + (ct + 1) * 16, m1x2.stride} : m1x1;
             // ct even: ca -> cb, odd: cb -> ca
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(
         for (int co = 0; co < TM2; ++co) {
             f32x16 v;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = HREG_L2_EXP ? y2[co][q] : gmax_w(y2[co][q]);
+            for (int q = 0; q < 16; ++q) v[q] = gmax_w(y2[co][q]);
             store_tile(desc + (size_t)g * CM2, co, v, writer, h);
         }
     }

@@ -318,9 +318,6 @@ __global__ __launch_bounds__(256) void knnd_wave_kernel(const float *__restrict_
 // order as the point distances and fl() is monotone (for p in the box,
 // |fl(q - p)| >= |fl(q - clamp(q, lo, hi))| per axis), and because every point
 // with d <= tau is still offered, so ties order by index as in the full scan.
-#ifndef HREG_SI_EXP
-#define HREG_SI_EXP 0  // tools/si_experiment.py: 1 no sort, 2 no boxes, 3 bbox + keys only
-#endif
 constexpr int SI_THREADS = 1024;
 constexpr int SI_LDSN = 16384;  // clouds up to this size sort through an LDS index list
 constexpr int SI_MAXN = 65536;  // larger ones (Model_V2's config 5) scatter straight to HBM
@@ -433,7 +430,7 @@ __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *
             S[i] = make_float4(P[id * 3], P[id * 3 + 1], P[id * 3 + 2], __int_as_float(id));
         }
     }
-    const int nblk = (HREG_SI_EXP & 2) ? 0 : (n + 63) / 64;
+    const int nblk = (n + 63) / 64;
     float4 *B = boxes + (size_t)c * (np / 64) * 2;
     for (int b = w; b < nblk; b += SI_THREADS / 64) {
         const int i = b * 64 + lane;
@@ -556,15 +553,6 @@ __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
     }
 }
 
-// HREG_KNND (A/B switch): 1 (default) = knnd_wave_kernel where it applies, 0 = the
-// LDS-staged 16-query blocks everywhere
-inline int knnd_mode() {
-    static const int m = [] {
-        const char *e = getenv("HREG_KNND");
-        return e ? atoi(e) : 1;
-    }();
-    return m;
-}
 
 template <int K>
 int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim, int k,
@@ -573,8 +561,7 @@ int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim,
     if (dim == 3) {
         hipLaunchKernelGGL((knn3_kernel<K>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
                            p2, b, n1, n2, dists, idx64, idx32, nn, k);
-    } else if (dim % 4 == 0 && !((reinterpret_cast<uintptr_t>(p1) | reinterpret_cast<uintptr_t>(p2)) & 15) &&
-               knnd_mode() == 1) {
+    } else if (dim % 4 == 0 && !((reinterpret_cast<uintptr_t>(p1) | reinterpret_cast<uintptr_t>(p2)) & 15)) {
         hipLaunchKernelGGL((knnd_wave_kernel<K>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
                            p2, b, n1, n2, dim, dists, idx64, idx32, nn, k);
     } else {

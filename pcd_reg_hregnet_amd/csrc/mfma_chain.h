@@ -5,13 +5,6 @@
 
 #include "common.h"
 
-// tools/l2_experiment.py builds variants: 1 = no epilogue / reductions (MFMA +
-// loads only), 2 = additionally no weight loads (MFMA issue structure only),
-// 3 = feature rows read without the kNN indirection (no dependent gather)
-#ifndef HREG_L2_EXP
-#define HREG_L2_EXP 0
-#endif
-
 namespace hreg_chain {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -55,15 +48,7 @@ constexpr int first_win() { return NSTEP < win_for<COUT_T>() ? NSTEP : win_for<C
 // base (SGPR pair) + the lane's byte offset.
 template <int GS>
 __device__ __forceinline__ void ldgroup(const gfloat *__restrict__ wf, int f0, int lane, float (&v)[GS]) {
-    if constexpr (HREG_L2_EXP == 2) {
-        // opaque register values: no load, nothing the compiler can hoist or fold
-#pragma unroll
-        for (int i = 0; i < GS; ++i) {
-            float x = __int_as_float(lane);
-            asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
-            v[i] = x;
-        }
-    } else if constexpr (GS == 4) {
+    if constexpr (GS == 4) {
         typedef float v4f __attribute__((ext_vector_type(4)));
         typedef __attribute__((address_space(1))) const v4f gv4f;
         const v4f t = *reinterpret_cast<const gv4f *>(wf + f0 * 64 + (unsigned)lane * 4);
@@ -131,7 +116,6 @@ __device__ __forceinline__ void mfma_pipe(const gfloat *__restrict__ wf, int lan
 
 template <int COUT_T>
 __device__ __forceinline__ void epilogue(const float *ab, int lane, f32x16 (&acc)[COUT_T]) {
-    if (HREG_L2_EXP) return;
     const int h = lane >> 5;
     constexpr int C = COUT_T * 32;
 #pragma unroll
@@ -262,22 +246,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
-// tools/b6_experiment.py timing variants (results wrong): 2 = weight pieces not loaded
-// (ld6 leaves its registers as they are), 5 = B not split (the hi piece for all three)
-#ifndef HREG_B6_EXP
-#define HREG_B6_EXP 0
-#endif
-
 // 8 fp32 values (one lane's chunk of B) -> hi / mid / lo packed bf16x8
 __device__ __forceinline__ void split8(const float (&x)[8], u32x4 (&o)[3]) {
-    if constexpr (HREG_B6_EXP == 5) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            o[0][i] = __builtin_amdgcn_perm(__float_as_uint(x[2 * i + 1]), __float_as_uint(x[2 * i]), 0x07060302u);
-        o[1] = o[0];
-        o[2] = o[0];
-        return;
-    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         uint32_t hb[2], mb[2], lb[2];
@@ -318,11 +288,6 @@ constexpr int CARRY6 = 8;  // output tiles of a call's first chunk carried betwe
 // (signed pointer arithmetic: a wave-uniform f stays an SGPR base, the lane a VGPR offset,
 // the piece an immediate -- no per-fragment VGPR address to hoist and spill)
 __device__ __forceinline__ void ld6(const gu32x4 *__restrict__ wt, int f, int lane, u32x4 (&o)[3]) {
-    if constexpr (HREG_B6_EXP == 2) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(o[p]));
-        return;
-    }
     const gu32x4 *fp = wt + f * 192;
 #pragma unroll
     for (int p = 0; p < 3; ++p) o[p] = fp[p * 64 + lane];
@@ -450,9 +415,6 @@ typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 #ifndef HREG_RING_ABUF
 #define HREG_RING_ABUF 2
 #endif
-#ifndef HREG_RING_EXP
-#define HREG_RING_EXP 0
-#endif
 
 template <int SLOT_TILES, int NWAVES>
 struct Ring6 {
@@ -490,11 +452,8 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
     (void)bn;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        // (HREG_RING_EXP timing experiments, results wrong: 1 = no wait and no barrier,
-        // 2 = no barrier)
-        if constexpr (HREG_RING_EXP != 1)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of this step landed
-        if constexpr (HREG_RING_EXP == 0) __syncthreads();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of this step landed
+        __syncthreads();
         const int cur = ring.step & 1;
         if (c + 1 < NCH)
             ring_fill<COUT_T>(ring, cur ^ 1, f, c + 1, lane);

@@ -51,9 +51,6 @@ using H512 = HCfg<512, 8, 1, 8>;  // 2 waves per SIMD: 128 VGPRs + AGPRs, short 
 // B6: the two layers on the bf16 matrix cores at fp32 accuracy (bf16x6, split_chain.h
 // pipe_lds6: each wave splits the B chunks it reads from LDS into bf16 pieces)
 template <class K, bool B6>
-#ifndef HREG_MLP_EXP
-#define HREG_MLP_EXP 0  // timing experiment (bench A/B only, results wrong): 1 skips the MFMA pipes
-#endif
 __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__restrict__ table,
                                                               const float *__restrict__ x, int ldx,
                                                               int G, int mode, float *__restrict__ out) {
@@ -121,7 +118,7 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
         else
             zero_tiles(y1);
         if constexpr (B6)
-{ if (!HREG_MLP_EXP) pipe_lds6<K::NCH, P, P>(wt, lane, g1, ChanB{A + j * LDSW, h}, y1, carry6, g2, ca6); }
+{ pipe_lds6<K::NCH, P, P>(wt, lane, g1, ChanB{A + j * LDSW, h}, y1, carry6, g2, ca6); }
         else
             pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f1, ChanB{A + j * LDSW, h}, y1, carry, f2, ca);
         if constexpr (B6)
@@ -139,7 +136,7 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
         else
             zero_tiles(y2);
         if constexpr (B6)
-{ if (!HREG_MLP_EXP) pipe_lds6<K::NCH, P, P>(wt, lane, g2, ChanB{A + j * LDSW, h}, y2, ca6, g1, carry6); }
+{ pipe_lds6<K::NCH, P, P>(wt, lane, g2, ChanB{A + j * LDSW, h}, y2, ca6, g1, carry6); }
         else
             pipe_lds<NS, P, P, WIN, WIN>(tb, lane, f2, ChanB{A + j * LDSW, h}, y2, ca, f1, carry);
         if constexpr (B6)

@@ -11,14 +11,7 @@ namespace hreg_split {
 
 using namespace hreg_chain;
 
-// tools/split_experiment.py: 1 = no workgroup barriers, 2 = B operand not read from
-// LDS (timing experiments only: results are wrong)
-#ifndef HREG_SPLIT_EXP
-#define HREG_SPLIT_EXP 0
-#endif
-__device__ __forceinline__ void tile_sync() {
-    if constexpr (HREG_SPLIT_EXP != 1) __syncthreads();
-}
+__device__ __forceinline__ void tile_sync() { __syncthreads(); }
 
 constexpr int SCARRY = 32;
 constexpr int SWIN = 16;  // k-steps per window (P <= 2 tiles: <= 32 fragments in flight)
@@ -47,16 +40,7 @@ __device__ __forceinline__ void pipe_lds(const gfloat *__restrict__ wf, int lane
 #pragma unroll
     for (int s0 = 0; s0 < WIN; s0 += GS) {
         float v[GS];
-        if constexpr (HREG_SPLIT_EXP == 2) {
-#pragma unroll
-            for (int i = 0; i < GS; ++i) {
-                float x = __int_as_float(lane);
-                asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
-                v[i] = x;
-            }
-        } else {
-            bl(s0, v);
-        }
+        bl(s0, v);
 #pragma unroll
         for (int i = 0; i < GS; ++i) bbuf[0][s0 + i] = v[i];
     }
@@ -73,16 +57,7 @@ __device__ __forceinline__ void pipe_lds(const gfloat *__restrict__ wf, int lane
                     for (int i = 0; i < GS; ++i) abuf[(w + 1) & 1][s0 + i][co] = v[i];
                 }
                 float v[GS];
-                if constexpr (HREG_SPLIT_EXP == 2) {
-#pragma unroll
-                    for (int i = 0; i < GS; ++i) {
-                        float x = __int_as_float(lane);
-                        asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
-                        v[i] = x;
-                    }
-                } else {
-                    bl((w + 1) * WIN + s0, v);
-                }
+                bl((w + 1) * WIN + s0, v);
 #pragma unroll
                 for (int i = 0; i < GS; ++i) bbuf[(w + 1) & 1][s0 + i] = v[i];
             }
