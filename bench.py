@@ -334,6 +334,39 @@ def cpu_baseline(budget_s: float = 30.0, batches=(1, PAIRS_PER_GPU), reps: int =
                       "section 2): 0.55 pairs/s at B=1, 0.50 at B=8"}
 
 
+def fps_latency(src, dst, m: int = 1024):
+    """The level-1 FPS (latency-bound, 1023 dependent iterations) against
+    its latency floor: hreg_debug_fps_stamps runs the product
+    kernel (same geometry) on the batch's 2B clouds with s_memtime stamps around each
+    phase of every iteration (cloud 0's workgroup): the distance scan (VALU work), and the
+    dependent exchange -- wave max + winner pick, the LDS hand-off + barrier, the block max
+    -- which no FPS on one CU can overlap: that exchange per iteration is the floor."""
+    from pcd_reg_hregnet_amd import _lib
+    pts = torch.cat([src, dst], 0).contiguous()
+    nb, n, _ = pts.shape
+    idx = torch.empty(nb, m, dtype=torch.int32, device=pts.device)
+    stamps = torch.zeros(6, dtype=torch.int64, device=pts.device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    _lib.call("hreg_debug_fps_stamps", nb, n, m, pts, None, idx, stamps, _lib.stream_handle())
+    ev[1].record()
+    torch.cuda.synchronize()
+    st = [int(x) for x in stamps.cpu()]
+    scan, pick, barrier, final, total, ticks = st
+    ghz = total / (ticks * 10.0) if ticks else 0.0  # s_memrealtime: 100 MHz
+    per_iter = lambda c: round(c / max(ghz, 1e-9) / 1e3 / (m - 1), 4)  # noqa: E731
+    return {"kernel": "fps_reg_kernel (level 1, 512 threads x 32 points per cloud)",
+            "clouds": nb, "points": n, "dependent_iterations": m - 1,
+            "launch_us": round(ev[0].elapsed_time(ev[1]) * 1e3, 1),
+            "us_per_iteration": per_iter(total),
+            "floor_us_per_iteration": per_iter(pick + barrier + final),
+            "scan_us_per_iteration": per_iter(scan),
+            "frac_of_floor": round((pick + barrier + final) / max(total, 1), 3),
+            "clock_ghz": round(ghz, 3),
+            "basis": "s_memtime phase stamps of cloud 0's workgroup; floor = the dependent "
+                     "exchange (wave max + pick, LDS barrier, block max) per iteration"}
+
+
 def shard_batch(rank: int, pairs: int, points: int):
     """Rank r's own pairs (seeded by rank: shards are disjoint, no data exchange)."""
     from pcd_reg_hregnet_amd import synthetic
@@ -731,6 +764,12 @@ def main():
                              "tflops": round(alg_fl / max(tot_ms, 1e-9) / 1e9, 2),
                              "executed_gflop_per_pair": round(tot_xf / args.steps / B / 1e9, 3),
                              "executed_tflops": round(tot_xf / max(tot_ms, 1e-9) / 1e9, 2)}}
+        fps = None
+        if not v2:
+            try:
+                fps = fps_latency(src, dst)
+            except Exception as e:  # a diagnostic must never sink the GPU number
+                fps = {"error": repr(e)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not v2:
             try:
@@ -760,6 +799,7 @@ def main():
                        "global_batch": B * world, "points": args.points,
                        "parallelism": f"dp{world} (pairs sharded, no collective)"},
             "roofline": roof,
+            "fps": fps,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
