@@ -336,35 +336,48 @@ def cpu_baseline(budget_s: float = 30.0, batches=(1, PAIRS_PER_GPU), reps: int =
 
 def fps_latency(src, dst, m: int = 1024):
     """The level-1 FPS (latency-bound, 1023 dependent iterations) against
-    its latency floor: hreg_debug_fps_stamps runs the product
-    kernel (same geometry) on the batch's 2B clouds with s_memtime stamps around each
-    phase of every iteration (cloud 0's workgroup): the distance scan (VALU work), and the
-    dependent exchange -- wave max + winner pick, the LDS hand-off + barrier, the block max
-    -- which no FPS on one CU can overlap: that exchange per iteration is the floor."""
+    a measured latency floor, on the batch's 2B clouds:
+    * the product kernel's launch time (HIP events) per dependent iteration;
+    * the same kernel with s_memtime stamps around each phase of every iteration (cloud 0's
+      workgroup): the distance scan vs the exchange (wave max + winner pick, LDS hand-off +
+      barrier, block max);
+    * the floor: the same 8-wave workgroup and exchange with 2 points per thread instead of
+      32 (hreg_debug_fps_floor, stamped alike), i.e. the dependent chain alone."""
     from pcd_reg_hregnet_amd import _lib
     pts = torch.cat([src, dst], 0).contiguous()
     nb, n, _ = pts.shape
+    st_ = _lib.stream_handle()
     idx = torch.empty(nb, m, dtype=torch.int32, device=pts.device)
-    stamps = torch.zeros(6, dtype=torch.int64, device=pts.device)
+    temp = torch.empty(nb, n, device=pts.device)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
-    _lib.call("hreg_debug_fps_stamps", nb, n, m, pts, None, idx, stamps, _lib.stream_handle())
+    _lib.call("hreg_furthest_point_sampling", nb, n, m, pts, temp, idx, None, st_)
     ev[1].record()
+    stamps = torch.zeros(6, dtype=torch.int64, device=pts.device)
+    _lib.call("hreg_debug_fps_stamps", nb, n, m, pts, None, idx, stamps, st_)
+    floor = torch.zeros(6, dtype=torch.int64, device=pts.device)
+    small = pts[:, :1024].contiguous()
+    _lib.call("hreg_debug_fps_floor", nb, m, small, idx, floor, st_)
     torch.cuda.synchronize()
-    st = [int(x) for x in stamps.cpu()]
-    scan, pick, barrier, final, total, ticks = st
+    scan, pick, barrier, final, total, ticks = [int(x) for x in stamps.cpu()]
+    f_total, f_ticks = int(floor[4]), int(floor[5])
     ghz = total / (ticks * 10.0) if ticks else 0.0  # s_memrealtime: 100 MHz
-    per_iter = lambda c: round(c / max(ghz, 1e-9) / 1e3 / (m - 1), 4)  # noqa: E731
+    per_iter = lambda c, g=ghz: round(c / max(g, 1e-9) / 1e3 / (m - 1), 4)  # noqa: E731
+    f_ghz = f_total / (f_ticks * 10.0) if f_ticks else 0.0
+    launch_us = ev[0].elapsed_time(ev[1]) * 1e3
     return {"kernel": "fps_reg_kernel (level 1, 512 threads x 32 points per cloud)",
             "clouds": nb, "points": n, "dependent_iterations": m - 1,
-            "launch_us": round(ev[0].elapsed_time(ev[1]) * 1e3, 1),
-            "us_per_iteration": per_iter(total),
-            "floor_us_per_iteration": per_iter(pick + barrier + final),
-            "scan_us_per_iteration": per_iter(scan),
-            "frac_of_floor": round((pick + barrier + final) / max(total, 1), 3),
+            "launch_us": round(launch_us, 1),
+            "us_per_iteration": round(launch_us / (m - 1), 4),
+            "stamped_us_per_iteration": per_iter(total),
+            "stamped_scan_us_per_iteration": per_iter(scan),
+            "stamped_exchange_us_per_iteration": per_iter(pick + barrier + final),
+            "floor_us_per_iteration": per_iter(f_total, f_ghz),
+            "frac_floor_over_kernel": round(per_iter(f_total, f_ghz) / max(per_iter(total), 1e-9), 3),
             "clock_ghz": round(ghz, 3),
-            "basis": "s_memtime phase stamps of cloud 0's workgroup; floor = the dependent "
-                     "exchange (wave max + pick, LDS barrier, block max) per iteration"}
+            "basis": "floor = the same workgroup and per-iteration exchange with 2 instead of 32 "
+                     "points per thread (hreg_debug_fps_floor); stamped figures carry the "
+                     "s_memtime overhead on both sides"}
 
 
 def shard_batch(rank: int, pairs: int, points: int):

@@ -619,10 +619,14 @@ int hreg_nbr_head6s(const float *table, const float *desc, const int32_t *gidx, 
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */
 int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,
                           int32_t *idx, uint64_t *stamps, void *stream);
+/* Latency floor of the level-1 FPS geometry: the same 8-wave workgroup and per-iteration
+ * exchange, 2 points per thread (n = 1024); points [b][1024][3], stamps[6] as above. */
+int hreg_debug_fps_floor(int b, int m, const float *points, int32_t *idx, uint64_t *stamps,
+                         void *stream);
 
 /* Reads the device status word (HREG_STATUS_* bits raised by kernels since the last
- * clear) into *status after the device work issued so far; clear != 0 resets it.
- * Synchronous (a device-to-host copy). */
+ * clear) into *status; clear != 0 takes it atomically (read and reset in one step).
+ * Synchronous: waits for all work on the device (every stream) first. */
 int hreg_device_status(int *status, int clear);
 
 /* Diagnostic: the multi-workgroup FPS kernel forced on any n with at most polls_max

@@ -113,6 +113,7 @@ _SIGS = {
     "hreg_rowdot_bwd": [_vp, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_relu_bwd": [_vp, _vp, ctypes.c_size_t, _vp, _vp],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_debug_fps_floor": [_i, _i, _vp, _vp, _vp, _vp],
     "hreg_debug_fps_cluster": [_i, _i, _i, _vp, _vp, _vp, _vp, _i, ctypes.c_uint, _vp],
     "hreg_device_status": [ctypes.POINTER(ctypes.c_int), _i],
     "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],

@@ -611,6 +611,20 @@ extern "C" int hreg_debug_fps_stamps(int b, int n, int m, const float *points, c
     return HREG_OK;
 }
 
+// Diagnostic: the latency floor of the level-1 FPS geometry -- the same 512-thread,
+// 8-wave workgroup, per-iteration exchange and barrier as the n = 16384 kernel
+// (fps_reg_kernel<512, 2, 16>), but 2 points per thread (n = 1024), so an iteration is the
+// dependent chain (wave max, winner pick, LDS hand-off + barrier, block max) with almost no
+// scan.  stamps as hreg_debug_fps_stamps.  points [b][1024][3].
+extern "C" int hreg_debug_fps_floor(int b, int m, const float *points, int32_t *idx, uint64_t *stamps,
+                                    void *stream) {
+    if (b <= 0 || m <= 0 || !points || !idx || !stamps) return HREG_ERR_INVALID;
+    hipLaunchKernelGGL((fps_reg_kernel<512, 2, 1, false, true>), dim3(b), dim3(512), 0, as_stream(stream), points,
+                       nullptr, nullptr, idx, nullptr, 1024, m, 1024, 10, __builtin_huge_valf(), stamps);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
 extern "C" int hreg_furthest_point_sampling(int b, int n, int m, const float *points,
                                             float *temp, int32_t *idx, float *sampled_xyz,
                                             void *stream) {
