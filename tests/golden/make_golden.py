@@ -303,13 +303,19 @@ def model_fixture(HRegNet, pu, src: np.ndarray, dst: np.ndarray, sd: dict, args=
         out[f"R{3 - i}_64"] = R.numpy()
         out[f"t{3 - i}_64"] = t.numpy()
     for lv in (1, 2, 3):
-        out[f"corres_{lv}_64"] = r64[f"src_xyz_corres_{lv}"].numpy()
-        out[f"weights_{lv}_64"] = r64[f"src_dst_weights_{lv}"].numpy()
+        out[f"corres_{lv}_64"] = _f32(r64[f"src_xyz_corres_{lv}"].numpy())
+        out[f"weights_{lv}_64"] = _f32(r64[f"src_dst_weights_{lv}"].numpy())
         for part in ("src", "dst"):
             f = r64[f"{part}_feats"]
             for q in ("xyz", "sigmas", "desc"):
-                out[f"{part}_{q}_{lv}_64"] = f[f"{q}_{lv}"].numpy()
+                out[f"{part}_{q}_{lv}_64"] = _f32(f[f"{q}_{lv}"].numpy())
     return out
+
+
+def _f32(x):
+    """float64 replay outputs are stored as fp32: the rounding (6e-8 relative) is far below
+    every spread and bar they serve (tests/parity.py), at half the fixture size"""
+    return np.asarray(x, np.float64).astype(np.float32)
 
 
 def _replay64(Model, pu, sd, src, dst, seed=None, args=None):
@@ -393,12 +399,12 @@ def model_v2_fixture(Model_V2, pu, src: np.ndarray, dst: np.ndarray, sd: dict, s
         out[f"t{3 - i}_64"] = t.numpy()
     for key in ("src_xyz_corres_3", "src_xyz_corres_2", "src_xyz_corres_1", "src_xyz_2_trans",
                 "src_dst_feats_2", "src_dst_weights_2"):
-        out[key + "_64"] = r64[key].numpy()
+        out[key + "_64"] = _f32(r64[key].numpy())
     for lv in (1, 2, 3):
         for part in ("src", "dst"):
             f = r64[f"{part}_feats"]
             for q in ("xyz", "sigmas", "desc"):
-                out[f"{part}_{q}_{lv}_64"] = f[f"{q}_{lv}"].numpy()
+                out[f"{part}_{q}_{lv}_64"] = _f32(f[f"{q}_{lv}"].numpy())
     return out
 
 
