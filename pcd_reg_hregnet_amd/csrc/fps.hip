@@ -120,6 +120,10 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         // invalid slots can never be selected: d2 = -inf never reaches the max
         PT[s / 2][s % 2] = ok ? 1e10f : -__builtin_huge_valf();
     }
+    // opaque: pick_slot must read its coordinates from these pairs, not from the loaded
+    // scalars (otherwise every point stays live twice: +96 VGPRs at 32 slots)
+#pragma unroll
+    for (int s = 0; s < S2; ++s) asm volatile("" : "+v"(PX[s]), "+v"(PY[s]), "+v"(PZ[s]));
 
     float x1 = P[0], y1 = P[1], z1 = P[2];
     if (tid == 0) {
@@ -383,6 +387,8 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
             PW[s / 2][s % 2] = WEIGHTED ? W[kk] : 1.0f;
             PT[s / 2][s % 2] = ok ? 1e10f : -__builtin_huge_valf();
         }
+#pragma unroll
+        for (int s = 0; s < S2; ++s) asm volatile("" : "+v"(PX[s]), "+v"(PY[s]), "+v"(PZ[s]));  // (fps_reg_kernel)
         float x1 = P[0], y1 = P[1], z1 = P[2];
         if (p == 0 && lane == 0) {
             idx_out[(size_t)cloud * m] = 0;
@@ -537,6 +543,42 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     }
 }
 
+// Co-residency of the cluster kernel's spinning participants.  A
+// cluster makes progress once all its NP single-wave workgroups are resident; waves of
+// other (finite) kernels always drain, so it can only stall if spinning waves alone fill
+// every wave slot the kernel's registers allow.  This process runs at most
+// GPU_MAX_HW_QUEUES kernels at once (HIP's hardware queues, default 4; kernels sharing a
+// queue run in order), so a launch spins at most (resident waves of this kernel on the
+// whole device) / queues waves -- every concurrent cluster launch together fits on the
+// chip at once -- and never more than 256.  The budget is queried once per variant
+// (occupancy API x CU count); if it cannot hold one cluster, the launch uses the
+// non-spinning fps_mem_kernel.  The poll bound + HREG_STATUS_FPS_TIMEOUT stay the
+// backstop (other processes on the same device are outside this bound).
+int cluster_wave_budget(int S, bool weighted) {
+    static int cache[2][3] = {{-1, -1, -1}, {-1, -1, -1}};
+    const int si = S == 8 ? 0 : S == 16 ? 1 : 2;
+    int &c = cache[weighted ? 1 : 0][si];
+    if (c >= 0) return c;
+    int dev = 0, cus = 0, per_cu = 0;
+    const void *fn = nullptr;
+#define HREG_FPS_CLK(SS, WW) \
+    if (S == SS && weighted == WW) fn = reinterpret_cast<const void *>(&fps_cluster_kernel<SS, WW>);
+    HREG_FPS_CLK(8, false) HREG_FPS_CLK(16, false) HREG_FPS_CLK(32, false)
+    HREG_FPS_CLK(8, true) HREG_FPS_CLK(16, true) HREG_FPS_CLK(32, true)
+#undef HREG_FPS_CLK
+    if (!fn || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return c = 0;
+    }
+    const char *q = getenv("GPU_MAX_HW_QUEUES");
+    int queues = q ? atoi(q) : 4;
+    if (queues < 1) queues = 4;
+    const long budget = (long)per_cu * cus / queues;
+    return c = (int)(budget < 256 ? budget : 256);
+}
+
 template <bool WEIGHTED>
 int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *temp, int32_t *idx,
                float *sampled, hipStream_t st, uint32_t polls_max = FPS_CL_POLLS, int stall = -1,
@@ -561,11 +603,10 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
     for (int s : {8, 16, 32})
         if (ranks <= (long)FPS_CL_MAXP * 64 * s) { S = s; break; }
     const size_t slot_bytes = (size_t)2 * FPS_CL_MAXP * sizeof(SyncSlot);
-    if (S && (size_t)n * sizeof(float) >= slot_bytes) {
-        const int NP = (int)((ranks + 64L * S - 1) / (64L * S));
-        // <= 256 spinning waves per launch: with a few launches in flight on other
-        // streams (GraphPipeline lanes) every launch still fits on the chip at once
-        const int clusters = b < 256 / NP ? b : 256 / NP;
+    const int NP = S ? (int)((ranks + 64L * S - 1) / (64L * S)) : 0;
+    const int spin = S ? cluster_wave_budget(S, WEIGHTED) : 0;
+    if (S && (size_t)n * sizeof(float) >= slot_bytes && spin >= NP) {
+        const int clusters = b < spin / NP ? b : spin / NP;
         SyncSlot *slots = reinterpret_cast<SyncSlot *>(temp);
         if (hipMemsetAsync(slots, 0, (size_t)b * slot_bytes, st) != hipSuccess) return HREG_ERR_LAUNCH;
         // valid outputs even if the exchange times out (participant 0 writes; see above)

@@ -61,7 +61,6 @@ B6_L3 = os.environ.get("HREG_B6_L3", "1") != "0"
 B6_GEMM = os.environ.get("HREG_B6_GEMM", "1") != "0"
 # every addend-free GEMM (the precomputed first-layer blocks, the batched descriptor
 # products, the cosine similarities) on hreg_gemm6 (bf16x6, 128 x 128 tiles)
-B6_SMALL_GEMM = os.environ.get("HREG_B6_SMALL_GEMM", "0") != "0"
 B6_MLP = os.environ.get("HREG_B6_MLP", "1") != "0"  # mlp heads on hreg_mlp_head6
 # CoarseReg convs_1 (split first layer) + attention in one launch (coarse6.hip, bf16x6)
 FUSED_COARSE = os.environ.get("HREG_FUSED_COARSE", "1") != "0"
@@ -599,7 +598,7 @@ def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=(), b6=Fa
     g.out = out.data_ptr()
     g.ldo = out.shape[-1]
     g.out_batch_stride = 0
-    if ((b6 and B6_GEMM) or B6_SMALL_GEMM) and not adds:
+    if b6 and B6_GEMM and not adds:
         _lib.gemm6(g)
     else:
         _lib.gemm(g)
@@ -630,7 +629,7 @@ def _gemm_batched_desc(lin: Lin, desc3, rows: int, C: int, out, x1=None):
     g.out = out.data_ptr()
     g.ldo = N
     g.out_batch_stride = rows * N
-    (_lib.gemm6 if B6_SMALL_GEMM else _lib.gemm)(g)
+    _lib.gemm(g)
     return out
 
 
@@ -653,7 +652,7 @@ def cosine_gemm(a, b, na, nb_, nb: int, n1: int, n2: int, C: int, out):
     g.out = out.data_ptr()
     g.ldo = n2
     g.out_batch_stride = n1 * n2
-    (_lib.gemm6 if B6_SMALL_GEMM else _lib.gemm)(g)
+    _lib.gemm(g)
     return out
 
 
