@@ -343,15 +343,17 @@ int hreg_bn_apply(const float *y, int R, int C, const float *mean, const float *
                   const float *gamma, const float *beta, int relu, float *out, void *stream);
 /* backward of hreg_bn_apply given dout: dgamma, dbeta [C], dy [R][C] (the
  * batch-statistics BN input gradient).  ReLU mask: out > 0 when out is given, else
- * recomputed bit-identically from y, gamma and beta (one fewer [R][C] stream). */
+ * recomputed bit-identically from y, gamma and beta (one fewer [R][C] stream).
+ * accumulate != 0: dgamma / dbeta are added to (a parameter's .grad over its uses). */
 int hreg_bn_backward(const float *dout, const float *out, const float *y, int R, int C,
                      const float *mean, const float *invstd, const float *gamma, const float *beta,
-                     int relu, void *ws, float *dy, float *dgamma, float *dbeta, void *stream);
+                     int relu, void *ws, float *dy, float *dgamma, float *dbeta, int accumulate,
+                     void *stream);
 /* running = (1 - momentum) * running + momentum * batch (nn.BatchNorm's momentum 0.1) */
 int hreg_bn_running_update(const float *mean, const float *var_unbiased, int C, float momentum,
                            float *running_mean, float *running_var, void *stream);
-/* out[c] = sum_r x[r][c] (conv bias gradients) */
-int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, void *stream);
+/* out[c] = sum_r x[r][c] (conv bias gradients); accumulate != 0: out[c] += the sum */
+int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, int accumulate, void *stream);
 /* out[n][k] = beta * out[n][k] + sum_r A[r][n] * B[r][k] (dW = dY^T X), fp32 MFMA,
  * ws = hreg_gemm_tn_ws_bytes(R, N, K) bytes */
 size_t hreg_gemm_tn_ws_bytes(int R, int N, int K);

@@ -118,9 +118,9 @@ _SIGS = {
     "hreg_device_status": [ctypes.POINTER(ctypes.c_int), _i],
     "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
     "hreg_bn_apply": [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp],
-    "hreg_bn_backward": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_bn_backward": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp],
     "hreg_bn_running_update": [_vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp],
-    "hreg_col_sum": [_vp, _i, _i, _vp, _vp, _vp],
+    "hreg_col_sum": [_vp, _i, _i, _vp, _vp, _i, _vp],
     "hreg_gemm_tn": [_vp, _i, _vp, _i, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp],
     "hreg_transpose": [_vp, _i, _i, _vp, _vp],
     "hreg_adam_step": [_vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_float, ctypes.c_float,

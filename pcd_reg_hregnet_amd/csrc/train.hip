@@ -116,10 +116,13 @@ __global__ __launch_bounds__(CR_THREADS) void col_reduce_kernel(
 // splits l, l+32, ... in order, then the 32 lanes in order), then MODE's finalisation
 constexpr int FIN_COLS = 8, FIN_LANES = 32;
 
+// acc0 / acc1 (MODE 1, 2; optional): the totals are also added to these (a parameter's
+// .grad accumulating over its uses, as autograd's accumulation would: one fp32 add each)
 template <int MODE>
 __global__ __launch_bounds__(FIN_COLS * FIN_LANES) void col_finalize_kernel(
     const double *__restrict__ partial, int S, int R, int C, float eps, float *__restrict__ o0,
-    float *__restrict__ o1, float *__restrict__ o2) {
+    float *__restrict__ o1, float *__restrict__ o2, float *__restrict__ acc0 = nullptr,
+    float *__restrict__ acc1 = nullptr) {
     __shared__ double s0[FIN_COLS * FIN_LANES], s1[FIN_COLS * FIN_LANES];
     const int cl = threadIdx.x % FIN_COLS, sl = threadIdx.x / FIN_COLS;
     const int c = blockIdx.x * FIN_COLS + cl;
@@ -152,8 +155,11 @@ __global__ __launch_bounds__(FIN_COLS * FIN_LANES) void col_finalize_kernel(
     } else if (MODE == 1) {
         o0[c] = (float)b;  // dgamma = sum g * xhat
         o1[c] = (float)a;  // dbeta = sum g
+        if (acc0) acc0[c] = fadd_rn(acc0[c], (float)b);
+        if (acc1) acc1[c] = fadd_rn(acc1[c], (float)a);
     } else {
-        o0[c] = (float)a;
+        if (o0) o0[c] = (float)a;
+        if (acc0) acc0[c] = fadd_rn(acc0[c], (float)a);
     }
 }
 
@@ -437,10 +443,16 @@ static int cr_blocks(int C) {
 // up to 4096 (a wave keeps only 16 loads in flight: more workgroups, not longer loops)
 static int cr_splits(int R, int C, bool bwd) { return splits_for(R, cr_blocks(C), 256, 2048, bwd ? 4096 : 1024); }
 
-extern "C" size_t hreg_col_reduce_ws_bytes(int R, int C) {
-    if (R <= 0 || C <= 0) return 0;
+// partials [S][C][2] doubles, then 2C floats (hreg_bn_backward's own dgamma / dbeta when
+// it accumulates into the caller's)
+static size_t cr_partial_bytes(int R, int C) {
     const int S = cr_splits(R, C, true);  // (>= every mode's)
     return (size_t)S * C * 2 * sizeof(double);
+}
+
+extern "C" size_t hreg_col_reduce_ws_bytes(int R, int C) {
+    if (R <= 0 || C <= 0) return 0;
+    return cr_partial_bytes(R, C) + (size_t)2 * C * sizeof(float);
 }
 
 extern "C" int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, float *mean,
@@ -479,7 +491,7 @@ extern "C" int hreg_bn_apply(const float *y, int R, int C, const float *mean, co
 extern "C" int hreg_bn_backward(const float *dout, const float *out, const float *y, int R, int C,
                                 const float *mean, const float *invstd, const float *gamma,
                                 const float *beta, int relu, void *ws, float *dy, float *dgamma,
-                                float *dbeta, void *stream) {
+                                float *dbeta, int accumulate, void *stream) {
     if (!dout || !y || !mean || !invstd || !gamma || !ws || !dy || !dgamma || !dbeta || R <= 0 ||
         C <= 0 || (relu && !out && !beta))
         return HREG_ERR_INVALID;
@@ -490,9 +502,19 @@ extern "C" int hreg_bn_backward(const float *dout, const float *out, const float
     hipLaunchKernelGGL(red, dim3(cb, S), dim3(CR_THREADS), 0, st, dout, out, y, mean, invstd, gamma, beta, relu, R,
                        C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
+    // accumulate: this call's dgamma / dbeta (read by the dy pass) go to the workspace tail
+    // and are added to the caller's
+    float *dg = dgamma, *db = dbeta;
+    if (accumulate) {
+        dg = reinterpret_cast<float *>(static_cast<char *>(ws) + cr_partial_bytes(R, C));
+        db = dg + C;
+    }
     hipLaunchKernelGGL(col_finalize_kernel<1>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
-                       (const double *)ws, S, R, C, 0.f, dgamma, dbeta, nullptr);
+                       (const double *)ws, S, R, C, 0.f, dg, db, nullptr, accumulate ? dgamma : nullptr,
+                       accumulate ? dbeta : nullptr);
     HREG_CHECK_LAUNCH();
+    dgamma = dg;
+    dbeta = db;
     const size_t total = (size_t)R * C;
     if (C % 4 == 0 && C <= BN4_MAXC && total / 4 < (size_t)INT32_MAX &&
         !((reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(out) |
@@ -518,7 +540,8 @@ extern "C" int hreg_bn_running_update(const float *mean, const float *var_unbias
     return HREG_OK;
 }
 
-extern "C" int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, void *stream) {
+extern "C" int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, int accumulate,
+                            void *stream) {
     if (!x || !ws || !out || R <= 0 || C <= 0) return HREG_ERR_INVALID;
     const int cb = cr_blocks(C), S = splits_for(R, cb, 256);
     const int rps = (R + S - 1) / S;
@@ -527,7 +550,8 @@ extern "C" int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, 
                        nullptr, nullptr, nullptr, nullptr, 0, R, C, rps, cr_width_log2(C), (double *)ws);
     HREG_CHECK_LAUNCH();
     hipLaunchKernelGGL(col_finalize_kernel<2>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
-                       (const double *)ws, S, R, C, 0.f, out, nullptr, nullptr);
+                       (const double *)ws, S, R, C, 0.f, accumulate ? nullptr : out, nullptr, nullptr,
+                       accumulate ? out : nullptr);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

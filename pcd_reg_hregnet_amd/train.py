@@ -62,13 +62,15 @@ def bn_stats(y: torch.Tensor, eps: float = BN_EPS):
     return mean, invstd, var
 
 
-def gemm_tn(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
-    """A [R][N], B [R][K] -> A^T B [N][K] (fp32 MFMA, deterministic split-R reduction)."""
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, into: torch.Tensor | None = None) -> torch.Tensor:
+    """A [R][N], B [R][K] -> A^T B [N][K] (fp32 MFMA, deterministic split-R reduction);
+    into: added to that [N][K] tensor instead (returned)."""
     R, N = A.shape
     K = B.shape[1]
-    out = torch.empty(N, K, device=A.device)
+    out = into if into is not None else torch.empty(N, K, device=A.device)
     ws = _ws(_lib.load().hreg_gemm_tn_ws_bytes(R, N, K), A.device)
-    _lib.call("hreg_gemm_tn", A, A.stride(0), B, B.stride(0), R, N, K, 0.0, ws, out, _stream())
+    _lib.call("hreg_gemm_tn", A, A.stride(0), B, B.stride(0), R, N, K,
+              1.0 if into is not None else 0.0, ws, out, _stream())
     return out
 
 
@@ -79,11 +81,28 @@ def transpose(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def col_sum(x: torch.Tensor) -> torch.Tensor:
+def col_sum(x: torch.Tensor, into: torch.Tensor | None = None) -> torch.Tensor:
+    """column sums of x [R][C]; into: added to that tensor instead (returned)"""
     R, C = x.shape
-    out = torch.empty(C, device=x.device)
-    _lib.call("hreg_col_sum", x, R, C, col_reduce_ws(R, C, x.device), out, _stream())
+    out = into if into is not None else torch.empty(C, device=x.device)
+    _lib.call("hreg_col_sum", x, R, C, col_reduce_ws(R, C, x.device), out,
+              1 if into is not None else 0, _stream())
     return out
+
+
+DIRECT_GRAD = True  # (A/B switch: False returns every parameter gradient to autograd)
+
+
+def _grad_slot(p):
+    """p.grad when the backward may add to it in place (autograd's own accumulation into
+    an existing .grad: the flat gradient bucket is attached and zeroed every step), else
+    None (return the gradient to autograd)"""
+    if p is None or not p.requires_grad or not DIRECT_GRAD:
+        return None
+    g = p.grad
+    if g is None or not g.is_contiguous() or g.dtype != torch.float32:
+        return None
+    return g
 
 
 _CONST = {}
@@ -110,7 +129,8 @@ def _plain_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None) ->
 
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, bias, gamma, beta, running_mean, running_var, relu, momentum, eps):
+    def forward(ctx, x, W, bias, gamma, beta, running_mean, running_var, relu, momentum, eps,
+                wparam=None):
         R = x.shape[0]
         y = _plain_gemm(x, W, bias)
         mean, invstd, var = bn_stats(y, eps)
@@ -124,6 +144,9 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.save_for_backward(x, W, y, mean, invstd, gamma, beta)
         ctx.relu = relu
         ctx.has_bias = bias is not None
+        # the parameter objects whose .grad the backward may add to directly (W is usually
+        # a [N][K] view of the conv weight; bias / gamma / beta are the parameters)
+        ctx.params = (wparam, bias, gamma, beta)
         return out
 
     @staticmethod
@@ -133,24 +156,46 @@ class _ConvBNAct(torch.autograd.Function):
         R, C = y.shape
         dev = y.device
         dy = torch.empty_like(y)
-        dgamma = torch.empty(C, device=dev)
-        dbeta = torch.empty(C, device=dev)
+        # parameter gradients straight into an existing .grad (the gradient bucket): the
+        # same fp32 sums autograd's accumulation would make (g_src + g_dst, added to the
+        # zeroed .grad), without its two elementwise additions per parameter and use
+        wp, bp, gp, btp = ctx.params
+        gw = _grad_slot(wp) if ctx.needs_input_grad[1] else None
+        gb = _grad_slot(bp) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gg, gbt = _grad_slot(gp), _grad_slot(btp)
+        acc = gg is not None and gbt is not None and ctx.needs_input_grad[3] and ctx.needs_input_grad[4]
+        dgamma = gg if acc else torch.empty(C, device=dev)
+        dbeta = gbt if acc else torch.empty(C, device=dev)
         # the ReLU mask is recomputed from y (bit-identical to bn_apply's): out is not read
         _lib.call("hreg_bn_backward", dout, None, y, R, C, mean, invstd, gamma, beta,
-                  1 if ctx.relu else 0, col_reduce_ws(R, C, dev), dy, dgamma, dbeta, _stream())
-        dW = gemm_tn(dy, x) if ctx.needs_input_grad[1] else None
-        dbias = col_sum(dy) if ctx.has_bias and ctx.needs_input_grad[2] else None
+                  1 if ctx.relu else 0, col_reduce_ws(R, C, dev), dy, dgamma, dbeta,
+                  1 if acc else 0, _stream())
+        dW = None
+        if ctx.needs_input_grad[1]:
+            if gw is not None:
+                gemm_tn(dy, x, into=gw.view(W.shape))
+            else:
+                dW = gemm_tn(dy, x)
+        dbias = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            if gb is not None:
+                col_sum(dy, into=gb)
+            else:
+                dbias = col_sum(dy)
         dx = _plain_gemm(dy, transpose(W), None) if ctx.needs_input_grad[0] else None
-        return dx, dW, dbias, dgamma, dbeta, None, None, None, None, None
+        if acc:
+            dgamma = dbeta = None
+        return dx, dW, dbias, dgamma, dbeta, None, None, None, None, None, None
 
 
 def conv_bn_act(x, W, bias, gamma, beta, running_mean=None, running_var=None, relu=True,
-                momentum=BN_MOMENTUM, eps=BN_EPS):
+                momentum=BN_MOMENTUM, eps=BN_EPS, wparam=None):
     """Train-mode Conv1x1 + BatchNorm + [ReLU] over rows: x [R][K] (K % 4 == 0),
     W [N][K] -> [R][N].  Matches nn.Conv1d/Conv2d(k=1) + nn.BatchNorm*d(train) + nn.ReLU
-    on the same rows (every position of the batch is a row)."""
+    on the same rows (every position of the batch is a row).  wparam: the parameter W is a
+    view of (its .grad, like bias' / gamma's / beta's, is added to in place when present)."""
     return _ConvBNAct.apply(x.contiguous(), W, bias, gamma, beta, running_mean, running_var,
-                            relu, momentum, eps)
+                            relu, momentum, eps, wparam if wparam is not None else W)
 
 
 class ConvBNAct(torch.nn.Module):

@@ -519,7 +519,7 @@ def conv_bn(x, conv, bn, relu=True):
     """Conv(1x1) + train-mode BatchNorm (+ ReLU) over rows (num_batches_tracked += 1)."""
     W = conv.weight.view(conv.out_channels, -1)
     y = train.conv_bn_act(x, W, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                          relu, momentum=bn.momentum, eps=bn.eps)
+                          relu, momentum=bn.momentum, eps=bn.eps, wparam=conv.weight)
     if bn.num_batches_tracked is not None:
         _BN_COUNTERS.append(bn.num_batches_tracked)
     return y

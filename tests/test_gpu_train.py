@@ -56,6 +56,42 @@ def test_conv_bn_act_matches_torch(R, K, N, bias, relu):
         torch.testing.assert_close(bl.grad, tb.grad, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("bias", [False, True])
+def test_conv_bn_act_accumulates_into_existing_grad_bitwise(bias):
+    """A parameter used twice (src and dst pass) with its .grad pre-attached and zeroed
+    (the trainer's gradient bucket): the backward adds dW / dbias / dgamma / dbeta into
+    .grad itself (train._grad_slot) -- bitwise the gradients autograd's own accumulation
+    gives when .grad starts as None."""
+    from pcd_reg_hregnet_amd.train import conv_bn_act
+    g = torch.Generator(device="cpu").manual_seed(7)
+    R, K, N = 8192, 36, 64
+    xs = [(torch.randn(R, K, generator=g) * 2).cuda() for _ in range(2)]
+    Gs = [torch.randn(R, N, generator=g).cuda() for _ in range(2)]
+    W4 = (torch.randn(N, K, 1, 1, generator=g) / K ** 0.5).cuda()
+    b = torch.randn(N, generator=g).cuda()
+    gamma = (torch.rand(N, generator=g) + 0.5).cuda()
+    beta = torch.randn(N, generator=g).cuda()
+    grads = []
+    for attach in (False, True):
+        ps = [t.clone().requires_grad_(True) for t in (W4, b, gamma, beta)]
+        if attach:
+            for p in ps:
+                p.grad = torch.zeros_like(p)
+        loss = 0
+        for x, G in zip(xs, Gs):
+            rm, rv = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+            out = conv_bn_act(x, ps[0].view(N, K), ps[1] if bias else None, ps[2], ps[3], rm, rv,
+                              True, wparam=ps[0])
+            loss = loss + (out * G).sum()
+        loss.backward()
+        grads.append([p.grad.clone() if p.grad is not None else None for p in ps])
+    for a, r, name in zip(grads[1], grads[0], ("dW", "dbias", "dgamma", "dbeta")):
+        if name == "dbias" and not bias:
+            assert r is None and not a.abs().max() > 0
+            continue
+        assert torch.equal(a, r), name
+
+
 def test_gemm_tn_and_transpose():
     from pcd_reg_hregnet_amd.train import gemm_tn, transpose
     g = torch.Generator(device="cpu").manual_seed(3)

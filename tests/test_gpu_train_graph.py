@@ -554,7 +554,7 @@ def test_train_descriptor_backward_replay():
     caps = []
     orig_kl = train_graph.keypoint_level
 
-    def kl(det, desc, lvl, xyz, feats, weights, hook=None, part="src"):
+    def kl(det, desc, lvl, xyz, feats, weights, hook=None, part="src", use_fps=True):
         rec = {"lvl": lvl}
         o_seq, o_cat = train_graph.seq_convs, train_graph.cat_rows
 
@@ -570,7 +570,7 @@ def test_train_descriptor_backward_replay():
 
         train_graph.seq_convs, train_graph.cat_rows = seq, cat
         try:
-            out = orig_kl(det, desc, lvl, xyz, feats, weights, hook, part)
+            out = orig_kl(det, desc, lvl, xyz, feats, weights, hook, part, use_fps)
         finally:
             train_graph.seq_convs, train_graph.cat_rows = o_seq, o_cat
         out[3].retain_grad()

@@ -33,8 +33,8 @@ for R, C in ((524288, 32), (524288, 64), (262144, 128)):
     out = torch.empty_like(y)
     s = t_us(lambda: _lib.call("hreg_bn_stats", y, R, C, 1e-5, ws, mean, invstd, var, st))
     ap = t_us(lambda: _lib.call("hreg_bn_apply", y, R, C, mean, invstd, g, b, 1, out, st))
-    bw = t_us(lambda: _lib.call("hreg_bn_backward", dout, None, y, R, C, mean, invstd, g, b, 1, ws, dy, dg, db, st))
-    bwo = t_us(lambda: _lib.call("hreg_bn_backward", dout, out, y, R, C, mean, invstd, g, b, 1, ws, dy, dg, db, st))
+    bw = t_us(lambda: _lib.call("hreg_bn_backward", dout, None, y, R, C, mean, invstd, g, b, 1, ws, dy, dg, db, 0, st))
+    bwo = t_us(lambda: _lib.call("hreg_bn_backward", dout, out, y, R, C, mean, invstd, g, b, 1, ws, dy, dg, db, 0, st))
     mb = R * C * 4 / 1e6
     print(f"R={R} C={C} ({mb:.0f} MB/stream): stats {s:.1f} us, apply {ap:.1f}, backward {bw:.1f} "
           f"(with out {bwo:.1f})", flush=True)
