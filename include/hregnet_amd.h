@@ -338,6 +338,14 @@ size_t hreg_col_reduce_ws_bytes(int R, int C);
 /* per channel of y [R][C]: mean, invstd = 1/sqrt(var_biased + eps), var_unbiased (may be NULL) */
 int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, float *mean, float *invstd,
                   float *var_unbiased, void *stream);
+/* Tall-skinny conv GEMM of the training step (csrc/ts_gemm.hip): out[r][n] = act(scale[n] *
+ * sum_k A[r][k] W'[n][k] + shift[n]) with W' = W [N][K] (w_trans 0) or the transpose of
+ * W [K][N] (w_trans 1); scale / shift may be NULL (1 / 0), act = ReLU if relu.  The same
+ * fp32 sums as hreg_gemm (same k-order).  K, N, lda, ldo multiples of 4, 16-byte aligned
+ * pointers; hreg_ts_gemm_supported(R, K, N) != 0 when W' fits the kernel's LDS. */
+int hreg_ts_gemm_supported(int R, int K, int N);
+int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
+                 const float *scale, const float *shift, int relu, float *out, int ldo, void *stream);
 /* out = act(gamma * (y - mean) * invstd + beta), act = ReLU if relu (out may alias y) */
 int hreg_bn_apply(const float *y, int R, int C, const float *mean, const float *invstd,
                   const float *gamma, const float *beta, int relu, float *out, void *stream);

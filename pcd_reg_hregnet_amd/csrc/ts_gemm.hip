@@ -1,0 +1,229 @@
+// ts_gemm.hip -- tall-skinny fp32 GEMM for the training step's 1x1 convs.
+//
+// out[r][n] = act(scale[n] * sum_k A[r][k] W'[n][k] + shift[n]) for R in the 10^5..10^6 rows of
+// the level-1 / level-2 grouped rows and K, N <= a few hundred channels (the conv forward
+// y = x W^T of every train-mode layer and its input gradient dx = dy W, train.py; reference
+// layers.py:115-130, 183-198 in .train()).  hreg_gemm stages both operands through LDS tile
+// by tile and ran these shapes at 2-3 TB/s; here a workgroup keeps the whole W' column group
+// (<= 64 KB) in LDS for its life and its four waves stream 32-row tiles of A straight from
+// HBM into MFMA operand registers (one K-group of 64 ahead), with no barrier in the loop.
+//
+// W' is W [N][K] (w_trans 0) or the transpose of a [K][N] matrix (w_trans 1: the input
+// gradient dy W_layer reads the layer's own weight, no transposed copy).
+//
+// Products: v_mfma_f32_32x32x2_f32 with A as the first operand (tile rows = MFMA rows) and W'
+// as the second (output channels = MFMA columns), hreg_gemm's orientation: lane (j, h) holds
+// column j of each output tile for rows (q & 3) + 8 (q >> 2) + 4 h, so one dword store
+// writes two full 128-B row segments.  k-order: within each 16-deep sub-chunk, lane half h
+// takes k = 16 sub + 8 h + s at k-step s -- exactly hreg_gemm's, so every output is the
+// same fp32 sum as hreg_gemm's (tests/test_gpu_train.py checks bitwise equality).
+#include "common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TS_LDS_FLOATS = 16384;  // W' column group: NT * 32 rows x (K16 + 4) floats
+constexpr int TS_GRP = 4;             // 16-deep sub-chunks per A load group (k = 64)
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+
+template <int NT, bool TAIL, bool FULL>
+__global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict__ A, int lda, int R, int K,
+                                                         const float *__restrict__ W, int w_trans, int N,
+                                                         const float *__restrict__ scale,
+                                                         const float *__restrict__ shift, int relu,
+                                                         float *__restrict__ out, int ldo) {
+    extern __shared__ __attribute__((aligned(16))) float Ws[];
+    const int K16 = (K + 15) & ~15, KP = K16 + 4, nsub = K16 / 16;
+    const int ngrp = (nsub + TS_GRP - 1) / TS_GRP;
+    const int n0 = blockIdx.y * NT * 32;
+    constexpr int NR = NT * 32;
+    // stage W' [NR][K16] (zero beyond N / K)
+    if (!w_trans) {
+        for (int i = threadIdx.x; i < NR * (K16 / 4); i += 256) {
+            const int nn = i / (K16 / 4), k = (i - nn * (K16 / 4)) * 4;
+            const int n = n0 + nn;
+            const float4 v = (n < N && k < K) ? ld4(W + (size_t)n * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4 *>(Ws + nn * KP + k) = v;
+        }
+    } else {
+        for (int i = threadIdx.x; i < NR * K16; i += 256) {
+            const int k = i / NR, nn = i - k * NR;
+            const int n = n0 + nn;
+            Ws[nn * KP + k] = (n < N && k < K) ? W[(size_t)k * N + n] : 0.f;
+        }
+    }
+    // the epilogue's shift / scale from LDS (a global load there would make the tile's
+    // stores wait for the next group's prefetch: vmcnt counts in order)
+    float *Sh = Ws + NR * KP, *Sc = Sh + NR;
+    for (int i = threadIdx.x; i < NR; i += 256) {
+        const int n = n0 + i;
+        Sh[i] = (shift && n < N) ? shift[n] : 0.f;
+        if (FULL) Sc[i] = (scale && n < N) ? scale[n] : 1.f;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, j = lane & 31;
+    const int ntiles = (R + 31) / 32;
+    const int tstride = gridDim.x * 4;
+    int t = blockIdx.x * 4 + wave;
+    // A through a buffer descriptor: unconditional loads (rows clamped to R - 1; a sub-chunk
+    // past the row reads the next row -- finite values the zero columns of W' cancel, masked
+    // exactly in the tail sub-chunk -- or, past the buffer, 0), so no load sits in a branch
+    // and the waits stay counted
+    const uint32_t abytes = (uint32_t)((size_t)R * lda * sizeof(float));
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(A), (short)0, (int)abytes, 0x00020000);
+    auto load_group = [&](int tt, int g, float4 (&v)[2 * TS_GRP]) {
+        int r = tt * 32 + j;
+        r = r < R ? r : R - 1;
+#pragma unroll
+        for (int u = 0; u < TS_GRP; ++u) {
+            const int k = (g * TS_GRP + u) * 16 + 8 * h;
+            const uint32_t off = (uint32_t)(r * lda + k) * 4u;
+            v[2 * u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+            v[2 * u + 1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0));
+        }
+    };
+
+    f32x16 acc[NT];
+    float4 bufA[2 * TS_GRP], bufB[2 * TS_GRP];
+    int g = 0;
+    // one (tile, group) step: the next step's A into `nx` while this step's (`cu`) MFMAs run
+    // (ping-pong buffers, two steps per loop trip: no register copy, so the wait for `nx`
+    // falls at its use one step later; past the last tile the prefetch reads a clamped tile)
+    auto step = [&](float4 (&cu)[2 * TS_GRP], float4 (&nx)[2 * TS_GRP]) {
+        int t2 = t, g2 = g + 1;
+        if (g2 == ngrp) {
+            g2 = 0;
+            t2 += tstride;
+        }
+        load_group(t2 < ntiles ? t2 : t, g2, nx);
+        if (g == 0) {
+#pragma unroll
+            for (int co = 0; co < NT; ++co)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc[co][q] = 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < TS_GRP; ++u) {
+            const int sub = g * TS_GRP + u;
+            if (sub < nsub) {
+                float bv[8] = {cu[2 * u].x,     cu[2 * u].y,     cu[2 * u].z,     cu[2 * u].w,
+                               cu[2 * u + 1].x, cu[2 * u + 1].y, cu[2 * u + 1].z, cu[2 * u + 1].w};
+                if (TAIL && sub == nsub - 1) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bv[e] = sub * 16 + 8 * h + e < K ? bv[e] : 0.f;
+                }
+                // W' fragments one output tile ahead of their MFMAs
+                const float *wr = Ws + j * KP + sub * 16 + 8 * h;
+                float4 w0 = ld4(wr), w1 = ld4(wr + 4);
+#pragma unroll
+                for (int co = 0; co < NT; ++co) {
+                    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+                    if (co + 1 < NT) {
+                        w0 = ld4(wr + (co + 1) * 32 * KP);
+                        w1 = ld4(wr + (co + 1) * 32 * KP + 4);
+                    }
+#pragma unroll
+                    for (int s = 0; s < 8; ++s)
+                        acc[co] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[s], wv[s], acc[co], 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (g == ngrp - 1) {
+            // lane (j, h), register q: row (q & 3) + 8 (q >> 2) + 4 h of the tile, column j of
+            // output tile co -- each dword store instruction writes two 128-B row segments
+            // (full rate; 16-B stores of a row-per-lane layout wrote 32-B pieces at ~3 TB/s)
+#pragma unroll
+            for (int co = 0; co < NT; ++co) {
+                const int nl = co * 32 + j, n = n0 + nl;
+                if (n < N) {
+                    const float sh = Sh[nl];
+                    const float sc = FULL ? Sc[nl] : 1.f;
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int r = t * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                        if (r < R) {
+                            float v = acc[co][q];
+                            if constexpr (FULL) {
+                                v = fadd_rn(fmul_rn(v, sc), sh);
+                                if (relu) v = fmaxf(v, 0.f);
+                            } else {
+                                v = fadd_rn(v, sh);
+                            }
+                            out[(size_t)r * ldo + n] = v;
+                        }
+                    }
+                }
+            }
+        }
+        t = t2;
+        g = g2;
+    };
+    if (t < ntiles) load_group(t, 0, bufA);
+    while (t < ntiles) {
+        step(bufA, bufB);
+        if (t >= ntiles) break;
+        step(bufB, bufA);
+    }
+}
+
+// output tiles per workgroup for this K (W' column group within TS_LDS_FLOATS), 0: unsupported
+int ts_nt(int K, int N) {
+    const int KP = ((K + 15) & ~15) + 4 + 2;  // (+ the tile's shift / scale)
+    int nt = TS_LDS_FLOATS / (32 * KP);
+    if (nt > 8) nt = 8;
+    const int need = (N + 31) / 32;
+    nt = nt < need ? nt : need;
+    // instantiated: 1, 2, 4, 8 (3 / 6 tiles took 224 / 256+ VGPRs): round up when W' still fits
+    const int cap = TS_LDS_FLOATS / (32 * KP);
+    if (nt == 3) nt = 4 <= cap ? 4 : 2;
+    else if (nt > 4 && nt < 8) nt = 8 <= cap ? 8 : 4;
+    return nt;
+}
+
+}  // namespace
+
+extern "C" int hreg_ts_gemm_supported(int R, int K, int N) {
+    // (the A extent is addressed through a buffer descriptor: < 2 GB)
+    return R > 0 && K > 0 && N > 0 && (K & 3) == 0 && (N & 3) == 0 && ts_nt(K, N) > 0 &&
+           (size_t)R * K * sizeof(float) < ((size_t)1 << 31);
+}
+
+extern "C" int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
+                            const float *scale, const float *shift, int relu, float *out, int ldo, void *stream) {
+    if (!A || !W || !out || R < 0 || K <= 0 || N <= 0 || lda < K || ldo < N || (K & 3) || (N & 3) ||
+        (lda & 3) || (ldo & 3) || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W) |
+                                     reinterpret_cast<uintptr_t>(out)) & 15))
+        return HREG_ERR_INVALID;
+    if (R == 0) return HREG_OK;
+    if ((size_t)R * lda * sizeof(float) >= ((size_t)1 << 31)) return HREG_ERR_UNSUPPORTED;
+    const int nt = ts_nt(K, N);
+    if (nt <= 0) return HREG_ERR_UNSUPPORTED;
+    const int gy = (N + nt * 32 - 1) / (nt * 32);
+    const int tiles = (R + 31) / 32;
+    int gx = (tiles + 3) / 4;
+    // persistent: as many workgroups as fit at once (<= 4 tiles: <= 156 VGPRs, three per CU)
+    const int per_cu = nt >= 8 ? 2 : 3;
+    const int cap = 256 * per_cu / gy > 0 ? 256 * per_cu / gy : 1;
+    if (gx > cap) gx = cap;
+    const size_t lds = ((size_t)nt * 32 * (((K + 15) & ~15) + 4) + 2 * nt * 32) * sizeof(float);
+    hipStream_t st = as_stream(stream);
+    const bool tail = (K & 15) != 0, full = scale != nullptr || relu;
+#define HREG_TS(NTT, TT, FF)                                                                                 \
+    if (nt == NTT && tail == TT && full == FF) {                                                            \
+        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF>), dim3(gx, gy), dim3(256), lds, st, A, lda, R, K, W, \
+                           w_trans, N, scale, shift, relu, out, ldo);                                        \
+        HREG_CHECK_LAUNCH();                                                                                 \
+        return HREG_OK;                                                                                      \
+    }
+#define HREG_TS_NT(NTT) HREG_TS(NTT, false, false) HREG_TS(NTT, true, false) HREG_TS(NTT, false, true) \
+    HREG_TS(NTT, true, true)
+    HREG_TS_NT(1) HREG_TS_NT(2) HREG_TS_NT(4) HREG_TS_NT(8)
+#undef HREG_TS_NT
+#undef HREG_TS
+    return HREG_ERR_UNSUPPORTED;
+}

@@ -127,12 +127,33 @@ def _plain_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None) ->
     return engine.gemm([engine._seg(x, 0, K)], lin, R, b6=TRAIN_B6 and N >= TRAIN_B6_MIN_N)
 
 
+# conv GEMMs of >= TS_MIN_ROWS rows on hreg_ts_gemm (the tall-skinny kernel: W in LDS, A
+# streamed from HBM; the same fp32 sums as hreg_gemm); the input gradient reads W in place
+TS_GEMM = True
+TS_MIN_ROWS = 16384
+
+
+def _conv_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None,
+               w_trans: bool = False) -> torch.Tensor:
+    """x [R][K] @ W'^T (+ shift) with W' = W [N][K], or W [K][N] transposed (w_trans)."""
+    R, K = x.shape
+    N = W.shape[1] if w_trans else W.shape[0]
+    lib = _lib.load()
+    if (TS_GEMM and R >= TS_MIN_ROWS and x.is_contiguous() and W.is_contiguous()
+            and lib.hreg_ts_gemm_supported(R, K, N)):
+        out = torch.empty(R, N, device=x.device)
+        _lib.call("hreg_ts_gemm", x, K, R, K, W, 1 if w_trans else 0, N, None,
+                  None if shift is None else shift.contiguous(), 0, out, N, _stream())
+        return out
+    return _plain_gemm(x, transpose(W) if w_trans else W, shift)
+
+
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, bias, gamma, beta, running_mean, running_var, relu, momentum, eps,
                 wparam=None):
         R = x.shape[0]
-        y = _plain_gemm(x, W, bias)
+        y = _conv_gemm(x, W, bias)
         mean, invstd, var = bn_stats(y, eps)
         C = y.shape[1]
         out = torch.empty_like(y)
@@ -182,7 +203,7 @@ class _ConvBNAct(torch.autograd.Function):
                 col_sum(dy, into=gb)
             else:
                 dbias = col_sum(dy)
-        dx = _plain_gemm(dy, transpose(W), None) if ctx.needs_input_grad[0] else None
+        dx = _conv_gemm(dy, W, None, w_trans=True) if ctx.needs_input_grad[0] else None
         if acc:
             dgamma = dbeta = None
         return dx, dW, dbias, dgamma, dbeta, None, None, None, None, None, None

@@ -92,6 +92,29 @@ def test_conv_bn_act_accumulates_into_existing_grad_bitwise(bias):
         assert torch.equal(a, r), name
 
 
+@pytest.mark.parametrize("R,K,N", [(40000, 32, 192), (40000, 4, 32), (33000, 36, 68), (20000, 192, 32),
+                                   (17000, 384, 64), (16384, 128, 256), (16400, 68, 64)])
+@pytest.mark.parametrize("w_trans", [False, True])
+def test_ts_gemm_bitwise_equals_gemm(R, K, N, w_trans):
+    """hreg_ts_gemm (tall-skinny training conv GEMM) gives hreg_gemm's bits: the same k-order,
+    with W [N][K] or the transposed layout [K][N] read in place; ragged R, K % 16 != 0, N % 32
+    != 0, bias shift, several column groups (K = 384)."""
+    from pcd_reg_hregnet_amd import _lib, train
+    g = torch.Generator(device="cpu").manual_seed(R + K + N)
+    x = torch.randn(R, K, generator=g).cuda()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).cuda()
+    b = torch.randn(N, generator=g).cuda()
+    assert _lib.load().hreg_ts_gemm_supported(R, K, N)
+    ref = train._plain_gemm(x, W, b)
+    Wl = W.t().contiguous() if w_trans else W  # [K][N]: the dx GEMM's layout
+    out = torch.empty(R, N, device="cuda")
+    _lib.call("hreg_ts_gemm", x, K, R, K, Wl, 1 if w_trans else 0, N, None, b, 0, out, N,
+              _lib.stream_handle())
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert torch.equal(train._conv_gemm(x, Wl, b, w_trans=w_trans), ref)
+
+
 def test_gemm_tn_and_transpose():
     from pcd_reg_hregnet_amd.train import gemm_tn, transpose
     g = torch.Generator(device="cpu").manual_seed(3)
