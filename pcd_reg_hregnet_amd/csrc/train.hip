@@ -276,63 +276,97 @@ __global__ void bn_running_kernel(const float *__restrict__ mean, const float *_
 
 // ---------------------------------------------------------------- gemm_tn
 // out[n][k] = sum_r A[r][n] * B[r][k] (weight gradients: tall, skinny operands, HBM-bound).
-// A workgroup owns a 64 x 64 output tile and a range of rows; each of its 4 waves keeps
-// the whole tile in 4 v_mfma_f32_32x32x2_f32 accumulators and takes every 4th block of
-// 16 rows, loading its operands straight from global memory: at k-step s lane (h, j)
-// needs A[r][n0 + j (+32)] and B[r][k0 + j (+32)] with r = 2s + h, so each half-wave
-// reads 128 contiguous bytes of a row and no LDS staging or barrier sits in the loop
-// (8 k-steps = 32 loads in flight per lane).  The waves' tiles are added in wave order
-// through LDS at the end; split z of the rows writes ws[z][N][K] and tn_reduce_kernel
-// sums the splits in order (same bits every run).
+// A workgroup owns a (32 TNN) x (32 TNK) output tile (TNN, TNK in {1, 2}: no MFMAs on tiles
+// past N / K) and a range of rows; each of its 4 waves keeps the tile in TNN x TNK
+// v_mfma_f32_32x32x2_f32 accumulators and takes every 4th block of 16 rows, loading its
+// operands straight from global memory: at k-step s lane (h, j) needs A[r][n0 + j (+32)] and
+// B[r][k0 + j (+32)] with r = 2s + h, so each load instruction reads two 128-byte row
+// segments and no LDS staging or barrier sits in the loop.  The next block's operands load
+// while this block's MFMAs run (ping-pong registers); loads go through buffer descriptors
+// with no bounds tests -- a split's blocks lie inside its rows (splits are multiples of 64
+// rows), rows past R read 0, and columns past N / K only feed accumulator entries that are
+// never stored.  The waves' tiles are added in wave order through LDS at the end; split z of
+// the rows writes ws[z][N][K] and tn_reduce_kernel sums the splits in order (same bits every
+// run, and the same sums as the unpipelined form).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int TN_ROWS = 64;  // rows per workgroup iteration (16 per wave)
 
+template <int TNN, int TNK>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const float *__restrict__ A, int lda,
                                                       const float *__restrict__ Bm, int ldb, int R,
                                                       int N, int K, int rows_per_split,
                                                       float *__restrict__ ws) {
-    __shared__ float red[3][64 * 64];
+    __shared__ float red[3][(32 * TNN) * (32 * TNK)];
+    constexpr int TW = 32 * TNK;  // tile width (k)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int h = lane >> 5, j = lane & 31;
-    const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+    const int n0 = blockIdx.x * 32 * TNN, k0 = blockIdx.y * TW;
     const int r0 = blockIdx.z * rows_per_split;
     const int r1 = min(R, r0 + rows_per_split);
-    const bool okn0 = n0 + j < N, okn1 = n0 + 32 + j < N;
-    const bool okk0 = k0 + j < K, okk1 = k0 + 32 + j < K;
-    f32x16 acc00, acc01, acc10, acc11;
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(A), (short)0,
+                                                      (int)((size_t)R * lda * sizeof(float)), 0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Bm), (short)0,
+                                                      (int)((size_t)R * ldb * sizeof(float)), 0x00020000);
+    f32x16 acc[TNN][TNK];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc00[q] = acc01[q] = acc10[q] = acc11[q] = 0.f;
-    for (int base = r0 + 16 * w; base < r1; base += TN_ROWS) {
-        float a0[8], a1[8], b0[8], b1[8];
+    for (int a = 0; a < TNN; ++a)
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const int r = base + 2 * s + h;
-            const bool okr = r < r1;
-            const float *pa = A + (size_t)r * lda + n0 + j;
-            const float *pb = Bm + (size_t)r * ldb + k0 + j;
-            a0[s] = (okr && okn0) ? pa[0] : 0.f;
-            a1[s] = (okr && okn1) ? pa[32] : 0.f;
-            b0[s] = (okr && okk0) ? pb[0] : 0.f;
-            b1[s] = (okr && okk1) ? pb[32] : 0.f;
-        }
+        for (int b = 0; b < TNK; ++b)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+    typedef float Blk[TNN + TNK][8];
+    auto load = [&](int base, Blk &v) {
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-            acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc00, 0, 0, 0);
-            acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc01, 0, 0, 0);
-            acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc10, 0, 0, 0);
-            acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc11, 0, 0, 0);
+            const uint32_t r = (uint32_t)(base + 2 * s + h);
+#pragma unroll
+            for (int a = 0; a < TNN; ++a)
+                v[a][s] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(ra, (r * (uint32_t)lda + n0 + 32 * a + j) * 4u, 0, 0));
+#pragma unroll
+            for (int b = 0; b < TNK; ++b)
+                v[TNN + b][s] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rb, (r * (uint32_t)ldb + k0 + 32 * b + j) * 4u, 0, 0));
         }
+    };
+    auto mma = [&](const Blk &v) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+            for (int a = 0; a < TNN; ++a)
+#pragma unroll
+                for (int b = 0; b < TNK; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[a][s], v[TNN + b][s], acc[a][b], 0, 0, 0);
+    };
+    // blocks in pairs, no exit between them (a mid-loop exit made the compiler keep two copies
+    // of the accumulators): an odd count's last partner block is zeroed, adding 0 * 0 (the
+    // prefetch past the split's last block reads rows that are never used, or 0 past R)
+    Blk p0, p1;
+    const int base0 = r0 + 16 * w;
+    const int nblk = base0 < r1 ? (r1 - base0 + TN_ROWS - 1) / TN_ROWS : 0;
+    if (nblk) load(base0, p0);
+    for (int i = 0; i < nblk; i += 2) {
+        load(base0 + (i + 1) * TN_ROWS, p1);
+        mma(p0);
+        load(base0 + (i + 2) * TN_ROWS, p0);
+        if (i + 1 >= nblk) {
+#pragma unroll
+            for (int c = 0; c < TNN + TNK; ++c)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) p1[c][s] = 0.f;
+        }
+        mma(p1);
     }
-    // acc[q]: tile row n = (q&3) + 8(q>>2) + 4h, column k = j (per 32 x 32 quarter)
+    // acc[a][b][q]: tile row n = 32 a + (q&3) + 8(q>>2) + 4h, column k = 32 b + j
     if (w > 0) {
         float *o = red[w - 1];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
-            o[n * 64 + j] = acc00[q];
-            o[n * 64 + 32 + j] = acc01[q];
-            o[(n + 32) * 64 + j] = acc10[q];
-            o[(n + 32) * 64 + 32 + j] = acc11[q];
+#pragma unroll
+            for (int a = 0; a < TNN; ++a)
+#pragma unroll
+                for (int b = 0; b < TNK; ++b) o[(32 * a + n) * TW + 32 * b + j] = acc[a][b][q];
         }
     }
     __syncthreads();
@@ -342,14 +376,16 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float *__restrict__ 
     for (int q = 0; q < 16; ++q) {
         const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
 #pragma unroll
-        for (int quarter = 0; quarter < 4; ++quarter) {
-            const int nn = n + 32 * (quarter >> 1), kk = j + 32 * (quarter & 1);
-            float v = quarter == 0 ? acc00[q] : quarter == 1 ? acc01[q] : quarter == 2 ? acc10[q] : acc11[q];
-            v = fadd_rn(v, red[0][nn * 64 + kk]);
-            v = fadd_rn(v, red[1][nn * 64 + kk]);
-            v = fadd_rn(v, red[2][nn * 64 + kk]);
-            if (n0 + nn < N && k0 + kk < K) o[(size_t)(n0 + nn) * K + k0 + kk] = v;
-        }
+        for (int a = 0; a < TNN; ++a)
+#pragma unroll
+            for (int b = 0; b < TNK; ++b) {
+                const int nn = 32 * a + n, kk = 32 * b + j;
+                float v = acc[a][b][q];
+                v = fadd_rn(v, red[0][nn * TW + kk]);
+                v = fadd_rn(v, red[1][nn * TW + kk]);
+                v = fadd_rn(v, red[2][nn * TW + kk]);
+                if (n0 + nn < N && k0 + kk < K) o[(size_t)(n0 + nn) * K + k0 + kk] = v;
+            }
     }
 }
 
@@ -569,12 +605,24 @@ extern "C" int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, in
                             float beta, void *ws, float *out, void *stream) {
     if (!A || !B || !ws || !out || R <= 0 || N <= 0 || K <= 0 || lda < N || ldb < K)
         return HREG_ERR_INVALID;
+    if ((size_t)R * lda * sizeof(float) >= ((size_t)1 << 31) || (size_t)R * ldb * sizeof(float) >= ((size_t)1 << 31))
+        return HREG_ERR_UNSUPPORTED;  // (buffer-descriptor addressing)
     const int S = tn_splits(R, N, K);
     int rps = (R + S - 1) / S;
     rps = (rps + TN_ROWS - 1) / TN_ROWS * TN_ROWS;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(gemm_tn_kernel, dim3((N + 63) / 64, (K + 63) / 64, S), dim3(256), 0, st, A, lda,
-                       B, ldb, R, N, K, rps, (float *)ws);
+    // 64-wide output tiles as before (same splits, same sums); a 32-wide dimension runs one
+    // tile of MFMAs across it instead of two
+    const int tnn = N <= 32 ? 1 : 2, tnk = K <= 32 ? 1 : 2;
+    const dim3 grid((N + 32 * tnn - 1) / (32 * tnn), (K + 32 * tnk - 1) / (32 * tnk), S);
+    if (tnn == 1 && tnk == 1)
+        hipLaunchKernelGGL((gemm_tn_kernel<1, 1>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws);
+    else if (tnn == 1)
+        hipLaunchKernelGGL((gemm_tn_kernel<1, 2>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws);
+    else if (tnk == 1)
+        hipLaunchKernelGGL((gemm_tn_kernel<2, 1>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws);
+    else
+        hipLaunchKernelGGL((gemm_tn_kernel<2, 2>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws);
     HREG_CHECK_LAUNCH();
     const size_t NK = (size_t)N * K;
     if (S >= 16)
