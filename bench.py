@@ -433,6 +433,8 @@ class TrainGemmTimer:
         def call(name, *a):
             if name == "hreg_gemm_tn":
                 return self._timed("tn", lambda: orig_call(name, *a), 2.0 * a[4] * a[5] * a[6])
+            if name in ("hreg_ts_gemm", "hreg_ts_gemm_bn"):  # (A, lda, R, K, W, w_trans, N, ...)
+                return self._timed("nt", lambda: orig_call(name, *a), 2.0 * a[2] * a[3] * a[6])
             return orig_call(name, *a)
         _lib.gemm, _lib.call = gemm, call
 
@@ -455,6 +457,14 @@ def bench_train(args, world, rank, device):
     s, d, Rg, tg = shard_batch(rank, B, args.points)
     src, dst = torch.from_numpy(s).to(device), torch.from_numpy(d).to(device)
     gR, gt = torch.from_numpy(Rg).to(device), torch.from_numpy(tg).to(device)
+    graphed = world == 1 and not args.train_eager
+    eager_tr = tr
+    if graphed:
+        # the step replayed from captured HIP graphs (trainer.GraphTrainer; bitwise the eager
+        # step, tests/test_gpu_train_capture.py); DDP (world > 1) stays eager
+        gtr = trainer.GraphTrainer(tr, B, args.points)
+        gtr.capture(src, dst, gR, gt)
+        tr = gtr
     timer = TrainGemmTimer()
     timer.install()
     nxt = (src, dst)  # the next step's batch: its level-1 grouping overlaps this step
@@ -464,14 +474,21 @@ def bench_train(args, world, rank, device):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timer.enabled = True
+    timer.enabled = not graphed  # (HIP events cannot sit inside a replayed graph)
     t0 = time.perf_counter()
-    losses = [tr.step(src, dst, gR, gt, next_batch=nxt)[0] for _ in range(args.steps)]
+    losses = [tr.step(src, dst, gR, gt, next_batch=nxt)[0].clone() for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if graphed:
+        # the GEMM family's HIP events from an instrumented eager pass of the same steps right
+        # after the timed region (the eager step launches the same kernels)
+        timer.enabled = True
+        for _ in range(args.steps):
+            eager_tr.step(src, dst, gR, gt, next_batch=nxt)
+        torch.cuda.synchronize()
     timer.enabled = False
     elapsed = max_over_ranks(elapsed, device)
     value = job_throughput(B, args.steps, world, elapsed)
@@ -479,7 +496,7 @@ def bench_train(args, world, rank, device):
         nt_ms, nt_n, nt_fl = timer.result("nt")
         tn_ms, tn_n, tn_fl = timer.result("tn")
         ach = (nt_fl + tn_fl) / max(nt_ms + tn_ms, 1e-9) / 1e9
-        fam = {"gemm_nt_kernel (forward + input gradients)": {
+        fam = {"ts_gemm_kernel / gemm_nt_kernel (forward + input gradients)": {
                    "launches_per_step": nt_n // args.steps,
                    "ms_per_step": round(nt_ms / args.steps, 3),
                    "tflops": round(nt_fl / max(nt_ms, 1e-9) / 1e9, 2)},
@@ -501,9 +518,12 @@ def bench_train(args, world, rank, device):
                        "global_batch": B * world, "points": args.points,
                        "parallelism": f"dp{world} (one 9.87 MB gradient all-reduce per step)"},
             "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
+            "executor": "HIP graphs (two captured steps, ping-pong inputs)" if graphed else "eager",
             "roofline": {"kernel": "fp32 MFMA GEMM family of the step (forward, input- and "
                                    "weight-gradient GEMMs)",
-                         "timing": "HIP events on the launch stream inside the timed region",
+                         "timing": ("HIP events on the launch stream, instrumented eager pass of the "
+                                    "same steps after the timed region" if graphed else
+                                    "HIP events on the launch stream inside the timed region"),
                          "bound": "mfma", "achieved": round(ach, 3),
                          "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
@@ -581,6 +601,8 @@ def main():
     ap.add_argument("--points", type=int, default=None,
                     help=f"points per cloud (default {POINTS}; {V2_POINTS} for v2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train-eager", action="store_true",
+                    help="--model train: launch the step eagerly instead of replaying captured graphs")
     ap.add_argument("--executor", choices=("graph", "pipeline", "serial"), default="graph",
                     help="graph: pipelined forward replayed as HIP graphs; pipeline: same "
                          "eagerly; serial: no cross-batch overlap")

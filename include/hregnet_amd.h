@@ -346,6 +346,16 @@ int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, float *mean
 int hreg_ts_gemm_supported(int R, int K, int N);
 int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
                  const float *scale, const float *shift, int relu, float *out, int ldo, void *stream);
+/* hreg_ts_gemm (no scale / activation) with the output's train-mode BatchNorm statistics
+ * computed in its epilogue (fp64 sums, fixed order; the hreg_bn_stats pass over out it
+ * replaces): mean, invstd, var_unbiased as hreg_bn_stats (var_unbiased may be NULL without
+ * running stats), and running_mean / running_var (both or neither) updated with momentum as
+ * hreg_bn_running_update.  ws = hreg_ts_gemm_bn_ws_bytes(R, K, N) bytes. */
+size_t hreg_ts_gemm_bn_ws_bytes(int R, int K, int N);
+int hreg_ts_gemm_bn(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
+                    const float *shift, float *out, int ldo, float eps, float momentum, void *ws,
+                    float *mean, float *invstd, float *var_unbiased, float *running_mean,
+                    float *running_var, void *stream);
 /* out = act(gamma * (y - mean) * invstd + beta), act = ReLU if relu (out may alias y) */
 int hreg_bn_apply(const float *y, int R, int C, const float *mean, const float *invstd,
                   const float *gamma, const float *beta, int relu, float *out, void *stream);
@@ -372,6 +382,10 @@ int hreg_transpose(const float *in, int R, int C, float *out, void *stream);
 /* torch.optim.Adam step t (>= 1) over n floats, weight decay 0, amsgrad off */
 int hreg_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, size_t n,
                    float lr, float beta1, float beta2, float eps, int step, void *stream);
+/* the same update with scalars[2] = {lr / (1 - beta1^t), sqrt(1 - beta2^t)} (as hreg_adam_step
+ * computes them) read from device memory when the kernel runs: a captured graph's replays */
+int hreg_adam_step_dev(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, size_t n,
+                       float lr, float beta1, float beta2, float eps, const float *scalars, void *stream);
 
 /* ---------------- training graph ops (csrc/train_ops.hip) ----------------
  * Forward/backward of every non-GEMM op of the HRegNet training step

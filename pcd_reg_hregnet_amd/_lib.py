@@ -124,9 +124,13 @@ _SIGS = {
     "hreg_gemm_tn": [_vp, _i, _vp, _i, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp],
     "hreg_ts_gemm_supported": [_i, _i, _i],
     "hreg_ts_gemm": [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _vp],
+    "hreg_ts_gemm_bn": [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, ctypes.c_float, ctypes.c_float, _vp,
+                        _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_transpose": [_vp, _i, _i, _vp, _vp],
     "hreg_adam_step": [_vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_float, ctypes.c_float,
                        ctypes.c_float, ctypes.c_float, _i, _vp],
+    "hreg_adam_step_dev": [_vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_float, ctypes.c_float,
+                           ctypes.c_float, ctypes.c_float, _vp, _vp],
     "hreg_copy_rows": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp],
     "hreg_group_sum": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp],
     "hreg_gather_rows": [_vp, _i, _vp, _i, _i, _vp, _i, _vp],
@@ -160,7 +164,7 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_reduce_ws_bytes",
-                          "hreg_gemm_tn_ws_bytes", "hreg_csr_ws_bytes",
+                          "hreg_gemm_tn_ws_bytes", "hreg_csr_ws_bytes", "hreg_ts_gemm_bn_ws_bytes",
                           "hreg_sim_feats_bwd_ws_bytes", "hreg_group_l1_table_floats",
                           "hreg_group_l2_table_floats", "hreg_group_l3_table_floats",
                           "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
@@ -200,6 +204,8 @@ def load(require_gpu: bool = True):
         L.hreg_sim_feats_bwd_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.hreg_icp_ws_bytes.restype = ctypes.c_size_t
         L.hreg_icp_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.hreg_ts_gemm_bn_ws_bytes.restype = ctypes.c_size_t
+        L.hreg_ts_gemm_bn_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
                      "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
                      "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats",

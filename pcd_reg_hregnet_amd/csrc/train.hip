@@ -118,11 +118,13 @@ constexpr int FIN_COLS = 8, FIN_LANES = 32;
 
 // acc0 / acc1 (MODE 1, 2; optional): the totals are also added to these (a parameter's
 // .grad accumulating over its uses, as autograd's accumulation would: one fp32 add each)
+// MODE 0: acc0 / acc1 (optional) = running mean / var, updated with `momentum` as
+// bn_running_kernel does (from the fp32 mean and unbiased variance just written)
 template <int MODE>
 __global__ __launch_bounds__(FIN_COLS * FIN_LANES) void col_finalize_kernel(
     const double *__restrict__ partial, int S, int R, int C, float eps, float *__restrict__ o0,
     float *__restrict__ o1, float *__restrict__ o2, float *__restrict__ acc0 = nullptr,
-    float *__restrict__ acc1 = nullptr) {
+    float *__restrict__ acc1 = nullptr, float momentum = 0.f) {
     __shared__ double s0[FIN_COLS * FIN_LANES], s1[FIN_COLS * FIN_LANES];
     const int cl = threadIdx.x % FIN_COLS, sl = threadIdx.x / FIN_COLS;
     const int c = blockIdx.x * FIN_COLS + cl;
@@ -151,7 +153,12 @@ __global__ __launch_bounds__(FIN_COLS * FIN_LANES) void col_finalize_kernel(
         if (var < 0.0) var = 0.0;
         o0[c] = (float)m;
         o1[c] = (float)(1.0 / sqrt(var + (double)eps));
-        if (o2) o2[c] = (float)(R > 1 ? var * R / (R - 1) : var);
+        const float vu = (float)(R > 1 ? var * R / (R - 1) : var);
+        if (o2) o2[c] = vu;
+        if (acc0) {
+            acc0[c] = fadd_rn(fmul_rn(1.f - momentum, acc0[c]), fmul_rn(momentum, (float)m));
+            acc1[c] = fadd_rn(fmul_rn(1.f - momentum, acc1[c]), fmul_rn(momentum, vu));
+        }
     } else if (MODE == 1) {
         o0[c] = (float)b;  // dgamma = sum g * xhat
         o1[c] = (float)a;  // dbeta = sum g
@@ -438,9 +445,15 @@ __global__ void transpose_kernel(const float *__restrict__ in, int R, int C, flo
 // torch.optim.Adam (torch/optim/adam.py, foreach path, weight_decay 0), same order:
 //   m = lerp(m, g, 1 - b1) = m + (1 - b1)(g - m);  v = b2 v + ((1 - b2) g) g
 //   denom = sqrt(v) / sqrt(1 - b2^t) + eps;  p += (-lr / (1 - b1^t)) * (m / denom)
+// scal (optional): {step_size, bc2_sqrt} read from device memory (a captured graph's replays
+// take each step's bias corrections from there, hreg_adam_step_dev)
 __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
                             float *__restrict__ v, size_t n, float lr, float b1, float b2, float eps,
-                            float step_size, float bc2_sqrt) {
+                            float step_size, float bc2_sqrt, const float *__restrict__ scal = nullptr) {
+    if (scal) {
+        step_size = scal[0];
+        bc2_sqrt = scal[1];
+    }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
         const float gi = g[i];
@@ -502,6 +515,16 @@ extern "C" int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, 
     HREG_CHECK_LAUNCH();
     hipLaunchKernelGGL(col_finalize_kernel<0>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
                        (const double *)ws, S, R, C, eps, mean, invstd, var_unbiased);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+// statistics of S column partials [S][C][2] (sum y, sum y^2; ts_gemm.hip's fused epilogue)
+int hreg_bn_finalize_stats(const double *part, int S, int R, int C, float eps, float *mean, float *invstd,
+                           float *var_unbiased, float momentum, float *running_mean, float *running_var,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(col_finalize_kernel<0>, dim3((C + FIN_COLS - 1) / FIN_COLS), dim3(FIN_COLS * FIN_LANES), 0, st,
+                       part, S, R, C, eps, mean, invstd, var_unbiased, running_mean, running_var, momentum);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -653,6 +676,19 @@ extern "C" int hreg_adam_step(float *param, const float *grad, float *exp_avg, f
     hipLaunchKernelGGL(adam_kernel, dim3(grid1d(n)), dim3(256), 0, as_stream(stream), param, grad,
                        exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, (float)(lr / bc1),
                        (float)sqrt(bc2));
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+// Adam with the step's bias corrections {lr / (1 - b1^t), sqrt(1 - b2^t)} (fp32, computed on
+// the host in double as hreg_adam_step does) read from device memory at run time
+extern "C" int hreg_adam_step_dev(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, size_t n,
+                                  float lr, float beta1, float beta2, float eps, const float *scalars,
+                                  void *stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !scalars) return HREG_ERR_INVALID;
+    if (!n) return HREG_OK;
+    hipLaunchKernelGGL(adam_kernel, dim3(grid1d(n)), dim3(256), 0, as_stream(stream), param, grad, exp_avg,
+                       exp_avg_sq, n, lr, beta1, beta2, eps, 0.f, 1.f, scalars);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

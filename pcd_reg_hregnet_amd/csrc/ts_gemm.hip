@@ -28,12 +28,18 @@ constexpr int TS_GRP = 4;             // 16-deep sub-chunks per A load group (k 
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
-template <int NT, bool TAIL, bool FULL>
+// STATS: the train-mode BatchNorm statistics of the output ride along in the epilogue (the
+// col_reduce pass over y it replaces): every lane keeps fp64 sums of its column's values and
+// squares (exact products) over its rows, in its fixed tile order; the lane halves, then the
+// four waves (in order, through LDS) combine, and each workgroup writes its partial
+// [blockIdx.x][N][2] for col_finalize (train.hip) to sum over workgroups in order.
+template <int NT, bool TAIL, bool FULL, bool STATS = false>
 __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict__ A, int lda, int R, int K,
                                                          const float *__restrict__ W, int w_trans, int N,
                                                          const float *__restrict__ scale,
                                                          const float *__restrict__ shift, int relu,
-                                                         float *__restrict__ out, int ldo) {
+                                                         float *__restrict__ out, int ldo,
+                                                         double *__restrict__ part = nullptr) {
     extern __shared__ __attribute__((aligned(16))) float Ws[];
     const int K16 = (K + 15) & ~15, KP = K16 + 4, nsub = K16 / 16;
     const int ngrp = (nsub + TS_GRP - 1) / TS_GRP;
@@ -88,6 +94,9 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
     };
 
     f32x16 acc[NT];
+    double st1[NT], st2[NT];
+#pragma unroll
+    for (int co = 0; co < NT; ++co) st1[co] = st2[co] = 0.0;
     float4 bufA[2 * TS_GRP], bufB[2 * TS_GRP];
     int g = 0;
     // one (tile, group) step: the next step's A into `nx` while this step's (`cu`) MFMAs run
@@ -155,6 +164,11 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
                                 v = fadd_rn(v, sh);
                             }
                             out[(size_t)r * ldo + n] = v;
+                            if constexpr (STATS) {
+                                const double d = (double)v;
+                                st1[co] += d;
+                                st2[co] = fma(d, d, st2[co]);
+                            }
                         }
                     }
                 }
@@ -169,11 +183,37 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
         if (t >= ntiles) break;
         step(bufB, bufA);
     }
+    if constexpr (STATS) {
+        double *red = reinterpret_cast<double *>(Ws + NR * KP + 2 * NR);  // [4 waves][NR][2]
+#pragma unroll
+        for (int co = 0; co < NT; ++co) {
+            const double o1 = __shfl_xor(st1[co], 32), o2 = __shfl_xor(st2[co], 32);
+            if (h == 0) {
+                red[(wave * NR + co * 32 + j) * 2 + 0] = st1[co] + o1;
+                red[(wave * NR + co * 32 + j) * 2 + 1] = st2[co] + o2;
+            }
+        }
+        __syncthreads();
+        for (int nl = threadIdx.x; nl < NR; nl += 256) {
+            const int n = n0 + nl;
+            if (n < N) {
+                double a = red[nl * 2], b = red[nl * 2 + 1];
+#pragma unroll
+                for (int w = 1; w < 4; ++w) {
+                    a += red[(w * NR + nl) * 2];
+                    b += red[(w * NR + nl) * 2 + 1];
+                }
+                part[((size_t)blockIdx.x * N + n) * 2 + 0] = a;
+                part[((size_t)blockIdx.x * N + n) * 2 + 1] = b;
+            }
+        }
+    }
 }
 
 // output tiles per workgroup for this K (W' column group within TS_LDS_FLOATS), 0: unsupported
 int ts_nt(int K, int N) {
-    const int KP = ((K + 15) & ~15) + 4 + 2;  // (+ the tile's shift / scale)
+    // (+ the tile's shift / scale and the statistics' wave partials: 8 floats per column)
+    const int KP = ((K + 15) & ~15) + 4 + 2 + 8;
     int nt = TS_LDS_FLOATS / (32 * KP);
     if (nt > 8) nt = 8;
     const int need = (N + 31) / 32;
@@ -185,7 +225,24 @@ int ts_nt(int K, int N) {
     return nt;
 }
 
+// workgroups along the rows: persistent (tiles assigned statically), so exactly as many as
+// fit at once -- three per CU up to 168 VGPRs (<= 4 tiles; 2 with the statistics), else two
+int ts_grid_x(int R, int K, int N, bool stats) {
+    const int nt = ts_nt(K, N);
+    const int gy = (N + nt * 32 - 1) / (nt * 32);
+    const int tiles = (R + 31) / 32;
+    const int gx = (tiles + 3) / 4;
+    const int per_cu = nt >= 8 || (stats && nt >= 4) ? 2 : 3;
+    const int cap = 256 * per_cu / gy > 0 ? 256 * per_cu / gy : 1;
+    return gx < cap ? gx : cap;
+}
+
 }  // namespace
+
+// (train.hip) the statistics' finalisation over S partials [S][C][2] (+ the running update)
+int hreg_bn_finalize_stats(const double *part, int S, int R, int C, float eps, float *mean, float *invstd,
+                           float *var_unbiased, float momentum, float *running_mean, float *running_var,
+                           hipStream_t st);
 
 extern "C" int hreg_ts_gemm_supported(int R, int K, int N) {
     // (the A extent is addressed through a buffer descriptor: < 2 GB)
@@ -193,37 +250,67 @@ extern "C" int hreg_ts_gemm_supported(int R, int K, int N) {
            (size_t)R * K * sizeof(float) < ((size_t)1 << 31);
 }
 
-extern "C" int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
-                            const float *scale, const float *shift, int relu, float *out, int ldo, void *stream) {
-    if (!A || !W || !out || R < 0 || K <= 0 || N <= 0 || lda < K || ldo < N || (K & 3) || (N & 3) ||
+namespace {
+
+// launch (STATS: the workgroups' statistic partials into part, see ts_gemm_kernel); returns
+// the number of workgroups along the rows (the partials' count), or a negative HREG_ERR_*
+template <bool STATS>
+int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans, int N, const float *scale,
+              const float *shift, int relu, float *out, int ldo, double *part, hipStream_t st) {
+    if (!A || !W || !out || R <= 0 || K <= 0 || N <= 0 || lda < K || ldo < N || (K & 3) || (N & 3) ||
         (lda & 3) || (ldo & 3) || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W) |
                                      reinterpret_cast<uintptr_t>(out)) & 15))
-        return HREG_ERR_INVALID;
-    if (R == 0) return HREG_OK;
-    if ((size_t)R * lda * sizeof(float) >= ((size_t)1 << 31)) return HREG_ERR_UNSUPPORTED;
+        return -HREG_ERR_INVALID;
+    if ((size_t)R * lda * sizeof(float) >= ((size_t)1 << 31)) return -HREG_ERR_UNSUPPORTED;
     const int nt = ts_nt(K, N);
-    if (nt <= 0) return HREG_ERR_UNSUPPORTED;
+    if (nt <= 0) return -HREG_ERR_UNSUPPORTED;
+    const int gx = ts_grid_x(R, K, N, STATS);
     const int gy = (N + nt * 32 - 1) / (nt * 32);
-    const int tiles = (R + 31) / 32;
-    int gx = (tiles + 3) / 4;
-    // persistent: as many workgroups as fit at once (<= 4 tiles: <= 156 VGPRs, three per CU)
-    const int per_cu = nt >= 8 ? 2 : 3;
-    const int cap = 256 * per_cu / gy > 0 ? 256 * per_cu / gy : 1;
-    if (gx > cap) gx = cap;
-    const size_t lds = ((size_t)nt * 32 * (((K + 15) & ~15) + 4) + 2 * nt * 32) * sizeof(float);
-    hipStream_t st = as_stream(stream);
+    const size_t lds = ((size_t)nt * 32 * (((K + 15) & ~15) + 4) + 2 * nt * 32 + (STATS ? 16 * nt * 32 : 0)) *
+                       sizeof(float);
     const bool tail = (K & 15) != 0, full = scale != nullptr || relu;
-#define HREG_TS(NTT, TT, FF)                                                                                 \
-    if (nt == NTT && tail == TT && full == FF) {                                                            \
-        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF>), dim3(gx, gy), dim3(256), lds, st, A, lda, R, K, W, \
-                           w_trans, N, scale, shift, relu, out, ldo);                                        \
-        HREG_CHECK_LAUNCH();                                                                                 \
-        return HREG_OK;                                                                                      \
+    if (STATS && full) return -HREG_ERR_UNSUPPORTED;
+#define HREG_TS(NTT, TT, FF)                                                                                   \
+    if (nt == NTT && tail == TT && full == FF) {                                                              \
+        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF, STATS>), dim3(gx, gy), dim3(256), lds, st, A, lda, R, K, \
+                           W, w_trans, N, scale, shift, relu, out, ldo, part);                                 \
+        if (hipGetLastError() != hipSuccess) return -HREG_ERR_LAUNCH;                                          \
+        return gx;                                                                                             \
     }
-#define HREG_TS_NT(NTT) HREG_TS(NTT, false, false) HREG_TS(NTT, true, false) HREG_TS(NTT, false, true) \
-    HREG_TS(NTT, true, true)
+#define HREG_TS_NT(NTT) HREG_TS(NTT, false, false) HREG_TS(NTT, true, false)                           \
+    if constexpr (!STATS) { HREG_TS(NTT, false, true) HREG_TS(NTT, true, true) }
     HREG_TS_NT(1) HREG_TS_NT(2) HREG_TS_NT(4) HREG_TS_NT(8)
 #undef HREG_TS_NT
 #undef HREG_TS
-    return HREG_ERR_UNSUPPORTED;
+    return -HREG_ERR_UNSUPPORTED;
+}
+
+}  // namespace
+
+extern "C" int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
+                            const float *scale, const float *shift, int relu, float *out, int ldo, void *stream) {
+    if (R == 0 && A && W && out) return HREG_OK;
+    const int rc = ts_launch<false>(A, lda, R, K, W, w_trans, N, scale, shift, relu, out, ldo, nullptr,
+                                    as_stream(stream));
+    return rc < 0 ? -rc : HREG_OK;
+}
+
+extern "C" size_t hreg_ts_gemm_bn_ws_bytes(int R, int K, int N) {
+    if (R <= 0 || K <= 0 || N <= 0 || ts_nt(K, N) <= 0) return 0;
+    return (size_t)ts_grid_x(R, K, N, true) * N * 2 * sizeof(double);
+}
+
+extern "C" int hreg_ts_gemm_bn(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
+                               const float *shift, float *out, int ldo, float eps, float momentum, void *ws,
+                               float *mean, float *invstd, float *var_unbiased, float *running_mean,
+                               float *running_var, void *stream) {
+    if (!ws || !mean || !invstd || R <= 0 || ((running_mean == nullptr) != (running_var == nullptr)) ||
+        (running_mean && !var_unbiased))
+        return HREG_ERR_INVALID;
+    hipStream_t st = as_stream(stream);
+    const int S = ts_launch<true>(A, lda, R, K, W, w_trans, N, nullptr, shift, 0, out, ldo,
+                                  static_cast<double *>(ws), st);
+    if (S < 0) return -S;
+    return hreg_bn_finalize_stats(static_cast<const double *>(ws), S, R, N, eps, mean, invstd, var_unbiased,
+                                  momentum, running_mean, running_var, st);
 }

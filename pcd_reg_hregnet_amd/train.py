@@ -148,20 +148,46 @@ def _conv_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None,
     return _plain_gemm(x, transpose(W) if w_trans else W, shift)
 
 
+TS_BN = True  # (A/B switch: the statistics pass fused into hreg_ts_gemm's epilogue)
+
+
+def _conv_gemm_bn(x, W, shift, eps, momentum, running_mean, running_var):
+    """(y, mean, invstd, var_unbiased) from hreg_ts_gemm_bn when the conv takes the tall-skinny
+    path (running stats updated there), else None."""
+    R, K = x.shape
+    N = W.shape[0]
+    lib = _lib.load()
+    if not (TS_GEMM and TS_BN and R >= TS_MIN_ROWS and x.is_contiguous() and W.is_contiguous()
+            and lib.hreg_ts_gemm_supported(R, K, N)):
+        return None
+    dev = x.device
+    y = torch.empty(R, N, device=dev)
+    mean, invstd, var = (torch.empty(N, device=dev) for _ in range(3))
+    ws = _ws(lib.hreg_ts_gemm_bn_ws_bytes(R, K, N), dev)
+    _lib.call("hreg_ts_gemm_bn", x, K, R, K, W, 0, N, None if shift is None else shift.contiguous(),
+              y, N, float(eps), float(momentum), ws, mean, invstd, var, running_mean, running_var,
+              _stream())
+    return y, mean, invstd, var
+
+
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, bias, gamma, beta, running_mean, running_var, relu, momentum, eps,
                 wparam=None):
         R = x.shape[0]
-        y = _conv_gemm(x, W, bias)
-        mean, invstd, var = bn_stats(y, eps)
+        fused = _conv_gemm_bn(x, W, bias, eps, momentum, running_mean, running_var)
+        if fused is not None:
+            y, mean, invstd, var = fused  # statistics (+ running update) in the GEMM's epilogue
+        else:
+            y = _conv_gemm(x, W, bias)
+            mean, invstd, var = bn_stats(y, eps)
+            if running_mean is not None:
+                _lib.call("hreg_bn_running_update", mean, var, y.shape[1], float(momentum),
+                          running_mean, running_var, _stream())
         C = y.shape[1]
         out = torch.empty_like(y)
         _lib.call("hreg_bn_apply", y, R, C, mean, invstd, gamma, beta, 1 if relu else 0, out,
                   _stream())
-        if running_mean is not None:
-            _lib.call("hreg_bn_running_update", mean, var, C, float(momentum), running_mean,
-                      running_var, _stream())
         ctx.save_for_backward(x, W, y, mean, invstd, gamma, beta)
         ctx.relu = relu
         ctx.has_bias = bias is not None

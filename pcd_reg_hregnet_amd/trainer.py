@@ -19,8 +19,10 @@ forward, l_trans = mean over the 3 levels of ``transformation_loss`` (alpha), ba
 """
 from __future__ import annotations
 
+import math
 import weakref
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -176,3 +178,169 @@ class Trainer:
         self.bucket.all_reduce_mean(self.group)  # DDP gradient averaging, one collective
         self.opt.step()
         return loss.detach(), l_R.detach(), l_t.detach()
+
+
+def level1_selections(src, dst):
+    """The weight-independent level-1 selections of a batch (FPS + kNN grouping of src and dst
+    in one launch set) in the IndexHook ``prepared`` form (Level1Prefetch's)."""
+    B, n, _ = src.shape
+    M, k = engine.LEVELS[0][:2]
+    idx, _, gidx, _, _ = engine.grouping(torch.cat([src, dst], 0), 0)
+    src_fps, dst_fps = idx[:B], idx[B:]
+    return {
+        "src_fps_1": (src_fps, train_graph.offset_index(src_fps, n)),
+        "dst_fps_1": (dst_fps, train_graph.offset_index(dst_fps, n)),
+        "src_knn_1": (None, gidx[:B * M * k]),
+        "dst_knn_1": (None, (gidx[B * M * k:] - B * n).to(torch.int32)),
+    }
+
+
+class GraphTrainer:
+    """``Trainer.step`` replayed from two captured HIP graphs (the step's
+    ~1,500 launches and their host gaps).  Two static input sets ping-pong: replay i runs the
+    step on set k = i % 2 with the level-1 selections the previous replay computed for it, and,
+    on a side stream inside the same graph, the selections of set 1 - k (the next batch, copied
+    in before the replay) -- Level1Prefetch's overlap, captured.  Adam reads its step's bias
+    corrections from device memory (hreg_adam_step_dev), written before each replay, so lr
+    changes (``set_lr``) need no recapture.  Everything else a step does -- BN running stats,
+    num_batches_tracked, the gradient bucket -- is device work in the graph.  Single process
+    (the DDP all-reduce stays on the eager Trainer).  Capture runs two warm-up steps first; the
+    parameters, optimizer moments and BN buffers are restored afterwards, so the first
+    ``step`` continues from the state the Trainer had."""
+
+    def __init__(self, trainer: "Trainer", batch: int, points: int):
+        if _dist_world(trainer.group) > 1:
+            raise NotImplementedError("GraphTrainer: single process (use Trainer with DDP)")
+        self.tr = trainer
+        dev = trainer.params.flat.device
+        self.src = [torch.zeros(batch, points, 3, device=dev) for _ in range(2)]
+        self.dst = [torch.zeros(batch, points, 3, device=dev) for _ in range(2)]
+        self.gR = [torch.eye(3, device=dev).repeat(batch, 1, 1) for _ in range(2)]
+        self.gt = [torch.zeros(batch, 3, device=dev) for _ in range(2)]
+        self.scal = torch.zeros(2, device=dev)
+        # two pinned staging slots: a slot is rewritten only after its previous asynchronous
+        # copy ran (its event), so a host running ahead never changes a pending step's scalars
+        self.scal_h = [torch.zeros(2, pin_memory=True) for _ in range(2)]
+        self.scal_ev = [None, None]
+        self.scal_slot = 0
+        self.side = torch.cuda.Stream(device=dev)
+        self.sel = [None, None]
+        self.graphs = [None, None]
+        self.outs = [None, None]
+        self.k = 0
+        self.loaded = False
+
+    def _sel_into(self, k):
+        fresh = level1_selections(self.src[k], self.dst[k])
+        if self.sel[k] is None:
+            self.sel[k] = {nm: (None if a is None else a.clone(), b.clone()) for nm, (a, b) in fresh.items()}
+            return
+        for nm, (a, b) in fresh.items():
+            sa, sb = self.sel[k][nm]
+            if a is not None:
+                sa.copy_(a)
+            sb.copy_(b)
+
+    def _set_scalars(self):
+        """hreg_adam_step's bias corrections for the next step, with its arithmetic: lr and the
+        betas as the fp32 kernel arguments, powers and quotient in double, rounded to fp32"""
+        opt = self.tr.opt
+        t = opt.step_count + 1
+        f32 = lambda x: float(np.float32(x))  # noqa: E731
+        lr, b1, b2 = f32(opt.lr), f32(opt.betas[0]), f32(opt.betas[1])
+        i = self.scal_slot
+        self.scal_slot ^= 1
+        if self.scal_ev[i] is not None:
+            self.scal_ev[i].synchronize()
+        h = self.scal_h[i]
+        h[0] = f32(lr / (1.0 - math.pow(b1, t)))
+        h[1] = f32(math.sqrt(1.0 - math.pow(b2, t)))
+        self.scal.copy_(h, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.scal_ev[i] = ev
+
+    def _body(self, k):
+        tr = self.tr
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)  # the next set was copied in on this stream
+        with torch.cuda.stream(self.side):
+            self._sel_into(1 - k)
+        tr.bucket.attach()
+        hook = train_graph.IndexHook(prepared=self.sel[k])
+        ret = train_graph.hregnet_train_forward(tr.net, self.src[k], self.dst[k], hook)
+        loss, l_R, l_t = train_graph.registration_loss(ret, self.gR[k], self.gt[k], tr.alpha)
+        loss.backward()
+        tr.bucket.collect()
+        opt = tr.opt
+        _lib.call("hreg_adam_step_dev", opt.p, opt.g, opt.m, opt.v, opt.p.numel(), float(opt.lr),
+                  float(opt.betas[0]), float(opt.betas[1]), float(opt.eps), self.scal,
+                  _lib.stream_handle())
+        cur.wait_stream(self.side)
+        return loss.detach(), l_R.detach(), l_t.detach()
+
+    def _state(self):
+        tr = self.tr
+        bufs = [b for b in tr.net.buffers()]
+        return [tr.params.flat, tr.opt.m, tr.opt.v] + bufs
+
+    def capture(self, src, dst, gt_R, gt_t):
+        """Warm up and capture both graphs on this batch; the trainer's state is restored."""
+        tr = self.tr
+        saved = [t.detach().clone() for t in self._state()]
+        step_count = tr.opt.step_count
+        for k in (0, 1):
+            self._load(k, src, dst, gt_R, gt_t)
+        self._sel_into(0)
+        s = torch.cuda.Stream(device=self.scal.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for k in (0, 1):  # eager warm-up of the exact bodies (allocator, lazy builds)
+                self._set_scalars()
+                self._body(k)
+                tr.opt.step_count += 1
+        torch.cuda.current_stream().wait_stream(s)
+        for k in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.outs[k] = self._body(k)
+            self.graphs[k] = g
+        torch.cuda.synchronize()
+        for t, v in zip(self._state(), saved):
+            t.copy_(v)
+        tr.opt.step_count = step_count
+        torch.cuda.synchronize()
+        self.k = 0
+        self.loaded = True
+        self.first = True
+
+    def _load(self, k, src, dst, gt_R, gt_t):
+        self.src[k].copy_(src)
+        self.dst[k].copy_(dst)
+        self.gR[k].copy_(gt_R)
+        self.gt[k].copy_(gt_t)
+
+    def step(self, src, dst, gt_R, gt_t, next_batch=None):
+        """One training step on (src, dst, gt_R, gt_t) -- which must be the batch passed as
+        ``next_batch`` to the previous step (or to ``capture``) -- and the level-1 selections
+        of ``next_batch`` (default: the same batch again).  -> (loss, l_R, l_t), static
+        tensors overwritten by the next replay."""
+        if not self.loaded:
+            raise RuntimeError("GraphTrainer.capture() first")
+        k = self.k
+        nb = next_batch if next_batch is not None else (src, dst)
+        if self.first:  # nothing prefetched this batch yet
+            self.src[k].copy_(src)
+            self.dst[k].copy_(dst)
+            self._sel_into(k)
+            self.first = False
+        # the set this replay consumes holds (src, dst) since the previous replay's prefetch
+        self.gR[k].copy_(gt_R)
+        self.gt[k].copy_(gt_t)
+        self.src[1 - k].copy_(nb[0])
+        self.dst[1 - k].copy_(nb[1])
+        self._set_scalars()
+        self.graphs[k].replay()
+        self.tr.opt.step_count += 1
+        self.k = 1 - k
+        return self.outs[k]

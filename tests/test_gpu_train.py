@@ -115,6 +115,36 @@ def test_ts_gemm_bitwise_equals_gemm(R, K, N, w_trans):
     assert torch.equal(train._conv_gemm(x, Wl, b, w_trans=w_trans), ref)
 
 
+@pytest.mark.parametrize("R,K,N", [(40000, 32, 192), (40000, 4, 32), (33000, 36, 68), (17000, 384, 64),
+                                   (16384, 128, 256)])
+def test_ts_gemm_bn_statistics(R, K, N):
+    """hreg_ts_gemm_bn: y bitwise hreg_ts_gemm's; mean / invstd / unbiased var and the running
+    update as hreg_bn_stats + hreg_bn_running_update (fp64 sums in another fixed order: equal
+    to within an fp32 ulp); bitwise repeatable."""
+    from pcd_reg_hregnet_amd import _lib, train
+    g = torch.Generator(device="cpu").manual_seed(R + K)
+    x = (torch.randn(R, K, generator=g) * 3 + 1).cuda()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).cuda()
+    b = torch.randn(N, generator=g).cuda()
+    rm0, rv0 = torch.randn(N, generator=g).cuda(), (torch.rand(N, generator=g) + 0.5).cuda()
+    y_ref = train._conv_gemm(x, W, b)
+    m_ref, i_ref, v_ref = train.bn_stats(y_ref, 1e-5)
+    rm_ref, rv_ref = rm0.clone(), rv0.clone()
+    _lib.call("hreg_bn_running_update", m_ref, v_ref, N, 0.1, rm_ref, rv_ref, _lib.stream_handle())
+    outs = []
+    for _ in range(2):
+        rm, rv = rm0.clone(), rv0.clone()
+        y, m, i, v = train._conv_gemm_bn(x, W, b, 1e-5, 0.1, rm, rv)
+        outs.append((y, m, i, v, rm, rv))
+    torch.cuda.synchronize()
+    y, m, i, v, rm, rv = outs[0]
+    assert torch.equal(y, y_ref)
+    for a, r in ((m, m_ref), (i, i_ref), (v, v_ref), (rm, rm_ref), (rv, rv_ref)):
+        torch.testing.assert_close(a, r, rtol=2e-7, atol=1e-7)
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+
+
 def test_gemm_tn_and_transpose():
     from pcd_reg_hregnet_amd.train import gemm_tn, transpose
     g = torch.Generator(device="cpu").manual_seed(3)
