@@ -556,6 +556,11 @@ int hreg_group_split6_l2(const float *table, const float *geom, const float *knn
                          const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                          float *desc, const float *pre, void *stream);
 int hreg_group_split6_l3_table_floats(void);
+/* hreg_group_split6_l3 with two 32-row tiles per wave (each streamed weight piece feeds both
+ * tiles' MFMAs; the same outputs bit for bit); pre (the precomputed feature block) required */
+int hreg_group_split6j_l3(const float *table, const float *geom, const float *knn_xyz,
+                          const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
+                          float *desc, const float *pre, void *stream);
 int hreg_group_split6_l3(const float *table, const float *geom, const float *knn_xyz,
                          const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                          float *desc, const float *pre, void *stream);

@@ -343,6 +343,306 @@ __global__ __launch_bounds__(RING ? RING_RT * 256 : 256, RING ? 1 : ONE ? 3 : 2)
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Two row tiles per wave (level 3, PRE + one-buffer form): each wave of channel group cw runs
+// the same layers as group_split6_kernel on two 32-row tiles at once (split_chain.h
+// pipe_lds6_jt), so every weight piece it streams feeds the MFMAs of both tiles -- half the
+// weight bytes per row on the L2 -> CU path that bounds the channel-split kernel (DESIGN.md
+// 4c: "no weight loads" -26 % at level 3).  The two tiles' activations share one LDS buffer
+// (64 rows); the epilogue constants are read from the table in global memory (the LDS copy
+// would leave one workgroup per CU), so two 4-wave workgroups fit per CU.  Same products,
+// same order per output as group_split6_kernel (bitwise equal, tests/test_gpu_model.py).
+constexpr int SJT = 2;
+
+template <int P, int C>
+__device__ __forceinline__ void beta_pj(const float *ab, int co0, int h, f32x16 (&acc)[P][SJT]) {
+#pragma unroll
+    for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float4 a = *reinterpret_cast<const float4 *>(ab + C + (co0 + i) * 32 + 8 * r + 4 * h);
+                acc[i][jt][4 * r] = a.x; acc[i][jt][4 * r + 1] = a.y;
+                acc[i][jt][4 * r + 2] = a.z; acc[i][jt][4 * r + 3] = a.w;
+            }
+}
+
+template <int P>
+__device__ __forceinline__ void relu_j(f32x16 (&t)[P][SJT]) {
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+        for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t[i][jt][q] = relu_i(t[i][jt][q]);
+}
+
+template <int LDSW, int P>
+__device__ __forceinline__ void put_j(float *buf, int co0, int j, int h, const f32x16 (&t)[P][SJT]) {
+#pragma unroll
+    for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+        for (int i = 0; i < P; ++i) put_tile<LDSW>(buf + jt * 32 * LDSW, co0 + i, j, h, t[i][jt]);
+}
+
+// conv stack [geom | precomputed feature block] -> C1 -> C1 -> C3 on two row tiles
+template <class K, int NP, class WT>
+__device__ __forceinline__ void conv_stack_split6j(WT wt, const float *eb, int gg, int g2, int g3, int e2, int e3,
+                                                   float *A, int cw, int lane, f32x16 (&out)[K::P3][SJT],
+                                                   const Carry6 &cin, FragSeq next, Carry6 &cout,
+                                                   const float *const (&pre_row)[SJT], const float2 (&gin)[SJT]) {
+    constexpr int P1 = K::P1, P3 = K::P3, LDSW = K::LDSW, N1 = K::N1;
+    const int h = lane >> 5, j = lane & 31;
+    const int c1 = cw * P1, c3 = cw * P3;
+    const FragSeq sg{gg + c1, 1}, s2{g2 + c1 * N1, N1}, s3{g3 + c3 * N1, N1};
+    const float *arow = A + j * LDSW;
+    Carry6 ca, cb;
+    f32x16 h1[P1][SJT];
+#pragma unroll
+    for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+        for (int i = 0; i < P1; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // engine.level_pre6: alpha-folded W_f f + beta
+                const float4 a = *reinterpret_cast<const float4 *>(pre_row[jt] + (c1 + i) * 32 + 8 * r + 4 * h);
+                h1[i][jt][4 * r] = a.x; h1[i][jt][4 * r + 1] = a.y;
+                h1[i][jt][4 * r + 2] = a.z; h1[i][jt][4 * r + 3] = a.w;
+            }
+    // geometry chunk: f32 k-steps 0, 1 (channels 2h, 2h + 1), the rest zero
+    pipe_lds6_jt<1, P1, P1, SJT>(
+        wt, lane, sg,
+        [&](int jt, int st0, float (&v)[4]) {
+            v[0] = st0 == 0 ? gin[jt].x : 0.f;
+            v[1] = st0 == 0 ? gin[jt].y : 0.f;
+            v[2] = 0.f; v[3] = 0.f;
+        },
+        h1, cin, s2, cb);
+    relu_j(h1);
+    put_j<LDSW>(A, c1, j, h, h1);
+    tile_sync();
+    f32x16 h2[P1][SJT];
+    beta_pj<P1, K::T1 * 32>(eb + e2, c1, h, h2);
+    pipe_lds6_jt<N1, P1, P3, SJT>(wt, lane, s2, ChanBJ<LDSW>{arow, h}, h2, cb, s3, ca);
+    relu_j(h2);
+    tile_sync();  // one buffer: every wave has read layer 2's input
+    put_j<LDSW>(A, c1, j, h, h2);
+    tile_sync();
+    beta_pj<P3, K::T3 * 32>(eb + e3, c3, h, out);
+    pipe_lds6_jt<N1, P3, NP, SJT>(wt, lane, s3, ChanBJ<LDSW>{arow, h}, out, ca, next, cout);
+    relu_j(out);
+}
+
+template <class K>
+__global__ __launch_bounds__(256, 2) void group_split6j_kernel(
+    const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
+    const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
+    float *__restrict__ att_feat, float *__restrict__ desc, const float *__restrict__ pre) {
+    constexpr int C3 = K::T3 * 32, CM2 = K::TM2 * 32, LDSW = K::LDSW, X2W = K::X2W;
+    constexpr int TM1 = K::TM1, P3 = K::P3, PM1 = K::PM1, PM2 = K::PM2;
+    constexpr int N3 = K::N3, NM1 = K::NM1;
+    constexpr int KN = K::KN, GPT = K::GPT, CW = K::CW;
+    static_assert(K::RT == 1 && CW == 4, "level-3 configuration");
+    __shared__ __attribute__((aligned(16))) float sA[SJT * 32 * LDSW];
+    __shared__ __attribute__((aligned(16))) float sX2[SJT][GPT * X2W];
+    __shared__ int sMax[SJT][CW][32];
+    const float *eb = table;  // epilogue constants from global memory
+    const int lane = threadIdx.x & 63, cw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, j = lane & 31;
+    const int NT = G / GPT;
+    const int NPAIR = (NT + 1) / 2;
+    float *A = sA;
+    const bool writer = KN == 32 ? j == 31 : (j & 15) == 15;
+    auto gsum_w = [&](float v) { return KN == 32 ? half_sum_hi(v) : row_sum16(v); };
+    auto gsum_b = [&](float v) { return KN == 32 ? half_bcast(half_sum_hi(v), h) : row_sum16(v); };
+    auto gmax_w = [&](float v) { return KN == 32 ? half_max_hi_nonneg(v) : row_max16_nonneg(v); };
+    auto gmax_b = [&](float v) {
+        return KN == 32 ? half_bcast(half_max_hi_nonneg(v), h) : row_max16_nonneg(v);
+    };
+    const int c3 = cw * P3, m1 = cw * PM1, m2 = cw * PM2;
+    const FragSeq det_g{K::G_DG + cw * K::P1, 1}, desc_g{K::G_EG + cw * K::P1, 1};
+    const FragSeq m1x1{K::G_M1 + m1 * 3 * N3 + N3, 3 * N3};
+    const FragSeq m1em{K::G_M1 + m1 * 3 * N3 + 2 * N3, 3 * N3};
+    const FragSeq fm2{K::G_M2 + m2 * NM1, NM1};
+
+    Carry6 carry;
+    {
+        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table));
+#pragma unroll
+        for (int i = 0; i < K::P1; ++i) ld6(wt, det_g.base + i * det_g.stride, lane, carry[i]);
+    }
+    for (int pb = blockIdx.x; pb < NPAIR; pb += gridDim.x) {
+        // a tile past the end recomputes the last tile (identical values, identical stores)
+        int t[SJT], g[SJT];
+        size_t row[SJT];
+        const float *prow[SJT];
+        float2 gin[SJT];
+#pragma unroll
+        for (int jt = 0; jt < SJT; ++jt) {
+            t[jt] = min(2 * pb + jt, NT - 1);
+            g[jt] = t[jt] * GPT + (KN == 32 ? 0 : j >> 4);
+            row[jt] = (size_t)t[jt] * 32 + j;
+            prow[jt] = pre + (size_t)gidx[row[jt]] * (2 * K::T1 * 32);
+            gin[jt] = *reinterpret_cast<const float2 *>(geom + row[jt] * 4 + 2 * h);
+        }
+        uint64_t tba = reinterpret_cast<uint64_t>(table);
+        asm volatile("" : "+s"(tba));
+        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
+        Carry6 ca, cb;
+        tile_sync();  // previous pair's readers of A are done
+
+        // ---- detector -> emb
+        f32x16 emb[P3][SJT];
+        conv_stack_split6j<K, PM1>(wt, eb, K::G_DG, K::G_D2, K::G_D3, K::E_D2, K::E_D3, A, cw, lane, emb, carry,
+                                   m1em, ca, prow, gin);
+
+        // ---- attention per tile
+#pragma unroll
+        for (int jt = 0; jt < SJT; ++jt) {
+            int mi = __float_as_int(emb[0][jt][0]);
+#pragma unroll
+            for (int i = 0; i < P3; ++i)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(emb[i][jt][q]));
+            mi = max(mi, __shfl_xor(mi, 32));
+            if (h == 0) sMax[jt][cw][j] = mi;
+        }
+        tile_sync();
+        float a[SJT];
+#pragma unroll
+        for (int jt = 0; jt < SJT; ++jt) {
+            int xm = sMax[jt][0][j];
+#pragma unroll
+            for (int c = 1; c < CW; ++c) xm = max(xm, sMax[jt][c][j]);
+            const float x1 = __int_as_float(xm);
+            const float mx = gmax_b(x1);
+            const float e = expf(fsub_rn(x1, mx));
+            a[jt] = e / gsum_b(e);
+            if (cw == 0) {
+                const float *p = knn_xyz + row[jt] * 3;
+                const float kx = gsum_w(fmul_rn(a[jt], p[0]));
+                const float ky = gsum_w(fmul_rn(a[jt], p[1]));
+                const float kz = gsum_w(fmul_rn(a[jt], p[2]));
+                if (writer && h == 0) {
+                    kp[(size_t)g[jt] * 3 + 0] = kx;
+                    kp[(size_t)g[jt] * 3 + 1] = ky;
+                    kp[(size_t)g[jt] * 3 + 2] = kz;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < P3; ++i) {
+                f32x16 v, ea;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    ea[q] = fmul_rn(emb[i][jt][q], a[jt]);
+                    v[q] = gsum_w(ea[q]);
+                }
+                store_tile(att_feat + (size_t)g[jt] * C3, c3 + i, v, writer, h);
+                put_tile<LDSW>(A + jt * 32 * LDSW, c3 + i, j, h, ea);
+            }
+        }
+        tile_sync();
+
+        // ---- mlp1, emb * a part (y1 stays in registers through the descriptor stack)
+        f32x16 y1[PM1][SJT];
+        beta_pj<PM1, TM1 * 32>(eb + K::E_M1, m1, h, y1);
+        pipe_lds6_jt<N3, PM1, K::P1, SJT>(wt, lane, m1em, ChanBJ<LDSW>{A + j * LDSW, h}, y1, ca, desc_g, cb);
+        tile_sync();  // every wave has read emb * a
+
+        // ---- descriptor -> x1d
+        f32x16 x1d[P3][SJT];
+        const float *prow_d[SJT] = {prow[0] + K::T1 * 32, prow[1] + K::T1 * 32};
+        conv_stack_split6j<K, PM1>(wt, eb, K::G_EG, K::G_E2, K::G_E3, K::E_E2, K::E_E3, A, cw, lane, x1d, cb, m1x1,
+                                   ca, prow_d, gin);
+        tile_sync();  // every wave has read layer 3's input
+#pragma unroll
+        for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+            for (int i = 0; i < P3; ++i) {
+                f32x16 v;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = gmax_w(x1d[i][jt][q]);
+                if (writer) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        *reinterpret_cast<float4 *>(sX2[jt] + (KN == 32 ? 0 : j >> 4) * X2W + (c3 + i) * 32 + 8 * r +
+                                                    4 * h) = make_float4(v[4 * r], v[4 * r + 1], v[4 * r + 2],
+                                                                         v[4 * r + 3]);
+                }
+                put_tile<LDSW>(A + jt * 32 * LDSW, c3 + i, j, h, x1d[i][jt]);
+            }
+        tile_sync();
+
+        // ---- mlp1, x2 part: one matrix-vector product per group, the weight rows shared by
+        // both tiles' groups
+        {
+            constexpr int CH = C3 / 2;
+            float v[PM1][SJT][GPT];
+#pragma unroll
+            for (int i = 0; i < PM1; ++i) {
+#pragma unroll
+                for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+                    for (int g2 = 0; g2 < GPT; ++g2) v[i][jt][g2] = 0.f;
+                const float *wr = table + K::F_X2 + (size_t)((m1 + i) * 32 + j) * C3 + h * CH;
+#pragma unroll 8
+                for (int c4 = 0; c4 < CH / 4; ++c4) {
+                    const float4 wv = *reinterpret_cast<const float4 *>(wr + c4 * 4);
+#pragma unroll
+                    for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+                        for (int g2 = 0; g2 < GPT; ++g2) {
+                            const float4 xv = *reinterpret_cast<const float4 *>(sX2[jt] + g2 * X2W + h * CH + c4 * 4);
+                            v[i][jt][g2] = fmaf(wv.x, xv.x, v[i][jt][g2]);
+                            v[i][jt][g2] = fmaf(wv.y, xv.y, v[i][jt][g2]);
+                            v[i][jt][g2] = fmaf(wv.z, xv.z, v[i][jt][g2]);
+                            v[i][jt][g2] = fmaf(wv.w, xv.w, v[i][jt][g2]);
+                        }
+                }
+#pragma unroll
+                for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+                    for (int g2 = 0; g2 < GPT; ++g2) v[i][jt][g2] = fadd_rn(v[i][jt][g2], __shfl_xor(v[i][jt][g2], 32));
+            }
+            const int mg = KN == 32 ? 0 : j >> 4;
+#pragma unroll
+            for (int i = 0; i < PM1; ++i)
+#pragma unroll
+                for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int src = (q & 3) + 8 * (q >> 2) + 4 * h;
+                        float av = __shfl(v[i][jt][0], src);
+                        if constexpr (GPT == 2) {
+                            const float bv = __shfl(v[i][jt][1], src);
+                            av = mg ? bv : av;
+                        }
+                        y1[i][jt][q] = fadd_rn(y1[i][jt][q], av);
+                    }
+        }
+        pipe_lds6_jt<N3, PM1, PM2, SJT>(wt, lane, m1x1, ChanBJ<LDSW>{A + j * LDSW, h}, y1, ca, fm2, cb);
+        relu_j(y1);
+        tile_sync();  // every wave has read x1d
+        put_j<LDSW>(A, m1, j, h, y1);
+        tile_sync();
+
+        // ---- mlp2 + k-max -> descriptor; prefetches the next pair's first chunk
+        f32x16 y2[PM2][SJT];
+        beta_pj<PM2, CM2>(eb + K::E_M2, m2, h, y2);
+        pipe_lds6_jt<NM1, PM2, K::P1, SJT>(wt, lane, fm2, ChanBJ<LDSW>{A + j * LDSW, h}, y2, cb, det_g, carry);
+        relu_j(y2);
+#pragma unroll
+        for (int jt = 0; jt < SJT; ++jt)
+#pragma unroll
+            for (int i = 0; i < PM2; ++i) {
+                f32x16 v;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = gmax_w(y2[i][jt][q]);
+                store_tile(desc + (size_t)g[jt] * CM2, m2 + i, v, writer, h);
+            }
+    }
+}
+
 template <class K>
 int launch_split6(const float *table, const float *geom, const float *knn_xyz, const int32_t *gidx,
                   const float *feats, int G, float *kp, float *att_feat, float *desc, const float *pre,
@@ -387,6 +687,29 @@ extern "C" int hreg_group_split6_l2(const float *table, const float *geom, const
                                     const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                                     float *desc, const float *pre, void *stream) {
     return launch_split6<S2x6>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre, stream);
+}
+
+// level 3 with two row tiles per wave (group_split6j_kernel): the precomputed-block form only
+extern "C" int hreg_group_split6j_l3(const float *table, const float *geom, const float *knn_xyz,
+                                     const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
+                                     float *desc, const float *pre, void *stream) {
+    using K = S3x6;
+    if (!table || !geom || !knn_xyz || !gidx || !feats || !kp || !att_feat || !desc || !pre || G < 0)
+        return HREG_ERR_INVALID;
+    if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(geom) & 15) ||
+        (reinterpret_cast<uintptr_t>(att_feat) & 15) || (reinterpret_cast<uintptr_t>(desc) & 15) ||
+        (reinterpret_cast<uintptr_t>(pre) & 15))
+        return HREG_ERR_INVALID;
+    if (G % K::GPT) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    const int NT = G / K::GPT, NPAIR = (NT + 1) / 2;
+    int grid = NPAIR;
+    const int cap = 256 * 2 * 2;  // two workgroups per CU, two rounds
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(group_split6j_kernel<K>, dim3(grid), dim3(256), 0, as_stream(stream), table, geom, knn_xyz,
+                       gidx, feats, G, kp, att_feat, desc, pre);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
 }
 
 extern "C" int hreg_group_split6_l3(const float *table, const float *geom, const float *knn_xyz,

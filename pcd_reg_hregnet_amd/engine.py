@@ -42,6 +42,8 @@ FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
 # accumulator-chained one (group_fused.hip); measured per level (tools/group_bench.py)
 SPLIT_L2 = os.environ.get("HREG_SPLIT_L2", "0") != "0"
 SPLIT_L3 = os.environ.get("HREG_SPLIT_L3", "1") != "0"
+# level 3 on the two-row-tile form of the channel-split kernel (hreg_group_split6j_l3)
+SPLIT_JT = True
 # the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
 # (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
 B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
@@ -936,6 +938,8 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
                       "hreg_group_split6_l3")
         pre = (gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl],
                     feats.shape[0]) if LEVEL_PRE else None)
+        if name == "hreg_group_split6_l3" and pre is not None and SPLIT_JT:
+            name = "hreg_group_split6j_l3"
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())
         sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)

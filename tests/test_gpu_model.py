@@ -713,3 +713,30 @@ def test_b6_kernels_deterministic(net):
         assert torch.equal(r["src_dst_weights_1"], runs[0]["src_dst_weights_1"])
     for a, b in zip(ref[:4], b6[:4]):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("G", [4096, 4094, 2])
+def test_level3_two_tile_kernel_bitwise(net, G):
+    """hreg_group_split6j_l3 (two 32-row tiles per wave sharing every weight piece) gives
+    hreg_group_split6_l3's bits -- keypoints, attentive features, descriptors -- including an
+    odd tile count (G = 4094: the last pair recomputes its tile) and a single tile."""
+    from pcd_reg_hregnet_amd import _lib, engine
+    P = net.prepared(torch.device("cuda"))
+    g = torch.Generator(device="cpu").manual_seed(G)
+    K, C, nrows = 16, 128, 2 * G
+    R = G * K
+    geom = torch.randn(R, 4, generator=g).cuda()
+    kx = torch.randn(R, 3, generator=g).cuda()
+    gidx = torch.randint(0, nrows, (R,), generator=g, dtype=torch.int32).cuda()
+    feats = torch.rand(nrows, C, generator=g).cuda()
+    pre = engine.gemm([engine._seg(feats, 0, C)], P.level_pre6[2], nrows)
+    outs = []
+    for name in ("hreg_group_split6_l3", "hreg_group_split6j_l3"):
+        kp = torch.empty(G, 3, device="cuda")
+        att = torch.empty(G, 256, device="cuda")
+        desc = torch.empty(G, 256, device="cuda")
+        _lib.call(name, P.l3s_table6, geom, kx, gidx, feats, G, kp, att, desc, pre, _lib.stream_handle())
+        outs.append((kp, att, desc))
+    torch.cuda.synchronize()
+    for a, b, nm in zip(outs[0], outs[1], ("kp", "att_feat", "desc")):
+        assert torch.equal(a, b), nm
