@@ -643,6 +643,14 @@ int hreg_nbr_head6(const float *table, const float *desc, const int32_t *gidx, c
  * 64 channels, activations through LDS): same arguments, table and outputs. */
 int hreg_nbr_head6s(const float *table, const float *desc, const int32_t *gidx, const float *geom,
                     int G, float *out, const float *pre, void *stream);
+/* hreg_corr_head6 / hreg_nbr_head6s with the 32-row tiles per workgroup chosen: row_tiles 0 =
+ * the default (2 at N1 <= 256: every streamed weight piece feeds both tiles; 1 at 512),
+ * 1 or 2 (2 only at N1 <= 256); the same outputs bit for bit. */
+int hreg_corr_head6x(const float *table, int N1, const float *small, const float *ud0, const float *ud1,
+                     const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                     int row_tiles, void *stream);
+int hreg_nbr_head6sx(const float *table, const float *desc, const int32_t *gidx, const float *geom,
+                     int G, float *out, const float *pre, int row_tiles, void *stream);
 
 /* Diagnostic: the register FPS kernel (weights optional) with per-iteration clock
  * stamps [b][m] (tools/op_bench.py stamps) -- same selection as the two FPS entries. */

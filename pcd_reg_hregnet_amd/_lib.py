@@ -98,6 +98,8 @@ _SIGS = {
     "hreg_corr_head6_table_floats": [_i],
     "hreg_coarse_head6": [_vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
     "hreg_corr_head6": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],
+    "hreg_corr_head6x": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _i, _vp],
+    "hreg_nbr_head6sx": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _i, _vp],
     "hreg_mlp_head": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "hreg_mlp_head_table_floats": [_i],
     "hreg_mlp_head6": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],

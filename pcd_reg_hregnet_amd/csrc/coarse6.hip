@@ -45,28 +45,28 @@ struct CorrCfg {
     static constexpr int TABLE = F_END + NE;
 };
 
-// HREG_COARSE_JT: 32-row tiles per workgroup.  2: every wave computes its P output tiles
-// for both row tiles, so each streamed weight chunk feeds twice the MFMAs (the one-tile
-// weight stream, 512 B of pieces per MFMA, keeps the CU's texture-data return unit ~82 %
-// busy) -- but the 64-row activation buffer (132 KB) leaves one workgroup per CU, and at
-// half the waves it measured slower (154 vs 134 us).  Default 1.
-#ifndef HREG_COARSE_JT
-#define HREG_COARSE_JT 1
-#endif
-constexpr int JT = HREG_COARSE_JT, RW = 32 * JT;  // row tiles / rows per workgroup
+// JT: 32-row tiles per workgroup.  2: every wave computes its P output tiles for both row
+// tiles, so each streamed weight chunk feeds twice the MFMAs (the one-tile weight stream,
+// 512 B of pieces per MFMA, keeps the CU's texture-data return unit ~82 % busy).  At C = 512
+// the 64-row activation buffer (132 KB) leaves one workgroup per CU and measured slower (154
+// vs 134 us): JT = 1 there; at C <= 256 (FineReg heads, neighbour branch; 73 KB) two
+// workgroups still fit per CU: JT = 2 (corr_jt; same products and order: the same bits).
+template <class K>
+constexpr int corr_jt() { return K::C <= 256 ? 2 : 1; }
 
 // NBR: CoarseReg's neighbour branch (layers.py:315-337, nbr_head6_kernel's job): rows
 // [desc[nbr] C | dxyz, |d|] through convs_2, the descriptor block precomputed per point
 // with its beta (ud1 = engine.nbr_pre6 rows gathered by gidx; no per-keypoint block), the
 // 4 geometry columns as k-steps 0, 1 of each lane half (small = geom [rows][4]); output
 // sum_j a_j desc[nbr_j] (knn_xyz = desc, att = out; no corres).
-template <class K, bool NBR>
+template <class K, bool NBR, int JT>
 __global__ __launch_bounds__(K::CW * 64) void coarse_head6_kernel(
     const float *__restrict__ table, const float *__restrict__ small, const float *__restrict__ ud0,
     const float *__restrict__ ud1, const int32_t *__restrict__ gidx, const float *__restrict__ knn_xyz, int G,
     float *__restrict__ corres, float *__restrict__ att) {
     constexpr int C = K::C, T = K::T, P = K::P, CW = K::CW, LDSW = K::LDSW, NCH = K::NCH;
     constexpr int G_1 = K::G_1, G_2 = K::G_2, G_3 = K::G_3, F_END = K::F_END, NE = K::NE;
+    constexpr int RW = 32 * JT;  // rows per workgroup step
     (void)T;
     __shared__ float ep[NE];
     __shared__ __attribute__((aligned(16))) float sA[RW * LDSW];
@@ -230,16 +230,28 @@ __global__ __launch_bounds__(K::CW * 64) void coarse_head6_kernel(
     }
 }
 
-template <class K, bool NBR = false>
-int launch_corr6(const float *table, const float *small, const float *ud0, const float *ud1, const int32_t *gidx,
-                 const float *knn_xyz, int G, float *corres, float *att, void *stream) {
+template <class K, bool NBR, int JT>
+int launch_corr6_jt(const float *table, const float *small, const float *ud0, const float *ud1, const int32_t *gidx,
+                    const float *knn_xyz, int G, float *corres, float *att, void *stream) {
     const int NW = (G * KH / 32 + JT - 1) / JT;
     const int cap = 256 * (JT == 1 ? 4 : 2);  // a few rounds of the resident workgroups
     const int grid = NW < cap ? NW : cap;
-    hipLaunchKernelGGL((coarse_head6_kernel<K, NBR>), dim3(grid), dim3(K::CW * 64), 0, as_stream(stream), table, small,
-                       ud0, ud1, gidx, knn_xyz, G, corres, att);
+    hipLaunchKernelGGL((coarse_head6_kernel<K, NBR, JT>), dim3(grid), dim3(K::CW * 64), 0, as_stream(stream), table,
+                       small, ud0, ud1, gidx, knn_xyz, G, corres, att);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
+}
+
+// row_tiles: 0 = the configuration's default (corr_jt), 1 or 2 (A/B and the bitwise test)
+template <class K, bool NBR = false>
+int launch_corr6(const float *table, const float *small, const float *ud0, const float *ud1, const int32_t *gidx,
+                 const float *knn_xyz, int G, float *corres, float *att, void *stream, int row_tiles = 0) {
+    const int jt = row_tiles ? row_tiles : corr_jt<K>();
+    if constexpr (K::C <= 256) {
+        if (jt == 2) return launch_corr6_jt<K, NBR, 2>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+    }
+    if (jt == 1) return launch_corr6_jt<K, NBR, 1>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+    return HREG_ERR_UNSUPPORTED;
 }
 
 }  // namespace
@@ -270,9 +282,9 @@ extern "C" int hreg_corr_head6_table_floats(int N1) {
     return N1 == 512 ? Corr512::TABLE : N1 == 256 ? Corr256::TABLE : N1 == 128 ? Corr128::TABLE : -1;
 }
 
-extern "C" int hreg_corr_head6(const float *table, int N1, const float *small, const float *ud0, const float *ud1,
-                               const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
-                               void *stream) {
+extern "C" int hreg_corr_head6x(const float *table, int N1, const float *small, const float *ud0, const float *ud1,
+                                const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                                int row_tiles, void *stream) {
     if (!table || !small || !ud0 || !ud1 || !gidx || !knn_xyz || !corres || !att || G < 0)
         return HREG_ERR_INVALID;
     if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(small) & 15) ||
@@ -282,9 +294,18 @@ extern "C" int hreg_corr_head6(const float *table, int N1, const float *small, c
     if ((G * KH) % 32) return HREG_ERR_INVALID;  // whole 32-row tiles
     if (N1 != 512 && N1 != 256 && N1 != 128) return HREG_ERR_UNSUPPORTED;
     if (!G) return HREG_OK;
-    if (N1 == 512) return launch_corr6<Corr512>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
-    if (N1 == 256) return launch_corr6<Corr256>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
-    return launch_corr6<Corr128>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
+    if (row_tiles < 0 || row_tiles > 2) return HREG_ERR_INVALID;
+    if (N1 == 512)
+        return launch_corr6<Corr512>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream, row_tiles);
+    if (N1 == 256)
+        return launch_corr6<Corr256>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream, row_tiles);
+    return launch_corr6<Corr128>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream, row_tiles);
+}
+
+extern "C" int hreg_corr_head6(const float *table, int N1, const float *small, const float *ud0, const float *ud1,
+                               const int32_t *gidx, const float *knn_xyz, int G, float *corres, float *att,
+                               void *stream) {
+    return hreg_corr_head6x(table, N1, small, ud0, ud1, gidx, knn_xyz, G, corres, att, 0, stream);
 }
 
 extern "C" int hreg_coarse_head6(const float *table, const float *small, const float *ud0, const float *ud1,
@@ -296,8 +317,8 @@ extern "C" int hreg_coarse_head6(const float *table, const float *small, const f
 // hreg_nbr_head6 (group_head.hip) on the channel-split kernel: same arguments and table
 // (engine.nbr_head_table6 -- the layout of coarse_head_table6 at C = 256 with a 2-k-step
 // first block), bitwise-identical attention sums
-extern "C" int hreg_nbr_head6s(const float *table, const float *desc, const int32_t *gidx, const float *geom,
-                               int G, float *out, const float *pre, void *stream) {
+extern "C" int hreg_nbr_head6sx(const float *table, const float *desc, const int32_t *gidx, const float *geom,
+                                int G, float *out, const float *pre, int row_tiles, void *stream) {
     if (!table || !desc || !gidx || !geom || !out || !pre || G < 0) return HREG_ERR_INVALID;
     if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(desc) & 15) ||
         (reinterpret_cast<uintptr_t>(geom) & 7) || (reinterpret_cast<uintptr_t>(out) & 15) ||
@@ -305,5 +326,11 @@ extern "C" int hreg_nbr_head6s(const float *table, const float *desc, const int3
         return HREG_ERR_INVALID;
     if ((G * KH) % 32) return HREG_ERR_INVALID;
     if (!G) return HREG_OK;
-    return launch_corr6<Nbr256, true>(table, geom, nullptr, pre, gidx, desc, G, nullptr, out, stream);
+    if (row_tiles < 0 || row_tiles > 2) return HREG_ERR_INVALID;
+    return launch_corr6<Nbr256, true>(table, geom, nullptr, pre, gidx, desc, G, nullptr, out, stream, row_tiles);
+}
+
+extern "C" int hreg_nbr_head6s(const float *table, const float *desc, const int32_t *gidx, const float *geom,
+                               int G, float *out, const float *pre, void *stream) {
+    return hreg_nbr_head6sx(table, desc, gidx, geom, G, out, pre, 0, stream);
 }

@@ -44,6 +44,9 @@ SPLIT_L2 = os.environ.get("HREG_SPLIT_L2", "0") != "0"
 SPLIT_L3 = os.environ.get("HREG_SPLIT_L3", "1") != "0"
 # level 3 on the two-row-tile form of the channel-split kernel (hreg_group_split6j_l3)
 SPLIT_JT = True
+# 32-row tiles per workgroup of the channel-split FineReg / neighbour heads (0: the library's
+# default, two at N1 <= 256; hreg_corr_head6x / hreg_nbr_head6sx)
+HEAD_ROW_TILES = 0
 # the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
 # (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
 B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
@@ -1053,8 +1056,11 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
         b6 = B6_HEADS and HEAD_PRE
         pre = gemm([_seg(desc3, 0, C)], P.nbr_pre6 if b6 else P.nbr_pre, G2) if HEAD_PRE else None
         if b6:
-            call("hreg_nbr_head6s" if SPLIT_NBR else "hreg_nbr_head6", P.nbr_table6, desc3, gself, geom_self, G2,
-                 nbr, pre, _stream())
+            if SPLIT_NBR:
+                call("hreg_nbr_head6sx", P.nbr_table6, desc3, gself, geom_self, G2, nbr, pre, HEAD_ROW_TILES,
+                     _stream())
+            else:
+                call("hreg_nbr_head6", P.nbr_table6, desc3, gself, geom_self, G2, nbr, pre, _stream())
         else:
             call("hreg_nbr_head", P.nbr_table, desc3, gself, geom_self, G2, nbr, pre, _stream())
     else:
@@ -1130,8 +1136,8 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
             _gemm_batched_desc((P.fine_pre6 if B6_HEADS else P.fine_pre)[name], src_desc, B * N, C,
                                pre, x1=dst_desc)
         if B6_HEADS and HEAD_PRE and SPLIT_FINE:
-            call("hreg_corr_head6", P.fine_table6[name], N1, small, pre[0], pre[1], gidx, kx, B * N,
-                 corres, att, _stream())
+            call("hreg_corr_head6x", P.fine_table6[name], N1, small, pre[0], pre[1], gidx, kx, B * N,
+                 corres, att, HEAD_ROW_TILES, _stream())
         elif B6_HEADS and HEAD_PRE:
             call("hreg_fine_head6", P.fine_table6[name], C, small, gidx, kx, B * N, corres, att,
                  pre[0], pre[1], _stream())

@@ -740,3 +740,30 @@ def test_level3_two_tile_kernel_bitwise(net, G):
     torch.cuda.synchronize()
     for a, b, nm in zip(outs[0], outs[1], ("kp", "att_feat", "desc")):
         assert torch.equal(a, b), nm
+
+
+def test_heads_two_tile_bitwise(net):
+    """The FineReg heads (N1 = 256 / 128) and the neighbour branch on two 32-row tiles per
+    workgroup (hreg_corr_head6x / hreg_nbr_head6sx, row_tiles 2: the default) give the
+    one-tile kernels' bits: the whole forward compared with engine.HEAD_ROW_TILES = 1."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    s, d, _, _ = synthetic.lidar_batch(3, 16384, seed0=91)
+    src, dst = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    outs = []
+    old = engine.HEAD_ROW_TILES
+    try:
+        for rt in (1, 0):
+            engine.HEAD_ROW_TILES = rt
+            with torch.no_grad():
+                outs.append(engine.hregnet_forward(P, src, dst))
+    finally:
+        engine.HEAD_ROW_TILES = old
+    torch.cuda.synchronize()
+    a, b = outs
+    for key in a:
+        if isinstance(a[key], torch.Tensor):
+            assert torch.equal(a[key], b[key]), key
+    for i in range(3):
+        assert torch.equal(a["rotation"][i], b["rotation"][i])
+        assert torch.equal(a["translation"][i], b["translation"][i])
