@@ -49,10 +49,11 @@ struct CorrCfg {
 // tiles, so each streamed weight chunk feeds twice the MFMAs (the one-tile weight stream,
 // 512 B of pieces per MFMA, keeps the CU's texture-data return unit ~82 % busy).  At C = 512
 // the 64-row activation buffer (132 KB) leaves one workgroup per CU and measured slower (154
-// vs 134 us): JT = 1 there; at C <= 256 (FineReg heads, neighbour branch; 73 KB) two
-// workgroups still fit per CU: JT = 2 (corr_jt; same products and order: the same bits).
+// vs 134 us): JT = 1 there; at C = 256 (FineReg level-2 head, neighbour branch; 73 KB) two
+// workgroups still fit per CU: JT = 2 (corr_jt; same products and order: the same bits); the
+// C = 128 head (a smaller grid) measured 48 vs 37 us on two tiles and stays on one.
 template <class K>
-constexpr int corr_jt() { return K::C <= 256 ? 2 : 1; }
+constexpr int corr_jt() { return K::C == 256 ? 2 : 1; }
 
 // NBR: CoarseReg's neighbour branch (layers.py:315-337, nbr_head6_kernel's job): rows
 // [desc[nbr] C | dxyz, |d|] through convs_2, the descriptor block precomputed per point

@@ -1,10 +1,11 @@
 """Paired A/B timing of the bench's graph executor in ONE process (run-to-run box noise of
-separate bench processes is +-3 % at --steps 20).  Every variant gets its own GraphPipeline,
-captured while its switches are set (hreg_debug_set keys, engine module attributes); the
-timed rounds then alternate A B A B ... exactly as bench.py times one (barrier-free: one GPU).
+separate bench processes is +-3 % at --steps 20).  Every variant gets two GraphPipelines,
+captured while its switches are set (engine module attributes) and created in mirrored order
+(A B B A) to cancel the creation-order bias; the timed rounds then alternate over all of them
+exactly as bench.py times one (barrier-free: one GPU).
 
 usage: python tools/ab_graph.py [--steps 20] [--reps 8] VARIANT [VARIANT ...]
-  VARIANT = comma-separated key=value (or "base"): fps_track=1,fps_pad_kb=140,engine.FLAG=0
+  VARIANT = comma-separated key=value (or "base"): engine.FLAG=0
 """
 import argparse
 import json
@@ -61,9 +62,13 @@ def main():
     P = net.prepared(dev)
     s, d, _, _ = bench.shard_batch(0, bench.PAIRS_PER_GPU, bench.POINTS)
     src, dst = torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev)
+    # every variant twice, created in mirrored order (A B ... B A): pipelines created earlier
+    # measured ~3-4 % faster than later ones in the same process (the same variant in first and
+    # second position, tools/ab_graph.py base base), so a single creation order biases the A/B
+    order = list(a.variants) + list(a.variants)[::-1]
     pipes = []
     with torch.no_grad():
-        for v in a.variants:
+        for v in order:
             undo = apply(v, lib, engine)
             g = engine.GraphPipeline(P, src, dst, lanes=a.steps)
             g.prepare(a.warmup)
@@ -74,16 +79,22 @@ def main():
             revert(undo, lib, engine)
             pipes.append(g)
     times = {v: [] for v in a.variants}
+    inst = [[] for _ in order]  # per created instance (the creation-order bias)
     with torch.no_grad():
         for r in range(a.reps):
-            order = a.variants if r % 2 == 0 else a.variants[::-1]
-            for v, g in ((v, pipes[a.variants.index(v)]) for v in order):
+            idxs = list(range(len(order))) if r % 2 == 0 else list(range(len(order)))[::-1]
+            for i in idxs:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                g.run_forwards(a.steps, stream=True)
+                pipes[i].run_forwards(a.steps, stream=True)
                 torch.cuda.synchronize()
-                times[v].append((time.perf_counter() - t0) / a.steps * 1e3)
-            print(f"rep {r}: " + "  ".join(f"{v} {times[v][-1]:.4f}" for v in a.variants), flush=True)
+                ms = (time.perf_counter() - t0) / a.steps * 1e3
+                times[order[i]].append(ms)
+                inst[i].append(ms)
+            print(f"rep {r}: " + "  ".join(f"{order[i]}#{i} {inst[i][-1]:.4f}" for i in range(len(order))),
+                  flush=True)
+    print("per instance (creation order):",
+          [(order[i], round(statistics.median(inst[i]), 4)) for i in range(len(order))])
     base = statistics.median(times[a.variants[0]])
     out = {}
     for v in a.variants:
