@@ -274,6 +274,8 @@ def level_kernel(engine, lv: int) -> str:
     split = engine.SPLIT_L2 if lv == 2 else engine.SPLIT_L3
     b6 = engine.B6_L2 if lv == 2 else engine.B6_L3
     if split:
+        if b6 and lv == 3 and engine.SPLIT_JT and engine.LEVEL_PRE:
+            return "group_split6j_kernel"  # two row tiles per workgroup (csrc/group_split6.hip)
         return "group_split6_kernel" if b6 else "group_split_kernel"
     if b6 and lv == 2 and engine.PAIR_L2 and engine.LEVEL_PRE:
         return "group_pair6_kernel"
@@ -285,7 +287,7 @@ def pmc_traffic(kernel: str):
     (profiles/r*_traffic.json, made by tools/rocpd_summary.py traffic; the latest round
     that measured every kernel of the family)."""
     names = [n.split(" (")[0] for n in kernel.split(" + ")]
-    for rnd in ("r2", "r1"):
+    for rnd in ("r3", "r2", "r1"):
         path = os.path.join(REPO, "profiles", f"{rnd}_traffic.json")
         try:
             per = json.load(open(path))["bytes_per_launch"]
