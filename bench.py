@@ -168,14 +168,17 @@ MFMA_ENTRIES = {
     "hreg_group6x2_l2": ("level", _level_work(2)),
     "hreg_group_split6_l2": ("level", _level_work(2)),
     "hreg_group_split6_l3": ("level", _level_work(3)),
+    "hreg_group_split6j_l3": ("level", _level_work(3)),
     "hreg_group6_l3": ("level", _level_work(3)),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
     "hreg_fine_head6": ("head", _fine6_work),
     "hreg_nbr_head6": ("head", _nbr_work),
     "hreg_nbr_head6s": ("head", _nbr_work),
+    "hreg_nbr_head6sx": ("head", _nbr_work),
     "hreg_coarse_head6": ("head", _coarse6_work),
     "hreg_corr_head6": ("head", _corr6_work),
+    "hreg_corr_head6x": ("head", _corr6_work),
     "hreg_mlp_head": ("mlp", _mlp_work),
     "hreg_mlp_head6": ("mlp", _mlp_work),
 }

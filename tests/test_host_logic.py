@@ -316,3 +316,21 @@ def test_level1_prefetch_key_identity_and_version():
     assert pf.key[0]() is None
     pf.discard()
     assert pf.key is None and not pf.matches(s, d)
+
+
+def test_bench_times_every_mfma_entry_the_engine_calls():
+    """bench.MfmaTimer brackets the level / head kernels by C-ABI entry name: every fused
+    level or head entry engine.py can launch must be in bench.MFMA_ENTRIES, or the roofline
+    family silently drops it (r3: hreg_group_split6j_l3 / hreg_corr_head6x / hreg_nbr_head6sx
+    were missing, so the level-3 launches fell out of `roofline.achieved`)."""
+    import os
+    import re
+    import bench
+    src = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "pcd_reg_hregnet_amd",
+                            "engine.py")).read()
+    names = set(re.findall(r'"(hreg_(?:group_l\d\w*|group\d?\w*_l\d|group_split\w*|\w*head\d?\w*))"', src))
+    names -= {"hreg_head_out"}
+    names = {n for n in names if not n.endswith("_table_floats")}
+    assert "hreg_group_split6j_l3" in names and "hreg_corr_head6x" in names
+    missing = sorted(n for n in names if n not in bench.MFMA_ENTRIES)
+    assert not missing, missing
