@@ -18,6 +18,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -265,8 +266,10 @@ class MfmaTimer:
 def entry_peak(name: str) -> float:
     """MFMA peak (fp32-equivalent TFLOP/s) of a C-ABI entry's kernel: bf16x6 kernels
     (hreg_group_l1_6, hreg_group6_*, hreg_group_split6_*, hreg_*_head6) run on the bf16
-    matrix cores, the others on v_mfma_f32_32x32x2_f32."""
-    b6 = name.endswith(("6", "6s")) or "6_" in name or "6x2_" in name
+    matrix cores, the others on v_mfma_f32_32x32x2_f32.  (r3: a suffix rule missed
+    hreg_group_split6j_l3 / hreg_corr_head6x / hreg_nbr_head6sx and priced them at the fp32
+    peak, inflating roofline.frac; tests/test_host_logic.py pins every entry's peak.)"""
+    b6 = re.search(r"(l1_6|group6|split6|head6|gemm6)", name) is not None
     return PEAK_B6_TFLOPS if b6 else PEAK_FP32_MFMA_TFLOPS
 
 

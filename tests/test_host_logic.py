@@ -334,3 +334,18 @@ def test_bench_times_every_mfma_entry_the_engine_calls():
     assert "hreg_group_split6j_l3" in names and "hreg_corr_head6x" in names
     missing = sorted(n for n in names if n not in bench.MFMA_ENTRIES)
     assert not missing, missing
+
+
+def test_bench_entry_peaks():
+    """Every timed MFMA entry is priced at its kernel's peak: the bf16x6 kernels (built on
+    mfma_chain.h / split_chain.h, v_mfma_f32_32x32x16_bf16) at the bf16 dense peak / 6, the
+    fp32-MFMA kernels at the f32 matrix peak.  r3: hreg_group_split6j_l3, hreg_corr_head6x and
+    hreg_nbr_head6sx were priced at the fp32 peak (roofline.frac 0.71 instead of 0.45)."""
+    import bench
+    b6 = {"hreg_group_l1_6", "hreg_group_l1_6g", "hreg_group6_l2", "hreg_group6x2_l2",
+          "hreg_group_split6_l2", "hreg_group_split6_l3", "hreg_group_split6j_l3", "hreg_group6_l3",
+          "hreg_fine_head6", "hreg_nbr_head6", "hreg_nbr_head6s", "hreg_nbr_head6sx",
+          "hreg_coarse_head6", "hreg_corr_head6", "hreg_corr_head6x", "hreg_mlp_head6", "hreg_gemm6"}
+    for name in set(bench.MFMA_ENTRIES) | {"hreg_gemm", "hreg_gemm6"}:
+        want = bench.PEAK_B6_TFLOPS if name in b6 else bench.PEAK_FP32_MFMA_TFLOPS
+        assert bench.entry_peak(name) == want, name
