@@ -673,6 +673,11 @@ int hreg_debug_fps_cluster(int b, int n, int m, const float *points, float *temp
                            int32_t *idx, float *sampled_xyz, int stall, unsigned polls_max,
                            void *stream);
 
+/* Diagnostic: hreg_gemm_tn with S row splits instead of its own choice (ws: S * N * K
+ * floats) -- tools/tn_split_sweep.py. */
+int hreg_debug_gemm_tn_s(const float *A, int lda, const float *B, int ldb, int R, int N, int K,
+                         float beta, void *ws, float *out, void *stream, int S);
+
 /* library build id (for the loaded-.so audit) */
 const char *hreg_version(void);
 

@@ -624,13 +624,12 @@ extern "C" size_t hreg_gemm_tn_ws_bytes(int R, int N, int K) {
     return (size_t)tn_splits(R, N, K) * N * K * sizeof(float);
 }
 
-extern "C" int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N, int K,
-                            float beta, void *ws, float *out, void *stream) {
-    if (!A || !B || !ws || !out || R <= 0 || N <= 0 || K <= 0 || lda < N || ldb < K)
+static int gemm_tn_launch(const float *A, int lda, const float *B, int ldb, int R, int N, int K, float beta,
+                          void *ws, float *out, void *stream, int S) {
+    if (!A || !B || !ws || !out || R <= 0 || N <= 0 || K <= 0 || lda < N || ldb < K || S <= 0)
         return HREG_ERR_INVALID;
     if ((size_t)R * lda * sizeof(float) >= ((size_t)1 << 31) || (size_t)R * ldb * sizeof(float) >= ((size_t)1 << 31))
         return HREG_ERR_UNSUPPORTED;  // (buffer-descriptor addressing)
-    const int S = tn_splits(R, N, K);
     int rps = (R + S - 1) / S;
     rps = (rps + TN_ROWS - 1) / TN_ROWS * TN_ROWS;
     hipStream_t st = as_stream(stream);
@@ -656,6 +655,17 @@ extern "C" int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, in
                            S, NK, beta, out);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
+}
+
+extern "C" int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N, int K,
+                            float beta, void *ws, float *out, void *stream) {
+    return gemm_tn_launch(A, lda, B, ldb, R, N, K, beta, ws, out, stream, R > 0 ? tn_splits(R, N, K) : 1);
+}
+
+// tools only (tools/tn_split_sweep.py): the same GEMM with S row splits (ws: S * N * K floats)
+extern "C" int hreg_debug_gemm_tn_s(const float *A, int lda, const float *B, int ldb, int R, int N, int K,
+                                    float beta, void *ws, float *out, void *stream, int S) {
+    return gemm_tn_launch(A, lda, B, ldb, R, N, K, beta, ws, out, stream, S);
 }
 
 extern "C" int hreg_transpose(const float *in, int R, int C, float *out, void *stream) {

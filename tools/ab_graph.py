@@ -5,7 +5,9 @@ captured while its switches are set (engine module attributes) and created in mi
 exactly as bench.py times one (barrier-free: one GPU).
 
 usage: python tools/ab_graph.py [--steps 20] [--reps 8] VARIANT [VARIANT ...]
-  VARIANT = comma-separated key=value (or "base"): engine.FLAG=0
+  VARIANT = comma-separated key=value (or "base"): engine.FLAG=0, or probe.nofps1=1 (timing
+  probe, results wrong: the level-1 FPS replaced by a copy of a cached selection, to price the
+  FPS's share of the step)
 """
 import argparse
 import json
@@ -19,7 +21,24 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
-DBG = {"fps_track": 1, "fps_pad_kb": 2}
+def _nofps1(engine):
+    """engine.fps with the level-1 (unweighted, 16384-point) selection served from a cache
+    (one D2D copy per call) -- a timing probe only"""
+    real = engine.fps
+    cache = {}
+
+    def fps(xyz, npoint, weights=None, out=None):
+        if weights is not None or xyz.shape[1] != bench.POINTS:
+            return real(xyz, npoint, weights, out)
+        key = tuple(xyz.shape)
+        if key not in cache:
+            cache[key] = tuple(t.clone() for t in real(xyz, npoint))
+        if out is None:
+            return tuple(t.clone() for t in cache[key])
+        for o, c in zip(out, cache[key]):
+            o.copy_(c)
+        return out
+    return fps
 
 
 def apply(variant, lib, engine):
@@ -34,18 +53,17 @@ def apply(variant, lib, engine):
             old = getattr(engine, name)
             setattr(engine, name, type(old)(int(v)) if isinstance(old, (bool, int)) else v)
             undo.append(("engine", name, old))
+        elif k == "probe.nofps1" and int(v):
+            undo.append(("engine", "fps", engine.fps))
+            engine.fps = _nofps1(engine)
         else:
-            prev = lib.hreg_debug_set(DBG[k], int(v))
-            undo.append(("dbg", DBG[k], prev))
+            raise ValueError(f"unknown switch {k}")
     return undo
 
 
 def revert(undo, lib, engine):
     for kind, k, old in reversed(undo):
-        if kind == "engine":
-            setattr(engine, k, old)
-        else:
-            lib.hreg_debug_set(k, old)
+        setattr(engine, k, old)
 
 
 def main():
@@ -70,6 +88,7 @@ def main():
     with torch.no_grad():
         for v in order:
             undo = apply(v, lib, engine)
+            engine.fps(torch.cat([src, dst], 0), engine.LEVELS[0][0])  # (fills a probe's cache uncaptured)
             g = engine.GraphPipeline(P, src, dst, lanes=a.steps)
             g.prepare(a.warmup)
             g.prepare(a.steps)
