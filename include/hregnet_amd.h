@@ -379,6 +379,9 @@ int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N,
                  void *ws, float *out, void *stream);
 /* out [C][R] = in [R][C]^T */
 int hreg_transpose(const float *in, int R, int C, float *out, void *stream);
+/* y[i] += x[i] (fp32, one rounding) over n floats: the second gradient bucket of the
+ * two-stream training step added into the first */
+int hreg_add_into(const float *x, float *y, size_t n, void *stream);
 /* torch.optim.Adam step t (>= 1) over n floats, weight decay 0, amsgrad off */
 int hreg_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, size_t n,
                    float lr, float beta1, float beta2, float eps, int step, void *stream);

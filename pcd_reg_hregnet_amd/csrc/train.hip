@@ -466,6 +466,20 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g, 
     }
 }
 
+__global__ void add_into_kernel(const float4 *__restrict__ x, float4 *__restrict__ y, size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 a = x[i];
+        float4 b = y[i];
+        b.x = fadd_rn(b.x, a.x); b.y = fadd_rn(b.y, a.y); b.z = fadd_rn(b.z, a.z); b.w = fadd_rn(b.w, a.w);
+        y[i] = b;
+    }
+}
+
+__global__ void add_into_tail_kernel(const float *__restrict__ x, float *__restrict__ y, size_t i0, size_t n) {
+    for (size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        y[i] = fadd_rn(y[i], x[i]);
+}
+
 // row splits so that col_blocks x S reaches `target` workgroups (2048 = 8 per CU: a
 // streaming reduction needs several waves per SIMD in flight to reach HBM rate; for
 // the weight-gradient GEMM too, despite the extra N x K partials: A/B 235 vs 232
@@ -674,6 +688,24 @@ extern "C" int hreg_transpose(const float *in, int R, int C, float *out, void *s
     hipLaunchKernelGGL(transpose_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(32, 8), 0,
                        as_stream(stream), in, R, C, out);
     HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_add_into(const float *x, float *y, size_t n, void *stream) {
+    if (!x || !y) return HREG_ERR_INVALID;
+    if (!n) return HREG_OK;
+    hipStream_t st = as_stream(stream);
+    const bool al = !((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15);
+    const size_t n4 = al ? n / 4 : 0;
+    if (n4) {
+        hipLaunchKernelGGL(add_into_kernel, dim3(grid1d(n4)), dim3(256), 0, st, reinterpret_cast<const float4 *>(x),
+                           reinterpret_cast<float4 *>(y), n4);
+        HREG_CHECK_LAUNCH();
+    }
+    if (4 * n4 < n) {  // the < 4 tail of aligned buffers, or everything of unaligned ones
+        hipLaunchKernelGGL(add_into_tail_kernel, dim3(grid1d(n - 4 * n4)), dim3(256), 0, st, x, y, 4 * n4, n);
+        HREG_CHECK_LAUNCH();
+    }
     return HREG_OK;
 }
 

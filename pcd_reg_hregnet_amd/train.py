@@ -19,6 +19,7 @@ arithmetic op runs in the HIP library, which must be present (no CPU fallback).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -92,14 +93,47 @@ def col_sum(x: torch.Tensor, into: torch.Tensor | None = None) -> torch.Tensor:
 
 DIRECT_GRAD = True  # (A/B switch: False returns every parameter gradient to autograd)
 
+# Two-stream training step (train_graph.hregnet_train_forward(concurrent=True)): the src and
+# dst feature extractions run on two streams, and so do their backwards.  A layer records the
+# side it ran on; side 1 adds its parameter gradients into the gradient bucket's second buffer
+# (GradBucket(sides=2): p._grad_side1), side 0 into p.grad, so the two streams never add into
+# the same memory; GradBucket.collect adds the second buffer into the first (g_src + g_dst:
+# the same fp32 sum as autograd's serial accumulation, which is commutative for two terms).
+# The dst side's BN running-statistics updates are deferred (DEFERRED_RUNNING) and applied
+# after the src side's, in the reference's order.
+_SIDE = 0
+DEFERRED_RUNNING: list | None = None  # when a list: (mean, var, running_mean, running_var, momentum)
 
-def _grad_slot(p):
-    """p.grad when the backward may add to it in place (autograd's own accumulation into
-    an existing .grad: the flat gradient bucket is attached and zeroed every step), else
-    None (return the gradient to autograd)"""
+
+@contextlib.contextmanager
+def side(s: int, defer_running: bool = False):
+    """layers built inside run as side s (gradient bucket s); defer_running: their BN
+    running-statistics updates are queued in the yielded list instead of applied"""
+    global _SIDE, DEFERRED_RUNNING
+    old = (_SIDE, DEFERRED_RUNNING)
+    queued = [] if defer_running else None
+    _SIDE, DEFERRED_RUNNING = s, queued
+    try:
+        yield queued
+    finally:
+        _SIDE, DEFERRED_RUNNING = old
+
+
+def apply_running(updates) -> None:
+    """hreg_bn_running_update for queued (mean, var_unbiased, running_mean, running_var,
+    momentum) entries, in order, on the current stream"""
+    for mean, var, rm, rv, momentum in updates:
+        _lib.call("hreg_bn_running_update", mean, var, mean.shape[0], float(momentum), rm, rv, _stream())
+
+
+def _grad_slot(p, side: int = 0):
+    """The buffer the backward of a side-`side` layer may add p's gradient to in place
+    (autograd's own accumulation into an existing .grad: the flat gradient bucket is
+    attached and zeroed every step; side 1: the bucket's second buffer), else None (return
+    the gradient to autograd)"""
     if p is None or not p.requires_grad or not DIRECT_GRAD:
         return None
-    g = p.grad
+    g = p.grad if side == 0 else getattr(p, "_grad_side1", None)
     if g is None or not g.is_contiguous() or g.dtype != torch.float32:
         return None
     return g
@@ -175,15 +209,20 @@ class _ConvBNAct(torch.autograd.Function):
     def forward(ctx, x, W, bias, gamma, beta, running_mean, running_var, relu, momentum, eps,
                 wparam=None):
         R = x.shape[0]
-        fused = _conv_gemm_bn(x, W, bias, eps, momentum, running_mean, running_var)
+        defer = DEFERRED_RUNNING is not None and running_mean is not None
+        rm, rv = (None, None) if defer else (running_mean, running_var)
+        fused = _conv_gemm_bn(x, W, bias, eps, momentum, rm, rv)
         if fused is not None:
             y, mean, invstd, var = fused  # statistics (+ running update) in the GEMM's epilogue
         else:
             y = _conv_gemm(x, W, bias)
             mean, invstd, var = bn_stats(y, eps)
-            if running_mean is not None:
+            if rm is not None:
                 _lib.call("hreg_bn_running_update", mean, var, y.shape[1], float(momentum),
-                          running_mean, running_var, _stream())
+                          rm, rv, _stream())
+        if defer:
+            DEFERRED_RUNNING.append((mean, var, running_mean, running_var, momentum))
+        ctx.side = _SIDE
         C = y.shape[1]
         out = torch.empty_like(y)
         _lib.call("hreg_bn_apply", y, R, C, mean, invstd, gamma, beta, 1 if relu else 0, out,
@@ -207,9 +246,9 @@ class _ConvBNAct(torch.autograd.Function):
         # same fp32 sums autograd's accumulation would make (g_src + g_dst, added to the
         # zeroed .grad), without its two elementwise additions per parameter and use
         wp, bp, gp, btp = ctx.params
-        gw = _grad_slot(wp) if ctx.needs_input_grad[1] else None
-        gb = _grad_slot(bp) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        gg, gbt = _grad_slot(gp), _grad_slot(btp)
+        gw = _grad_slot(wp, ctx.side) if ctx.needs_input_grad[1] else None
+        gb = _grad_slot(bp, ctx.side) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gg, gbt = _grad_slot(gp, ctx.side), _grad_slot(btp, ctx.side)
         acc = gg is not None and gbt is not None and ctx.needs_input_grad[3] and ctx.needs_input_grad[4]
         dgamma = gg if acc else torch.empty(C, device=dev)
         dbeta = gbt if acc else torch.empty(C, device=dev)
@@ -311,27 +350,41 @@ class GradBucket:
     every parameter's .grad is a view into the buffer, so the backward writes straight
     into it."""
 
-    def __init__(self, params):
+    def __init__(self, params, sides: int = 1):
         self.params = [p for p in params if p.requires_grad]
         offs, n = flat_offsets(self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
         self.views = [self.flat[o:o + p.numel()].view_as(p) for p, o in zip(self.params, offs)]
+        # sides = 2: a second buffer for the gradients of side-1 layers (train.side), so the
+        # two streams of the two-stream step never add into the same memory
+        self.flat1 = torch.zeros(n, dtype=torch.float32, device=dev) if sides == 2 else None
+        self.views1 = ([self.flat1[o:o + p.numel()].view_as(p) for p, o in zip(self.params, offs)]
+                       if sides == 2 else None)
 
     def attach(self):
-        """Point every .grad at its slice (zeroed)."""
+        """Point every .grad at its slice (zeroed); sides = 2: also p._grad_side1."""
         self.flat.zero_()
         for p, v in zip(self.params, self.views):
             p.grad = v
+        if self.flat1 is not None:
+            self.flat1.zero_()
+            for p, v in zip(self.params, self.views1):
+                p._grad_side1 = v
 
-    def collect(self):
-        """Copy gradients that autograd allocated separately into the buffer."""
+    def collect(self, two_sides: bool = False):
+        """Copy gradients that autograd allocated separately into the buffer; two_sides (after a
+        two-stream step): add the second buffer (side-1 gradients) into it."""
         for p, v in zip(self.params, self.views):
             if p.grad is None:
                 v.zero_()
             elif p.grad.data_ptr() != v.data_ptr():
                 v.copy_(p.grad)
                 p.grad = v
+        if two_sides:
+            if self.flat1 is None:
+                raise RuntimeError("GradBucket: two_sides needs sides=2")
+            _lib.call("hreg_add_into", self.flat1, self.flat, self.flat.numel(), _stream())
 
     def all_reduce_mean(self, group=None):
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:

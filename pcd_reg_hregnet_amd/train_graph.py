@@ -307,13 +307,16 @@ class _HeadOut(torch.autograd.Function):
     (1/(sigma+1e-5))/mean (models.py:30-32) as a non-differentiable output."""
 
     @staticmethod
-    def forward(ctx, x, w3, b3, mode, nclouds, rows, want_weights):
+    def forward(ctx, x, w3, b3, mode, nclouds, rows, want_weights, params=(None, None)):
         G, C = x.shape
         out = _empty(G, device=x.device)
         wout = _empty(G, device=x.device) if want_weights else None
         call("hreg_head_out", x, C, C, nclouds, rows, w3, b3, mode, out, wout, _stream())
         ctx.save_for_backward(x, w3, b3)
         ctx.mode = mode
+        # the conv's parameters (w3 is a view of the weight): their gradients are added
+        # straight into the attached bucket when it is there (train._grad_slot)
+        ctx.params, ctx.side = params, train._SIDE
         if wout is not None:
             ctx.mark_non_differentiable(wout)
         return out, wout
@@ -327,16 +330,28 @@ class _HeadOut(torch.autograd.Function):
         dz = _empty(G, 1, device=dev)
         dx = _empty(G, C, device=dev)
         call("hreg_head_out_bwd", x, C, C, w3, b3, dy, ctx.mode, G, dz, dx, C, _stream())
-        dw = train.gemm_tn(dz, x).view(-1) if ctx.needs_input_grad[1] else None
-        db = train.col_sum(dz) if ctx.needs_input_grad[2] else None
-        return dx, dw, db, None, None, None, None
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            gw = train._grad_slot(ctx.params[0], ctx.side)
+            if gw is not None:
+                train.gemm_tn(dz, x, into=gw.view(1, C))
+            else:
+                dw = train.gemm_tn(dz, x).view(-1)
+        if ctx.needs_input_grad[2]:
+            gb = train._grad_slot(ctx.params[1], ctx.side)
+            if gb is not None:
+                train.col_sum(dz, into=gb)
+            else:
+                db = train.col_sum(dz)
+        return dx, dw, db, None, None, None, None, None
 
 
 def head_out(x, conv, mode, nclouds=1, rows=None, want_weights=False):
     C = x.shape[1]
     w3 = conv.weight.view(C)
     return _HeadOut.apply(x.contiguous(), w3, conv.bias, mode, nclouds,
-                          rows if rows is not None else x.shape[0], want_weights)
+                          rows if rows is not None else x.shape[0], want_weights,
+                          (conv.weight, conv.bias))
 
 
 class _SimFeats(torch.autograd.Function):
@@ -704,20 +719,64 @@ def batch_shuffle(x, perm):
     return gather_rows(rows, imap).view_as(x)
 
 
-def hregnet_train_forward(net, src, dst, hook=None, v2=False):
+_SIDE_STREAMS: dict = {}
+
+
+def side_stream(device) -> "torch.cuda.Stream":
+    """the stream the src feature extraction (and its backward) runs on in the two-stream step"""
+    key = str(device)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _SIDE_STREAMS[key]
+
+
+def join_side_stream(device) -> None:
+    """the current stream waits for everything enqueued on the side stream (after the backward
+    of a two-stream step: the src side's direct gradient additions ran there)"""
+    key = str(device)
+    if key in _SIDE_STREAMS:
+        torch.cuda.current_stream().wait_stream(_SIDE_STREAMS[key])
+
+
+def _two_stream_features(fe, src, dst, hook):
+    """src feature extraction on the side stream (gradient side 0, its BN running statistics
+    updated in the GEMM epilogues as it runs), dst on the current stream (side 1, running
+    updates queued), joined; the dst updates then run on the side stream after the src ones
+    -- the reference's order of the two calls of each module -- beside the heads."""
+    main = torch.cuda.current_stream()
+    s = side_stream(src.device)
+    s.wait_stream(main)
+    with torch.cuda.stream(s):
+        sf = feature_extraction(fe, src, hook, "src")
+    with train.side(1, defer_running=True) as queued:
+        df = feature_extraction(fe, dst, hook, "dst")
+    main.wait_stream(s)
+    s.wait_stream(main)
+    with torch.cuda.stream(s):
+        train.apply_running(queued)
+    return sf, df
+
+
+def hregnet_train_forward(net, src, dst, hook=None, v2=False, concurrent=False):
     """HRegNet.forward (models/HRegNet/models.py:77-148) in train mode -> the reference's
     result dict; differentiable in every parameter that requires grad.  v2: Model_V2's
     forward (model_v2/models.py:77-183): fine_corres_2 is FineReg2, whose attentive
     features also pass mlpx (Conv1d + train-mode BN + ReLU) and whose prime copies are
     batch shuffles by two host torch.randperm(B) draws, features first
-    (model_v2/layers.py:484-497); returns Model_V2's dict."""
+    (model_v2/layers.py:484-497); returns Model_V2's dict.  concurrent: the src and dst
+    feature extractions on two streams (needs a GradBucket(sides=2) attached; the caller
+    joins the side stream after the backward, join_side_stream) -- the same arithmetic and
+    the same results as the serial order."""
     fe = net.feature_extraction
     src = src.float().contiguous()
     dst = dst.float().contiguous()
     B = src.shape[0]
     _BN_COUNTERS.clear()
-    sf = feature_extraction(fe, src, hook, "src")
-    df = feature_extraction(fe, dst, hook, "dst")
+    if concurrent:
+        sf, df = _two_stream_features(fe, src, dst, hook)
+    else:
+        sf = feature_extraction(fe, src, hook, "src")
+        df = feature_extraction(fe, dst, hook, "dst")
     c3, w3 = coarse_reg(net.coarse_corres, sf["xyz_3"], sf["desc_3"], df["xyz_3"], df["desc_3"],
                         sf["sigmas_3"], df["sigmas_3"], hook)
     R3, t3 = weighted_svd(sf["xyz_3"], c3, w3)
@@ -743,6 +802,8 @@ def hregnet_train_forward(net, src, dst, hook=None, v2=False):
     R1_, t1_ = weighted_svd(x1t, c1, w1)
     R1, t1 = compose(R1_, t1_, R2, t2)
     _flush_bn_counters()
+    if concurrent:
+        join_side_stream(src.device)  # (the dst running-statistics updates)
 
     def feats(f):
         d = {}

@@ -30,6 +30,11 @@ from . import _lib, engine, train_graph
 from .train import GradBucket, flat_offsets
 
 
+# src and dst feature extraction (and their backwards) on two streams
+# (train_graph.hregnet_train_forward(concurrent=True)): the same results as the serial step
+TWO_STREAM = True
+
+
 def _dist_world(group=None) -> int:
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size(group)
@@ -155,7 +160,7 @@ class Trainer:
         self.group = group
         self.params = FlatParams(net.parameters())
         self.params.broadcast(0, group)
-        self.bucket = GradBucket(self.params.params)
+        self.bucket = GradBucket(self.params.params, sides=2)
         self.opt = FlatAdam(self.params, self.bucket, lr=lr)
         self.prefetch = Level1Prefetch(self.params.flat.device)
 
@@ -171,10 +176,13 @@ class Trainer:
             self.prefetch.start(*next_batch)
         self.bucket.attach()                     # optimizer.zero_grad()
         hook = train_graph.IndexHook(prepared=prepared) if prepared else None
-        ret = train_graph.hregnet_train_forward(self.net, src, dst, hook)
+        two = TWO_STREAM and src.is_cuda
+        ret = train_graph.hregnet_train_forward(self.net, src, dst, hook, concurrent=two)
         loss, l_R, l_t = train_graph.registration_loss(ret, gt_R, gt_t, self.alpha)
         loss.backward()
-        self.bucket.collect()
+        if two:
+            train_graph.join_side_stream(src.device)
+        self.bucket.collect(two_sides=two)
         self.bucket.all_reduce_mean(self.group)  # DDP gradient averaging, one collective
         self.opt.step()
         return loss.detach(), l_R.detach(), l_t.detach()
@@ -268,10 +276,13 @@ class GraphTrainer:
             self._sel_into(1 - k)
         tr.bucket.attach()
         hook = train_graph.IndexHook(prepared=self.sel[k])
-        ret = train_graph.hregnet_train_forward(tr.net, self.src[k], self.dst[k], hook)
+        two = TWO_STREAM
+        ret = train_graph.hregnet_train_forward(tr.net, self.src[k], self.dst[k], hook, concurrent=two)
         loss, l_R, l_t = train_graph.registration_loss(ret, self.gR[k], self.gt[k], tr.alpha)
         loss.backward()
-        tr.bucket.collect()
+        if two:
+            train_graph.join_side_stream(self.src[k].device)
+        tr.bucket.collect(two_sides=two)
         opt = tr.opt
         _lib.call("hreg_adam_step_dev", opt.p, opt.g, opt.m, opt.v, opt.p.numel(), float(opt.lr),
                   float(opt.betas[0]), float(opt.betas[1]), float(opt.eps), self.scal,

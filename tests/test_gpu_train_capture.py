@@ -68,3 +68,41 @@ def test_graph_trainer_host_running_ahead():
     torch.cuda.synchronize()
     assert all(torch.equal(a, b) for a, b in zip(le, lg)), ([float(x) for x in le], [float(x) for x in lg])
     assert torch.equal(eager.params.flat, graphed.params.flat)
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_two_stream_step_matches_serial_bitwise(graphed):
+    """trainer.TWO_STREAM (src and dst feature extraction, and their backwards, on two streams;
+    side-1 parameter gradients in the bucket's second buffer, added once; the dst BN running
+    updates after the src ones) against the serial step: the same losses, parameters, Adam
+    moments and BN buffers, bitwise, over steps on changing batches -- eager and captured."""
+    from pcd_reg_hregnet_amd import _lib, trainer
+    _lib.load()
+    B, n = 2, 4096
+    batches = _batches(B, n, 4)
+    old = trainer.TWO_STREAM
+    try:
+        trainer.TWO_STREAM = False
+        ser = _trainer()
+        ls = [ser.step(*batches[i], next_batch=batches[i + 1][:2] if i + 1 < 4 else None)[0].clone()
+              for i in range(4)]
+        trainer.TWO_STREAM = True
+        two = _trainer()
+        if graphed:
+            gt = trainer.GraphTrainer(two, B, n)
+            gt.capture(*batches[0])
+            run = gt.step
+        else:
+            run = two.step
+        lt = [run(*batches[i], next_batch=batches[i + 1][:2] if i + 1 < 4 else None)[0].clone()
+              for i in range(4)]
+    finally:
+        trainer.TWO_STREAM = old
+    torch.cuda.synchronize()
+    print("serial", [float(x) for x in ls], "two-stream", [float(x) for x in lt])
+    for a, b in zip(ls, lt):
+        assert torch.equal(a, b)
+    assert torch.equal(ser.params.flat, two.params.flat)
+    assert torch.equal(ser.opt.m, two.opt.m) and torch.equal(ser.opt.v, two.opt.v)
+    for (na, a), (_, b) in zip(ser.net.named_buffers(), two.net.named_buffers()):
+        assert torch.equal(a, b), na
