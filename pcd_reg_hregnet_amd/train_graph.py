@@ -754,7 +754,11 @@ def _two_stream_features(fe, src, dst, hook):
     s.wait_stream(main)
     with torch.cuda.stream(s):
         train.apply_running(queued)
-    return sf, df
+    # the queued statistics (made on the current stream, read on the side stream) stay
+    # referenced until the caller's join: freed earlier, their blocks could be handed to a
+    # current-stream allocation while the side stream still reads them (a race a captured
+    # graph replays: r3, running_var off by ~20 %)
+    return sf, df, queued
 
 
 def hregnet_train_forward(net, src, dst, hook=None, v2=False, concurrent=False):
@@ -772,8 +776,9 @@ def hregnet_train_forward(net, src, dst, hook=None, v2=False, concurrent=False):
     dst = dst.float().contiguous()
     B = src.shape[0]
     _BN_COUNTERS.clear()
+    keep = None
     if concurrent:
-        sf, df = _two_stream_features(fe, src, dst, hook)
+        sf, df, keep = _two_stream_features(fe, src, dst, hook)
     else:
         sf = feature_extraction(fe, src, hook, "src")
         df = feature_extraction(fe, dst, hook, "dst")
@@ -804,6 +809,7 @@ def hregnet_train_forward(net, src, dst, hook=None, v2=False, concurrent=False):
     _flush_bn_counters()
     if concurrent:
         join_side_stream(src.device)  # (the dst running-statistics updates)
+        del keep
 
     def feats(f):
         d = {}
