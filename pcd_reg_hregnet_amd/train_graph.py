@@ -656,9 +656,12 @@ def _nbr_desc(convs_2, xyz, desc, k, hook, name):
     return nbr
 
 
-def coarse_reg(m, s_xyz, s_desc, d_xyz, d_desc, s_w, d_w, hook=None):
+def coarse_reg(m, s_xyz, s_desc, d_xyz, d_desc, s_w, d_w, hook=None, keep=None):
     """CoarseReg.forward (layers.py:273-396), train mode.  xyz [B,N,3], desc [B*N][C]
-    point-major, w [B*N] (the sigmas, models.py:84-85)."""
+    point-major, w [B*N] (the sigmas, models.py:84-85).  keep (a list; the two-stream step):
+    the src neighbour branch on the side stream (gradient side 0), the dst one on the current
+    stream (side 1, BN running updates queued into keep and applied after the src ones on the
+    side stream; the caller joins it)."""
     k = m.k
     B, N1, _ = s_xyz.shape
     N2 = d_xyz.shape[1]
@@ -674,8 +677,22 @@ def coarse_reg(m, s_xyz, s_desc, d_xyz, d_desc, s_w, d_w, hook=None):
     kdesc = gather_rows(d_desc, kmap)                               # src_knn_desc
     kw = gather_rows(d_w.reshape(B * N2, 1), kmap)                  # src_knn_weights
     sims_a = sim_feats(s_desc, d_desc, kidx, B, N1, N2)             # original similarity
-    nbr_s = _nbr_desc(m.convs_2, s_xyz, s_desc, k, hook, "coarse_nbr_src")
-    nbr_d = _nbr_desc(m.convs_2, d_xyz, d_desc, k, hook, "coarse_nbr_dst")
+    if keep is not None:
+        main = torch.cuda.current_stream()
+        side = side_stream(s_xyz.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            nbr_s = _nbr_desc(m.convs_2, s_xyz, s_desc, k, hook, "coarse_nbr_src")
+        with train.side(1, defer_running=True) as queued:
+            nbr_d = _nbr_desc(m.convs_2, d_xyz, d_desc, k, hook, "coarse_nbr_dst")
+        main.wait_stream(side)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            train.apply_running(queued)
+        keep.append(queued)
+    else:
+        nbr_s = _nbr_desc(m.convs_2, s_xyz, s_desc, k, hook, "coarse_nbr_src")
+        nbr_d = _nbr_desc(m.convs_2, d_xyz, d_desc, k, hook, "coarse_nbr_dst")
     sims_b = sim_feats(nbr_s, nbr_d, kidx, B, N1, N2)               # neighbour-aware
     feats = cat_rows(geom, (s_flat, k), kx, (s_desc, k), kdesc, (s_w.reshape(B * N1, 1), k), kw,
                      sims_a, sims_b)
@@ -778,12 +795,13 @@ def hregnet_train_forward(net, src, dst, hook=None, v2=False, concurrent=False):
     _BN_COUNTERS.clear()
     keep = None
     if concurrent:
-        sf, df, keep = _two_stream_features(fe, src, dst, hook)
+        sf, df, queued = _two_stream_features(fe, src, dst, hook)
+        keep = [queued]
     else:
         sf = feature_extraction(fe, src, hook, "src")
         df = feature_extraction(fe, dst, hook, "dst")
     c3, w3 = coarse_reg(net.coarse_corres, sf["xyz_3"], sf["desc_3"], df["xyz_3"], df["desc_3"],
-                        sf["sigmas_3"], df["sigmas_3"], hook)
+                        sf["sigmas_3"], df["sigmas_3"], hook, keep)
     R3, t3 = weighted_svd(sf["xyz_3"], c3, w3)
     x2t = transform(sf["xyz_2"], R3, t3)
     if v2:
