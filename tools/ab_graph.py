@@ -5,9 +5,9 @@ captured while its switches are set (engine module attributes) and created in mi
 exactly as bench.py times one (barrier-free: one GPU).
 
 usage: python tools/ab_graph.py [--steps 20] [--reps 8] VARIANT [VARIANT ...]
-  VARIANT = comma-separated key=value (or "base"): engine.FLAG=0, or probe.nofps1=1 (timing
-  probe, results wrong: the level-1 FPS replaced by a copy of a cached selection, to price the
-  FPS's share of the step)
+  VARIANT = comma-separated key=value (or "base"): engine.FLAG=0, or probe.nofps1=1 / probe.nostage1=1
+  (timing probes, results wrong: the level-1 FPS, or the whole level-1 grouping, replaced by a
+  copy of a cached result, to price its share of the step)
 """
 import argparse
 import json
@@ -41,6 +41,26 @@ def _nofps1(engine):
     return fps
 
 
+def _nostage1(engine):
+    """engine.grouping with level 1 (FPS + spatial-index kNN grouping) served from a cache
+    (D2D copies into the caller's buffers) -- a timing probe only"""
+    real = engine.grouping
+    cache = {}
+
+    def grouping(xyz, lvl, weights=None, out=None, ws=None, sample=None):
+        if lvl != 0 or sample is not None or xyz.shape[1] != bench.POINTS:
+            return real(xyz, lvl, weights, out, ws, sample)
+        key = tuple(xyz.shape)
+        if key not in cache:
+            cache[key] = tuple(t.clone() for t in real(xyz, lvl, weights, None, None, None))
+        if out is None:
+            return tuple(t.clone() for t in cache[key])
+        for o, c in zip(out[:5], cache[key]):
+            o.copy_(c)
+        return tuple(out[:5])
+    return grouping
+
+
 def apply(variant, lib, engine):
     """set a variant's switches; returns the undo list"""
     undo = []
@@ -53,6 +73,9 @@ def apply(variant, lib, engine):
             old = getattr(engine, name)
             setattr(engine, name, type(old)(int(v)) if isinstance(old, (bool, int)) else v)
             undo.append(("engine", name, old))
+        elif k == "probe.nostage1" and int(v):
+            undo.append(("engine", "grouping", engine.grouping))
+            engine.grouping = _nostage1(engine)
         elif k == "probe.nofps1" and int(v):
             undo.append(("engine", "fps", engine.fps))
             engine.fps = _nofps1(engine)
@@ -88,7 +111,7 @@ def main():
     with torch.no_grad():
         for v in order:
             undo = apply(v, lib, engine)
-            engine.fps(torch.cat([src, dst], 0), engine.LEVELS[0][0])  # (fills a probe's cache uncaptured)
+            engine.grouping(torch.cat([src, dst], 0), 0)  # (fills a probe's cache uncaptured)
             g = engine.GraphPipeline(P, src, dst, lanes=a.steps)
             g.prepare(a.warmup)
             g.prepare(a.steps)
