@@ -40,6 +40,15 @@ def _empty(*shape, dtype=_f32, device):
     return torch.empty(shape, dtype=dtype, device=device)
 
 
+def _rows_ld(t):
+    """(t, its row stride) for a [rows][C] gradient that may be a column view of a wider
+    row block (_CatRows' backward); anything else is made contiguous"""
+    if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]:
+        return t, t.stride(0)
+    t = t.contiguous()
+    return t, t.shape[-1]
+
+
 # ------------------------------------------------------------------ index maps
 
 class IndexMap:
@@ -122,9 +131,9 @@ class _GatherRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         imap = ctx.imap
-        dout = dout.contiguous()
+        dout, ldd = _rows_ld(dout)
         dx = _empty(imap.n, ctx.C, device=dout.device)
-        call("hreg_scatter_rows", dout, ctx.C, imap.csr(), imap.M, imap.n, ctx.C, dx, ctx.C, 0,
+        call("hreg_scatter_rows", dout, ldd, imap.csr(), imap.M, imap.n, ctx.C, dx, ctx.C, 0,
              _stream())
         return dx, None
 
@@ -149,10 +158,10 @@ class _GeomRows(torch.autograd.Function):
         (geom,) = ctx.saved_tensors
         k = ctx.k
         G = geom.shape[0] // k
-        dgeom = dgeom.contiguous()
+        dgeom, lddg = _rows_ld(dgeom)
         dq = _empty(G, 3, device=geom.device) if ctx.needs_input_grad[0] else None
         dkx = _empty(G * k, 3, device=geom.device) if ctx.needs_input_grad[1] else None
-        call("hreg_geom_rows_bwd", geom, 4, dgeom, 4, None, G, k, dq, dkx, _stream())
+        call("hreg_geom_rows_bwd", geom, 4, dgeom, lddg, None, G, k, dq, dkx, _stream())
         return dq, dkx, None
 
 
@@ -194,9 +203,9 @@ class _CatRows(torch.autograd.Function):
             if not ctx.needs_input_grad[1 + i]:
                 grads.append(None)
             elif r == 1:
-                g = _empty(ctx.R, C, device=dout.device)
-                call("hreg_copy_rows", dout[:, c0:], Ct, 1, ctx.R, C, g, C, 0, _stream())
-                grads.append(g)
+                # the block's columns of dout as a strided view (no copy): the consumers'
+                # backward kernels take the row stride (_rows_ld)
+                grads.append(dout[:, c0:c0 + C])
             else:
                 g = _empty(ctx.R // r, C, device=dout.device)
                 call("hreg_group_sum", dout[:, c0:], Ct, ctx.R // r, r, C, g, C, 0, _stream())
@@ -251,7 +260,7 @@ class _Attention(torch.autograd.Function):
         v = logits if same else vals
         Cv = v.shape[1] if v is not None else 0
         dkp = dkp.contiguous() if dkp is not None else None
-        dvmap = dvmap.contiguous() if dvmap is not None else None
+        dvmap, lddm = _rows_ld(dvmap) if dvmap is not None else (None, Cv)
         dvsum = dvsum.contiguous() if dvsum is not None else None
         dlogits = _empty(R, C, device=dev)
         dvals = _empty(R, Cv, device=dev) if (not same and vals is not None and
@@ -260,7 +269,7 @@ class _Attention(torch.autograd.Function):
                                            ctx.needs_input_grad[2]) else None
         if dvals is not None and dvmap is None and dvsum is None:
             dvals.zero_()
-        call("hreg_attention_bwd", logits, C, C, v, Cv, Cv, kx, G, k, a, amax, dkp, dvmap, Cv,
+        call("hreg_attention_bwd", logits, C, C, v, Cv, Cv, kx, G, k, a, amax, dkp, dvmap, lddm,
              dvsum, Cv, 1 if same else 0, dlogits, C, dvals, Cv, dkx, _stream())
         return dlogits, dvals, dkx, None, None, None, None
 
@@ -388,8 +397,9 @@ class _SimFeats(torch.autograd.Function):
                          device=dev)
         da = _empty(nb * N1, C, device=dev)
         db = _empty(nb * N2, C, device=dev)
+        dout, ldd = _rows_ld(dout)
         call("hreg_sim_feats_bwd", S, a, b, na, nbv, nb, N1, N2, C, kidx, k, rmax, rarg, cmax,
-             carg, dout.contiguous(), 2, ws, da, db, _stream())
+             carg, dout, ldd, ws, da, db, _stream())
         return da, db, None, None, None, None
 
 
