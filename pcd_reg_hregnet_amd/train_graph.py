@@ -310,6 +310,55 @@ def group_max(x, k):
     return _GroupMax.apply(x.contiguous(), k)
 
 
+class _DescTail(torch.autograd.Function):
+    """x2 = max over each group of k rows of x1 (layers.py:202), then
+    cat([x2 repeated over the group's k rows, x1, att_map]) (layers.py:204-206) as one
+    function: x1 feeds both, and its gradient is the concatenation's x1 columns with the
+    group-max gradient added at each group's argmax rows (group_max_bwd accumulating into
+    the copy) -- no dense zero-filled max gradient and no separate addition (autograd's
+    sum of the two uses: the same fp32 additions)."""
+
+    @staticmethod
+    def forward(ctx, x1, att_map, k):
+        R, C1 = x1.shape
+        Ca = att_map.shape[1]
+        G = R // k
+        dev = x1.device
+        x2 = _empty(G, C1, device=dev)
+        arg = _empty(G, C1, dtype=torch.int32, device=dev)
+        call("hreg_group_max_arg", x1, C1, G, k, C1, x2, C1, arg, _stream())
+        Ct = 2 * C1 + Ca
+        y = _empty(R, Ct, device=dev)
+        call("hreg_copy_rows", x2, C1, k, R, C1, y, Ct, 0, _stream())
+        call("hreg_copy_rows", x1, C1, 1, R, C1, y[:, C1:], Ct, 0, _stream())
+        call("hreg_copy_rows", att_map, Ca, 1, R, Ca, y[:, 2 * C1:], Ct, 0, _stream())
+        ctx.save_for_backward(arg)
+        ctx.dims = (R, C1, Ca, k)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        R, C1, Ca, k = ctx.dims
+        G = R // k
+        dy = dy.contiguous()
+        Ct = dy.shape[1]
+        dev = dy.device
+        dx1 = dx2 = None
+        if ctx.needs_input_grad[0]:
+            dx2 = _empty(G, C1, device=dev)
+            call("hreg_group_sum", dy, Ct, G, k, C1, dx2, C1, 0, _stream())
+            dx1 = _empty(R, C1, device=dev)
+            call("hreg_copy_rows", dy[:, C1:], Ct, 1, R, C1, dx1, C1, 0, _stream())
+            call("hreg_group_max_bwd", dx2, C1, arg, G, k, C1, dx1, C1, 1, _stream())
+        datt = dy[:, 2 * C1:] if ctx.needs_input_grad[1] else None
+        return dx1, datt, None
+
+
+def desc_tail(x1, att_map, k):
+    return _DescTail.apply(x1.contiguous(), att_map.contiguous(), k)
+
+
 class _HeadOut(torch.autograd.Function):
     """mlp3 (Conv1d C->1) + softplus + 0.001 (layers.py:161-163) or sigmoid
     (layers.py:393-394, 451-452); optionally the next level's WFPS weights
@@ -615,8 +664,7 @@ def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src", u
                            nb, M, want_weights=True)
     # descriptor (layers.py:200-209)
     x1 = seq_convs(grouped_rows, desc.convs)
-    x2 = group_max(x1, k)
-    y = cat_rows((x2, k), x1, att_map)
+    y = desc_tail(x1, att_map, k)  # cat([max_k x1 repeated, x1, att_map])
     y = conv_bn(y, desc.mlp1[0], desc.mlp1[1])
     y = conv_bn(y, desc.mlp2[0], desc.mlp2[1])
     d = group_max(y, k)

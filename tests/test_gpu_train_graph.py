@@ -556,23 +556,22 @@ def test_train_descriptor_backward_replay():
 
     def kl(det, desc, lvl, xyz, feats, weights, hook=None, part="src", use_fps=True):
         rec = {"lvl": lvl}
-        o_seq, o_cat = train_graph.seq_convs, train_graph.cat_rows
+        o_seq, o_tail = train_graph.seq_convs, train_graph.desc_tail
 
         def seq(x, s):
             if s is desc.convs:
                 rec["grouped"] = x.detach().clone()
             return o_seq(x, s)
 
-        def cat(*blocks):
-            if len(blocks) == 3 and isinstance(blocks[0], tuple):
-                rec["att_map"] = blocks[2].detach().clone()
-            return o_cat(*blocks)
+        def tail(x1, att_map, k):  # the descriptor's [x2 repeated, x1, att_map] concatenation
+            rec["att_map"] = att_map.detach().clone()
+            return o_tail(x1, att_map, k)
 
-        train_graph.seq_convs, train_graph.cat_rows = seq, cat
+        train_graph.seq_convs, train_graph.desc_tail = seq, tail
         try:
             out = orig_kl(det, desc, lvl, xyz, feats, weights, hook, part, use_fps)
         finally:
-            train_graph.seq_convs, train_graph.cat_rows = o_seq, o_cat
+            train_graph.seq_convs, train_graph.desc_tail = o_seq, o_tail
         out[3].retain_grad()
         rec["d"] = out[3]
         caps.append(rec)
