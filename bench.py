@@ -332,8 +332,13 @@ def cpu_baseline(budget_s: float = 30.0, batches=(1, PAIRS_PER_GPU), reps: int =
                            "s_per_batch_median": round(float(np.median(ts)), 3),
                            "runs_s": [round(t, 3) for t in ts]}
     best_b = max(med)
-    threads = oracle.lib().oracle_num_threads()
-    return {"value": round(1.0 / med[best_b], 4), "unit": "pairs/s", "cores": int(threads),
+    threads = int(oracle.lib().oracle_num_threads())
+    # cores = the CPUs the oracle actually ran on: its OpenMP / BLAS threads, bounded by the
+    # CPUs this process may be scheduled on (its affinity mask; os.cpu_count() is the whole
+    # host's count, 256 on the GPU box)
+    affinity = len(os.sched_getaffinity(0))
+    return {"value": round(1.0 / med[best_b], 4), "unit": "pairs/s",
+            "cores": min(threads, affinity), "omp_threads": threads, "affinity_cpus": affinity,
             "host_cpus": os.cpu_count(), "kind": "port", "batch": best_b, "per_batch": per_b,
             "sample": f"2x{POINTS}-pt KITTI-shape synthetic LiDAR pairs (the GPU run's "
                       f"generator), B in {sorted(med)}, 1 warm-up + median of {reps} each; "

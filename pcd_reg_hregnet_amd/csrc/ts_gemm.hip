@@ -211,9 +211,12 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
 }
 
 // output tiles per workgroup for this K (W' column group within TS_LDS_FLOATS), 0: unsupported
-int ts_nt(int K, int N) {
-    // (+ the tile's shift / scale and the statistics' wave partials: 8 floats per column)
-    const int KP = ((K + 15) & ~15) + 4 + 2 + 8;
+int ts_nt(int K, int N, bool stats) {
+    // (+ the tile's shift / scale, 2 floats per column, and with the statistics their wave
+    // partials: 4 waves x 2 doubles = 16 floats per column, as ts_launch reserves them; the
+    // plain kernel keeps its historical 8-float margin).  The whole request then stays
+    // within TS_LDS_FLOATS (64 KB), which ts_grid_x's workgroups-per-CU count assumes.
+    const int KP = ((K + 15) & ~15) + 4 + 2 + (stats ? 16 : 8);
     int nt = TS_LDS_FLOATS / (32 * KP);
     if (nt > 8) nt = 8;
     const int need = (N + 31) / 32;
@@ -228,7 +231,7 @@ int ts_nt(int K, int N) {
 // workgroups along the rows: persistent (tiles assigned statically), so exactly as many as
 // fit at once -- three per CU up to 168 VGPRs (<= 4 tiles; 2 with the statistics), else two
 int ts_grid_x(int R, int K, int N, bool stats) {
-    const int nt = ts_nt(K, N);
+    const int nt = ts_nt(K, N, stats);
     const int gy = (N + nt * 32 - 1) / (nt * 32);
     const int tiles = (R + 31) / 32;
     const int gx = (tiles + 3) / 4;
@@ -246,7 +249,7 @@ int hreg_bn_finalize_stats(const double *part, int S, int R, int C, float eps, f
 
 extern "C" int hreg_ts_gemm_supported(int R, int K, int N) {
     // (the A extent is addressed through a buffer descriptor: < 2 GB)
-    return R > 0 && K > 0 && N > 0 && (K & 3) == 0 && (N & 3) == 0 && ts_nt(K, N) > 0 &&
+    return R > 0 && K > 0 && N > 0 && (K & 3) == 0 && (N & 3) == 0 && ts_nt(K, N, true) > 0 &&
            (size_t)R * K * sizeof(float) < ((size_t)1 << 31);
 }
 
@@ -262,12 +265,13 @@ int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans
                                      reinterpret_cast<uintptr_t>(out)) & 15))
         return -HREG_ERR_INVALID;
     if ((size_t)R * lda * sizeof(float) >= ((size_t)1 << 31)) return -HREG_ERR_UNSUPPORTED;
-    const int nt = ts_nt(K, N);
+    const int nt = ts_nt(K, N, STATS);
     if (nt <= 0) return -HREG_ERR_UNSUPPORTED;
     const int gx = ts_grid_x(R, K, N, STATS);
     const int gy = (N + nt * 32 - 1) / (nt * 32);
     const size_t lds = ((size_t)nt * 32 * (((K + 15) & ~15) + 4) + 2 * nt * 32 + (STATS ? 16 * nt * 32 : 0)) *
                        sizeof(float);
+    if (lds > TS_LDS_FLOATS * sizeof(float)) return -HREG_ERR_UNSUPPORTED;  // (ts_nt's budget)
     const bool tail = (K & 15) != 0, full = scale != nullptr || relu;
     if (STATS && full) return -HREG_ERR_UNSUPPORTED;
 #define HREG_TS(NTT, TT, FF)                                                                                   \
@@ -296,7 +300,7 @@ extern "C" int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *
 }
 
 extern "C" size_t hreg_ts_gemm_bn_ws_bytes(int R, int K, int N) {
-    if (R <= 0 || K <= 0 || N <= 0 || ts_nt(K, N) <= 0) return 0;
+    if (R <= 0 || K <= 0 || N <= 0 || ts_nt(K, N, true) <= 0) return 0;
     return (size_t)ts_grid_x(R, K, N, true) * N * 2 * sizeof(double);
 }
 

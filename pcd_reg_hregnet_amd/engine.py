@@ -22,7 +22,7 @@ from dataclasses import dataclass
 
 import torch
 
-from . import _lib
+from . import _lib, capture
 from ._lib import Gemm, Seg, call
 
 BN_EPS = 1e-5
@@ -1401,19 +1401,19 @@ class GraphPipeline:
         check_device_status()
         self.pool = torch.cuda.graph_pool_handle()
         self.g_first = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_first, pool=self.pool):
+        with capture.graph(self.g_first, pool=self.pool):
             self._first_stage1()
         self.g_step, self.outs = [], []
         for cur in (0, 1):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
+            with capture.graph(g, pool=self.pool):
                 out = self._fork(lambda ln: self._rest(ln, cur), **self._side_kw(1 - cur))
             self.g_step.append(g)
             self.outs.append(out)
         self.g_last, self.outs_last = [], []
         for cur in (0, 1):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
+            with capture.graph(g, pool=self.pool):
                 out = self._fork(lambda ln: self._rest(ln, cur))
             self.g_last.append(g)
             self.outs_last.append(out)
@@ -1515,7 +1515,7 @@ class GraphPipeline:
         torch.cuda.synchronize()
         g = {"first": torch.cuda.CUDAGraph(), "steps": [], "souts": [], "lasts": [],
              "louts": [], "psteps": [], "pouts": []}
-        with torch.cuda.graph(g["first"], pool=self.pool):
+        with capture.graph(g["first"], pool=self.pool):
             self._first_stage1(lanes=r)  # (batched: every lane's stage 1, the extra lanes unused)
         for cur in (0, 1):
             variants = [("steps", "souts", self._side_kw(1 - cur, side_lanes=r)),
@@ -1524,7 +1524,7 @@ class GraphPipeline:
                 variants.append(("psteps", "pouts", {"lanes": r, **self._side_kw(1 - cur)}))
             for gk, ok, kw in variants:
                 gr = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gr, pool=self.pool):
+                with capture.graph(gr, pool=self.pool):
                     out = self._fork(lambda ln: self._rest(ln, cur), **kw)
                 g[gk].append(gr)
                 g[ok].append(out)

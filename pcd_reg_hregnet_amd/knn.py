@@ -55,14 +55,27 @@ class _KnnGather(Function):
 
     @staticmethod
     def backward(ctx, grad):
+        """dx[b, n] = sum of grad[b, m, k] over the (m, k) with idx[b, m, k] == n, summed in
+        ascending (m, k) order by the library's CSR scatter (hreg_csr_build +
+        hreg_scatter_rows: deterministic, no atomics); padded entries (idx < 0) go to a
+        discarded row (out-of-range entries gather zeros in the forward)."""
         (idx,) = ctx.saved_tensors
         B, M, K = idx.shape
         C = grad.shape[-1]
-        gx = torch.zeros((B, ctx.N, C), dtype=grad.dtype, device=grad.device)
-        flat = (idx.clamp_min(0) + torch.arange(B, device=idx.device).view(B, 1, 1) * ctx.N)
-        valid = (idx >= 0).reshape(-1, 1).to(grad.dtype)
-        gx.view(-1, C).index_add_(0, flat.reshape(-1), grad.reshape(-1, C) * valid)
-        return gx, None
+        N = ctx.N
+        n = B * N + 1                                   # + the row that takes idx < 0
+        rows = idx + torch.arange(B, device=idx.device).view(B, 1, 1) * N
+        gi = torch.where((idx >= 0) & (idx < N), rows, torch.full_like(rows, n - 1)).to(torch.int32)
+        gi = gi.reshape(-1).contiguous()
+        Mt = gi.numel()
+        st = _lib.stream_handle()
+        ws = torch.empty(max(int(_lib.load().hreg_csr_ws_bytes(Mt, n)), 16), dtype=torch.uint8,
+                         device=grad.device)
+        _lib.call("hreg_csr_build", gi, Mt, n, ws, st)
+        dy = grad.float().contiguous().view(Mt, C)
+        dx = torch.empty((n, C), dtype=torch.float32, device=grad.device)
+        _lib.call("hreg_scatter_rows", dy, C, ws, Mt, n, C, dx, C, 0, st)
+        return dx[:B * N].view(B, N, C).to(grad.dtype), None
 
 
 def knn_gather(x: torch.Tensor, idx: torch.Tensor, lengths=None):

@@ -92,6 +92,23 @@ def col_sum(x: torch.Tensor, into: torch.Tensor | None = None) -> torch.Tensor:
 
 
 DIRECT_GRAD = True  # (A/B switch: False returns every parameter gradient to autograd)
+# Direct gradients are on only between GradBucket.attach and GradBucket.collect (the
+# trainers' steps) or inside direct_gradients(): outside them every parameter gradient goes
+# back to autograd, so torch.autograd.grad / backward(inputs=...) and gradient hooks see the
+# usual behaviour.
+_DIRECT_ON = False
+
+
+@contextlib.contextmanager
+def direct_gradients():
+    """backwards run inside add parameter gradients into existing .grad tensors in place"""
+    global _DIRECT_ON
+    old = _DIRECT_ON
+    _DIRECT_ON = True
+    try:
+        yield
+    finally:
+        _DIRECT_ON = old
 
 # Two-stream training step (train_graph.hregnet_train_forward(concurrent=True)): the src and
 # dst feature extractions run on two streams, and so do their backwards.  A layer records the
@@ -131,7 +148,7 @@ def _grad_slot(p, side: int = 0):
     (autograd's own accumulation into an existing .grad: the flat gradient bucket is
     attached and zeroed every step; side 1: the bucket's second buffer), else None (return
     the gradient to autograd)"""
-    if p is None or not p.requires_grad or not DIRECT_GRAD:
+    if p is None or not p.requires_grad or not (DIRECT_GRAD and _DIRECT_ON):
         return None
     g = p.grad if side == 0 else getattr(p, "_grad_side1", None)
     if g is None or not g.is_contiguous() or g.dtype != torch.float32:
@@ -363,7 +380,10 @@ class GradBucket:
                        if sides == 2 else None)
 
     def attach(self):
-        """Point every .grad at its slice (zeroed); sides = 2: also p._grad_side1."""
+        """Point every .grad at its slice (zeroed); sides = 2: also p._grad_side1.  Turns the
+        direct parameter gradients on until ``collect``."""
+        global _DIRECT_ON
+        _DIRECT_ON = True
         self.flat.zero_()
         for p, v in zip(self.params, self.views):
             p.grad = v
@@ -374,7 +394,10 @@ class GradBucket:
 
     def collect(self, two_sides: bool = False):
         """Copy gradients that autograd allocated separately into the buffer; two_sides (after a
-        two-stream step): add the second buffer (side-1 gradients) into it."""
+        two-stream step): add the second buffer (side-1 gradients) into it.  Turns the direct
+        parameter gradients off."""
+        global _DIRECT_ON
+        _DIRECT_ON = False
         for p, v in zip(self.params, self.views):
             if p.grad is None:
                 v.zero_()

@@ -747,6 +747,9 @@ def coarse_reg(m, s_xyz, s_desc, d_xyz, d_desc, s_w, d_w, hook=None, keep=None):
         side.wait_stream(main)
         with torch.cuda.stream(side):
             train.apply_running(queued)
+        record_on((nbr_s,), main)                  # made on the side stream, read here
+        for mean, var, _, _, _ in queued:
+            record_on((mean, var), side)           # made here, read on the side stream
         keep.append(queued)
     else:
         nbr_s = _nbr_desc(m.convs_2, s_xyz, s_desc, k, hook, "coarse_nbr_src")
@@ -829,11 +832,24 @@ def _two_stream_features(fe, src, dst, hook):
     s.wait_stream(main)
     with torch.cuda.stream(s):
         train.apply_running(queued)
-    # the queued statistics (made on the current stream, read on the side stream) stay
-    # referenced until the caller's join: freed earlier, their blocks could be handed to a
-    # current-stream allocation while the side stream still reads them (a race a captured
-    # graph replays: r3, running_var off by ~20 %)
+    # tensors crossing streams are recorded on the stream that reads them, so the allocator
+    # cannot hand their blocks to another allocation before that stream is done with them:
+    # the src features (made on the side stream, read on the current one) and the queued
+    # statistics (made on the current stream, read on the side stream; a block freed early
+    # here was a race a captured graph replayed: r3, running_var off by ~20 %).  They also
+    # stay referenced until the caller's join.
+    record_on(sf.values(), main)
+    for mean, var, _, _, _ in queued:
+        record_on((mean, var), s)
     return sf, df, queued
+
+
+def record_on(tensors, stream) -> None:
+    """t.record_stream(stream) for every tensor (a consumer on another stream than the
+    producer's: the caching allocator then keeps the block until that stream's work is done)"""
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            t.record_stream(stream)
 
 
 def hregnet_train_forward(net, src, dst, hook=None, v2=False, concurrent=False):

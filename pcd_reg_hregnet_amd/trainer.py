@@ -26,7 +26,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import _lib, engine, train_graph
+from . import _lib, capture, engine, train_graph
 from .train import GradBucket, flat_offsets
 
 
@@ -174,8 +174,18 @@ class Trainer:
         # forward, in the reference's order
         if next_batch is not None and self.net.feature_extraction.use_fps:
             self.prefetch.start(*next_batch)
-        self.bucket.attach()                     # optimizer.zero_grad()
         hook = train_graph.IndexHook(prepared=prepared) if prepared else None
+        out = self.local_gradients(src, dst, gt_R, gt_t, hook)
+        self.bucket.all_reduce_mean(self.group)  # DDP gradient averaging, one collective
+        self.opt.step()
+        return out
+
+    def local_gradients(self, src, dst, gt_R, gt_t, hook=None):
+        """This rank's half of a step: ``optimizer.zero_grad()``, the train-mode forward on
+        the shard (BN statistics of the shard alone, running stats updated), the loss and its
+        backward into the gradient bucket -- everything before DDP's all-reduce.  hook: an
+        IndexHook (prepared / injected selections).  -> (loss, l_R, l_t), detached."""
+        self.bucket.attach()                     # optimizer.zero_grad()
         two = TWO_STREAM and src.is_cuda
         ret = train_graph.hregnet_train_forward(self.net, src, dst, hook, concurrent=two)
         loss, l_R, l_t = train_graph.registration_loss(ret, gt_R, gt_t, self.alpha)
@@ -183,8 +193,6 @@ class Trainer:
         if two:
             train_graph.join_side_stream(src.device)
         self.bucket.collect(two_sides=two)
-        self.bucket.all_reduce_mean(self.group)  # DDP gradient averaging, one collective
-        self.opt.step()
         return loss.detach(), l_R.detach(), l_t.detach()
 
 
@@ -219,6 +227,11 @@ class GraphTrainer:
     def __init__(self, trainer: "Trainer", batch: int, points: int):
         if _dist_world(trainer.group) > 1:
             raise NotImplementedError("GraphTrainer: single process (use Trainer with DDP)")
+        if not trainer.net.feature_extraction.use_fps:
+            # use_fps=False (layers.py:144-147) draws torch.randperm samples on the host per
+            # step; a captured graph would freeze one draw and replay it forever
+            raise NotImplementedError("GraphTrainer needs use_fps=True (random sampling draws "
+                                      "on the host every step: use Trainer)")
         self.tr = trainer
         dev = trainer.params.flat.device
         self.src = [torch.zeros(batch, points, 3, device=dev) for _ in range(2)]
@@ -313,7 +326,7 @@ class GraphTrainer:
         torch.cuda.current_stream().wait_stream(s)
         for k in (0, 1):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with capture.graph(g):
                 self.outs[k] = self._body(k)
             self.graphs[k] = g
         torch.cuda.synchronize()
@@ -324,6 +337,15 @@ class GraphTrainer:
         self.k = 0
         self.loaded = True
         self.first = True
+        self.pending = None
+
+    def _announced(self, src, dst) -> bool:
+        """(src, dst) are the next_batch the previous step copied into the current set"""
+        if self.pending is None:
+            return False
+        rs, rd, vs, vd, ps, pd, shape = self.pending
+        return (rs() is src and rd() is dst and src._version == vs and dst._version == vd
+                and (src.data_ptr(), dst.data_ptr(), tuple(src.shape)) == (ps, pd, shape))
 
     def _load(self, k, src, dst, gt_R, gt_t):
         self.src[k].copy_(src)
@@ -332,19 +354,23 @@ class GraphTrainer:
         self.gt[k].copy_(gt_t)
 
     def step(self, src, dst, gt_R, gt_t, next_batch=None):
-        """One training step on (src, dst, gt_R, gt_t) -- which must be the batch passed as
-        ``next_batch`` to the previous step (or to ``capture``) -- and the level-1 selections
-        of ``next_batch`` (default: the same batch again).  -> (loss, l_R, l_t), static
-        tensors overwritten by the next replay."""
+        """One training step on (src, dst, gt_R, gt_t), and the level-1 selections of
+        ``next_batch`` (default: the same batch again) on the side stream.  When (src, dst) are
+        the tensors the previous step was given as ``next_batch``, unchanged since (the same
+        objects, version counters and storage), the replay uses the set and selections that
+        step prepared; any other batch is copied in and its selections computed first, so a
+        step always trains on the points it is given.  -> (loss, l_R, l_t), static tensors
+        overwritten by the next replay."""
         if not self.loaded:
             raise RuntimeError("GraphTrainer.capture() first")
         k = self.k
         nb = next_batch if next_batch is not None else (src, dst)
-        if self.first:  # nothing prefetched this batch yet
+        if self.first or not self._announced(src, dst):  # nothing prefetched for this batch
             self.src[k].copy_(src)
             self.dst[k].copy_(dst)
             self._sel_into(k)
             self.first = False
+        self.pending = Level1Prefetch._key(nb[0], nb[1])
         # the set this replay consumes holds (src, dst) since the previous replay's prefetch
         self.gR[k].copy_(gt_R)
         self.gt[k].copy_(gt_t)

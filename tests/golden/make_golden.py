@@ -21,7 +21,7 @@ Weights: feature extractor from ckpt/pretrained/nusc_feats.pth
 from pcd_reg_hregnet_amd.weights.synthetic_value (trained heads are missing
 from the snapshot, .MISSING_LARGE_BLOBS:2-4).
 
-Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --traj-only [--traj-c4] | --forward-only | --v2-train-only | --metrics-only | --perturb-only | --mi-only]   (a few minutes on 8 CPUs)
+Usage: python tests/golden/make_golden.py [--v2-only | --loss-only | --train-only | --traj-only [--traj-c4] | --ddp-only | --v2-b2-65536 | --forward-only | --v2-train-only | --metrics-only | --perturb-only | --mi-only]   (a few minutes on 8 CPUs)
 """
 from __future__ import annotations
 
@@ -435,6 +435,25 @@ def v2_fixtures(pu):
     np.savez_compressed(os.path.join(HERE, "model_v2_lidar_b1_n65536.npz"),
                         **model_v2_fixture(Model_V2, pu, s, d, sd, seed=8))
     print("model_v2 b1 n65536 fixture written", flush=True)
+    v2_b2_65536_fixture(pu, Model_V2, sd)
+
+
+def v2_b2_65536_fixture(pu, Model_V2=None, sd=None):
+    """config 5's cloud size with two pairs: seed 1 makes both prime
+    shuffles (model_v2/layers.py:492,497: torch.randperm(B) for the features, then the
+    weights) the swap [1, 0], so the batch permutation is exercised at 65536 points."""
+    if Model_V2 is None:
+        v2_fixtures_setup()
+        from models.model_v2.models import Model_V2  # noqa: E402  (reference code)
+        from pcd_reg_hregnet_amd import weights
+        sd = weights.make_state_dict(Model_V2(_Args()).state_dict(), seed=0, pretrained_feats=True)
+    from pcd_reg_hregnet_amd import synthetic
+    torch.manual_seed(1)
+    assert torch.randperm(2).tolist() == [1, 0] and torch.randperm(2).tolist() == [1, 0]
+    s, d, _, _ = synthetic.lidar_batch(2, 65536, seed0=61)
+    np.savez_compressed(os.path.join(HERE, "model_v2_lidar_b2_n65536.npz"),
+                        **model_v2_fixture(Model_V2, pu, s, d, sd, seed=1))
+    print("model_v2 b2 n65536 fixture written", flush=True)
 
 
 def p3d_angle_from_tan(axis, other_axis, data, horizontal, tait_bryan):
@@ -530,6 +549,20 @@ def _save_feat_grads(ret, out, suffix):
             out[key] = (g[:, :, :64] if k.startswith("desc") else g).float().numpy()
 
 
+def _save_outputs(ret, out, suffix):
+    """the train-mode forward's per-level outputs and head results in the tests/parity.py
+    fixture layout (so the selections of the train forward are held to the same near-tie
+    contract as the eval forward's)"""
+    for part in ("src", "dst"):
+        f = ret[f"{part}_feats"]
+        for lv in (1, 2, 3):
+            for q in ("xyz", "sigmas", "desc"):
+                out[f"{part}_{q}_{lv}{suffix}"] = _f32(f[f"{q}_{lv}"].detach().numpy())
+    for lv in (1, 2, 3):
+        out[f"corres_{lv}{suffix}"] = _f32(ret[f"src_xyz_corres_{lv}"].detach().numpy())
+        out[f"weights_{lv}{suffix}"] = _f32(ret[f"src_dst_weights_{lv}"].detach().numpy())
+
+
 def train_fixtures(pu):
     """One reference training step (train/train_reg_v0.py:264-294): HRegNet in .train()
     (batch-statistics BN), l_trans = mean over the 3 levels of transformation_loss
@@ -579,6 +612,7 @@ def train_fixtures(pu):
         out["ghead_" + name] = g[:256].float().numpy()
     out["param_names"] = np.array(names)
     _save_feat_grads(ret, out, "")
+    _save_outputs(ret, out, "")
     for name, b in net.named_buffers():
         if name.endswith("running_mean") or name.endswith("running_var"):
             out["buf_" + name] = b.detach().numpy()
@@ -609,6 +643,7 @@ def train_fixtures(pu):
         KNN_REPLAY = None
     out["loss64"] = (l64 / 3.0).detach().numpy()
     _save_feat_grads(ret64, out, "_64")
+    _save_outputs(ret64, out, "_64")
     for i, (R, t) in enumerate(zip(ret64["rotation"], ret64["translation"])):
         out[f"R{3 - i}_64"] = R.detach().numpy()
         out[f"t{3 - i}_64"] = t.detach().numpy()
@@ -618,6 +653,119 @@ def train_fixtures(pu):
         out["g64head_" + name] = g[:256].numpy()
     np.savez_compressed(os.path.join(HERE, "train_step_b2_n2048.npz"), **out)
     print("train_step_b2_n2048.npz written, loss", float(loss), flush=True)
+
+
+def _ref_shard_step(HRegNet, L, sd, pu, s, d, Rg, tg):
+    """One rank's half of a DDP step (train_reg_v0.py:279-294 on this rank's shard, BN
+    statistics of the shard alone): the fp32 train-mode forward + backward and its float64
+    replay on the same selections.  -> dict: selections, loss, full fp32 / float64 parameter
+    gradients, the BN running stats after the forward."""
+    global KNN_REPLAY
+    net = HRegNet(_Args())
+    net.load_state_dict(sd)
+    net.train()
+    pu.calls.clear()
+    KNN_CALLS.clear()
+    ret = net(torch.from_numpy(s), torch.from_numpy(d))
+    gR, gt = torch.from_numpy(Rg), torch.from_numpy(tg)
+    loss = sum(L.transformation_loss(ret["rotation"][i], ret["translation"][i], gR, gt, 1.0)[0]
+               for i in range(3)) / 3.0
+    loss.backward()
+    out = {"loss": float(loss.detach()), "sel": {}, "g32": {}, "g64": {}, "bufs": {}}
+    for name, (_, idx) in zip(TRAIN_FPS_NAMES, pu.calls):
+        out["sel"][name] = idx.numpy().astype(np.int32)
+    assert len(KNN_CALLS) == len(TRAIN_KNN_NAMES), len(KNN_CALLS)
+    for name, idx in zip(TRAIN_KNN_NAMES, KNN_CALLS):
+        out["sel"][name] = idx.numpy().astype(np.int32)
+    for name, p in net.named_parameters():
+        out["g32"][name] = p.grad.detach().reshape(-1).double().numpy()
+    for name, b in net.named_buffers():
+        if name.endswith("running_mean") or name.endswith("running_var"):
+            out["bufs"][name] = b.detach().numpy().copy()
+    net64 = HRegNet(_Args())
+    net64.load_state_dict(sd)
+    net64 = net64.double().train()
+    pu.replay = [c[1].clone() for c in pu.calls]
+    KNN_REPLAY = [c.clone() for c in KNN_CALLS]
+    pu.calls.clear()
+    KNN_CALLS.clear()
+    torch_eye, torch_zeros = torch.eye, torch.zeros
+    torch.eye = lambda *a, **k: torch_eye(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+    torch.zeros = lambda *a, **k: torch_zeros(*a, **{**k, "dtype": k.get("dtype", torch.float64)})
+    try:
+        r64 = net64(torch.from_numpy(s).double(), torch.from_numpy(d).double())
+        l64 = sum(L.transformation_loss(r64["rotation"][i], r64["translation"][i], gR.double(),
+                                        gt.double(), 1.0)[0] for i in range(3)) / 3.0
+        l64.backward()
+    finally:
+        torch.eye, torch.zeros = torch_eye, torch_zeros
+        pu.replay = None
+        KNN_REPLAY = None
+    out["loss64"] = float(l64.detach())
+    for name, p in net64.named_parameters():
+        out["g64"][name] = p.grad.detach().reshape(-1).numpy()
+    return out
+
+
+def ddp_fixtures(pu, B=8, N=2048, seed0=70, ranks=2):
+    """SURVEY.md 8(e) / VERDICT r3 item 1: the DDP step of train_reg_v0.py:279-296 over
+    `ranks` disjoint shards of one global batch (B / ranks pairs each, rank-local train-mode
+    BN as DDP without SyncBN runs it): each rank's gradients, their mean (what the all-reduce
+    of DistributedDataParallel hands every rank), each rank's BN running stats, and the
+    parameters after torch.optim.Adam(lr=1e-3) applies the mean gradient (identical on every
+    rank).  Saved per parameter: norms and the first 256 entries (fp32 and float64 replays)."""
+    sys.modules["pytorch3d.transforms"].matrix_to_euler_angles = p3d_matrix_to_euler_angles
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_losses", os.path.join(REF, "losses/losses.py"))
+    L = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(L)
+    from models.HRegNet.models import HRegNet  # noqa: E402  (reference code)
+    from pcd_reg_hregnet_amd import synthetic, weights
+    sd = weights.make_state_dict(HRegNet(_Args()).state_dict(), seed=0, pretrained_feats=True)
+    s, d, Rg, tg = synthetic.lidar_batch(B, N, seed0=seed0)
+    torch.set_num_threads(os.cpu_count())
+    out = {"src": s, "dst": d, "R_gt": Rg, "t_gt": tg, "ranks": np.array(ranks),
+           "lr": np.array(1e-3)}
+    per = B // ranks
+    shards = []
+    for r in range(ranks):
+        sl = slice(r * per, (r + 1) * per)
+        sh = _ref_shard_step(HRegNet, L, sd, pu, s[sl], d[sl], Rg[sl], tg[sl])
+        shards.append(sh)
+        out[f"r{r}_loss"], out[f"r{r}_loss64"] = np.array(sh["loss"]), np.array(sh["loss64"])
+        for name, idx in sh["sel"].items():
+            out[f"r{r}_idx_{name}"] = idx
+        for name, b in sh["bufs"].items():
+            out[f"r{r}_buf_{name}"] = b
+        for name, g in sh["g32"].items():
+            out[f"r{r}_gnorm_{name}"] = np.array(np.linalg.norm(g))
+            out[f"r{r}_ghead_{name}"] = g[:256].astype(np.float32)
+            g64 = sh["g64"][name]
+            out[f"r{r}_g64norm_{name}"] = np.array(np.linalg.norm(g64))
+            out[f"r{r}_g64head_{name}"] = g64[:256]
+        print(f"rank {r} shard step: loss {sh['loss']:.6f} (float64 {sh['loss64']:.6f})", flush=True)
+    names = list(shards[0]["g32"])
+    out["param_names"] = np.array(names)
+    # the all-reduced gradient: SUM over ranks, then / world (torch DDP's averaging)
+    net = HRegNet(_Args())
+    net.load_state_dict(sd)
+    params = dict(net.named_parameters())
+    for name in names:
+        g32 = sum(sh["g32"][name].astype(np.float32) for sh in shards) / np.float32(ranks)
+        g64 = sum(sh["g64"][name] for sh in shards) / ranks
+        out["mean_gnorm_" + name] = np.array(np.linalg.norm(g32.astype(np.float64)))
+        out["mean_ghead_" + name] = g32[:256].astype(np.float32)
+        out["mean_g64norm_" + name] = np.array(np.linalg.norm(g64))
+        out["mean_g64head_" + name] = g64[:256]
+        params[name].grad = torch.from_numpy(g32.astype(np.float32)).view_as(params[name])
+        out["p0head_" + name] = params[name].detach().reshape(-1)[:256].numpy().copy()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    opt.step()
+    for name in names:
+        out["p1head_" + name] = params[name].detach().reshape(-1)[:256].numpy().copy()
+    fn = f"ddp_step_r{ranks}_b{B}_n{N}.npz"
+    np.savez_compressed(os.path.join(HERE, fn), **out)
+    print(fn, "written", flush=True)
 
 
 def _ref_adam_trajectory(HRegNet, L, sd, s, d, Rg, tg, steps, dtype):
@@ -1020,6 +1168,9 @@ def main():
     if "--train-only" in sys.argv:
         train_fixtures(pu)
         return
+    if "--ddp-only" in sys.argv:
+        ddp_fixtures(pu)
+        return
     if "--traj-only" in sys.argv:
         # B=2 x 2048 pts, 6 steps (test fixture); config 4's shard shape (8 x 16384, the
         # bench's rank-0 batch, seed0 0) with --traj-c4, 14 steps
@@ -1030,6 +1181,9 @@ def main():
         return
     if "--v2-train-only" in sys.argv:
         v2_train_fixtures(pu)
+        return
+    if "--v2-b2-65536" in sys.argv:
+        v2_b2_65536_fixture(pu)
         return
     if "--v2-only" in sys.argv:
         v2_fixtures(pu)

@@ -608,12 +608,15 @@ def net_v2():
 
 
 @pytest.mark.parametrize("fixture", ["model_v2_lidar_b2_n4096.npz",
-                                     "model_v2_lidar_b1_n65536.npz"])
+                                     "model_v2_lidar_b1_n65536.npz",
+                                     "model_v2_lidar_b2_n65536.npz"])
 def test_model_v2_matches_reference_fixture(net_v2, fixture):
     """Model_V2 against the reference's own run of the same
     weights/inputs; torch's generator is seeded as the fixture run was, so the
-    randperm "prime" shuffles are the same draws.  The N=65536 case is config 5's
-    cloud size (level-1 FPS from HBM, brute-force level-1 grouping)."""
+    randperm "prime" shuffles are the same draws.  The N=65536 cases are config 5's
+    cloud size (level-1 FPS on the multi-workgroup cluster kernel, spatially indexed
+    level-1 grouping); at B=2 the fixture's seed makes both prime shuffles the swap
+    (model_v2/layers.py:492,497), so the batch permutation is exercised at that size."""
     from test_oracle_golden import compare_v2
     from pcd_reg_hregnet_amd import engine
     g = load_npz(fixture)
@@ -642,6 +645,9 @@ def test_model_v2_matches_reference_fixture(net_v2, fixture):
     np.testing.assert_array_equal(r["_fps_idx"][0][:B], g["src_fps_1"])
     np.testing.assert_array_equal(r["_fps_idx"][0][B:], g["dst_fps_1"])
     compare_v2(r, g, title="GPU vs " + fixture)
+    if fixture == "model_v2_lidar_b2_n65536.npz":  # the shuffle is the swap, not the identity
+        np.testing.assert_array_equal(g["src_dst_weights_2_prime"][0], g["src_dst_weights_2"][1])
+        np.testing.assert_array_equal(r["src_dst_weights_2_prime"][0], r["src_dst_weights_2"][1])
 
 
 def test_model_v2_module_api(net_v2):

@@ -169,6 +169,24 @@ def test_knn_gather_and_grad():
     for b in range(2):
         np.add.at(cnt[b], idx[b].reshape(-1), 1)
     np.testing.assert_allclose(xt.grad.cpu().numpy(), np.repeat(cnt[..., None], 7, -1), rtol=1e-6)
+    # random gradients, padded (-1) entries: the CSR scatter sums in ascending (m, k) order --
+    # the fp32 serial sum, bitwise -- and is deterministic run to run (no atomics)
+    idx[0, 3, 2] = -1
+    idx[1, 7, :] = -1
+    go = rng.normal(size=(2, 20, 4, 7)).astype(np.float32)
+    grads = []
+    for _ in range(2):
+        xt.grad = None
+        knn_gather(xt, dev(idx)).backward(dev(go))
+        grads.append(xt.grad.cpu().numpy())
+    want = np.zeros((2, 50, 7), np.float32)
+    for b in range(2):
+        for m in range(20):
+            for k in range(4):
+                if idx[b, m, k] >= 0:
+                    want[b, idx[b, m, k]] += go[b, m, k]
+    np.testing.assert_array_equal(grads[0], want)
+    np.testing.assert_array_equal(grads[1], grads[0])
 
 
 @pytest.mark.parametrize("R,N,segs", [

@@ -62,7 +62,7 @@ def test_conv_bn_act_accumulates_into_existing_grad_bitwise(bias):
     (the trainer's gradient bucket): the backward adds dW / dbias / dgamma / dbeta into
     .grad itself (train._grad_slot) -- bitwise the gradients autograd's own accumulation
     gives when .grad starts as None."""
-    from pcd_reg_hregnet_amd.train import conv_bn_act
+    from pcd_reg_hregnet_amd.train import conv_bn_act, direct_gradients
     g = torch.Generator(device="cpu").manual_seed(7)
     R, K, N = 8192, 36, 64
     xs = [(torch.randn(R, K, generator=g) * 2).cuda() for _ in range(2)]
@@ -83,7 +83,8 @@ def test_conv_bn_act_accumulates_into_existing_grad_bitwise(bias):
             out = conv_bn_act(x, ps[0].view(N, K), ps[1] if bias else None, ps[2], ps[3], rm, rv,
                               True, wparam=ps[0])
             loss = loss + (out * G).sum()
-        loss.backward()
+        with direct_gradients():
+            loss.backward()
         grads.append([p.grad.clone() if p.grad is not None else None for p in ps])
     for a, r, name in zip(grads[1], grads[0], ("dW", "dbias", "dgamma", "dbeta")):
         if name == "dbias" and not bias:

@@ -106,3 +106,46 @@ def test_two_stream_step_matches_serial_bitwise(graphed):
     assert torch.equal(ser.opt.m, two.opt.m) and torch.equal(ser.opt.v, two.opt.v)
     for (na, a), (_, b) in zip(ser.net.named_buffers(), two.net.named_buffers()):
         assert torch.equal(a, b), na
+
+
+def test_graph_trainer_plain_loop_trains_on_given_batches():
+    """``for b in loader: gt.step(*b)`` (no next_batch announced) trains each step on
+    the points it is given -- a batch that was not announced is copied in and its selections
+    computed before the replay -- bitwise the eager trainer's steps; a batch mutated in place
+    after being announced is reloaded too."""
+    from pcd_reg_hregnet_amd import _lib, trainer
+    _lib.load()
+    B, n = 2, 4096
+    batches = _batches(B, n, 4)
+    eager, graphed = _trainer(), _trainer()
+    gt = trainer.GraphTrainer(graphed, B, n)
+    gt.capture(*batches[0])
+    le = [eager.step(*b)[0].clone() for b in batches]
+    lg = [gt.step(*b)[0].clone() for b in batches]
+    # announced, then rewritten in place before its step: the new contents are used
+    s, d, R, t = (x.clone() for x in batches[0])
+    le.append(eager.step(s, d, R, t, next_batch=(s, d))[0].clone())
+    lg.append(gt.step(s, d, R, t, next_batch=(s, d))[0].clone())
+    s.copy_(batches[1][0])
+    le.append(eager.step(s, d, R, t)[0].clone())
+    lg.append(gt.step(s, d, R, t)[0].clone())
+    torch.cuda.synchronize()
+    print("eager", [float(x) for x in le], "graph", [float(x) for x in lg])
+    for a, b in zip(le, lg):
+        assert torch.equal(a, b)
+    assert torch.equal(eager.params.flat, graphed.params.flat)
+
+
+def test_graph_trainer_rejects_random_sampling():
+    """use_fps=False draws host samples every step; a graph would freeze one draw."""
+    import bench
+    from pcd_reg_hregnet_amd import trainer, weights
+    from pcd_reg_hregnet_amd.models import HRegNet
+
+    class NoFps(bench._Args):
+        use_fps = False
+    net = HRegNet(NoFps())
+    net.load_state_dict(weights.make_state_dict(net.state_dict(), seed=0, pretrained_feats=True))
+    tr = trainer.Trainer(net.cuda(), lr=1e-3)
+    with pytest.raises(NotImplementedError):
+        trainer.GraphTrainer(tr, 2, 4096)

@@ -1,0 +1,158 @@
+"""SURVEY.md 8(e) / VERDICT r3 item 1: the data-parallel training step against the reference's.
+
+tests/golden/ddp_step_r2_b8_n2048.npz (make_golden.py ddp_fixtures) holds the reference's
+DDP step of train/train_reg_v0.py:279-296 over two disjoint shards of one 8-pair batch: each
+rank's train-mode forward + backward on its 4 pairs (BatchNorm statistics of the shard alone,
+as DistributedDataParallel without SyncBN), the all-reduced gradient (sum over ranks / world),
+each rank's BN running statistics, and the parameters after torch.optim.Adam(lr 1e-3) applies
+the averaged gradient.  Here two trainer.Trainer instances, one per rank, run their shards in
+one process (``local_gradients``: everything before the collective), the two gradient buckets
+are averaged as GradBucket.all_reduce_mean does (SUM, then / world; the wire itself is the
+gloo test in tests/test_distributed.py), and each rank's FlatAdam steps.  Checked:
+
+* each rank's loss (rtol 1e-5) and local gradients, and the averaged gradient, against the
+  reference's float64 replay within max(4 x the fp32 reference's own error, floor) -- the bars
+  of test_train_step_matches_reference_gradients (FLIP_BAR for the near-tie-prone
+  feature-extraction and neighbour-branch parameters, 1e-3 elsewhere);
+* each rank's BN running statistics (rtol 1e-4, atol 1e-5): rank-local, not synchronised;
+* the parameters after the step: bitwise equal on both ranks, and equal to the reference's
+  post-Adam parameters wherever Adam's first update (lr * g / (|g| + eps), a sign step for
+  |g| >> eps) is determined by the gradient: entries whose float64 mean gradient is larger than
+  4 x the fp32 reference's own error there.  Entries below that are rounding noise (conv
+  biases feeding a train-mode BN) whose sign is arbitrary in any fp32 implementation; their
+  count is printed.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import load_npz
+from test_gpu_train_graph import FLIP_BAR, _train_net
+
+pytestmark = pytest.mark.gpu
+
+FIXTURE = "ddp_step_r2_b8_n2048.npz"
+
+
+def _grad_rows(fx, grads, prefix, ref64, label):
+    """(ratio to bar, ours, ref, name) per parameter: ours / the fp32 reference's distance
+    from the float64 gradient (norm and leading entries, max-normalised)"""
+    names = [str(n) for n in fx["param_names"]]
+    gmax = max(float(fx[ref64 + "norm_" + n]) for n in names)
+    rows, noise, bars = [], [], {}
+    for name in names:
+        g = grads[name]
+        n64 = float(fx[ref64 + "norm_" + name])
+        n32 = float(fx[prefix + "gnorm_" + name])
+        h64 = fx[ref64 + "head_" + name].astype(np.float64)
+        h32 = fx[prefix + "ghead_" + name].astype(np.float64)
+        if n64 < 1e-6 * gmax:  # rounding noise (conv bias before a train-mode BN)
+            noise.append(name)
+            assert np.linalg.norm(g) < 1e-5 * gmax, (label, name)
+            continue
+        hs = max(np.abs(h64).max(), 1e-30)
+        ours = max(abs(np.linalg.norm(g) - n64) / n64, np.abs(g[:h64.size] - h64).max() / hs)
+        ref = max(abs(n32 - n64) / n64, np.abs(h32 - h64).max() / hs)
+        floor = FLIP_BAR if (name.startswith("feature_extraction.") or ".convs_2." in name) else 1e-3
+        rows.append((ours / max(4 * ref, floor), ours, ref, name))
+        bars[name] = max(4 * ref, floor) * hs  # the absolute error the entries are held to
+    return rows, noise, bars
+
+
+def _bucket_grads(tr):
+    """parameter name -> this rank's gradient (float64 numpy) from its bucket"""
+    views = {id(p): v for p, v in zip(tr.bucket.params, tr.bucket.views)}
+    return {n: views[id(p)].detach().reshape(-1).double().cpu().numpy()
+            for n, p in tr.net.named_parameters() if p.requires_grad}
+
+
+def test_ddp_step_matches_reference_shards():
+    from pcd_reg_hregnet_amd import train_graph, trainer
+    fx = load_npz(FIXTURE)
+    ranks = int(fx["ranks"])
+    B = fx["src"].shape[0]
+    per = B // ranks
+    dev = torch.device("cuda")
+    src, dst = torch.from_numpy(fx["src"]).to(dev), torch.from_numpy(fx["dst"]).to(dev)
+    gR, gt = torch.from_numpy(fx["R_gt"]).to(dev), torch.from_numpy(fx["t_gt"]).to(dev)
+    trs = [trainer.Trainer(_train_net(), lr=float(fx["lr"])) for _ in range(ranks)]
+    p0 = trs[0].params.flat.clone()
+    report = []
+    for r, tr in enumerate(trs):
+        sl = slice(r * per, (r + 1) * per)
+        pre = f"r{r}_idx_"
+        hook = train_graph.IndexHook({k[len(pre):]: fx[k] for k in fx if k.startswith(pre)})
+        loss = tr.local_gradients(src[sl].contiguous(), dst[sl].contiguous(), gR[sl].contiguous(),
+                                  gt[sl].contiguous(), hook)[0]
+        np.testing.assert_allclose(float(loss), float(fx[f"r{r}_loss"]), rtol=1e-5)
+        rows, _, _ = _grad_rows(fx, _bucket_grads(tr), f"r{r}_", f"r{r}_g64", f"rank {r}")
+        report.append((f"rank {r} local gradients", rows))
+        # rank-local BN running statistics (no SyncBN)
+        bufs = dict(tr.net.named_buffers())
+        nb = 0
+        for key in fx:
+            if key.startswith(f"r{r}_buf_"):
+                name = key[len(f"r{r}_buf_"):]
+                np.testing.assert_allclose(bufs[name].cpu().numpy(), fx[key], rtol=1e-4, atol=1e-5,
+                                           err_msg=f"rank {r} {name}")
+                nb += 1
+        assert nb > 0
+    # the all-reduce (GradBucket.all_reduce_mean: SUM over ranks, then / world)
+    total = trs[0].bucket.flat.clone()
+    for tr in trs[1:]:
+        total += tr.bucket.flat
+    mean = total / ranks
+    for tr in trs:
+        tr.bucket.flat.copy_(mean)
+    rows, noise, bars = _grad_rows(fx, _bucket_grads(trs[0]), "mean_", "mean_g64", "mean")
+    report.append(("all-reduced (mean) gradients", rows))
+    for tr in trs:
+        tr.opt.step()
+    torch.cuda.synchronize()
+    for title, rows in report:
+        print(f"\n{title}: ratio to bar, ours vs fp64, fp32 ref vs fp64 (worst 8 of {len(rows)})")
+        for row in sorted(rows, reverse=True)[:8]:
+            print("  %.3f  %.2e  %.2e  %s" % row)
+        worst = max(rows)
+        assert worst[0] <= 1.0, (title, worst)
+    assert torch.equal(trs[0].params.flat, trs[1].params.flat)  # every rank applies one update
+    # post-Adam parameters vs the reference's, where the update is determined by the gradient
+    from pcd_reg_hregnet_amd.train import flat_offsets
+    params = dict(trs[0].net.named_parameters())
+    flat_before = {}
+    offs, _ = flat_offsets(trs[0].params.params)
+    name_of = {id(p): n for n, p in trs[0].net.named_parameters()}
+    for p, o in zip(trs[0].params.params, offs):
+        flat_before[name_of[id(p)]] = p0[o:o + min(256, p.numel())].double().cpu().numpy()
+    checked = ambiguous = 0
+    worst = 0.0
+    for name in [str(n) for n in fx["param_names"]]:
+        after = params[name].detach().reshape(-1)[:256].double().cpu().numpy()
+        np.testing.assert_array_equal(flat_before[name].astype(np.float32),
+                                      fx["p0head_" + name], err_msg=name)
+        if name in noise:
+            ambiguous += after.size
+            continue
+        ref_after = fx["p1head_" + name].astype(np.float64)
+        g64 = fx["mean_g64head_" + name].astype(np.float64)
+        g32 = fx["mean_ghead_" + name].astype(np.float64)
+        # the update's sign is fixed where |g64| exceeds both the fp32 reference's error and
+        # the error bar our gradient passed above (so both gradients share g64's sign)
+        err = np.maximum(4 * np.abs(g32 - g64), bars[name])
+        determined = np.abs(g64) > 2 * err
+        ambiguous += int((~determined).sum())
+        checked += int(determined.sum())
+        if determined.any():
+            # Adam's first update lr * g / (|g| + eps) moves by at most
+            # lr * eps * 2 err / (|g| - err)^2 when g moves by err (both gradients lie within err
+            # of g64), plus the fp32 rounding of p -+ lr (~6e-8 |p|)
+            lr, eps = float(fx["lr"]), 1e-8
+            a = np.abs(g64) - err
+            tol = lr * eps * 2 * err / a ** 2 + 1e-7 + 2e-7 * np.abs(ref_after)
+            e = np.abs(after - ref_after)
+            worst = max(worst, float(e[determined].max()))
+            bad = determined & (e > tol)
+            assert not bad.any(), (name, e[bad][:4], tol[bad][:4])
+    print(f"\npost-Adam parameters: {checked} leading entries compared (max |diff| {worst:.2e}), "
+          f"{ambiguous} entries below their gradient's error bar or rounding noise skipped")
+    assert checked > ambiguous

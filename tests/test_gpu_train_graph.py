@@ -379,31 +379,58 @@ def _ref_fixture():
     return load_npz("train_step_b2_n2048.npz")
 
 
+def _train_layout(fx, ret, record):
+    """our train-mode forward (and its recorded selections) and the reference's
+    (train_step_b2_n2048.npz) in the tests/parity.py fixture layout"""
+    B = fx["src"].shape[0]
+    ours, ref = {}, {k: fx[k] for k in ("src", "dst")}
+    for part in ("src", "dst"):
+        f = ret[f"{part}_feats"]
+        for lv in (1, 2, 3):
+            for q in ("xyz", "sigmas", "desc"):
+                ours[f"{part}_{q}_{lv}"] = f[f"{q}_{lv}"].detach().cpu().numpy()
+                ref[f"{part}_{q}_{lv}"] = fx[f"{part}_{q}_{lv}"]
+            ref[f"{part}_fps_{lv}"] = fx[f"idx_{part}_fps_{lv}"]
+            ours[f"{part}_fps_{lv}"] = record[f"{part}_fps_{lv}"].cpu().numpy().reshape(B, -1)
+    for i, lv in enumerate((3, 2, 1)):
+        ours[f"R{lv}"] = ret["rotation"][i].detach().cpu().numpy()
+        ours[f"t{lv}"] = ret["translation"][i].detach().cpu().numpy()
+        ref[f"R{lv}"], ref[f"t{lv}"] = fx[f"R{lv}"], fx[f"t{lv}"]
+        ours[f"corres_{lv}"] = ret[f"src_xyz_corres_{lv}"].detach().cpu().numpy()
+        ours[f"weights_{lv}"] = ret[f"src_dst_weights_{lv}"].detach().cpu().numpy()
+        ref[f"corres_{lv}"], ref[f"weights_{lv}"] = fx[f"corres_{lv}"], fx[f"weights_{lv}"]
+    import parity
+    for name in parity.KNN_NAMES:
+        r = fx["idx_" + name]
+        ref["knn_" + name] = r
+        ours["knn_" + name] = record[name].cpu().numpy().reshape(r.shape)
+    return ours, ref
+
+
 def test_train_selections_match_reference():
-    """Our FPS/WFPS and kNN selections in the train-mode forward vs the reference's own
-    (tests/golden/train_step_b2_n2048.npz, make_golden.py train_fixtures): input-only
-    level-1 selections bit-exact; the later ones depend on fp32 GEMM sums and may flip a
-    near tie (<= 1 % of indices)."""
+    """Our FPS/WFPS and kNN selections in the train-mode forward (batch-statistics BN) vs the
+    reference's own (tests/golden/train_step_b2_n2048.npz, make_golden.py train_fixtures),
+    under the eval forward's contract (tests/parity.py): level-1 FPS and kNN indices bit-exact
+    (input-only); every later selection the reference's unless it is a float64 near tie on the
+    reference's own train-mode outputs (WFPS relative margin <= 2e-5, kNN k-th / (k+1)-th
+    <= 1e-5) or downstream of one; >= 95 % of every level's and head's rows unaffected; R/t
+    within 1e-4."""
+    import parity
     from pcd_reg_hregnet_amd import train_graph
     fx = _ref_fixture()
     net = _train_net()
     hook = train_graph.IndexHook()
     with torch.no_grad():
-        train_graph.hregnet_train_forward(net, torch.from_numpy(fx["src"]).to(DEV),
-                                          torch.from_numpy(fx["dst"]).to(DEV), hook)
+        ret = train_graph.hregnet_train_forward(net, torch.from_numpy(fx["src"]).to(DEV),
+                                                torch.from_numpy(fx["dst"]).to(DEV), hook)
     for name in ("src_fps_1", "dst_fps_1", "src_knn_1", "dst_knn_1"):
         ref = fx["idx_" + name]
         np.testing.assert_array_equal(hook.record[name].cpu().numpy().reshape(ref.shape), ref,
                                       name)
-    for key in fx:
-        if not key.startswith("idx_"):
-            continue
-        name = key[4:]
-        ref = fx[key]
-        ours = hook.record[name].cpu().numpy().reshape(ref.shape)
-        assert ours.shape == ref.shape, name
-        frac = (ours != ref).mean()
-        assert frac <= 0.01, (name, frac)
+    ours, ref = _train_layout(fx, ret, hook.record)
+    st, bad = parity.evaluate(ours, ref, continuous=False)
+    parity.report(st, "train-mode forward (GPU) vs train_step_b2_n2048.npz", bad)
+    assert not bad, "\n".join(bad)
 
 
 # Near-tie bar for feature-extraction gradients.  A max over k (DescExtractor k-max,

@@ -103,14 +103,6 @@ def test_random_sample_draws_match_reference():
         np.testing.assert_array_equal(got[lv - 1].numpy(), want)
 
 
-# Model_V2 outputs indexed by source keypoint: [B, M, ...] (channel-major ones transposed)
-V2_ROWS = {"src_xyz_corres_3": 1e-3, "src_xyz_corres_2": 1e-3, "src_xyz_corres_1": 1e-3,
-           "src_xyz_2_trans": 1e-3, "src_feats_sigmas_2": 1e-3, "src_feats_desc_2": 1e-3,
-           "src_dst_feats_2": 1e-3, "src_dst_feats_2_prime": 1e-3,
-           "src_dst_weights_2": 1e-3, "src_dst_weights_2_prime": 1e-3}
-V2_CHANNEL_MAJOR = ("src_feats_desc_2", "src_dst_feats_2", "src_dst_feats_2_prime")
-
-
 def compare_v2(r, g, title=""):
     """Model_V2 parity (model_v2/models.py:170-183): the HRegNet contract of
     compare_forward on its shared outputs, then the Model_V2 extras (the transformed level-2
@@ -133,7 +125,7 @@ def compare_v2(r, g, title=""):
         st[key + "_vs_f64"] = e = parity.nerr(a[ok], b[ok])
         if e > parity.feat_bar(q):
             bad.append(f"{key}: {e:.2e} > bar {parity.feat_bar(q):.2e}")
-    parity.report(st, title)
+    parity.report(st, title, bad)
     assert not bad, "\n".join(bad)
     a = np.asarray(r["dst_xyz_2"])
     assert np.array_equal(a, np.asarray(r["dst_feats"]["xyz_2"]))
@@ -150,7 +142,8 @@ def compare_v2(r, g, title=""):
 
 
 @pytest.mark.parametrize("fixture", ["model_v2_lidar_b2_n4096.npz",
-                                     "model_v2_lidar_b1_n65536.npz"])
+                                     "model_v2_lidar_b1_n65536.npz",
+                                     "model_v2_lidar_b2_n65536.npz"])
 def test_model_v2_matches_reference(fixture):
     """oracle.model_v2_forward vs the reference Model_V2 run (make_golden.py)."""
     g = load_npz(fixture)

@@ -1,7 +1,12 @@
 """Summaries of rocprofv3 runs for profiles/ (reads the rocpd SQLite output or the
 --output-format csv files).
 
-  kernel stats:  python tools/rocpd_summary.py stats <run_results.db | kernel_stats.csv> <steps> [out.md]
+  kernel stats:  python tools/rocpd_summary.py stats <run_results.db | kernel_stats.csv> <steps | per:KERNEL[/n]> [out.md]
+                 per:KERNEL -- normalise by the forwards the trace holds: calls of the kernel
+                 family KERNEL (launched n times per forward, default 1), so every launch of the
+                 run (warm-up, capture, graph replays, instrumented eager pass) is counted once
+                 and divided by the number of forwards that made it (VERDICT r3 weak item 9:
+                 dividing ~100 launches per kernel by the 48 timed steps overstated ms/step)
   HBM traffic:   python tools/rocpd_summary.py traffic <fetch .db|csv> <write .db|csv> [out.md] [out.json]
   MFMA use:      python tools/rocpd_summary.py mfma <counter_collection.csv> [out.md] [out.json]
 
@@ -56,7 +61,18 @@ def counter_values(path, counter):
 def stats(path, steps, out=None):
     rows = kernel_rows(path)
     tot = sum(r[2] for r in rows)
-    lines = ["| kernel | calls | calls/step | avg us | ms/step | % |", "|---|---|---|---|---|---|"]
+    head = []
+    if isinstance(steps, str) and steps.startswith("per:"):
+        fam, _, per = steps[4:].partition("/")
+        calls = sum(r[1] for r in rows if fam in r[0])
+        if calls == 0:
+            raise SystemExit(f"no launches of {fam} in {path}")
+        steps = calls / int(per or 1)
+        head = [f"Normalised per forward: {steps:g} forwards in the trace ({calls} launches of "
+                f"`{fam}`, {per or 1} per forward); every launch of the run is included.", ""]
+    else:
+        steps = int(steps)
+    lines = head + ["| kernel | calls | calls/step | avg us | ms/step | % |", "|---|---|---|---|---|---|"]
     for name, calls, ns in sorted(rows, key=lambda r: -r[2]):
         lines.append(f"| `{short(name)[:90]}` | {calls} | {calls / steps:.1f} | {ns / calls / 1e3:.2f} | "
                      f"{ns / 1e6 / steps:.3f} | {100 * ns / tot:.1f} |")
@@ -185,7 +201,7 @@ if __name__ == "__main__":
         mfma(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None,
              sys.argv[4] if len(sys.argv) > 4 else None)
     elif sys.argv[1] == "stats":
-        stats(sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else None)
+        stats(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None)
     else:
         traffic(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None,
                 sys.argv[5] if len(sys.argv) > 5 else None)
