@@ -491,42 +491,13 @@ int hreg_spatial_index(const float *p, int nb, int n, void *ws, void *stream);
 int hreg_knn_group_indexed(const float *q, const float *p, const void *ws, int nb, int m, int n,
                            int k, int32_t *gidx, float *geom, float *knn_xyz, void *stream);
 
-/* Fused level-1 grouping stage (KeypointDetector.convs/mlp + attention + DescExtractor
- * convs + k-max + mlp, layers.py:115-130 and 183-198, with C=64, nsample=32):
- * one wavefront per group of 32 neighbours, every 1x1-conv+BN+ReLU layer chained
- * through MFMA accumulators.  table = the folded, fragment-permuted weights
- * (hreg_group_l1_table_floats() floats, built by engine.l1_table);
- * geom [G][32] float4 and knn_xyz [G][32][3] from hreg_knn_group ->
- * kp [G][3], att_feat [G][64] (attentive feature), desc [G][64]. */
-int hreg_group_l1_table_floats(void);
-int hreg_group_l1(const float *table, const float *geom, const float *knn_xyz, int G,
-                  float *kp, float *att_feat, float *desc, void *stream);
-
-/* Fused level-2 grouping stage (same layers as hreg_group_l1 with C_in = 4 + 64,
- * convs 68->64->64->128, mlp 384->64->128, nsample = 32): one wavefront per group.
- * table = hreg_group_l2_table_floats() floats (engine.l2_table); geom [G][32] float4
- * and knn_xyz [G][32][3] from hreg_knn_group; gidx [G*32] rows of feats
- * [*][64] (the level-1 attentive features, 16-byte aligned) ->
- * kp [G][3], att_feat [G][128], desc [G][128].  pre (optional, levels 2 and 3, both
- * kernels): [*][2 * C1] = [W_det_f | W_desc_f] feats, the feature blocks of the two
- * first layers precomputed once per feature row (same gidx): then only the 4 geometry
- * columns of those layers run per grouped row. */
-int hreg_group_l2_table_floats(void);
-int hreg_group_l2(const float *table, const float *geom, const float *knn_xyz,
-                  const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
-                  float *desc, const float *pre, void *stream);
-
-/* Fused level-3 grouping stage: C_in = 4 + 128, convs 132->128->128->256,
- * mlp 768->128->256, nsample = 16 (two groups per 32-row tile, G even);
- * feats [*][128] (the level-2 attentive features) -> kp [G][3],
- * att_feat [G][256], desc [G][256]. */
-int hreg_group_l3_table_floats(void);
-int hreg_group_l3(const float *table, const float *geom, const float *knn_xyz,
-                  const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
-                  float *desc, const float *pre, void *stream);
-
-/* The level-1 stage (hreg_group_l1) with fp32-accurate products on the bf16 matrix cores
- * (bf16x6 split, group_l1_6.hip): same arguments and outputs, table =
+/* Fused level-1 grouping stage (KeypointDetector.convs/mlp + attention + DescExtractor convs
+ * + k-max + mlp, layers.py:115-130 and 183-198, with C = 64, nsample = 64): one wavefront per
+ * group, every 1x1-conv+BN+ReLU layer chained through the MFMA accumulators, fp32-accurate
+ * products on the bf16 matrix cores (bf16x6 split, group_l1_6.hip); geom [G][64] float4 and
+ * knn_xyz [G][64][3] from hreg_knn_group(_indexed) -> kp [G][3], att_feat [G][64] (attentive
+ * feature), desc [G][64].  (The fp32-MFMA twins hreg_group_l1 / _l2 / _l3 / _split_l{2,3} are
+ * test checkers in libhregnet_checkers.so, include/hregnet_amd_checkers.h.)  table =
  * hreg_group_l1_6_table_floats() floats (engine.l1_table6), 16-byte aligned. */
 int hreg_group_l1_6_table_floats(void);
 int hreg_group_l1_6(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
@@ -537,8 +508,13 @@ int hreg_group_l1_6(const float *table, const float *geom, const float *knn_xyz,
 int hreg_group_l1_6g(const float *table, const float *geom, const float *knn_xyz, int G, float *kp,
                      float *att_feat, float *desc, void *stream);
 
-/* The level-2 / level-3 stages above with fp32-accurate products on the bf16 matrix
- * cores (bf16x6 split, group_fused6.hip): same arguments and outputs, table =
+/* Fused level-2 / level-3 grouping stages (C_in = 4 + 64 / 4 + 128, convs 68->64->64->128 /
+ * 132->128->128->256, mlp 384->64->128 / 768->128->256, nsample = 32 / 16), fp32-accurate
+ * products on the bf16 matrix cores (bf16x6 split, group_fused6.hip): geom [G][k] float4 and
+ * knn_xyz [G][k][3] from hreg_knn_group; gidx [G*k] rows of feats (the previous level's
+ * attentive features, 16-byte aligned) -> kp [G][3], att_feat [G][2C], desc [G][2C]; pre
+ * (optional): [*][2 * C1] = [W_det_f | W_desc_f] feats, the feature blocks of the two first
+ * layers precomputed once per feature row.  table =
  * hreg_group6_l{2,3}_table_floats() floats (engine.l2_table6: bf16 piece fragments of
  * the same blocks, then the f32 epilogues), 16-byte aligned. */
 int hreg_group6_l2_table_floats(void);
@@ -571,19 +547,6 @@ int hreg_group6_l3_table_floats(void);
 int hreg_group6_l3(const float *table, const float *geom, const float *knn_xyz,
                    const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                    float *desc, const float *pre, void *stream);
-
-/* The level-2 / level-3 stages above on the channel-split kernel (group_split.hip):
- * same arguments and outputs, table = hreg_group_split_l{2,3}_table_floats() floats
- * (engine.split_table: the same blocks, fragments grouped 4 k-steps per lane); geom
- * must be 16-byte aligned. */
-int hreg_group_split_l2_table_floats(void);
-int hreg_group_split_l2(const float *table, const float *geom, const float *knn_xyz,
-                        const int32_t *gidx, const float *feats, int G, float *kp,
-                        float *att_feat, float *desc, const float *pre, void *stream);
-int hreg_group_split_l3_table_floats(void);
-int hreg_group_split_l3(const float *table, const float *geom, const float *knn_xyz,
-                        const int32_t *gidx, const float *feats, int G, float *kp,
-                        float *att_feat, float *desc, const float *pre, void *stream);
 
 /* Fused FineReg head (layers.py:433-451) for C = 64 (fine_corres_1) or 128
  * (fine_corres_2): small [G*8][16] from hreg_pair_feats (ldf 16), src_desc [G][C]

@@ -75,16 +75,11 @@ _SIGS = {
     "hreg_transform_points": [_vp, _vp, _vp, _i, _i, _vp, _vp],
     "hreg_transformation_loss": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
                                  _vp],
-    "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l1_6": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l1_6g": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
-    "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
-    "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
-    "hreg_group_split_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group6_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group6x2_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group6_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
-    "hreg_group_split_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split6_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split6_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split6j_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
@@ -168,18 +163,51 @@ _SIGS = {
     "hreg_icp_result": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 
+# the fp32-MFMA twins of the level kernels: test checkers in libhregnet_checkers.so
+# (include/hregnet_amd_checkers.h), loaded only when a checker is called
+_CHECKER_SIGS = {
+    "hreg_group_l1": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
+    "hreg_group_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group_split_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_group_split_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+}
+_CHECKER_TABLES = ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
+                   "hreg_group_l3_table_floats", "hreg_group_split_l2_table_floats",
+                   "hreg_group_split_l3_table_floats")
+CHECKER_EXPORTS = tuple(_CHECKER_SIGS) + _CHECKER_TABLES
+CHECKER_PATH = os.path.join(_HERE, "libhregnet_checkers.so")
+
 EXPORTS = tuple(_SIGS) + ("hreg_version", "hreg_spatial_index_bytes", "hreg_col_reduce_ws_bytes",
                           "hreg_gemm_tn_ws_bytes", "hreg_csr_ws_bytes", "hreg_ts_gemm_bn_ws_bytes",
-                          "hreg_sim_feats_bwd_ws_bytes", "hreg_group_l1_table_floats",
-                          "hreg_group_l2_table_floats", "hreg_group_l3_table_floats",
-                          "hreg_nbr_head_table_floats", "hreg_group_split_l2_table_floats",
-                          "hreg_group_split_l3_table_floats", "hreg_group6_l2_table_floats",
+                          "hreg_sim_feats_bwd_ws_bytes",
+                          "hreg_nbr_head_table_floats", "hreg_group6_l2_table_floats",
                           "hreg_group6_l3_table_floats", "hreg_group_l1_6_table_floats",
                           "hreg_group_split6_l2_table_floats", "hreg_group_split6_l3_table_floats",
                           "hreg_coarse_head6_table_floats", "hreg_icp_ws_bytes")
 
 _lib = None
+_checkers = None
 
+
+def load_checkers(require_gpu: bool = True):
+    """The test-only checker library (fp32-MFMA level kernels); raises if it is not built."""
+    global _checkers
+    load(require_gpu)  # the product library first: one HIP runtime, one set of streams
+    if _checkers is None:
+        if not os.path.exists(CHECKER_PATH):
+            raise RuntimeError(f"{CHECKER_PATH} not found: build it with "
+                               "`python -m pcd_reg_hregnet_amd.build` (test checkers only)")
+        L = ctypes.CDLL(CHECKER_PATH)
+        for name, args in _CHECKER_SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        for name in _CHECKER_TABLES:
+            getattr(L, name).restype = ctypes.c_int
+            getattr(L, name).argtypes = []
+        _checkers = L
+    return _checkers
 
 
 def load(require_gpu: bool = True):
@@ -211,10 +239,7 @@ def load(require_gpu: bool = True):
         L.hreg_icp_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.hreg_ts_gemm_bn_ws_bytes.restype = ctypes.c_size_t
         L.hreg_ts_gemm_bn_ws_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
-        for name in ("hreg_group_l1_table_floats", "hreg_group_l2_table_floats",
-                     "hreg_group_l3_table_floats", "hreg_nbr_head_table_floats",
-                     "hreg_group_split_l2_table_floats", "hreg_group_split_l3_table_floats",
-                     "hreg_group6_l2_table_floats", "hreg_group6_l3_table_floats",
+        for name in ("hreg_nbr_head_table_floats", "hreg_group6_l2_table_floats", "hreg_group6_l3_table_floats",
                      "hreg_group_l1_6_table_floats", "hreg_group_split6_l2_table_floats",
                      "hreg_group_split6_l3_table_floats", "hreg_coarse_head6_table_floats"):
             getattr(L, name).restype = ctypes.c_int
@@ -238,7 +263,7 @@ def stream_handle() -> int:
 
 
 def call(name: str, *args) -> None:
-    L = load()
+    L = load_checkers() if name in _CHECKER_SIGS else load()
     conv = []
     for a in args:
         if isinstance(a, torch.Tensor):

@@ -3,7 +3,9 @@
 Used by ``__graft_entry__.build()`` and ``python -m pcd_reg_hregnet_amd.build``.
 Each ``csrc/*.hip`` is compiled to an object (in parallel), then linked into
 one shared library next to this file, so it travels to the GPU box with the
-repo snapshot.
+repo snapshot.  ``csrc/checkers/*.hip`` (the fp32-MFMA twins of the level kernels,
+test checkers only) go into a separate ``libhregnet_checkers.so`` that the product path
+never loads (include/hregnet_amd_checkers.h).
 """
 from __future__ import annotations
 
@@ -17,6 +19,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJDIR = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libhregnet_amd.so")
+CHECKERS = os.path.join(CSRC, "checkers")
+CHECKER_LIB = os.path.join(HERE, "libhregnet_checkers.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HREG_ARCH", "gfx950")
 
@@ -62,15 +66,12 @@ def _compile(src: str, obj: str) -> tuple[str, int, str]:
     return src, p.returncode, p.stdout + p.stderr
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
-    os.makedirs(OBJDIR, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(
-        os.path.join(HERE, "..", "include", "*.h")) + [os.path.abspath(__file__)]
+def _build_lib(srcs, objdir, lib, headers, verbose, force) -> str:
+    os.makedirs(objdir, exist_ok=True)
     jobs = []
     objs = []
     for s in srcs:
-        o = os.path.join(OBJDIR, os.path.basename(s).replace(".hip", ".o"))
+        o = os.path.join(objdir, os.path.basename(s).replace(".hip", ".o"))
         objs.append(o)
         if force or _needs(o, [s, *headers]):
             jobs.append((s, o))
@@ -81,12 +82,21 @@ def build(verbose: bool = False, force: bool = False) -> str:
                     sys.stderr.write(f"[hipcc] {os.path.basename(src)} rc={rc}\n{log}")
                 if rc:
                     raise RuntimeError(f"hipcc failed for {src}")
-    if force or jobs or _needs(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    if force or jobs or _needs(lib, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs]
         p = subprocess.run(cmd, capture_output=True, text=True)
         if p.returncode:
             raise RuntimeError("link failed:\n" + p.stdout + p.stderr)
-    return LIB
+    return lib
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(
+        os.path.join(HERE, "..", "include", "*.h")) + [os.path.abspath(__file__)]
+    _build_lib(sorted(glob.glob(os.path.join(CHECKERS, "*.hip"))), os.path.join(OBJDIR, "checkers"),
+               CHECKER_LIB, headers, verbose, force)
+    return _build_lib(sorted(glob.glob(os.path.join(CSRC, "*.hip"))), OBJDIR, LIB, headers, verbose,
+                      force)
 
 
 if __name__ == "__main__":

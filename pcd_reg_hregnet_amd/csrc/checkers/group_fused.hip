@@ -20,7 +20,7 @@
 // The reference materialises [B, 68..384, 512, 32] tensors for this stage
 // (~1 GB of HBM traffic per batch of 8 pairs); here only the group outputs
 // (keypoint 3, attentive feature C3, descriptor CM2 floats) reach HBM.
-#include "mfma_chain.h"
+#include "../mfma_chain.h"
 
 namespace {
 

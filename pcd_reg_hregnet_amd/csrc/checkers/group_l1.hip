@@ -15,7 +15,7 @@
 // y = relu(acc * alpha + beta).  Only the group outputs (keypoint 3, attentive
 // feature 64, descriptor 64 floats) are written to HBM -- the reference
 // materialises ~1 GB of [B,C,M,k] tensors per batch here.
-#include "common.h"
+#include "../common.h"
 
 namespace {
 

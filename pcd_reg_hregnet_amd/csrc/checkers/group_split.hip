@@ -23,7 +23,7 @@
 //   stage again -> A; desc conv1 A->B, conv2 B->A, conv3 A->x1d
 //   x2 = k-max(x1d) -> X2 (one row per group), x1d -> B; mlp1 (x2, x1d parts) -> y1
 //   y1 -> A; mlp2 A -> y2, k-max -> descriptor
-#include "split_chain.h"
+#include "../split_chain.h"
 
 namespace {
 

@@ -36,6 +36,21 @@ static inline int hreg_ilog2(int v) {
 
 // ---------------------------------------------------------------- device --
 
+// XCD-aware block order (MI355X_MICROARCH.md, workgroup dispatch; cdna_hip_programming.md
+// T1): blocks are dealt round-robin over the 8 XCDs, each with its own L2, so block b and
+// b + 8 share one.  The bijective remap below hands every XCD a CONTIGUOUS range of logical
+// blocks; kernels whose neighbouring blocks read the same data (the queries of one cloud,
+// which all read that cloud's points) then fetch it into one L2 instead of eight.  Speed only:
+// the result never depends on the placement.
+#ifndef HREG_XCD
+#define HREG_XCD 1  // (A/B builds: 0 keeps the dispatch order)
+#endif
+__device__ __forceinline__ int xcd_block(int b, int nwg) {
+    if (!HREG_XCD) return b;
+    const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 // Non-contracted float arithmetic: the whole library builds with
 // -ffp-contract=off; these make the intent explicit where order matters.
 __device__ __forceinline__ float fmul_rn(float a, float b) { return __fmul_rn(a, b); }

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void knn3_kernel(const float *__restrict__ q,
                                                    float *__restrict__ nn, int k) {
     __shared__ uint64_t sbuf[WAVES][128];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = blockIdx.x * WAVES + w;
+    const int qi = xcd_block(blockIdx.x, gridDim.x) * WAVES + w;
     if (qi >= nb * n1) return;
     const int cloud = qi / n1;
     const float *P = p + (size_t)cloud * n2 * 3;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void knn_group_kernel(const float *__restrict_
                                                         float *__restrict__ knn_xyz) {
     __shared__ uint64_t sbuf[WAVES][128];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = blockIdx.x * WAVES + w;
+    const int qi = xcd_block(blockIdx.x, gridDim.x) * WAVES + w;
     if (qi >= nb * m) return;
     const int cloud = qi / m;
     const float *P = p + (size_t)cloud * n * 3;
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void knnd_kernel(const float *__restrict__ q,
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const int nq = nb * n1;
-    const int q0 = blockIdx.x * QB;  // queries of one block never straddle clouds: n1 % QB == 0
+    const int q0 = xcd_block(blockIdx.x, gridDim.x) * QB;  // queries of one block never straddle clouds: n1 % QB == 0
     const int cloud = q0 / n1;
     const float *P = p + (size_t)cloud * n2 * dim;
     WaveList L[QPW];
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void knnd_wave_kernel(const float *__restrict_
                                                         float *__restrict__ nn, int k) {
     __shared__ uint64_t sbuf[WAVES][128];
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int qi = blockIdx.x * WAVES + w;
+    const int qi = xcd_block(blockIdx.x, gridDim.x) * WAVES + w;
     if (qi >= nb * n1) return;  // wave-uniform
     const int cloud = qi / n1;
     const float *P = p + (size_t)cloud * n2 * dim;
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
     constexpr uint32_t HI = ~((1u << IDB) - 1u);
     __shared__ uint64_t sbuf[WAVES][128];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = blockIdx.x * WAVES + w;
+    const int qi = xcd_block(blockIdx.x, gridDim.x) * WAVES + w;
     if (qi >= nb * m) return;
     const int cloud = qi / m;
     int np = 64;

@@ -17,12 +17,11 @@ order-independent up to fp32 rounding).
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 
 import torch
 
-from . import _lib, capture
+from . import _lib, capture, switches
 from ._lib import Gemm, Seg, call
 
 BN_EPS = 1e-5
@@ -40,8 +39,8 @@ FUSED_L2 = True  # level 2 through the fused group_fused kernel (k = 32)
 FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
 # levels 2 / 3 on the channel-split kernel (group_split.hip) instead of the
 # accumulator-chained one (group_fused.hip); measured per level (tools/group_bench.py)
-SPLIT_L2 = os.environ.get("HREG_SPLIT_L2", "0") != "0"
-SPLIT_L3 = os.environ.get("HREG_SPLIT_L3", "1") != "0"
+SPLIT_L2 = switches.flag("SPLIT_L2", False)
+SPLIT_L3 = switches.flag("SPLIT_L3", True)
 # level 3 on the two-row-tile form of the channel-split kernel (hreg_group_split6j_l3)
 SPLIT_JT = True
 # 32-row tiles per workgroup of the channel-split FineReg / neighbour heads (0: the library's
@@ -49,52 +48,52 @@ SPLIT_JT = True
 HEAD_ROW_TILES = 0
 # the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
 # (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
-B6_L2 = os.environ.get("HREG_B6_L2", "1") != "0"
+B6_L2 = switches.flag("B6_L2", True)
 # level 2 on the pair form of the bf16x6 kernel (two groups per wave: half the weight
 # bytes streamed per row, hreg_group6x2_l2).  Off: at one wave per SIMD it measured level
 # with the one-group kernel (183 vs 184 us; tools/b6_experiment.py: 180 vs 182 us)
-PAIR_L2 = os.environ.get("HREG_PAIR_L2", "0") != "0"
+PAIR_L2 = switches.flag("PAIR_L2", False)
 # GraphPipeline: level-1 stage of all lanes as one batched launch per kernel (one side
 # stream) instead of one per lane
-BATCH_STAGE1 = os.environ.get("HREG_BATCH_STAGE1", "1") != "0"
-B6_L1 = os.environ.get("HREG_B6_L1", "1") != "0"  # group_l1_6.hip for level 1
+BATCH_STAGE1 = switches.flag("BATCH_STAGE1", True)
+B6_L1 = switches.flag("B6_L1", True)  # group_l1_6.hip for level 1
 # level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
 # (group_split6.hip)
-B6_L3 = os.environ.get("HREG_B6_L3", "1") != "0"
+B6_L3 = switches.flag("B6_L3", True)
 # the big plain GEMMs (CoarseReg convs_1 layers 2-3, 512 -> 512 over B*256*8 rows) on
 # hreg_gemm6 (bf16x6 products)
-B6_GEMM = os.environ.get("HREG_B6_GEMM", "1") != "0"
+B6_GEMM = switches.flag("B6_GEMM", True)
 # every addend-free GEMM (the precomputed first-layer blocks, the batched descriptor
 # products, the cosine similarities) on hreg_gemm6 (bf16x6, 128 x 128 tiles)
-B6_MLP = os.environ.get("HREG_B6_MLP", "1") != "0"  # mlp heads on hreg_mlp_head6
+B6_MLP = switches.flag("B6_MLP", True)  # mlp heads on hreg_mlp_head6
 # CoarseReg convs_1 (split first layer) + attention in one launch (coarse6.hip, bf16x6)
-FUSED_COARSE = os.environ.get("HREG_FUSED_COARSE", "1") != "0"
+FUSED_COARSE = switches.flag("FUSED_COARSE", True)
 # the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
 # precomputed-block form, HEAD_PRE)
-B6_HEADS = os.environ.get("HREG_B6_HEADS", "1") != "0"
+B6_HEADS = switches.flag("B6_HEADS", True)
 # the FineReg heads on coarse6.hip's channel-split correspondence kernel (hreg_corr_head6:
 # N1/64 waves of two output tiles, activations through LDS, ~136 VGPRs) instead of the
 # register-chained fine_head6_kernel (one wave per SIMD at N1 = 256)
 # level 1 with its weight table resident in LDS (hreg_group_l1_6) for clouds up to this many
 # points; above, the cluster FPS co-runs on every CU and the 92 KB LDS claim would wait for
 # it, so the global-table form (hreg_group_l1_6g) runs: Model_V2 942 vs 856 pairs/s
-L1_LDS_MAX_N = int(os.environ.get("HREG_L1_LDS_MAX_N", "16384"))
-SPLIT_FINE = os.environ.get("HREG_SPLIT_FINE", "1") != "0"
-SPLIT_NBR = os.environ.get("HREG_SPLIT_NBR", "1") != "0"  # the neighbour branch likewise
+L1_LDS_MAX_N = switches.integer("L1_LDS_MAX_N", 16384)
+SPLIT_FINE = switches.flag("SPLIT_FINE", True)
+SPLIT_NBR = switches.flag("SPLIT_NBR", True)  # the neighbour branch likewise
 FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
 FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
 FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip)
 # CoarseReg convs_1[0] as [small] GEMM + per-keypoint desc / knn_desc products added in the
 # epilogue (distributivity over the concatenation, layers.py:364-384; False: one 528-deep GEMM)
-COARSE_SPLIT = os.environ.get("HREG_COARSE_SPLIT", "1") != "0"
+COARSE_SPLIT = switches.flag("COARSE_SPLIT", True)
 # the same for the fused FineReg heads (descriptor blocks of convs_1[0]) and the CoarseReg
 # neighbour branch (descriptor block of convs_2[0]): per-point products precomputed, the
 # fused kernels multiply only the small / geometry columns per row
-HEAD_PRE = os.environ.get("HREG_HEAD_PRE", "1") != "0"
+HEAD_PRE = switches.flag("HEAD_PRE", True)
 # levels 2 / 3: the feature blocks of the detector's and the descriptor's first conv,
 # W_f f per level-(l-1) feature row, precomputed once (one GEMM) instead of once per
 # grouped row (k = 32 / 16 rows gather each feature row)
-LEVEL_PRE = os.environ.get("HREG_LEVEL_PRE", "1") != "0"
+LEVEL_PRE = switches.flag("LEVEL_PRE", True)
 
 
 @dataclass
@@ -239,17 +238,22 @@ class PreparedWeights:
         # Model_V2's FineReg2.mlpx (model_v2/layers.py:457-459), when the state dict has it
         self.mlpx = (_conv_bn(sd, "fine_corres_2.mlpx.0", "fine_corres_2.mlpx.1")
                      if "fine_corres_2.mlpx.0.weight" in sd else None)
-        self.l1_table = l1_table(self.det[0], self.desc[0], self.desc_mlp[0])
+        # the fp32-MFMA checker kernels' tables (libhregnet_checkers.so, test-only): built on
+        # first use by a debug switch / a test, never by the product path
+        det, desc, dmlp = list(self.det), list(self.desc), list(self.desc_mlp)  # (host copies)
+        self._lazy = {
+            "l1_table": lambda: l1_table(det[0], desc[0], dmlp[0]),
+            "l2_table": lambda: l2_table(det[1], desc[1], dmlp[1]),
+            "l3_table": lambda: l2_table(det[2], desc[2], dmlp[2]),
+            "l2s_table": lambda: split_table(det[1], desc[1], dmlp[1]),
+            "l3s_table": lambda: split_table(det[2], desc[2], dmlp[2]),
+        }
         self.l1_table6 = l1_table6(_fold_all(self.det[0]), _fold_all(self.desc[0]),
                                    _fold_all(self.desc_mlp[0]))
-        self.l2_table = l2_table(self.det[1], self.desc[1], self.desc_mlp[1])
-        self.l3_table = l2_table(self.det[2], self.desc[2], self.desc_mlp[2])
         self.l2_table6 = l2_table6(*(_fold_all(x) for x in (self.det[1], self.desc[1], self.desc_mlp[1])))
         self.l3_table6 = l2_table6(*(_fold_all(x) for x in (self.det[2], self.desc[2], self.desc_mlp[2])))
-        self.l2s_table = split_table(self.det[1], self.desc[1], self.desc_mlp[1])
         self.l2s_table6 = split_table6(*(_fold_all(x) for x in (self.det[1], self.desc[1], self.desc_mlp[1])))
         self.l3s_table6 = split_table6(*(_fold_all(x) for x in (self.det[2], self.desc[2], self.desc_mlp[2])))
-        self.l3s_table = split_table(self.det[2], self.desc[2], self.desc_mlp[2])
         self.fine_table = {name: fine_head_table(self.fine[name][0], C)
                            for name, C in (("fine_corres_2", 128), ("fine_corres_1", 64))}
         self.nbr_table = nbr_head_table(self.coarse_convs2, 256)
@@ -267,11 +271,20 @@ class PreparedWeights:
             [(n, self.fine[n][1]) for n in ("fine_corres_2", "fine_corres_1")])}
         for attr in ("det", "det_head", "desc", "desc_mlp", "coarse_convs1", "coarse_c1_small",
                      "coarse_c1_desc", "coarse_convs2", "nbr_pre", "fine_pre", "fine_pre6", "nbr_pre6", "level_pre", "level_pre6", "coarse_c1_desc6",
-                     "coarse_head", "fine", "l1_table", "l1_table6", "l2_table", "l3_table", "l2_table6",
-                     "l3_table6", "l2s_table", "l2s_table6", "l3s_table6",
-                     "l3s_table", "fine_table", "fine_table6", "nbr_table6", "coarse_table6",
+                     "coarse_head", "fine", "l1_table6", "l2_table6",
+                     "l3_table6", "l2s_table6", "l3s_table6",
+                     "fine_table", "fine_table6", "nbr_table6", "coarse_table6",
                      "nbr_table", "head_table", "head_table6", "mlpx"):
             setattr(self, attr, _to_device(getattr(self, attr), device))
+        self._device = device
+
+    def __getattr__(self, name):
+        lazy = self.__dict__.get("_lazy")
+        if lazy is None or name not in lazy:
+            raise AttributeError(name)
+        t = _to_device(lazy.pop(name)(), self.__dict__["_device"])
+        setattr(self, name, t)
+        return t
 
 
 # ---------------------------------------------------------- fused level 1
@@ -797,7 +810,7 @@ def knn_idx32(p1, p2, k):
 # ------------------------------------------------------------------ stages
 
 SPATIAL_KNN_MIN = 4096  # clouds at least this large group through the spatial index
-SPATIAL_KNN_MAX = int(os.environ.get("HREG_SPATIAL_KNN_MAX", "65536"))  # <= csrc/knn.hip SI_MAXN
+SPATIAL_KNN_MAX = switches.integer("SPATIAL_KNN_MAX", 65536)  # <= csrc/knn.hip SI_MAXN
 
 
 # Tests set this to a dict to receive every kNN selection of an eager forward as cloud-

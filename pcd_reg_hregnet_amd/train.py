@@ -20,12 +20,11 @@ arithmetic op runs in the HIP library, which must be present (no CPU fallback).
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 import torch.distributed as dist
 
-from . import _lib, engine
+from . import _lib, engine, switches
 
 BN_MOMENTUM = 0.1  # nn.BatchNorm default
 BN_EPS = 1e-5
@@ -35,8 +34,8 @@ BN_EPS = 1e-5
 # outputs stay on hreg_gemm's 256 x 32 / 256 x 64 tiles).  Off: the step gains 1-3 % (noise
 # level, tools/train_ab.sh) and the reference-gradient test's d/d dst_sigmas_3 error moves
 # to 1.16x its bar.
-TRAIN_B6 = os.environ.get("HREG_TRAIN_B6", "0") != "0"
-TRAIN_B6_MIN_N = int(os.environ.get("HREG_TRAIN_B6_MIN_N", "128"))
+TRAIN_B6 = switches.flag("TRAIN_B6", False)
+TRAIN_B6_MIN_N = switches.integer("TRAIN_B6_MIN_N", 128)
 
 
 def _stream():

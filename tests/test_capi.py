@@ -1,5 +1,7 @@
 """The C-ABI library: every symbol include/hregnet_amd.h declares is exported, and the
-ctypes signatures in pcd_reg_hregnet_amd/_lib.py agree with the header (no GPU needed)."""
+ctypes signatures in pcd_reg_hregnet_amd/_lib.py agree with the header (no GPU needed); the
+same for the test-only checker library (include/hregnet_amd_checkers.h ->
+libhregnet_checkers.so), whose symbols the product library must NOT carry."""
 import ctypes
 import os
 import re
@@ -8,10 +10,11 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "hregnet_amd.h")
+CHECKER_HEADER = os.path.join(REPO, "include", "hregnet_amd_checkers.h")
 
 
-def _declared():
-    text = open(HEADER).read()
+def _declared(header=HEADER):
+    text = open(header).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
     for m in re.finditer(r"(?:int|size_t|const char \*)\s*(hreg_\w+)\s*\(([^;]*?)\)\s*;", text, flags=re.S):
@@ -50,6 +53,20 @@ def test_ctypes_signatures_match_header(lib):
         assert len(args) == d[name], (name, len(args), d[name])
     for name in d:
         assert name in lib.EXPORTS, f"{name} declared but not bound in _lib"
+
+
+def test_checker_library_is_separate(lib):
+    """the fp32-MFMA twin kernels live only in the checker library, bound with the header's
+    arity; the product library exports none of them"""
+    d = _declared(CHECKER_HEADER)
+    assert set(d) == set(lib.CHECKER_EXPORTS), (sorted(d), lib.CHECKER_EXPORTS)
+    for name, args in lib._CHECKER_SIGS.items():
+        assert len(args) == d[name], name
+    C = ctypes.CDLL(lib.CHECKER_PATH)
+    P = ctypes.CDLL(lib.LIB_PATH)
+    for name in d:
+        assert hasattr(C, name), name
+        assert not hasattr(P, name), f"{name} is in the product library"
 
 
 def test_load_without_gpu_is_allowed_but_ops_fail_loudly(lib):

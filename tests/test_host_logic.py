@@ -146,7 +146,7 @@ def test_l1_fragment_tables_emulated():
 def test_l1_table_size_matches_kernel(P):
     _, prep = P
     from pcd_reg_hregnet_amd import _lib
-    L = _lib.load(require_gpu=False)
+    L = _lib.load_checkers(require_gpu=False)  # (test-only checker library)
     assert prep.l1_table.numel() == L.hreg_group_l1_table_floats()
 
 
@@ -195,14 +195,14 @@ def test_l2_input_fragments_emulated():
 def test_l2_table_size_matches_kernel(P):
     _, prep = P
     from pcd_reg_hregnet_amd import _lib
-    L = _lib.load(require_gpu=False)
+    L = _lib.load_checkers(require_gpu=False)  # (test-only checker library)
     assert prep.l2_table.numel() == L.hreg_group_l2_table_floats()
 
 
 def test_l3_table_size_matches_kernel(P):
     _, prep = P
     from pcd_reg_hregnet_amd import _lib
-    L = _lib.load(require_gpu=False)
+    L = _lib.load_checkers(require_gpu=False)  # (test-only checker library)
     assert prep.l3_table.numel() == L.hreg_group_l3_table_floats()
 
 
@@ -212,7 +212,7 @@ def test_split_tables_match_kernel(P):
     matrix-vector product) before the epilogues."""
     _, prep = P
     from pcd_reg_hregnet_amd import _lib
-    L = _lib.load(require_gpu=False)
+    L = _lib.load_checkers(require_gpu=False)  # (test-only checker library)
     assert prep.l2s_table.numel() == L.hreg_group_split_l2_table_floats()
     assert prep.l3s_table.numel() == L.hreg_group_split_l3_table_floats()
     for a, b, lvl in ((prep.l2_table, prep.l2s_table, 1), (prep.l3_table, prep.l3s_table, 2)):
