@@ -470,11 +470,12 @@ def bench_train(args, world, rank, device):
     s, d, Rg, tg = shard_batch(rank, B, args.points)
     src, dst = torch.from_numpy(s).to(device), torch.from_numpy(d).to(device)
     gR, gt = torch.from_numpy(Rg).to(device), torch.from_numpy(tg).to(device)
-    graphed = world == 1 and not args.train_eager
+    # the step replayed from captured HIP graphs (trainer.GraphTrainer; bitwise the eager
+    # step, tests/test_gpu_train_capture.py); with world > 1 the bucket all-reduce (RCCL) is
+    # captured inside the graph
+    graphed = not args.train_eager and (world == 1 or dist.get_backend() == "nccl")
     eager_tr = tr
     if graphed:
-        # the step replayed from captured HIP graphs (trainer.GraphTrainer; bitwise the eager
-        # step, tests/test_gpu_train_capture.py); DDP (world > 1) stays eager
         gtr = trainer.GraphTrainer(tr, B, args.points)
         gtr.capture(src, dst, gR, gt)
         tr = gtr

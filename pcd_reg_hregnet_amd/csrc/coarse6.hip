@@ -88,7 +88,7 @@ __global__ __launch_bounds__(K::CW * 64) void coarse_head6_kernel(
 #pragma unroll
         for (int i = 0; i < P; ++i) ld6(wt, g1.base + i, lane, carry[i]);
     }
-    for (int tw = xcd_block(blockIdx.x, gridDim.x); tw < NW; tw += gridDim.x) {
+    for (int tw = blockIdx.x; tw < NW; tw += gridDim.x) {
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);

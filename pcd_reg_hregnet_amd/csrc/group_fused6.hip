@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256, RING ? ring_wps<K>() : K::WPS) void group_fuse
     // RING: every wave of the workgroup runs the same tiles count (a tile past the end
     // recomputes the last one: identical values, identical stores)
     const int tstride = gridDim.x * WAVES;
-    for (int t0 = xcd_block(blockIdx.x, gridDim.x) * WAVES + (RING ? 0 : w); t0 < NT; t0 += tstride) {
+    for (int t0 = blockIdx.x * WAVES + (RING ? 0 : w); t0 < NT; t0 += tstride) {
         const int t = RING ? min(t0 + w, NT - 1) : t0;
         const int g = t * GPT + (KN == 32 ? 0 : j >> 4);  // this lane's group
         // opaque per-tile table pointer: keeps the loop-invariant weight loads in the loop
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256, 1) void group_pair6_kernel(
 #pragma unroll
         for (int co = 0; co < T1; ++co) ld6(wt, det_g.base + co, lane, carry[co]);
     }
-    for (int pp = xcd_block(blockIdx.x, gridDim.x) * WAVES + w; pp < NP; pp += gridDim.x * WAVES) {
+    for (int pp = blockIdx.x * WAVES + w; pp < NP; pp += gridDim.x * WAVES) {
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);

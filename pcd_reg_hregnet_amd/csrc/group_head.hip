@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256, K::WPS) void fine_head_kernel(
                 for (int i = 0; i < GS0; ++i) carry[(s0 + i) * T1 + co] = v[i];
             }
     }
-    for (int t = xcd_block(blockIdx.x, gridDim.x) * WAVES + w; t < NT; t += gridDim.x * WAVES) {
+    for (int t = blockIdx.x * WAVES + w; t < NT; t += gridDim.x * WAVES) {
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head_kernel(
                 for (int i = 0; i < GS0; ++i) carry[(s0 + i) * T1 + co] = v[i];
             }
     }
-    for (int t = xcd_block(blockIdx.x, gridDim.x) * WAVES + w; t < NT; t += gridDim.x * WAVES) {
+    for (int t = blockIdx.x * WAVES + w; t < NT; t += gridDim.x * WAVES) {
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gfloat *tb = reinterpret_cast<const gfloat *>(tba);
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256, K::WPS) void fine_head6_kernel(
 #pragma unroll
         for (int co = 0; co < T1; ++co) ld6(wt, K::G_S + co, lane, carry[co]);
     }
-    for (int t = xcd_block(blockIdx.x, gridDim.x) * WAVES + w; t < NT; t += gridDim.x * WAVES) {
+    for (int t = blockIdx.x * WAVES + w; t < NT; t += gridDim.x * WAVES) {
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(256, K::WPS) void nbr_head6_kernel(
 #pragma unroll
         for (int co = 0; co < T1; ++co) ld6(wt, K::G_S + co, lane, carry[co]);
     }
-    for (int t = xcd_block(blockIdx.x, gridDim.x) * WAVES + w; t < NT; t += gridDim.x * WAVES) {
+    for (int t = blockIdx.x * WAVES + w; t < NT; t += gridDim.x * WAVES) {
         uint64_t tba = reinterpret_cast<uint64_t>(table);
         asm volatile("" : "+s"(tba));
         const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);

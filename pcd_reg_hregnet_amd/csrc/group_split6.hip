@@ -184,7 +184,7 @@ __global__ __launch_bounds__(RING ? RING_RT * 256 : 256, RING ? 1 : ONE ? 3 : 2)
 #pragma unroll
         for (int i = 0; i < K::P1; ++i) ld6(wt, det_g.base + i * det_g.stride, lane, carry[i]);
     }
-    for (int base = xcd_block(blockIdx.x, gridDim.x) * RT; base < NT; base += gridDim.x * RT) {
+    for (int base = blockIdx.x * RT; base < NT; base += gridDim.x * RT) {
         // every wave of the workgroup runs the same trip count (barriers): a row tile
         // past the end recomputes the last tile (identical values, identical stores)
         const int t = min(base + rt, NT - 1);
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256, 2) void group_split6j_kernel(
 #pragma unroll
         for (int i = 0; i < K::P1; ++i) ld6(wt, det_g.base + i * det_g.stride, lane, carry[i]);
     }
-    for (int pb = xcd_block(blockIdx.x, gridDim.x); pb < NPAIR; pb += gridDim.x) {
+    for (int pb = blockIdx.x; pb < NPAIR; pb += gridDim.x) {
         // a tile past the end recomputes the last tile (identical values, identical stores)
         int t[SJT], g[SJT];
         size_t row[SJT];

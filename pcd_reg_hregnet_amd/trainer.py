@@ -150,6 +150,14 @@ class Level1Prefetch:
         return prepared
 
 
+def ddp_average(bucket: GradBucket, group=None) -> None:
+    """DistributedDataParallel's gradient averaging for one step: ONE all_reduce (SUM) of the
+    whole flat bucket (every parameter's gradient in FlatParams order), then / world -- a no-op
+    in a single process.  Trainer.step and the captured GraphTrainer step both call exactly
+    this (tests/test_distributed.py counts the collectives)."""
+    bucket.all_reduce_mean(group)
+
+
 class Trainer:
     """``step(src, dst, gt_R, gt_t)`` = one train_reg_v0 iteration on this rank's shard.
     ``next_batch=(src, dst)`` starts the next batch's level-1 grouping on a side stream."""
@@ -176,7 +184,7 @@ class Trainer:
             self.prefetch.start(*next_batch)
         hook = train_graph.IndexHook(prepared=prepared) if prepared else None
         out = self.local_gradients(src, dst, gt_R, gt_t, hook)
-        self.bucket.all_reduce_mean(self.group)  # DDP gradient averaging, one collective
+        ddp_average(self.bucket, self.group)
         self.opt.step()
         return out
 
@@ -219,14 +227,20 @@ class GraphTrainer:
     in before the replay) -- Level1Prefetch's overlap, captured.  Adam reads its step's bias
     corrections from device memory (hreg_adam_step_dev), written before each replay, so lr
     changes (``set_lr``) need no recapture.  Everything else a step does -- BN running stats,
-    num_batches_tracked, the gradient bucket -- is device work in the graph.  Single process
-    (the DDP all-reduce stays on the eager Trainer).  Capture runs two warm-up steps first; the
+    num_batches_tracked, the gradient bucket -- is device work in the graph; with world > 1
+    (RCCL) the bucket's one all-reduce is captured too (a graph node between the backward and
+    Adam: ``ddp_average``, the same call the eager Trainer makes; the two eager warm-up steps
+    before the capture initialise the communicator).  Capture runs two warm-up steps first; the
     parameters, optimizer moments and BN buffers are restored afterwards, so the first
     ``step`` continues from the state the Trainer had."""
 
     def __init__(self, trainer: "Trainer", batch: int, points: int):
-        if _dist_world(trainer.group) > 1:
-            raise NotImplementedError("GraphTrainer: single process (use Trainer with DDP)")
+        self.world = _dist_world(trainer.group)
+        if self.world > 1 and dist.get_backend(trainer.group) != "nccl":
+            # RCCL collectives are captured into the graph (the bucket all-reduce is a graph
+            # node on the step's stream); gloo's host-side collectives cannot be
+            raise NotImplementedError("GraphTrainer with world > 1 needs the nccl (RCCL) backend; "
+                                      "with gloo use Trainer")
         if not trainer.net.feature_extraction.use_fps:
             # use_fps=False (layers.py:144-147) draws torch.randperm samples on the host per
             # step; a captured graph would freeze one draw and replay it forever
@@ -296,6 +310,7 @@ class GraphTrainer:
         if two:
             train_graph.join_side_stream(self.src[k].device)
         tr.bucket.collect(two_sides=two)
+        ddp_average(tr.bucket, tr.group)  # world > 1: the RCCL all-reduce, captured
         opt = tr.opt
         _lib.call("hreg_adam_step_dev", opt.p, opt.g, opt.m, opt.v, opt.p.numel(), float(opt.lr),
                   float(opt.betas[0]), float(opt.betas[1]), float(opt.eps), self.scal,

@@ -106,7 +106,21 @@ def _bucket_worker(rank, world, port, q):
     params[0].grad.add_(float(rank + 1))
     params[1].grad = torch.full((7,), 10.0 * (rank + 1))
     b.collect()
-    b.all_reduce_mean()
+    # the trainer's collective (trainer.ddp_average, eager and captured steps alike): exactly
+    # one all_reduce per step, over the whole flat bucket (every gradient in parameter order)
+    from pcd_reg_hregnet_amd import trainer as T
+    calls = []
+    orig = dist.all_reduce
+
+    def counting(t, *a, **k):
+        calls.append((t.data_ptr(), t.numel()))
+        return orig(t, *a, **k)
+    dist.all_reduce = counting
+    try:
+        T.ddp_average(b)
+    finally:
+        dist.all_reduce = orig
+    one_collective = calls == [(b.flat.data_ptr(), b.flat.numel())]
     # the trainer's flat parameters: rank 0's values everywhere after the broadcast
     from pcd_reg_hregnet_amd.trainer import FlatParams
     mine = [torch.nn.Parameter(torch.full((5, 3), float(rank))),
@@ -120,7 +134,7 @@ def _bucket_worker(rank, world, port, q):
     # that the receiver can only open while this process is still alive
     q.put((rank, params[0].grad.numpy().copy(), params[1].grad.numpy().copy(), b.flat.numel(),
            params[0].grad.data_ptr() == b.flat.data_ptr() and
-           params[1].grad.data_ptr() == b.flat.data_ptr() + 64 * 4, synced))
+           params[1].grad.data_ptr() == b.flat.data_ptr() + 64 * 4, synced, one_collective))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -139,8 +153,22 @@ def test_gloo_grad_bucket_all_reduce():
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for _, g0, g1, n, view, synced in res:
+    for _, g0, g1, n, view, synced, one_collective in res:
         assert n == 128 and view  # 5x3 + 7 trainable floats, each padded to 64 (256 B)
-        assert synced
+        assert synced and one_collective
         assert torch.equal(torch.from_numpy(g0), torch.full((5, 3), 1.5))   # mean of 1 and 2
         assert torch.equal(torch.from_numpy(g1), torch.full((7,), 15.0))    # mean of 10 and 20
+
+
+def test_train_steps_issue_one_collective():
+    """Trainer.step (eager) and GraphTrainer's captured body reduce gradients through the same
+    single call, trainer.ddp_average, once per step and after the backward's bucket collect
+    (the captured DDP step keeps the bucket order and one collective)."""
+    import inspect
+    from pcd_reg_hregnet_amd import trainer as T
+    for fn in (T.Trainer.step, T.GraphTrainer._body):
+        src = inspect.getsource(fn)
+        assert src.count("ddp_average(") == 1, fn
+        assert "all_reduce" not in src.replace("ddp_average", ""), fn
+    body = inspect.getsource(T.GraphTrainer._body)
+    assert body.index("collect(") < body.index("ddp_average(") < body.index("hreg_adam_step_dev")

@@ -32,6 +32,13 @@ from test_gpu_train_graph import FLIP_BAR, _train_net
 pytestmark = pytest.mark.gpu
 
 FIXTURE = "ddp_step_r2_b8_n2048.npz"
+# The registration heads' convs_1 stacks (CoarseReg layers.py:364-396, FineReg :433-451) feed
+# the attention's max over channels (layers.py:151's pattern): a row whose top-2 channels lie
+# within fp32 rounding routes its whole gradient to the other channel, which moves the last BN's
+# bias / weight gradients by that row's share.  Measured on this fixture: rank 1's
+# coarse_corres.convs_1.7.bias at 1.8e-3 of its max (the fp32 reference 2.1e-4), every other
+# convs_1 parameter within 1e-3.  The mlp heads after the attention stay at 1e-3.
+ATT_BAR = 5e-3
 
 
 def _grad_rows(fx, grads, prefix, ref64, label):
@@ -53,7 +60,12 @@ def _grad_rows(fx, grads, prefix, ref64, label):
         hs = max(np.abs(h64).max(), 1e-30)
         ours = max(abs(np.linalg.norm(g) - n64) / n64, np.abs(g[:h64.size] - h64).max() / hs)
         ref = max(abs(n32 - n64) / n64, np.abs(h32 - h64).max() / hs)
-        floor = FLIP_BAR if (name.startswith("feature_extraction.") or ".convs_2." in name) else 1e-3
+        if name.startswith("feature_extraction.") or ".convs_2." in name:
+            floor = FLIP_BAR
+        elif ".convs_1." in name:
+            floor = ATT_BAR
+        else:
+            floor = 1e-3
         rows.append((ours / max(4 * ref, floor), ours, ref, name))
         bars[name] = max(4 * ref, floor) * hs  # the absolute error the entries are held to
     return rows, noise, bars
