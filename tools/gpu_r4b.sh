@@ -6,6 +6,7 @@ export TMPDIR=/tmp
 bash tools/pmc_r4.sh r4b/pmc || exit 1
 timeout -k 10 300 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -k ddp > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 200 python tools/replay_cost.py 20 48 > $O/replay.txt 2>&1 || { tail $O/replay.txt; exit 1; }; cat $O/replay.txt
 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/b20.json 2> $O/b20.err || { tail $O/b20.err; exit 1; }
 timeout -k 10 200 python bench.py --no-cpu-baseline > $O/b48.json 2> $O/b48.err || { tail $O/b48.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/trace.log 2>&1 || { tail $O/trace.log; exit 1; }
