@@ -239,8 +239,15 @@ class MfmaTimer:
                 fl, nb, xf = work(args)
                 return self._timed(kind, lambda: orig_call(name, *args), fl, nb, xf, entry=name)
             return orig_call(name, *args)
+        orig_grouped = _lib.gemm_grouped
+
+        def gemm_grouped(gs):
+            fl = sum(2.0 * g.R * g.N * g.K * g.batch for g in gs)
+            nb = sum(4.0 * g.batch * (g.R * g.K + g.N * g.K + g.R * g.N) for g in gs)
+            return self._timed("gemm", lambda: orig_grouped(gs), fl, nb, entry="hreg_gemm_grouped")
         _lib.gemm = gemm_of(orig_gemm, "hreg_gemm")
         _lib.gemm6 = gemm_of(orig_gemm6, "hreg_gemm6")
+        _lib.gemm_grouped = gemm_grouped
         engine.call = call
 
     def result(self, kind):

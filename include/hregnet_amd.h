@@ -163,6 +163,14 @@ typedef struct {
 
 int hreg_gemm(const hreg_gemm_t *g, void *stream);
 
+/* n <= HREG_GEMM_GROUP_MAX independent hreg_gemm problems (no addends) in ONE launch: the
+ * grid runs every problem's 64 x 64 tiles; each output has the bits its own hreg_gemm launch
+ * gives (the per-output accumulation order does not depend on the tile shape).  For the
+ * per-row products the registration heads precompute from the feature-extraction outputs
+ * (engine.head_products). */
+#define HREG_GEMM_GROUP_MAX 6
+int hreg_gemm_grouped(const hreg_gemm_t *gs, int n, void *stream);
+
 /* hreg_gemm with fp32-accurate products on the bf16 matrix cores (bf16x6: A and W split
  * exactly into three bf16 pieces while staged into LDS, 6 v_mfma_f32_32x32x16_bf16 per
  * 16-deep k sub-chunk; gemm.hip gemm6_kernel).  Same arguments; addends (nadd > 0) are

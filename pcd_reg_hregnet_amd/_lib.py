@@ -64,6 +64,7 @@ _SIGS = {
     "hreg_knn_group_indexed": [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "hreg_gemm": [ctypes.POINTER(Gemm), _vp],
     "hreg_gemm6": [ctypes.POINTER(Gemm), _vp],
+    "hreg_gemm_grouped": [ctypes.POINTER(Gemm), _i, _vp],
     "hreg_attend": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp],
     "hreg_group_max": [_vp, _i, _i, _i, _i, _vp, _i, _vp],
     "hreg_head_out": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp],
@@ -290,6 +291,15 @@ def gemm(g: Gemm) -> None:
     rc = L.hreg_gemm(ctypes.byref(g), stream_handle())
     if rc != HREG_OK:
         raise RuntimeError(f"hreg_gemm failed: {_ERRORS.get(rc, rc)} (code {rc})")
+
+
+def gemm_grouped(gs) -> None:
+    """hreg_gemm_grouped: independent GEMMs (a list of Gemm, no addends) in one launch."""
+    L = load()
+    arr = (Gemm * len(gs))(*gs)
+    rc = L.hreg_gemm_grouped(arr, len(gs), stream_handle())
+    if rc != HREG_OK:
+        raise RuntimeError(f"hreg_gemm_grouped failed: {_ERRORS.get(rc, rc)} (code {rc})")
 
 
 def gemm6(g: Gemm) -> None:

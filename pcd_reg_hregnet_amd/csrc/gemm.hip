@@ -53,8 +53,10 @@ __device__ __forceinline__ float4 load_w4(const hreg_gemm_t &g, int b, int n, in
 }
 
 
+// one BM x BN output tile (r0, n0) of batch b (the body of gemm_nt_kernel and
+// gemm_grouped_kernel)
 template <int BM, int BN, int WM, int WN, int BK, bool ADD = false>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
+__device__ __forceinline__ void gemm_nt_tile(const hreg_gemm_t &g, const int b, const int r0, const int n0) {
     static_assert(WM * WN == 4, "4 waves");
     static_assert(BK == 16 || BK == 32, "BK");
     constexpr int LDS_STRIDE = BK + 4;          // pad: 16-row ds_read_b128 groups hit distinct slots
@@ -71,9 +73,6 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wr = wave / WN, wc = wave % WN;
-    const int b = blockIdx.z;
-    const int r0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
     const int nchunks = (g.K + BK - 1) / BK;
 
     f32x16 acc[TM][TN];
@@ -206,6 +205,34 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
             }
         }
     }
+}
+
+template <int BM, int BN, int WM, int WN, int BK, bool ADD = false>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(const hreg_gemm_t g) {
+    gemm_nt_tile<BM, BN, WM, WN, BK, ADD>(g, blockIdx.z, blockIdx.x * BM, blockIdx.y * BN);
+}
+
+// Several independent GEMMs in one launch (hreg_gemm_grouped): a flat grid over every
+// problem's 64 x 64 tiles, problem p owning blocks [start[p], start[p + 1]).  Each tile runs
+// gemm_nt_kernel's body, so every output has the same bits as its own hreg_gemm launch (the
+// accumulation order does not depend on the tile shape).
+struct GemmGroup {
+    hreg_gemm_t g[HREG_GEMM_GROUP_MAX];
+    int start[HREG_GEMM_GROUP_MAX + 1];
+    int tm[HREG_GEMM_GROUP_MAX];
+    int tn[HREG_GEMM_GROUP_MAX];
+    int n;
+};
+
+__global__ __launch_bounds__(256) void gemm_grouped_kernel(const GemmGroup gg) {
+    const int bid = blockIdx.x;
+    int p = 0;
+    while (p + 1 < gg.n && bid >= gg.start[p + 1]) ++p;
+    const int local = bid - gg.start[p];
+    const int per_b = gg.tm[p] * gg.tn[p];
+    const int b = local / per_b, rem = local - b * per_b;
+    const int bx = rem % gg.tm[p], by = rem / gg.tm[p];
+    gemm_nt_tile<64, 64, 2, 2, 32>(gg.g[p], b, bx * 64, by * 64);
 }
 
 // ------------------------------------------------------------------------
@@ -442,3 +469,26 @@ extern "C" int hreg_gemm(const hreg_gemm_t *gp, void *stream) {
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
+
+extern "C" int hreg_gemm_grouped(const hreg_gemm_t *gs, int n, void *stream) {
+    if (!gs || n < 1 || n > HREG_GEMM_GROUP_MAX) return HREG_ERR_INVALID;
+    GemmGroup gg;
+    int total = 0;
+    for (int p = 0; p < n; ++p) {
+        const hreg_gemm_t &g = gs[p];
+        if (const int rc = gemm_check(g)) return rc;
+        if (g.nadd) return HREG_ERR_UNSUPPORTED;  // addends: hreg_gemm
+        gg.g[p] = g;
+        gg.tm[p] = (g.R + 63) / 64;
+        gg.tn[p] = (g.N + 63) / 64;
+        gg.start[p] = total;
+        total += gg.tm[p] * gg.tn[p] * g.batch;
+    }
+    gg.start[n] = total;
+    gg.n = n;
+    if (total == 0) return HREG_OK;
+    hipLaunchKernelGGL(gemm_grouped_kernel, dim3(total), dim3(256), 0, as_stream(stream), gg);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+

@@ -597,6 +597,16 @@ def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=(), b6=Fa
     b6: on hreg_gemm6 (bf16x6 products) when B6_GEMM (no addends)."""
     if out is None:
         out = torch.empty((R, lin.N), device=lin.W.device, dtype=torch.float32)
+    g = _gemm_struct(segs, lin, R, out, adds)
+    if b6 and B6_GEMM and not adds:
+        _lib.gemm6(g)
+    else:
+        _lib.gemm(g)
+    return out
+
+
+def _gemm_struct(segs, lin: Lin, R: int, out: torch.Tensor, adds=()) -> Gemm:
+    """the hreg_gemm_t of gemm() (not launched)"""
     g = Gemm()
     for i, s in enumerate(segs):
         g.seg[i] = s
@@ -616,22 +626,24 @@ def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=(), b6=Fa
     g.out = out.data_ptr()
     g.ldo = out.shape[-1]
     g.out_batch_stride = 0
-    if b6 and B6_GEMM and not adds:
-        _lib.gemm6(g)
-    else:
-        _lib.gemm(g)
-    return out
+    return g
 
 
 def _gemm_batched_desc(lin: Lin, desc3, rows: int, C: int, out, x1=None):
     """out[i] = x_i @ lin.W[i]^T for i in {0, 1}, x_0 = desc3[:rows], x_1 = desc3[rows:2 rows]
     (or x1 when given and not contiguous after x_0: then two launches); one launch with
     grid.z = 2 otherwise; lin.W [2][N][C], identity epilogue."""
-    N = lin.W.shape[1]
     if x1 is not None and x1.data_ptr() != desc3.data_ptr() + rows * C * 4:
         for i, x in enumerate((desc3, x1)):
             gemm([_seg(x, 0, C, ld=C)], Lin(lin.W[i], lin.alpha, lin.beta, False), rows, out=out[i])
         return out
+    _lib.gemm(_batched_desc_struct(lin, desc3, rows, C, out))
+    return out
+
+
+def _batched_desc_struct(lin: Lin, desc3, rows: int, C: int, out) -> Gemm:
+    """the batch-2 hreg_gemm_t of _gemm_batched_desc (x_1 contiguous after x_0; not launched)"""
+    N = lin.W.shape[1]
     g = Gemm()
     g.seg[0] = _seg(desc3, 0, C, ld=C, batch_stride=rows * C)
     g.nseg = 1
@@ -647,12 +659,16 @@ def _gemm_batched_desc(lin: Lin, desc3, rows: int, C: int, out, x1=None):
     g.out = out.data_ptr()
     g.ldo = N
     g.out_batch_stride = rows * N
-    _lib.gemm(g)
-    return out
+    return g
 
 
 def cosine_gemm(a, b, na, nb_, nb: int, n1: int, n2: int, C: int, out):
     """S[b][i][j] = <a_i, b_j> / (|a_i||b_j| + 1e-6) per pair (layers.py:29-41)."""
+    _lib.gemm(_cosine_struct(a, b, na, nb_, nb, n1, n2, C, out))
+    return out
+
+
+def _cosine_struct(a, b, na, nb_, nb: int, n1: int, n2: int, C: int, out) -> Gemm:
     g = Gemm()
     g.seg[0] = _seg(a, 0, C, ld=C, batch_stride=n1 * C)
     g.nseg = 1
@@ -670,8 +686,7 @@ def cosine_gemm(a, b, na, nb_, nb: int, n1: int, n2: int, C: int, out):
     g.out = out.data_ptr()
     g.ldo = n2
     g.out_batch_stride = n1 * n2
-    _lib.gemm(g)
-    return out
+    return g
 
 
 def _stream():
@@ -1040,8 +1055,47 @@ def _mlp_weights(P: PreparedWeights, key, x, nclouds, rows):
     return w
 
 
-def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
-    """CoarseReg.forward (layers.py:273-396); xyz3 [2B,256,3], desc3 [2B*256,256], sig3 [2B*256]."""
+# The registration heads' products of the feature-extraction outputs -- CoarseReg's neighbour
+# branch block (W_desc desc3), its convs_1 desc / knn_desc blocks, the original cosine
+# similarity, and both FineReg heads' descriptor blocks -- depend on nothing but desc_1..3, so
+# they run as ONE grouped launch right after the feature extraction (hreg_gemm_grouped: the
+# same bits as five separate hreg_gemm launches, one launch instead of five small ones)
+GROUPED_HEAD_GEMMS = switches.flag("GROUPED_HEAD_GEMMS", True)
+
+
+def _grouped_heads_ok(C3: int) -> bool:
+    return (GROUPED_HEAD_GEMMS and FUSED_NBR and HEAD_PRE and B6_HEADS and COARSE_SPLIT and
+            FUSED_COARSE and FUSED_FINE and C3 == 256)
+
+
+def head_products(P: PreparedWeights, B: int, desc):
+    """desc = [desc_1, desc_2, desc_3] (each [2B*M][C], src rows then dst rows) -> the products
+    coarse_reg / fine_reg would compute (see GROUPED_HEAD_GEMMS), from one launch."""
+    d3 = desc[2]
+    dev = d3.device
+    C = d3.shape[1]
+    N1 = d3.shape[0] // (2 * B)
+    norms = row_norms(d3)
+    nbr_pre = _empty(2 * B * N1, P.nbr_pre6.N, device=dev)
+    ud = _empty(2, B * N1, P.coarse_c1_desc6.W.shape[1], device=dev)
+    S = _empty(B, N1, N1, device=dev)
+    gs = [_gemm_struct([_seg(d3, 0, C)], P.nbr_pre6, 2 * B * N1, nbr_pre),
+          _batched_desc_struct(P.coarse_c1_desc6, d3, B * N1, C, ud),
+          _cosine_struct(d3[:B * N1], d3[B * N1:], norms[:B * N1], norms[B * N1:], B, N1, N1, C, S)]
+    fine = {}
+    for name, lv in (("fine_corres_2", 1), ("fine_corres_1", 0)):
+        dl = desc[lv]
+        M, Cl = dl.shape[0] // (2 * B), dl.shape[1]
+        pre = _empty(2, B * M, P.fine[name][0][0].W.shape[0], device=dev)
+        gs.append(_batched_desc_struct(P.fine_pre6[name], dl, B * M, Cl, pre))
+        fine[name] = pre
+    _lib.gemm_grouped(gs)
+    return {"nbr_pre": nbr_pre, "ud": ud, "S": S, "fine_pre": fine}
+
+
+def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3, prod=None):
+    """CoarseReg.forward (layers.py:273-396); xyz3 [2B,256,3], desc3 [2B*256,256], sig3 [2B*256].
+    prod: head_products' precomputed blocks and original similarity (else computed here)."""
     dev = xyz3.device
     k = K_HEAD
     N1 = xyz3.shape[1]
@@ -1053,9 +1107,12 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     kidx = knn_idx32(s_desc.view(B, N1, C), d_desc.view(B, N1, C), k)
     _record_knn("coarse_desc_knn", kidx, B, N1, k, False)
     # original similarity (layers.py:290-313)
-    norms = row_norms(desc3)
-    S = _empty(B, N1, N1, device=dev)
-    cosine_gemm(s_desc, d_desc, norms[:B * N1], norms[B * N1:], B, N1, N1, C, S)
+    if prod is not None:
+        S = prod["S"]
+    else:
+        norms = row_norms(desc3)
+        S = _empty(B, N1, N1, device=dev)
+        cosine_gemm(s_desc, d_desc, norms[:B * N1], norms[B * N1:], B, N1, N1, C, S)
     sims_a = _empty(B * N1 * k, 2, device=dev)
     maxes = _empty(B, 2 * N1, device=dev)
     call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_a, 2, _stream())
@@ -1067,7 +1124,10 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
     if FUSED_NBR and C == 256:
         nbr = _empty(G2, C, device=dev)
         b6 = B6_HEADS and HEAD_PRE
-        pre = gemm([_seg(desc3, 0, C)], P.nbr_pre6 if b6 else P.nbr_pre, G2) if HEAD_PRE else None
+        if prod is not None:
+            pre = prod["nbr_pre"]
+        else:
+            pre = gemm([_seg(desc3, 0, C)], P.nbr_pre6 if b6 else P.nbr_pre, G2) if HEAD_PRE else None
         if b6:
             if SPLIT_NBR:
                 call("hreg_nbr_head6sx", P.nbr_table6, desc3, gself, geom_self, G2, nbr, pre, HEAD_ROW_TILES,
@@ -1099,9 +1159,12 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
         # keypoint, so both are multiplied once per keypoint (one batch-2 GEMM over
         # desc3 = [src; dst]) and added in the layer's epilogue: 8.86 -> 1.34 GFLOP
         # per step at B=8 for this layer
-        ud = _empty(2, B * N1, P.coarse_c1_desc.W.shape[1], device=dev)
         fused = FUSED_COARSE and C == 256
-        _gemm_batched_desc(P.coarse_c1_desc6 if fused else P.coarse_c1_desc, desc3, B * N1, C, ud)
+        if prod is not None:
+            ud = prod["ud"]
+        else:
+            ud = _empty(2, B * N1, P.coarse_c1_desc.W.shape[1], device=dev)
+            _gemm_batched_desc(P.coarse_c1_desc6 if fused else P.coarse_c1_desc, desc3, B * N1, C, ud)
         if fused:
             # convs_1 + attention in one launch (coarse6.hip)
             corres = _empty(B * N1, 3, device=dev)
@@ -1124,8 +1187,9 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3):
 
 
 def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w,
-             return_att=False):
-    """FineReg.forward (layers.py:433-454); xyz [B,N,3], desc [B*N,C], w [B*N]."""
+             return_att=False, pre=None):
+    """FineReg.forward (layers.py:433-454); xyz [B,N,3], desc [B*N,C], w [B*N].
+    pre: the descriptor blocks head_products made (else computed here)."""
     dev = src_xyz.device
     k = K_HEAD
     N = src_xyz.shape[1]
@@ -1143,11 +1207,12 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
         N1 = convs[0].W.shape[0]
         corres = _empty(B * N, 3, device=dev)
         att = _empty(B * N, N1, device=dev)
-        pre = [None, None]
-        if HEAD_PRE:
-            pre = _empty(2, B * N, N1, device=dev)
-            _gemm_batched_desc((P.fine_pre6 if B6_HEADS else P.fine_pre)[name], src_desc, B * N, C,
-                               pre, x1=dst_desc)
+        if pre is None:
+            pre = [None, None]
+            if HEAD_PRE:
+                pre = _empty(2, B * N, N1, device=dev)
+                _gemm_batched_desc((P.fine_pre6 if B6_HEADS else P.fine_pre)[name], src_desc, B * N, C,
+                                   pre, x1=dst_desc)
         if B6_HEADS and HEAD_PRE and SPLIT_FINE:
             call("hreg_corr_head6x", P.fine_table6[name], N1, small, pre[0], pre[1], gidx, kx, B * N,
                  corres, att, HEAD_ROW_TILES, _stream())
@@ -1227,7 +1292,9 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts
     xyz = [fe[f"xyz_{i + 1}"] for i in range(3)]
     sig = [fe[f"sigmas_{i + 1}"] for i in range(3)]
     desc = [fe[f"desc_{i + 1}"] for i in range(3)]
-    c3, w3 = coarse_reg(P, B, xyz[2], desc[2], sig[2])
+    prod = head_products(P, B, desc) if _grouped_heads_ok(desc[2].shape[1]) else None
+    fpre = (lambda name: None) if prod is None else (lambda name: prod["fine_pre"][name])
+    c3, w3 = coarse_reg(P, B, xyz[2], desc[2], sig[2], prod)
     _, _, R3, t3 = weighted_svd(xyz[2][:B], c3, w3)
     x2t = transform(xyz[1][:B], R3, t3)
     sd2, dd2 = split(desc[1], M[1])
@@ -1236,15 +1303,17 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts
         if P.mlpx is None:
             raise RuntimeError("Model_V2 forward: the state dict has no fine_corres_2.mlpx")
         c2, w2, att2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2,
-                                return_att=True)
+                                return_att=True, pre=fpre("fine_corres_2"))
         f2 = gemm([_seg(att2, 0, att2.shape[1])], P.mlpx, B * M[1])
     else:
-        c2, w2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2)
+        c2, w2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2,
+                          pre=fpre("fine_corres_2"))
     _, _, R2, t2 = weighted_svd(x2t, c2, w2, prev=(R3, t3))
     x1t = transform(xyz[0][:B], R2, t2)
     sd1, dd1 = split(desc[0], M[0])
     ss1, ds1 = split(sig[0], M[0])
-    c1, w1 = fine_reg(P, "fine_corres_1", B, x1t, sd1, xyz[0][B:], dd1, ss1, ds1)
+    c1, w1 = fine_reg(P, "fine_corres_1", B, x1t, sd1, xyz[0][B:], dd1, ss1, ds1,
+                      pre=fpre("fine_corres_1"))
     _, _, R1, t1 = weighted_svd(x1t, c1, w1, prev=(R2, t2))
 
     def feats(part):

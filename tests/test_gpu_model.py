@@ -773,3 +773,25 @@ def test_heads_two_tile_bitwise(net):
     for i in range(3):
         assert torch.equal(a["rotation"][i], b["rotation"][i])
         assert torch.equal(a["translation"][i], b["translation"][i])
+
+
+def test_grouped_head_gemms_bitwise(net):
+    """engine.GROUPED_HEAD_GEMMS: the heads' precomputed blocks and the original cosine
+    similarity from one hreg_gemm_grouped launch give the same bits as their five separate
+    hreg_gemm launches (every output of the forward)."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    s, d, _, _ = synthetic.lidar_batch(3, 4096, seed0=77)
+    old = engine.GROUPED_HEAD_GEMMS
+    try:
+        engine.GROUPED_HEAD_GEMMS = True
+        a = _run(net, s, d)
+        engine.GROUPED_HEAD_GEMMS = False
+        b = _run(net, s, d)
+    finally:
+        engine.GROUPED_HEAD_GEMMS = old
+    for key in ("src_xyz_corres_3", "src_xyz_corres_2", "src_xyz_corres_1", "src_dst_weights_3",
+                "src_dst_weights_2", "src_dst_weights_1"):
+        np.testing.assert_array_equal(a[key], b[key], key)
+    for i in range(3):
+        np.testing.assert_array_equal(a["rotation"][i], b["rotation"][i])
+        np.testing.assert_array_equal(a["translation"][i], b["translation"][i])

@@ -30,6 +30,7 @@ def main():
                 torch.cuda.synchronize()
                 t2 = time.perf_counter()
                 gp.ready = 1 - gp.ready
+                time.sleep(0.005)  # (an idle gap: tools/timeline.py splits the trace here)
                 print(f"lanes {lanes}: replay() call {1e3 * (t1 - t0):.3f} ms, replay + sync "
                       f"{1e3 * (t2 - t0):.3f} ms = {1e3 * (t2 - t0) / lanes:.4f} ms/forward", flush=True)
         del gp
