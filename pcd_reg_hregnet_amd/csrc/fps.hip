@@ -30,10 +30,7 @@
 #include <stdlib.h>
 
 #ifndef HREG_FPS_MAX3
-#define HREG_FPS_MAX3 0
-#endif
-#ifndef HREG_FPS_SX
-#define HREG_FPS_SX 0
+#define HREG_FPS_MAX3 1  // one v_max3_f32 per slot pair in the scan (A/B: 0, two v_med3)
 #endif
 
 namespace {
@@ -160,7 +157,8 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             t.y = fmin_nc(d.y, PT[s].y, inf);
             PT[s] = t;
 #if HREG_FPS_MAX3
-            // one v_max3_f32 per pair instead of two v_med3 (t and best are never NaN)
+            // one v_max3_f32 per pair instead of two v_med3 (t and best are never NaN):
+            // level-1 FPS 1.634 -> 1.588 us per iteration, bench +0.7 % (A/B on one box, r4)
             asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(t.x), "v"(t.y));
 #else
             best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
@@ -168,20 +166,6 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         }
         if constexpr (STAMP) t1 = stamp();
         const float wmax = wave_max_uniform(best, inf);
-#if HREG_FPS_SX
-        // the winning lane first (lowest lane holding the wave max = lowest reference order),
-        // then its first slot holding it: the lane's temps read into SGPRs (one v_readlane each)
-        // and compared on the scalar unit -- no per-lane mask pass over every slot
-        const uint64_t hit = __ballot(best == wmax);
-        const int wl = (int)__builtin_ctzll(hit);
-        const uint32_t wbits = __float_as_uint(wmax);
-        int sl = 0;
-#pragma unroll
-        for (int s = 2 * S2 - 1; s >= 0; --s) {
-            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(PT[s / 2][s % 2]), wl);
-            sl = v == wbits ? s : sl;
-        }
-#else
         // this lane's first slot holding the wave max (bit mask + find-first-set)
         uint32_t smask = 0;
 #pragma unroll
@@ -191,7 +175,6 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         const uint64_t hit = __ballot(best == wmax);
         const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest reference order
         const int sl = __builtin_amdgcn_readlane(myslot, wl);
-#endif
         const int rp = (wv * 64 + wl) * G + sl / QT;
         const int kwin = (int)bitrev_bits((uint32_t)rp, L) + (sl % QT) * bs;
         float wx = 0.f, wy = 0.f, wz = 0.f;

@@ -133,12 +133,6 @@ __global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : HREG_L16_WPS) voi
         }
     };
 
-#ifndef HREG_L1_PRIO
-#define HREG_L1_PRIO 0  // (A/B: the second half of the 8 waves at s_setprio 1, MI355X_MICROARCH.md)
-#endif
-    if constexpr (LDSW && HREG_L1_PRIO) {
-        if (w >= 4) __builtin_amdgcn_s_setprio(1);
-    }
     Carry carry;
     ld6(table_ptr(), G_DC1, lane, carry[0]);
     for (int g = blockIdx.x * L1_WAVES + w; g < G; g += gridDim.x * L1_WAVES) {
