@@ -17,6 +17,10 @@
 // sum_d (q_d - p_d)^2, non-contracted, sequential in d.
 #include "common.h"
 
+#ifndef HREG_KNN_PAIR
+#define HREG_KNN_PAIR 0  // (A/B: two blocks per best-first round trip in the indexed kNN)
+#endif
+
 namespace {
 
 constexpr int WAVES = 4;
@@ -506,7 +510,10 @@ __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
     // approximate (bound bits truncated to make room for the block id), the stop
     // test is exact: stop when even the truncated bound exceeds tau; a block whose
     // exact bound exceeds tau is skipped, not visited.
-    for (;;) {
+    // the next block by (truncated) lower bound, removed from the candidates; returns the
+    // block (or -1 when none is left or even the truncated bound exceeds tau_bits) and its
+    // exact bound
+    auto next_block = [&](uint32_t tau_bits, uint32_t &lbb) -> int {
         uint32_t kmin = 0xffffffffu;
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
@@ -515,24 +522,47 @@ __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
             kmin = kk < kmin ? kk : kmin;
         }
         kmin = wave_min_u32(kmin);
-        if (kmin == 0xffffffffu) break;
-        const uint32_t tau_bits = (uint32_t)(L.tau >> 32);  // >= 0x7f800000 while unset
-        if ((kmin & HI) > tau_bits) break;
+        if (kmin == 0xffffffffu || (kmin & HI) > tau_bits) return -1;
         const int b = (int)(kmin & ~HI);
-        const uint32_t lbb = __builtin_amdgcn_readlane(lb[b >> 6], b & 63);
+        lbb = __builtin_amdgcn_readlane(lb[b >> 6], b & 63);
 #pragma unroll
         for (int t = 0; t < NBL; ++t)
             if ((b >> 6) == t && lane == (b & 63)) lb[t] = 0xffffffffu;
+        return b;
+    };
+    auto block_key = [&](const float4 v, int i) -> uint64_t {
+        if (i >= n) return KEY_INF;
+        const float d = sqdist3(qx, qy, qz, v.x, v.y, v.z);
+        return ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)__float_as_int(v.w);
+    };
+    for (;;) {
+        const uint32_t tau_bits = (uint32_t)(L.tau >> 32);  // >= 0x7f800000 while unset
+        uint32_t lbb = 0, lbb2 = 0;
+        const int b = next_block(tau_bits, lbb);
+        if (b < 0) break;
+#if HREG_KNN_PAIR
+        // (r4) the second-best block too, its points loaded in the same round trip: half the
+        // dependent L2 round trips per query.  Exact: a block whose bound exceeds tau is
+        // skipped, every offered point is filtered by the running K-th key, and the stop test
+        // is unchanged (any extra block visited only offers more candidates).
+        const int b2 = L.tau == KEY_INF ? -1 : next_block(tau_bits, lbb2);
+        const bool use1 = lbb <= tau_bits, use2 = b2 >= 0 && lbb2 <= tau_bits;
+        const int i1 = b * 64 + lane, i2 = b2 * 64 + lane;
+        float4 v1 = make_float4(0.f, 0.f, 0.f, 0.f), v2 = v1;
+        if (use1 && i1 < n) v1 = S[i1];
+        if (use2 && i2 < n) v2 = S[i2];
+        if (use1) {
+            offer<K>(L, sbuf[w], block_key(v1, i1), lane);
+            if (L.tau == KEY_INF && L.cnt > 0) flush64<K>(L, sbuf[w], lane);  // first tau early
+        }
+        if (use2) offer<K>(L, sbuf[w], block_key(v2, i2), lane);
+#else
         if (lbb > tau_bits) continue;
         const int i = b * 64 + lane;
-        uint64_t key = KEY_INF;
-        if (i < n) {
-            const float4 v = S[i];
-            const float d = sqdist3(qx, qy, qz, v.x, v.y, v.z);
-            key = ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)__float_as_int(v.w);
-        }
-        offer<K>(L, sbuf[w], key, lane);
+        const float4 v = i < n ? S[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        offer<K>(L, sbuf[w], block_key(v, i), lane);
         if (L.tau == KEY_INF && L.cnt > 0) flush64<K>(L, sbuf[w], lane);  // first tau early
+#endif
     }
     if (L.cnt > 0) flush64<K>(L, sbuf[w], lane);
 
