@@ -598,6 +598,8 @@ def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=(), b6=Fa
     if out is None:
         out = torch.empty((R, lin.N), device=lin.W.device, dtype=torch.float32)
     g = _gemm_struct(segs, lin, R, out, adds)
+    if PROBE_SKIP_GEMM:
+        return out
     if b6 and B6_GEMM and not adds:
         _lib.gemm6(g)
     else:
@@ -664,7 +666,8 @@ def _batched_desc_struct(lin: Lin, desc3, rows: int, C: int, out) -> Gemm:
 
 def cosine_gemm(a, b, na, nb_, nb: int, n1: int, n2: int, C: int, out):
     """S[b][i][j] = <a_i, b_j> / (|a_i||b_j| + 1e-6) per pair (layers.py:29-41)."""
-    _lib.gemm(_cosine_struct(a, b, na, nb_, nb, n1, n2, C, out))
+    if not PROBE_SKIP_GEMM:
+        _lib.gemm(_cosine_struct(a, b, na, nb_, nb, n1, n2, C, out))
     return out
 
 
@@ -1036,6 +1039,11 @@ def mlp_head(P: PreparedWeights, key, x, nclouds, rows, mode, want_weights=False
         dev = x.device
         out = _empty(nclouds * rows, device=dev)
         wout = _empty(nclouds * rows, device=dev) if want_weights else None
+        if PROBE_SKIP_MLP:
+            out.fill_(1.0)
+            if wout is not None:
+                wout.fill_(1.0)
+            return out, wout
         if B6_MLP:
             call("hreg_mlp_head6", P.head_table6[key], C, x, C, nclouds, rows, mode, out, wout,
                  _stream())
@@ -1054,6 +1062,11 @@ def _mlp_weights(P: PreparedWeights, key, x, nclouds, rows):
     w, _ = mlp_head(P, key, x, nclouds, rows, _lib.HREG_HEAD_SIGMOID)
     return w
 
+
+# Timing probes (results WRONG, A/B timing only; tools/gpu_abn.sh sw:...): skip the plain /
+# grouped GEMM launches, or replace the mlp heads by constant fills
+PROBE_SKIP_GEMM = switches.flag("PROBE_SKIP_GEMM", False)
+PROBE_SKIP_MLP = switches.flag("PROBE_SKIP_MLP", False)
 
 # The registration heads' products of the feature-extraction outputs -- CoarseReg's neighbour
 # branch block (W_desc desc3), its convs_1 desc / knn_desc blocks, the original cosine
@@ -1089,7 +1102,8 @@ def head_products(P: PreparedWeights, B: int, desc):
         pre = _empty(2, B * M, P.fine[name][0][0].W.shape[0], device=dev)
         gs.append(_batched_desc_struct(P.fine_pre6[name], dl, B * M, Cl, pre))
         fine[name] = pre
-    _lib.gemm_grouped(gs)
+    if not PROBE_SKIP_GEMM:
+        _lib.gemm_grouped(gs)
     return {"nbr_pre": nbr_pre, "ud": ud, "S": S, "fine_pre": fine}
 
 

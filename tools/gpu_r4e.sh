@@ -12,6 +12,9 @@ for r in 1 2; do
   timeout -k 10 200 python bench.py --no-cpu-baseline > $O/b48_base.$r.json 2> $O/e || { tail $O/e; exit 1; }
   HREG_LIB=$V timeout -k 10 200 python bench.py --no-cpu-baseline > $O/b48_pair.$r.json 2> $O/e || { tail $O/e; exit 1; }
 done
+for v in PROBE_SKIP_GEMM=1 PROBE_SKIP_MLP=1; do
+  HREG_SWITCHES=$v timeout -k 10 200 python bench.py --no-cpu-baseline > $O/probe_$v.json 2> $O/e || { tail $O/e; exit 1; }
+done
 for r in 1 2 3; do
   timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/s20_up.$r.json 2> $O/e || { tail $O/e; exit 1; }
   HREG_SWITCHES=GRAPH_UPLOAD=0 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/s20_noup.$r.json 2> $O/e || { tail $O/e; exit 1; }
