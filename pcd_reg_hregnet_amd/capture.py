@@ -14,10 +14,7 @@ mirror the forward's (Python) fork structure, so checking the forward's is suffi
 from __future__ import annotations
 
 import contextlib
-import ctypes
 import threading
-
-from . import switches
 
 
 class NestedForkError(RuntimeError):
@@ -80,37 +77,12 @@ def guard(origin, stream_cls=None, event_cls=None):
         _ACTIVE.checker = prev
 
 
-# Upload every captured graph to the device right after its capture (hipGraphUpload), so its
-# first replay does not pay the upload inside whatever region it runs in -- the bench's timed
-# region launches a graph for the first time whenever the warm-up used other graphs (a
-# partial round at --steps 20 --warmup 5).
-UPLOAD = switches.flag("GRAPH_UPLOAD", True)
-_HIP = None
-
-
-def upload(g) -> None:
-    """hipGraphUpload of a captured torch CUDAGraph on the current stream (PyTorch's HIP
-    runtime: the library of the same soname this process already loaded)."""
-    global _HIP
-    import torch
-    if _HIP is None:
-        lib = ctypes.CDLL("libamdhip64.so.7")
-        lib.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        lib.hipGraphUpload.restype = ctypes.c_int
-        _HIP = lib
-    rc = _HIP.hipGraphUpload(ctypes.c_void_p(g.raw_cuda_graph_exec()),
-                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-    if rc != 0:
-        raise RuntimeError(f"hipGraphUpload failed ({rc})")
-
-
 @contextlib.contextmanager
 def graph(g, pool=None):
-    """``torch.cuda.graph(g, pool)`` with the fork/join guard on its capture stream; the
-    captured graph is uploaded to the device afterwards (UPLOAD)."""
+    """``torch.cuda.graph(g, pool)`` with the fork/join guard on its capture stream.  (r4: an
+    explicit hipGraphUpload after each capture made the driver's --steps 20 line 2.5 % slower,
+    6853 / 6823 / 6998 vs 7041 / 7034 / 7071 pairs/s on one box, and was removed.)"""
     import torch
     with torch.cuda.graph(g, pool=pool):
         with guard(torch.cuda.current_stream()):
             yield
-    if UPLOAD:
-        upload(g)
