@@ -60,13 +60,13 @@ def _needs(obj: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src: str, obj: str) -> tuple[str, int, str]:
-    cmd = [HIPCC, *CFLAGS, *file_flags(src), "-c", src, "-o", obj]
+def _compile(src: str, obj: str, extra=()) -> tuple[str, int, str]:
+    cmd = [HIPCC, *CFLAGS, *file_flags(src), *extra, "-c", src, "-o", obj]
     p = subprocess.run(cmd, capture_output=True, text=True)
     return src, p.returncode, p.stdout + p.stderr
 
 
-def _build_lib(srcs, objdir, lib, headers, verbose, force) -> str:
+def _build_lib(srcs, objdir, lib, headers, verbose, force, extra=()) -> str:
     os.makedirs(objdir, exist_ok=True)
     jobs = []
     objs = []
@@ -77,7 +77,7 @@ def _build_lib(srcs, objdir, lib, headers, verbose, force) -> str:
             jobs.append((s, o))
     if jobs:
         with cf.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
-            for src, rc, log in ex.map(lambda a: _compile(*a), jobs):
+            for src, rc, log in ex.map(lambda a: _compile(*a, extra), jobs):
                 if verbose or rc:
                     sys.stderr.write(f"[hipcc] {os.path.basename(src)} rc={rc}\n{log}")
                 if rc:
@@ -99,5 +99,20 @@ def build(verbose: bool = False, force: bool = False) -> str:
                       force)
 
 
+def variant(name: str, defines: list[str], verbose: bool = False) -> str:
+    """A/B build of the core library with extra -D switches (the csrc/*.hip HREG_* compile
+    switches) into pcd_reg_hregnet_amd/ab_<name>.so, loaded by HREG_LIB (tools/gpu_abn.sh
+    lib:ab_<name>.so).  Always a full rebuild: a variant must export what the tree does."""
+    headers = []
+    return _build_lib(sorted(glob.glob(os.path.join(CSRC, "*.hip"))), os.path.join(OBJDIR, "ab_" + name),
+                      os.path.join(HERE, f"ab_{name}.so"), headers, verbose, True,
+                      [f"-D{d}" for d in defines])
+
+
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv, force="-f" in sys.argv))
+    # python -m pcd_reg_hregnet_amd.build [-v] [-f] | --variant NAME DEF=V ...
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        print(variant(sys.argv[i + 1], sys.argv[i + 2:], verbose="-v" in sys.argv[:i]))
+    else:
+        print(build(verbose="-v" in sys.argv, force="-f" in sys.argv))

@@ -170,14 +170,138 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
     }
 }
 
+// HREG_HEAD_JT (bf16x6 only): one workgroup of CW waves owns JT row tiles at once and every
+// wave multiplies each chunk of weight pieces it streams from L2 into all JT row tiles
+// (split_chain.h pipe_lds6_jt), so a head moves JT x fewer weight bytes per MFMA -- the
+// pieces of a C = 512 head are 3 MB per pass, and that stream, not the matrix cores, set
+// the kernel's CU time.  Per row the arithmetic is the JT = 1 kernel's, in the same order,
+// whatever row tiles share a workgroup (test_gpu_model.py: a pair alone and inside a batch,
+// ragged row-tile counts).
+#ifndef HREG_HEAD_JT
+#define HREG_HEAD_JT 1
+#endif
+
+template <int C> struct HeadJT { static constexpr int v = C >= 256 ? 2 : 4; };
+
+template <class K, int JT>
+__global__ __launch_bounds__(K::CW * 64) void mlp_head6_jt_kernel(const float *__restrict__ table,
+                                                                   const float *__restrict__ x, int ldx,
+                                                                   int G, int mode, float *__restrict__ out) {
+    constexpr int C = K::C, P = K::P, CW = K::CW, LDSW = K::LDSW, NE = K::NE, NCH = K::NCH;
+    __shared__ float ep[NE];
+    __shared__ __attribute__((aligned(16))) float sA[JT * 32 * LDSW];
+    __shared__ float sPart[CW][JT][32];
+    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END6 + i];
+    const float *eb = ep;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, j = lane & 31;
+    const int NT = G / 32;
+    const int c0 = w * P;
+    const FragSeq g1{K::G_M1 + c0 * NCH, NCH}, g2{K::G_M2 + c0 * NCH, NCH};
+    const ChanBJ<LDSW> xb{sA + j * LDSW, h};
+
+    Carry6 carry6;
+    {
+        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table));
+#pragma unroll
+        for (int i = 0; i < P; ++i) ld6(wt, g1.base + i * g1.stride, lane, carry6[i]);
+    }
+    for (int base = blockIdx.x * JT; base < NT; base += gridDim.x * JT) {
+        uint64_t tba = reinterpret_cast<uint64_t>(table);
+        asm volatile("" : "+s"(tba));
+        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
+        Carry6 ca6;
+
+        tile_sync();  // the previous group's readers of sA are done (and ep is loaded)
+        // row tiles past the end restage the last tile (their outputs are not stored)
+        constexpr int F4 = C / 4;
+#pragma unroll
+        for (int i = threadIdx.x; i < JT * 32 * F4; i += CW * 64) {
+            const int r = i / F4, c4 = i - r * F4;
+            const int t = min(base + (r >> 5), NT - 1);
+            *reinterpret_cast<float4 *>(sA + r * LDSW + c4 * 4) =
+                *reinterpret_cast<const float4 *>(x + ((size_t)t * 32 + (r & 31)) * ldx + c4 * 4);
+        }
+        tile_sync();
+
+        f32x16 y[P][JT];
+        {
+            f32x16 b[P];
+            beta_p<P, C>(eb + K::R_M1, c0, h, b);  // folded BN (engine._fold_bn)
+#pragma unroll
+            for (int i = 0; i < P; ++i)
+#pragma unroll
+                for (int jt = 0; jt < JT; ++jt) y[i][jt] = b[i];
+        }
+        pipe_lds6_jt<NCH, P, P, JT>(wt, lane, g1, xb, y, carry6, g2, ca6);
+#pragma unroll
+        for (int i = 0; i < P; ++i) relu_tiles(y[i]);
+        tile_sync();  // every wave has read x from sA
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt) put_tile<LDSW>(sA + jt * 32 * LDSW, c0 + i, j, h, y[i][jt]);
+        tile_sync();
+
+        {
+            f32x16 b[P];
+            beta_p<P, C>(eb + K::R_M2, c0, h, b);
+#pragma unroll
+            for (int i = 0; i < P; ++i)
+#pragma unroll
+                for (int jt = 0; jt < JT; ++jt) y[i][jt] = b[i];
+        }
+        pipe_lds6_jt<NCH, P, P, JT>(wt, lane, g2, xb, y, ca6, g1, carry6);
+#pragma unroll
+        for (int i = 0; i < P; ++i) relu_tiles(y[i]);
+
+        // mlp3 as in mlp_head_kernel, per row tile
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) {
+            float p = 0.f;
+#pragma unroll
+            for (int i = 0; i < P; ++i)
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    p = fadd_rn(p, fmul_rn(y[i][jt][q], eb[K::R_W3 + chan(c0 + i, q, h)]));
+            p = fadd_rn(p, __shfl_xor(p, 32));
+            if (h == 0) sPart[w][jt][j] = p;
+        }
+        tile_sync();
+        if (threadIdx.x < JT * 32) {
+            const int jt = threadIdx.x >> 5, r = threadIdx.x & 31, t = base + jt;
+            float z = sPart[0][jt][r];
+#pragma unroll
+            for (int c = 1; c < CW; ++c) z = fadd_rn(z, sPart[c][jt][r]);
+            z = fadd_rn(z, eb[K::R_B3]);
+            float o;
+            if (mode == HREG_HEAD_SOFTPLUS) {
+                const float sp = z > 20.f ? z : log1pf(expf(z));
+                o = fadd_rn(sp, 0.001f);
+            } else {
+                o = 1.0f / fadd_rn(1.0f, expf(-z));
+            }
+            if (t < NT) out[(size_t)t * 32 + r] = o;
+        }
+    }
+}
+
 template <class K, bool B6>
 int launch_head(const float *table, const float *x, int ldx, int G, int mode, float *out, void *stream) {
     const int NT = G / 32;
-    int grid = (NT + K::RT - 1) / K::RT;
-    if (grid > 2048) grid = 2048;
     if (B6 && (reinterpret_cast<uintptr_t>(table) & 15)) return HREG_ERR_INVALID;
-    hipLaunchKernelGGL((mlp_head_kernel<K, B6>), dim3(grid), dim3(K::THREADS), 0, as_stream(stream), table,
-                       x, ldx, G, mode, out);
+    if constexpr (B6 && HREG_HEAD_JT) {
+        constexpr int JT = HeadJT<K::C>::v;
+        int grid = (NT + JT - 1) / JT;
+        if (grid > 2048) grid = 2048;
+        hipLaunchKernelGGL((mlp_head6_jt_kernel<K, JT>), dim3(grid), dim3(K::CW * 64), 0, as_stream(stream),
+                           table, x, ldx, G, mode, out);
+    } else {
+        int grid = (NT + K::RT - 1) / K::RT;
+        if (grid > 2048) grid = 2048;
+        hipLaunchKernelGGL((mlp_head_kernel<K, B6>), dim3(grid), dim3(K::THREADS), 0, as_stream(stream), table,
+                           x, ldx, G, mode, out);
+    }
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

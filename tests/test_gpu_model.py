@@ -553,7 +553,10 @@ def test_nbr_head6_split_matches_chained(net, G):
 @pytest.mark.parametrize("key,C,rows,mode", [(("det", 0), 64, 1024, 0), (("det", 1), 128, 512, 0),
                                            (("det", 2), 256, 256, 0), ("coarse", 512, 256, 1),
                                            ("fine_corres_2", 256, 512, 1),
-                                           ("fine_corres_1", 128, 1024, 1)])
+                                           ("fine_corres_1", 128, 1024, 1),
+                                           # ragged: row-tile counts not a multiple of the
+                                           # head's row tiles per workgroup (HREG_HEAD_JT)
+                                           ("coarse", 512, 96, 1), ("fine_corres_1", 128, 160, 1)])
 @pytest.mark.parametrize("b6", [False, True])
 def test_fused_mlp_head_matches_layerwise(net, key, C, rows, mode, b6, monkeypatch):
     """mlp_head.hip (mlp1 -> mlp2 -> mlp3 + softplus/sigmoid in one launch; b6: bf16x6
