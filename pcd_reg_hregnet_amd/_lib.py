@@ -263,6 +263,12 @@ def stream_handle() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+# timing probe (tools/train_probe.sh only): the entries named in HREG_PROBE_TWICE run twice per
+# call, so a run's extra wall time is that kernel family's cost under the step's stream overlap
+# (results change -- accumulating entries add twice -- so no test sets it)
+_TWICE = frozenset(filter(None, os.environ.get("HREG_PROBE_TWICE", "").split(",")))
+
+
 def call(name: str, *args) -> None:
     L = load_checkers() if name in _CHECKER_SIGS else load()
     conv = []
@@ -272,6 +278,8 @@ def call(name: str, *args) -> None:
         else:
             conv.append(a)
     rc = getattr(L, name)(*conv)
+    if rc == HREG_OK and name in _TWICE:
+        rc = getattr(L, name)(*conv)
     if rc != HREG_OK:
         raise RuntimeError(f"{name} failed: {_ERRORS.get(rc, rc)} (code {rc})")
 
