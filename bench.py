@@ -300,7 +300,7 @@ def pmc_traffic(kernel: str):
     (profiles/r*_traffic.json, made by tools/rocpd_summary.py traffic; the latest round
     that measured every kernel of the family)."""
     names = [n.split(" (")[0] for n in kernel.split(" + ")]
-    for rnd in ("r3", "r2", "r1"):
+    for rnd in ("r4", "r3", "r2", "r1"):
         path = os.path.join(REPO, "profiles", f"{rnd}_traffic.json")
         try:
             per = json.load(open(path))["bytes_per_launch"]

@@ -120,7 +120,8 @@ def traffic(fetch_path, write_path, out=None, out_json=None):
                   open(out_json, "w"), indent=1)
 
 
-SIMD_NUM = 256 * 4
+CU_NUM = 256
+SIMD_NUM = CU_NUM * 4
 XCD_NUM = 8  # the CSV's GRBM_GUI_ACTIVE is summed over the 8 XCDs; the derived formula
 #              takes reduce(GRBM_GUI_ACTIVE, max), i.e. one XCD's count
 PEAK_F32_TFLOPS = 157.3
@@ -138,7 +139,8 @@ def mfma(path, out=None, out_json=None):
         key = (short(r["Kernel_Name"]), r["Dispatch_Id"])
         per[key][r["Counter_Name"]] = float(r["Counter_Value"])
         per[key]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
-    agg = defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0.0, 0.0])
+        per[key]["_wg"] = float(r["Grid_Size"]) / max(1.0, float(r["Workgroup_Size"]))
+    agg = defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0])
     for (name, _), c in per.items():
         if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
             continue
@@ -149,19 +151,27 @@ def mfma(path, out=None, out_json=None):
         a[3] += c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) * 512
         a[4] += c["_ns"]
         a[5] += c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512
-    lines = ["| kernel | dispatches | MfmaUtil % | f32 MFMA GFLOP/dispatch | f32 TF/s (% of 157.3) | "
-             "bf16 MFMA GFLOP/dispatch | bf16 TF/s (% of 2500) |", "|---|---|---|---|---|---|---|"]
+        a[6] += c["_wg"]
+    # MfmaUtil is a whole-chip average: a launch of fewer workgroups than CUs can reach at most
+    # WGs / 256 of it, so the CUs it occupies are also shown (util x 256 / min(256, WGs))
+    lines = ["| kernel | dispatches | workgroups | MfmaUtil % | on occupied CUs % | f32 MFMA GFLOP/dispatch | "
+             "f32 TF/s (% of 157.3) | bf16 MFMA GFLOP/dispatch | bf16 TF/s (% of 2500) |",
+             "|---|---|---|---|---|---|---|---|---|"]
     res = {}
-    for name, (n, busy, active, flops, ns, bflops) in sorted(agg.items(), key=lambda kv: -(kv[1][3] + kv[1][5])):
+    for name, (n, busy, active, flops, ns, bflops, wgs) in sorted(agg.items(),
+                                                                  key=lambda kv: -(kv[1][3] + kv[1][5])):
         if flops <= 0 and bflops <= 0:
             continue
         util = 100.0 * busy / active if active else 0.0
+        wg = wgs / n
+        occ = util * CU_NUM / min(CU_NUM, wg) if wg else 0.0
         tf = flops / ns / 1e3 if ns else 0.0
         btf = bflops / ns / 1e3 if ns else 0.0
-        res[name] = {"mfma_util_pct": round(util, 1), "f32_gflop_per_dispatch": round(flops / n / 1e9, 3),
+        res[name] = {"mfma_util_pct": round(util, 1), "workgroups": round(wg),
+                     "mfma_util_occupied_cus_pct": round(occ, 1), "f32_gflop_per_dispatch": round(flops / n / 1e9, 3),
                      "f32_tflops": round(tf, 1), "bf16_gflop_per_dispatch": round(bflops / n / 1e9, 3),
                      "bf16_tflops": round(btf, 1)}
-        lines.append(f"| `{name[:80]}` | {n} | {util:.1f} | {flops / n / 1e9:.3f} | {tf:.1f} "
+        lines.append(f"| `{name[:80]}` | {n} | {wg:.0f} | {util:.1f} | {occ:.1f} | {flops / n / 1e9:.3f} | {tf:.1f} "
                      f"({100 * tf / PEAK_F32_TFLOPS:.1f} %) | {bflops / n / 1e9:.3f} | {btf:.1f} "
                      f"({100 * btf / 2500.0:.1f} %) |")
     text = "\n".join(lines)
