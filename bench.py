@@ -736,6 +736,12 @@ def main():
             return pipe.run([(src, dst)] * n)
 
     run(args.warmup)
+    if gpipe is not None:
+        # (front streaming, engine.GraphPipeline: fill the pipeline so that every timed round
+        # runs the registration half of its batches and the feature extraction of the next
+        # round's -- whole forwards per round, as the streamed stage 1 already is)
+        with torch.no_grad():
+            gpipe.prime()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

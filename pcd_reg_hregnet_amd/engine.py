@@ -56,6 +56,12 @@ PAIR_L2 = switches.flag("PAIR_L2", False)
 # GraphPipeline: level-1 stage of all lanes as one batched launch per kernel (one side
 # stream) instead of one per lane
 BATCH_STAGE1 = switches.flag("BATCH_STAGE1", True)
+FRONT_STREAM = switches.flag("FRONT_STREAM", True)  # GraphPipeline: halves of a forward in consecutive rounds
+FRONT_ORDER = switches.integer("FRONT_ORDER", 0)  # per lane: 0 back then front, 1 front then back, 2 by lane parity
+# front streaming pays for a round's tail; with many lanes the tail is a small part of the round
+# (measured, one box, 3 paired lines each: 20 lanes 7112 -> 7253 pairs/s with order 0; 48 lanes
+# 7504 -> 7416 with order 0, 7505 with order 1)
+FRONT_STREAM_MAX_LANES = switches.integer("FRONT_STREAM_MAX_LANES", 24)
 B6_L1 = switches.flag("B6_L1", True)  # group_l1_6.hip for level 1
 # level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
 # (group_split6.hip)
@@ -1289,6 +1295,13 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts
     FineReg2 (model_v2/layers.py:462-500), whose attentive features also pass
     through mlpx (Conv1d 2C->C + BN + ReLU) -> "src_dst_feats_2" [B, C, M2]; the
     batch-shuffled prime copies are added by model_v2_finish (host RNG)."""
+    return hregnet_back(P, hregnet_front(P, src, dst, use_weights, l1, pts, use_fps), src.shape[0], v2)
+
+
+def hregnet_front(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=None, use_fps=True):
+    """The feature extraction of both clouds of HRegNet.forward (models.py:79-80): the
+    dict hregnet_back continues from (GraphPipeline runs the two halves of a forward in
+    consecutive rounds)."""
     B, N, _ = src.shape
     if pts is None:
         pts = torch.cat([src, dst], 0).contiguous()
@@ -1297,7 +1310,15 @@ def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts
         if l1 is not None:
             raise ValueError("use_fps=False draws its level-1 sample in the forward (no l1)")
         samples = random_samples(2, B, level_input_sizes(N), src.device)
-    fe = feature_extraction(P, pts, use_weights, l1, samples)
+    return feature_extraction(P, pts, use_weights, l1, samples)
+
+
+# what hregnet_back reads of the feature-extraction dict
+FRONT_KEYS = tuple(f"{k}_{i + 1}" for k in ("xyz", "sigmas", "desc", "fps_idx") for i in range(3))
+
+
+def hregnet_back(P: PreparedWeights, fe, B: int, v2=False):
+    """The registration half of HRegNet.forward (models.py:82-148) from hregnet_front's dict."""
 
     def split(t, rows):
         return t[:B * rows], t[B * rows:]
@@ -1452,6 +1473,17 @@ class GraphPipeline:
     complete forward; outputs are bitwise those of ``hregnet_forward``.
     v2: the Model_V2 forward; the prime shuffles (host torch.randperm, as the
     reference draws them) are gathered eagerly after each round's replay.
+
+    FRONT_STREAM (batched stage 1, streaming calls of whole rounds): a forward's two halves
+    run in consecutive rounds -- round r replays, per lane, the registration half of the
+    batch whose feature extraction round r - 1 ran (``hregnet_back``) and the feature
+    extraction of the next batch (``hregnet_front``, its dict copied into static buffers),
+    beside the batched stage 1 of the batch after that.  Every round still completes
+    ``lanes`` whole forwards, but each lane's dependent chain per round is half a forward,
+    so the round's tail (the last chains draining, ~1.3 ms of a 20-lane round) is shorter:
+    +2 % at 20 lanes; at 48 lanes, where the tail is 2.5 % of the round, it measured 1 %
+    slower, hence FRONT_STREAM_MAX_LANES.  ``prime()`` fills the pipeline (untimed: the
+    bench calls it after its warm-up).
     """
 
     def __init__(self, P: PreparedWeights, src, dst, use_weights=True, lanes: int = 1,
@@ -1515,6 +1547,29 @@ class GraphPipeline:
             self.outs_last.append(out)
         self._part = {}
         self.ready = None  # buffer set holding a streamed next-round stage 1 (run_forwards)
+        # front streaming: fe[c][ln] = static copies of a lane's feature-extraction dict;
+        # fready = c: the fronts for the next round are in fe[1 - c] and its next stage 1
+        # in bufs[c], so the next replay is g_fs[c]
+        self.fs = FRONT_STREAM and self.bs1 and not v2 and lanes <= FRONT_STREAM_MAX_LANES
+        self.fready = None
+        if self.fs:
+            with torch.no_grad():
+                pts, g = self.bufs[0][0]
+                fe0 = hregnet_front(P, self.src[0], self.dst[0], use_weights, l1=g, pts=pts)
+            self.fe = [[{k: torch.empty_like(fe0[k]) for k in FRONT_KEYS} for _ in range(lanes)]
+                       for _ in (0, 1)]
+            del fe0
+            self.g_fs, self.outs_fs, self.g_prime = [], [], []
+            for cur in (0, 1):
+                g = torch.cuda.CUDAGraph()
+                with capture.graph(g, pool=self.pool):
+                    out = self._fork(lambda ln: self._halves(ln, cur), **self._side_kw(1 - cur))
+                self.g_fs.append(g)
+                self.outs_fs.append(out)
+                g = torch.cuda.CUDAGraph()
+                with capture.graph(g, pool=self.pool):
+                    self._fork(lambda ln: self._front_into(ln, cur), **self._side_kw(1 - cur))
+                self.g_prime.append(g)
         torch.cuda.synchronize()
 
     def _lane_view(self, ab: int, ln: int):
@@ -1588,10 +1643,44 @@ class GraphPipeline:
         return hregnet_forward(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g,
                                pts=pts, v2=self.v2)
 
+    def _front_into(self, ln, cur):
+        """Lane ln's feature extraction from stage-1 set cur, copied into fe[cur][ln]."""
+        pts, g = self.bufs[ln][cur]
+        fe = hregnet_front(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g, pts=pts)
+        for k, t in self.fe[cur][ln].items():
+            t.copy_(fe[k])
+
+    def _halves(self, ln, cur):
+        """One front-streamed round of lane ln: the registration half from fe[1 - cur] and the
+        next batch's feature extraction from stage-1 set cur into fe[cur] (FRONT_ORDER 0, the
+        default: in that order; 1: the other way round; 2: by lane parity)."""
+        if FRONT_ORDER == 1 or (FRONT_ORDER == 2 and ln % 2):
+            self._front_into(ln, cur)
+            return hregnet_back(self.P, self.fe[1 - cur][ln], self.B, self.v2)
+        out = hregnet_back(self.P, self.fe[1 - cur][ln], self.B, self.v2)
+        self._front_into(ln, cur)
+        return out
+
+    def prime(self):
+        """Front streaming: run the next round's feature extraction (and the stage 1 of the
+        round after) now, so that the next streaming call of whole rounds replays g_fs only.
+        A no-op without front streaming or when already primed."""
+        if not self.fs or self.fready is not None:
+            return
+        if self.ready is not None:
+            cur = self.ready
+        else:
+            self.g_first.replay()
+            cur = 0
+        self.g_prime[cur].replay()
+        self.ready = None
+        self.fready = 1 - cur
+
     def load(self, src, dst, lane: int = 0):
         self.src[lane].copy_(src)
         self.dst[lane].copy_(dst)
         self.ready = None  # a streamed stage 1 was made from the old contents
+        self.fready = None  # (and streamed fronts)
 
     def check(self):
         """Raise if a replayed multi-workgroup FPS flagged a poll timeout (synchronous
@@ -1653,6 +1742,20 @@ class GraphPipeline:
             return None
         q, r = divmod(n, self.lanes)
         streaming = stream and self.bs1
+        if self.fready is not None:
+            if streaming and r == 0:
+                cur = self.fready
+                full = [None] * self.lanes
+                for _ in range(q):
+                    self.g_fs[cur].replay()
+                    full = self._finish(self.outs_fs[cur])
+                    cur = 1 - cur
+                self.fready = cur
+                self.check()
+                return full
+            # (static inputs: the pending fronts would repeat the forwards this call runs;
+            # their stage 1 -- the same batches' -- is the next round's)
+            self.ready, self.fready = self.fready, None
         part = self._partial(r) if r else None
         if self.ready is not None:
             cur = self.ready

@@ -299,6 +299,55 @@ def test_graph_streaming_matches_eager(net):
         assert gp.ready is None
 
 
+def test_graph_front_streaming_matches_eager(net):
+    """Front streaming (engine.FRONT_STREAM, the bench's executor after prime()): a round
+    replays each lane's registration half of the batch whose feature extraction the previous
+    round ran, beside the next batch's feature extraction.  Every lane's outputs stay bitwise
+    its eager forward over several calls; a partial or non-streaming call falls back to the
+    plain rounds; load() discards the pending fronts."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    data = [synthetic.lidar_batch(2, 4096, seed0=sd)[:2] for sd in (59, 60, 61, 62)]
+    dev = [(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()) for s, d in data]
+    with torch.no_grad():
+        gp = engine.GraphPipeline(P, dev[0][0], dev[0][1], lanes=3)
+        assert gp.fs
+        for ln in (1, 2):
+            gp.load(dev[ln][0], dev[ln][1], lane=ln)
+        refs = [engine.hregnet_forward(P, s, d) for s, d in dev]
+
+        def check(outs, want):
+            torch.cuda.synchronize()
+            for ln, out in enumerate(outs):
+                if out is None:
+                    continue
+                for i in range(3):
+                    assert torch.equal(out["rotation"][i], refs[want[ln]]["rotation"][i]), ln
+                    assert torch.equal(out["translation"][i], refs[want[ln]]["translation"][i]), ln
+                    assert torch.equal(out["_fps_idx"][i], refs[want[ln]]["_fps_idx"][i]), ln
+                for k in ("src_xyz_corres_1", "src_dst_weights_1", "src_xyz_corres_3"):
+                    assert torch.equal(out[k], refs[want[ln]][k]), (ln, k)
+                assert torch.equal(out["src_feats"]["desc_3"], refs[want[ln]]["src_feats"]["desc_3"])
+                assert torch.equal(out["dst_feats"]["sigmas_1"], refs[want[ln]]["dst_feats"]["sigmas_1"])
+
+        gp.run_forwards(2, stream=True)  # a partial round (the bench's warm-up shape)
+        gp.prime()
+        assert gp.fready is not None
+        for n in (3, 6, 3):
+            check(gp.run_forwards(n, stream=True), [0, 1, 2])
+            assert gp.fready is not None
+        gp.prepare(4)
+        check(gp.run_forwards(4, stream=True), [0, 1, 2])  # partial: plain rounds
+        assert gp.fready is None
+        gp.prime()
+        gp.load(dev[3][0], dev[3][1], lane=2)
+        assert gp.fready is None and gp.ready is None
+        gp.prime()
+        check(gp.run_forwards(3, stream=True), [0, 1, 3])
+        check(gp.run_forwards(3), [0, 1, 3])  # non-streaming after front streaming
+        assert gp.fready is None
+
+
 @pytest.mark.parametrize("lvl,split,pre,b6", [
     (0, False, False, False), (1, False, False, False), (2, False, False, False),
     (1, True, False, False), (2, True, False, False), (1, False, True, False),
