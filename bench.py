@@ -857,7 +857,11 @@ def main():
                        "executor": args.executor + ("" if args.executor == "serial" else
                                    " (level-1 FPS of step i+1 overlaps step i)") + (
                                    f", {args.lanes} batches in flight" if args.lanes > 1 and
-                                   args.executor == "graph" else ""),
+                                   args.executor == "graph" else "") + (
+                                   "; front streaming: each timed round runs the registration "
+                                   "half of its batches and the feature extraction of the next "
+                                   "round's (pipeline primed after the warm-up)"
+                                   if gpipe is not None and gpipe.fs else ""),
                        "global_batch": B * world, "points": args.points,
                        "parallelism": f"dp{world} (pairs sharded, no collective)"},
             "roofline": roof,

@@ -57,10 +57,10 @@ PAIR_L2 = switches.flag("PAIR_L2", False)
 # stream) instead of one per lane
 BATCH_STAGE1 = switches.flag("BATCH_STAGE1", True)
 FRONT_STREAM = switches.flag("FRONT_STREAM", True)  # GraphPipeline: halves of a forward in consecutive rounds
-FRONT_ORDER = switches.integer("FRONT_ORDER", 0)  # per lane: 0 back then front, 1 front then back, 2 by lane parity
+FRONT_ORDER = switches.integer("FRONT_ORDER", 3)  # per lane: 0 back then front, 1 front then back, 2 by lane parity, 3 on two streams
 # front streaming pays for a round's tail; with many lanes the tail is a small part of the round
-# (measured, one box, 3 paired lines each: 20 lanes 7112 -> 7253 pairs/s with order 0; 48 lanes
-# 7504 -> 7416 with order 0, 7505 with order 1)
+# (measured, 3 paired lines each: 20 lanes 7084 -> 7141 pairs/s with order 0, -> 7311 with
+# order 3; 48 lanes 7456 -> 7417 / 7388)
 FRONT_STREAM_MAX_LANES = switches.integer("FRONT_STREAM_MAX_LANES", 24)
 B6_L1 = switches.flag("B6_L1", True)  # group_l1_6.hip for level 1
 # level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
@@ -1476,13 +1476,13 @@ class GraphPipeline:
 
     FRONT_STREAM (batched stage 1, streaming calls of whole rounds): a forward's two halves
     run in consecutive rounds -- round r replays, per lane, the registration half of the
-    batch whose feature extraction round r - 1 ran (``hregnet_back``) and the feature
-    extraction of the next batch (``hregnet_front``, its dict copied into static buffers),
-    beside the batched stage 1 of the batch after that.  Every round still completes
-    ``lanes`` whole forwards, but each lane's dependent chain per round is half a forward,
-    so the round's tail (the last chains draining, ~1.3 ms of a 20-lane round) is shorter:
-    +2 % at 20 lanes; at 48 lanes, where the tail is 2.5 % of the round, it measured 1 %
-    slower, hence FRONT_STREAM_MAX_LANES.  ``prime()`` fills the pipeline (untimed: the
+    batch whose feature extraction round r - 1 ran (``hregnet_back``) and, on a second
+    stream of the lane, the feature extraction of the next batch (``hregnet_front``, its dict
+    copied into static buffers), beside the batched stage 1 of the batch after that.  Every
+    round still completes ``lanes`` whole forwards, but each lane's dependent chain per round
+    is half a forward, so the round's tail (the last chains draining, ~1.3 ms of a 20-lane
+    round) is shorter: +3.2 % at 20 lanes; at 48 lanes, where the tail is 2.5 % of the
+    round, it measured ~1 % slower, hence FRONT_STREAM_MAX_LANES.  ``prime()`` fills the pipeline (untimed: the
     bench calls it after its warm-up).
     """
 
@@ -1560,10 +1560,17 @@ class GraphPipeline:
                        for _ in (0, 1)]
             del fe0
             self.g_fs, self.outs_fs, self.g_prime = [], [], []
+            if FRONT_ORDER == 3:
+                self.lane_streams2 = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
             for cur in (0, 1):
                 g = torch.cuda.CUDAGraph()
                 with capture.graph(g, pool=self.pool):
-                    out = self._fork(lambda ln: self._halves(ln, cur), **self._side_kw(1 - cur))
+                    if FRONT_ORDER == 3:  # the two halves of a lane on two streams
+                        out = self._fork(lambda ln: hregnet_back(P, self.fe[1 - cur][ln], B, v2),
+                                         body2=lambda ln: self._front_into(ln, cur),
+                                         **self._side_kw(1 - cur))
+                    else:
+                        out = self._fork(lambda ln: self._halves(ln, cur), **self._side_kw(1 - cur))
                 self.g_fs.append(g)
                 self.outs_fs.append(out)
                 g = torch.cuda.CUDAGraph()
@@ -1604,7 +1611,7 @@ class GraphPipeline:
         return {"side": lambda ln: stage1_into(self.bufs[ln][ab], self.src[ln], self.dst[ln]),
                 "side_lanes": side_lanes}
 
-    def _fork(self, body, side=None, lanes=None, side_lanes=None, side_all=None):
+    def _fork(self, body, side=None, lanes=None, side_lanes=None, side_all=None, body2=None):
         """Inside a capture: body(lane) for every lane < lanes on its own stream (lane 0
         on the capturing stream) and side(lane) for lane < side_lanes on the lane's side
         stream, all forked from the capturing stream and joined back to it (one level of
@@ -1621,6 +1628,8 @@ class GraphPipeline:
             if side is not None and ln < side_lanes:
                 jobs.append((self.side[ln], side, ln))
             jobs.append((None if ln == 0 else self.lane_streams[ln], body, ln))
+            if body2 is not None:  # (a second job per lane on its own stream)
+                jobs.append((self.lane_streams2[ln], body2, ln))
         for st, _, _ in jobs:
             if st is not None:
                 st.wait_stream(main)
