@@ -17,8 +17,8 @@
 // sum_d (q_d - p_d)^2, non-contracted, sequential in d.
 #include "common.h"
 
-#ifndef HREG_KNN_PAIR
-#define HREG_KNN_PAIR 0  // (A/B: two blocks per best-first round trip in the indexed kNN)
+#ifndef HREG_KNN_MULTI
+#define HREG_KNN_MULTI 1  // (A/B: blocks per best-first round trip in the indexed kNN)
 #endif
 
 namespace {
@@ -461,6 +461,139 @@ __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *
     }
 }
 
+// HREG_SI_MORTON (clouds of <= SI_LDSN points): the points ordered by an 18-bit Morton prefix
+// (64 cells per axis; ties by index) instead of the 12-bit cell alone.  Inside a 12-bit cell
+// (1/16 of the cloud's extent per axis) the counting sort leaves the points in atomic order,
+// so a 64-point block spans most of its cell and a level-1 query (k = 64 of 16384 LiDAR
+// points) scanned ~34 blocks; in 18-bit order ~13 (full 30-bit order ~11;
+// tools/knn_block_sim.py).  The kNN result does not depend on the order (exact bounds, ties
+// by index).  Sort: keys (prefix << 14 | index) packed in 32 bits, three stable LSD counting
+// passes of 6-bit digits in LDS (ping-pong, 2 x 64 KB); each wave owns a contiguous range of
+// the keys, so per-(digit, wave) offsets plus the in-chunk rank among lanes holding the same
+// digit (6 ballots) keep every pass stable.
+#ifndef HREG_SI_MORTON
+#define HREG_SI_MORTON 1
+#endif
+constexpr int SI_DIG = 6, SI_BUCKETS = 1 << SI_DIG, SI_WAVES = SI_THREADS / 64;
+
+__global__ __launch_bounds__(SI_THREADS) void spatial_index_morton_kernel(const float *__restrict__ p, int n,
+                                                                          float4 *__restrict__ spts,
+                                                                          float4 *__restrict__ boxes) {
+    __shared__ uint32_t keys[2][SI_LDSN];
+    __shared__ uint32_t off[SI_BUCKETS][SI_WAVES];  // per-(digit, wave) running scatter offsets
+    __shared__ float red[6][SI_WAVES];
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float *P = p + (size_t)c * n * 3;
+    // cloud bounding box (as spatial_index_kernel)
+    float mn[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+    float mx[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+    for (int i = tid; i < n; i += SI_THREADS)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            mn[d] = fminf(mn[d], P[i * 3 + d]);
+            mx[d] = fmaxf(mx[d], P[i * 3 + d]);
+        }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        mn[d] = -wave_max_f32(-mn[d]);
+        mx[d] = wave_max_f32(mx[d]);
+        if (lane == 0) { red[d][w] = mn[d]; red[3 + d][w] = mx[d]; }
+    }
+    __syncthreads();
+    float lo[3], sc[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        float a = red[d][0], b = red[3 + d][0];
+        for (int i = 1; i < SI_WAVES; ++i) { a = fminf(a, red[d][i]); b = fmaxf(b, red[3 + d][i]); }
+        lo[d] = a;
+        sc[d] = b > a ? 1023.99f / (b - a) : 0.f;
+    }
+    int np = 64;
+    while (np < n) np <<= 1;
+    for (int e = tid; e < np; e += SI_THREADS) {
+        uint32_t v = ~0u;  // padding sorts last (and stays after every real key of equal bits)
+        if (e < n) {
+            const uint32_t code = spread10(quant10(P[e * 3], lo[0], sc[0])) |
+                                  (spread10(quant10(P[e * 3 + 1], lo[1], sc[1])) << 1) |
+                                  (spread10(quant10(P[e * 3 + 2], lo[2], sc[2])) << 2);
+            v = ((code >> 12) << 14) | (uint32_t)e;
+        }
+        keys[0][e] = v;
+    }
+    // wave w owns keys [w * per, (w + 1) * per), in 64-key chunks
+    const int per = np / SI_WAVES >= 64 ? np / SI_WAVES : 64;
+    const int e_lo = w * per, e_hi = min(np, e_lo + per);
+    const uint64_t below = (1ull << lane) - 1ull;
+    int src = 0;
+    for (int pass = 0; pass < 3; ++pass, src ^= 1) {
+        const int shift = 14 + SI_DIG * pass;
+        for (int i = tid; i < SI_BUCKETS * SI_WAVES; i += SI_THREADS) (&off[0][0])[i] = 0;
+        __syncthreads();
+        for (int e0 = e_lo; e0 < e_hi; e0 += 64) {  // counts (lane order inside the wave's range)
+            const uint32_t d = (keys[src][e0 + lane] >> shift) & (SI_BUCKETS - 1);
+            atomicAdd(&off[d][w], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {  // exclusive scan over (digit, wave) in that order: 64 digits x 16 waves
+            uint32_t v[SI_WAVES], t = 0;
+#pragma unroll
+            for (int q = 0; q < SI_WAVES; ++q) { v[q] = off[tid][q]; t += v[q]; }
+            uint32_t incl = t;
+#pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t o = __shfl_up(incl, dd);
+                if (lane >= dd) incl += o;
+            }
+            uint32_t run = incl - t;
+#pragma unroll
+            for (int q = 0; q < SI_WAVES; ++q) { off[tid][q] = run; run += v[q]; }
+        }
+        __syncthreads();
+        for (int e0 = e_lo; e0 < e_hi; e0 += 64) {  // stable scatter
+            const uint32_t v = keys[src][e0 + lane];
+            const uint32_t d = (v >> shift) & (SI_BUCKETS - 1);
+            uint64_t same = ~0ull;
+#pragma unroll
+            for (int b = 0; b < SI_DIG; ++b) {
+                const uint64_t m = __ballot((d >> b) & 1u);
+                same &= ((d >> b) & 1u) ? m : ~m;
+            }
+            const uint32_t base = off[d][w];
+            keys[src ^ 1][base + (uint32_t)__popcll(same & below)] = v;
+            wave_sync();  // every lane has read its digit's offset
+            if ((same & below) == 0) off[d][w] = base + (uint32_t)__popcll(same);
+            wave_sync();
+        }
+        __syncthreads();
+    }
+    const uint32_t *K = keys[src];
+    float4 *S = spts + (size_t)c * np;
+    for (int i = tid; i < n; i += SI_THREADS) {
+        const int id = (int)(K[i] & 0x3fffu);
+        S[i] = make_float4(P[id * 3], P[id * 3 + 1], P[id * 3 + 2], __int_as_float(id));
+    }
+    const int nblk = (n + 63) / 64;
+    float4 *B = boxes + (size_t)c * (np / 64) * 2;
+    for (int b = w; b < nblk; b += SI_WAVES) {
+        const int i = b * 64 + lane;
+        float v3[3], u3[3];
+        if (i < n) {
+            const int id = (int)(K[i] & 0x3fffu);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) v3[d] = u3[d] = P[id * 3 + d];
+        } else {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { v3[d] = __builtin_huge_valf(); u3[d] = -__builtin_huge_valf(); }
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) { v3[d] = -wave_max_f32(-v3[d]); u3[d] = wave_max_f32(u3[d]); }
+        if (lane == 0) {
+            B[b * 2] = make_float4(v3[0], v3[1], v3[2], 0.f);
+            B[b * 2 + 1] = make_float4(u3[0], u3[1], u3[2], 0.f);
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     // DPP row minima, then the four row results
     v = min(v, (uint32_t)dpp_all_i<0xb1>((int)v));
@@ -537,25 +670,37 @@ __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
     };
     for (;;) {
         const uint32_t tau_bits = (uint32_t)(L.tau >> 32);  // >= 0x7f800000 while unset
-        uint32_t lbb = 0, lbb2 = 0;
+        uint32_t lbb = 0;
         const int b = next_block(tau_bits, lbb);
         if (b < 0) break;
-#if HREG_KNN_PAIR
-        // (r4) the second-best block too, its points loaded in the same round trip: half the
+#if HREG_KNN_MULTI > 1
+        // (r4) the next best blocks too, their points loaded in the same round trip: fewer
         // dependent L2 round trips per query.  Exact: a block whose bound exceeds tau is
         // skipped, every offered point is filtered by the running K-th key, and the stop test
         // is unchanged (any extra block visited only offers more candidates).
-        const int b2 = L.tau == KEY_INF ? -1 : next_block(tau_bits, lbb2);
-        const bool use1 = lbb <= tau_bits, use2 = b2 >= 0 && lbb2 <= tau_bits;
-        const int i1 = b * 64 + lane, i2 = b2 * 64 + lane;
-        float4 v1 = make_float4(0.f, 0.f, 0.f, 0.f), v2 = v1;
-        if (use1 && i1 < n) v1 = S[i1];
-        if (use2 && i2 < n) v2 = S[i2];
-        if (use1) {
-            offer<K>(L, sbuf[w], block_key(v1, i1), lane);
-            if (L.tau == KEY_INF && L.cnt > 0) flush64<K>(L, sbuf[w], lane);  // first tau early
+        constexpr int NV = HREG_KNN_MULTI;
+        int bv[NV];
+        uint32_t lbv[NV];
+        bv[0] = b;
+        lbv[0] = lbb;
+        const bool first = L.tau == KEY_INF;
+#pragma unroll
+        for (int t = 1; t < NV; ++t) {
+            lbv[t] = 0xffffffffu;
+            bv[t] = first ? -1 : next_block(tau_bits, lbv[t]);
         }
-        if (use2) offer<K>(L, sbuf[w], block_key(v2, i2), lane);
+        float4 v[NV];
+#pragma unroll
+        for (int t = 0; t < NV; ++t) {
+            const int i = bv[t] * 64 + lane;
+            v[t] = (bv[t] >= 0 && lbv[t] <= tau_bits && i < n) ? S[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int t = 0; t < NV; ++t) {
+            if (bv[t] < 0 || lbv[t] > tau_bits) continue;
+            offer<K>(L, sbuf[w], block_key(v[t], bv[t] * 64 + lane), lane);
+            if (t == 0 && L.tau == KEY_INF && L.cnt > 0) flush64<K>(L, sbuf[w], lane);  // first tau early
+        }
 #else
         if (lbb > tau_bits) continue;
         const int i = b * 64 + lane;
@@ -676,6 +821,9 @@ extern "C" int hreg_spatial_index(const float *p, int nb, int n, void *ws, void 
     if (n > SI_LDSN)
         hipLaunchKernelGGL(spatial_index_kernel<true>, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream),
                            p, n, spts, boxes);
+    else if (HREG_SI_MORTON)
+        hipLaunchKernelGGL(spatial_index_morton_kernel, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream), p, n,
+                           spts, boxes);
     else
         hipLaunchKernelGGL(spatial_index_kernel<false>, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream),
                            p, n, spts, boxes);

@@ -62,6 +62,12 @@ FRONT_ORDER = switches.integer("FRONT_ORDER", 3)  # per lane: 0 back then front,
 # (measured, 3 paired lines each: 20 lanes 7084 -> 7141 pairs/s with order 0, -> 7311 with
 # order 3; 48 lanes 7456 -> 7417 / 7388)
 FRONT_STREAM_MAX_LANES = switches.integer("FRONT_STREAM_MAX_LANES", 24)
+# timing probe (tools only): the level-1 grouping into preallocated buffers skips its FPS (1), its
+# spatial index + kNN (2) or its spatial index (3), leaving the buffers' previous values (static
+# inputs: unchanged)
+PROBE_S1_SKIP = switches.integer("PROBE_S1_SKIP", 0)
+# timing probe (tools only): rounds without the streamed batched stage 1 of the next round
+PROBE_NO_S1 = switches.flag("PROBE_NO_S1", False)
 B6_L1 = switches.flag("B6_L1", True)  # group_l1_6.hip for level 1
 # level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
 # (group_split6.hip)
@@ -818,7 +824,8 @@ def knn_group_indexed(q, p, k, ws, out=None):
         kx = _empty(R, 3, device=dev)
     else:
         gidx, geom, kx = out
-    call("hreg_spatial_index", p, nb, n, ws, _stream())
+    if PROBE_S1_SKIP != 3 or out is None:
+        call("hreg_spatial_index", p, nb, n, ws, _stream())
     call("hreg_knn_group_indexed", q, p, ws, nb, m, n, k, gidx, geom, kx, _stream())
     return gidx, geom, kx
 
@@ -894,10 +901,14 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None):
     nb, n, _ = xyz.shape
     if sample is not None:
         idx, sampled = sample, gather_xyz(xyz, sample)
+    elif PROBE_S1_SKIP == 1 and out is not None and lvl == 0:
+        idx, sampled = out[0], out[1]  # (timing probe: the buffers' previous selection)
     else:
         idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
                            out=None if out is None else out[:2])
     kout = None if out is None else out[2:5]
+    if PROBE_S1_SKIP == 2 and out is not None and lvl == 0:
+        return idx, sampled, out[2], out[3], out[4]
     if SPATIAL_KNN_MIN <= n <= SPATIAL_KNN_MAX:
         if ws is None:
             ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
@@ -1607,6 +1618,8 @@ class GraphPipeline:
         """_fork keywords for the next batch's stage 1 into buffer set ab (batched: one job
         for all lanes; per lane: lanes < side_lanes)."""
         if self.bs1:
+            if PROBE_NO_S1:  # (timing probe: static inputs keep the stage-1 buffers valid)
+                return {}
             return {"side_all": lambda: self._stage1_all(ab)}
         return {"side": lambda ln: stage1_into(self.bufs[ln][ab], self.src[ln], self.dst[ln]),
                 "side_lanes": side_lanes}

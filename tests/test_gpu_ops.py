@@ -319,6 +319,45 @@ def test_transform_points():
                                atol=1e-5)
 
 
+@pytest.mark.parametrize("n", [16384, 5001, 600])
+def test_spatial_index_morton_order(n):
+    """hreg_spatial_index (clouds <= 16384 points): every point exactly once, in ascending
+    18-bit Morton prefix order, ties by index (the stable radix passes), the block boxes
+    enclosing their points."""
+    from pcd_reg_hregnet_amd import _lib, engine, synthetic
+    p = synthetic.lidar_batch(1, 16384, seed0=3)[1][:, :n]
+    p = np.concatenate([p, np.random.default_rng(1).uniform(-40, 40, (1, n, 3)).astype(np.float32)], 0)
+    nb = p.shape[0]
+    ws = torch.empty(engine.spatial_index_bytes(nb, n), dtype=torch.uint8, device="cuda")
+    _lib.call("hreg_spatial_index", torch.from_numpy(np.ascontiguousarray(p)).cuda(), nb, n, ws,
+              _lib.stream_handle())
+    torch.cuda.synchronize()
+    np_ = 64
+    while np_ < n:
+        np_ *= 2
+    raw = ws.cpu().numpy()
+    spts = raw[:nb * np_ * 16].view(np.float32).reshape(nb, np_, 4)
+    boxes = raw[nb * np_ * 16:].view(np.float32).reshape(nb, np_ // 64, 2, 4)
+    for c in range(nb):
+        ids = spts[c, :n, 3].view(np.int32)
+        assert np.array_equal(np.sort(ids), np.arange(n))
+        P = p[c]
+        np.testing.assert_array_equal(spts[c, :n, :3], P[ids])
+        lo, hi = P.min(0), P.max(0)
+        sc = np.where(hi > lo, np.float32(1023.99) / (hi - lo), np.float32(0)).astype(np.float32)
+        t = ((P - lo) * sc).astype(np.float32)
+        qz = np.where(t <= 0, 0, np.where(t >= 1023, 1023, t.astype(np.int64)))
+        code = np.zeros(n, np.int64)
+        for b in range(10):
+            for d in range(3):
+                code |= ((qz[:, d] >> b) & 1) << (3 * b + d)
+        key = (code[ids] >> 12) * n + ids
+        assert np.all(np.diff(key) > 0)
+        for b in range((n + 63) // 64):
+            blk = spts[c, b * 64:min(n, b * 64 + 64), :3]
+            assert np.all(boxes[c, b, 0, :3] <= blk.min(0)) and np.all(boxes[c, b, 1, :3] >= blk.max(0))
+
+
 @pytest.mark.parametrize("case", ["lidar", "cube", "dups", "ragged", "lidar64k", "ragged64k"])
 @pytest.mark.parametrize("K", [8, 32, 64])
 def test_knn_group_indexed_matches_bruteforce(case, K):
