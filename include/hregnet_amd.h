@@ -488,8 +488,9 @@ int hreg_transformation_loss_bwd(const float *pred_R, const float *pred_t, const
                                  const float *gt_t, int nb, float alpha, float scale,
                                  const float *dloss, float *dR, float *dt, void *stream);
 
-/* Spatial index for exact culled kNN grouping (n <= 16384 points per cloud):
- * hreg_spatial_index sorts each cloud of p [nb][n][3] by Morton code and records
+/* Spatial index for exact culled kNN grouping (n <= 65536 points per cloud):
+ * hreg_spatial_index sorts each cloud of p [nb][n][3] by Morton code (n <= 16384: an 18-bit
+ * prefix, ties by index; larger clouds: the 12-bit cell) and records
  * the bounding box of every 64 sorted points into ws (16-byte aligned,
  * hreg_spatial_index_bytes(nb, n) bytes); hreg_knn_group_indexed is
  * hreg_knn_group over that index -- bit-identical results, visiting only the
