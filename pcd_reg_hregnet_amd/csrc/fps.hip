@@ -29,6 +29,9 @@
 
 #include <stdlib.h>
 
+#ifndef HREG_FPS_BESTMASK
+#define HREG_FPS_BESTMASK 1  // the winner-slot mask from the lane's own max (A/B: 0, from the wave max)
+#endif
 #ifndef HREG_FPS_MAX3
 #define HREG_FPS_MAX3 1  // one v_max3_f32 per slot pair in the scan (A/B: 0, two v_med3)
 #endif
@@ -165,12 +168,23 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
 #endif
         }
         if constexpr (STAMP) t1 = stamp();
+#if HREG_FPS_BESTMASK
+        // this lane's first slot holding its own maximum (the winning lane's own maximum is the
+        // wave max, and only its slot is read): no dependence on the wave reduction, so these
+        // compares fill that reduction's latency
+        uint32_t smask = 0;
+#pragma unroll
+        for (int s = 0; s < 2 * S2; ++s)
+            smask |= (PT[s / 2][s % 2] == best) ? (1u << s) : 0u;
+        const float wmax = wave_max_uniform(best, inf);
+#else
         const float wmax = wave_max_uniform(best, inf);
         // this lane's first slot holding the wave max (bit mask + find-first-set)
         uint32_t smask = 0;
 #pragma unroll
         for (int s = 0; s < 2 * S2; ++s)
             smask |= (PT[s / 2][s % 2] == wmax) ? (1u << s) : 0u;
+#endif
         const int myslot = smask ? (int)__builtin_ctz(smask) : 0;
         const uint64_t hit = __ballot(best == wmax);
         const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest reference order
