@@ -295,15 +295,23 @@ def level_kernel(engine, lv: int) -> str:
     return "group_fused6_kernel" if b6 else "group_fused_kernel"
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/r*_traffic.json, made by tools/rocpd_summary.py traffic; the latest round
-    that measured every kernel of the family)."""
+def pmc_traffic(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of THIS
+    workload (the Model_V2 line had borrowed the 16384-point pass):
+    profiles/r*_traffic.json keyed by workload ("hregnet:b8:n16384", "v2:b2:n65536"; made by
+    tools/rocpd_summary.py traffic ... --key); the r1-r4 files hold the configs[1] pass alone.
+    The latest round that measured every kernel of the family; (None, None) when no pass of
+    this workload exists."""
     names = [n.split(" (")[0] for n in kernel.split(" + ")]
-    for rnd in ("r4", "r3", "r2", "r1"):
+    for rnd in ("r5", "r4", "r3", "r2", "r1"):
         path = os.path.join(REPO, "profiles", f"{rnd}_traffic.json")
         try:
-            per = json.load(open(path))["bytes_per_launch"]
+            d = json.load(open(path))
+            if workload in d:
+                d = d[workload]
+            elif "bytes_per_launch" not in d or workload != "hregnet:b8:n16384":
+                continue
+            per = d["bytes_per_launch"]
             # one launch of each per step: mean over the family
             return sum(per[n] for n in names) / len(names), os.path.relpath(path, REPO)
         except (OSError, KeyError, ValueError):
@@ -350,34 +358,39 @@ def cpu_baseline(budget_s: float = 30.0, batches=(1, PAIRS_PER_GPU), reps: int =
             "sample": f"2x{POINTS}-pt KITTI-shape synthetic LiDAR pairs (the GPU run's "
                       f"generator), B in {sorted(med)}, 1 warm-up + median of {reps} each; "
                       "numpy BLAS + OpenMP C oracle (oracle/); value at B="
-                      f"{best_b}; reference Python on 8 vCPU (SURVEY container, BASELINE.md "
-                      "section 2): 0.55 pairs/s at B=1, 0.50 at B=8"}
+                      f"{best_b}; {threads} OpenMP/BLAS threads = OMP_NUM_THREADS as the GPU box "
+                      "sets it: the box's CPU share per GPU (the host's other CPUs serve the "
+                      "other GPUs' jobs; affinity_cpus is the whole mask); reference Python on 8 "
+                      "vCPU (SURVEY container, BASELINE.md section 2): 0.55 pairs/s at B=1, "
+                      "0.50 at B=8"}
 
 
-def fps_latency(src, dst, m: int = 1024):
-    """The level-1 FPS (latency-bound, 1023 dependent iterations) against
-    a measured latency floor, on the batch's 2B clouds:
-    * the product kernel's launch time (HIP events) per dependent iteration;
-    * the same kernel with s_memtime stamps around each phase of every iteration (cloud 0's
-      workgroup): the distance scan vs the exchange (wave max + winner pick, LDS hand-off +
-      barrier, block max);
-    * the floor: the same 8-wave workgroup and exchange with 2 points per thread instead of
-      32 (hreg_debug_fps_floor, stamped alike), i.e. the dependent chain alone."""
+def _fps_level(pts, m, weights, floor_call, floor_pts, floor_w, kernel):
+    """one FPS level: the product kernel's launch time (HIP events) per dependent iteration,
+    its s_memtime phase stamps (cloud 0's workgroup), and the floor geometry's stamps"""
     from pcd_reg_hregnet_amd import _lib
-    pts = torch.cat([src, dst], 0).contiguous()
     nb, n, _ = pts.shape
     st_ = _lib.stream_handle()
     idx = torch.empty(nb, m, dtype=torch.int32, device=pts.device)
     temp = torch.empty(nb, n, device=pts.device)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    name = "hreg_weighted_furthest_point_sampling" if weights is not None else "hreg_furthest_point_sampling"
+    args = (nb, n, m, pts, weights, temp, idx, None, st_) if weights is not None else \
+        (nb, n, m, pts, temp, idx, None, st_)
+    _lib.call(name, *args)  # warm
     ev[0].record()
-    _lib.call("hreg_furthest_point_sampling", nb, n, m, pts, temp, idx, None, st_)
+    _lib.call(name, *args)
     ev[1].record()
+    if floor_call is None:  # (clouds above 16384 points: the multi-workgroup cluster kernel)
+        torch.cuda.synchronize()
+        launch_us = ev[0].elapsed_time(ev[1]) * 1e3
+        return {"kernel": kernel, "clouds": nb, "points": n, "dependent_iterations": m - 1,
+                "launch_us": round(launch_us, 1), "us_per_iteration": round(launch_us / (m - 1), 4)}
     stamps = torch.zeros(6, dtype=torch.int64, device=pts.device)
-    _lib.call("hreg_debug_fps_stamps", nb, n, m, pts, None, idx, stamps, st_)
+    _lib.call("hreg_debug_fps_stamps", nb, n, m, pts, weights, idx, stamps, st_)
     floor = torch.zeros(6, dtype=torch.int64, device=pts.device)
-    small = pts[:, :1024].contiguous()
-    _lib.call("hreg_debug_fps_floor", nb, m, small, idx, floor, st_)
+    fidx = torch.empty(nb, m, dtype=torch.int32, device=pts.device)
+    floor_call(floor_pts, floor_w, fidx, floor, st_)
     torch.cuda.synchronize()
     scan, pick, barrier, final, total, ticks = [int(x) for x in stamps.cpu()]
     f_total, f_ticks = int(floor[4]), int(floor[5])
@@ -385,19 +398,136 @@ def fps_latency(src, dst, m: int = 1024):
     per_iter = lambda c, g=ghz: round(c / max(g, 1e-9) / 1e3 / (m - 1), 4)  # noqa: E731
     f_ghz = f_total / (f_ticks * 10.0) if f_ticks else 0.0
     launch_us = ev[0].elapsed_time(ev[1]) * 1e3
-    return {"kernel": "fps_reg_kernel (level 1, 512 threads x 32 points per cloud)",
-            "clouds": nb, "points": n, "dependent_iterations": m - 1,
+    return {"kernel": kernel, "clouds": nb, "points": n, "dependent_iterations": m - 1,
             "launch_us": round(launch_us, 1),
             "us_per_iteration": round(launch_us / (m - 1), 4),
             "stamped_us_per_iteration": per_iter(total),
             "stamped_scan_us_per_iteration": per_iter(scan),
             "stamped_exchange_us_per_iteration": per_iter(pick + barrier + final),
+            "stamped_pick_us": per_iter(pick), "stamped_barrier_us": per_iter(barrier),
+            "stamped_final_us": per_iter(final),
             "floor_us_per_iteration": per_iter(f_total, f_ghz),
             "frac_floor_over_kernel": round(per_iter(f_total, f_ghz) / max(per_iter(total), 1e-9), 3),
-            "clock_ghz": round(ghz, 3),
-            "basis": "floor = the same workgroup and per-iteration exchange with 2 instead of 32 "
-                     "points per thread (hreg_debug_fps_floor); stamped figures carry the "
-                     "s_memtime overhead on both sides"}
+            "clock_ghz": round(ghz, 3)}
+
+
+def fps_latency(src, dst):
+    """The FPS chain of one forward (latency-bound, 1023 + 511 + 255 dependent
+    iterations) against measured latency floors, on the batch's 2B
+    clouds, per level:
+    * the product kernel's launch time (HIP events) per dependent iteration;
+    * the same kernel with s_memtime stamps around each phase of every iteration (cloud 0's
+      workgroup): the distance scan vs the exchange (wave max + winner pick, LDS hand-off +
+      barrier, block max);
+    * the floor: the same workgroup and per-iteration exchange with (almost) no scan --
+      level 1: 2 instead of 32 points per thread (hreg_debug_fps_floor); levels 2 / 3 (WFPS on
+      1024 / 512 points): one weighted point per thread in the level's 4-wave / 1-wave
+      geometry (hreg_debug_wfps_floor), i.e. the dependent chain alone.
+    Levels 2 / 3 run on the first 1024 / 512 points of each cloud with seeded weights in
+    [0.5, 2] (the WFPS cost does not depend on the values)."""
+    from pcd_reg_hregnet_amd import _lib
+    pts = torch.cat([src, dst], 0).contiguous()
+    nb = pts.shape[0]
+    g = torch.Generator(device="cpu").manual_seed(5)
+    out = {"basis": "floor = the same workgroup and per-iteration exchange with (almost) no "
+                    "scan; stamped figures carry the s_memtime overhead on both sides"}
+    if pts.shape[1] <= 16384:
+        out["level1"] = _fps_level(
+            pts, 1024, None,
+            lambda fp, fw, i, s, st: _lib.call("hreg_debug_fps_floor", nb, 1024, fp, i, s, st),
+            pts[:, :1024].contiguous(), None,
+            "fps_reg_kernel<512, 2, 16> (level 1: 512 threads x 32 points per cloud)")
+    else:  # Model_V2's 65536-point clouds: one cloud over up to 64 single-wave workgroups
+        out["level1"] = _fps_level(pts, 1024, None, None, None, None,
+                                   "fps_cluster_kernel (level 1: one cloud over single-wave "
+                                   "workgroups exchanging candidates through L2)")
+    for lvl, n, m, T, kern in ((2, 1024, 512, 256, "fps_reg_kernel<256, 4, 1, weighted> (level 2: 4 waves x 4 points)"),
+                               (3, 512, 256, 64, "fps_reg_kernel<64, 8, 1, weighted> (level 3: 1 wave x 8 points)")):
+        p = pts[:, :n].contiguous()
+        w = (0.5 + 1.5 * torch.rand(nb, n, generator=g)).to(pts.device)
+        fp = pts[:, :T].contiguous()
+        fw = w[:, :T].contiguous()
+        out[f"level{lvl}"] = _fps_level(
+            p, m, w,
+            lambda fp_, fw_, i, s, st, T=T, m=m: _lib.call("hreg_debug_wfps_floor", nb, T, m, fp_, fw_, i, s, st),
+            fp, fw, kern)
+    out["chain_us"] = round(sum(out[f"level{k}"]["launch_us"] for k in (1, 2, 3)), 1)
+    # (the r4 lines' flat fields: level 1)
+    for k in ("us_per_iteration", "frac_floor_over_kernel", "floor_us_per_iteration",
+              "stamped_us_per_iteration"):
+        if k in out["level1"]:
+            out[k] = out["level1"][k]
+    return out
+
+
+def forward_latency(P, src, dst, reps: int = 7):
+    """Single-batch latency (the reference's callers run one batch at a
+    time, test/test_v3.py:82,120): one batch-B forward alone on the device, median of `reps`
+    after 2 warm-ups, (a) launched eagerly (engine.hregnet_forward, host launches) and (b) as
+    the captured graph of a 1-lane GraphPipeline (stage 1 + the rest, two replays)."""
+    from pcd_reg_hregnet_amd import engine
+
+    def med(fn):
+        ts = []
+        for i in range(reps + 2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            if i >= 2:
+                ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3
+    with torch.no_grad():
+        eager = med(lambda: engine.hregnet_forward(P, src, dst))
+        gp = engine.GraphPipeline(P, src, dst, lanes=1)
+        graph = med(lambda: gp.run_forwards(1))
+        del gp
+    B = src.shape[0]
+    return {"batch": B, "eager_ms": round(eager, 3), "graph_ms": round(graph, 3),
+            "pairs_per_s_alone": round(B / graph * 1e3, 1),
+            "basis": f"one batch of {B} pairs alone on the GPU, median of {reps} (synchronised); "
+                     "graph = 1-lane GraphPipeline (stage-1 graph + rest-of-forward graph)"}
+
+
+def in_executor(steps: int, B: int, points: int, entries_flops: dict):
+    """roofline of the level family inside the timed graph executor: the
+    level kernels' mean durations over the timed region's dispatches, from the committed
+    rocprofv3 kernel trace of `bench.py --steps S --warmup W --no-eager-roofline`
+    (tools/in_executor.py -> profiles/r*_in_executor.json, keyed by workload), against the
+    same algorithmic FLOPs per launch as the eager figure.  None when no trace of this
+    workload is committed."""
+    key = f"hregnet:b{B}:n{points}:s{steps}"
+    for rnd in ("r5",):
+        path = os.path.join(REPO, "profiles", f"{rnd}_in_executor.json")
+        try:
+            d = json.load(open(path))[key]
+        except (OSError, KeyError, ValueError):
+            continue
+        t = 0.0
+        fl = 0.0
+        per = {}
+        for kern, us in d["avg_us"].items():
+            f = entries_flops.get(kern)
+            if f is None:
+                return None
+            per[kern] = {"avg_us": us, "tflops": round(f / us / 1e6, 2)}
+            t += us
+            fl += f
+        ach = fl / t / 1e6
+        return {"achieved": round(ach, 3), "frac": round(ach / PEAK_B6_TFLOPS, 4),
+                "per_kernel": per, "source": os.path.relpath(path, REPO),
+                "dispatches": d.get("dispatches"), "tree": d.get("tree")}
+    return None
+
+
+def provenance() -> dict:
+    """HREG_SWITCHES / HREG_LIB of this run, and the timing probes among them (a line with
+    probes is marked: it is not a measurement)"""
+    from pcd_reg_hregnet_amd import switches
+    out = switches.provenance()
+    if switches.probes():
+        out["PROBES_ACTIVE_NOT_A_MEASUREMENT"] = switches.probes()
+    return out
 
 
 def shard_batch(rank: int, pairs: int, points: int):
@@ -480,7 +610,12 @@ def bench_train(args, world, rank, device):
     # the step replayed from captured HIP graphs (trainer.GraphTrainer; bitwise the eager
     # step, tests/test_gpu_train_capture.py); with world > 1 the bucket all-reduce (RCCL) is
     # captured inside the graph
-    graphed = not args.train_eager and (world == 1 or dist.get_backend() == "nccl")
+    # With world > 1 the captured RCCL all-reduce path runs only when asked for
+    # (--train-graph-ddp): its one hardware execution so far is the 1-rank test
+    # (tests/test_gpu_train_ddp.py::test_graph_trainer_rccl_world1), so the default multi-GPU
+    # line keeps the eager DDP step the earlier rounds measured.  step_path records which ran.
+    graphed = not args.train_eager and (world == 1 or (args.train_graph_ddp and
+                                                       dist.get_backend() == "nccl"))
     eager_tr = tr
     if graphed:
         gtr = trainer.GraphTrainer(tr, B, args.points)
@@ -540,6 +675,11 @@ def bench_train(args, world, rank, device):
                        "parallelism": f"dp{world} (one 9.87 MB gradient all-reduce per step)"},
             "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
             "executor": "HIP graphs (two captured steps, ping-pong inputs)" if graphed else "eager",
+            "step_path": ("GraphTrainer (captured step" + (", RCCL all-reduce captured in the graph)"
+                                                          if world > 1 else ", no collective at world 1)")
+                          if graphed else "Trainer (eager step" + (
+                              ", RCCL all-reduce launched eagerly)" if world > 1 else ")")),
+            "provenance": provenance(),
             "roofline": {"kernel": "fp32 MFMA GEMM family of the step (forward, input- and "
                                    "weight-gradient GEMMs)",
                          "timing": ("HIP events on the launch stream, instrumented eager pass of the "
@@ -624,6 +764,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train-eager", action="store_true",
                     help="--model train: launch the step eagerly instead of replaying captured graphs")
+    ap.add_argument("--train-graph-ddp", action="store_true",
+                    help="--model train with --gpus > 1: replay the captured step with the RCCL "
+                         "all-reduce inside the graph (default: the eager DDP step)")
+    ap.add_argument("--no-eager-roofline", action="store_true",
+                    help="skip the instrumented eager pass after the timed graph region (the "
+                         "rocprofv3 trace run behind roofline.in_executor: the timed replays are "
+                         "then the last level-kernel dispatches of the run)")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the single-batch latency entry")
+    ap.add_argument("--allow-probes", action="store_true",
+                    help="run with PROBE_* timing switches set (results change: the line is "
+                         "marked as a probe, never a measurement)")
     ap.add_argument("--executor", choices=("graph", "pipeline", "serial"), default="graph",
                     help="graph: pipelined forward replayed as HIP graphs; pipeline: same "
                          "eagerly; serial: no cross-batch overlap")
@@ -687,6 +839,10 @@ def main():
         print(f"bench: --steps {args.steps} is not a multiple of --lanes {args.lanes}; "
               f"using {lanes} lanes", file=sys.stderr)
         args.lanes = lanes
+    from pcd_reg_hregnet_amd import switches
+    if switches.probes() and not args.allow_probes:
+        raise SystemExit(f"bench: timing probes {switches.probes()} are set in HREG_SWITCHES "
+                         "(they skip or repeat work: no measurement); --allow-probes to run them")
     world, rank, local = init_world(args)
     device = torch.device("cuda", local)
 
@@ -758,7 +914,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if args.executor == "graph":
+    if args.executor == "graph" and not args.no_eager_roofline:
         timer.enabled = True
         with torch.no_grad():
             pipe.run([(src, dst)] * args.steps)
@@ -791,7 +947,8 @@ def main():
         # the family's peak: its FLOPs over the time they need at each kernel's own peak
         t_peak = sum(e["_flops"] / (e["peak"] * 1e12) for e in lev.values())
         peak = sum(e["_flops"] for e in lev.values()) / t_peak / 1e12 if t_peak else PEAK_B6_TFLOPS
-        traffic, traffic_src = pmc_traffic(" + ".join(level_names))
+        traffic, traffic_src = pmc_traffic(" + ".join(level_names),
+                                           f"{args.model}:b{B}:n{args.points}")
         tot_ms = sum(r[0] for r in res.values())
         tot_xf = sum(r[4] for r in res.values())
         alg_fl = ALG_GFLOP_PER_PAIR * 1e9 * B * args.steps
@@ -826,12 +983,24 @@ def main():
                              "tflops": round(alg_fl / max(tot_ms, 1e-9) / 1e9, 2),
                              "executed_gflop_per_pair": round(tot_xf / args.steps / B / 1e9, 3),
                              "executed_tflops": round(tot_xf / max(tot_ms, 1e-9) / 1e9, 2)}}
+        # level-kernel FLOPs per launch at this batch (groups = 2B clouds x the level's
+        # keypoints), by rocprof kernel name: the in-executor figure's numerators
+        lv_fl = {level_kernel(engine, 1): L1_FLOPS_PER_GROUP * 2 * B * engine.LEVELS[0][0],
+                 level_kernel(engine, 2): L2_FLOPS_PER_GROUP * 2 * B * engine.LEVELS[1][0],
+                 level_kernel(engine, 3): L3_FLOPS_PER_GROUP * 2 * B * engine.LEVELS[2][0]}
+        if not v2 and args.executor == "graph":
+            roof["in_executor"] = in_executor(args.steps, B, args.points, lv_fl)
         fps = None
-        if not v2:
+        try:
+            fps = fps_latency(src, dst)
+        except Exception as e:  # a diagnostic must never sink the GPU number
+            fps = {"error": repr(e)}
+        lat = None
+        if not v2 and not args.no_latency:
             try:
-                fps = fps_latency(src, dst)
+                lat = forward_latency(P, src, dst)
             except Exception as e:  # a diagnostic must never sink the GPU number
-                fps = {"error": repr(e)}
+                lat = {"error": repr(e)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not v2:
             try:
@@ -866,7 +1035,9 @@ def main():
                        "parallelism": f"dp{world} (pairs sharded, no collective)"},
             "roofline": roof,
             "fps": fps,
+            "latency": lat,
             "cpu_baseline": cpu,
+            "provenance": provenance(),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -350,8 +350,9 @@ int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, float *mean
  * sum_k A[r][k] W'[n][k] + shift[n]) with W' = W [N][K] (w_trans 0) or the transpose of
  * W [K][N] (w_trans 1); scale / shift may be NULL (1 / 0), act = ReLU if relu.  The same
  * fp32 sums as hreg_gemm (same k-order).  K, N, lda, ldo multiples of 4, 16-byte aligned
- * pointers; hreg_ts_gemm_supported(R, K, N) != 0 when W' fits the kernel's LDS. */
-int hreg_ts_gemm_supported(int R, int K, int N);
+ * pointers; hreg_ts_gemm_supported(R, K, N, 0) != 0 when W' fits the kernel's LDS
+ * (stats 1: with hreg_ts_gemm_bn's statistics buffers as well). */
+int hreg_ts_gemm_supported(int R, int K, int N, int stats);
 int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
                  const float *scale, const float *shift, int relu, float *out, int ldo, void *stream);
 /* hreg_ts_gemm (no scale / activation) with the output's train-mode BatchNorm statistics
@@ -633,6 +634,10 @@ int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float 
                           int32_t *idx, uint64_t *stamps, void *stream);
 /* Latency floor of the level-1 FPS geometry: the same 8-wave workgroup and per-iteration
  * exchange, 2 points per thread (n = 1024); points [b][1024][3], stamps[6] as above. */
+/* Diagnostic: the latency floor of the level-2 (T = 256) / level-3 (T = 64) WFPS geometry: T
+ * threads, one weighted point each (n = T); stamps as hreg_debug_fps_stamps. */
+int hreg_debug_wfps_floor(int b, int T, int m, const float *points, const float *weights,
+                          int32_t *idx, uint64_t *stamps, void *stream);
 int hreg_debug_fps_floor(int b, int m, const float *points, int32_t *idx, uint64_t *stamps,
                          void *stream);
 

@@ -15,6 +15,9 @@ from .utils import (furthest_point_sample, weighted_furthest_point_sample,  # no
 from .knn import knn_points, knn_gather  # noqa: F401
 from .losses import transformation_loss, calc_rot_rre_err, calc_tran_rte_err  # noqa: F401
 from . import point_utils_cuda  # noqa: F401
+from . import train as _train, trainer as _trainer, switches as _switches  # noqa: F401
+
+_switches.check()  # every module that declares switches is imported by now
 
 __all__ = ["HRegNet", "HierFeatureExtraction", "Model_V2", "furthest_point_sample",
            "weighted_furthest_point_sample", "gather_operation", "set_seed", "calc_error_np",

@@ -13,6 +13,8 @@ import os
 
 import torch
 
+from . import switches
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # HREG_LIB: an alternative build of the same library (A/B timing experiments only)
 LIB_PATH = os.environ.get("HREG_LIB") or os.path.join(_HERE, "libhregnet_amd.so")
@@ -113,6 +115,7 @@ _SIGS = {
     "hreg_relu_bwd": [_vp, _vp, ctypes.c_size_t, _vp, _vp],
     "hreg_debug_fps_stamps": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_debug_fps_floor": [_i, _i, _vp, _vp, _vp, _vp],
+    "hreg_debug_wfps_floor": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_debug_fps_cluster": [_i, _i, _i, _vp, _vp, _vp, _vp, _i, ctypes.c_uint, _vp],
     "hreg_device_status": [ctypes.POINTER(ctypes.c_int), _i],
     "hreg_bn_stats": [_vp, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
@@ -122,7 +125,7 @@ _SIGS = {
     "hreg_col_sum": [_vp, _i, _i, _vp, _vp, _i, _vp],
     "hreg_gemm_tn": [_vp, _i, _vp, _i, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp],
     "hreg_debug_gemm_tn_s": [_vp, _i, _vp, _i, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp, _i],
-    "hreg_ts_gemm_supported": [_i, _i, _i],
+    "hreg_ts_gemm_supported": [_i, _i, _i, _i],
     "hreg_ts_gemm": [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _vp],
     "hreg_ts_gemm_bn": [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, ctypes.c_float, ctypes.c_float, _vp,
                         _vp, _vp, _vp, _vp, _vp, _vp],
@@ -263,10 +266,11 @@ def stream_handle() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-# timing probe (tools/train_probe.sh only): the entries named in HREG_PROBE_TWICE run twice per
-# call, so a run's extra wall time is that kernel family's cost under the step's stream overlap
-# (results change -- accumulating entries add twice -- so no test sets it)
-_TWICE = frozenset(filter(None, os.environ.get("HREG_PROBE_TWICE", "").split(",")))
+# timing probe (tools/train_probe.sh only): the entries named in HREG_SWITCHES=PROBE_TWICE=a+b
+# run twice per call, so a run's extra wall time is that kernel family's cost under the step's
+# stream overlap (results change -- accumulating entries add twice -- so no test sets it, and
+# bench.py refuses to report a measurement with it set)
+_TWICE = frozenset(filter(None, switches.text("PROBE_TWICE").split("+")))
 
 
 def call(name: str, *args) -> None:

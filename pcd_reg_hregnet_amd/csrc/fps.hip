@@ -690,6 +690,29 @@ extern "C" int hreg_debug_fps_floor(int b, int m, const float *points, int32_t *
     return HREG_OK;
 }
 
+// Diagnostic: the latency floor of a WFPS level's geometry -- T threads
+// with one point each (n = T, bs = T, G = QT = 1: the same waves, per-iteration wave reduction,
+// LDS hand-off + barrier (T > 64) and block reduction as the level's kernel, almost no scan and
+// a one-slot pick), weighted.  T = 256: level 2's 4-wave workgroup (n = 1024 runs
+// fps_reg_kernel<256, 4, 1, true>); T = 64: level 3's single wave (n = 512:
+// fps_reg_kernel<64, 8, 1, true>).  points [b][T][3], weights [b][T]; stamps as
+// hreg_debug_fps_stamps.
+extern "C" int hreg_debug_wfps_floor(int b, int T, int m, const float *points, const float *weights,
+                                     int32_t *idx, uint64_t *stamps, void *stream) {
+    if (b <= 0 || m <= 0 || !points || !weights || !idx || !stamps) return HREG_ERR_INVALID;
+    hipStream_t st = as_stream(stream);
+    if (T == 256)
+        hipLaunchKernelGGL((fps_reg_kernel<256, 1, 1, true, true>), dim3(b), dim3(256), 0, st, points, weights,
+                           nullptr, idx, nullptr, 256, m, 256, 8, __builtin_huge_valf(), stamps);
+    else if (T == 64)
+        hipLaunchKernelGGL((fps_reg_kernel<64, 1, 1, true, true>), dim3(b), dim3(64), 0, st, points, weights,
+                           nullptr, idx, nullptr, 64, m, 64, 6, __builtin_huge_valf(), stamps);
+    else
+        return HREG_ERR_UNSUPPORTED;
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
 extern "C" int hreg_furthest_point_sampling(int b, int n, int m, const float *points,
                                             float *temp, int32_t *idx, float *sampled_xyz,
                                             void *stream) {

@@ -247,9 +247,10 @@ int hreg_bn_finalize_stats(const double *part, int S, int R, int C, float eps, f
                            float *var_unbiased, float momentum, float *running_mean, float *running_var,
                            hipStream_t st);
 
-extern "C" int hreg_ts_gemm_supported(int R, int K, int N) {
-    // (the A extent is addressed through a buffer descriptor: < 2 GB)
-    return R > 0 && K > 0 && N > 0 && (K & 3) == 0 && (N & 3) == 0 && ts_nt(K, N, true) > 0 &&
+extern "C" int hreg_ts_gemm_supported(int R, int K, int N, int stats) {
+    // (the A extent is addressed through a buffer descriptor: < 2 GB); stats: the budget of
+    // hreg_ts_gemm_bn (16 more floats of LDS per column), else the plain kernel's own
+    return R > 0 && K > 0 && N > 0 && (K & 3) == 0 && (N & 3) == 0 && ts_nt(K, N, stats != 0) > 0 &&
            (size_t)R * K * sizeof(float) < ((size_t)1 << 31);
 }
 

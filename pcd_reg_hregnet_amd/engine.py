@@ -1468,6 +1468,47 @@ class Pipeline:
         return outs
 
 
+# GPU_MAX_HW_QUEUES (HIP's hardware queues per process, default 4) the graph executor has run
+# on: 4, 8 and 16 (DESIGN.md section 10, r4 queue sweep).  With 2 the r4 bench process died in
+# the HIP runtime (core dump, gpurun_out/hwq/q2.s20.1.err) while replaying a round of 20 lanes
+# whose graph forks 2 x 20 + 1 streams (lane stream, front stream, the batched stage-1 stream).
+# Nothing in the graph needs more than one queue for correctness (every cross-stream order is a
+# graph edge), so the crash is the runtime's, not a dependency the graph leaves to queue
+# order; what the executor can do is not walk into it: fewer queues than MIN_HW_QUEUES are
+# refused up front with this error instead of a segfault mid-replay.
+MIN_HW_QUEUES = 4
+
+
+def hw_queues(env=None) -> int:
+    """GPU_MAX_HW_QUEUES as the HIP runtime reads it (unset or invalid: its default 4)."""
+    import os
+    v = (os.environ if env is None else env).get("GPU_MAX_HW_QUEUES", "")
+    try:
+        q = int(v)
+    except ValueError:
+        return 4
+    return q if q > 0 else 4
+
+
+def check_hw_queues(streams: int, env=None) -> int:
+    """Refuse a graph executor whose fork width (``streams`` concurrent streams per replay)
+    would run on fewer hardware queues than have been measured to work; -> the queue count."""
+    q = hw_queues(env)
+    if q < MIN_HW_QUEUES and streams > 1:
+        raise RuntimeError(
+            f"GraphPipeline: GPU_MAX_HW_QUEUES={q} with {streams} forked streams per replay; the "
+            f"graph executor runs on >= {MIN_HW_QUEUES} hardware queues (measured 4, 8, 16; 2 "
+            "crashed the HIP runtime in r4). Unset GPU_MAX_HW_QUEUES or set it to 4.")
+    return q
+
+
+def fork_width(lanes: int, batched_stage1: bool, front_two_streams: bool) -> int:
+    """Streams one replay of the executor forks: a stream per lane (lane 0 the capture
+    stream), a second per lane for the front half (FRONT_ORDER 3), and the stage-1 side
+    stream(s) -- one batched, or one per lane."""
+    return lanes * (2 if front_two_streams else 1) + (1 if batched_stage1 else lanes)
+
+
 class GraphPipeline:
     """The pipelined forward captured as HIP graphs (kernel boundaries ~1.5 us
     instead of a host launch each).
@@ -1514,6 +1555,8 @@ class GraphPipeline:
         # multi-workgroup FPS spins every participant of a launch, and one batched launch
         # measured slower: 803 vs 844 pairs/s)
         self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1 and N <= 16384
+        check_hw_queues(fork_width(lanes, self.bs1, FRONT_STREAM and FRONT_ORDER == 3 and self.bs1
+                                   and not v2 and lanes <= FRONT_STREAM_MAX_LANES))
         if self.bs1:
             self.src_all = src.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
             self.dst_all = dst.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()

@@ -190,7 +190,7 @@ def _conv_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None,
     N = W.shape[1] if w_trans else W.shape[0]
     lib = _lib.load()
     if (TS_GEMM and R >= TS_MIN_ROWS and x.is_contiguous() and W.is_contiguous()
-            and lib.hreg_ts_gemm_supported(R, K, N)):
+            and lib.hreg_ts_gemm_supported(R, K, N, 0)):
         out = torch.empty(R, N, device=x.device)
         _lib.call("hreg_ts_gemm", x, K, R, K, W, 1 if w_trans else 0, N, None,
                   None if shift is None else shift.contiguous(), 0, out, N, _stream())
@@ -208,7 +208,7 @@ def _conv_gemm_bn(x, W, shift, eps, momentum, running_mean, running_var):
     N = W.shape[0]
     lib = _lib.load()
     if not (TS_GEMM and TS_BN and R >= TS_MIN_ROWS and x.is_contiguous() and W.is_contiguous()
-            and lib.hreg_ts_gemm_supported(R, K, N)):
+            and lib.hreg_ts_gemm_supported(R, K, N, 1)):
         return None
     dev = x.device
     y = torch.empty(R, N, device=dev)
@@ -391,6 +391,14 @@ class GradBucket:
             for p, v in zip(self.params, self.views1):
                 p._grad_side1 = v
 
+    @staticmethod
+    def direct_off():
+        """Turn the direct parameter gradients off (idempotent).  The trainers call it in a
+        ``finally`` after ``attach``, so a forward / backward that raises between ``attach``
+        and ``collect`` cannot leave them on for later autograd calls."""
+        global _DIRECT_ON
+        _DIRECT_ON = False
+
     def collect(self, two_sides: bool = False):
         """Copy gradients that autograd allocated separately into the buffer; two_sides (after a
         two-stream step): add the second buffer (side-1 gradients) into it.  Turns the direct
@@ -408,8 +416,11 @@ class GradBucket:
                 raise RuntimeError("GradBucket: two_sides needs sides=2")
             _lib.call("hreg_add_into", self.flat1, self.flat, self.flat.numel(), _stream())
 
-    def all_reduce_mean(self, group=None):
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    def all_reduce_mean(self, group=None, force: bool = False):
+        """SUM over the ranks, then / world.  At world 1 it is skipped unless ``force`` (the
+        1-rank RCCL test issues the collective, captured, on the one GPU a box has)."""
+        up = dist.is_available() and dist.is_initialized()
+        if up and (force or dist.get_world_size(group) > 1):
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
             self.flat.div_(dist.get_world_size(group))
         return self.flat

@@ -94,7 +94,8 @@ class Level1Prefetch:
     seen: pass a fresh tensor, or call ``discard()``, after such a write."""
 
     def __init__(self, device):
-        self.stream = torch.cuda.Stream(device=device)
+        # (no side stream for a CPU trainer: the host-logic tests build one around stubs)
+        self.stream = torch.cuda.Stream(device=device) if torch.device(device).type == "cuda" else None
         self.key = None
         self.prepared = None
         self.event = None
@@ -150,22 +151,27 @@ class Level1Prefetch:
         return prepared
 
 
-def ddp_average(bucket: GradBucket, group=None) -> None:
+def ddp_average(bucket: GradBucket, group=None, force: bool = False) -> None:
     """DistributedDataParallel's gradient averaging for one step: ONE all_reduce (SUM) of the
     whole flat bucket (every parameter's gradient in FlatParams order), then / world -- a no-op
-    in a single process.  Trainer.step and the captured GraphTrainer step both call exactly
-    this (tests/test_distributed.py counts the collectives)."""
-    bucket.all_reduce_mean(group)
+    in a single process unless ``force`` (Trainer(always_reduce=True): the collective runs at
+    world 1 too, so the captured RCCL node is exercised on a one-GPU box).  Trainer.step and
+    the captured GraphTrainer step both call exactly this (tests/test_distributed.py counts the
+    collectives of a real Trainer.step on gloo)."""
+    bucket.all_reduce_mean(group, force=force)
 
 
 class Trainer:
     """``step(src, dst, gt_R, gt_t)`` = one train_reg_v0 iteration on this rank's shard.
     ``next_batch=(src, dst)`` starts the next batch's level-1 grouping on a side stream."""
 
-    def __init__(self, net, lr=1e-3, alpha=1.0, group=None):
+    def __init__(self, net, lr=1e-3, alpha=1.0, group=None, always_reduce: bool = False):
         self.net = net.train()
         self.alpha = alpha
         self.group = group
+        # issue the bucket all-reduce even in a 1-rank process group (tests: the RCCL node of
+        # the captured step on a one-GPU box); the sum over one rank / 1 is the identity
+        self.always_reduce = always_reduce
         self.params = FlatParams(net.parameters())
         self.params.broadcast(0, group)
         self.bucket = GradBucket(self.params.params, sides=2)
@@ -184,7 +190,7 @@ class Trainer:
             self.prefetch.start(*next_batch)
         hook = train_graph.IndexHook(prepared=prepared) if prepared else None
         out = self.local_gradients(src, dst, gt_R, gt_t, hook)
-        ddp_average(self.bucket, self.group)
+        ddp_average(self.bucket, self.group, force=self.always_reduce)
         self.opt.step()
         return out
 
@@ -194,13 +200,16 @@ class Trainer:
         backward into the gradient bucket -- everything before DDP's all-reduce.  hook: an
         IndexHook (prepared / injected selections).  -> (loss, l_R, l_t), detached."""
         self.bucket.attach()                     # optimizer.zero_grad()
-        two = TWO_STREAM and src.is_cuda
-        ret = train_graph.hregnet_train_forward(self.net, src, dst, hook, concurrent=two)
-        loss, l_R, l_t = train_graph.registration_loss(ret, gt_R, gt_t, self.alpha)
-        loss.backward()
-        if two:
-            train_graph.join_side_stream(src.device)
-        self.bucket.collect(two_sides=two)
+        try:
+            two = TWO_STREAM and src.is_cuda
+            ret = train_graph.hregnet_train_forward(self.net, src, dst, hook, concurrent=two)
+            loss, l_R, l_t = train_graph.registration_loss(ret, gt_R, gt_t, self.alpha)
+            loss.backward()
+            if two:
+                train_graph.join_side_stream(src.device)
+            self.bucket.collect(two_sides=two)
+        finally:
+            GradBucket.direct_off()
         return loss.detach(), l_R.detach(), l_t.detach()
 
 
@@ -236,7 +245,9 @@ class GraphTrainer:
 
     def __init__(self, trainer: "Trainer", batch: int, points: int):
         self.world = _dist_world(trainer.group)
-        if self.world > 1 and dist.get_backend(trainer.group) != "nccl":
+        collective = self.world > 1 or (trainer.always_reduce and dist.is_available()
+                                        and dist.is_initialized())
+        if collective and dist.get_backend(trainer.group) != "nccl":
             # RCCL collectives are captured into the graph (the bucket all-reduce is a graph
             # node on the step's stream); gloo's host-side collectives cannot be
             raise NotImplementedError("GraphTrainer with world > 1 needs the nccl (RCCL) backend; "
@@ -302,15 +313,20 @@ class GraphTrainer:
         with torch.cuda.stream(self.side):
             self._sel_into(1 - k)
         tr.bucket.attach()
-        hook = train_graph.IndexHook(prepared=self.sel[k])
-        two = TWO_STREAM
-        ret = train_graph.hregnet_train_forward(tr.net, self.src[k], self.dst[k], hook, concurrent=two)
-        loss, l_R, l_t = train_graph.registration_loss(ret, self.gR[k], self.gt[k], tr.alpha)
-        loss.backward()
-        if two:
-            train_graph.join_side_stream(self.src[k].device)
-        tr.bucket.collect(two_sides=two)
-        ddp_average(tr.bucket, tr.group)  # world > 1: the RCCL all-reduce, captured
+        try:
+            hook = train_graph.IndexHook(prepared=self.sel[k])
+            two = TWO_STREAM
+            ret = train_graph.hregnet_train_forward(tr.net, self.src[k], self.dst[k], hook,
+                                                    concurrent=two)
+            loss, l_R, l_t = train_graph.registration_loss(ret, self.gR[k], self.gt[k], tr.alpha)
+            loss.backward()
+            if two:
+                train_graph.join_side_stream(self.src[k].device)
+            tr.bucket.collect(two_sides=two)
+        finally:
+            GradBucket.direct_off()
+        # world > 1 (or always_reduce): the RCCL all-reduce, captured
+        ddp_average(tr.bucket, tr.group, force=tr.always_reduce)
         opt = tr.opt
         _lib.call("hreg_adam_step_dev", opt.p, opt.g, opt.m, opt.v, opt.p.numel(), float(opt.lr),
                   float(opt.betas[0]), float(opt.betas[1]), float(opt.eps), self.scal,

@@ -105,7 +105,7 @@ def test_ts_gemm_bitwise_equals_gemm(R, K, N, w_trans):
     x = torch.randn(R, K, generator=g).cuda()
     W = (torch.randn(N, K, generator=g) / K ** 0.5).cuda()
     b = torch.randn(N, generator=g).cuda()
-    assert _lib.load().hreg_ts_gemm_supported(R, K, N)
+    assert _lib.load().hreg_ts_gemm_supported(R, K, N, 0)
     ref = train._plain_gemm(x, W, b)
     Wl = W.t().contiguous() if w_trans else W  # [K][N]: the dx GEMM's layout
     out = torch.empty(R, N, device="cuda")

@@ -168,3 +168,68 @@ def test_ddp_step_matches_reference_shards():
     print(f"\npost-Adam parameters: {checked} leading entries compared (max |diff| {worst:.2e}), "
           f"{ambiguous} entries below their gradient's error bar or rounding noise skipped")
     assert checked > ambiguous
+
+
+def test_graph_trainer_rccl_world1():
+    """the captured RCCL all-reduce, executed.  A 1-rank ``nccl`` (RCCL)
+    process group on the box's one GPU; ``Trainer(always_reduce=True)`` issues the bucket's
+    all-reduce even at world 1, so ``GraphTrainer`` captures it as a node of the step graph
+    between the backward and Adam (the path ``bench.py --model train --gpus N --train-graph-ddp``
+    replays at N > 1).  Replayed steps against the eager world-1 trainer with no collective: the
+    same losses, parameters, Adam moments and BN buffers, bitwise (a sum over one rank and a
+    division by 1 are exact).  The collective calls are counted: one per eager step, one per
+    capture of the body (a replay re-runs the node without a host call)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from test_gpu_train_capture import _batches, _trainer
+    from pcd_reg_hregnet_amd import _lib, trainer
+    _lib.load()
+    assert not dist.is_initialized()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    calls = []
+    orig = dist.all_reduce
+
+    def counting(t, *a, **k):
+        calls.append(t.numel())
+        return orig(t, *a, **k)
+    try:
+        B, n = 2, 4096
+        batches = _batches(B, n, 4)
+        plain = _trainer()
+        red = _trainer()
+        red.always_reduce = True
+        dist.all_reduce = counting
+        # eager: the collective runs once per step
+        le = [plain.step(*batches[0])[0].clone()]
+        lr_ = [red.step(*batches[0])[0].clone()]
+        torch.cuda.synchronize()
+        assert calls == [red.bucket.flat.numel()], calls
+        assert torch.equal(le[0], lr_[0]) and torch.equal(plain.params.flat, red.params.flat)
+        calls.clear()
+        gt = trainer.GraphTrainer(red, B, n)
+        gt.capture(*batches[1])
+        n_capture = len(calls)
+        # two eager warm-up bodies + the two captured bodies
+        assert n_capture == 4, calls
+        for i in range(1, 4):
+            nxt = batches[i + 1][:2] if i + 1 < 4 else None
+            le.append(plain.step(*batches[i], next_batch=nxt)[0].clone())
+            lr_.append(gt.step(*batches[i], next_batch=nxt)[0].clone())
+        torch.cuda.synchronize()
+        assert len(calls) == n_capture  # replays issue no host-side collective call
+    finally:
+        dist.all_reduce = orig
+        dist.destroy_process_group()
+    print("eager", [float(x) for x in le], "rccl graph", [float(x) for x in lr_])
+    for a, b in zip(le, lr_):
+        assert torch.equal(a, b)
+    assert torch.equal(plain.params.flat, red.params.flat)
+    assert torch.equal(plain.opt.m, red.opt.m) and torch.equal(plain.opt.v, red.opt.v)
+    for (na, a), (_, b) in zip(plain.net.named_buffers(), red.net.named_buffers()):
+        assert torch.equal(a, b), na

@@ -349,3 +349,21 @@ def test_bench_entry_peaks():
     for name in set(bench.MFMA_ENTRIES) | {"hreg_gemm", "hreg_gemm6"}:
         want = bench.PEAK_B6_TFLOPS if name in b6 else bench.PEAK_FP32_MFMA_TFLOPS
         assert bench.entry_peak(name) == want, name
+
+
+def test_graph_executor_refuses_too_few_hw_queues():
+    """the graph executor refuses GPU_MAX_HW_QUEUES below 4 (2 crashed the
+    HIP runtime in r4's 20-lane replay) with a clear error before any capture; unset, invalid
+    and the measured 4 / 8 / 16 pass; a single-stream executor is not affected."""
+    import pytest
+    from pcd_reg_hregnet_amd import engine
+    w = engine.fork_width(20, True, True)
+    assert w == 41
+    assert engine.fork_width(4, False, False) == 8
+    for env in ({}, {"GPU_MAX_HW_QUEUES": "4"}, {"GPU_MAX_HW_QUEUES": "16"},
+                {"GPU_MAX_HW_QUEUES": "x"}):
+        assert engine.check_hw_queues(w, env) >= 4
+    for q in ("1", "2", "3"):
+        with pytest.raises(RuntimeError, match="GPU_MAX_HW_QUEUES"):
+            engine.check_hw_queues(w, {"GPU_MAX_HW_QUEUES": q})
+    assert engine.check_hw_queues(1, {"GPU_MAX_HW_QUEUES": "2"}) == 2
