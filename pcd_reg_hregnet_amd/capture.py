@@ -78,11 +78,15 @@ def guard(origin, stream_cls=None, event_cls=None):
 
 
 @contextlib.contextmanager
-def graph(g, pool=None):
+def graph(g, pool=None, capture_error_mode="global"):
     """``torch.cuda.graph(g, pool)`` with the fork/join guard on its capture stream.  (r4: an
     explicit hipGraphUpload after each capture made the driver's --steps 20 line 2.5 % slower,
-    6853 / 6823 / 6998 vs 7041 / 7034 / 7071 pairs/s on one box, and was removed.)"""
+    6853 / 6823 / 6998 vs 7041 / 7034 / 7071 pairs/s on one box, and was removed.)
+    capture_error_mode "thread_local": other threads' HIP calls stay legal during the capture --
+    the RCCL process group's watchdog thread queries its work events at any time, and in the
+    default global mode that query fails the capture and the watchdog terminates the process
+    ("operation not permitted when stream is capturing", r5's 1-rank RCCL test)."""
     import torch
-    with torch.cuda.graph(g, pool=pool):
+    with torch.cuda.graph(g, pool=pool, capture_error_mode=capture_error_mode):
         with guard(torch.cuda.current_stream()):
             yield

@@ -35,6 +35,14 @@
 #ifndef HREG_FPS_MAX3
 #define HREG_FPS_MAX3 1  // one v_max3_f32 per slot pair in the scan (A/B: 0, two v_med3)
 #endif
+// The winner's coordinates by a uniform-index register read (r5): the slot coordinates live in
+// one ext_vector per axis (a contiguous VGPR tuple), so VX[sl] with the wave-uniform slot sl
+// is s_set_gpr_idx_on + v_mov + s_set_gpr_idx_off, then v_readlane -- instead of a log2(S)-deep
+// tree of uniform branches (whose structurised Flow blocks were ~0.2-0.4 us of every
+// iteration).  A/B: 0 keeps the branch tree.
+#ifndef HREG_FPS_MOVREL
+#define HREG_FPS_MOVREL 1
+#endif
 
 namespace {
 
@@ -72,18 +80,59 @@ __device__ __forceinline__ uint64_t stamp() {
     return t;
 }
 
-// Binary branch tree over a wave-uniform slot index -> three v_readlane.
+// Binary branch tree over a wave-uniform slot index -> three v_readlane (the cluster kernel:
+// its coordinates as packed pairs, which keep it at 129 VGPRs; one tuple per axis took 159)
 template <int LO, int HI, int N2>
-__device__ __forceinline__ void pick_slot(int sl, int wl, const f2 (&PX)[N2], const f2 (&PY)[N2],
-                                          const f2 (&PZ)[N2], float &x, float &y, float &z) {
+__device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N2], const f2 (&PY)[N2],
+                                                const f2 (&PZ)[N2], float &x, float &y, float &z) {
     if constexpr (HI - LO == 1) {
         x = readlane_f(PX[LO / 2][LO % 2], wl);
         y = readlane_f(PY[LO / 2][LO % 2], wl);
         z = readlane_f(PZ[LO / 2][LO % 2], wl);
     } else {
         constexpr int MID = (LO + HI) / 2;
-        if (sl < MID) pick_slot<LO, MID>(sl, wl, PX, PY, PZ, x, y, z);
-        else pick_slot<MID, HI>(sl, wl, PX, PY, PZ, x, y, z);
+        if (sl < MID) pick_slot_pairs<LO, MID>(sl, wl, PX, PY, PZ, x, y, z);
+        else pick_slot_pairs<MID, HI>(sl, wl, PX, PY, PZ, x, y, z);
+    }
+}
+
+// HREG_FPS_PAIRMASK (r5): the lane's first slot of its maximum found over the pair maxima
+// (16 compares at 32 slots instead of 32), then, for the winning lane only, the pair's x / y
+// slot by one uniform-index register read of the temps.  A/B: 0 keeps the per-slot mask.
+#ifndef HREG_FPS_PAIRMASK
+#define HREG_FPS_PAIRMASK 0
+#endif
+
+// per-axis slot coordinates of a thread: one contiguous VGPR tuple
+template <int N>
+struct SlotVec {
+    typedef float type __attribute__((ext_vector_type(N)));
+};
+
+// slot pair s of a coordinate tuple as a packed pair (subregisters: no moves)
+template <class V>
+__device__ __forceinline__ f2 pair_of(const V &v, int s) {
+    return f2{v[2 * s], v[2 * s + 1]};
+}
+
+// The winner's coordinates: slot sl (wave-uniform) of lane wl.  HREG_FPS_MOVREL: one indexed
+// register read per axis (s_set_gpr_idx_on) + v_readlane; else a binary tree of uniform
+// branches down to the slot.
+template <int LO, int HI, class V>
+__device__ __forceinline__ void pick_slot(int sl, int wl, const V &VX, const V &VY, const V &VZ, float &x,
+                                          float &y, float &z) {
+    if constexpr (HREG_FPS_MOVREL) {
+        x = readlane_f(VX[sl], wl);
+        y = readlane_f(VY[sl], wl);
+        z = readlane_f(VZ[sl], wl);
+    } else if constexpr (HI - LO == 1) {
+        x = readlane_f(VX[LO], wl);
+        y = readlane_f(VY[LO], wl);
+        z = readlane_f(VZ[LO], wl);
+    } else {
+        constexpr int MID = (LO + HI) / 2;
+        if (sl < MID) pick_slot<LO, MID>(sl, wl, VX, VY, VZ, x, y, z);
+        else pick_slot<MID, HI>(sl, wl, VX, VY, VZ, x, y, z);
     }
 }
 
@@ -112,7 +161,8 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
     const float *P = xyz + (size_t)cloud * n * 3;
     const float *W = WEIGHTED ? wts + (size_t)cloud * n : nullptr;
 
-    f2 PX[S2], PY[S2], PZ[S2], PT[S2], PW[S2];
+    typename SlotVec<2 * S2>::type VX, VY, VZ, VT;  // VT: the running minima ("temp")
+    f2 PW[S2];
 #pragma unroll
     for (int s = 0; s < 2 * S2; ++s) {
         const int g = s / QT, i = s % QT;
@@ -120,19 +170,19 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         const int k = (int)bitrev_bits((uint32_t)rp, L) + i * bs;
         const bool ok = (s < S) && (rp < bs) && (k < n);
         const int kk = ok ? k : 0;
-        PX[s / 2][s % 2] = P[kk * 3 + 0];
-        PY[s / 2][s % 2] = P[kk * 3 + 1];
-        PZ[s / 2][s % 2] = P[kk * 3 + 2];
+        VX[s] = P[kk * 3 + 0];
+        VY[s] = P[kk * 3 + 1];
+        VZ[s] = P[kk * 3 + 2];
         PW[s / 2][s % 2] = WEIGHTED ? W[kk] : 1.0f;
         // invalid slots can never be selected: d2 = -inf never reaches the max
-        PT[s / 2][s % 2] = ok ? 1e10f : -__builtin_huge_valf();
+        VT[s] = ok ? 1e10f : -__builtin_huge_valf();
     }
-    // opaque: pick_slot must read its coordinates from these pairs, not from the loaded
+    // opaque: pick_slot must read its coordinates from these tuples, not from the loaded
     // scalars (otherwise every point stays live twice: +96 VGPRs at 32 slots)
-#pragma unroll
-    for (int s = 0; s < S2; ++s) asm volatile("" : "+v"(PX[s]), "+v"(PY[s]), "+v"(PZ[s]));
+    asm volatile("" : "+v"(VX), "+v"(VY), "+v"(VZ));
 
     float x1 = P[0], y1 = P[1], z1 = P[2];
+    const float x0 = x1, y0 = y1, z0 = z1;  // (the reference's fallback point, .cu:115-116)
     if (tid == 0) {
         idx_out[(size_t)cloud * m] = 0;
         if (sampled_out) {
@@ -150,16 +200,22 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         if constexpr (STAMP) t0 = stamp();
         const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
         float best = -1.0f;
+        float pmx[S2];  // (HREG_FPS_PAIRMASK) the pair maxima
 #pragma unroll
         for (int s = 0; s < S2; ++s) {
-            const f2 dx = PX[s] - X1, dy = PY[s] - Y1, dz = PZ[s] - Z1;
+            const f2 dx = pair_of(VX, s) - X1, dy = pair_of(VY, s) - Y1, dz = pair_of(VZ, s) - Z1;
             f2 d = (dx * dx + dy * dy) + dz * dz;
             if (WEIGHTED) d = PW[s] * d;
             f2 t;
-            t.x = fmin_nc(d.x, PT[s].x, inf);
-            t.y = fmin_nc(d.y, PT[s].y, inf);
-            PT[s] = t;
-#if HREG_FPS_MAX3
+            t.x = fmin_nc(d.x, VT[2 * s], inf);
+            t.y = fmin_nc(d.y, VT[2 * s + 1], inf);
+            VT[2 * s] = t.x;
+            VT[2 * s + 1] = t.y;
+#if HREG_FPS_PAIRMASK
+            pmx[s] = fmax_nc(t.x, t.y, inf);
+            if (s & 1) asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(pmx[s - 1]), "v"(pmx[s]));
+            else if (s + 1 == S2) best = fmax_nc(best, pmx[s], inf);
+#elif HREG_FPS_MAX3
             // one v_max3_f32 per pair instead of two v_med3 (t and best are never NaN):
             // level-1 FPS 1.634 -> 1.588 us per iteration, bench +0.7 % (A/B on one box, r4)
             asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(t.x), "v"(t.y));
@@ -167,15 +223,23 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
 #endif
         }
+        (void)pmx;
         if constexpr (STAMP) t1 = stamp();
-#if HREG_FPS_BESTMASK
+#if HREG_FPS_PAIRMASK
+        // this lane's first PAIR holding its own maximum (16 compares at 32 slots); the winning
+        // lane's slot inside that pair comes after the wave reduction (below)
+        uint32_t smask = 0;
+#pragma unroll
+        for (int s = 0; s < S2; ++s) smask |= (pmx[s] == best) ? (1u << s) : 0u;
+        const float wmax = wave_max_uniform(best, inf);
+#elif HREG_FPS_BESTMASK
         // this lane's first slot holding its own maximum (the winning lane's own maximum is the
         // wave max, and only its slot is read): no dependence on the wave reduction, so these
         // compares fill that reduction's latency
         uint32_t smask = 0;
 #pragma unroll
         for (int s = 0; s < 2 * S2; ++s)
-            smask |= (PT[s / 2][s % 2] == best) ? (1u << s) : 0u;
+            smask |= (VT[s] == best) ? (1u << s) : 0u;
         const float wmax = wave_max_uniform(best, inf);
 #else
         const float wmax = wave_max_uniform(best, inf);
@@ -183,27 +247,32 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         uint32_t smask = 0;
 #pragma unroll
         for (int s = 0; s < 2 * S2; ++s)
-            smask |= (PT[s / 2][s % 2] == wmax) ? (1u << s) : 0u;
+            smask |= (VT[s] == wmax) ? (1u << s) : 0u;
 #endif
         const int myslot = smask ? (int)__builtin_ctz(smask) : 0;
         const uint64_t hit = __ballot(best == wmax);
         const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest reference order
+#if HREG_FPS_PAIRMASK
+        // the winning lane's pair, then its x slot if that holds the max (ties: the lower slot)
+        const int sp = __builtin_amdgcn_readlane(myslot, wl);
+        const int sl = 2 * sp + (readlane_f(VT[2 * sp], wl) == wmax ? 0 : 1);
+#else
         const int sl = __builtin_amdgcn_readlane(myslot, wl);
+#endif
         const int rp = (wv * 64 + wl) * G + sl / QT;
         const int kwin = (int)bitrev_bits((uint32_t)rp, L) + (sl % QT) * bs;
         float wx = 0.f, wy = 0.f, wz = 0.f;
-        pick_slot<0, 2 * S2>(sl, wl, PX, PY, PZ, wx, wy, wz);
+        pick_slot<0, 2 * S2>(sl, wl, VX, VY, VZ, wx, wy, wz);
         if constexpr (STAMP) t2 = stamp();
         int old;
         if constexpr (NW == 1) {
-            // one wave: its winner is the block winner, no LDS round trip or barrier
-            if (wmax > -1.0f) {
-                old = kwin;
-                x1 = wx; y1 = wy; z1 = wz;
-            } else {  // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0)
-                old = 0;
-                x1 = P[0]; y1 = P[1]; z1 = P[2];
-            }
+            // one wave: its winner is the block winner, no LDS round trip or barrier; no
+            // d2 > -1 anywhere: the reference keeps (best=-1, besti=0) (selects, no branch)
+            const bool any = wmax > -1.0f;
+            old = any ? kwin : 0;
+            x1 = any ? wx : x0;
+            y1 = any ? wy : y0;
+            z1 = any ? wz : z0;
         } else {
             const int buf = j & 1;
             if (lane == 0) {
@@ -221,15 +290,12 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             const float gmax = readlane_f(row_max16(c.w, inf), 0);
             const uint64_t ghit = __ballot(lane < NW && c.w == gmax);
             const int gw = (int)__builtin_ctzll(ghit);  // lowest wave = lowest reference order
-            if (gmax > -1.0f) {
-                old = __builtin_amdgcn_readlane(ck, gw);
-                x1 = readlane_f(c.x, gw);
-                y1 = readlane_f(c.y, gw);
-                z1 = readlane_f(c.z, gw);
-            } else {  // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0)
-                old = 0;
-                x1 = P[0]; y1 = P[1]; z1 = P[2];
-            }
+            // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0) (selects, no branch)
+            const bool any = gmax > -1.0f;
+            old = any ? __builtin_amdgcn_readlane(ck, gw) : 0;
+            x1 = any ? readlane_f(c.x, gw) : x0;
+            y1 = any ? readlane_f(c.y, gw) : y0;
+            z1 = any ? readlane_f(c.z, gw) : z0;
         }
         if (tid == 0) {
             idx_out[(size_t)cloud * m + j] = old;
@@ -263,7 +329,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             const int g = s / QT, i = s % QT;
             const int rp = tid * G + g;
             const int k = (int)bitrev_bits((uint32_t)rp, L2) + i * bs2;
-            if ((rp < bs2) && (k < n)) tp[k] = PT[s / 2][s % 2];
+            if ((rp < bs2) && (k < n)) tp[k] = VT[s];
         }
     }
 }
@@ -445,7 +511,7 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
             const int wl = (int)__builtin_ctzll(hit);
             const int ws = __builtin_amdgcn_readlane(myslot, wl);
             float wx = 0.f, wy = 0.f, wz = 0.f;
-            pick_slot<0, S>(ws, wl, PX, PY, PZ, wx, wy, wz);
+            pick_slot_pairs<0, S>(ws, wl, PX, PY, PZ, wx, wy, wz);
             const uint32_t rank = (uint32_t)((p * 64 + wl) * S + ws);
             SyncSlot *cur = sl + (j & 1) * FPS_CL_MAXP;
             const uint64_t tag = (uint64_t)(uint32_t)j << 32;

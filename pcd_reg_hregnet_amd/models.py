@@ -154,14 +154,22 @@ class HierFeatureExtraction(nn.Module):
         self._prep = _Prepared()
 
     def forward(self, points):
+        B = points.shape[0]
         if self.training:
-            raise NotImplementedError("train-mode forward is not implemented on the HIP path yet")
+            # (models.py:26-58 in train mode, as train_feats.py trains it: batch-statistics BN,
+            # running statistics updated, differentiable in every parameter -- the same
+            # train_graph.feature_extraction HRegNet's training step runs for src and dst)
+            from . import train_graph
+            out = train_graph.feature_extraction(self, points.float().contiguous())
+            return {k: (v if k.startswith("xyz") else
+                        v.view(B, -1) if k.startswith("sigmas") else
+                        v.view(B, v.shape[0] // B, -1).transpose(1, 2))
+                    for k, v in out.items() if not k.startswith("fps_idx")}
         P = self._prep.get(_Prefixed(self), points.device)
         samples = None if self.use_fps else engine.random_samples(
             1, points.shape[0], engine.level_input_sizes(points.shape[1]), points.device)
         out = engine.feature_extraction(P, points.float().contiguous(), self.use_weights,
                                         samples=samples)
-        B = points.shape[0]
         res = {}
         for i, m in enumerate((1024, 512, 256)):
             res[f"xyz_{i + 1}"] = out[f"xyz_{i + 1}"]

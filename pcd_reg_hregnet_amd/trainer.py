@@ -355,9 +355,12 @@ class GraphTrainer:
                 self._body(k)
                 tr.opt.step_count += 1
         torch.cuda.current_stream().wait_stream(s)
+        # with a process group up, its watchdog thread queries work events while we capture:
+        # thread-local capture mode keeps those queries legal (capture.graph)
+        mode = "thread_local" if (dist.is_available() and dist.is_initialized()) else "global"
         for k in (0, 1):
             g = torch.cuda.CUDAGraph()
-            with capture.graph(g):
+            with capture.graph(g, capture_error_mode=mode):
                 self.outs[k] = self._body(k)
             self.graphs[k] = g
         torch.cuda.synchronize()

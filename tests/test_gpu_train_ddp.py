@@ -178,58 +178,30 @@ def test_graph_trainer_rccl_world1():
     replays at N > 1).  Replayed steps against the eager world-1 trainer with no collective: the
     same losses, parameters, Adam moments and BN buffers, bitwise (a sum over one rank and a
     division by 1 are exact).  The collective calls are counted: one per eager step, one per
-    capture of the body (a replay re-runs the node without a host call)."""
-    import os
-    import socket
-    import torch.distributed as dist
-    from test_gpu_train_capture import _batches, _trainer
-    from pcd_reg_hregnet_amd import _lib, trainer
-    _lib.load()
-    assert not dist.is_initialized()
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    calls = []
-    orig = dist.all_reduce
+    body run at capture (a replay re-runs the node without a host call).
 
-    def counting(t, *a, **k):
-        calls.append(t.numel())
-        return orig(t, *a, **k)
-    try:
-        B, n = 2, 4096
-        batches = _batches(B, n, 4)
-        plain = _trainer()
-        red = _trainer()
-        red.always_reduce = True
-        dist.all_reduce = counting
-        # eager: the collective runs once per step
-        le = [plain.step(*batches[0])[0].clone()]
-        lr_ = [red.step(*batches[0])[0].clone()]
-        torch.cuda.synchronize()
-        assert calls == [red.bucket.flat.numel()], calls
-        assert torch.equal(le[0], lr_[0]) and torch.equal(plain.params.flat, red.params.flat)
-        calls.clear()
-        gt = trainer.GraphTrainer(red, B, n)
-        gt.capture(*batches[1])
-        n_capture = len(calls)
-        # two eager warm-up bodies + the two captured bodies
-        assert n_capture == 4, calls
-        for i in range(1, 4):
-            nxt = batches[i + 1][:2] if i + 1 < 4 else None
-            le.append(plain.step(*batches[i], next_batch=nxt)[0].clone())
-            lr_.append(gt.step(*batches[i], next_batch=nxt)[0].clone())
-        torch.cuda.synchronize()
-        assert len(calls) == n_capture  # replays issue no host-side collective call
-    finally:
-        dist.all_reduce = orig
-        dist.destroy_process_group()
-    print("eager", [float(x) for x in le], "rccl graph", [float(x) for x in lr_])
-    for a, b in zip(le, lr_):
-        assert torch.equal(a, b)
-    assert torch.equal(plain.params.flat, red.params.flat)
-    assert torch.equal(plain.opt.m, red.opt.m) and torch.equal(plain.opt.v, red.opt.v)
-    for (na, a), (_, b) in zip(plain.net.named_buffers(), red.net.named_buffers()):
-        assert torch.equal(a, b), na
+    Runs in a child process (tests/rccl_world1_child.py): the process group, its communicator
+    and the graphs that hold its kernels live and die there, in that order, so this pytest
+    process never holds an RCCL communicator; the child reports every check and its teardown."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1",
+               HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    p = subprocess.run([sys.executable, "-u", os.path.join(here, "rccl_world1_child.py")], env=env,
+                       capture_output=True, text=True, timeout=600)
+    print(p.stdout[-4000:])
+    print(p.stderr[-4000:])
+    res = {}
+    for line in p.stdout.splitlines():
+        if line.startswith("RESULT "):
+            res.update(json.loads(line[7:]))
+    assert res.get("eager_calls") == 1, res
+    assert res.get("capture_calls") == 4, res      # two eager warm-up bodies + two captured
+    assert res.get("replay_calls") == 0, res       # replays issue no host-side collective call
+    assert res.get("eager_equal") and res.get("losses_equal") and res.get("params_equal"), res
+    assert res.get("moments_equal") and res.get("buffers_equal"), res
+    assert res.get("teardown") == "ok", (res, p.returncode)
+    assert p.returncode == 0, p.returncode
