@@ -79,6 +79,13 @@ enum {
  * contents are unspecified -- it holds the workgroups' exchange slots; the
  * reference's caller discards temp, models/utils.py:24-27), idx [b,m] int32 (out),
  * sampled_xyz [b,m,3] (optional out: gathered coordinates of idx). */
+/* hreg_furthest_point_sampling for a caller that guarantees at most `concurrent` (>= 1)
+ * multi-workgroup FPS launches (clouds above 16384 points) of this process run at once -- e.g. a
+ * graph whose one stage-1 stream carries all of them: such a launch may keep more clouds' worker
+ * waves spinning at once (device capacity / concurrent instead of / GPU_MAX_HW_QUEUES, capped at
+ * 1024 waves).  Same results as hreg_furthest_point_sampling. */
+int hreg_fps_bounded(int b, int n, int m, const float *points, float *temp, int32_t *idx,
+                     float *sampled_xyz, int concurrent, void *stream);
 int hreg_furthest_point_sampling(int b, int n, int m, const float *points, float *temp,
                                  int32_t *idx, float *sampled_xyz, void *stream);
 

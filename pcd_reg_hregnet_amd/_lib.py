@@ -56,6 +56,7 @@ class Gemm(ctypes.Structure):
 
 _SIGS = {
     "hreg_furthest_point_sampling": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "hreg_fps_bounded": [_i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp],
     "hreg_weighted_furthest_point_sampling": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_gather_points": [_i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "hreg_gather_points_grad": [_i, _i, _i, _i, _vp, _vp, _vp, _vp],
@@ -224,6 +225,10 @@ def load(require_gpu: bool = True):
                 "(hipcc --offload-arch=gfx950); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
         for name, args in _SIGS.items():
+            if os.environ.get("HREG_LIB") and not hasattr(L, name):
+                # an A/B build of an older tree (HREG_LIB, timing only) may predate newer
+                # entries: they raise when called; the product library must export them all
+                continue
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = ctypes.c_int

@@ -41,7 +41,7 @@
 // tree of uniform branches (whose structurised Flow blocks were ~0.2-0.4 us of every
 // iteration).  A/B: 0 keeps the branch tree.
 #ifndef HREG_FPS_MOVREL
-#define HREG_FPS_MOVREL 1
+#define HREG_FPS_MOVREL 8  // the smallest slot count that takes the indexed read (A/B: 0 = never)
 #endif
 
 namespace {
@@ -98,9 +98,16 @@ __device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N
 
 // HREG_FPS_PAIRMASK (r5): the lane's first slot of its maximum found over the pair maxima
 // (16 compares at 32 slots instead of 32), then, for the winning lane only, the pair's x / y
-// slot by one uniform-index register read of the temps.  A/B: 0 keeps the per-slot mask.
+// slot by one uniform-index register read of the temps; used from this many slots up.
+// Measured (bench lines, one box): level 1 (32 slots) 1.567 -> 1.43 us per iteration; level 2
+// (4 slots) 0.545 -> 0.60, so the small geometries keep the per-slot mask.  A/B: 0 = never.
 #ifndef HREG_FPS_PAIRMASK
-#define HREG_FPS_PAIRMASK 0
+#define HREG_FPS_PAIRMASK 16
+#endif
+// HREG_FPS_PRIO: s_setprio for the FPS waves (they share SIMDs with the MFMA kernels of other
+// lanes, and every iteration waits for the slowest wave / participant).  0 = off.
+#ifndef HREG_FPS_PRIO
+#define HREG_FPS_PRIO 0
 #endif
 
 // per-axis slot coordinates of a thread: one contiguous VGPR tuple
@@ -121,7 +128,8 @@ __device__ __forceinline__ f2 pair_of(const V &v, int s) {
 template <int LO, int HI, class V>
 __device__ __forceinline__ void pick_slot(int sl, int wl, const V &VX, const V &VY, const V &VZ, float &x,
                                           float &y, float &z) {
-    if constexpr (HREG_FPS_MOVREL) {
+    constexpr int N = sizeof(V) / sizeof(float);
+    if constexpr (HREG_FPS_MOVREL && N >= HREG_FPS_MOVREL) {
         x = readlane_f(VX[sl], wl);
         y = readlane_f(VY[sl], wl);
         z = readlane_f(VZ[sl], wl);
@@ -149,12 +157,14 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
     constexpr int S = G * QT;
     constexpr int S2 = (S + 1) / 2;
     constexpr int NW = T / HREG_WAVE;
+    constexpr bool PM = HREG_FPS_PAIRMASK && 2 * S2 >= HREG_FPS_PAIRMASK;
     static_assert(NW <= 16, "block winner reduction uses one 16-lane row");
     static_assert(2 * S2 <= 32, "slot mask is 32 bits");
     __shared__ float4 s_cand[2][NW];
     __shared__ int s_k[2][NW];
     uint64_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, r0 = 0, c0 = 0;
 
+    if constexpr (HREG_FPS_PRIO > 0) __builtin_amdgcn_s_setprio(HREG_FPS_PRIO);
     const int cloud = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -200,7 +210,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         if constexpr (STAMP) t0 = stamp();
         const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
         float best = -1.0f;
-        float pmx[S2];  // (HREG_FPS_PAIRMASK) the pair maxima
+        float pmx[S2];  // (PM) the pair maxima
 #pragma unroll
         for (int s = 0; s < S2; ++s) {
             const f2 dx = pair_of(VX, s) - X1, dy = pair_of(VY, s) - Y1, dz = pair_of(VZ, s) - Z1;
@@ -211,54 +221,52 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             t.y = fmin_nc(d.y, VT[2 * s + 1], inf);
             VT[2 * s] = t.x;
             VT[2 * s + 1] = t.y;
-#if HREG_FPS_PAIRMASK
-            pmx[s] = fmax_nc(t.x, t.y, inf);
-            if (s & 1) asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(pmx[s - 1]), "v"(pmx[s]));
-            else if (s + 1 == S2) best = fmax_nc(best, pmx[s], inf);
-#elif HREG_FPS_MAX3
-            // one v_max3_f32 per pair instead of two v_med3 (t and best are never NaN):
-            // level-1 FPS 1.634 -> 1.588 us per iteration, bench +0.7 % (A/B on one box, r4)
-            asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(t.x), "v"(t.y));
-#else
-            best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
-#endif
+            if constexpr (PM) {
+                pmx[s] = fmax_nc(t.x, t.y, inf);
+                if (s & 1) asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(pmx[s - 1]), "v"(pmx[s]));
+                else if (s + 1 == S2) best = fmax_nc(best, pmx[s], inf);
+            } else if constexpr (HREG_FPS_MAX3) {
+                // one v_max3_f32 per pair instead of two v_med3 (t and best are never NaN):
+                // level-1 FPS 1.634 -> 1.588 us per iteration, bench +0.7 % (A/B on one box, r4)
+                asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(t.x), "v"(t.y));
+            } else {
+                best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
+            }
         }
         (void)pmx;
         if constexpr (STAMP) t1 = stamp();
-#if HREG_FPS_PAIRMASK
-        // this lane's first PAIR holding its own maximum (16 compares at 32 slots); the winning
-        // lane's slot inside that pair comes after the wave reduction (below)
         uint32_t smask = 0;
+        float wmax;
+        if constexpr (PM) {
+            // this lane's first PAIR holding its own maximum (16 compares at 32 slots); the
+            // winning lane's slot inside that pair comes after the wave reduction (below)
 #pragma unroll
-        for (int s = 0; s < S2; ++s) smask |= (pmx[s] == best) ? (1u << s) : 0u;
-        const float wmax = wave_max_uniform(best, inf);
-#elif HREG_FPS_BESTMASK
-        // this lane's first slot holding its own maximum (the winning lane's own maximum is the
-        // wave max, and only its slot is read): no dependence on the wave reduction, so these
-        // compares fill that reduction's latency
-        uint32_t smask = 0;
+            for (int s = 0; s < S2; ++s) smask |= (pmx[s] == best) ? (1u << s) : 0u;
+            wmax = wave_max_uniform(best, inf);
+        } else if constexpr (HREG_FPS_BESTMASK) {
+            // this lane's first slot holding its own maximum (the winning lane's own maximum is
+            // the wave max, and only its slot is read): no dependence on the wave reduction, so
+            // these compares fill that reduction's latency
 #pragma unroll
-        for (int s = 0; s < 2 * S2; ++s)
-            smask |= (VT[s] == best) ? (1u << s) : 0u;
-        const float wmax = wave_max_uniform(best, inf);
-#else
-        const float wmax = wave_max_uniform(best, inf);
-        // this lane's first slot holding the wave max (bit mask + find-first-set)
-        uint32_t smask = 0;
+            for (int s = 0; s < 2 * S2; ++s) smask |= (VT[s] == best) ? (1u << s) : 0u;
+            wmax = wave_max_uniform(best, inf);
+        } else {
+            wmax = wave_max_uniform(best, inf);
+            // this lane's first slot holding the wave max (bit mask + find-first-set)
 #pragma unroll
-        for (int s = 0; s < 2 * S2; ++s)
-            smask |= (VT[s] == wmax) ? (1u << s) : 0u;
-#endif
+            for (int s = 0; s < 2 * S2; ++s) smask |= (VT[s] == wmax) ? (1u << s) : 0u;
+        }
         const int myslot = smask ? (int)__builtin_ctz(smask) : 0;
         const uint64_t hit = __ballot(best == wmax);
         const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest reference order
-#if HREG_FPS_PAIRMASK
-        // the winning lane's pair, then its x slot if that holds the max (ties: the lower slot)
-        const int sp = __builtin_amdgcn_readlane(myslot, wl);
-        const int sl = 2 * sp + (readlane_f(VT[2 * sp], wl) == wmax ? 0 : 1);
-#else
-        const int sl = __builtin_amdgcn_readlane(myslot, wl);
-#endif
+        int sl;
+        if constexpr (PM) {
+            // the winning lane's pair, then its x slot if that holds the max (ties: the lower slot)
+            const int sp = __builtin_amdgcn_readlane(myslot, wl);
+            sl = 2 * sp + (readlane_f(VT[2 * sp], wl) == wmax ? 0 : 1);
+        } else {
+            sl = __builtin_amdgcn_readlane(myslot, wl);
+        }
         const int rp = (wv * 64 + wl) * G + sl / QT;
         const int kwin = (int)bitrev_bits((uint32_t)rp, L) + (sl % QT) * bs;
         float wx = 0.f, wy = 0.f, wz = 0.f;
@@ -457,6 +465,7 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                                                          float inf, uint32_t polls_max, int stall) {
     constexpr int S2 = S / 2;
     static_assert(S % 2 == 0 && S <= 32, "slots");
+    if constexpr (HREG_FPS_PRIO > 0) __builtin_amdgcn_s_setprio(HREG_FPS_PRIO);
     const int p = blockIdx.x;  // participant
     const int lane = threadIdx.x;
     for (int cloud = blockIdx.y; cloud < b; cloud += gridDim.y) {
@@ -644,35 +653,50 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
 // (occupancy API x CU count); if it cannot hold one cluster, the launch uses the
 // non-spinning fps_mem_kernel.  The poll bound + HREG_STATUS_FPS_TIMEOUT stay the
 // backstop (other processes on the same device are outside this bound).
-int cluster_wave_budget(int S, bool weighted) {
-    static int cache[2][3] = {{-1, -1, -1}, {-1, -1, -1}};
+//
+// `concurrent` (hreg_fps_bounded): the caller guarantees at most that many cluster launches of
+// this process run at once -- a graph whose ONE stage-1 stream runs every multi-workgroup FPS
+// (Model_V2's batched stage 1) passes 1 -- so a launch may spin up to (resident waves) /
+// concurrent, capped at FPS_SPIN_CAP_BOUNDED (leaves 2/3 of the chip's wave slots to the
+// other kernels: 1024 of 3072 at 129 VGPRs).  0: the hardware-queue bound above.
+constexpr int FPS_SPIN_CAP = 256, FPS_SPIN_CAP_BOUNDED = 1024;
+int cluster_wave_budget(int S, bool weighted, int concurrent = 0) {
+    static int cache[2][3] = {{-1, -1, -1}, {-1, -1, -1}};  // resident waves of the variant
     const int si = S == 8 ? 0 : S == 16 ? 1 : 2;
     int &c = cache[weighted ? 1 : 0][si];
-    if (c >= 0) return c;
-    int dev = 0, cus = 0, per_cu = 0;
-    const void *fn = nullptr;
+    if (c < 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        const void *fn = nullptr;
 #define HREG_FPS_CLK(SS, WW) \
     if (S == SS && weighted == WW) fn = reinterpret_cast<const void *>(&fps_cluster_kernel<SS, WW>);
-    HREG_FPS_CLK(8, false) HREG_FPS_CLK(16, false) HREG_FPS_CLK(32, false)
-    HREG_FPS_CLK(8, true) HREG_FPS_CLK(16, true) HREG_FPS_CLK(32, true)
+        HREG_FPS_CLK(8, false) HREG_FPS_CLK(16, false) HREG_FPS_CLK(32, false)
+        HREG_FPS_CLK(8, true) HREG_FPS_CLK(16, true) HREG_FPS_CLK(32, true)
 #undef HREG_FPS_CLK
-    if (!fn || hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        return c = 0;
+        if (!fn || hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            c = 0;
+        } else {
+            c = per_cu * cus;
+        }
+    }
+    if (c <= 0) return 0;
+    if (concurrent > 0) {
+        const long b = (long)c / concurrent;
+        return (int)(b < FPS_SPIN_CAP_BOUNDED ? b : FPS_SPIN_CAP_BOUNDED);
     }
     const char *q = getenv("GPU_MAX_HW_QUEUES");
     int queues = q ? atoi(q) : 4;
     if (queues < 1) queues = 4;
-    const long budget = (long)per_cu * cus / queues;
-    return c = (int)(budget < 256 ? budget : 256);
+    const long budget = (long)c / queues;
+    return (int)(budget < FPS_SPIN_CAP ? budget : FPS_SPIN_CAP);
 }
 
 template <bool WEIGHTED>
 int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *temp, int32_t *idx,
                float *sampled, hipStream_t st, uint32_t polls_max = FPS_CL_POLLS, int stall = -1,
-               bool force_cluster = false) {
+               bool force_cluster = false, int concurrent = 0) {
     if (b < 0 || n <= 0 || xyz == nullptr || idx == nullptr) return HREG_ERR_INVALID;
     if (WEIGHTED && w == nullptr) return HREG_ERR_INVALID;
     if (b == 0 || m <= 0) return HREG_OK;  // .cu:92: if (m <= 0) return;
@@ -694,7 +718,7 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
         if (ranks <= (long)FPS_CL_MAXP * 64 * s) { S = s; break; }
     const size_t slot_bytes = (size_t)2 * FPS_CL_MAXP * sizeof(SyncSlot);
     const int NP = S ? (int)((ranks + 64L * S - 1) / (64L * S)) : 0;
-    const int spin = S ? cluster_wave_budget(S, WEIGHTED) : 0;
+    const int spin = S ? cluster_wave_budget(S, WEIGHTED, concurrent) : 0;
     if (S && (size_t)n * sizeof(float) >= slot_bytes && spin >= NP) {
         const int clusters = b < spin / NP ? b : spin / NP;
         SyncSlot *slots = reinterpret_cast<SyncSlot *>(temp);
@@ -783,6 +807,17 @@ extern "C" int hreg_furthest_point_sampling(int b, int n, int m, const float *po
                                             float *temp, int32_t *idx, float *sampled_xyz,
                                             void *stream) {
     return launch_fps<false>(b, n, m, points, nullptr, temp, idx, sampled_xyz, as_stream(stream));
+}
+
+// hreg_furthest_point_sampling whose caller guarantees that at most `concurrent` (>= 1)
+// multi-workgroup FPS launches of this process run at once (one stream carries them all): the
+// launch may then keep (resident waves) / concurrent participants spinning instead of
+// (resident waves) / GPU_MAX_HW_QUEUES (cluster_wave_budget).  Same results.
+extern "C" int hreg_fps_bounded(int b, int n, int m, const float *points, float *temp, int32_t *idx,
+                                float *sampled_xyz, int concurrent, void *stream) {
+    if (concurrent < 1) return HREG_ERR_INVALID;
+    return launch_fps<false>(b, n, m, points, nullptr, temp, idx, sampled_xyz, as_stream(stream), FPS_CL_POLLS,
+                             -1, false, concurrent);
 }
 
 extern "C" int hreg_weighted_furthest_point_sampling(int b, int n, int m, const float *points,

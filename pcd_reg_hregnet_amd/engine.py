@@ -56,6 +56,7 @@ PAIR_L2 = switches.flag("PAIR_L2", False)
 # GraphPipeline: level-1 stage of all lanes as one batched launch per kernel (one side
 # stream) instead of one per lane
 BATCH_STAGE1 = switches.flag("BATCH_STAGE1", True)
+V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", False)  # GraphPipeline(v2=True): see bs1
 FRONT_STREAM = switches.flag("FRONT_STREAM", True)  # GraphPipeline: halves of a forward in consecutive rounds
 FRONT_ORDER = switches.integer("FRONT_ORDER", 3)  # per lane: 0 back then front, 1 front then back, 2 by lane parity, 3 on two streams
 # front streaming pays for a round's tail; with many lanes the tail is a small part of the round
@@ -734,7 +735,9 @@ def check_device_status(force: bool = False):
         raise RuntimeError(f"device status {st:#x}")
 
 
-def fps(xyz, npoint, weights=None, out=None):
+def fps(xyz, npoint, weights=None, out=None, concurrent=0):
+    """FPS / WFPS of nb clouds; concurrent >= 1: the caller guarantees at most that many
+    multi-workgroup FPS launches run at once (hreg_fps_bounded: a larger spin budget)."""
     global _status_pending
     nb, n, _ = xyz.shape
     dev = xyz.device
@@ -747,7 +750,9 @@ def fps(xyz, npoint, weights=None, out=None):
     # clouds above 8192 points (their register geometry has no single-workgroup case)
     temp = _empty(nb, n, device=dev) if n > 8192 else None
     _status_pending |= n > 16384 or (weights is not None and n > 8192)
-    if weights is None:
+    if weights is None and concurrent > 0:
+        call("hreg_fps_bounded", nb, n, npoint, xyz, temp, idx, sampled, concurrent, _stream())
+    elif weights is None:
         call("hreg_furthest_point_sampling", nb, n, npoint, xyz, temp, idx, sampled, _stream())
     else:
         call("hreg_weighted_furthest_point_sampling", nb, n, npoint, xyz, weights, temp, idx,
@@ -892,7 +897,7 @@ def gather_xyz(xyz, idx):
     return out
 
 
-def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None):
+def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_concurrent=0):
     """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz).
     out: optional preallocated tensors of the same tuple; ws: spatial-index workspace
     (uint8, spatial_index_bytes) for large clouds; sample: the level's random-sampling
@@ -905,7 +910,7 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None):
         idx, sampled = out[0], out[1]  # (timing probe: the buffers' previous selection)
     else:
         idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
-                           out=None if out is None else out[:2])
+                           out=None if out is None else out[:2], concurrent=fps_concurrent)
     kout = None if out is None else out[2:5]
     if PROBE_S1_SKIP == 2 and out is not None and lvl == 0:
         return idx, sampled, out[2], out[3], out[4]
@@ -1554,7 +1559,11 @@ class GraphPipeline:
         # (clouds above 16384 points -- Model_V2's config -- keep the per-lane stage: their
         # multi-workgroup FPS spins every participant of a launch, and one batched launch
         # measured slower: 803 vs 844 pairs/s)
-        self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1 and N <= 16384
+        # (Model_V2's 65536-point clouds, V2_BATCH_STAGE1: one cluster-FPS launch over every
+        # lane's clouds with the bounded-concurrency spin budget -- its stream is the only one
+        # that runs multi-workgroup FPS -- instead of one launch per lane on per-lane side streams,
+        # which shared the 4 hardware queues with the lanes' own streams)
+        self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1 and (N <= 16384 or (v2 and V2_BATCH_STAGE1))
         check_hw_queues(fork_width(lanes, self.bs1, FRONT_STREAM and FRONT_ORDER == 3 and self.bs1
                                    and not v2 and lanes <= FRONT_STREAM_MAX_LANES))
         if self.bs1:
@@ -1649,7 +1658,7 @@ class GraphPipeline:
         v = pts.view(self.lanes, 2, self.B, self.N, 3)
         v[:, 0].copy_(self.src_all)
         v[:, 1].copy_(self.dst_all)
-        grouping(pts, 0, out=g, ws=g[5])
+        grouping(pts, 0, out=g, ws=g[5], fps_concurrent=1 if self.N > 16384 else 0)
 
     def _first_stage1(self, lanes=None):
         if self.bs1:

@@ -160,7 +160,7 @@ class HierFeatureExtraction(nn.Module):
             # running statistics updated, differentiable in every parameter -- the same
             # train_graph.feature_extraction HRegNet's training step runs for src and dst)
             from . import train_graph
-            out = train_graph.feature_extraction(self, points.float().contiguous())
+            out = train_graph.feature_extraction_call(self, points.float().contiguous())
             return {k: (v if k.startswith("xyz") else
                         v.view(B, -1) if k.startswith("sigmas") else
                         v.view(B, v.shape[0] // B, -1).transpose(1, 2))

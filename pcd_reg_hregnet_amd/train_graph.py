@@ -691,6 +691,16 @@ def feature_extraction(fe, points, hook=None, part="src"):
     return out
 
 
+def feature_extraction_call(fe, points):
+    """HierFeatureExtraction called by itself in train mode (train_feats.py's use): the
+    forward above plus the BN num_batches_tracked bumps hregnet_train_forward makes once per
+    forward (one per BN call)."""
+    _BN_COUNTERS.clear()
+    out = feature_extraction(fe, points)
+    _flush_bn_counters()
+    return out
+
+
 def _knn_local(hook, name, p1, p2, k, dev):
     loc = hook(name, lambda: engine.knn_idx32(p1, p2, k), p2.shape[1], dev) if hook is not None \
         else engine.knn_idx32(p1, p2, k)

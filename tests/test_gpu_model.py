@@ -716,21 +716,29 @@ def test_model_v2_module_api(net_v2):
     np.testing.assert_allclose(r["translation"][-1].cpu().numpy(), g["t1"], atol=1e-4)
 
 
-def test_model_v2_graph_pipeline_matches_eager(net_v2):
-    """Model_V2 through the graph executor (2 lanes, N=65536 level-1 on the side
-    streams): outputs bitwise those of the eager forward, prime shuffles drawn from
-    the host generator per round exactly as the eager forward draws them."""
+@pytest.mark.parametrize("batched", [False, True])
+def test_model_v2_graph_pipeline_matches_eager(net_v2, batched):
+    """Model_V2 through the graph executor (2 lanes, N=65536 level-1 on the side streams, or
+    batched: one bounded-concurrency cluster-FPS launch over both lanes' clouds,
+    engine.V2_BATCH_STAGE1): outputs bitwise those of the eager forward, prime shuffles drawn
+    from the host generator per round exactly as the eager forward draws them."""
     from pcd_reg_hregnet_amd import engine
     g = load_npz("model_v2_lidar_b1_n65536.npz")
     P = net_v2.prepared(torch.device("cuda"))
     src = torch.from_numpy(g["src"]).cuda()
     dst = torch.from_numpy(g["dst"]).cuda()
-    with torch.no_grad():
-        gp = engine.GraphPipeline(P, src, dst, lanes=2, v2=True)
-        torch.manual_seed(int(g["perm_seed"]))
-        outs = gp.run(1)
-        torch.manual_seed(int(g["perm_seed"]))
-        ref = engine.model_v2_forward(P, src, dst)
+    old = engine.V2_BATCH_STAGE1
+    try:
+        engine.V2_BATCH_STAGE1 = batched
+        with torch.no_grad():
+            gp = engine.GraphPipeline(P, src, dst, lanes=2, v2=True)
+            assert gp.bs1 == batched
+            torch.manual_seed(int(g["perm_seed"]))
+            outs = gp.run(1)
+            torch.manual_seed(int(g["perm_seed"]))
+            ref = engine.model_v2_forward(P, src, dst)
+    finally:
+        engine.V2_BATCH_STAGE1 = old
     torch.cuda.synchronize()
     for o in outs[:1]:
         for key in ("src_dst_feats_2", "src_dst_feats_2_prime", "src_dst_weights_2",
