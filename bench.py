@@ -43,6 +43,8 @@ PAIRS_PER_GPU = 8
 LANES_MAX = 48         # graph executor: most batches in flight (memory: one forward's buffers each)
 V2_POINTS = 65536      # config 5 (MANTruckScenes-shape): B=16 over 8 GPUs -> 2 pairs/GPU
 V2_PAIRS_PER_GPU = 2
+V2_LANES = 4           # Model_V2 graph executor: lanes (forwards in flight)
+V2_MERGE = 1           # Model_V2: reference batches merged per forward (--merge)
 
 
 class _Args:
@@ -671,7 +673,7 @@ def bench_train(args, world, rank, device):
             "config": {"workload": f"HRegNet train step (train-mode BN, 3-level "
                                    f"transformation_loss, backward, Adam), batch={B} pairs/GPU, "
                                    f"2x{args.points}-pt pairs (BASELINE configs[3])",
-                       "global_batch": B * world, "points": args.points,
+                       "global_batch": B * world, "points": args.points, "merge": merge,
                        "parallelism": f"dp{world} (one 9.87 MB gradient all-reduce per step)"},
             "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
             "executor": "HIP graphs (two captured steps, ping-pong inputs)" if graphed else "eager",
@@ -762,6 +764,9 @@ def main():
     ap.add_argument("--points", type=int, default=None,
                     help=f"points per cloud (default {POINTS}; {V2_POINTS} for v2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--merge", type=int, default=None,
+                    help="reference batches (of --batch pairs) per executor forward, one launch set "
+                         f"(default 1; {V2_MERGE} for v2); a step is still one batch")
     ap.add_argument("--train-eager", action="store_true",
                     help="--model train: launch the step eagerly instead of replaying captured graphs")
     ap.add_argument("--train-graph-ddp", action="store_true",
@@ -811,6 +816,17 @@ def main():
         args.batch = V2_PAIRS_PER_GPU if v2 else PAIRS_PER_GPU
     if args.points is None:
         args.points = V2_POINTS if v2 else POINTS
+    # --merge M (Model_V2 line): each forward of the executor runs M reference batches of
+    # --batch pairs merged into one launch set (engine.hregnet_forward sub_batch: every pair's
+    # result bitwise that of its own batch's forward, the weighted SVD's identity fallback and
+    # the prime shuffles per batch); a step is still one batch of --batch pairs
+    merge = args.merge if args.merge is not None else (V2_MERGE if v2 else 1)
+    if merge < 1 or args.steps % merge or args.warmup % merge:
+        raise SystemExit(f"bench: --steps {args.steps} / --warmup {args.warmup} are not multiples "
+                         f"of --merge {merge}")
+    steps_arg = args.steps
+    args.steps //= merge  # forwards (of merged batches) from here on; restored for the line
+    args.warmup //= merge
     lanes_auto = args.lanes is None
     if lanes_auto:
         # one round when it fits: a replay boundary drains the pipeline and the round's
@@ -820,7 +836,7 @@ def main():
         # 6295 / 6432 pairs/s; --steps 48 on 16 / 24 / 48 lanes 6802 / 6697 / 6891), else
         # LANES_MAX with a final partial round (GraphPipeline.run_forwards); v2: 4
         if v2:
-            args.lanes = 4
+            args.lanes = V2_LANES if args.steps % V2_LANES == 0 else 1
         elif args.steps <= LANES_MAX:
             args.lanes = max(args.steps, 1)
         else:
@@ -862,18 +878,19 @@ def main():
     net = make_model(device, args.model)
     P = net.prepared(device)
     B = args.batch
-    s, d, _, _ = shard_batch(rank, B, args.points)
+    s, d, _, _ = shard_batch(rank, B * merge, args.points)
     src = torch.from_numpy(s).to(device)
     dst = torch.from_numpy(d).to(device)
+    sb = B if merge > 1 else None
 
     timer = MfmaTimer()
     timer.install()
 
-    pipe = engine.Pipeline(P, device, v2=v2)
+    pipe = engine.Pipeline(P, device, v2=v2, sub_batch=sb)
     gpipe = None
     if args.executor == "graph":
         with torch.no_grad():
-            gpipe = engine.GraphPipeline(P, src, dst, lanes=args.lanes, v2=v2)
+            gpipe = engine.GraphPipeline(P, src, dst, lanes=args.lanes, v2=v2, sub_batch=sb)
             gpipe.prepare(args.warmup)
             gpipe.prepare(args.steps)  # captured before the timed region
 
@@ -881,8 +898,9 @@ def main():
         with torch.no_grad():
             if args.executor == "serial":
                 if v2:
-                    return [engine.model_v2_forward(P, src, dst) for _ in range(n)]
-                return [engine.hregnet_forward(P, src, dst) for _ in range(n)]
+                    return [engine.model_v2_finish(engine.hregnet_forward(P, src, dst, v2=True, sub_batch=sb), sb)
+                            for _ in range(n)]
+                return [engine.hregnet_forward(P, src, dst, sub_batch=sb) for _ in range(n)]
             if args.executor == "graph":
                 # a continuous stream of batches: each call's last replay also runs the next
                 # round's batched stage 1, so the warm-up leaves the first timed round's
@@ -921,6 +939,8 @@ def main():
         torch.cuda.synchronize()
     timer.enabled = False
     res = {k: timer.result(k) for k in MfmaTimer.KINDS}
+    # per reference batch of B pairs from here on (a forward ran `merge` of them)
+    args.steps, args.warmup = steps_arg, args.warmup * merge
 
     elapsed = max_over_ranks(elapsed, device)
     value = job_throughput(B, args.steps, world, elapsed)
@@ -1025,8 +1045,14 @@ def main():
                                    f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])"),
                        "executor": args.executor + ("" if args.executor == "serial" else
                                    " (level-1 FPS of step i+1 overlaps step i)") + (
-                                   f", {args.lanes} batches in flight" if args.lanes > 1 and
+                                   f", {args.lanes} forwards in flight" if args.lanes > 1 and
                                    args.executor == "graph" else "") + (
+                                   f"; {merge} batches of {B} pairs merged per forward (one launch "
+                                   "set; per-batch SVD fallback and prime shuffles)" if merge > 1
+                                   else "") + (
+                                   "; batched stage 1 (one bounded-concurrency cluster-FPS launch "
+                                   "over every lane's clouds)" if gpipe is not None and gpipe.bs1
+                                   and args.points > 16384 else "") + (
                                    "; front streaming: each timed round runs the registration "
                                    "half of its batches and the feature extraction of the next "
                                    "round's (pipeline primed after the warm-up)"

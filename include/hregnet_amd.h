@@ -304,6 +304,12 @@ int hreg_pair_feats(const float *src_xyz, const float *dst_xyz, const float *src
 int hreg_weighted_svd(const float *src, const float *corres, const float *w, int nb, int n,
                       const float *prev_R, const float *prev_t, float *R_, float *t_, float *R,
                       float *t, void *stream);
+/* hreg_weighted_svd over nb pairs that are nb / group reference batches of `group` pairs each
+ * (several batches merged into one launch set): the identity fallback of layers.py:485-493
+ * applies per batch.  group = nb is hreg_weighted_svd. */
+int hreg_weighted_svd_grouped(const float *src, const float *corres, const float *w, int nb, int group,
+                              int n, const float *prev_R, const float *prev_t, float *R_, float *t_,
+                              float *R, float *t, void *stream);
 
 /* out[b][i] = R[b] xyz[b][i] + t[b], xyz/out [nb][n][3] */
 int hreg_transform_points(const float *xyz, const float *R, const float *t, int nb, int n,

@@ -76,6 +76,7 @@ _SIGS = {
     "hreg_pair_feats": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp,
                         _vp],
     "hreg_weighted_svd": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_weighted_svd_grouped": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_transform_points": [_vp, _vp, _vp, _i, _i, _vp, _vp],
     "hreg_transformation_loss": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
                                  _vp],

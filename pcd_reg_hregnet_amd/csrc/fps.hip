@@ -104,6 +104,16 @@ __device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N
 #ifndef HREG_FPS_PAIRMASK
 #define HREG_FPS_PAIRMASK 16
 #endif
+// HREG_FPS_L1_WIDE (A/B): level 1 (n = 16384) on 1024 threads x 16 points instead of 512 x 32
+#ifndef HREG_FPS_L1_WIDE
+#define HREG_FPS_L1_WIDE 0
+#endif
+// HREG_FPS_POLL_SLEEP: s_sleep between unsuccessful exchange polls of the cluster kernel
+// (its spinning participants share SIMDs with the other lanes' kernels; a poll is four
+// agent-scope loads per lane and a wave-wide vote).  0 = off.
+#ifndef HREG_FPS_POLL_SLEEP
+#define HREG_FPS_POLL_SLEEP 0
+#endif
 // HREG_FPS_PRIO: s_setprio for the FPS waves (they share SIMDs with the MFMA kernels of other
 // lanes, and every iteration waits for the slowest wave / participant).  0 = off.
 #ifndef HREG_FPS_PRIO
@@ -171,7 +181,16 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
     const float *P = xyz + (size_t)cloud * n * 3;
     const float *W = WEIGHTED ? wts + (size_t)cloud * n : nullptr;
 
-    typename SlotVec<2 * S2>::type VX, VY, VZ, VT;  // VT: the running minima ("temp")
+    typename SlotVec<2 * S2>::type VX, VY, VZ;
+    // the running minima ("temp"): one tuple when the pair-mask search reads them by a uniform
+    // index (PM), else packed pairs (level 2's 4-slot geometry measured 0.545 vs 0.598 us per
+    // iteration with the tuple)
+    typename SlotVec<2 * S2>::type VT;
+    f2 PT[S2];
+    auto tget = [&](int s) -> float {
+        if constexpr (PM) return VT[s];
+        else return PT[s / 2][s % 2];
+    };
     f2 PW[S2];
 #pragma unroll
     for (int s = 0; s < 2 * S2; ++s) {
@@ -185,7 +204,8 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         VZ[s] = P[kk * 3 + 2];
         PW[s / 2][s % 2] = WEIGHTED ? W[kk] : 1.0f;
         // invalid slots can never be selected: d2 = -inf never reaches the max
-        VT[s] = ok ? 1e10f : -__builtin_huge_valf();
+        if constexpr (PM) VT[s] = ok ? 1e10f : -__builtin_huge_valf();
+        else PT[s / 2][s % 2] = ok ? 1e10f : -__builtin_huge_valf();
     }
     // opaque: pick_slot must read its coordinates from these tuples, not from the loaded
     // scalars (otherwise every point stays live twice: +96 VGPRs at 32 slots)
@@ -217,10 +237,14 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             f2 d = (dx * dx + dy * dy) + dz * dz;
             if (WEIGHTED) d = PW[s] * d;
             f2 t;
-            t.x = fmin_nc(d.x, VT[2 * s], inf);
-            t.y = fmin_nc(d.y, VT[2 * s + 1], inf);
-            VT[2 * s] = t.x;
-            VT[2 * s + 1] = t.y;
+            t.x = fmin_nc(d.x, tget(2 * s), inf);
+            t.y = fmin_nc(d.y, tget(2 * s + 1), inf);
+            if constexpr (PM) {
+                VT[2 * s] = t.x;
+                VT[2 * s + 1] = t.y;
+            } else {
+                PT[s] = t;
+            }
             if constexpr (PM) {
                 pmx[s] = fmax_nc(t.x, t.y, inf);
                 if (s & 1) asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(pmx[s - 1]), "v"(pmx[s]));
@@ -248,13 +272,13 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             // the wave max, and only its slot is read): no dependence on the wave reduction, so
             // these compares fill that reduction's latency
 #pragma unroll
-            for (int s = 0; s < 2 * S2; ++s) smask |= (VT[s] == best) ? (1u << s) : 0u;
+            for (int s = 0; s < 2 * S2; ++s) smask |= (tget(s) == best) ? (1u << s) : 0u;
             wmax = wave_max_uniform(best, inf);
         } else {
             wmax = wave_max_uniform(best, inf);
             // this lane's first slot holding the wave max (bit mask + find-first-set)
 #pragma unroll
-            for (int s = 0; s < 2 * S2; ++s) smask |= (VT[s] == wmax) ? (1u << s) : 0u;
+            for (int s = 0; s < 2 * S2; ++s) smask |= (tget(s) == wmax) ? (1u << s) : 0u;
         }
         const int myslot = smask ? (int)__builtin_ctz(smask) : 0;
         const uint64_t hit = __ballot(best == wmax);
@@ -298,12 +322,17 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             const float gmax = readlane_f(row_max16(c.w, inf), 0);
             const uint64_t ghit = __ballot(lane < NW && c.w == gmax);
             const int gw = (int)__builtin_ctzll(ghit);  // lowest wave = lowest reference order
-            // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0) (selects, no branch)
-            const bool any = gmax > -1.0f;
-            old = any ? __builtin_amdgcn_readlane(ck, gw) : 0;
-            x1 = any ? readlane_f(c.x, gw) : x0;
-            y1 = any ? readlane_f(c.y, gw) : y0;
-            z1 = any ? readlane_f(c.z, gw) : z0;
+            // (a uniform branch here: the selects of the one-wave path measured 0.26 vs 0.22 us
+            // for this phase at level 2)
+            if (gmax > -1.0f) {
+                old = __builtin_amdgcn_readlane(ck, gw);
+                x1 = readlane_f(c.x, gw);
+                y1 = readlane_f(c.y, gw);
+                z1 = readlane_f(c.z, gw);
+            } else {  // no d2 > -1 anywhere: the reference keeps (best=-1, besti=0)
+                old = 0;
+                x1 = x0; y1 = y0; z1 = z0;
+            }
         }
         if (tid == 0) {
             idx_out[(size_t)cloud * m + j] = old;
@@ -337,7 +366,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             const int g = s / QT, i = s % QT;
             const int rp = tid * G + g;
             const int k = (int)bitrev_bits((uint32_t)rp, L2) + i * bs2;
-            if ((rp < bs2) && (k < n)) tp[k] = VT[s];
+            if ((rp < bs2) && (k < n)) tp[k] = tget(s);
         }
     }
 }
@@ -553,6 +582,7 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                             (w2 >> 32) == (uint64_t)j && (w3 >> 32) == (uint64_t)j;
                 }
                 if (__all(fresh)) break;
+                if constexpr (HREG_FPS_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(HREG_FPS_POLL_SLEEP);
                 if (++polls > polls_max) {
                     timed_out = true;
                     break;
@@ -637,7 +667,7 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     // work per SIMD, half the per-wave reduction/winner overhead; both fill a CU's VGPRs
     // (127 x 1024 vs 254 x 512).  768 clouds (the batched level-1 stage) 5.70 -> 5.19 ms,
     // identical indices (tools/micro/fps_l1_geom.py).
-    if (!weighted && T == 1024 && QT == 16) {
+    if (!HREG_FPS_L1_WIDE && !weighted && T == 1024 && QT == 16) {
         T = 512; G = 2;
     }
 }

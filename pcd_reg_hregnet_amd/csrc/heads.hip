@@ -312,16 +312,20 @@ __global__ __launch_bounds__(256) void svd_pair_kernel(const float *__restrict__
     }
 }
 
-__global__ void svd_batch_kernel(int nb, float *__restrict__ R_, float *__restrict__ t_,
+// one workgroup per group of `group` consecutive pairs (the reference's batch: its identity
+// fallback resets the whole batch it ran, layers.py:485-493; a forward of several batches
+// merged into one launch set keeps each batch's own fallback)
+__global__ void svd_batch_kernel(int nb, int group, float *__restrict__ R_, float *__restrict__ t_,
                                  const float *__restrict__ pR, const float *__restrict__ pt,
                                  float *__restrict__ R, float *__restrict__ t) {
     __shared__ int bad;
+    const int b0 = blockIdx.x * group, b1 = min(b0 + group, nb);
     if (threadIdx.x == 0) bad = 0;
     __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += blockDim.x)
+    for (int b = b0 + threadIdx.x; b < b1; b += blockDim.x)
         if (!(R_[(size_t)b * 9] == R_[(size_t)b * 9])) atomicOr(&bad, 1);
     __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    for (int b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
         float *Rb = R_ + (size_t)b * 9, *tb = t_ + (size_t)b * 3;
         if (bad) {
             for (int q = 0; q < 9; ++q) Rb[q] = (q % 4 == 0) ? 1.f : 0.f;
@@ -482,19 +486,27 @@ extern "C" int hreg_pair_feats(const float *src_xyz, const float *dst_xyz, const
     return HREG_OK;
 }
 
-extern "C" int hreg_weighted_svd(const float *src, const float *corres, const float *w, int nb,
-                                 int n, const float *prev_R, const float *prev_t, float *R_,
-                                 float *t_, float *R, float *t, void *stream) {
-    if (!src || !corres || !w || !R_ || !t_ || nb < 0 || n <= 0) return HREG_ERR_INVALID;
+extern "C" int hreg_weighted_svd_grouped(const float *src, const float *corres, const float *w, int nb,
+                                         int group, int n, const float *prev_R, const float *prev_t, float *R_,
+                                         float *t_, float *R, float *t, void *stream) {
+    if (!src || !corres || !w || !R_ || !t_ || nb < 0 || n <= 0 || group <= 0) return HREG_ERR_INVALID;
     if ((prev_R == nullptr) != (prev_t == nullptr)) return HREG_ERR_INVALID;
     if ((R == nullptr) != (t == nullptr)) return HREG_ERR_INVALID;
     if (!nb) return HREG_OK;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(svd_pair_kernel, dim3(nb), dim3(256), 0, st, src, corres, w, n, R_, t_);
     HREG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(svd_batch_kernel, dim3(1), dim3(256), 0, st, nb, R_, t_, prev_R, prev_t, R, t);
+    hipLaunchKernelGGL(svd_batch_kernel, dim3((nb + group - 1) / group), dim3(256), 0, st, nb, group, R_, t_,
+                       prev_R, prev_t, R, t);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
+}
+
+extern "C" int hreg_weighted_svd(const float *src, const float *corres, const float *w, int nb,
+                                 int n, const float *prev_R, const float *prev_t, float *R_,
+                                 float *t_, float *R, float *t, void *stream) {
+    return hreg_weighted_svd_grouped(src, corres, w, nb, nb > 0 ? nb : 1, n, prev_R, prev_t, R_, t_, R, t,
+                                     stream);
 }
 
 extern "C" int hreg_transform_points(const float *xyz, const float *R, const float *t, int nb,

@@ -57,6 +57,7 @@ PAIR_L2 = switches.flag("PAIR_L2", False)
 # stream) instead of one per lane
 BATCH_STAGE1 = switches.flag("BATCH_STAGE1", True)
 V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", False)  # GraphPipeline(v2=True): see bs1
+V2_FRONT_STREAM = switches.flag("V2_FRONT_STREAM", False)  # GraphPipeline(v2=True): front streaming
 FRONT_STREAM = switches.flag("FRONT_STREAM", True)  # GraphPipeline: halves of a forward in consecutive rounds
 FRONT_ORDER = switches.integer("FRONT_ORDER", 3)  # per lane: 0 back then front, 1 front then back, 2 by lane parity, 3 on two streams
 # front streaming pays for a round's tail; with many lanes the tail is a small part of the round
@@ -1278,8 +1279,10 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
     return corres.view(B, N, 3), w.view(B, N)
 
 
-def weighted_svd(src, corres, w, prev=None):
-    """WeightedSVDHead (layers.py:469-504) (+ T = T_ @ T_prev, models.py:100-127)."""
+def weighted_svd(src, corres, w, prev=None, group=None):
+    """WeightedSVDHead (layers.py:469-504) (+ T = T_ @ T_prev, models.py:100-127).  group:
+    the pairs are batches of `group` pairs merged into one call (the identity fallback of
+    layers.py:485-493 per batch); None = one batch."""
     B, n, _ = src.shape
     dev = src.device
     R_ = _empty(B, 3, 3, device=dev)
@@ -1287,7 +1290,12 @@ def weighted_svd(src, corres, w, prev=None):
     R = _empty(B, 3, 3, device=dev)
     t = _empty(B, 3, device=dev)
     pR, pt = (prev if prev is not None else (None, None))
-    call("hreg_weighted_svd", src, corres, w, B, n, pR, pt, R_, t_, R, t, _stream())
+    if group is None or group == B:
+        call("hreg_weighted_svd", src, corres, w, B, n, pR, pt, R_, t_, R, t, _stream())
+    else:
+        if B % group:
+            raise ValueError(f"weighted_svd: {B} pairs are not whole batches of {group}")
+        call("hreg_weighted_svd_grouped", src, corres, w, B, group, n, pR, pt, R_, t_, R, t, _stream())
     return R_, t_, R, t
 
 
@@ -1304,14 +1312,20 @@ def level_input_sizes(N: int):
 
 
 def hregnet_forward(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=None, v2=False,
-                    use_fps=True):
+                    use_fps=True, sub_batch=None):
     """HRegNet.forward (models/HRegNet/models.py:77-148), eval mode.
 
     v2: the Model_V2 variant (models/model_v2/models.py:77-183): fine_corres_2 is
     FineReg2 (model_v2/layers.py:462-500), whose attentive features also pass
     through mlpx (Conv1d 2C->C + BN + ReLU) -> "src_dst_feats_2" [B, C, M2]; the
-    batch-shuffled prime copies are added by model_v2_finish (host RNG)."""
-    return hregnet_back(P, hregnet_front(P, src, dst, use_weights, l1, pts, use_fps), src.shape[0], v2)
+    batch-shuffled prime copies are added by model_v2_finish (host RNG).
+
+    sub_batch: src / dst are B / sub_batch reference batches of sub_batch pairs merged into one
+    launch set (an executor choice: every pair's result is bitwise the same as in its own
+    batch's forward -- the kernels are batch-independent -- and the one batch-level step, the
+    weighted SVD's identity fallback, applies per batch)."""
+    return hregnet_back(P, hregnet_front(P, src, dst, use_weights, l1, pts, use_fps), src.shape[0], v2,
+                        sub_batch)
 
 
 def hregnet_front(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=None, use_fps=True):
@@ -1333,7 +1347,7 @@ def hregnet_front(P: PreparedWeights, src, dst, use_weights=True, l1=None, pts=N
 FRONT_KEYS = tuple(f"{k}_{i + 1}" for k in ("xyz", "sigmas", "desc", "fps_idx") for i in range(3))
 
 
-def hregnet_back(P: PreparedWeights, fe, B: int, v2=False):
+def hregnet_back(P: PreparedWeights, fe, B: int, v2=False, sub_batch=None):
     """The registration half of HRegNet.forward (models.py:82-148) from hregnet_front's dict."""
 
     def split(t, rows):
@@ -1346,7 +1360,7 @@ def hregnet_back(P: PreparedWeights, fe, B: int, v2=False):
     prod = head_products(P, B, desc) if _grouped_heads_ok(desc[2].shape[1]) else None
     fpre = (lambda name: None) if prod is None else (lambda name: prod["fine_pre"][name])
     c3, w3 = coarse_reg(P, B, xyz[2], desc[2], sig[2], prod)
-    _, _, R3, t3 = weighted_svd(xyz[2][:B], c3, w3)
+    _, _, R3, t3 = weighted_svd(xyz[2][:B], c3, w3, group=sub_batch)
     x2t = transform(xyz[1][:B], R3, t3)
     sd2, dd2 = split(desc[1], M[1])
     ss2, ds2 = split(sig[1], M[1])
@@ -1359,13 +1373,13 @@ def hregnet_back(P: PreparedWeights, fe, B: int, v2=False):
     else:
         c2, w2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2,
                           pre=fpre("fine_corres_2"))
-    _, _, R2, t2 = weighted_svd(x2t, c2, w2, prev=(R3, t3))
+    _, _, R2, t2 = weighted_svd(x2t, c2, w2, prev=(R3, t3), group=sub_batch)
     x1t = transform(xyz[0][:B], R2, t2)
     sd1, dd1 = split(desc[0], M[0])
     ss1, ds1 = split(sig[0], M[0])
     c1, w1 = fine_reg(P, "fine_corres_1", B, x1t, sd1, xyz[0][B:], dd1, ss1, ds1,
                       pre=fpre("fine_corres_1"))
-    _, _, R1, t1 = weighted_svd(x1t, c1, w1, prev=(R2, t2))
+    _, _, R1, t1 = weighted_svd(x1t, c1, w1, prev=(R2, t2), group=sub_batch)
 
     def feats(part):
         sl = slice(0, B) if part == 0 else slice(B, 2 * B)
@@ -1390,15 +1404,24 @@ def hregnet_back(P: PreparedWeights, fe, B: int, v2=False):
     return out
 
 
-def model_v2_finish(out):
+def model_v2_finish(out, sub_batch=None):
     """The Model_V2 result dict (models/model_v2/models.py:145-183) from
     hregnet_forward(..., v2=True): the "prime" copies are batch shuffles drawn with
     torch.randperm(B) on the default (host) generator, features first, then weights
-    (model_v2/layers.py:491-497), as the reference draws them."""
+    (model_v2/layers.py:491-497), as the reference draws them.  sub_batch (merged batches,
+    hregnet_forward): each batch of sub_batch pairs is shuffled within itself, its two draws
+    in batch order -- the draws of the forwards of those batches one after another."""
     f2, w2 = out["src_dst_feats_2"], out["src_dst_weights_2"]
     B = w2.shape[0]
-    pf = torch.randperm(B)
-    pw = torch.randperm(B)
+    sb = B if sub_batch is None else sub_batch
+    if B % sb:
+        raise ValueError(f"model_v2_finish: {B} pairs are not whole batches of {sb}")
+    pfs, pws = [], []
+    for b0 in range(0, B, sb):
+        pfs.append(torch.randperm(sb) + b0)
+        pws.append(torch.randperm(sb) + b0)
+    pf = torch.cat(pfs)
+    pw = torch.cat(pws)
     sf, df = out["src_feats"], out["dst_feats"]
     return {
         "src_xyz_corres_3": out["src_xyz_corres_3"], "src_xyz_corres_2": out["src_xyz_corres_2"],
@@ -1428,9 +1451,10 @@ class Pipeline:
     through the complete forward; results are identical to hregnet_forward.
     """
 
-    def __init__(self, P: PreparedWeights, device, v2: bool = False):
+    def __init__(self, P: PreparedWeights, device, v2: bool = False, sub_batch=None):
         self.P = P
         self.v2 = v2
+        self.sub_batch = sub_batch  # (hregnet_forward's merged reference batches)
         self.side = torch.cuda.Stream(device=device)
 
     def _stage1(self, src, dst):
@@ -1467,8 +1491,9 @@ class Pipeline:
             pts.record_stream(main)
             for t in g:
                 t.record_stream(main)
-            out = hregnet_forward(self.P, src, dst, use_weights, l1=g, pts=pts, v2=self.v2)
-            outs.append(model_v2_finish(out) if self.v2 else out)
+            out = hregnet_forward(self.P, src, dst, use_weights, l1=g, pts=pts, v2=self.v2,
+                                  sub_batch=self.sub_batch)
+            outs.append(model_v2_finish(out, self.sub_batch) if self.v2 else out)
         check_device_status()  # syncs only when a multi-workgroup FPS ran
         return outs
 
@@ -1544,9 +1569,12 @@ class GraphPipeline:
     """
 
     def __init__(self, P: PreparedWeights, src, dst, use_weights=True, lanes: int = 1,
-                 v2: bool = False):
+                 v2: bool = False, sub_batch=None):
         self.P = P
         self.v2 = v2
+        # sub_batch: every lane's batch is B / sub_batch reference batches merged into one
+        # launch set (hregnet_forward's sub_batch; the bench's Model_V2 line)
+        self.sub_batch = sub_batch
         self.use_weights = use_weights
         self.lanes = lanes
         dev = src.device
@@ -1565,7 +1593,7 @@ class GraphPipeline:
         # which shared the 4 hardware queues with the lanes' own streams)
         self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1 and (N <= 16384 or (v2 and V2_BATCH_STAGE1))
         check_hw_queues(fork_width(lanes, self.bs1, FRONT_STREAM and FRONT_ORDER == 3 and self.bs1
-                                   and not v2 and lanes <= FRONT_STREAM_MAX_LANES))
+                                   and (not v2 or V2_FRONT_STREAM) and lanes <= FRONT_STREAM_MAX_LANES))
         if self.bs1:
             self.src_all = src.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
             self.dst_all = dst.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
@@ -1613,7 +1641,8 @@ class GraphPipeline:
         # front streaming: fe[c][ln] = static copies of a lane's feature-extraction dict;
         # fready = c: the fronts for the next round are in fe[1 - c] and its next stage 1
         # in bufs[c], so the next replay is g_fs[c]
-        self.fs = FRONT_STREAM and self.bs1 and not v2 and lanes <= FRONT_STREAM_MAX_LANES
+        self.fs = (FRONT_STREAM and self.bs1 and (not v2 or V2_FRONT_STREAM)
+                   and lanes <= FRONT_STREAM_MAX_LANES)
         self.fready = None
         if self.fs:
             with torch.no_grad():
@@ -1629,7 +1658,7 @@ class GraphPipeline:
                 g = torch.cuda.CUDAGraph()
                 with capture.graph(g, pool=self.pool):
                     if FRONT_ORDER == 3:  # the two halves of a lane on two streams
-                        out = self._fork(lambda ln: hregnet_back(P, self.fe[1 - cur][ln], B, v2),
+                        out = self._fork(lambda ln: hregnet_back(P, self.fe[1 - cur][ln], B, v2, sub_batch),
                                          body2=lambda ln: self._front_into(ln, cur),
                                          **self._side_kw(1 - cur))
                     else:
@@ -1715,7 +1744,7 @@ class GraphPipeline:
     def _rest(self, ln, cur):
         pts, g = self.bufs[ln][cur]
         return hregnet_forward(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g,
-                               pts=pts, v2=self.v2)
+                               pts=pts, v2=self.v2, sub_batch=self.sub_batch)
 
     def _front_into(self, ln, cur):
         """Lane ln's feature extraction from stage-1 set cur, copied into fe[cur][ln]."""
@@ -1730,8 +1759,8 @@ class GraphPipeline:
         default: in that order; 1: the other way round; 2: by lane parity)."""
         if FRONT_ORDER == 1 or (FRONT_ORDER == 2 and ln % 2):
             self._front_into(ln, cur)
-            return hregnet_back(self.P, self.fe[1 - cur][ln], self.B, self.v2)
-        out = hregnet_back(self.P, self.fe[1 - cur][ln], self.B, self.v2)
+            return hregnet_back(self.P, self.fe[1 - cur][ln], self.B, self.v2, self.sub_batch)
+        out = hregnet_back(self.P, self.fe[1 - cur][ln], self.B, self.v2, self.sub_batch)
         self._front_into(ln, cur)
         return out
 
@@ -1799,7 +1828,7 @@ class GraphPipeline:
     def _finish(self, outs):
         """Per-lane outputs of one replay (Model_V2: the host-RNG prime shuffles of this
         round, drawn after its replay as the reference draws them per forward)."""
-        return [model_v2_finish(o) for o in outs] if self.v2 else list(outs)
+        return [model_v2_finish(o, self.sub_batch) for o in outs] if self.v2 else list(outs)
 
     def run_forwards(self, n: int, stream: bool = False):
         """n forwards in all: full rounds of every lane, then (n % lanes) forwards on the

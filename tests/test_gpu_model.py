@@ -7,6 +7,8 @@ continuous outputs on the rows with identical selections within max(1e-5, 4 x th
 reference's own distance from its float64 replay); R/t within 1e-4 absolute.
 """
 import numpy as np
+import math
+
 import pytest
 import torch
 
@@ -855,3 +857,44 @@ def test_grouped_head_gemms_bitwise(net):
     for i in range(3):
         np.testing.assert_array_equal(a["rotation"][i], b["rotation"][i])
         np.testing.assert_array_equal(a["translation"][i], b["translation"][i])
+
+
+def test_model_v2_merged_batches_match_separate_forwards(net_v2):
+    """engine.hregnet_forward(sub_batch=2) over 3 reference batches of 2 pairs merged into one
+    launch set (the bench's Model_V2 executor, --merge): every output of every batch bitwise that
+    of the batch's own forward, including the prime copies -- shuffled within each batch, the
+    draws in batch order as three separate forwards draw them -- and the weighted SVD's identity
+    fallback applies per batch (a non-finite pair resets its own batch only)."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net_v2.prepared(torch.device("cuda"))
+    s, d, _, _ = synthetic.lidar_batch(6, 8192, seed0=31)
+    src, dst = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    with torch.no_grad():
+        torch.manual_seed(7)
+        merged = engine.model_v2_finish(engine.hregnet_forward(P, src, dst, v2=True, sub_batch=2), 2)
+        torch.manual_seed(7)
+        sep = [engine.model_v2_forward(P, src[i:i + 2], dst[i:i + 2]) for i in (0, 2, 4)]
+    torch.cuda.synchronize()
+    for j, o in enumerate(sep):
+        b = slice(2 * j, 2 * j + 2)
+        for key in ("src_dst_feats_2", "src_dst_feats_2_prime", "src_dst_weights_2",
+                    "src_dst_weights_2_prime", "src_xyz_2_trans", "src_xyz_corres_1"):
+            assert torch.equal(merged[key][b], o[key]), (j, key)
+        for i in range(3):
+            assert torch.equal(merged["rotation"][i][b], o["rotation"][i]), (j, i)
+            assert torch.equal(merged["translation"][i][b], o["translation"][i]), (j, i)
+    # the identity fallback of layers.py:485-493 per batch: pair 3 (batch 1) has no weight
+    x = torch.randn(6, 64, 3, device="cuda")
+    a = 0.3
+    Rz = torch.tensor([[math.cos(a), -math.sin(a), 0.0], [math.sin(a), math.cos(a), 0.0], [0.0, 0.0, 1.0]],
+                      device="cuda")
+    c = x @ Rz.T + 0.01
+    w = torch.rand(6, 64, device="cuda") + 0.1
+    w[3] = float("nan")
+    R_, t_, _, _ = engine.weighted_svd(x, c, w, group=2)
+    eye = torch.eye(3, device="cuda")
+    assert torch.equal(R_[2], eye) and torch.equal(R_[3], eye)
+    for i in (0, 1, 4, 5):
+        assert not torch.equal(R_[i], eye) and torch.isfinite(R_[i]).all()
+    R1_, _, _, _ = engine.weighted_svd(x, c, w)  # one batch of 6: all reset
+    assert all(torch.equal(R1_[i], eye) for i in range(6))

@@ -945,8 +945,8 @@ def test_hier_feature_extraction_train_mode():
     loss_s, loss_f = 0.0, 0.0
     for lv, M in zip((1, 2, 3), (1024, 512, 256)):
         xs, ss, ds = out[f"xyz_{lv}"], out[f"sigmas_{lv}"], out[f"desc_{lv}"]
+        # (the full forward's dict already holds the reference layout: desc [B,C,M])
         xf, sf, df = full[f"xyz_{lv}"], full[f"sigmas_{lv}"].view(B, M), full[f"desc_{lv}"]
-        df = df.view(B, M, -1).transpose(1, 2)
         assert ss.shape == (B, M) and ds.shape == (B, df.shape[1], M) and xs.shape == (B, M, 3)
         assert torch.equal(xs, xf) and torch.equal(ss, sf) and torch.equal(ds, df), lv
         for a, b in ((xs, xf), (ss, sf), (ds, df)):

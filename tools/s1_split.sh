@@ -8,7 +8,7 @@ for r in 1 2; do
   for v in PROBE_S1_SKIP=0 PROBE_S1_SKIP=1 PROBE_S1_SKIP=2 PROBE_NO_S1=1; do
     for st in 20 48; do
       t=$(echo $v | tr '=' '_').s$st.$r
-      HREG_SWITCHES=$v timeout -k 10 300 python bench.py --steps $st --warmup 5 --no-cpu-baseline > $O/$t.json 2> $O/$t.err || { echo "$t failed"; tail $O/$t.err; exit 1; }
+      HREG_SWITCHES=$v timeout -k 10 300 python bench.py --allow-probes --steps $st --warmup 5 --no-cpu-baseline > $O/$t.json 2> $O/$t.err || { echo "$t failed"; tail $O/$t.err; exit 1; }
       python -c "import json; d=json.load(open('$O/$t.json')); print('$t', d['value'], d['ms_per_step'])"
     done
   done

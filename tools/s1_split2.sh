@@ -8,7 +8,7 @@ for r in 1 2; do
     L=""; [ $lib = old ] && L=$PWD/pcd_reg_hregnet_amd/ab_simold.so
     for v in 0 3 2; do
       t=$lib.skip$v.$r
-      HREG_LIB=$L HREG_SWITCHES=PROBE_S1_SKIP=$v timeout -k 10 300 python bench.py --steps 48 --warmup 5 --no-cpu-baseline > $O/$t.json 2> $O/$t.err || { echo "$t failed"; tail $O/$t.err; exit 1; }
+      HREG_LIB=$L HREG_SWITCHES=PROBE_S1_SKIP=$v timeout -k 10 300 python bench.py --allow-probes --steps 48 --warmup 5 --no-cpu-baseline > $O/$t.json 2> $O/$t.err || { echo "$t failed"; tail $O/$t.err; exit 1; }
       python -c "import json; d=json.load(open('$O/$t.json')); print('$t', d['value'], d['ms_per_step'])"
     done
   done
