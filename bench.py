@@ -43,8 +43,8 @@ PAIRS_PER_GPU = 8
 LANES_MAX = 48         # graph executor: most batches in flight (memory: one forward's buffers each)
 V2_POINTS = 65536      # config 5 (MANTruckScenes-shape): B=16 over 8 GPUs -> 2 pairs/GPU
 V2_PAIRS_PER_GPU = 2
-V2_LANES = 4           # Model_V2 graph executor: lanes (forwards in flight)
-V2_MERGE = 1           # Model_V2: reference batches merged per forward (--merge)
+V2_LANES = 2           # Model_V2 graph executor: lanes (forwards in flight)
+V2_MERGE = 8           # Model_V2: reference batches merged per forward (--merge)
 
 
 class _Args:
@@ -379,6 +379,8 @@ def _fps_level(pts, m, weights, floor_call, floor_pts, floor_w, kernel):
     name = "hreg_weighted_furthest_point_sampling" if weights is not None else "hreg_furthest_point_sampling"
     args = (nb, n, m, pts, weights, temp, idx, None, st_) if weights is not None else \
         (nb, n, m, pts, temp, idx, None, st_)
+    if floor_call is None:  # the multi-workgroup kernel as the batched stage 1 launches it
+        name, args = "hreg_fps_bounded", (nb, n, m, pts, temp, idx, None, 1, st_)
     _lib.call(name, *args)  # warm
     ev[0].record()
     _lib.call(name, *args)
@@ -442,7 +444,8 @@ def fps_latency(src, dst):
     else:  # Model_V2's 65536-point clouds: one cloud over up to 64 single-wave workgroups
         out["level1"] = _fps_level(pts, 1024, None, None, None, None,
                                    "fps_cluster_kernel (level 1: one cloud over single-wave "
-                                   "workgroups exchanging candidates through L2)")
+                                   "workgroups exchanging candidates through L2; hreg_fps_bounded, "
+                                   "one launch at a time, as the batched stage 1 runs it)")
     for lvl, n, m, T, kern in ((2, 1024, 512, 256, "fps_reg_kernel<256, 4, 1, weighted> (level 2: 4 waves x 4 points)"),
                                (3, 512, 256, 64, "fps_reg_kernel<64, 8, 1, weighted> (level 3: 1 wave x 8 points)")):
         p = pts[:, :n].contiguous()
@@ -821,9 +824,9 @@ def main():
     # result bitwise that of its own batch's forward, the weighted SVD's identity fallback and
     # the prime shuffles per batch); a step is still one batch of --batch pairs
     merge = args.merge if args.merge is not None else (V2_MERGE if v2 else 1)
-    if merge < 1 or args.steps % merge or args.warmup % merge:
-        raise SystemExit(f"bench: --steps {args.steps} / --warmup {args.warmup} are not multiples "
-                         f"of --merge {merge}")
+    if merge < 1 or args.steps % merge:
+        raise SystemExit(f"bench: --steps {args.steps} is not a multiple of --merge {merge}")
+    args.warmup = -(-args.warmup // merge) * merge  # (untimed: rounded up to whole forwards)
     steps_arg = args.steps
     args.steps //= merge  # forwards (of merged batches) from here on; restored for the line
     args.warmup //= merge

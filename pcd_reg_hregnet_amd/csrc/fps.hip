@@ -686,10 +686,23 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
 //
 // `concurrent` (hreg_fps_bounded): the caller guarantees at most that many cluster launches of
 // this process run at once -- a graph whose ONE stage-1 stream runs every multi-workgroup FPS
-// (Model_V2's batched stage 1) passes 1 -- so a launch may spin up to (resident waves) /
-// concurrent, capped at FPS_SPIN_CAP_BOUNDED (leaves 2/3 of the chip's wave slots to the
-// other kernels: 1024 of 3072 at 129 VGPRs).  0: the hardware-queue bound above.
-constexpr int FPS_SPIN_CAP = 256, FPS_SPIN_CAP_BOUNDED = 1024;
+// (Model_V2's batched stage 1) passes 1 -- so a launch may spin up to 3/4 of (resident waves) /
+// concurrent (the quarter kept back is margin for the occupancy API's over-reports,
+// MI355X_MICROARCH.md Residency: every other kernel's waves are finite and drain, so the
+// spinning participants of one launch all become resident once they fit on the chip alone).
+// 0: the hardware-queue bound above.
+#ifndef HREG_FPS_CAP_BOUNDED
+#define HREG_FPS_CAP_BOUNDED 4096
+#endif
+// The fewest slots per lane of a cluster participant (r5): 32 slots = 32 single-wave
+// participants for a 65536-point cloud (253 VGPRs) instead of 64 x 16 slots (129 VGPRs).
+// With the bounded budget of the batched Model_V2 stage 1 every lane's clouds then run at once
+// (64 clouds of 32 waves): Model_V2 line 1410 -> 3279 pairs/s (merge 8, 2 lanes, one box;
+// 16 slots with a 2048-wave cap: 1685).  A/B: 8 (the r4 sizing).
+#ifndef HREG_FPS_CL_SMIN
+#define HREG_FPS_CL_SMIN 32
+#endif
+constexpr int FPS_SPIN_CAP = 256, FPS_SPIN_CAP_BOUNDED = HREG_FPS_CAP_BOUNDED;
 int cluster_wave_budget(int S, bool weighted, int concurrent = 0) {
     static int cache[2][3] = {{-1, -1, -1}, {-1, -1, -1}};  // resident waves of the variant
     const int si = S == 8 ? 0 : S == 16 ? 1 : 2;
@@ -713,7 +726,7 @@ int cluster_wave_budget(int S, bool weighted, int concurrent = 0) {
     }
     if (c <= 0) return 0;
     if (concurrent > 0) {
-        const long b = (long)c / concurrent;
+        const long b = (long)c * 3 / 4 / concurrent;
         return (int)(b < FPS_SPIN_CAP_BOUNDED ? b : FPS_SPIN_CAP_BOUNDED);
     }
     const char *q = getenv("GPU_MAX_HW_QUEUES");
@@ -745,6 +758,7 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
     const long ranks = (long)bs * Q;
     int S = 0;
     for (int s : {8, 16, 32})
+        if (s >= HREG_FPS_CL_SMIN)
         if (ranks <= (long)FPS_CL_MAXP * 64 * s) { S = s; break; }
     const size_t slot_bytes = (size_t)2 * FPS_CL_MAXP * sizeof(SyncSlot);
     const int NP = S ? (int)((ranks + 64L * S - 1) / (64L * S)) : 0;

@@ -56,7 +56,7 @@ PAIR_L2 = switches.flag("PAIR_L2", False)
 # GraphPipeline: level-1 stage of all lanes as one batched launch per kernel (one side
 # stream) instead of one per lane
 BATCH_STAGE1 = switches.flag("BATCH_STAGE1", True)
-V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", False)  # GraphPipeline(v2=True): see bs1
+V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", True)  # GraphPipeline(v2=True): see bs1
 V2_FRONT_STREAM = switches.flag("V2_FRONT_STREAM", False)  # GraphPipeline(v2=True): front streaming
 FRONT_STREAM = switches.flag("FRONT_STREAM", True)  # GraphPipeline: halves of a forward in consecutive rounds
 FRONT_ORDER = switches.integer("FRONT_ORDER", 3)  # per lane: 0 back then front, 1 front then back, 2 by lane parity, 3 on two streams
