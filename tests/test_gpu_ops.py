@@ -477,7 +477,8 @@ def test_fps_cluster_timeout_flags_and_leaves_valid_indices():
     np.testing.assert_array_equal(idx.cpu().numpy(), oracle.fps(x.cpu().numpy(), m, None))
     assert L.device_status(clear=True) == 0
     idx.fill_(-7)
-    L.call("hreg_debug_fps_cluster", B, n, m, x, temp, idx, smp, 3, 2000, L.stream_handle())
+    # (participant 1: at n = 4096 the 32-slot cluster has 2 participants)
+    L.call("hreg_debug_fps_cluster", B, n, m, x, temp, idx, smp, 1, 2000, L.stream_handle())
     torch.cuda.synchronize()
     got = idx.cpu().numpy()
     assert ((got >= 0) & (got < n)).all()
@@ -504,7 +505,7 @@ def test_fps_cluster_timeout_seen_from_side_stream_without_sync():
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        L.call("hreg_debug_fps_cluster", B, n, m, x, temp, idx, smp, 2, 20000, L.stream_handle())
+        L.call("hreg_debug_fps_cluster", B, n, m, x, temp, idx, smp, 1, 20000, L.stream_handle())
     engine._status_pending = True
     with pytest.raises(RuntimeError, match="timed out"):
         engine.check_device_status()

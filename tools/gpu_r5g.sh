@@ -5,7 +5,7 @@ set -o pipefail
 O=gpurun_out/r5g; mkdir -p $O; rm -f $O/*.json
 export TMPDIR=/tmp
 export HREG_PARITY_REPORT=$O/parity_gpu.txt; rm -f $HREG_PARITY_REPORT
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ${PYK:+-k "$PYK"} \
   > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 unset HREG_PARITY_REPORT
@@ -26,4 +26,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/v2t
 B="python3 bench.py --model v2 --steps 16 --warmup 8 --no-cpu-baseline --executor pipeline"
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/v2fetch -o run -- $B > $O/v2fetch.log 2>&1 || { tail -5 $O/v2fetch.log; exit 1; }
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/v2write -o run -- $B > $O/v2write.log 2>&1 || { tail -5 $O/v2write.log; exit 1; }
+bash tools/pmc_kernels.sh pmck > /dev/null 2>&1 || echo "pmc failed"
+head -30 gpurun_out/pmck/summary.txt
 echo done
