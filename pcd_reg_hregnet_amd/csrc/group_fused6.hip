@@ -108,6 +108,57 @@ constexpr bool ring_on() { return HREG_RING && (K::KN == 32 || HREG_RING_L3); }
 template <class K>
 constexpr int ring_wps() { return K::KN == 32 ? HREG_RING_WPS : HREG_RING_WPS_L3; }
 
+// HREG_L2_X2B (level 2 on the ring): mlp1's x2 block batched over the workgroup.  x2 (the
+// k-max row of the descriptor stack, layers.py:204-206) is the same for all 32 rows of a
+// group, so the per-wave block (N3 chunks x TM1 tiles, 96 MFMAs) computes one column 32
+// times.  Batched: the 4 waves' x2 rows go to LDS as the 4 columns of one B operand and the
+// block's TM1 x N3 chunk-tiles are dealt out, one tile and half of the chunks per wave (24
+// MFMAs, 4 ring steps instead of 8); the partial columns meet in LDS and each wave adds its
+// group's (lower-half + upper-half chunks) to mlp1 after the x1d block.
+#ifndef HREG_L2_X2B
+#define HREG_L2_X2B 1
+#endif
+template <class K, bool RING>
+constexpr bool x2b_on() { return HREG_L2_X2B && RING && K::KN == 32 && K::TM1 == 2 && WAVES == 4; }
+
+// the batched x2 block (x2b_on): P (zeroed here) <- this wave's tile (w & 1) of W_x2 over
+// chunks 4 (w >> 1) .. + 3, the B columns = the workgroup's x2 rows (sX[col][channel]).
+// Step s's slot holds tiles {0, 1} x chunks {s, s + 4} (FragSeq tt = 2, cs = 4; the
+// previous call prefetched step 0's); the last step prefetches nf's first chunk.
+template <class K, class R>
+__device__ __forceinline__ void x2_batched(R &ring, int lane, int w, const float *sX, f32x16 &P, FragSeq nf) {
+    constexpr int N3 = K::N3, C3 = K::T3 * 32;
+    static_assert(N3 == 8 && K::TM1 == 2, "x2 block shape");
+    const FragSeq f{K::G_M1, 3 * N3, 2, 4};
+    const int h = lane >> 5;
+    const float *xr = sX + (lane & 3) * C3 + 4 * h;  // B column = lane % 4 (columns 4..31 repeat)
+    P = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of this step landed
+        __syncthreads();
+        const int cur = ring.step & 1;
+        if (s + 1 < 4)
+            ring_fill<4>(ring, cur ^ 1, f, s + 1, lane);
+        else
+            ring_fill<K::TM1>(ring, cur ^ 1, nf, 0, lane);
+        const int c = s + 4 * (w >> 1);  // chunk of the block: channels 16 c + 8 (i >> 2) + 4 h + (i & 3)
+        float x[8];
+        const float4 lo = *reinterpret_cast<const float4 *>(xr + 16 * c);
+        const float4 hi = *reinterpret_cast<const float4 *>(xr + 16 * c + 8);
+        x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w;
+        x[4] = hi.x; x[5] = hi.y; x[6] = hi.z; x[7] = hi.w;
+        u32x4 b[3], a[3];
+        split8(x, b);
+        const lds_cu32x4 *sp = ring.lds + cur * R::SLOT + w * 192 + lane;  // slot tile w = (w & 1, half w >> 1)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = sp[p * 64];
+        P = mma6(a, b, P);
+        __builtin_amdgcn_sched_barrier(0);
+        ++ring.step;
+    }
+}
+
 template <class K, bool PRE, bool RING = false>
 __global__ __launch_bounds__(256, RING ? ring_wps<K>() : K::WPS) void group_fused6_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
@@ -138,6 +189,10 @@ __global__ __launch_bounds__(256, RING ? ring_wps<K>() : K::WPS) void group_fuse
     Carry carry;
     constexpr int RT_TILES = T3 > TM2 ? (T3 > T1 ? T3 : T1) : (TM2 > T1 ? TM2 : T1);
     __shared__ __attribute__((aligned(16))) u32x4 ring_lds[RING ? 2 * RT_TILES * 192 : 1];
+    constexpr bool X2B = x2b_on<K, RING>();
+    static_assert(!X2B || RT_TILES >= 4, "x2 steps: 4 chunk-tiles per slot");
+    __shared__ __attribute__((aligned(16))) float sX[X2B ? WAVES * C3 : 1];       // x2 rows [wave][channel]
+    __shared__ __attribute__((aligned(16))) float sZ[X2B ? WAVES * 4 * 32 : 1];   // partials [wave][column][32]
     Ring6<RT_TILES, WAVES> ring{reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table)),
                                 (lds_u32x4 *)ring_lds, 0, w};
     if constexpr (RING) {
@@ -226,10 +281,47 @@ __global__ __launch_bounds__(256, RING ? ring_wps<K>() : K::WPS) void group_fuse
 #pragma unroll
                 for (int i = 0; i < K::TF / 4; ++i) fin[i] = *reinterpret_cast<const float4 *>(fr2 + 4 * i);
             }
-            conv_stack6<K, TM1, PRE>(wt, eb, K::G_EG, K::G_EF, K::G_E2, K::G_E3, K::E_E1, K::E_E2, K::E_E3,
-                                     lane, gin, fin, PRE ? pr + K::T1 * 32 : nullptr, x1d, cb, m1x2, ca);
+            if constexpr (X2B)  // the next call is the batched x2 block: its first step's 4 chunk-tiles
+                conv_stack6<K, 4, PRE>(wt, eb, K::G_EG, K::G_EF, K::G_E2, K::G_E3, K::E_E1, K::E_E2, K::E_E3,
+                                       lane, gin, fin, PRE ? pr + K::T1 * 32 : nullptr, x1d, cb,
+                                       FragSeq{K::G_M1, 3 * N3, 2, 4}, ca);
+            else
+                conv_stack6<K, TM1, PRE>(wt, eb, K::G_EG, K::G_EF, K::G_E2, K::G_E3, K::E_E1, K::E_E2, K::E_E3,
+                                         lane, gin, fin, PRE ? pr + K::T1 * 32 : nullptr, x1d, cb, m1x2, ca);
         }
 
+        if constexpr (X2B) {
+            // x2 of this wave's group -> sX[w]; the block over the workgroup's 4 columns
+#pragma unroll
+            for (int ct = 0; ct < T3; ++ct) {
+                float v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = x1d[ct][q];
+                reduce_store<32, MaxNN>(sX + w * C3, ct, v, lane);
+            }
+            f32x16 P;
+            x2_batched<K>(ring, lane, w, sX, P, m1x1);
+            if (j < 4) {  // column j's partial (tile w & 1, chunk half w >> 1)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    *reinterpret_cast<float4 *>(sZ + (w * 4 + j) * 32 + 8 * r + 4 * h) =
+                        make_float4(P[4 * r], P[4 * r + 1], P[4 * r + 2], P[4 * r + 3]);
+            }
+            // (the next call's first barrier publishes sZ)
+            mfma_pipe6<N3, TM1, TM2>(wt, lane, m1x1, [&](int st) { return x1d[st >> 4][st & 15]; }, y1, ca, m2,
+                                     cb);
+#pragma unroll
+            for (int t = 0; t < TM1; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float4 za = *reinterpret_cast<const float4 *>(sZ + (t * 4 + w) * 32 + 8 * r + 4 * h);
+                    const float4 zb = *reinterpret_cast<const float4 *>(sZ + ((t + 2) * 4 + w) * 32 + 8 * r + 4 * h);
+                    y1[t][4 * r] = fadd_rn(y1[t][4 * r], fadd_rn(za.x, zb.x));
+                    y1[t][4 * r + 1] = fadd_rn(y1[t][4 * r + 1], fadd_rn(za.y, zb.y));
+                    y1[t][4 * r + 2] = fadd_rn(y1[t][4 * r + 2], fadd_rn(za.z, zb.z));
+                    y1[t][4 * r + 3] = fadd_rn(y1[t][4 * r + 3], fadd_rn(za.w, zb.w));
+                }
+        } else {
 #pragma unroll
         for (int ct = 0; ct < T3; ++ct) {
             float x2[16];
@@ -251,6 +343,7 @@ __global__ __launch_bounds__(256, RING ? ring_wps<K>() : K::WPS) void group_fuse
         }
         static_assert(T3 % 2 == 0, "carry parity");
         mfma_pipe6<N3, TM1, TM2>(wt, lane, m1x1, [&](int st) { return x1d[st >> 4][st & 15]; }, y1, ca, m2, cb);
+        }
         relu_tiles(y1);
 
         // ---- mlp2 + k-max -> descriptor; prefetches the next tile's first chunk

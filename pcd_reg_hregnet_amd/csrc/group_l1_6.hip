@@ -88,6 +88,11 @@ __device__ __forceinline__ void conv_stack6(WP wt, const float *eb, int g1, int 
 #ifndef HREG_L16_WPS
 #define HREG_L16_WPS 2  // waves per SIMD the register budget targets (A/B builds: 3)
 #endif
+// HREG_L1_X2ONE: mlp1's x2 block (the k-max row repeated over the 64 rows, layers.py:204-206)
+// on one row tile's MFMAs instead of both -- 24 of the group's 360 MFMAs fewer
+#ifndef HREG_L1_X2ONE
+#define HREG_L1_X2ONE 1
+#endif
 // LDSW (hreg_group_l1_6): the whole weight-piece table (90 KB) resident in LDS -- each 8-wave
 // workgroup copies it once and loops over 16+ groups; chunk fragments are ds_read_b128
 // (the per-wave weight streams through the vector-memory path keep the CU's texture-data
@@ -205,10 +210,25 @@ __global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : HREG_L16_WPS) voi
             bfly32<MaxNN>(x2[co], lane);
             bcast32(x2[co], lane);
         }
-        pipe6_jt<4, 1, 1, true>(wt, lane, m1x2, [&](int, int st) { return x2[st >> 4][st & 15]; }, y1, ca, m1x1,
-                                cb);
-        pipe6_jt<4, 1, 2, false>(wt, lane, m1x1, [&](int jt, int st) { return x1d[st >> 4][jt][st & 15]; }, y1,
-                                 cb, m2, ca);
+        if constexpr (HREG_L1_X2ONE) {
+            // the x2 block once (its B, and so its product, is the same for both row tiles),
+            // added to both tiles after the x1d block
+            f32x16 z[1][1];
+            z[0][0] = zero16();
+            pipe6_jt<4, 1, 1, true>(wt, lane, m1x2, [&](int, int st) { return x2[st >> 4][st & 15]; }, z, ca,
+                                    m1x1, cb);
+            pipe6_jt<4, 1, 2, false>(wt, lane, m1x1, [&](int jt, int st) { return x1d[st >> 4][jt][st & 15]; },
+                                     y1, cb, m2, ca);
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) y1[0][jt][q] = fadd_rn(y1[0][jt][q], z[0][0][q]);
+        } else {
+            pipe6_jt<4, 1, 1, true>(wt, lane, m1x2, [&](int, int st) { return x2[st >> 4][st & 15]; }, y1, ca,
+                                    m1x1, cb);
+            pipe6_jt<4, 1, 2, false>(wt, lane, m1x1, [&](int jt, int st) { return x1d[st >> 4][jt][st & 15]; },
+                                     y1, cb, m2, ca);
+        }
         relu_jt(y1);
 
         // ---- mlp2: 32 -> 64, k-max -> descriptor; prefetches the next group's first chunk

@@ -352,9 +352,11 @@ __global__ __launch_bounds__(RING ? RING_RT * 256 : 256, RING ? 1 : ONE ? 3 : 2)
 // (64 rows); the epilogue constants are read from the table in global memory (the LDS copy
 // would leave one workgroup per CU), so two 4-wave workgroups fit per CU.  Same products,
 // same order per output as group_split6_kernel (bitwise equal, tests/test_gpu_model.py).
-constexpr int SJT = 2;
+#ifndef HREG_L3_SJT
+#define HREG_L3_SJT 2
+#endif
 
-template <int P, int C>
+template <int P, int C, int SJT>
 __device__ __forceinline__ void beta_pj(const float *ab, int co0, int h, f32x16 (&acc)[P][SJT]) {
 #pragma unroll
     for (int jt = 0; jt < SJT; ++jt)
@@ -368,7 +370,7 @@ __device__ __forceinline__ void beta_pj(const float *ab, int co0, int h, f32x16 
             }
 }
 
-template <int P>
+template <int P, int SJT>
 __device__ __forceinline__ void relu_j(f32x16 (&t)[P][SJT]) {
 #pragma unroll
     for (int i = 0; i < P; ++i)
@@ -378,7 +380,7 @@ __device__ __forceinline__ void relu_j(f32x16 (&t)[P][SJT]) {
             for (int q = 0; q < 16; ++q) t[i][jt][q] = relu_i(t[i][jt][q]);
 }
 
-template <int LDSW, int P>
+template <int LDSW, int P, int SJT>
 __device__ __forceinline__ void put_j(float *buf, int co0, int j, int h, const f32x16 (&t)[P][SJT]) {
 #pragma unroll
     for (int jt = 0; jt < SJT; ++jt)
@@ -387,7 +389,7 @@ __device__ __forceinline__ void put_j(float *buf, int co0, int j, int h, const f
 }
 
 // conv stack [geom | precomputed feature block] -> C1 -> C1 -> C3 on two row tiles
-template <class K, int NP, class WT>
+template <class K, int NP, int SJT, class WT>
 __device__ __forceinline__ void conv_stack_split6j(WT wt, const float *eb, int gg, int g2, int g3, int e2, int e3,
                                                    float *A, int cw, int lane, f32x16 (&out)[K::P3][SJT],
                                                    const Carry6 &cin, FragSeq next, Carry6 &cout,
@@ -422,19 +424,19 @@ __device__ __forceinline__ void conv_stack_split6j(WT wt, const float *eb, int g
     put_j<LDSW>(A, c1, j, h, h1);
     tile_sync();
     f32x16 h2[P1][SJT];
-    beta_pj<P1, K::T1 * 32>(eb + e2, c1, h, h2);
+    beta_pj<P1, K::T1 * 32, SJT>(eb + e2, c1, h, h2);
     pipe_lds6_jt<N1, P1, P3, SJT>(wt, lane, s2, ChanBJ<LDSW>{arow, h}, h2, cb, s3, ca);
     relu_j(h2);
     tile_sync();  // one buffer: every wave has read layer 2's input
     put_j<LDSW>(A, c1, j, h, h2);
     tile_sync();
-    beta_pj<P3, K::T3 * 32>(eb + e3, c3, h, out);
+    beta_pj<P3, K::T3 * 32, SJT>(eb + e3, c3, h, out);
     pipe_lds6_jt<N1, P3, NP, SJT>(wt, lane, s3, ChanBJ<LDSW>{arow, h}, out, ca, next, cout);
     relu_j(out);
 }
 
-template <class K>
-__global__ __launch_bounds__(256, 2) void group_split6j_kernel(
+template <class K, int SJT>
+__global__ __launch_bounds__(256, SJT >= 4 ? 1 : 2) void group_split6j_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     const int32_t *__restrict__ gidx, const float *__restrict__ feats, int G, float *__restrict__ kp,
     float *__restrict__ att_feat, float *__restrict__ desc, const float *__restrict__ pre) {
@@ -450,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void group_split6j_kernel(
     const int lane = threadIdx.x & 63, cw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
     const int NT = G / GPT;
-    const int NPAIR = (NT + 1) / 2;
+    const int NPAIR = (NT + SJT - 1) / SJT;  // row-tile sets of SJT
     float *A = sA;
     const bool writer = KN == 32 ? j == 31 : (j & 15) == 15;
     auto gsum_w = [&](float v) { return KN == 32 ? half_sum_hi(v) : row_sum16(v); };
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(256, 2) void group_split6j_kernel(
         float2 gin[SJT];
 #pragma unroll
         for (int jt = 0; jt < SJT; ++jt) {
-            t[jt] = min(2 * pb + jt, NT - 1);
+            t[jt] = min(SJT * pb + jt, NT - 1);
             g[jt] = t[jt] * GPT + (KN == 32 ? 0 : j >> 4);
             row[jt] = (size_t)t[jt] * 32 + j;
             prow[jt] = pre + (size_t)gidx[row[jt]] * (2 * K::T1 * 32);
@@ -493,7 +495,7 @@ __global__ __launch_bounds__(256, 2) void group_split6j_kernel(
 
         // ---- detector -> emb
         f32x16 emb[P3][SJT];
-        conv_stack_split6j<K, PM1>(wt, eb, K::G_DG, K::G_D2, K::G_D3, K::E_D2, K::E_D3, A, cw, lane, emb, carry,
+        conv_stack_split6j<K, PM1, SJT>(wt, eb, K::G_DG, K::G_D2, K::G_D3, K::E_D2, K::E_D3, A, cw, lane, emb, carry,
                                    m1em, ca, prow, gin);
 
         // ---- attention per tile
@@ -545,14 +547,16 @@ __global__ __launch_bounds__(256, 2) void group_split6j_kernel(
 
         // ---- mlp1, emb * a part (y1 stays in registers through the descriptor stack)
         f32x16 y1[PM1][SJT];
-        beta_pj<PM1, TM1 * 32>(eb + K::E_M1, m1, h, y1);
+        beta_pj<PM1, TM1 * 32, SJT>(eb + K::E_M1, m1, h, y1);
         pipe_lds6_jt<N3, PM1, K::P1, SJT>(wt, lane, m1em, ChanBJ<LDSW>{A + j * LDSW, h}, y1, ca, desc_g, cb);
         tile_sync();  // every wave has read emb * a
 
         // ---- descriptor -> x1d
         f32x16 x1d[P3][SJT];
-        const float *prow_d[SJT] = {prow[0] + K::T1 * 32, prow[1] + K::T1 * 32};
-        conv_stack_split6j<K, PM1>(wt, eb, K::G_EG, K::G_E2, K::G_E3, K::E_E2, K::E_E3, A, cw, lane, x1d, cb, m1x1,
+        const float *prow_d[SJT];
+#pragma unroll
+        for (int jt = 0; jt < SJT; ++jt) prow_d[jt] = prow[jt] + K::T1 * 32;
+        conv_stack_split6j<K, PM1, SJT>(wt, eb, K::G_EG, K::G_E2, K::G_E3, K::E_E2, K::E_E3, A, cw, lane, x1d, cb, m1x1,
                                    ca, prow_d, gin);
         tile_sync();  // every wave has read layer 3's input
 #pragma unroll
@@ -628,7 +632,7 @@ __global__ __launch_bounds__(256, 2) void group_split6j_kernel(
 
         // ---- mlp2 + k-max -> descriptor; prefetches the next pair's first chunk
         f32x16 y2[PM2][SJT];
-        beta_pj<PM2, CM2>(eb + K::E_M2, m2, h, y2);
+        beta_pj<PM2, CM2, SJT>(eb + K::E_M2, m2, h, y2);
         pipe_lds6_jt<NM1, PM2, K::P1, SJT>(wt, lane, fm2, ChanBJ<LDSW>{A + j * LDSW, h}, y2, cb, det_g, carry);
         relu_j(y2);
 #pragma unroll
@@ -702,12 +706,13 @@ extern "C" int hreg_group_split6j_l3(const float *table, const float *geom, cons
         return HREG_ERR_INVALID;
     if (G % K::GPT) return HREG_ERR_INVALID;
     if (!G) return HREG_OK;
-    const int NT = G / K::GPT, NPAIR = (NT + 1) / 2;
-    int grid = NPAIR;
-    const int cap = 256 * 2 * 2;  // two workgroups per CU, two rounds
+    constexpr int SJ = HREG_L3_SJT;
+    const int NT = G / K::GPT, NSET = (NT + SJ - 1) / SJ;
+    int grid = NSET;
+    const int cap = 256 * (SJ >= 4 ? 1 : 2) * 2;  // resident workgroups per CU, two rounds
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(group_split6j_kernel<K>, dim3(grid), dim3(256), 0, as_stream(stream), table, geom, knn_xyz,
-                       gidx, feats, G, kp, att_feat, desc, pre);
+    hipLaunchKernelGGL((group_split6j_kernel<K, SJ>), dim3(grid), dim3(256), 0, as_stream(stream), table, geom,
+                       knn_xyz, gidx, feats, G, kp, att_feat, desc, pre);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

@@ -31,9 +31,13 @@ __device__ __forceinline__ int chan(int co, int q, int h) {
 
 constexpr int CARRY = 16;  // max WIN * COUT_T
 
-// fragment f of call: index base + co * stride + step, in 64-float fragments
+// fragment f of call: index base + co * stride + step, in 64-float fragments.
+// tt > 0 (workgroup rings only, ring_fill): output slot co of a step is tile co % tt at chunk
+// step + (co / tt) * cs -- one step's slot then holds several chunks of the same tiles
+// (group_fused6.hip, the batched x2 block).
 struct FragSeq {
     int base, stride;
+    int tt = 0, cs = 0;
 };
 
 template <int COUT_T>
@@ -433,7 +437,8 @@ __device__ __forceinline__ void ring_fill(R &ring, int slot, FragSeq f, int c, i
         const int i = i0 + ring.w;  // piece i = co * 3 + p of this wave
         if (i < NP) {
             const int co = i / 3, p = i - 3 * co;
-            const gu32x4 *src = ring.wt + (f.base + co * f.stride + c) * 192 + p * 64 + lane;
+            const int fi = f.tt ? f.base + (co % f.tt) * f.stride + c + (co / f.tt) * f.cs : f.base + co * f.stride + c;
+            const gu32x4 *src = ring.wt + fi * 192 + p * 64 + lane;
 #if __HIP_DEVICE_COMPILE__  // (the gfx950 builtin does not exist in the host pass)
             __builtin_amdgcn_global_load_lds(src, ring.lds + slot * R::SLOT + i * 64, 16, 0, 0);
 #else

@@ -26,12 +26,13 @@ struct is_lds_table<const __attribute__((address_space(3))) u32x4 *> {
     static constexpr bool value = true;
 };
 
-template <int NCH, int COUT_T, int NCOUT, bool SAMEB, class BVal, class WP>
+template <int NCH, int COUT_T, int NCOUT, bool SAMEB, class BVal, class WP, int NJ>
 __device__ __forceinline__ void pipe6_jt(WP wt, int lane, FragSeq f, BVal bval,
-                                         f32x16 (&acc)[COUT_T][JT], const Carry &cin, FragSeq nf,
+                                         f32x16 (&acc)[COUT_T][NJ], const Carry &cin, FragSeq nf,
                                          Carry &cout) {
+    // NJ: row tiles (JT; 1 for a block whose B is the same for every row, group_l1_6.hip x2)
     static_assert(COUT_T <= CARRY6 && NCOUT <= CARRY6, "carry");
-    constexpr int NB = SAMEB ? 1 : JT;
+    constexpr int NB = SAMEB ? 1 : NJ;
     u32x4 buf[2][COUT_T][3];
 #pragma unroll
     for (int co = 0; co < COUT_T; ++co)
@@ -66,12 +67,12 @@ __device__ __forceinline__ void pipe6_jt(WP wt, int lane, FragSeq f, BVal bval,
 #pragma unroll
         for (int co = 0; co < COUT_T; ++co)
 #pragma unroll
-            for (int jt = 0; jt < JT; ++jt)
+            for (int jt = 0; jt < NJ; ++jt)
                 acc[co][jt] = mma6(buf[c & 1][co], b[c & 1][SAMEB ? 0 : jt], acc[co][jt]);
         if constexpr (HREG_SWP) {
             if (c + 1 < NCH) {  // next chunk's split in this chunk's MFMA shadow (mfma_chain.h)
                 split_jt(c + 1, b[(c + 1) & 1]);
-                interleave_mfma_valu<6 * COUT_T * JT, 48 * NB>();
+                interleave_mfma_valu<6 * COUT_T * NJ, 48 * NB>();
             }
         }
         if (!HREG_SWP || c + 1 < NCH) __builtin_amdgcn_sched_barrier(0);
