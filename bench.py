@@ -265,7 +265,7 @@ class MfmaTimer:
         out = {}
         for name, (ev, fl) in sorted(self.by_entry.items()):
             ms = sum(a.elapsed_time(b) for a, b in ev)
-            out[name] = {"launches_per_step": len(ev) // max(steps, 1),
+            out[name] = {"launches_per_step": round(len(ev) / max(steps, 1), 3),
                          "avg_launch_us": round(ms / max(len(ev), 1) * 1e3, 2),
                          "tflops": round(fl / max(ms, 1e-9) / 1e9, 2),
                          "peak": entry_peak(name), "_ms": ms, "_flops": fl}
@@ -300,7 +300,8 @@ def level_kernel(engine, lv: int) -> str:
 def pmc_traffic(kernel: str, workload: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of THIS
     workload (the Model_V2 line had borrowed the 16384-point pass):
-    profiles/r*_traffic.json keyed by workload ("hregnet:b8:n16384", "v2:b2:n65536"; made by
+    profiles/r*_traffic.json keyed by workload ("hregnet:b8:n16384", "v2:b2:n65536:m8" -- m: reference
+    batches merged per launch; made by
     tools/rocpd_summary.py traffic ... --key); the r1-r4 files hold the configs[1] pass alone.
     The latest round that measured every kernel of the family; (None, None) when no pass of
     this workload exists."""
@@ -952,7 +953,7 @@ def main():
     if rank == 0:
         def kind_summary(k):
             ms, n, fl, nb, xf = res[k]
-            return {"launches_per_step": n // args.steps,
+            return {"launches_per_step": round(n / args.steps, 3),
                     "avg_launch_us": round(ms / max(n, 1) * 1e3, 2),
                     "ms_per_step": round(ms / args.steps, 3),
                     "tflops": round(fl / max(ms, 1e-9) / 1e9, 2),
@@ -970,8 +971,8 @@ def main():
         # the family's peak: its FLOPs over the time they need at each kernel's own peak
         t_peak = sum(e["_flops"] / (e["peak"] * 1e12) for e in lev.values())
         peak = sum(e["_flops"] for e in lev.values()) / t_peak / 1e12 if t_peak else PEAK_B6_TFLOPS
-        traffic, traffic_src = pmc_traffic(" + ".join(level_names),
-                                           f"{args.model}:b{B}:n{args.points}")
+        traffic, traffic_src = pmc_traffic(" + ".join(level_names), f"{args.model}:b{B}:n{args.points}"
+                                           + (f":m{merge}" if merge > 1 else ""))
         tot_ms = sum(r[0] for r in res.values())
         tot_xf = sum(r[4] for r in res.values())
         alg_fl = ALG_GFLOP_PER_PAIR * 1e9 * B * args.steps
@@ -995,7 +996,7 @@ def main():
                 "flop_per_launch": round(per_launch_flops),
                 "executed_flop_per_launch": round(f_xf / max(f_n, 1)),
                 "executed_tflops": round(f_xf / max(f_ms, 1e-9) / 1e9, 3),
-                "launches_per_step": f_n // args.steps,
+                "launches_per_step": round(f_n / args.steps, 3),
                 "avg_launch_us": round(per_launch_s * 1e6, 2),
                 "other_mfma_kernels": {"gemm_nt_kernel": kind_summary("gemm"),
                                        "fine/nbr head kernels": kind_summary("head"),

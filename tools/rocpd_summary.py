@@ -7,7 +7,8 @@
                  run (warm-up, capture, graph replays, instrumented eager pass) is counted once
                  and divided by the number of forwards that made it (VERDICT r3 weak item 9:
                  dividing ~100 launches per kernel by the 48 timed steps overstated ms/step)
-  HBM traffic:   python tools/rocpd_summary.py traffic <fetch .db|csv> <write .db|csv> [out.md] [out.json]
+  HBM traffic:   python tools/rocpd_summary.py traffic <fetch .db|csv> <write .db|csv> [out.md] [out.json] [key]
+                 key: the workload ("v2:b2:n65536", "hregnet:b8:n16384"): out.json keeps one entry per key
   MFMA use:      python tools/rocpd_summary.py mfma <counter_collection.csv> [out.md] [out.json]
 
 Traffic follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE come
@@ -90,7 +91,7 @@ def stats(path, steps, out=None):
         open(out, "w").write(text + "\n")
 
 
-def traffic(fetch_path, write_path, out=None, out_json=None):
+def traffic(fetch_path, write_path, out=None, out_json=None, key=None):
     fetch = counter_values(fetch_path, "FETCH_SIZE")
     write = counter_values(write_path, "WRITE_SIZE")
     lines = ["| kernel | launches | read MB/launch (2 x FETCH_SIZE) | write MB/launch | HBM MB/launch |",
@@ -114,10 +115,16 @@ def traffic(fetch_path, write_path, out=None, out_json=None):
     if out:
         open(out, "w").write(text + "\n")
     if out_json:
-        json.dump({"bytes_per_launch": fam_bytes, "fetch_source": fetch_path,
-                   "write_source": write_path,
-                   "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024, per-launch mean over the family"},
-                  open(out_json, "w"), indent=1)
+        entry = {"bytes_per_launch": fam_bytes, "fetch_source": fetch_path, "write_source": write_path,
+                 "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024, per-launch mean over the family"}
+        if key:  # one entry per workload (bench.pmc_traffic reads the workload's own pass)
+            try:
+                doc = json.load(open(out_json))
+            except (OSError, ValueError):
+                doc = {}
+            doc[key] = entry
+            entry = doc
+        json.dump(entry, open(out_json, "w"), indent=1, sort_keys=True)
 
 
 CU_NUM = 256
@@ -214,4 +221,4 @@ if __name__ == "__main__":
         stats(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None)
     else:
         traffic(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None,
-                sys.argv[5] if len(sys.argv) > 5 else None)
+                sys.argv[5] if len(sys.argv) > 5 else None, sys.argv[6] if len(sys.argv) > 6 else None)
