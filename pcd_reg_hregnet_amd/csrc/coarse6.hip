@@ -19,6 +19,10 @@
 // pieces stream from the L2-resident table (engine.coarse_head_table6) one chunk ahead.
 // The channel max of the attention is reduced per wave, then across the 8 waves through
 // LDS; the reductions over a keypoint's 8 rows are 3 DPP steps.
+// chunk c + 1's B split under chunk c's MFMAs in pipe_lds6_jt (split_chain.h): the heads
+// measured 127.8 -> 123.5 (CoarseReg), 56.4 -> 54.2 (FineReg), 66.4 -> 64.4 us (neighbour
+// branch) eager; level 3's group_split6j (same pipe) neutral, so it stays off there
+#define HREG_SPLIT_SWP 1
 #include "split_chain.h"
 
 namespace {

@@ -300,6 +300,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         if constexpr (NW == 1) {
             // one wave: its winner is the block winner, no LDS round trip or barrier; no
             // d2 > -1 anywhere: the reference keeps (best=-1, besti=0) (selects, no branch)
+            if constexpr (STAMP) t3 = t2;  // (no barrier phase)
             const bool any = wmax > -1.0f;
             old = any ? kwin : 0;
             x1 = any ? wx : x0;

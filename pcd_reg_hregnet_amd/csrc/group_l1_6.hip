@@ -93,6 +93,11 @@ __device__ __forceinline__ void conv_stack6(WP wt, const float *eb, int g1, int 
 #ifndef HREG_L1_X2ONE
 #define HREG_L1_X2ONE 1
 #endif
+// HREG_L1_PRIO: the second half of the 8-wave workgroup (each SIMD's younger wave) at
+// s_setprio 1 for the whole kernel (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+#ifndef HREG_L1_PRIO
+#define HREG_L1_PRIO 0
+#endif
 // LDSW (hreg_group_l1_6): the whole weight-piece table (90 KB) resident in LDS -- each 8-wave
 // workgroup copies it once and loops over 16+ groups; chunk fragments are ds_read_b128
 // (the per-wave weight streams through the vector-memory path keep the CU's texture-data
@@ -123,6 +128,9 @@ __global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : HREG_L16_WPS) voi
     __syncthreads();
     const float *eb = LDSW ? table : ep - F_END;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if constexpr (HREG_L1_PRIO && LDSW) {
+        if (w >= 4) __builtin_amdgcn_s_setprio(1);
+    }
     const int h = lane >> 5, j = lane & 31;
     const FragSeq m1x2{G_M1, 12}, m1x1{G_M1 + 4, 12}, m1em{G_M1 + 8, 12}, m2{G_M2, 2};
     // opaque per-group table pointer: keeps the loop-invariant weight loads in the loop

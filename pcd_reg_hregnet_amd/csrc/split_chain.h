@@ -136,6 +136,11 @@ __device__ __forceinline__ void pipe_lds6(const gu32x4 *__restrict__ wt, int lan
     }
 }
 
+// HREG_SPLIT_SWP: pipe_lds6_jt splits chunk c + 1's B under chunk c's MFMAs
+#ifndef HREG_SPLIT_SWP
+#define HREG_SPLIT_SWP 0
+#endif
+
 // pipe_lds6 over JT row tiles: each chunk's weight pieces (P tiles) feed the MFMAs of
 // every row tile (JT x fewer weight bytes per MFMA); B of row tile jt through bl(jt, st0, v)
 template <int NCH, int P, int NP, int JT, class BL>
@@ -161,6 +166,35 @@ __device__ __forceinline__ void pipe_lds6_jt(const gu32x4 *__restrict__ wt, int 
         }
     };
     ldb(0, bb[0]);
+    if constexpr (HREG_SPLIT_SWP) {
+        // chunk c + 1's B split in chunk c's MFMA shadow (mfma_chain.h HREG_SWP), the VALU
+        // placed between the MFMAs by sched_group_barrier
+        u32x4 bs[2][JT][3];
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) split8(bb[0][jt], bs[0][jt]);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if (c + 1 < NCH) {
+#pragma unroll
+                for (int i = 0; i < P; ++i) ld6(wt, f.base + i * f.stride + c + 1, lane, abuf[(c + 1) & 1][i]);
+                ldb(c + 1, bb[(c + 1) & 1]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NP; ++i) ld6(wt, nf.base + i * nf.stride, lane, cout[i]);
+            }
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int i = 0; i < P; ++i) acc[i][jt] = mma6(abuf[c & 1][i], bs[c & 1][jt], acc[i][jt]);
+            if (c + 1 < NCH) {
+#pragma unroll
+                for (int jt = 0; jt < JT; ++jt) split8(bb[(c + 1) & 1][jt], bs[(c + 1) & 1][jt]);
+                interleave_mfma_valu<6 * P * JT, 44 * JT>();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+    }
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         if (c + 1 < NCH) {
