@@ -172,6 +172,7 @@ MFMA_ENTRIES = {
     "hreg_group_split6_l2": ("level", _level_work(2)),
     "hreg_group_split6_l3": ("level", _level_work(3)),
     "hreg_group_split6j_l3": ("level", _level_work(3)),
+    "hreg_group_split6p_l3": ("level", _level_work(3)),
     "hreg_group6_l3": ("level", _level_work(3)),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
@@ -289,6 +290,8 @@ def level_kernel(engine, lv: int) -> str:
     split = engine.SPLIT_L2 if lv == 2 else engine.SPLIT_L3
     b6 = engine.B6_L2 if lv == 2 else engine.B6_L3
     if split:
+        if b6 and lv == 3 and engine.L3_PIECES and engine.LEVEL_PRE:
+            return "group_split6p_kernel"  # activations as bf16x6 pieces in LDS (csrc/group_split6.hip)
         if b6 and lv == 3 and engine.SPLIT_JT and engine.LEVEL_PRE:
             return "group_split6j_kernel"  # two row tiles per workgroup (csrc/group_split6.hip)
         return "group_split6_kernel" if b6 else "group_split_kernel"
@@ -931,6 +934,7 @@ def main():
     timer.enabled = args.executor != "graph"
     t0 = time.perf_counter()
     out = run(args.steps)
+    host_submit_s = time.perf_counter() - t0  # the host's share: launches / replays submitted
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1036,6 +1040,7 @@ def main():
                        else "point-cloud pairs/sec, HRegNet forward, 16384-pt pairs"),
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "host_submit_ms": round(host_submit_s * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "precision": "fp32 throughout; the fused level and head kernels take their fp32 "
                          "products on the bf16 matrix cores as 3-piece exact splits (bf16x6, "

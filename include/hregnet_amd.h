@@ -563,6 +563,13 @@ int hreg_group_split6_l3_table_floats(void);
 int hreg_group_split6j_l3(const float *table, const float *geom, const float *knn_xyz,
                           const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                           float *desc, const float *pre, void *stream);
+/* hreg_group_split6_l3 in the pieces form: activations kept in LDS as their bf16x6 pieces, split
+ * once by the wave that produced them (8-wave workgroups of two 32-row tiles); the same table;
+ * keypoints and attentive features bitwise hreg_group_split6j_l3's, descriptors to fp32 rounding
+ * (mlp1 summed as two K-half partials); pre required */
+int hreg_group_split6p_l3(const float *table, const float *geom, const float *knn_xyz,
+                          const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
+                          float *desc, const float *pre, void *stream);
 int hreg_group_split6_l3(const float *table, const float *geom, const float *knn_xyz,
                          const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                          float *desc, const float *pre, void *stream);

@@ -43,6 +43,9 @@ SPLIT_L2 = switches.flag("SPLIT_L2", False)
 SPLIT_L3 = switches.flag("SPLIT_L3", True)
 # level 3 on the two-row-tile form of the channel-split kernel (hreg_group_split6j_l3)
 SPLIT_JT = True
+# level 3 on the pieces form (hreg_group_split6p_l3: activations split into bf16 pieces once by
+# their producer and stored in LDS as pieces; 8-wave workgroups; group_split6.hip)
+L3_PIECES = switches.flag("L3_PIECES", False)
 # 32-row tiles per workgroup of the channel-split FineReg / neighbour heads (0: the library's
 # default, two at N1 <= 256; hreg_corr_head6x / hreg_nbr_head6sx)
 HEAD_ROW_TILES = 0
@@ -995,8 +998,8 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
                       "hreg_group_split6_l3")
         pre = (gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl],
                     feats.shape[0]) if LEVEL_PRE else None)
-        if name == "hreg_group_split6_l3" and pre is not None and SPLIT_JT:
-            name = "hreg_group_split6j_l3"
+        if name == "hreg_group_split6_l3" and pre is not None and (SPLIT_JT or L3_PIECES):
+            name = "hreg_group_split6p_l3" if L3_PIECES else "hreg_group_split6j_l3"
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())
         sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)

@@ -791,6 +791,40 @@ def test_b6_kernels_deterministic(net):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("G", [4096, 4094, 2, 20000])
+def test_level3_pieces_kernel(net, G):
+    """hreg_group_split6p_l3 (activations kept in LDS as their bf16x6 pieces, split once by the
+    producing wave) against hreg_group_split6j_l3 on the same rows: the same products per output
+    up to mlp1, so keypoints and attentive features are bitwise equal; mlp1 is summed as two
+    K-half partials, so the descriptors agree to fp32 rounding (1e-4 relative, the fused-kernel
+    bar).  An odd tile count (4094: the last pair recomputes its tile), a single tile, and more
+    tile pairs than one pass of the capped grid (20000)."""
+    from pcd_reg_hregnet_amd import _lib, engine
+    P = net.prepared(torch.device("cuda"))
+    g = torch.Generator(device="cpu").manual_seed(G + 7)
+    K, C, nrows = 16, 128, 2 * G
+    R = G * K
+    geom = torch.randn(R, 4, generator=g).cuda()
+    kx = torch.randn(R, 3, generator=g).cuda()
+    gidx = torch.randint(0, nrows, (R,), generator=g, dtype=torch.int32).cuda()
+    feats = torch.rand(nrows, C, generator=g).cuda()
+    pre = engine.gemm([engine._seg(feats, 0, C)], P.level_pre6[2], nrows)
+    outs = []
+    for name in ("hreg_group_split6j_l3", "hreg_group_split6p_l3"):
+        kp = torch.full((G, 3), float("nan"), device="cuda")
+        att = torch.full((G, 256), float("nan"), device="cuda")
+        desc = torch.full((G, 256), float("nan"), device="cuda")
+        _lib.call(name, P.l3s_table6, geom, kx, gidx, feats, G, kp, att, desc, pre, _lib.stream_handle())
+        outs.append((kp, att, desc))
+    torch.cuda.synchronize()
+    for i, (a, b, nm) in enumerate(zip(outs[0], outs[1], ("kp", "att_feat", "desc"))):
+        assert not torch.isnan(b).any(), nm
+        if i < 2:
+            assert torch.equal(a, b), nm
+        else:
+            torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
+
+
 @pytest.mark.parametrize("G", [4096, 4094, 4090, 2])
 def test_level3_two_tile_kernel_bitwise(net, G):
     """hreg_group_split6j_l3 (HREG_L3_SJT 32-row tiles per wave sharing every weight piece)

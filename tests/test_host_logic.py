@@ -343,7 +343,8 @@ def test_bench_entry_peaks():
     hreg_nbr_head6sx were priced at the fp32 peak (roofline.frac 0.71 instead of 0.45)."""
     import bench
     b6 = {"hreg_group_l1_6", "hreg_group_l1_6g", "hreg_group6_l2", "hreg_group6x2_l2",
-          "hreg_group_split6_l2", "hreg_group_split6_l3", "hreg_group_split6j_l3", "hreg_group6_l3",
+          "hreg_group_split6_l2", "hreg_group_split6_l3", "hreg_group_split6j_l3", "hreg_group_split6p_l3",
+          "hreg_group6_l3",
           "hreg_fine_head6", "hreg_nbr_head6", "hreg_nbr_head6s", "hreg_nbr_head6sx",
           "hreg_coarse_head6", "hreg_corr_head6", "hreg_corr_head6x", "hreg_mlp_head6", "hreg_gemm6"}
     for name in set(bench.MFMA_ENTRIES) | {"hreg_gemm", "hreg_gemm6"}:

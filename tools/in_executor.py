@@ -17,7 +17,7 @@ import json
 import os
 import sys
 
-LEVEL_KERNELS = ("group_l1_6_kernel", "group_fused6_kernel", "group_split6j_kernel")
+LEVEL_KERNELS = ("group_l1_6_kernel", "group_fused6_kernel", "group_split6j_kernel", "group_split6p_kernel")
 
 
 def short(name):
@@ -38,6 +38,8 @@ def main():
     per = {}
     for k in LEVEL_KERNELS:
         ds = [(e - s) / 1e3 for s, e, n in rows if n == k]
+        if not ds:  # (one level-3 form runs: split6j or split6p)
+            continue
         if len(ds) < steps:
             raise SystemExit(f"{k}: {len(ds)} dispatches < {steps}")
         last = ds[-steps:]
