@@ -45,6 +45,11 @@ V2_POINTS = 65536      # config 5 (MANTruckScenes-shape): B=16 over 8 GPUs -> 2 
 V2_PAIRS_PER_GPU = 2
 V2_LANES = 2           # Model_V2 graph executor: lanes (forwards in flight)
 V2_MERGE = 8           # Model_V2: reference batches merged per forward (--merge)
+# HRegNet line: reference batches of 8 pairs merged per executor forward (the largest divisor of
+# --steps up to this).  Paired lines (one box, gpurun_out/r5m): --steps 20 on merge 1 / 2 / 4 /
+# 5 / 10 / 20: 7391 / 7518 / 7797 / 7716 / 7768 / 6901 pairs/s; --steps 48 on 1 / 4 / 6 / 8:
+# 7570 / 8024 / 7779 / 7672
+HREGNET_MERGE = 4
 
 
 class _Args:
@@ -773,7 +778,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--merge", type=int, default=None,
                     help="reference batches (of --batch pairs) per executor forward, one launch set "
-                         f"(default 1; {V2_MERGE} for v2); a step is still one batch")
+                         f"(default: the largest divisor of --steps up to {HREGNET_MERGE}, {V2_MERGE} "
+                         "for v2); a step is still one batch")
     ap.add_argument("--train-eager", action="store_true",
                     help="--model train: launch the step eagerly instead of replaying captured graphs")
     ap.add_argument("--train-graph-ddp", action="store_true",
@@ -823,11 +829,17 @@ def main():
         args.batch = V2_PAIRS_PER_GPU if v2 else PAIRS_PER_GPU
     if args.points is None:
         args.points = V2_POINTS if v2 else POINTS
-    # --merge M (Model_V2 line): each forward of the executor runs M reference batches of
+    # --merge M: each forward of the executor runs M reference batches of
     # --batch pairs merged into one launch set (engine.hregnet_forward sub_batch: every pair's
     # result bitwise that of its own batch's forward, the weighted SVD's identity fallback and
     # the prime shuffles per batch); a step is still one batch of --batch pairs
-    merge = args.merge if args.merge is not None else (V2_MERGE if v2 else 1)
+    if args.merge is None:
+        # the default: the largest divisor of --steps up to the model's merge factor (a step
+        # count the factor does not divide still times exactly --steps batches)
+        cap = V2_MERGE if v2 else HREGNET_MERGE
+        merge = max(m for m in range(1, cap + 1) if args.steps % m == 0)
+    else:
+        merge = args.merge
     if merge < 1 or args.steps % merge:
         raise SystemExit(f"bench: --steps {args.steps} is not a multiple of --merge {merge}")
     args.warmup = -(-args.warmup // merge) * merge  # (untimed: rounded up to whole forwards)
@@ -1057,8 +1069,9 @@ def main():
                                    f", {args.lanes} forwards in flight" if args.lanes > 1 and
                                    args.executor == "graph" else "") + (
                                    f"; {merge} batches of {B} pairs merged per forward (one launch "
-                                   "set; per-batch SVD fallback and prime shuffles)" if merge > 1
-                                   else "") + (
+                                   "set, every batch's outputs bitwise its own forward's; per-batch "
+                                   "SVD fallback" + (" and prime shuffles" if v2 else "") + ")"
+                                   if merge > 1 else "") + (
                                    "; batched stage 1 (one bounded-concurrency cluster-FPS launch "
                                    "over every lane's clouds)" if gpipe is not None and gpipe.bs1
                                    and args.points > 16384 else "") + (
@@ -1066,7 +1079,7 @@ def main():
                                    "half of its batches and the feature extraction of the next "
                                    "round's (pipeline primed after the warm-up)"
                                    if gpipe is not None and gpipe.fs else ""),
-                       "global_batch": B * world, "points": args.points,
+                       "global_batch": B * world, "points": args.points, "merge": merge,
                        "parallelism": f"dp{world} (pairs sharded, no collective)"},
             "roofline": roof,
             "fps": fps,

@@ -238,6 +238,37 @@ def test_graph_lanes_match_eager(net):
                 assert torch.equal(out["src_feats"]["desc_3"], ref["src_feats"]["desc_3"])
 
 
+def test_graph_merged_batches_match_eager(net):
+    """The bench's HRegNet executor with reference batches merged per forward (bench --merge,
+    engine.hregnet_forward sub_batch): two lanes, each forward running two batches of 2 pairs
+    as one launch set, streamed rounds with and without front streaming -- every batch's outputs
+    bitwise its own eager forward."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    data = [synthetic.lidar_batch(4, 4096, seed0=sd)[:2] for sd in (63, 64)]
+    dev = [(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()) for s, d in data]
+    with torch.no_grad():
+        gp = engine.GraphPipeline(P, dev[0][0], dev[0][1], lanes=2, sub_batch=2)
+        gp.load(dev[1][0], dev[1][1], lane=1)
+        refs = [[engine.hregnet_forward(P, s[i:i + 2], d[i:i + 2]) for i in (0, 2)] for s, d in dev]
+        plan = [(2, False), (4, False), (2, True), (4, True)]  # (front streaming after prime())
+        for n, front in plan:
+            gp.prepare(n)
+            if front:
+                gp.prime()
+                assert gp.fready is not None
+            outs = gp.run_forwards(n, stream=True)
+            torch.cuda.synchronize()
+            for out, ref in zip(outs, refs):
+                for k, r in enumerate(ref):
+                    b = slice(2 * k, 2 * k + 2)
+                    for i in range(3):
+                        assert torch.equal(out["rotation"][i][b], r["rotation"][i])
+                        assert torch.equal(out["translation"][i][b], r["translation"][i])
+                    assert torch.equal(out["src_xyz_corres_1"][b], r["src_xyz_corres_1"])
+                    assert torch.equal(out["src_feats"]["desc_3"][b], r["src_feats"]["desc_3"])
+
+
 def test_graph_partial_round_matches_eager(net):
     """run_forwards(n) with n not a multiple of the lanes: full rounds, then a partial
     round on the first lanes; every lane's last output is bitwise its eager forward."""
