@@ -503,14 +503,15 @@ def forward_latency(P, src, dst, reps: int = 7):
                      "graph = 1-lane GraphPipeline (stage-1 graph + rest-of-forward graph)"}
 
 
-def in_executor(steps: int, B: int, points: int, entries_flops: dict):
+def in_executor(steps: int, B: int, points: int, entries_flops: dict, merge: int = 1):
     """roofline of the level family inside the timed graph executor: the
     level kernels' mean durations over the timed region's dispatches, from the committed
     rocprofv3 kernel trace of `bench.py --steps S --warmup W --no-eager-roofline`
     (tools/in_executor.py -> profiles/r*_in_executor.json, keyed by workload), against the
     same algorithmic FLOPs per launch as the eager figure.  None when no trace of this
-    workload is committed."""
-    key = f"hregnet:b{B}:n{points}:s{steps}"
+    workload is committed (key: batch, points, timed steps and merge factor; the timed region
+    holds steps / merge launches of each level kernel)."""
+    key = f"hregnet:b{B}:n{points}:s{steps}" + (f":m{merge}" if merge > 1 else "")
     for rnd in ("r5",):
         path = os.path.join(REPO, "profiles", f"{rnd}_in_executor.json")
         try:
@@ -528,9 +529,18 @@ def in_executor(steps: int, B: int, points: int, entries_flops: dict):
             t += us
             fl += f
         ach = fl / t / 1e6
-        return {"achieved": round(ach, 3), "frac": round(ach / PEAK_B6_TFLOPS, 4),
-                "per_kernel": per, "source": os.path.relpath(path, REPO),
-                "dispatches": d.get("dispatches"), "tree": d.get("tree")}
+        out = {"achieved": round(ach, 3), "frac": round(ach / PEAK_B6_TFLOPS, 4),
+               "basis": "one launch of each level kernel: FLOPs over the sum of their mean "
+                        "in-executor durations (each kernel shares the chip with the round's "
+                        "other lanes, so this under-states the family's rate)",
+               "per_kernel": per, "source": os.path.relpath(path, REPO),
+               "dispatches": d.get("dispatches"), "tree": d.get("tree")}
+        if d.get("union_us"):
+            # every timed launch's FLOPs over the time any of them was running
+            ach_u = fl * d["dispatches"] / d["union_us"] / 1e6
+            out.update({"achieved_union": round(ach_u, 3), "frac_union": round(ach_u / PEAK_B6_TFLOPS, 4),
+                        "union_us": d["union_us"]})
+        return out
     return None
 
 
@@ -1025,20 +1035,24 @@ def main():
                              "executed_tflops": round(tot_xf / max(tot_ms, 1e-9) / 1e9, 2)}}
         # level-kernel FLOPs per launch at this batch (groups = 2B clouds x the level's
         # keypoints), by rocprof kernel name: the in-executor figure's numerators
-        lv_fl = {level_kernel(engine, 1): L1_FLOPS_PER_GROUP * 2 * B * engine.LEVELS[0][0],
-                 level_kernel(engine, 2): L2_FLOPS_PER_GROUP * 2 * B * engine.LEVELS[1][0],
-                 level_kernel(engine, 3): L3_FLOPS_PER_GROUP * 2 * B * engine.LEVELS[2][0]}
+        # (a launch covers the `merge` batches of one executor forward)
+        lv_fl = {level_kernel(engine, 1): L1_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[0][0],
+                 level_kernel(engine, 2): L2_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[1][0],
+                 level_kernel(engine, 3): L3_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[2][0]}
         if not v2 and args.executor == "graph":
-            roof["in_executor"] = in_executor(args.steps, B, args.points, lv_fl)
+            roof["in_executor"] = in_executor(args.steps, B, args.points, lv_fl, merge)
+        # the whole timed step: every MFMA family's algorithmic FLOPs per pair x pairs/s
+        roof["step_tflops"] = round(ALG_GFLOP_PER_PAIR * value / 1e3, 2)
+        roof["step_frac"] = round(ALG_GFLOP_PER_PAIR * value / 1e3 / PEAK_B6_TFLOPS, 4)
         fps = None
         try:
-            fps = fps_latency(src, dst)
+            fps = fps_latency(src[:B], dst[:B])
         except Exception as e:  # a diagnostic must never sink the GPU number
             fps = {"error": repr(e)}
         lat = None
         if not v2 and not args.no_latency:
             try:
-                lat = forward_latency(P, src, dst)
+                lat = forward_latency(P, src[:B], dst[:B])
             except Exception as e:  # a diagnostic must never sink the GPU number
                 lat = {"error": repr(e)}
         cpu = None

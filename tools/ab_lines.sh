@@ -1,7 +1,7 @@
 #!/bin/bash
 # Paired bench lines, alternating the current tree and variants (HREG_LIB / HREG_SWITCHES), after
 # an optional pytest -k selection.   bash tools/ab_lines.sh TAG REPS "BENCH ARGS" [TESTS|-] VARIANT...
-#   VARIANT: lib:<file in pcd_reg_hregnet_amd/> | sw:NAME=V[,NAME=V]     (outputs gpurun_out/TAG/)
+#   VARIANT: lib:<file in pcd_reg_hregnet_amd/> | sw:NAME=V[,NAME=V] | env:NAME=V   (outputs gpurun_out/TAG/)
 # Prints value, ms/step, roofline frac, single-batch latency and per-level FPS us/iteration.
 set -o pipefail
 TAG=$1; REPS=$2; BARGS=$3; TESTS=$4; shift 4
@@ -13,10 +13,10 @@ if [ "$TESTS" != "-" ]; then
 fi
 for r in $(seq 1 $REPS); do
   for v in base "$@"; do
-    L=""; S=""
-    case $v in lib:*) L=$PWD/pcd_reg_hregnet_amd/${v#lib:};; sw:*) S=${v#sw:};; esac
+    L=""; S=""; E="AB_VARIANT=0"
+    case $v in lib:*) L=$PWD/pcd_reg_hregnet_amd/${v#lib:};; sw:*) S=${v#sw:};; env:*) E=${v#env:};; esac
     tag=$(echo $v | tr ':=,/' '____')
-    HREG_LIB=$L HREG_SWITCHES=$S timeout -k 10 300 python bench.py --no-cpu-baseline $BARGS > $O/$tag.$r.json 2> $O/$tag.$r.err || { tail $O/$tag.$r.err; exit 1; }
+    env $E HREG_LIB=$L HREG_SWITCHES=$S timeout -k 10 300 python bench.py --no-cpu-baseline $BARGS > $O/$tag.$r.json 2> $O/$tag.$r.err || { tail $O/$tag.$r.err; exit 1; }
   done
 done
 python - "$O" <<'P'

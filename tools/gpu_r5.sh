@@ -30,7 +30,9 @@ if [[ $PARTS == *x* ]]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/xtrace -o run -- \
     python3 bench.py --steps 20 --warmup 5 --no-eager-roofline --no-latency --no-cpu-baseline \
     > $O/xtrace.log 2>&1 || { echo xtrace failed; tail $O/xtrace.log; exit 1; }
-  python tools/in_executor.py $O/xtrace hregnet:b8:n16384:s20 20 $O/in_executor.json > $O/in_executor.log 2>&1 \
+  M=$(python -c "import json; print(json.load(open('$O/bench20.json'))['config'].get('merge', 1))" 2>/dev/null || echo 4)
+  K=hregnet:b8:n16384:s20; [ "$M" -gt 1 ] && K=$K:m$M
+  python tools/in_executor.py $O/xtrace $K $((20 / M)) $O/in_executor.json > $O/in_executor.log 2>&1 \
     || { tail $O/in_executor.log; }
 fi
 if [[ $PARTS == *v* ]]; then
