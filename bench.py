@@ -695,7 +695,7 @@ def bench_train(args, world, rank, device):
             "config": {"workload": f"HRegNet train step (train-mode BN, 3-level "
                                    f"transformation_loss, backward, Adam), batch={B} pairs/GPU, "
                                    f"2x{args.points}-pt pairs (BASELINE configs[3])",
-                       "global_batch": B * world, "points": args.points, "merge": merge,
+                       "global_batch": B * world, "points": args.points,
                        "parallelism": f"dp{world} (one 9.87 MB gradient all-reduce per step)"},
             "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
             "executor": "HIP graphs (two captured steps, ping-pong inputs)" if graphed else "eager",
