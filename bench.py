@@ -44,11 +44,13 @@ LANES_MAX = 48         # graph executor: most batches in flight (memory: one for
 V2_POINTS = 65536      # config 5 (MANTruckScenes-shape): B=16 over 8 GPUs -> 2 pairs/GPU
 V2_PAIRS_PER_GPU = 2
 V2_LANES = 2           # Model_V2 graph executor: lanes (forwards in flight)
-V2_MERGE = 8           # Model_V2: reference batches merged per forward (--merge)
+# Model_V2: reference batches merged per forward (--merge; the largest divisor of --steps up to
+# this).  48 steps, paired lines (gpurun_out/r5p): merge 8 / 12 / 24 -> 2999 / 3164 / 3137 pairs/s
+V2_MERGE = 12
 # HRegNet line: reference batches of 8 pairs merged per executor forward (the largest divisor of
-# --steps up to this).  Paired lines (one box, gpurun_out/r5m): --steps 20 on merge 1 / 2 / 4 /
-# 5 / 10 / 20: 7391 / 7518 / 7797 / 7716 / 7768 / 6901 pairs/s; --steps 48 on 1 / 4 / 6 / 8:
-# 7570 / 8024 / 7779 / 7672
+# --steps up to this).  Paired lines (one box, gpurun_out/r5m, r5p): --steps 20 on merge 1 / 2 /
+# 4 / 5 / 10 / 20: 7391 / 7518 / 7797 / 7716 / 7768 / 6901 pairs/s; --steps 48 on 1 / 2 / 3 / 4 /
+# 6 / 8: 7570 / 7969 / 7945 / 8029 / 7779 / 7672
 HREGNET_MERGE = 4
 
 

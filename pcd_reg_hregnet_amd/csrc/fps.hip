@@ -119,6 +119,9 @@ __device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N
 #ifndef HREG_FPS_PRIO
 #define HREG_FPS_PRIO 0
 #endif
+#ifndef HREG_FPS_W1024_1W
+#define HREG_FPS_W1024_1W 0
+#endif
 
 // per-axis slot coordinates of a thread: one contiguous VGPR tuple
 template <int N>
@@ -654,8 +657,8 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     if (Q == 1 && bs >= 256) {
         // one wave (no barrier) while its scan stays short; 4 waves at bs = 1024
         // (measured, 16 clouds: n=512 0.130 ms at 1 wave vs 0.150 at 2; n=1024 0.300 ms
-        // at 4 waves vs 0.331 at 1)
-        T = bs >= 1024 ? bs / 4 : 64;
+        // at 4 waves vs 0.331 at 1; HREG_FPS_W1024_1W: one wave at bs = 1024 too, A/B)
+        T = bs >= 1024 && !HREG_FPS_W1024_1W ? bs / 4 : 64;
         G = bs / T;
         QT = 1;
         return;
