@@ -120,7 +120,7 @@ __device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N
 #define HREG_FPS_PRIO 0
 #endif
 #ifndef HREG_FPS_W1024_1W
-#define HREG_FPS_W1024_1W 0
+#define HREG_FPS_W1024_1W 1
 #endif
 
 // per-axis slot coordinates of a thread: one contiguous VGPR tuple
@@ -656,8 +656,11 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     while (QT < Q) QT <<= 1;
     if (Q == 1 && bs >= 256) {
         // one wave (no barrier) while its scan stays short; 4 waves at bs = 1024
-        // (measured, 16 clouds: n=512 0.130 ms at 1 wave vs 0.150 at 2; n=1024 0.300 ms
-        // at 4 waves vs 0.331 at 1; HREG_FPS_W1024_1W: one wave at bs = 1024 too, A/B)
+        // (measured, 16 clouds: n=512 0.130 ms at 1 wave vs 0.150 at 2; n=1024 (r1) 0.300 ms
+        // at 4 waves vs 0.331 at 1.  r5, HREG_FPS_W1024_1W: with the pair-maxima slot search
+        // and the indexed winner read, one wave x 16 weighted points per lane runs level 2 at
+        // 0.484 vs 0.564 us per iteration, single-batch latency 3.26 vs 3.32 ms, bench lines
+        // within noise -- on)
         T = bs >= 1024 && !HREG_FPS_W1024_1W ? bs / 4 : 64;
         G = bs / T;
         QT = 1;
