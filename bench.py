@@ -436,8 +436,8 @@ def fps_latency(src, dst):
       barrier, block max);
     * the floor: the same workgroup and per-iteration exchange with (almost) no scan --
       level 1: 2 instead of 32 points per thread (hreg_debug_fps_floor); levels 2 / 3 (WFPS on
-      1024 / 512 points): one weighted point per thread in the level's 4-wave / 1-wave
-      geometry (hreg_debug_wfps_floor), i.e. the dependent chain alone.
+      1024 / 512 points): one weighted point per thread in the level's one-wave geometry
+      (hreg_debug_wfps_floor), i.e. the dependent chain alone.
     Levels 2 / 3 run on the first 1024 / 512 points of each cloud with seeded weights in
     [0.5, 2] (the WFPS cost does not depend on the values)."""
     from pcd_reg_hregnet_amd import _lib
@@ -457,7 +457,8 @@ def fps_latency(src, dst):
                                    "fps_cluster_kernel (level 1: one cloud over single-wave "
                                    "workgroups exchanging candidates through L2; hreg_fps_bounded, "
                                    "one launch at a time, as the batched stage 1 runs it)")
-    for lvl, n, m, T, kern in ((2, 1024, 512, 256, "fps_reg_kernel<256, 4, 1, weighted> (level 2: 4 waves x 4 points)"),
+    for lvl, n, m, T, kern in ((2, 1024, 512, 64, "fps_reg_kernel<64, 16, 1, weighted> (level 2: 1 wave x 16 points, "
+                                                  "fps.hip HREG_FPS_W1024_1W)"),
                                (3, 512, 256, 64, "fps_reg_kernel<64, 8, 1, weighted> (level 3: 1 wave x 8 points)")):
         p = pts[:, :n].contiguous()
         w = (0.5 + 1.5 * torch.rand(nb, n, generator=g)).to(pts.device)
