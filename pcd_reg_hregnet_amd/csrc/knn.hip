@@ -267,49 +267,70 @@ __global__ __launch_bounds__(256) void knnd_kernel(const float *__restrict__ q,
 // of 16 barrier-separated staging round trips; this is 2048 independent waves.
 // Same distance order (q - p, squared, added in d order) and the same offer/merge:
 // bit-identical lists.
-template <int K>
+// HREG_KNND_QW: queries per wave.  Every database row a lane loads (1 KB at 256 dims) feeds
+// QW queries' distances, so the L2 -> CU row stream per query drops QW-fold; each query keeps
+// its own candidate list (WaveList + LDS buffer) and its own accumulation order (bit-identical
+// distances and lists).  The QW queries of a wave belong to one cloud (n1 % QW == 0, else 1).
+#ifndef HREG_KNND_QW
+#define HREG_KNND_QW 1
+#endif
+template <int K, int QW>
 __global__ __launch_bounds__(256) void knnd_wave_kernel(const float *__restrict__ q,
                                                         const float *__restrict__ p, int nb, int n1,
                                                         int n2, int dim, float *__restrict__ dists,
                                                         int64_t *__restrict__ idx64,
                                                         int32_t *__restrict__ idx32,
                                                         float *__restrict__ nn, int k) {
-    __shared__ uint64_t sbuf[WAVES][128];
+    __shared__ uint64_t sbuf[WAVES][QW][128];
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int qi = xcd_block(blockIdx.x, gridDim.x) * WAVES + w;
-    if (qi >= nb * n1) return;  // wave-uniform
-    const int cloud = qi / n1;
+    const int q0 = (xcd_block(blockIdx.x, gridDim.x) * WAVES + w) * QW;
+    if (q0 >= nb * n1) return;  // wave-uniform
+    const int cloud = q0 / n1;
     const float *P = p + (size_t)cloud * n2 * dim;
-    const float *Q = q + (size_t)qi * dim;
-    WaveList L;
-    L.key = KEY_INF; L.tau = KEY_INF; L.cnt = 0;
+    const float *Q = q + (size_t)q0 * dim;
+    WaveList L[QW];
+#pragma unroll
+    for (int t = 0; t < QW; ++t) {
+        L[t].key = KEY_INF; L[t].tau = KEY_INF; L[t].cnt = 0;
+    }
     for (int base = 0; base < n2; base += 64) {
         const int pi = base + lane;
         const float *pr = P + (size_t)(pi < n2 ? pi : n2 - 1) * dim;
-        float acc = 0.f;
+        float acc[QW];
+#pragma unroll
+        for (int t = 0; t < QW; ++t) acc[t] = 0.f;
 #pragma unroll 4
         for (int e = 0; e < dim; e += 4) {
             const float4 pv = *reinterpret_cast<const float4 *>(pr + e);
-            const float4 qv = *reinterpret_cast<const float4 *>(Q + e);
-            float d;
-            d = fsub_rn(qv.x, pv.x); acc = fadd_rn(acc, fmul_rn(d, d));
-            d = fsub_rn(qv.y, pv.y); acc = fadd_rn(acc, fmul_rn(d, d));
-            d = fsub_rn(qv.z, pv.z); acc = fadd_rn(acc, fmul_rn(d, d));
-            d = fsub_rn(qv.w, pv.w); acc = fadd_rn(acc, fmul_rn(d, d));
+#pragma unroll
+            for (int t = 0; t < QW; ++t) {
+                const float4 qv = *reinterpret_cast<const float4 *>(Q + (size_t)t * dim + e);
+                float d;
+                d = fsub_rn(qv.x, pv.x); acc[t] = fadd_rn(acc[t], fmul_rn(d, d));
+                d = fsub_rn(qv.y, pv.y); acc[t] = fadd_rn(acc[t], fmul_rn(d, d));
+                d = fsub_rn(qv.z, pv.z); acc[t] = fadd_rn(acc[t], fmul_rn(d, d));
+                d = fsub_rn(qv.w, pv.w); acc[t] = fadd_rn(acc[t], fmul_rn(d, d));
+            }
         }
-        const uint64_t key = pi < n2 ? (((uint64_t)__float_as_uint(acc) << 32) | (uint32_t)pi) : KEY_INF;
-        offer<K>(L, sbuf[w], key, lane);
+#pragma unroll
+        for (int t = 0; t < QW; ++t) {
+            const uint64_t key = pi < n2 ? (((uint64_t)__float_as_uint(acc[t]) << 32) | (uint32_t)pi) : KEY_INF;
+            offer<K>(L[t], sbuf[w][t], key, lane);
+        }
     }
-    if (L.cnt > 0) flush64<K>(L, sbuf[w], lane);
-    if (lane < k) {
-        const bool valid = L.key != KEY_INF;
-        const int id = valid ? (int)(uint32_t)(L.key & 0xffffffffu) : -1;
-        const size_t o = (size_t)qi * k + lane;
-        if (dists) dists[o] = valid ? __uint_as_float((uint32_t)(L.key >> 32)) : 0.f;
-        if (idx64) idx64[o] = id;
-        if (idx32) idx32[o] = id;
-        if (nn)
-            for (int e = 0; e < dim; ++e) nn[o * dim + e] = valid ? P[(size_t)id * dim + e] : 0.f;
+#pragma unroll
+    for (int t = 0; t < QW; ++t) {
+        if (L[t].cnt > 0) flush64<K>(L[t], sbuf[w][t], lane);
+        if (lane < k) {
+            const bool valid = L[t].key != KEY_INF;
+            const int id = valid ? (int)(uint32_t)(L[t].key & 0xffffffffu) : -1;
+            const size_t o = (size_t)(q0 + t) * k + lane;
+            if (dists) dists[o] = valid ? __uint_as_float((uint32_t)(L[t].key >> 32)) : 0.f;
+            if (idx64) idx64[o] = id;
+            if (idx32) idx32[o] = id;
+            if (nn)
+                for (int e = 0; e < dim; ++e) nn[o * dim + e] = valid ? P[(size_t)id * dim + e] : 0.f;
+        }
     }
 }
 
@@ -737,8 +758,14 @@ int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim,
         hipLaunchKernelGGL((knn3_kernel<K>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
                            p2, b, n1, n2, dists, idx64, idx32, nn, k);
     } else if (dim % 4 == 0 && !((reinterpret_cast<uintptr_t>(p1) | reinterpret_cast<uintptr_t>(p2)) & 15)) {
-        hipLaunchKernelGGL((knnd_wave_kernel<K>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
-                           p2, b, n1, n2, dim, dists, idx64, idx32, nn, k);
+        if (HREG_KNND_QW > 1 && n1 % HREG_KNND_QW == 0) {
+            constexpr int QW = HREG_KNND_QW;
+            hipLaunchKernelGGL((knnd_wave_kernel<K, QW>), dim3((nq / QW + WAVES - 1) / WAVES), dim3(256), 0, st,
+                               p1, p2, b, n1, n2, dim, dists, idx64, idx32, nn, k);
+        } else {
+            hipLaunchKernelGGL((knnd_wave_kernel<K, 1>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
+                               p2, b, n1, n2, dim, dists, idx64, idx32, nn, k);
+        }
     } else {
         constexpr int QB = WAVES * QPW;
         if (b > 1 && n1 % QB) {  // a block's queries must belong to one cloud
