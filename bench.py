@@ -506,6 +506,14 @@ def forward_latency(P, src, dst, reps: int = 7):
                      "graph = 1-lane GraphPipeline (stage-1 graph + rest-of-forward graph)"}
 
 
+def default_merge(steps: int, v2: bool) -> int:
+    """Reference batches merged per executor forward when --merge is not given: the largest
+    divisor of --steps up to the model's factor (HREGNET_MERGE / V2_MERGE), so any step count
+    still times exactly --steps batches."""
+    cap = V2_MERGE if v2 else HREGNET_MERGE
+    return max(m for m in range(1, cap + 1) if steps % m == 0) if steps > 0 else 1
+
+
 def in_executor(steps: int, B: int, points: int, entries_flops: dict, merge: int = 1):
     """roofline of the level family inside the timed graph executor: the
     level kernels' mean durations over the timed region's dispatches, from the committed
@@ -846,13 +854,7 @@ def main():
     # --batch pairs merged into one launch set (engine.hregnet_forward sub_batch: every pair's
     # result bitwise that of its own batch's forward, the weighted SVD's identity fallback and
     # the prime shuffles per batch); a step is still one batch of --batch pairs
-    if args.merge is None:
-        # the default: the largest divisor of --steps up to the model's merge factor (a step
-        # count the factor does not divide still times exactly --steps batches)
-        cap = V2_MERGE if v2 else HREGNET_MERGE
-        merge = max(m for m in range(1, cap + 1) if args.steps % m == 0)
-    else:
-        merge = args.merge
+    merge = default_merge(args.steps, v2) if args.merge is None else args.merge
     if merge < 1 or args.steps % merge:
         raise SystemExit(f"bench: --steps {args.steps} is not a multiple of --merge {merge}")
     args.warmup = -(-args.warmup // merge) * merge  # (untimed: rounded up to whole forwards)

@@ -368,3 +368,19 @@ def test_graph_executor_refuses_too_few_hw_queues():
         with pytest.raises(RuntimeError, match="GPU_MAX_HW_QUEUES"):
             engine.check_hw_queues(w, {"GPU_MAX_HW_QUEUES": q})
     assert engine.check_hw_queues(1, {"GPU_MAX_HW_QUEUES": "2"}) == 2
+
+
+def test_bench_default_merge_divides_steps():
+    """bench.default_merge: the largest divisor of --steps up to the model's merge factor, so
+    the timed region is always exactly --steps reference batches (the driver's 20, the default
+    48, and step counts the factor does not divide)."""
+    import bench
+    assert bench.HREGNET_MERGE == 4 and bench.V2_MERGE == 12
+    for steps, want in ((20, 4), (48, 4), (10, 2), (7, 1), (9, 3), (1, 1)):
+        assert bench.default_merge(steps, False) == want, steps
+    for steps, want in ((48, 12), (20, 10), (16, 8), (7, 7), (13, 1)):
+        assert bench.default_merge(steps, True) == want, steps
+    for steps in range(1, 100):
+        for v2 in (False, True):
+            m = bench.default_merge(steps, v2)
+            assert steps % m == 0 and 1 <= m <= (12 if v2 else 4)
