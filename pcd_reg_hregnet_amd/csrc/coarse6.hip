@@ -56,8 +56,12 @@ struct CorrCfg {
 // vs 134 us): JT = 1 there; at C = 256 (FineReg level-2 head, neighbour branch; 73 KB) two
 // workgroups still fit per CU: JT = 2 (corr_jt; same products and order: the same bits); the
 // C = 128 head (a smaller grid) measured 48 vs 37 us on two tiles and stays on one.
+// HREG_CORR512_JT (A/B): the C = 512 head on two row tiles (145 KB of LDS: one workgroup per CU)
+#ifndef HREG_CORR512_JT
+#define HREG_CORR512_JT 1
+#endif
 template <class K>
-constexpr int corr_jt() { return K::C == 256 ? 2 : 1; }
+constexpr int corr_jt() { return K::C == 256 ? 2 : K::C == 512 ? HREG_CORR512_JT : 1; }
 
 // NBR: CoarseReg's neighbour branch (layers.py:315-337, nbr_head6_kernel's job): rows
 // [desc[nbr] C | dxyz, |d|] through convs_2, the descriptor block precomputed per point
@@ -252,7 +256,7 @@ template <class K, bool NBR = false>
 int launch_corr6(const float *table, const float *small, const float *ud0, const float *ud1, const int32_t *gidx,
                  const float *knn_xyz, int G, float *corres, float *att, void *stream, int row_tiles = 0) {
     const int jt = row_tiles ? row_tiles : corr_jt<K>();
-    if constexpr (K::C <= 256) {
+    if constexpr (K::C <= 256 || (K::C == 512 && HREG_CORR512_JT == 2)) {
         if (jt == 2) return launch_corr6_jt<K, NBR, 2>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
     }
     if (jt == 1) return launch_corr6_jt<K, NBR, 1>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);

@@ -972,3 +972,35 @@ def test_model_v2_merged_batches_match_separate_forwards(net_v2):
         assert not torch.equal(R_[i], eye) and torch.isfinite(R_[i]).all()
     R1_, _, _, _ = engine.weighted_svd(x, c, w)  # one batch of 6: all reset
     assert all(torch.equal(R1_[i], eye) for i in range(6))
+
+
+@pytest.mark.parametrize("G", [2048, 2044])
+def test_coarse_head_row_tiles(net, G):
+    """hreg_corr_head6x at N1 = 512 (CoarseReg) on one vs two 32-row tiles per workgroup: the
+    two-tile form exists only in a build with HREG_CORR512_JT=2 (A/B, coarse6.hip); where it
+    exists it must give the one-tile kernel's bits (same products, same order per row), else
+    the library refuses the request as unsupported."""
+    from pcd_reg_hregnet_amd import _lib
+    P = net.prepared(torch.device("cuda"))
+    g = torch.Generator(device="cpu").manual_seed(G)
+    R = G * 8
+    small = torch.randn(R, 16, generator=g).cuda()
+    ud0 = torch.randn(G, 512, generator=g).cuda()
+    ud1 = torch.randn(G, 512, generator=g).cuda()
+    gidx = torch.randint(0, G, (R,), generator=g, dtype=torch.int32).cuda()
+    kx = torch.randn(R, 3, generator=g).cuda()
+    outs = []
+    for rt in (1, 2):
+        corres = torch.full((G, 3), float("nan"), device="cuda")
+        att = torch.full((G, 512), float("nan"), device="cuda")
+        try:
+            _lib.call("hreg_corr_head6x", P.coarse_table6, 512, small, ud0, ud1, gidx, kx, G, corres, att, rt,
+                      _lib.stream_handle())
+        except RuntimeError as e:
+            assert rt == 2 and "unsupported" in str(e).lower(), e
+            continue
+        outs.append((corres, att))
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[0][0]).any() and not torch.isnan(outs[0][1]).any()
+    if len(outs) == 2:
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
