@@ -271,8 +271,10 @@ __global__ __launch_bounds__(256) void knnd_kernel(const float *__restrict__ q,
 // QW queries' distances, so the L2 -> CU row stream per query drops QW-fold; each query keeps
 // its own candidate list (WaveList + LDS buffer) and its own accumulation order (bit-identical
 // distances and lists).  The QW queries of a wave belong to one cloud (n1 % QW == 0, else 1).
+// Measured (gpurun_out/r5r): CoarseReg's kNN over 32 pairs (256 x 256 x 256 dims) 0.274 ->
+// 0.091 ms at QW = 4; bench lines at --steps 20 7990 -> 8178 pairs/s (paired, one box).
 #ifndef HREG_KNND_QW
-#define HREG_KNND_QW 1
+#define HREG_KNND_QW 4
 #endif
 template <int K, int QW>
 __global__ __launch_bounds__(256) void knnd_wave_kernel(const float *__restrict__ q,
