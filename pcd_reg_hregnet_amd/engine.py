@@ -1753,8 +1753,9 @@ class GraphPipeline:
         """Lane ln's feature extraction from stage-1 set cur, copied into fe[cur][ln]."""
         pts, g = self.bufs[ln][cur]
         fe = hregnet_front(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g, pts=pts)
-        for k, t in self.fe[cur][ln].items():
-            t.copy_(fe[k])
+        # one multi-tensor copy per dtype instead of 12 copy kernels per lane and round
+        dst = self.fe[cur][ln]
+        torch._foreach_copy_([dst[k] for k in FRONT_KEYS], [fe[k] for k in FRONT_KEYS])
 
     def _halves(self, ln, cur):
         """One front-streamed round of lane ln: the registration half from fe[1 - cur] and the
