@@ -67,6 +67,7 @@ FRONT_ORDER = switches.integer("FRONT_ORDER", 3)  # per lane: 0 back then front,
 # (measured, 3 paired lines each: 20 lanes 7084 -> 7141 pairs/s with order 0, -> 7311 with
 # order 3; 48 lanes 7456 -> 7417 / 7388)
 FRONT_STREAM_MAX_LANES = switches.integer("FRONT_STREAM_MAX_LANES", 24)
+FRONT_FOREACH = switches.flag("FRONT_FOREACH", True)  # front outputs -> static buffers: one foreach copy
 # timing probe (tools only): the level-1 grouping into preallocated buffers skips its FPS (1), its
 # spatial index + kNN (2) or its spatial index (3), leaving the buffers' previous values (static
 # inputs: unchanged)
@@ -1755,7 +1756,11 @@ class GraphPipeline:
         fe = hregnet_front(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g, pts=pts)
         # one multi-tensor copy per dtype instead of 12 copy kernels per lane and round
         dst = self.fe[cur][ln]
-        torch._foreach_copy_([dst[k] for k in FRONT_KEYS], [fe[k] for k in FRONT_KEYS])
+        if FRONT_FOREACH:
+            torch._foreach_copy_([dst[k] for k in FRONT_KEYS], [fe[k] for k in FRONT_KEYS])
+        else:
+            for k in FRONT_KEYS:
+                dst[k].copy_(fe[k])
 
     def _halves(self, ln, cur):
         """One front-streamed round of lane ln: the registration half from fe[1 - cur] and the
