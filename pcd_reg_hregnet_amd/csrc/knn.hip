@@ -114,67 +114,115 @@ __device__ void knn3_query(const float *__restrict__ P, int n2, float qx, float 
     if (L.cnt > 0) flush64<K>(L, buf, lane);
 }
 
-template <int K>
+// QW queries (of one cloud) per wave: every database point a lane loads feeds QW distances;
+// each query keeps its own list, buffer and distance order (the lists of knn3_query).
+// HREG_KNN3_QW (A/B; the launchers fall back to 1 when the per-cloud query count is not a
+// multiple).
+#ifndef HREG_KNN3_QW
+#define HREG_KNN3_QW 1
+#endif
+template <int K, int QW>
+__device__ void knn3_query_multi(const float *__restrict__ P, int n2, const float (&qx)[QW], const float (&qy)[QW],
+                                 const float (&qz)[QW], uint64_t (*buf)[128], int lane, WaveList (&L)[QW]) {
+#pragma unroll
+    for (int t = 0; t < QW; ++t) {
+        L[t].key = KEY_INF; L[t].tau = KEY_INF; L[t].cnt = 0;
+    }
+    for (int base = 0; base < n2; base += 64) {
+        const int p = base + lane;
+        const bool ok = p < n2;
+        const int pp = ok ? p : 0;
+        const float px = P[pp * 3 + 0], py = P[pp * 3 + 1], pz = P[pp * 3 + 2];
+#pragma unroll
+        for (int t = 0; t < QW; ++t) {
+            uint64_t key = KEY_INF;
+            if (ok) {
+                const float d = sqdist3(qx[t], qy[t], qz[t], px, py, pz);
+                key = ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)p;
+            }
+            offer<K>(L[t], buf[t], key, lane);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < QW; ++t)
+        if (L[t].cnt > 0) flush64<K>(L[t], buf[t], lane);
+}
+
+template <int K, int QW>
 __global__ __launch_bounds__(256) void knn3_kernel(const float *__restrict__ q,
                                                    const float *__restrict__ p, int nb, int n1,
                                                    int n2, float *__restrict__ dists,
                                                    int64_t *__restrict__ idx64,
                                                    int32_t *__restrict__ idx32,
                                                    float *__restrict__ nn, int k) {
-    __shared__ uint64_t sbuf[WAVES][128];
+    __shared__ uint64_t sbuf[WAVES][QW][128];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = xcd_block(blockIdx.x, gridDim.x) * WAVES + w;
-    if (qi >= nb * n1) return;
-    const int cloud = qi / n1;
+    const int q0 = (xcd_block(blockIdx.x, gridDim.x) * WAVES + w) * QW;
+    if (q0 >= nb * n1) return;
+    const int cloud = q0 / n1;
     const float *P = p + (size_t)cloud * n2 * 3;
-    const float qx = q[(size_t)qi * 3], qy = q[(size_t)qi * 3 + 1], qz = q[(size_t)qi * 3 + 2];
-    WaveList L;
-    knn3_query<K>(P, n2, qx, qy, qz, sbuf[w], lane, L);
-    if (lane < k) {
-        const bool valid = L.key != KEY_INF;
-        const int id = valid ? (int)(uint32_t)(L.key & 0xffffffffu) : -1;
-        const size_t o = (size_t)qi * k + lane;
-        if (dists) dists[o] = valid ? __uint_as_float((uint32_t)(L.key >> 32)) : 0.f;
-        if (idx64) idx64[o] = id;
-        if (idx32) idx32[o] = id;
-        if (nn) {
-            nn[o * 3 + 0] = valid ? P[id * 3 + 0] : 0.f;
-            nn[o * 3 + 1] = valid ? P[id * 3 + 1] : 0.f;
-            nn[o * 3 + 2] = valid ? P[id * 3 + 2] : 0.f;
+    float qx[QW], qy[QW], qz[QW];
+#pragma unroll
+    for (int t = 0; t < QW; ++t) {
+        qx[t] = q[(size_t)(q0 + t) * 3]; qy[t] = q[(size_t)(q0 + t) * 3 + 1]; qz[t] = q[(size_t)(q0 + t) * 3 + 2];
+    }
+    WaveList L[QW];
+    knn3_query_multi<K, QW>(P, n2, qx, qy, qz, sbuf[w], lane, L);
+#pragma unroll
+    for (int t = 0; t < QW; ++t) {
+        if (lane < k) {
+            const bool valid = L[t].key != KEY_INF;
+            const int id = valid ? (int)(uint32_t)(L[t].key & 0xffffffffu) : -1;
+            const size_t o = (size_t)(q0 + t) * k + lane;
+            if (dists) dists[o] = valid ? __uint_as_float((uint32_t)(L[t].key >> 32)) : 0.f;
+            if (idx64) idx64[o] = id;
+            if (idx32) idx32[o] = id;
+            if (nn) {
+                nn[o * 3 + 0] = valid ? P[id * 3 + 0] : 0.f;
+                nn[o * 3 + 1] = valid ? P[id * 3 + 1] : 0.f;
+                nn[o * 3 + 2] = valid ? P[id * 3 + 2] : 0.f;
+            }
         }
     }
 }
 
 // knn_group: global neighbour rows + (p - q, |p - q|) + neighbour xyz
-template <int K>
+template <int K, int QW>
 __global__ __launch_bounds__(256) void knn_group_kernel(const float *__restrict__ q,
                                                         const float *__restrict__ p, int nb, int m,
                                                         int n, int k, int32_t *__restrict__ gidx,
                                                         float *__restrict__ geom,
                                                         float *__restrict__ knn_xyz) {
-    __shared__ uint64_t sbuf[WAVES][128];
+    __shared__ uint64_t sbuf[WAVES][QW][128];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = xcd_block(blockIdx.x, gridDim.x) * WAVES + w;
-    if (qi >= nb * m) return;
-    const int cloud = qi / m;
+    const int q0 = (xcd_block(blockIdx.x, gridDim.x) * WAVES + w) * QW;
+    if (q0 >= nb * m) return;
+    const int cloud = q0 / m;
     const float *P = p + (size_t)cloud * n * 3;
-    const float qx = q[(size_t)qi * 3], qy = q[(size_t)qi * 3 + 1], qz = q[(size_t)qi * 3 + 2];
-    WaveList L;
-    knn3_query<K>(P, n, qx, qy, qz, sbuf[w], lane, L);
-    if (lane < k) {
-        const size_t r = (size_t)qi * k + lane;
-        const bool valid = L.key != KEY_INF;
-        const int id = valid ? (int)(uint32_t)(L.key & 0xffffffffu) : 0;
-        const float px = P[id * 3], py = P[id * 3 + 1], pz = P[id * 3 + 2];
-        const float rx = fsub_rn(px, qx), ry = fsub_rn(py, qy), rz = fsub_rn(pz, qz);
-        const float d2 = fadd_rn(fadd_rn(fmul_rn(rx, rx), fmul_rn(ry, ry)), fmul_rn(rz, rz));
-        gidx[r] = cloud * n + id;
-        float4 gv = make_float4(rx, ry, rz, sqrtf(d2));
-        *reinterpret_cast<float4 *>(geom + r * 4) = gv;
-        if (knn_xyz) {
-            knn_xyz[r * 3 + 0] = px;
-            knn_xyz[r * 3 + 1] = py;
-            knn_xyz[r * 3 + 2] = pz;
+    float qx[QW], qy[QW], qz[QW];
+#pragma unroll
+    for (int t = 0; t < QW; ++t) {
+        qx[t] = q[(size_t)(q0 + t) * 3]; qy[t] = q[(size_t)(q0 + t) * 3 + 1]; qz[t] = q[(size_t)(q0 + t) * 3 + 2];
+    }
+    WaveList L[QW];
+    knn3_query_multi<K, QW>(P, n, qx, qy, qz, sbuf[w], lane, L);
+#pragma unroll
+    for (int t = 0; t < QW; ++t) {
+        if (lane < k) {
+            const size_t r = (size_t)(q0 + t) * k + lane;
+            const bool valid = L[t].key != KEY_INF;
+            const int id = valid ? (int)(uint32_t)(L[t].key & 0xffffffffu) : 0;
+            const float px = P[id * 3], py = P[id * 3 + 1], pz = P[id * 3 + 2];
+            const float rx = fsub_rn(px, qx[t]), ry = fsub_rn(py, qy[t]), rz = fsub_rn(pz, qz[t]);
+            const float d2 = fadd_rn(fadd_rn(fmul_rn(rx, rx), fmul_rn(ry, ry)), fmul_rn(rz, rz));
+            gidx[r] = cloud * n + id;
+            float4 gv = make_float4(rx, ry, rz, sqrtf(d2));
+            *reinterpret_cast<float4 *>(geom + r * 4) = gv;
+            if (knn_xyz) {
+                knn_xyz[r * 3 + 0] = px;
+                knn_xyz[r * 3 + 1] = py;
+                knn_xyz[r * 3 + 2] = pz;
+            }
         }
     }
 }
@@ -757,8 +805,14 @@ int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim,
                float *dists, int64_t *idx64, int32_t *idx32, float *nn, hipStream_t st) {
     const int nq = b * n1;
     if (dim == 3) {
-        hipLaunchKernelGGL((knn3_kernel<K>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
-                           p2, b, n1, n2, dists, idx64, idx32, nn, k);
+        if (HREG_KNN3_QW > 1 && n1 % HREG_KNN3_QW == 0) {
+            constexpr int QW = HREG_KNN3_QW;
+            hipLaunchKernelGGL((knn3_kernel<K, QW>), dim3((nq / QW + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
+                               p2, b, n1, n2, dists, idx64, idx32, nn, k);
+        } else {
+            hipLaunchKernelGGL((knn3_kernel<K, 1>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
+                               p2, b, n1, n2, dists, idx64, idx32, nn, k);
+        }
     } else if (dim % 4 == 0 && !((reinterpret_cast<uintptr_t>(p1) | reinterpret_cast<uintptr_t>(p2)) & 15)) {
         if (HREG_KNND_QW > 1 && n1 % HREG_KNND_QW == 0) {
             constexpr int QW = HREG_KNND_QW;
@@ -894,10 +948,17 @@ extern "C" int hreg_knn_group(const float *q, const float *p, int nb, int m, int
     if (k > 64) return HREG_ERR_UNSUPPORTED;
     if (nb == 0 || m == 0) return HREG_OK;
     hipStream_t st = as_stream(stream);
-    dim3 grid((nb * m + WAVES - 1) / WAVES);
-#define HREG_KG(KK)                                                                       \
-    hipLaunchKernelGGL((knn_group_kernel<KK>), grid, dim3(256), 0, st, q, p, nb, m, n, k, \
-                       gidx, geom, knn_xyz)
+    const bool multi = HREG_KNN3_QW > 1 && m % HREG_KNN3_QW == 0;
+    dim3 grid(multi ? (nb * m / HREG_KNN3_QW + WAVES - 1) / WAVES : (nb * m + WAVES - 1) / WAVES);
+#define HREG_KG(KK)                                                                                          \
+    do {                                                                                                    \
+        if (multi)                                                                                          \
+            hipLaunchKernelGGL((knn_group_kernel<KK, HREG_KNN3_QW>), grid, dim3(256), 0, st, q, p, nb, m, n,  \
+                               k, gidx, geom, knn_xyz);                                                     \
+        else                                                                                                \
+            hipLaunchKernelGGL((knn_group_kernel<KK, 1>), grid, dim3(256), 0, st, q, p, nb, m, n, k, gidx,   \
+                               geom, knn_xyz);                                                              \
+    } while (0)
     if (k <= 8) HREG_KG(8);
     else if (k <= 16) HREG_KG(16);
     else if (k <= 32) HREG_KG(32);
