@@ -66,7 +66,44 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// HREG_FPS_DPPMAX (r5): the reductions' DPP folded into the max itself -- v_max_f32_dpp, one
+// VOP2 per step instead of v_mov_b32_dpp + v_med3_f32 (the VOP3 med3 takes no DPP on gfx9) --
+// and the wave max finished by row_bcast:15 / row_bcast:31 into lane 63 (one v_readlane
+// instead of four + three maxima).  The values are never NaN (distances, -inf for invalid
+// slots); max returns one of its inputs, so the winners are the same bits.  gfx9 DPP reads a
+// VGPR two wait states after its VALU write at the earliest: the s_nop 1s.  A/B: 0 = med3.
+#ifndef HREG_FPS_DPPMAX
+#define HREG_FPS_DPPMAX 1
+#endif
+
+__device__ __forceinline__ float row_max16_dpp(float v) {
+    float r;
+    asm("s_nop 1\n\t"
+        "v_max_f32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
+        : "=&v"(r)
+        : "v"(v));
+    return r;
+}
+
+// the max of all 64 lanes in lane 63 (lanes 0-62 hold partial maxima)
+__device__ __forceinline__ float wave_max_to63_dpp(float v) {
+    float r = row_max16_dpp(v);
+    asm("s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "+v"(r));
+    return r;
+}
+
 __device__ __forceinline__ float wave_max_uniform(float v, float inf) {
+    if constexpr (HREG_FPS_DPPMAX) return readlane_f(wave_max_to63_dpp(v), 63);
     v = row_max16(v, inf);
     return fmax_nc(fmax_nc(readlane_f(v, 0), readlane_f(v, 16), inf),
                    fmax_nc(readlane_f(v, 32), readlane_f(v, 48), inf), inf);
@@ -121,6 +158,13 @@ __device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N
 #endif
 #ifndef HREG_FPS_W1024_1W
 #define HREG_FPS_W1024_1W 1
+#endif
+#ifndef HREG_FPS_LANEWRITE
+#define HREG_FPS_LANEWRITE 1
+#endif
+// HREG_FPS_SLOTCHAIN (r5): see the slot search in fps_reg_kernel.  A/B: 0 = bit mask + ctz.
+#ifndef HREG_FPS_SLOTCHAIN
+#define HREG_FPS_SLOTCHAIN 1
 #endif
 
 // per-axis slot coordinates of a thread: one contiguous VGPR tuple
@@ -181,6 +225,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
     const int cloud = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
     const float *P = xyz + (size_t)cloud * n * 3;
     const float *W = WEIGHTED ? wts + (size_t)cloud * n : nullptr;
 
@@ -264,7 +309,20 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         if constexpr (STAMP) t1 = stamp();
         uint32_t smask = 0;
         float wmax;
-        if constexpr (PM) {
+        int myslot;
+        if constexpr (HREG_FPS_SLOTCHAIN) {
+            // the lane's first pair (PM) / slot holding its own maximum by a select chain from
+            // the top: one compare + one select per entry, no mask, OR tree or find-first-set
+            myslot = 0;
+            if constexpr (PM) {
+#pragma unroll
+                for (int s = S2 - 1; s >= 0; --s) myslot = pmx[s] == best ? s : myslot;
+            } else {
+#pragma unroll
+                for (int s = 2 * S2 - 1; s >= 0; --s) myslot = tget(s) == best ? s : myslot;
+            }
+            wmax = wave_max_uniform(best, inf);
+        } else if constexpr (PM) {
             // this lane's first PAIR holding its own maximum (16 compares at 32 slots); the
             // winning lane's slot inside that pair comes after the wave reduction (below)
 #pragma unroll
@@ -283,21 +341,36 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
 #pragma unroll
             for (int s = 0; s < 2 * S2; ++s) smask |= (tget(s) == wmax) ? (1u << s) : 0u;
         }
-        const int myslot = smask ? (int)__builtin_ctz(smask) : 0;
+        if constexpr (!HREG_FPS_SLOTCHAIN) myslot = smask ? (int)__builtin_ctz(smask) : 0;
+        (void)smask;
         const uint64_t hit = __ballot(best == wmax);
         const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest reference order
         int sl;
         if constexpr (PM) {
             // the winning lane's pair, then its x slot if that holds the max (ties: the lower slot)
             const int sp = __builtin_amdgcn_readlane(myslot, wl);
-            sl = 2 * sp + (readlane_f(VT[2 * sp], wl) == wmax ? 0 : 1);
+            // (every lane's x slot of pair sp by one indexed read; lane wl's compare bit from a
+            // ballot, tested on the scalar unit -- no readlane / v_mov / select round trip)
+            const float vtx = VT[2 * sp];
+            sl = 2 * sp + (int)((~__ballot(vtx == wmax) >> wl) & 1);
         } else {
             sl = __builtin_amdgcn_readlane(myslot, wl);
         }
-        const int rp = (wv * 64 + wl) * G + sl / QT;
-        const int kwin = (int)bitrev_bits((uint32_t)rp, L) + (sl % QT) * bs;
+        const int rp = (wvu * 64 + wl) * G + sl / QT;  // (uniform: the index on the scalar unit)
+        int kwin = (int)bitrev_bits((uint32_t)rp, L) + (sl % QT) * bs;
+        asm volatile("" : "+s"(kwin));  // (kept scalar: else it is rebuilt per lane in the write below)
+        // HREG_FPS_LANEWRITE: with several waves the winner's coordinates only go to LDS, so lane
+        // wl writes its own slot sl (one indexed read per axis) instead of three v_readlane and
+        // four v_mov for a lane-0 write
+        constexpr bool LW = HREG_FPS_LANEWRITE && NW > 1;
         float wx = 0.f, wy = 0.f, wz = 0.f;
-        pick_slot<0, 2 * S2>(sl, wl, VX, VY, VZ, wx, wy, wz);
+        if constexpr (LW) {
+            wx = VX[sl];
+            wy = VY[sl];
+            wz = VZ[sl];
+        } else {
+            pick_slot<0, 2 * S2>(sl, wl, VX, VY, VZ, wx, wy, wz);
+        }
         if constexpr (STAMP) t2 = stamp();
         int old;
         if constexpr (NW == 1) {
@@ -311,20 +384,21 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             z1 = any ? wz : z0;
         } else {
             const int buf = j & 1;
-            if (lane == 0) {
+            if (lane == (LW ? wl : 0)) {
                 s_cand[buf][wv] = make_float4(wx, wy, wz, wmax);
                 s_k[buf][wv] = kwin;
             }
             lds_barrier();
             if constexpr (STAMP) t3 = stamp();
-            float4 c = make_float4(0.f, 0.f, 0.f, -__builtin_huge_valf());
-            int ck = 0;
-            if (lane < NW) {
-                c = s_cand[buf][lane];
-                ck = s_k[buf][lane];
-            }
-            const float gmax = readlane_f(row_max16(c.w, inf), 0);
-            const uint64_t ghit = __ballot(lane < NW && c.w == gmax);
+            // every lane reads candidate lane % NW (no exec mask, no fill values): the copies sit
+            // at higher lanes, so the lowest lane holding the max is still the lowest wave
+            const float4 c = s_cand[buf][lane & (NW - 1)];
+            const int ck = s_k[buf][lane & (NW - 1)];
+            // both loads issue before the reduction (else the compiler sinks x/y/z/k into the
+            // branch below: a second LDS round trip on the dependent chain)
+            asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(ck));
+            const float gmax = readlane_f(HREG_FPS_DPPMAX ? row_max16_dpp(c.w) : row_max16(c.w, inf), 0);
+            const uint64_t ghit = __ballot(c.w == gmax);
             const int gw = (int)__builtin_ctzll(ghit);  // lowest wave = lowest reference order
             // (a uniform branch here: the selects of the one-wave path measured 0.26 vs 0.22 us
             // for this phase at level 2)
