@@ -481,7 +481,8 @@ def forward_latency(P, src, dst, reps: int = 7):
     """Single-batch latency (the reference's callers run one batch at a
     time, test/test_v3.py:82,120): one batch-B forward alone on the device, median of `reps`
     after 2 warm-ups, (a) launched eagerly (engine.hregnet_forward, host launches) and (b) as
-    the captured graph of a 1-lane GraphPipeline (stage 1 + the rest, two replays)."""
+    the captured graph of a 1-lane GraphPipeline (stage 1 + the rest, two replays); both with
+    engine.chain_fork's side-stream forks (the 1-lane GraphPipeline enables them itself)."""
     from pcd_reg_hregnet_amd import engine
 
     def med(fn):
@@ -494,8 +495,11 @@ def forward_latency(P, src, dst, reps: int = 7):
             if i >= 2:
                 ts.append(time.perf_counter() - t0)
         return float(np.median(ts)) * 1e3
+    def eager_forward():
+        with engine.chain_fork():  # (the spatial index / level input projections beside the chain)
+            engine.hregnet_forward(P, src, dst)
     with torch.no_grad():
-        eager = med(lambda: engine.hregnet_forward(P, src, dst))
+        eager = med(eager_forward)
         gp = engine.GraphPipeline(P, src, dst, lanes=1)
         graph = med(lambda: gp.run_forwards(1))
         del gp

@@ -77,6 +77,12 @@ def guard(origin, stream_cls=None, event_cls=None):
         _ACTIVE.checker = prev
 
 
+def capture_origin():
+    """The origin stream of the guarded capture in progress on this thread, or None."""
+    c = getattr(_ACTIVE, "checker", None)
+    return None if c is None else c.origin
+
+
 @contextlib.contextmanager
 def graph(g, pool=None, capture_error_mode="global"):
     """``torch.cuda.graph(g, pool)`` with the fork/join guard on its capture stream.  (r4: an

@@ -159,6 +159,13 @@ __device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N
 #ifndef HREG_FPS_W1024_1W
 #define HREG_FPS_W1024_1W 1
 #endif
+// HREG_FPS_QUAD (r5): from this many slots up, each lane's maximum is located over quad maxima
+// (2 VALU per 4 slots, a select chain over S / 4 entries) instead of pair maxima (3 per 4, a
+// chain over S / 2), and the winning lane's slot inside its quad by three indexed reads + ballots.
+// 0 = pairs.
+#ifndef HREG_FPS_QUAD
+#define HREG_FPS_QUAD 32
+#endif
 #ifndef HREG_FPS_LANEWRITE
 #define HREG_FPS_LANEWRITE 1
 #endif
@@ -215,6 +222,8 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
     constexpr int S2 = (S + 1) / 2;
     constexpr int NW = T / HREG_WAVE;
     constexpr bool PM = HREG_FPS_PAIRMASK && 2 * S2 >= HREG_FPS_PAIRMASK;
+    // quad maxima (HREG_FPS_QUAD, above): the pair-maxima search one level coarser
+    constexpr bool QM = PM && HREG_FPS_SLOTCHAIN && HREG_FPS_QUAD && 2 * S2 >= HREG_FPS_QUAD && S2 % 2 == 0;
     static_assert(NW <= 16, "block winner reduction uses one 16-lane row");
     static_assert(2 * S2 <= 32, "slot mask is 32 bits");
     __shared__ float4 s_cand[2][NW];
@@ -278,7 +287,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         if constexpr (STAMP) t0 = stamp();
         const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
         float best = -1.0f;
-        float pmx[S2];  // (PM) the pair maxima
+        float pmx[S2];  // (PM) the pair maxima; (QM) the quad maxima in pmx[0, S2 / 2)
 #pragma unroll
         for (int s = 0; s < S2; ++s) {
             const f2 dx = pair_of(VX, s) - X1, dy = pair_of(VY, s) - Y1, dz = pair_of(VZ, s) - Z1;
@@ -293,7 +302,16 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             } else {
                 PT[s] = t;
             }
-            if constexpr (PM) {
+            if constexpr (QM) {
+                if (s & 1) {
+                    const int q = s >> 1;
+                    float m3;
+                    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m3) : "v"(VT[2 * s - 2]), "v"(VT[2 * s - 1]), "v"(t.x));
+                    pmx[q] = fmax_nc(m3, t.y, inf);
+                    if (q & 1) asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(pmx[q - 1]), "v"(pmx[q]));
+                    else if (s + 1 == S2) best = fmax_nc(best, pmx[q], inf);
+                }
+            } else if constexpr (PM) {
                 pmx[s] = fmax_nc(t.x, t.y, inf);
                 if (s & 1) asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(pmx[s - 1]), "v"(pmx[s]));
                 else if (s + 1 == S2) best = fmax_nc(best, pmx[s], inf);
@@ -314,7 +332,10 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             // the lane's first pair (PM) / slot holding its own maximum by a select chain from
             // the top: one compare + one select per entry, no mask, OR tree or find-first-set
             myslot = 0;
-            if constexpr (PM) {
+            if constexpr (QM) {
+#pragma unroll
+                for (int q = S2 / 2 - 1; q >= 0; --q) myslot = pmx[q] == best ? q : myslot;
+            } else if constexpr (PM) {
 #pragma unroll
                 for (int s = S2 - 1; s >= 0; --s) myslot = pmx[s] == best ? s : myslot;
             } else {
@@ -346,7 +367,15 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         const uint64_t hit = __ballot(best == wmax);
         const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest reference order
         int sl;
-        if constexpr (PM) {
+        if constexpr (QM) {
+            // the winning lane's quad, then the first of its slots holding the max: three indexed
+            // reads and ballots, each bit of lane wl tested on the scalar unit
+            const int sq = __builtin_amdgcn_readlane(myslot, wl);
+            const float v0 = VT[4 * sq], v1 = VT[4 * sq + 1], v2 = VT[4 * sq + 2];
+            const uint64_t b0 = __ballot(v0 == wmax) >> wl, b1 = __ballot(v1 == wmax) >> wl,
+                           b2 = __ballot(v2 == wmax) >> wl;
+            sl = 4 * sq + ((b0 & 1) ? 0 : (b1 & 1) ? 1 : (b2 & 1) ? 2 : 3);
+        } else if constexpr (PM) {
             // the winning lane's pair, then its x slot if that holds the max (ties: the lower slot)
             const int sp = __builtin_amdgcn_readlane(myslot, wl);
             // (every lane's x slot of pair sp by one indexed read; lane wl's compare bit from a

@@ -17,6 +17,7 @@ order-independent up to fp32 rounding).
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass
 
 import torch
@@ -68,6 +69,13 @@ FRONT_ORDER = switches.integer("FRONT_ORDER", 3)  # per lane: 0 back then front,
 # order 3; 48 lanes 7456 -> 7417 / 7388)
 FRONT_STREAM_MAX_LANES = switches.integer("FRONT_STREAM_MAX_LANES", 24)
 FRONT_FOREACH = switches.flag("FRONT_FOREACH", True)  # front outputs -> static buffers: one foreach copy
+# Single-batch latency (one forward alone on the GPU is one dependent chain of ~50 kernels): work
+# that does not depend on the chain's previous kernel runs beside it on a side stream -- the
+# level-1 spatial index (input points only) beside the level-1 FPS, and the level-2/3 input
+# projection (the previous level's features only) beside that level's WFPS + kNN.  On only where
+# chain_fork() enables it (the 1-lane GraphPipeline and bench.py's eager latency figure): with
+# many lanes in flight the chip is already full and a fork only adds streams.
+CHAIN_FORK = switches.flag("CHAIN_FORK", True)
 # timing probe (tools only): the level-1 grouping into preallocated buffers skips its FPS (1), its
 # spatial index + kNN (2) or its spatial index (3), leaving the buffers' previous values (static
 # inputs: unchanged)
@@ -718,6 +726,50 @@ def _empty(*shape, dtype=torch.float32, device):
     return torch.empty(shape, dtype=dtype, device=device)
 
 
+_fork_on = False
+_fork_side = None
+_fork_streams = {}
+
+
+class chain_fork:
+    """Context: enable the single-forward side-stream forks (CHAIN_FORK) inside it, on `side`
+    (a stream the caller owns: required for forks inside a graph capture, where no stream is
+    created) or else on a stream made per forking stream."""
+
+    def __init__(self, side=None):
+        self.side = side
+
+    def __enter__(self):
+        global _fork_on, _fork_side
+        self.prev = (_fork_on, _fork_side)
+        _fork_on, _fork_side = CHAIN_FORK, self.side
+        return self
+
+    def __exit__(self, *exc):
+        global _fork_on, _fork_side
+        _fork_on, _fork_side = self.prev
+        return False
+
+
+def _fork_begin():
+    """-> (main, side) with side ordered after everything enqueued on main so far, or None
+    (no fork: the work stays on main) inside a capture when main is not the capture's origin
+    (HIP capture takes one level of fork/join, capture.py) or no side stream was given."""
+    main = torch.cuda.current_stream()
+    origin = capture.capture_origin()
+    if origin is not None and main != origin:
+        return None
+    side = _fork_side
+    if side is None:
+        if origin is not None:
+            return None
+        side = _fork_streams.get(main.cuda_stream)
+        if side is None:
+            side = _fork_streams[main.cuda_stream] = torch.cuda.Stream(device=main.device)
+    side.wait_stream(main)
+    return main, side
+
+
 # set when a multi-workgroup FPS (n > 16384) has been enqueued since the last
 # check_device_status(): only those kernels raise device status bits
 _status_pending = False
@@ -821,7 +873,7 @@ def spatial_index_bytes(nb: int, n: int) -> int:
     return _lib.load(require_gpu=False).hreg_spatial_index_bytes(nb, n)
 
 
-def knn_group_indexed(q, p, k, ws, out=None):
+def knn_group_indexed(q, p, k, ws, out=None, build=True):
     """knn_group through a per-cloud Morton spatial index built into ws (n <= 65536):
     bit-identical to knn_group, visiting only the point blocks that can hold a neighbour."""
     nb, m, _ = q.shape
@@ -834,7 +886,7 @@ def knn_group_indexed(q, p, k, ws, out=None):
         kx = _empty(R, 3, device=dev)
     else:
         gidx, geom, kx = out
-    if PROBE_S1_SKIP != 3 or out is None:
+    if build and (PROBE_S1_SKIP != 3 or out is None):
         call("hreg_spatial_index", p, nb, n, ws, _stream())
     call("hreg_knn_group_indexed", q, p, ws, nb, m, n, k, gidx, geom, kx, _stream())
     return gidx, geom, kx
@@ -906,9 +958,25 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_co
     """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz).
     out: optional preallocated tensors of the same tuple; ws: spatial-index workspace
     (uint8, spatial_index_bytes) for large clouds; sample: the level's random-sampling
-    indices instead of FPS (use_fps=False, random_samples)."""
+    indices instead of FPS (use_fps=False, random_samples).  Under chain_fork() the spatial
+    index is built on a side stream while the FPS runs."""
     M, k = LEVELS[lvl][:2]
     nb, n, _ = xyz.shape
+    use_si = SPATIAL_KNN_MIN <= n <= SPATIAL_KNN_MAX
+    fk = _fork_begin() if (_fork_on and use_si and sample is None and not PROBE_S1_SKIP) else None
+    if fk is not None:
+        if ws is None:
+            ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
+        main, side = fk
+        with torch.cuda.stream(side):
+            call("hreg_spatial_index", xyz, nb, n, ws, _stream())
+        idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
+                           out=None if out is None else out[:2], concurrent=fps_concurrent)
+        main.wait_stream(side)
+        gidx, geom, kx = knn_group_indexed(sampled, xyz, k, ws, out=None if out is None else out[2:5],
+                                           build=False)
+        _record_knn(f"knn_{lvl + 1}", gidx, nb, n, k, True)
+        return idx, sampled, gidx, geom, kx
     if sample is not None:
         idx, sampled = sample, gather_xyz(xyz, sample)
     elif PROBE_S1_SKIP == 1 and out is not None and lvl == 0:
@@ -919,7 +987,7 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_co
     kout = None if out is None else out[2:5]
     if PROBE_S1_SKIP == 2 and out is not None and lvl == 0:
         return idx, sampled, out[2], out[3], out[4]
-    if SPATIAL_KNN_MIN <= n <= SPATIAL_KNN_MAX:
+    if use_si:
         if ws is None:
             ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
         gidx, geom, kx = knn_group_indexed(sampled, xyz, k, ws, out=kout)
@@ -948,6 +1016,28 @@ def stage1_into(bufs, src, dst):
     grouping(pts, 0, out=g, ws=g[5])
 
 
+def _fused23_kernel(P: PreparedWeights, lvl: int):
+    """The fused level-2/3 kernel's entry point, weight table and whether it is a bf16x6 one
+    (its input projection then uses the bf16x6 table too)."""
+    split = (SPLIT_L2, SPLIT_L3)[lvl - 1]
+    if lvl == 1 and B6_L2 and not SPLIT_L2:
+        name, table = ("hreg_group6x2_l2" if PAIR_L2 and LEVEL_PRE else "hreg_group6_l2"), P.l2_table6
+    elif lvl == 2 and B6_L3 and not SPLIT_L3:
+        name, table = "hreg_group6_l3", P.l3_table6
+    elif split and (B6_L2, B6_L3)[lvl - 1]:
+        name, table = (("hreg_group_split6_l2", P.l2s_table6) if lvl == 1 else
+                       ("hreg_group_split6_l3", P.l3s_table6))
+    elif split:
+        name, table = (("hreg_group_split_l2", P.l2s_table) if lvl == 1 else
+                       ("hreg_group_split_l3", P.l3s_table))
+    else:
+        name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
+                       ("hreg_group_l3", P.l3_table))
+    b6 = name in ("hreg_group6_l2", "hreg_group6x2_l2", "hreg_group6_l3", "hreg_group_split6_l2",
+                  "hreg_group_split6_l3")
+    return name, table, b6
+
+
 def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=None, sample=None):
     """KeypointDetector (layers.py:134-165) + DescExtractor (layers.py:200-209) for one level.
 
@@ -960,7 +1050,20 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
     nb, n, _ = xyz.shape
     G = nb * M
     R = G * k
-    if grouped is None:
+    fused23 = (lvl == 1 and FUSED_L2) or (lvl == 2 and FUSED_L3)
+    pre = None
+    fk = _fork_begin() if (grouped is None and fused23 and LEVEL_PRE and _fork_on) else None
+    if fk is not None:
+        # (chain_fork) the level's input projection beside its WFPS + kNN
+        name, table, b6 = _fused23_kernel(P, lvl)
+        lin = (P.level_pre6 if b6 else P.level_pre)[lvl]
+        pre = _empty(feats.shape[0], lin.N, device=feats.device)
+        main, side = fk
+        with torch.cuda.stream(side):
+            gemm([_seg(feats, 0, Cf)], lin, feats.shape[0], out=pre)
+        grouped = grouping(xyz, lvl, weights, sample=sample)
+        main.wait_stream(side)
+    elif grouped is None:
         grouped = grouping(xyz, lvl, weights, sample=sample)
     idx, sampled, gidx, geom, kx = grouped[:5]
     if lvl == 0 and FUSED_L1:
@@ -976,29 +1079,14 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)
         return kp.view(nb, M, 3), sig, att_feat, desc, wnext, idx
-    if (lvl == 1 and FUSED_L2) or (lvl == 2 and FUSED_L3):
+    if fused23:
         dev = xyz.device
         kp = _empty(G, 3, device=dev)
         att_feat = _empty(G, LEVELS[lvl][3][-1], device=dev)
         desc = _empty(G, LEVELS[lvl][5], device=dev)
-        split = (SPLIT_L2, SPLIT_L3)[lvl - 1]
-        if lvl == 1 and B6_L2 and not SPLIT_L2:
-            name, table = ("hreg_group6x2_l2" if PAIR_L2 and LEVEL_PRE else "hreg_group6_l2"), P.l2_table6
-        elif lvl == 2 and B6_L3 and not SPLIT_L3:
-            name, table = "hreg_group6_l3", P.l3_table6
-        elif split and (B6_L2, B6_L3)[lvl - 1]:
-            name, table = (("hreg_group_split6_l2", P.l2s_table6) if lvl == 1 else
-                           ("hreg_group_split6_l3", P.l3s_table6))
-        elif split:
-            name, table = (("hreg_group_split_l2", P.l2s_table) if lvl == 1 else
-                           ("hreg_group_split_l3", P.l3s_table))
-        else:
-            name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
-                           ("hreg_group_l3", P.l3_table))
-        b6 = name in ("hreg_group6_l2", "hreg_group6x2_l2", "hreg_group6_l3", "hreg_group_split6_l2",
-                      "hreg_group_split6_l3")
-        pre = (gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl],
-                    feats.shape[0]) if LEVEL_PRE else None)
+        name, table, b6 = _fused23_kernel(P, lvl)
+        if pre is None and LEVEL_PRE:
+            pre = gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl], feats.shape[0])
         if name == "hreg_group_split6_l3" and pre is not None and (SPLIT_JT or L3_PIECES):
             name = "hreg_group_split6p_l3" if L3_PIECES else "hreg_group_split6j_l3"
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())
@@ -1611,69 +1699,72 @@ class GraphPipeline:
             self.bufs = [[alloc_stage1(B, N, dev), alloc_stage1(B, N, dev)] for _ in range(lanes)]
         self.side = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
         self.lane_streams = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
-        # eager warm-up: library, allocator and workspace shapes
-        if self.bs1:
-            self._stage1_all(0)
-        else:
-            stage1_into(self.bufs[0][0], self.src[0], self.dst[0])
-        self._rest(0, 0)
-        torch.cuda.synchronize()
-        # the captured graphs contain multi-workgroup FPS launches (n > 16384): their
-        # device status is checked by check() after replays
-        self.status_check = _status_pending
-        check_device_status()
-        self.pool = torch.cuda.graph_pool_handle()
-        self.g_first = torch.cuda.CUDAGraph()
-        with capture.graph(self.g_first, pool=self.pool):
-            self._first_stage1()
-        self.g_step, self.outs = [], []
-        for cur in (0, 1):
-            g = torch.cuda.CUDAGraph()
-            with capture.graph(g, pool=self.pool):
-                out = self._fork(lambda ln: self._rest(ln, cur), **self._side_kw(1 - cur))
-            self.g_step.append(g)
-            self.outs.append(out)
-        self.g_last, self.outs_last = [], []
-        for cur in (0, 1):
-            g = torch.cuda.CUDAGraph()
-            with capture.graph(g, pool=self.pool):
-                out = self._fork(lambda ln: self._rest(ln, cur))
-            self.g_last.append(g)
-            self.outs_last.append(out)
-        self._part = {}
-        self.ready = None  # buffer set holding a streamed next-round stage 1 (run_forwards)
-        # front streaming: fe[c][ln] = static copies of a lane's feature-extraction dict;
-        # fready = c: the fronts for the next round are in fe[1 - c] and its next stage 1
-        # in bufs[c], so the next replay is g_fs[c]
-        self.fs = (FRONT_STREAM and self.bs1 and (not v2 or V2_FRONT_STREAM)
-                   and lanes <= FRONT_STREAM_MAX_LANES)
-        self.fready = None
-        if self.fs:
-            with torch.no_grad():
-                pts, g = self.bufs[0][0]
-                fe0 = hregnet_front(P, self.src[0], self.dst[0], use_weights, l1=g, pts=pts)
-            self.fe = [[{k: torch.empty_like(fe0[k]) for k in FRONT_KEYS} for _ in range(lanes)]
-                       for _ in (0, 1)]
-            del fe0
-            self.g_fs, self.outs_fs, self.g_prime = [], [], []
-            if FRONT_ORDER == 3:
-                self.lane_streams2 = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
+        # one lane: a forward alone is one dependent chain -- fork what does not depend on it
+        # (chain_fork) onto the lane's otherwise unused stream
+        with (chain_fork(side=self.lane_streams[0]) if lanes == 1 else contextlib.nullcontext()):
+            # eager warm-up: library, allocator and workspace shapes
+            if self.bs1:
+                self._stage1_all(0)
+            else:
+                stage1_into(self.bufs[0][0], self.src[0], self.dst[0])
+            self._rest(0, 0)
+            torch.cuda.synchronize()
+            # the captured graphs contain multi-workgroup FPS launches (n > 16384): their
+            # device status is checked by check() after replays
+            self.status_check = _status_pending
+            check_device_status()
+            self.pool = torch.cuda.graph_pool_handle()
+            self.g_first = torch.cuda.CUDAGraph()
+            with capture.graph(self.g_first, pool=self.pool):
+                self._first_stage1()
+            self.g_step, self.outs = [], []
             for cur in (0, 1):
                 g = torch.cuda.CUDAGraph()
                 with capture.graph(g, pool=self.pool):
-                    if FRONT_ORDER == 3:  # the two halves of a lane on two streams
-                        out = self._fork(lambda ln: hregnet_back(P, self.fe[1 - cur][ln], B, v2, sub_batch),
-                                         body2=lambda ln: self._front_into(ln, cur),
-                                         **self._side_kw(1 - cur))
-                    else:
-                        out = self._fork(lambda ln: self._halves(ln, cur), **self._side_kw(1 - cur))
-                self.g_fs.append(g)
-                self.outs_fs.append(out)
+                    out = self._fork(lambda ln: self._rest(ln, cur), **self._side_kw(1 - cur))
+                self.g_step.append(g)
+                self.outs.append(out)
+            self.g_last, self.outs_last = [], []
+            for cur in (0, 1):
                 g = torch.cuda.CUDAGraph()
                 with capture.graph(g, pool=self.pool):
-                    self._fork(lambda ln: self._front_into(ln, cur), **self._side_kw(1 - cur))
-                self.g_prime.append(g)
-        torch.cuda.synchronize()
+                    out = self._fork(lambda ln: self._rest(ln, cur))
+                self.g_last.append(g)
+                self.outs_last.append(out)
+            self._part = {}
+            self.ready = None  # buffer set holding a streamed next-round stage 1 (run_forwards)
+            # front streaming: fe[c][ln] = static copies of a lane's feature-extraction dict;
+            # fready = c: the fronts for the next round are in fe[1 - c] and its next stage 1
+            # in bufs[c], so the next replay is g_fs[c]
+            self.fs = (FRONT_STREAM and self.bs1 and (not v2 or V2_FRONT_STREAM)
+                       and lanes <= FRONT_STREAM_MAX_LANES)
+            self.fready = None
+            if self.fs:
+                with torch.no_grad():
+                    pts, g = self.bufs[0][0]
+                    fe0 = hregnet_front(P, self.src[0], self.dst[0], use_weights, l1=g, pts=pts)
+                self.fe = [[{k: torch.empty_like(fe0[k]) for k in FRONT_KEYS} for _ in range(lanes)]
+                           for _ in (0, 1)]
+                del fe0
+                self.g_fs, self.outs_fs, self.g_prime = [], [], []
+                if FRONT_ORDER == 3:
+                    self.lane_streams2 = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
+                for cur in (0, 1):
+                    g = torch.cuda.CUDAGraph()
+                    with capture.graph(g, pool=self.pool):
+                        if FRONT_ORDER == 3:  # the two halves of a lane on two streams
+                            out = self._fork(lambda ln: hregnet_back(P, self.fe[1 - cur][ln], B, v2, sub_batch),
+                                             body2=lambda ln: self._front_into(ln, cur),
+                                             **self._side_kw(1 - cur))
+                        else:
+                            out = self._fork(lambda ln: self._halves(ln, cur), **self._side_kw(1 - cur))
+                    self.g_fs.append(g)
+                    self.outs_fs.append(out)
+                    g = torch.cuda.CUDAGraph()
+                    with capture.graph(g, pool=self.pool):
+                        self._fork(lambda ln: self._front_into(ln, cur), **self._side_kw(1 - cur))
+                    self.g_prime.append(g)
+            torch.cuda.synchronize()
 
     def _lane_view(self, ab: int, ln: int):
         """Lane ln's stage-1 buffers as cloud-slice views of the batched set ab."""

@@ -79,3 +79,16 @@ def test_checker_rule():
     chk.check("x", "x")
     with pytest.raises(capture.NestedForkError):
         chk.check("x", "y")
+
+
+def test_capture_origin_exposed_inside_guard_only():
+    """engine._fork_begin forks only from the capture's origin (capture_origin) and never
+    inside a capture without a caller-owned side stream."""
+    o = StubStream("origin")
+    assert capture.capture_origin() is None
+    with _guard(o):
+        assert capture.capture_origin() == o
+        with _guard(StubStream("inner")):
+            assert capture.capture_origin() == StubStream("inner")
+        assert capture.capture_origin() == o
+    assert capture.capture_origin() is None

@@ -217,6 +217,25 @@ def test_graph_pipeline_matches_eager(net):
         assert torch.equal(out["rotation"][-1], ref2["rotation"][-1])
 
 
+def test_chain_fork_matches_serial(net):
+    """engine.chain_fork (the level-1 spatial index beside the FPS, the level-2/3 input
+    projections beside their WFPS + kNN, each on a side stream): bitwise the serial forward."""
+    from pcd_reg_hregnet_amd import engine, synthetic
+    P = net.prepared(torch.device("cuda"))
+    s, d, _, _ = synthetic.lidar_batch(2, 16384, seed0=44)
+    src, dst = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    with torch.no_grad():
+        ref = engine.hregnet_forward(P, src, dst)
+        with engine.chain_fork():
+            out = engine.hregnet_forward(P, src, dst)
+        torch.cuda.synchronize()
+    for i in range(3):
+        assert torch.equal(out["rotation"][i], ref["rotation"][i])
+        assert torch.equal(out["translation"][i], ref["translation"][i])
+    for key in ("desc_1", "desc_2", "desc_3", "xyz_3"):
+        assert torch.equal(out["src_feats"][key], ref["src_feats"][key])
+
+
 def test_graph_lanes_match_eager(net):
     """Two batches in flight (one stream each inside the graph): each lane's output
     is bitwise the eager forward of its own batch."""

@@ -63,13 +63,31 @@ def profile(seg):
     return conc, alone
 
 
+def listing(seg):
+    """every kernel of a segment in start order: offset, duration, idle time before it (no kernel
+    in flight) and the kernels in flight when it starts"""
+    t0 = seg[0][0]
+    end = t0
+    for s, e, n in seg:
+        live = sum(1 for s2, e2, _ in seg if s2 < s and e2 > s)
+        idle = max(0, s - end)
+        print(f"   {(s - t0) / 1e3:9.1f} us  {(e - s) / 1e3:8.1f} us  idle {idle / 1e3:6.1f}  "
+              f"with {live}  {short(n)}")
+        end = max(end, e)
+
+
 def main():
-    rows = load(sys.argv[1])
-    marker = sys.argv[2] if len(sys.argv) > 2 else "group_l1_6_kernel"
-    for i, seg in enumerate(segments(rows)):
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    rows = load(args[0])
+    marker = args[1] if len(args) > 1 else "group_l1_6_kernel"
+    segs = segments(rows)
+    last1 = None
+    for i, seg in enumerate(segs):
         span = max(e for _, e, _ in seg) - seg[0][0]
         fw = sum(1 for _, _, n in seg if marker in n)
         print(f"segment {i}: {span / 1e6:.3f} ms, {len(seg)} kernels, {fw} x {marker}")
+        if fw == 1:
+            last1 = seg
         if fw < 2:
             continue
         conc, alone = profile(seg)
@@ -79,6 +97,10 @@ def main():
         print(f"   per forward: {span / fw / 1e6:.4f} ms")
         for n, v in sorted(alone.items(), key=lambda kv: -kv[1])[:8]:
             print(f"     alone {v / 1e6:.3f} ms  {short(n)}")
+    if "--list" in sys.argv and last1:
+        # the last one-forward segment (the latency run's last replay)
+        print("last single-forward segment:")
+        listing(last1)
 
 
 if __name__ == "__main__":
