@@ -159,6 +159,14 @@ __device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N
 #ifndef HREG_FPS_W1024_1W
 #define HREG_FPS_W1024_1W 1
 #endif
+// threads of the one-slot geometries at bs = 1024 (level 2) / 512 (level 3): 64 = one wave
+// (A/B: 128 = two waves with the LDS hand-off)
+#ifndef HREG_FPS_WT1024
+#define HREG_FPS_WT1024 64
+#endif
+#ifndef HREG_FPS_WT512
+#define HREG_FPS_WT512 64
+#endif
 // HREG_FPS_QUAD (r5): from this many slots up, each lane's maximum is located over quad maxima
 // (2 VALU per 4 slots, a select chain over S / 4 entries) instead of pair maxima (3 per 4, a
 // chain over S / 2), and the winning lane's slot inside its quad by three indexed reads + ballots.
@@ -764,7 +772,7 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
         // and the indexed winner read, one wave x 16 weighted points per lane runs level 2 at
         // 0.484 vs 0.564 us per iteration, single-batch latency 3.26 vs 3.32 ms, bench lines
         // within noise -- on)
-        T = bs >= 1024 && !HREG_FPS_W1024_1W ? bs / 4 : 64;
+        T = bs >= 1024 ? (HREG_FPS_W1024_1W ? HREG_FPS_WT1024 : bs / 4) : bs >= 512 ? HREG_FPS_WT512 : 64;
         G = bs / T;
         QT = 1;
         return;
