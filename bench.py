@@ -192,6 +192,7 @@ MFMA_ENTRIES = {
     "hreg_corr_head6x": ("head", _corr6_work),
     "hreg_mlp_head": ("mlp", _mlp_work),
     "hreg_mlp_head6": ("mlp", _mlp_work),
+    "hreg_mlp_head6x": ("mlp", _mlp_work),
 }
 
 
@@ -426,6 +427,45 @@ def _fps_level(pts, m, weights, floor_call, floor_pts, floor_w, kernel):
             "clock_ghz": round(ghz, 3)}
 
 
+def _fps_sorted_level(pts, m, reg):
+    """level 1 as the engine runs it with FPS_SORTED: the spatial index, then the FPS over its
+    Morton-sorted copy with exact group pruning (hreg_fps_indexed), each timed with HIP events;
+    the floor is the unstamped level-1 floor kernel (hreg_debug_fps_floor without stamps), timed
+    the same way, so kernel and floor are compared unstamped.  reg: the register kernel's entry
+    (its stamped phases), kept beside it."""
+    from pcd_reg_hregnet_amd import _lib, engine
+    nb, n, _ = pts.shape
+    st_ = _lib.stream_handle()
+    ws = torch.empty(engine.spatial_index_bytes(nb, n), dtype=torch.uint8, device=pts.device)
+    idx = torch.empty(nb, m, dtype=torch.int32, device=pts.device)
+    fp = pts[:, :1024].contiguous()
+    fidx = torch.empty(nb, m, dtype=torch.int32, device=pts.device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    for rep in range(2):  # (the first pass warms up)
+        ev[0].record()
+        _lib.call("hreg_spatial_index", pts, nb, n, ws, st_)
+        ev[1].record()
+        _lib.call("hreg_fps_indexed", nb, n, m, pts, ws, None, idx, None, st_)
+        ev[2].record()
+        _lib.call("hreg_debug_fps_floor", nb, m, fp, fidx, None, st_)
+        ev[3].record()
+    torch.cuda.synchronize()
+    index_us = ev[0].elapsed_time(ev[1]) * 1e3
+    launch_us = ev[1].elapsed_time(ev[2]) * 1e3
+    floor_us = ev[2].elapsed_time(ev[3]) * 1e3
+    per = lambda us: round(us / (m - 1), 4)  # noqa: E731
+    return {"kernel": "fps_sorted_kernel (level 1: 512 threads x 32 points of the spatial index's "
+                      "Morton-sorted copy, 256-point groups skipped when their box cannot change them; "
+                      "hreg_fps_indexed, engine.FPS_SORTED)",
+            "clouds": nb, "points": n, "dependent_iterations": m - 1,
+            "index_us": round(index_us, 1), "launch_us": round(launch_us, 1),
+            "us_per_iteration": per(launch_us),
+            "floor_us_per_iteration": per(floor_us),
+            "frac_floor_over_kernel": round(floor_us / max(launch_us, 1e-9), 3),
+            "basis": "unstamped kernel and unstamped floor kernel launch times (HIP events)",
+            "reg_kernel": reg}
+
+
 def fps_latency(src, dst):
     """The FPS chain of one forward (latency-bound, 1023 + 511 + 255 dependent
     iterations) against measured latency floors, on the batch's 2B
@@ -452,6 +492,9 @@ def fps_latency(src, dst):
             lambda fp, fw, i, s, st: _lib.call("hreg_debug_fps_floor", nb, 1024, fp, i, s, st),
             pts[:, :1024].contiguous(), None,
             "fps_reg_kernel<512, 2, 16> (level 1: 512 threads x 32 points per cloud)")
+        from pcd_reg_hregnet_amd import engine
+        if engine.FPS_SORTED and pts.shape[1] == engine.FPS_SORTED_N:
+            out["level1"] = _fps_sorted_level(pts, 1024, out["level1"])
     else:  # Model_V2's 65536-point clouds: one cloud over up to 64 single-wave workgroups
         out["level1"] = _fps_level(pts, 1024, None, None, None, None,
                                    "fps_cluster_kernel (level 1: one cloud over single-wave "
@@ -468,7 +511,8 @@ def fps_latency(src, dst):
             p, m, w,
             lambda fp_, fw_, i, s, st, T=T, m=m: _lib.call("hreg_debug_wfps_floor", nb, T, m, fp_, fw_, i, s, st),
             fp, fw, kern)
-    out["chain_us"] = round(sum(out[f"level{k}"]["launch_us"] for k in (1, 2, 3)), 1)
+    out["chain_us"] = round(sum(out[f"level{k}"]["launch_us"] for k in (1, 2, 3))
+                            + out["level1"].get("index_us", 0.0), 1)
     # (the r4 lines' flat fields: level 1)
     for k in ("us_per_iteration", "frac_floor_over_kernel", "floor_us_per_iteration",
               "stamped_us_per_iteration"):

@@ -86,6 +86,13 @@ enum {
  * 1024 waves).  Same results as hreg_furthest_point_sampling. */
 int hreg_fps_bounded(int b, int n, int m, const float *points, float *temp, int32_t *idx,
                      float *sampled_xyz, int concurrent, void *stream);
+/* FPS of clouds of 16384 points over their spatial index (ws: hreg_spatial_index of the same
+ * points, enqueued before): the Morton-sorted copy is scanned in 256-point groups and a group
+ * whose box cannot hold a point nearer the new centre than its running minima is skipped (exact:
+ * the same idx / temp as hreg_furthest_point_sampling).  Other sizes: hreg_furthest_point_sampling.
+ * Replaces furthest_point_sampling_kernel for level 1 (furthest_point_sampling_gpu.cu:84-206). */
+int hreg_fps_indexed(int b, int n, int m, const float *points, const void *ws, float *temp,
+                     int32_t *idx, float *sampled_xyz, void *stream);
 int hreg_furthest_point_sampling(int b, int n, int m, const float *points, float *temp,
                                  int32_t *idx, float *sampled_xyz, void *stream);
 
@@ -225,6 +232,12 @@ int hreg_mlp_head(const float *table, int C, const float *x, int ldx, int ncloud
 int hreg_mlp_head6_table_floats(int C);
 int hreg_mlp_head6(const float *table, int C, const float *x, int ldx, int nclouds,
                    int rows_per_cloud, int mode, float *out, float *weights_out, void *stream);
+/* hreg_mlp_head6 with the row tiles per workgroup: 0 = the default (2-4: fewer weight bytes per
+ * MFMA when launches share the chip), 1 = one 32-row tile per workgroup (more workgroups for a
+ * small batch alone on the GPU).  Same outputs, bit for bit. */
+int hreg_mlp_head6x(const float *table, int C, const float *x, int ldx, int nclouds,
+                    int rows_per_cloud, int mode, float *out, float *weights_out, int row_tiles,
+                    void *stream);
 
 /* ---- data side in front of the path (perturb.hip) ----
  * Twists x = (w, v) [n][6], SE(3) matrices g [n][16] row-major. */
@@ -310,6 +323,12 @@ int hreg_weighted_svd(const float *src, const float *corres, const float *w, int
 int hreg_weighted_svd_grouped(const float *src, const float *corres, const float *w, int nb, int group,
                               int n, const float *prev_R, const float *prev_t, float *R_, float *t_,
                               float *R, float *t, void *stream);
+/* hreg_weighted_svd_grouped + hreg_transform_points of tr_xyz [nb][tr_n][3] by each pair's final
+ * R, t (R / t when given, else R_ / t_) into tr_out, in the batch step's launch: the same bits as
+ * the two calls (HRegNet.forward's src_xyz_{2,1} moves, models.py:100-127). */
+int hreg_weighted_svd_tr(const float *src, const float *corres, const float *w, int nb, int group, int n,
+                         const float *prev_R, const float *prev_t, float *R_, float *t_, float *R,
+                         float *t, const float *tr_xyz, int tr_n, float *tr_out, void *stream);
 
 /* out[b][i] = R[b] xyz[b][i] + t[b], xyz/out [nb][n][3] */
 int hreg_transform_points(const float *xyz, const float *R, const float *t, int nb, int n,
@@ -653,7 +672,8 @@ int hreg_nbr_head6sx(const float *table, const float *desc, const int32_t *gidx,
 int hreg_debug_fps_stamps(int b, int n, int m, const float *points, const float *weights,
                           int32_t *idx, uint64_t *stamps, void *stream);
 /* Latency floor of the level-1 FPS geometry: the same 8-wave workgroup and per-iteration
- * exchange, 2 points per thread (n = 1024); points [b][1024][3], stamps[6] as above. */
+ * exchange, 2 points per thread (n = 1024); points [b][1024][3], stamps[6] as above, or NULL for
+ * the unstamped kernel (its launch time is the floor of an unstamped level-1 kernel). */
 /* Diagnostic: the latency floor of the level-2 (T = 256) / level-3 (T = 64) WFPS geometry: T
  * threads, one weighted point each (n = T); stamps as hreg_debug_fps_stamps. */
 int hreg_debug_wfps_floor(int b, int T, int m, const float *points, const float *weights,

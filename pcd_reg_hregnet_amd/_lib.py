@@ -77,6 +77,8 @@ _SIGS = {
                         _vp],
     "hreg_weighted_svd": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_weighted_svd_grouped": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_fps_indexed": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_weighted_svd_tr": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp],
     "hreg_transform_points": [_vp, _vp, _vp, _i, _i, _vp, _vp],
     "hreg_transformation_loss": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
                                  _vp],
@@ -104,6 +106,7 @@ _SIGS = {
     "hreg_mlp_head": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "hreg_mlp_head_table_floats": [_i],
     "hreg_mlp_head6": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
+    "hreg_mlp_head6x": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp],
     "hreg_mlp_head6_table_floats": [_i],
     "hreg_sigma_weights": [_vp, _i, _i, _vp, _vp],
     "hreg_se3_exp": [_vp, _i, _vp, _vp],

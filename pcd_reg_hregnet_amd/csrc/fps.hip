@@ -907,6 +907,204 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
     return HREG_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Level-1 FPS over the spatial index's Morton-sorted copy, with exact group pruning (r5).
+//
+// The same selections as fps_reg_kernel<512, 2, 16> (n = 16384): 8 waves x 32 slots per lane, but
+// the slots hold hreg_spatial_index's Morton-sorted float4 (x, y, z, id) copy: group g (slots
+// 4g..4g+3) of wave w is the 256-point Morton range 8g + w (slot 4g + q of lane l: sorted point
+// (8g + w) * 256 + 64q + l), one bounding box per group.  Consecutive ranges sit in different
+// waves: a new centre's few affected ranges are neighbours, so they spread over the waves instead
+// of queueing in one (measured: ranges in wave order, w * 2048 + 64 s + l, ran 1.18 us per
+// iteration, no faster than fps_reg_kernel).  Per iteration, group g is scanned only if the box lower bound of its squared
+// distance to the new centre is below the group's largest running minimum: otherwise every point
+// has d >= lb >= max T >= T and min(d, T) = T for all of them (lb and d are computed with the same
+// rounded operations on coordinates the box orders, and rounding is monotone, so lb <= d holds
+// in fp32 too).  A scanned group is updated with the reference arithmetic (two-rounding squared
+// distance, min).  ~5 of 64 groups need a scan per iteration on KITTI-shape clouds (simulated).
+//
+// The reference's winner (max T, then the lowest reference thread in tree order, then its lowest
+// k) no longer follows the register order, so every point carries its reference
+// rank  rank(k) = bitrev_L(k mod bs) * Q + k div bs  (with its slot in the low 5 bits): a lane's
+// candidate per group is (max T, min rank among its slots at that T), the wave's is (max T, min
+// rank), and the workgroup's the same over the 8 waves.
+constexpr int FS_T = 512, FS_NW = 8, FS_S = 32, FS_NG = 8, FS_N = FS_T * FS_S;
+
+__device__ __forceinline__ uint32_t row_min16_u32_dpp(uint32_t v) {
+    uint32_t r;
+    asm("s_nop 1\n\t"
+        "v_min_u32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
+        : "=&v"(r)
+        : "v"(v));
+    return r;
+}
+
+// the minimum of all 64 lanes in lane 63
+__device__ __forceinline__ uint32_t wave_min_to63_u32_dpp(uint32_t v) {
+    uint32_t r = row_min16_u32_dpp(v);
+    asm("s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "+v"(r));
+    return r;
+}
+
+__device__ __forceinline__ float wave_min_uniform_dpp(float v) {
+    return -readlane_f(wave_max_to63_dpp(-v), 63);
+}
+
+__global__ __launch_bounds__(FS_T) void fps_sorted_kernel(const float4 *__restrict__ spts, int np,
+                                                          const float *__restrict__ xyz,
+                                                          float *__restrict__ temp_out,
+                                                          int32_t *__restrict__ idx_out,
+                                                          float *__restrict__ sampled_out, int m, int bs,
+                                                          int L, int LQ, float inf) {
+    typedef typename SlotVec<FS_S>::type V;
+    __shared__ float4 s_cand[2][FS_NW];
+    __shared__ uint32_t s_r[2][FS_NW];
+    __shared__ int s_k[2][FS_NW];
+    const int cloud = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    const float4 *SP = spts + (size_t)cloud * np + (size_t)wvu * 256;
+    // slot s -> offset from SP: range 8 (s / 4) + w, row s % 4 of its 4 x 64
+    auto soff = [&](int s) { return (s >> 2) * (FS_NW * 256) + (s & 3) * 64 + lane; };
+    const float *P = xyz + (size_t)cloud * FS_N * 3;
+
+    V VX, VY, VZ, VT;
+    uint32_t VE[FS_S];  // rank << 5 | slot
+#pragma unroll
+    for (int s = 0; s < FS_S; ++s) {
+        const float4 v = SP[soff(s)];
+        VX[s] = v.x;
+        VY[s] = v.y;
+        VZ[s] = v.z;
+        VT[s] = 1e10f;
+        const uint32_t id = (uint32_t)__float_as_int(v.w);
+        const uint32_t rank = (bitrev_bits(id & (uint32_t)(bs - 1), L) << LQ) + (id >> L);
+        VE[s] = (rank << 5) | (uint32_t)s;
+    }
+    asm volatile("" : "+v"(VX), "+v"(VY), "+v"(VZ));
+
+    // group boxes (wave-uniform) into lanes 0..7; per-lane group candidates
+    float glx = 0.f, gly = 0.f, glz = 0.f, ghx = 0.f, ghy = 0.f, ghz = 0.f;
+    float gm = -__builtin_huge_valf();  // lane g < 8: group g's largest running minimum
+    float tg[FS_NG];
+    uint32_t rg[FS_NG];
+#pragma unroll
+    for (int g = 0; g < FS_NG; ++g) {
+        float lx = VX[4 * g], ly = VY[4 * g], lz = VZ[4 * g], hx = lx, hy = ly, hz = lz;
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            lx = fminf(lx, VX[4 * g + q]); hx = fmaxf(hx, VX[4 * g + q]);
+            ly = fminf(ly, VY[4 * g + q]); hy = fmaxf(hy, VY[4 * g + q]);
+            lz = fminf(lz, VZ[4 * g + q]); hz = fmaxf(hz, VZ[4 * g + q]);
+        }
+        lx = wave_min_uniform_dpp(lx); ly = wave_min_uniform_dpp(ly); lz = wave_min_uniform_dpp(lz);
+        hx = readlane_f(wave_max_to63_dpp(hx), 63);
+        hy = readlane_f(wave_max_to63_dpp(hy), 63);
+        hz = readlane_f(wave_max_to63_dpp(hz), 63);
+        if (lane == g) {
+            glx = lx; gly = ly; glz = lz; ghx = hx; ghy = hy; ghz = hz;
+            gm = 1e10f;
+        }
+        tg[g] = 1e10f;
+        uint32_t r = VE[4 * g];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) r = min(r, VE[4 * g + q]);
+        rg[g] = r;
+    }
+
+    float x1 = P[0], y1 = P[1], z1 = P[2];
+    if (tid == 0) {
+        idx_out[(size_t)cloud * m] = 0;
+        if (sampled_out) {
+            float *o = sampled_out + (size_t)cloud * m * 3;
+            o[0] = x1; o[1] = y1; o[2] = z1;
+        }
+    }
+
+    for (int j = 1; j < m; ++j) {
+        // which groups can change: box lower bound below the group's largest T (lanes 0..7)
+        const float qx = fminf(fmaxf(x1, glx), ghx), qy = fminf(fmaxf(y1, gly), ghy), qz = fminf(fmaxf(z1, glz), ghz);
+        const float lb = sqdist3(x1, y1, z1, qx, qy, qz);
+        const uint32_t amask = (uint32_t)__ballot(lb < gm);
+        const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
+#pragma unroll
+        for (int g = 0; g < FS_NG; ++g) {
+            if (amask & (1u << g)) {
+#pragma unroll
+                for (int s = 2 * g; s < 2 * g + 2; ++s) {
+                    const f2 dx = pair_of(VX, s) - X1, dy = pair_of(VY, s) - Y1, dz = pair_of(VZ, s) - Z1;
+                    const f2 d = (dx * dx + dy * dy) + dz * dz;
+                    VT[2 * s] = fmin_nc(d.x, VT[2 * s], inf);
+                    VT[2 * s + 1] = fmin_nc(d.y, VT[2 * s + 1], inf);
+                }
+                float m4;
+                asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m4) : "v"(VT[4 * g]), "v"(VT[4 * g + 1]), "v"(VT[4 * g + 2]));
+                m4 = fmax_nc(m4, VT[4 * g + 3], inf);
+                uint32_t r = 0xffffffffu;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) r = VT[4 * g + q] == m4 ? min(r, VE[4 * g + q]) : r;
+                tg[g] = m4;
+                rg[g] = r;
+                const float gmx = readlane_f(wave_max_to63_dpp(m4), 63);
+                gm = lane == g ? gmx : gm;
+            }
+        }
+        // the wave's candidate: max T, then min rank (branch-free: skipping the min reductions when
+        // one lane holds the max measured 1.04 vs 0.96 us per iteration)
+        const float W = readlane_f(row_max16_dpp(gm), 0);
+        uint32_t rl = 0xffffffffu;
+#pragma unroll
+        for (int g = 0; g < FS_NG; ++g) rl = tg[g] == W ? min(rl, rg[g]) : rl;
+        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)wave_min_to63_u32_dpp(rl), 63);
+        const int wl = (int)__builtin_ctzll(__ballot(rl == R));
+        const int sl = (int)(R & 31u);
+        const uint32_t rank = R >> 5;
+        int kwin = (int)bitrev_bits(rank >> LQ, L) + (int)(rank & ((1u << LQ) - 1u)) * bs;
+        asm volatile("" : "+s"(kwin));
+        const float wx = VX[sl], wy = VY[sl], wz = VZ[sl];
+        const int buf = j & 1;
+        if (lane == wl) {
+            s_cand[buf][wv] = make_float4(wx, wy, wz, W);
+            s_r[buf][wv] = R;
+            s_k[buf][wv] = kwin;
+        }
+        lds_barrier();
+        const float4 c = s_cand[buf][lane & (FS_NW - 1)];
+        const uint32_t cr = s_r[buf][lane & (FS_NW - 1)];
+        const int ck = s_k[buf][lane & (FS_NW - 1)];
+        asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(cr), "v"(ck));
+        const float gmax = readlane_f(row_max16_dpp(c.w), 0);
+        const uint32_t rr = c.w == gmax ? cr : 0xffffffffu;
+        const uint32_t rmin = (uint32_t)__builtin_amdgcn_readlane((int)row_min16_u32_dpp(rr), 0);
+        const int gw = (int)__builtin_ctzll(__ballot(rr == rmin));
+        const int old = __builtin_amdgcn_readlane(ck, gw);
+        x1 = readlane_f(c.x, gw);
+        y1 = readlane_f(c.y, gw);
+        z1 = readlane_f(c.z, gw);
+        if (tid == 0) {
+            idx_out[(size_t)cloud * m + j] = old;
+            if (sampled_out) {
+                float *o = sampled_out + ((size_t)cloud * m + j) * 3;
+                o[0] = x1; o[1] = y1; o[2] = z1;
+            }
+        }
+    }
+    if (temp_out) {
+        float *tp = temp_out + (size_t)cloud * FS_N;
+#pragma unroll
+        for (int s = 0; s < FS_S; ++s) tp[__float_as_int(SP[soff(s)].w)] = VT[s];
+    }
+}
+
 }  // namespace
 
 // Diagnostic: per-phase cycle sums of block 0 / wave 0 of the register path
@@ -933,11 +1131,17 @@ extern "C" int hreg_debug_fps_stamps(int b, int n, int m, const float *points, c
 // (fps_reg_kernel<512, 2, 16>), but 2 points per thread (n = 1024), so an iteration is the
 // dependent chain (wave max, winner pick, LDS hand-off + barrier, block max) with almost no
 // scan.  stamps as hreg_debug_fps_stamps.  points [b][1024][3].
+// stamps == nullptr: the same kernel without stamps (its launch time per iteration is the floor
+// of an unstamped kernel).
 extern "C" int hreg_debug_fps_floor(int b, int m, const float *points, int32_t *idx, uint64_t *stamps,
                                     void *stream) {
-    if (b <= 0 || m <= 0 || !points || !idx || !stamps) return HREG_ERR_INVALID;
-    hipLaunchKernelGGL((fps_reg_kernel<512, 2, 1, false, true>), dim3(b), dim3(512), 0, as_stream(stream), points,
-                       nullptr, nullptr, idx, nullptr, 1024, m, 1024, 10, __builtin_huge_valf(), stamps);
+    if (b <= 0 || m <= 0 || !points || !idx) return HREG_ERR_INVALID;
+    if (stamps)
+        hipLaunchKernelGGL((fps_reg_kernel<512, 2, 1, false, true>), dim3(b), dim3(512), 0, as_stream(stream),
+                           points, nullptr, nullptr, idx, nullptr, 1024, m, 1024, 10, __builtin_huge_valf(), stamps);
+    else
+        hipLaunchKernelGGL((fps_reg_kernel<512, 2, 1, false, false>), dim3(b), dim3(512), 0, as_stream(stream),
+                           points, nullptr, nullptr, idx, nullptr, 1024, m, 1024, 10, __builtin_huge_valf(), nullptr);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -980,6 +1184,25 @@ extern "C" int hreg_fps_bounded(int b, int n, int m, const float *points, float 
     if (concurrent < 1) return HREG_ERR_INVALID;
     return launch_fps<false>(b, n, m, points, nullptr, temp, idx, sampled_xyz, as_stream(stream), FPS_CL_POLLS,
                              -1, false, concurrent);
+}
+
+// FPS of n = 16384-point clouds over the spatial index in ws (hreg_spatial_index of the same
+// points, built before this call): fps_sorted_kernel, the selections of
+// hreg_furthest_point_sampling bit for bit with most of each iteration's scan pruned.  Other
+// sizes: hreg_furthest_point_sampling's kernels (ws unused).
+extern "C" int hreg_fps_indexed(int b, int n, int m, const float *points, const void *ws, float *temp,
+                                int32_t *idx, float *sampled_xyz, void *stream) {
+    if (b < 0 || n <= 0 || !points || !idx || !ws) return HREG_ERR_INVALID;
+    if (b == 0 || m <= 0) return HREG_OK;
+    const int bs = hreg_opt_n_threads(n);
+    if (n != FS_N || bs * (n / bs) != n || (n / bs) > 32 || (reinterpret_cast<uintptr_t>(ws) & 15))
+        return launch_fps<false>(b, n, m, points, nullptr, temp, idx, sampled_xyz, as_stream(stream));
+    const int L = hreg_ilog2(bs), LQ = hreg_ilog2(n / bs);
+    hipLaunchKernelGGL(fps_sorted_kernel, dim3(b), dim3(FS_T), 0, as_stream(stream),
+                       static_cast<const float4 *>(ws), FS_N, points, temp, idx, sampled_xyz, m, bs, L, LQ,
+                       __builtin_huge_valf());
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
 }
 
 extern "C" int hreg_weighted_furthest_point_sampling(int b, int n, int m, const float *points,

@@ -164,8 +164,12 @@ __global__ __launch_bounds__(256) void sim_colmax_kernel(const float *__restrict
     const int g = threadIdx.x >> 6;
     const float *Sb = S + (size_t)b * N1 * N2;
     float m = -__builtin_huge_valf();
-    if (c < N2)
+    // (unrolled: the loads of 16 rows issue together instead of one L2 round trip per row; the
+    // maxima still run in row order)
+    if (c < N2) {
+#pragma unroll 16
         for (int i = g; i < N1; i += 4) m = fmaxf(m, Sb[(size_t)i * N2 + c]);
+    }
     part[g][threadIdx.x & 63] = m;
     __syncthreads();
     if (g == 0 && c < N2) {
@@ -315,9 +319,21 @@ __global__ __launch_bounds__(256) void svd_pair_kernel(const float *__restrict__
 // one workgroup per group of `group` consecutive pairs (the reference's batch: its identity
 // fallback resets the whole batch it ran, layers.py:485-493; a forward of several batches
 // merged into one launch set keeps each batch's own fallback)
+// tr_xyz (hreg_weighted_svd_tr): then the group's point sets [b][tr_n][3] are moved by the pair's
+// final R, t into tr_out, with transform_kernel's arithmetic (one launch less per FineReg stage)
+__device__ __forceinline__ void transform_point(const float *Rb, const float *tb, const float *p, float *o) {
+    const float x = p[0], y = p[1], z = p[2];
+    for (int i = 0; i < 3; ++i) {
+        const float s = fadd_rn(fadd_rn(fmul_rn(Rb[i * 3], x), fmul_rn(Rb[i * 3 + 1], y)), fmul_rn(Rb[i * 3 + 2], z));
+        o[i] = fadd_rn(s, tb[i]);
+    }
+}
+
 __global__ void svd_batch_kernel(int nb, int group, float *__restrict__ R_, float *__restrict__ t_,
                                  const float *__restrict__ pR, const float *__restrict__ pt,
-                                 float *__restrict__ R, float *__restrict__ t) {
+                                 float *__restrict__ R, float *__restrict__ t,
+                                 const float *__restrict__ tr_xyz = nullptr, int tr_n = 0,
+                                 float *__restrict__ tr_out = nullptr) {
     __shared__ int bad;
     const int b0 = blockIdx.x * group, b1 = min(b0 + group, nb);
     if (threadIdx.x == 0) bad = 0;
@@ -348,6 +364,13 @@ __global__ void svd_batch_kernel(int nb, int group, float *__restrict__ R_, floa
             for (int q = 0; q < 3; ++q) t[(size_t)b * 3 + q] = tb[q];
         }
     }
+    if (!tr_xyz) return;
+    __syncthreads();  // the group's final R, t (written above by other threads) are visible
+    const float *Rf = R ? R : R_, *tf = R ? t : t_;
+    for (size_t e = (size_t)b0 * tr_n + threadIdx.x; e < (size_t)b1 * tr_n; e += blockDim.x) {
+        const size_t b = e / tr_n;
+        transform_point(Rf + b * 9, tf + b * 3, tr_xyz + e * 3, tr_out + e * 3);
+    }
 }
 
 // ---------------------------------------------------------------- transform
@@ -358,12 +381,7 @@ __global__ void transform_kernel(const float *__restrict__ xyz, const float *__r
     if (e >= total) return;
     const size_t b = e / n;
     const float *Rb = R + b * 9, *tb = t + b * 3;
-    const float x = xyz[e * 3], y = xyz[e * 3 + 1], z = xyz[e * 3 + 2];
-    for (int i = 0; i < 3; ++i) {
-        const float s = fadd_rn(fadd_rn(fmul_rn(Rb[i * 3], x), fmul_rn(Rb[i * 3 + 1], y)),
-                                fmul_rn(Rb[i * 3 + 2], z));
-        out[e * 3 + i] = fadd_rn(s, tb[i]);
-    }
+    transform_point(Rb, tb, xyz + e * 3, out + e * 3);
 }
 
 // ------------------------------------------------------- gather (point_utils)
@@ -498,6 +516,24 @@ extern "C" int hreg_weighted_svd_grouped(const float *src, const float *corres, 
     HREG_CHECK_LAUNCH();
     hipLaunchKernelGGL(svd_batch_kernel, dim3((nb + group - 1) / group), dim3(256), 0, st, nb, group, R_, t_,
                        prev_R, prev_t, R, t);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_weighted_svd_tr(const float *src, const float *corres, const float *w, int nb, int group,
+                                    int n, const float *prev_R, const float *prev_t, float *R_, float *t_,
+                                    float *R, float *t, const float *tr_xyz, int tr_n, float *tr_out,
+                                    void *stream) {
+    if (!src || !corres || !w || !R_ || !t_ || nb < 0 || n <= 0 || group <= 0) return HREG_ERR_INVALID;
+    if ((prev_R == nullptr) != (prev_t == nullptr)) return HREG_ERR_INVALID;
+    if ((R == nullptr) != (t == nullptr)) return HREG_ERR_INVALID;
+    if (!tr_xyz || !tr_out || tr_n <= 0) return HREG_ERR_INVALID;
+    if (!nb) return HREG_OK;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(svd_pair_kernel, dim3(nb), dim3(256), 0, st, src, corres, w, n, R_, t_);
+    HREG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(svd_batch_kernel, dim3((nb + group - 1) / group), dim3(256), 0, st, nb, group, R_, t_,
+                       prev_R, prev_t, R, t, tr_xyz, tr_n, tr_out);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

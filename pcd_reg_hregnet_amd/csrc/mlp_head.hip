@@ -286,16 +286,26 @@ __global__ __launch_bounds__(K::CW * 64) void mlp_head6_jt_kernel(const float *_
     }
 }
 
+// row_tiles (bf16x6 heads): 0 = HeadJT's tiles per workgroup (the weight pieces of a chunk feed
+// 2-4 row tiles: fewer weight bytes per MFMA, for launches that share the chip); 1 = one row tile
+// per workgroup, 2-4x the workgroups, for a forward alone on the GPU, where a batch-8 head is
+// 32-128 workgroups on 256 CUs (engine.chain_fork).  Each row's sums are the same either way.
 template <class K, bool B6>
-int launch_head(const float *table, const float *x, int ldx, int G, int mode, float *out, void *stream) {
+int launch_head(const float *table, const float *x, int ldx, int G, int mode, float *out, void *stream,
+                int row_tiles = 0) {
     const int NT = G / 32;
     if (B6 && (reinterpret_cast<uintptr_t>(table) & 15)) return HREG_ERR_INVALID;
     if constexpr (B6 && HREG_HEAD_JT) {
         constexpr int JT = HeadJT<K::C>::v;
-        int grid = (NT + JT - 1) / JT;
+        const int jt = row_tiles == 1 ? 1 : JT;
+        int grid = (NT + jt - 1) / jt;
         if (grid > 2048) grid = 2048;
-        hipLaunchKernelGGL((mlp_head6_jt_kernel<K, JT>), dim3(grid), dim3(K::CW * 64), 0, as_stream(stream),
-                           table, x, ldx, G, mode, out);
+        if (jt == 1)
+            hipLaunchKernelGGL((mlp_head6_jt_kernel<K, 1>), dim3(grid), dim3(K::CW * 64), 0, as_stream(stream),
+                               table, x, ldx, G, mode, out);
+        else
+            hipLaunchKernelGGL((mlp_head6_jt_kernel<K, JT>), dim3(grid), dim3(K::CW * 64), 0, as_stream(stream),
+                               table, x, ldx, G, mode, out);
     } else {
         int grid = (NT + K::RT - 1) / K::RT;
         if (grid > 2048) grid = 2048;
@@ -330,9 +340,9 @@ extern "C" int hreg_mlp_head6_table_floats(int C) {
 
 template <bool B6>
 static int mlp_head_entry(const float *table, int C, const float *x, int ldx, int nclouds, int rows_per_cloud,
-                          int mode, float *out, float *weights_out, void *stream) {
+                          int mode, float *out, float *weights_out, void *stream, int row_tiles = 0) {
     if (!table || !x || !out || nclouds < 0 || rows_per_cloud <= 0 || ldx < C || (ldx & 3) ||
-        (mode != HREG_HEAD_SOFTPLUS && mode != HREG_HEAD_SIGMOID))
+        (mode != HREG_HEAD_SOFTPLUS && mode != HREG_HEAD_SIGMOID) || row_tiles < 0 || row_tiles > 1)
         return HREG_ERR_INVALID;
     if (reinterpret_cast<uintptr_t>(x) & 15) return HREG_ERR_INVALID;
     const int G = nclouds * rows_per_cloud;
@@ -341,10 +351,10 @@ static int mlp_head_entry(const float *table, int C, const float *x, int ldx, in
     if (!G) return HREG_OK;
     int rc;
     switch (C) {
-        case 64: rc = launch_head<H64, B6>(table, x, ldx, G, mode, out, stream); break;
-        case 128: rc = launch_head<H128, B6>(table, x, ldx, G, mode, out, stream); break;
-        case 256: rc = launch_head<H256, B6>(table, x, ldx, G, mode, out, stream); break;
-        default: rc = launch_head<H512, B6>(table, x, ldx, G, mode, out, stream); break;
+        case 64: rc = launch_head<H64, B6>(table, x, ldx, G, mode, out, stream, row_tiles); break;
+        case 128: rc = launch_head<H128, B6>(table, x, ldx, G, mode, out, stream, row_tiles); break;
+        case 256: rc = launch_head<H256, B6>(table, x, ldx, G, mode, out, stream, row_tiles); break;
+        default: rc = launch_head<H512, B6>(table, x, ldx, G, mode, out, stream, row_tiles); break;
     }
     if (rc != HREG_OK || !weights_out) return rc;
     return hreg_sigma_weights(out, nclouds, rows_per_cloud, weights_out, stream);
@@ -358,4 +368,11 @@ extern "C" int hreg_mlp_head(const float *table, int C, const float *x, int ldx,
 extern "C" int hreg_mlp_head6(const float *table, int C, const float *x, int ldx, int nclouds,
                               int rows_per_cloud, int mode, float *out, float *weights_out, void *stream) {
     return mlp_head_entry<true>(table, C, x, ldx, nclouds, rows_per_cloud, mode, out, weights_out, stream);
+}
+
+extern "C" int hreg_mlp_head6x(const float *table, int C, const float *x, int ldx, int nclouds,
+                               int rows_per_cloud, int mode, float *out, float *weights_out, int row_tiles,
+                               void *stream) {
+    return mlp_head_entry<true>(table, C, x, ldx, nclouds, rows_per_cloud, mode, out, weights_out, stream,
+                                row_tiles);
 }

@@ -71,11 +71,18 @@ FRONT_STREAM_MAX_LANES = switches.integer("FRONT_STREAM_MAX_LANES", 24)
 FRONT_FOREACH = switches.flag("FRONT_FOREACH", True)  # front outputs -> static buffers: one foreach copy
 # Single-batch latency (one forward alone on the GPU is one dependent chain of ~50 kernels): work
 # that does not depend on the chain's previous kernel runs beside it on a side stream -- the
-# level-1 spatial index (input points only) beside the level-1 FPS, and the level-2/3 input
-# projection (the previous level's features only) beside that level's WFPS + kNN.  On only where
+# level-1 spatial index (input points only) beside the level-1 FPS, the level-2/3 input
+# projection (the previous level's features only) beside that level's WFPS + kNN, CoarseReg's two
+# kNN selections beside the grouped head products and its neighbour head beside the first
+# similarity gather -- and the MLP heads take one row tile per workgroup.  On only where
 # chain_fork() enables it (the 1-lane GraphPipeline and bench.py's eager latency figure): with
 # many lanes in flight the chip is already full and a fork only adds streams.
 CHAIN_FORK = switches.flag("CHAIN_FORK", True)
+# Level-1 FPS over the spatial index's Morton-sorted copy with exact group pruning
+# (fps.hip fps_sorted_kernel, hreg_fps_indexed): the index is built first and the FPS skips the
+# 256-point groups its new centre cannot change; the same selections.  Clouds of FPS_SORTED_N.
+FPS_SORTED = switches.flag("FPS_SORTED", True)
+FPS_SORTED_N = 16384
 # timing probe (tools only): the level-1 grouping into preallocated buffers skips its FPS (1), its
 # spatial index + kNN (2) or its spatial index (3), leaving the buffers' previous values (static
 # inputs: unchanged)
@@ -817,6 +824,19 @@ def fps(xyz, npoint, weights=None, out=None, concurrent=0):
     return idx, sampled
 
 
+def fps_indexed(xyz, npoint, ws, out=None):
+    """FPS of nb clouds of FPS_SORTED_N points over their spatial index in ws (hreg_spatial_index
+    already enqueued): hreg_fps_indexed, bitwise fps(xyz, npoint)."""
+    nb, n, _ = xyz.shape
+    if out is None:
+        idx = _empty(nb, npoint, dtype=torch.int32, device=xyz.device)
+        sampled = _empty(nb, npoint, 3, device=xyz.device)
+    else:
+        idx, sampled = out
+    call("hreg_fps_indexed", nb, n, npoint, xyz, ws, None, idx, sampled, _stream())
+    return idx, sampled
+
+
 def head_out(x, C, nclouds, rows, w3, b3, mode, want_weights=False):
     dev = x.device
     out = _empty(nclouds * rows, device=dev)
@@ -892,10 +912,10 @@ def knn_group_indexed(q, p, k, ws, out=None, build=True):
     return gidx, geom, kx
 
 
-def knn_idx32(p1, p2, k):
+def knn_idx32(p1, p2, k, out=None):
     b, n1, d = p1.shape
     n2 = p2.shape[1]
-    idx = _empty(b, n1, k, dtype=torch.int32, device=p1.device)
+    idx = _empty(b, n1, k, dtype=torch.int32, device=p1.device) if out is None else out
     call("hreg_knn_points", p1, p2, b, n1, n2, d, k, None, None, idx, None, _stream())
     return idx
 
@@ -963,6 +983,17 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_co
     M, k = LEVELS[lvl][:2]
     nb, n, _ = xyz.shape
     use_si = SPATIAL_KNN_MIN <= n <= SPATIAL_KNN_MAX
+    if (FPS_SORTED and use_si and n == FPS_SORTED_N and weights is None and sample is None
+            and not PROBE_S1_SKIP):
+        # the index first: the FPS reads its Morton-sorted copy (fps_indexed), the kNN its blocks
+        if ws is None:
+            ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
+        call("hreg_spatial_index", xyz, nb, n, ws, _stream())
+        idx, sampled = fps_indexed(xyz, M, ws, out=None if out is None else out[:2])
+        gidx, geom, kx = knn_group_indexed(sampled, xyz, k, ws, out=None if out is None else out[2:5],
+                                           build=False)
+        _record_knn(f"knn_{lvl + 1}", gidx, nb, n, k, True)
+        return idx, sampled, gidx, geom, kx
     fk = _fork_begin() if (_fork_on and use_si and sample is None and not PROBE_S1_SKIP) else None
     if fk is not None:
         if ws is None:
@@ -1160,8 +1191,10 @@ def mlp_head(P: PreparedWeights, key, x, nclouds, rows, mode, want_weights=False
                 wout.fill_(1.0)
             return out, wout
         if B6_MLP:
-            call("hreg_mlp_head6", P.head_table6[key], C, x, C, nclouds, rows, mode, out, wout,
-                 _stream())
+            # (chain_fork: a forward alone) one row tile per workgroup -- a batch-8 head is 32-128
+            # workgroups at the default 2-4 tiles each
+            call("hreg_mlp_head6x", P.head_table6[key], C, x, C, nclouds, rows, mode, out, wout,
+                 1 if _fork_on else 0, _stream())
         else:
             call("hreg_mlp_head", P.head_table[key], C, x, C, nclouds, rows, mode, out, wout,
                  _stream())
@@ -1222,9 +1255,32 @@ def head_products(P: PreparedWeights, B: int, desc):
     return {"nbr_pre": nbr_pre, "ud": ud, "S": S, "fine_pre": fine}
 
 
-def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3, prod=None):
+def coarse_knns(B, xyz3, desc3, out=None):
+    """CoarseReg's two kNN selections, which depend on the level-3 keypoints only: the
+    descriptor-space kNN src -> dst (layers.py:278) and the xyz kNN of every keypoint among its
+    own cloud's (layers.py:315-337).  out: (kidx, (gidx, geom, kx)) preallocated."""
+    k = K_HEAD
+    N1 = xyz3.shape[1]
+    C = desc3.shape[1]
+    s_desc, d_desc = desc3[:B * N1], desc3[B * N1:]
+    kidx = knn_idx32(s_desc.view(B, N1, C), d_desc.view(B, N1, C), k, out=None if out is None else out[0])
+    g = knn_group(xyz3, xyz3, k, out=None if out is None else out[1])
+    return kidx, g
+
+
+def coarse_knns_alloc(B, xyz3):
+    dev = xyz3.device
+    N1 = xyz3.shape[1]
+    R2 = 2 * B * N1 * K_HEAD
+    return (_empty(B, N1, K_HEAD, dtype=torch.int32, device=dev),
+            (_empty(R2, dtype=torch.int32, device=dev), _empty(R2, 4, device=dev), _empty(R2, 3, device=dev)))
+
+
+def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3, prod=None, knns=None):
     """CoarseReg.forward (layers.py:273-396); xyz3 [2B,256,3], desc3 [2B*256,256], sig3 [2B*256].
-    prod: head_products' precomputed blocks and original similarity (else computed here)."""
+    prod: head_products' precomputed blocks and original similarity (else computed here);
+    knns: coarse_knns' result computed ahead (else computed here).  Under chain_fork() the
+    neighbour head runs on a side stream beside the first similarity gather."""
     dev = xyz3.device
     k = K_HEAD
     N1 = xyz3.shape[1]
@@ -1232,9 +1288,22 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3, prod=None):
     s_desc, d_desc = desc3[:B * N1], desc3[B * N1:]
     s_xyz, d_xyz = xyz3[:B], xyz3[B:]
     s_sig, d_sig = sig3[:B * N1], sig3[B * N1:]
-    # desc-space kNN (layers.py:278)
-    kidx = knn_idx32(s_desc.view(B, N1, C), d_desc.view(B, N1, C), k)
+    # desc-space kNN (layers.py:278) and the keypoints' own-cloud kNN (layers.py:315-337)
+    kidx, (gself, geom_self, _) = knns if knns is not None else coarse_knns(B, xyz3, desc3)
     _record_knn("coarse_desc_knn", kidx, B, N1, k, False)
+    _record_knn("coarse_nbr", gself, 2 * B, N1, k, True)
+    G2 = 2 * B * N1
+    R2 = G2 * k
+    b6 = B6_HEADS and HEAD_PRE
+    # (chain_fork) the fused neighbour head beside the first similarity gather
+    fk = (_fork_begin() if (_fork_on and prod is not None and FUSED_NBR and C == 256 and b6 and SPLIT_NBR)
+          else None)
+    if fk is not None:
+        nbr = _empty(G2, C, device=dev)
+        main, side = fk
+        with torch.cuda.stream(side):
+            call("hreg_nbr_head6sx", P.nbr_table6, desc3, gself, geom_self, G2, nbr, prod["nbr_pre"],
+                 HEAD_ROW_TILES, _stream())
     # original similarity (layers.py:290-313)
     if prod is not None:
         S = prod["S"]
@@ -1246,13 +1315,10 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3, prod=None):
     maxes = _empty(B, 2 * N1, device=dev)
     call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_a, 2, _stream())
     # neighbour-aware descriptors for src and dst together (layers.py:315-337)
-    gself, geom_self, _ = knn_group(xyz3, xyz3, k)
-    _record_knn("coarse_nbr", gself, 2 * B, N1, k, True)
-    G2 = 2 * B * N1
-    R2 = G2 * k
-    if FUSED_NBR and C == 256:
+    if fk is not None:
+        main.wait_stream(side)
+    elif FUSED_NBR and C == 256:
         nbr = _empty(G2, C, device=dev)
-        b6 = B6_HEADS and HEAD_PRE
         if prod is not None:
             pre = prod["nbr_pre"]
         else:
@@ -1371,10 +1437,12 @@ def fine_reg(P: PreparedWeights, name, B, src_xyz, src_desc, dst_xyz, dst_desc, 
     return corres.view(B, N, 3), w.view(B, N)
 
 
-def weighted_svd(src, corres, w, prev=None, group=None):
+def weighted_svd(src, corres, w, prev=None, group=None, move=None):
     """WeightedSVDHead (layers.py:469-504) (+ T = T_ @ T_prev, models.py:100-127).  group:
     the pairs are batches of `group` pairs merged into one call (the identity fallback of
-    layers.py:485-493 per batch); None = one batch."""
+    layers.py:485-493 per batch); None = one batch.  move [B, n2, 3]: points to move by the
+    final R, t in the same launches (hreg_weighted_svd_tr; the next FineReg stage's src
+    keypoints) -> (R_, t_, R, t, moved) instead of (R_, t_, R, t)."""
     B, n, _ = src.shape
     dev = src.device
     R_ = _empty(B, 3, 3, device=dev)
@@ -1382,6 +1450,13 @@ def weighted_svd(src, corres, w, prev=None, group=None):
     R = _empty(B, 3, 3, device=dev)
     t = _empty(B, 3, device=dev)
     pR, pt = (prev if prev is not None else (None, None))
+    if move is not None:
+        if group is not None and B % group:
+            raise ValueError(f"weighted_svd: {B} pairs are not whole batches of {group}")
+        moved = torch.empty_like(move)
+        call("hreg_weighted_svd_tr", src, corres, w, B, B if group is None else group, n, pR, pt, R_, t_, R, t,
+             move, move.shape[1], moved, _stream())
+        return R_, t_, R, t, moved
     if group is None or group == B:
         call("hreg_weighted_svd", src, corres, w, B, n, pR, pt, R_, t_, R, t, _stream())
     else:
@@ -1449,11 +1524,22 @@ def hregnet_back(P: PreparedWeights, fe, B: int, v2=False, sub_batch=None):
     xyz = [fe[f"xyz_{i + 1}"] for i in range(3)]
     sig = [fe[f"sigmas_{i + 1}"] for i in range(3)]
     desc = [fe[f"desc_{i + 1}"] for i in range(3)]
-    prod = head_products(P, B, desc) if _grouped_heads_ok(desc[2].shape[1]) else None
+    grouped = _grouped_heads_ok(desc[2].shape[1])
+    # (chain_fork) CoarseReg's kNN selections beside the grouped head products
+    fk = _fork_begin() if (_fork_on and grouped) else None
+    knns = None
+    if fk is not None:
+        knns = coarse_knns_alloc(B, xyz[2])
+        main, side = fk
+        with torch.cuda.stream(side):
+            coarse_knns(B, xyz[2], desc[2], out=knns)
+    prod = head_products(P, B, desc) if grouped else None
+    if fk is not None:
+        main.wait_stream(side)
     fpre = (lambda name: None) if prod is None else (lambda name: prod["fine_pre"][name])
-    c3, w3 = coarse_reg(P, B, xyz[2], desc[2], sig[2], prod)
-    _, _, R3, t3 = weighted_svd(xyz[2][:B], c3, w3, group=sub_batch)
-    x2t = transform(xyz[1][:B], R3, t3)
+    c3, w3 = coarse_reg(P, B, xyz[2], desc[2], sig[2], prod, knns=knns)
+    # (the src level-2 keypoints moved by (R3, t3) in the SVD's batch launch)
+    _, _, R3, t3, x2t = weighted_svd(xyz[2][:B], c3, w3, group=sub_batch, move=xyz[1][:B])
     sd2, dd2 = split(desc[1], M[1])
     ss2, ds2 = split(sig[1], M[1])
     if v2:
@@ -1465,8 +1551,7 @@ def hregnet_back(P: PreparedWeights, fe, B: int, v2=False, sub_batch=None):
     else:
         c2, w2 = fine_reg(P, "fine_corres_2", B, x2t, sd2, xyz[1][B:], dd2, ss2, ds2,
                           pre=fpre("fine_corres_2"))
-    _, _, R2, t2 = weighted_svd(x2t, c2, w2, prev=(R3, t3), group=sub_batch)
-    x1t = transform(xyz[0][:B], R2, t2)
+    _, _, R2, t2, x1t = weighted_svd(x2t, c2, w2, prev=(R3, t3), group=sub_batch, move=xyz[0][:B])
     sd1, dd1 = split(desc[0], M[0])
     ss1, ds1 = split(sig[0], M[0])
     c1, w1 = fine_reg(P, "fine_corres_1", B, x1t, sd1, xyz[0][B:], dd1, ss1, ds1,

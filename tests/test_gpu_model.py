@@ -992,6 +992,33 @@ def test_model_v2_merged_batches_match_separate_forwards(net_v2):
     R1_, _, _, _ = engine.weighted_svd(x, c, w)  # one batch of 6: all reset
     assert all(torch.equal(R1_[i], eye) for i in range(6))
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", [("det", 0), ("det", 1), ("det", 2), "coarse"])
+def test_mlp_head_row_tiles(net, key):
+    """hreg_mlp_head6x with one 32-row tile per workgroup (chain_fork's single-forward form) vs
+    the default 2-4 tiles per workgroup: the same bits, sigma / weight outputs and the per-cloud
+    weights alike, with a tile count that leaves the last workgroup's group partial."""
+    from pcd_reg_hregnet_amd import _lib
+    P = net.prepared(torch.device("cuda"))
+    C = {("det", 0): 64, ("det", 1): 128, ("det", 2): 256, "coarse": 512}[key]
+    nclouds, rows = 3, 96  # 9 tiles of 32 rows
+    g = torch.Generator(device="cpu").manual_seed(C)
+    x = torch.randn(nclouds * rows, C, generator=g).cuda()
+    mode = _lib.HREG_HEAD_SOFTPLUS if key != "coarse" else _lib.HREG_HEAD_SIGMOID
+    res = []
+    for rt in (0, 1):
+        out = torch.full((nclouds * rows,), float("nan"), device="cuda")
+        w = torch.full((nclouds * rows,), float("nan"), device="cuda") if key != "coarse" else None
+        _lib.call("hreg_mlp_head6x", P.head_table6[key], C, x, C, nclouds, rows, mode, out, w, rt,
+                  _lib.stream_handle())
+        res.append((out, w))
+    torch.cuda.synchronize()
+    assert not torch.isnan(res[0][0]).any()
+    assert torch.equal(res[0][0], res[1][0])
+    if key != "coarse":
+        assert torch.equal(res[0][1], res[1][1])
+
+
 
 @pytest.mark.parametrize("G", [2048, 2044])
 def test_coarse_head_row_tiles(net, G):

@@ -65,6 +65,42 @@ def test_fps_vs_oracle(n, m, weighted):
     np.testing.assert_array_equal(idx.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("kind", ["lidar", "uniform_ties", "grid_dups", "line"])
+def test_fps_indexed_matches_fps(kind):
+    """hreg_fps_indexed (level-1 FPS over the spatial index's sorted copy, exact group pruning):
+    indices and running minima bitwise those of hreg_furthest_point_sampling and the oracle's --
+    including clouds whose ties the reference order must break (rounded coordinates, an integer
+    grid with ~16 copies of every point, whose last selections are all at T = 0, and a line)."""
+    from pcd_reg_hregnet_amd import engine, synthetic, _lib
+    n, m, B = 16384, 1024, 3
+    rng = np.random.default_rng({"lidar": 1, "uniform_ties": 2, "grid_dups": 3, "line": 4}[kind])
+    if kind == "lidar":
+        s, d, _, _ = synthetic.lidar_batch(2, n, seed0=12)
+        xyz = np.concatenate([s, d])[:B]
+    elif kind == "uniform_ties":
+        xyz = rng.uniform(-40, 40, (B, n, 3)).astype(np.float32)
+        xyz[:, ::2] = np.round(xyz[:, ::2])
+    elif kind == "grid_dups":
+        xyz = rng.integers(-5, 5, (B, n, 3)).astype(np.float32)
+    else:
+        t = rng.integers(0, 3000, (B, n)).astype(np.float32)
+        xyz = np.stack([t * 0.01, -t * 0.02, np.full_like(t, 3.0)], -1).astype(np.float32)
+    xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+    x = dev(xyz)
+    ws = torch.empty(engine.spatial_index_bytes(B, n), dtype=torch.uint8, device="cuda")
+    _lib.call("hreg_spatial_index", x, B, n, ws, _lib.stream_handle())
+    idx = torch.full((B, m), -1, dtype=torch.int32, device="cuda")
+    temp = torch.full((B, n), -1.0, device="cuda")
+    _lib.call("hreg_fps_indexed", B, n, m, x, ws, temp, idx, None, _lib.stream_handle())
+    ref = torch.full((B, m), -2, dtype=torch.int32, device="cuda")
+    rtemp = torch.full((B, n), -2.0, device="cuda")
+    _lib.call("hreg_furthest_point_sampling", B, n, m, x, rtemp, ref, None, _lib.stream_handle())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref.cpu().numpy())
+    assert torch.equal(temp, rtemp)
+    np.testing.assert_array_equal(idx.cpu().numpy()[:1], oracle.fps(xyz[:1], m, None))
+
+
 def test_fps_cluster_many_clouds_and_mem_path():
     """n > 16384 runs on the multi-workgroup kernel; more clouds than resident clusters
     (256 / 64 participants = 4) loop; HREG_FPS_MEM forces the single-workgroup
@@ -306,6 +342,30 @@ def test_weighted_svd_nonfinite_batch_fallback():
     _, _, R, t = engine.weighted_svd(dev(src), dev(cor), dev(w))
     np.testing.assert_array_equal(R.cpu().numpy(), np.tile(np.eye(3, dtype=np.float32), (3, 1, 1)))
     np.testing.assert_array_equal(t.cpu().numpy(), np.zeros((3, 3), np.float32))
+
+
+@pytest.mark.parametrize("group,with_prev", [(None, False), (4, True), (2, False)])
+def test_weighted_svd_move_matches_transform(group, with_prev):
+    """hreg_weighted_svd_tr (weighted_svd(move=)): R_, t_, R, t and the moved points are bitwise
+    weighted_svd followed by transform, per batch group and with a previous transform composed."""
+    from pcd_reg_hregnet_amd import engine
+    rng = np.random.default_rng(9)
+    B, n, n2 = 8, 256, 512
+    src = dev(rng.uniform(-20, 20, (B, n, 3)).astype(np.float32))
+    cor = dev(rng.uniform(-20, 20, (B, n, 3)).astype(np.float32))
+    w = dev(rng.uniform(0.1, 1.0, (B, n)).astype(np.float32))
+    pts = dev(rng.uniform(-20, 20, (B, n2, 3)).astype(np.float32))
+    prev = None
+    if with_prev:
+        _, _, pR, pt = engine.weighted_svd(cor, src, w)
+        prev = (pR, pt)
+    a = engine.weighted_svd(src, cor, w, prev=prev, group=group)
+    ref_moved = engine.transform(pts, a[2], a[3])
+    b = engine.weighted_svd(src, cor, w, prev=prev, group=group, move=pts)
+    torch.cuda.synchronize()
+    for x, y in zip(a, b[:4]):
+        assert torch.equal(x, y)
+    assert torch.equal(ref_moved, b[4])
 
 
 def test_transform_points():

@@ -346,7 +346,8 @@ def test_bench_entry_peaks():
           "hreg_group_split6_l2", "hreg_group_split6_l3", "hreg_group_split6j_l3", "hreg_group_split6p_l3",
           "hreg_group6_l3",
           "hreg_fine_head6", "hreg_nbr_head6", "hreg_nbr_head6s", "hreg_nbr_head6sx",
-          "hreg_coarse_head6", "hreg_corr_head6", "hreg_corr_head6x", "hreg_mlp_head6", "hreg_gemm6"}
+          "hreg_coarse_head6", "hreg_corr_head6", "hreg_corr_head6x", "hreg_mlp_head6", "hreg_mlp_head6x",
+              "hreg_gemm6"}
     for name in set(bench.MFMA_ENTRIES) | {"hreg_gemm", "hreg_gemm6"}:
         want = bench.PEAK_B6_TFLOPS if name in b6 else bench.PEAK_FP32_MFMA_TFLOPS
         assert bench.entry_peak(name) == want, name
