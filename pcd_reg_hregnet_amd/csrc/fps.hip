@@ -929,6 +929,23 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
 // candidate per group is (max T, min rank among its slots at that T), the wave's is (max T, min
 // rank), and the workgroup's the same over the 8 waves.
 constexpr int FS_T = 512, FS_NW = 8, FS_S = 32, FS_NG = 8, FS_N = FS_T * FS_S;
+// A/B switches, both measured no faster (gpurun_out/r5ag, the FPS alone, 16 clouds, three
+// alternations: 0.956-0.958 us per iteration with neither, 0.967-0.972 with the tree,
+// 0.959-0.961 with both).  HREG_FS_TREE: the lane's candidate rank at the wave max as 8
+// independent selects + a v_min3_u32 tree instead of a serial select/min chain.  HREG_FS_EXPECT:
+// the group scans laid out as unlikely, so a skipped group falls through.
+#ifndef HREG_FS_TREE
+#define HREG_FS_TREE 0
+#endif
+#ifndef HREG_FS_EXPECT
+#define HREG_FS_EXPECT 0
+#endif
+
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 __device__ __forceinline__ uint32_t row_min16_u32_dpp(uint32_t v) {
     uint32_t r;
@@ -1038,7 +1055,7 @@ __global__ __launch_bounds__(FS_T) void fps_sorted_kernel(const float4 *__restri
         const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
 #pragma unroll
         for (int g = 0; g < FS_NG; ++g) {
-            if (amask & (1u << g)) {
+            if (HREG_FS_EXPECT ? __builtin_expect((amask >> g) & 1u, 0u) : (amask >> g) & 1u) {
 #pragma unroll
                 for (int s = 2 * g; s < 2 * g + 2; ++s) {
                     const f2 dx = pair_of(VX, s) - X1, dy = pair_of(VY, s) - Y1, dz = pair_of(VZ, s) - Z1;
@@ -1062,8 +1079,15 @@ __global__ __launch_bounds__(FS_T) void fps_sorted_kernel(const float4 *__restri
         // one lane holds the max measured 1.04 vs 0.96 us per iteration)
         const float W = readlane_f(row_max16_dpp(gm), 0);
         uint32_t rl = 0xffffffffu;
+        if constexpr (HREG_FS_TREE) {
+            uint32_t c[FS_NG];
 #pragma unroll
-        for (int g = 0; g < FS_NG; ++g) rl = tg[g] == W ? min(rl, rg[g]) : rl;
+            for (int g = 0; g < FS_NG; ++g) c[g] = tg[g] == W ? rg[g] : 0xffffffffu;
+            rl = min(umin3(c[0], c[1], c[2]), umin3(c[3], c[4], umin3(c[5], c[6], c[7])));
+        } else {
+#pragma unroll
+            for (int g = 0; g < FS_NG; ++g) rl = tg[g] == W ? min(rl, rg[g]) : rl;
+        }
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)wave_min_to63_u32_dpp(rl), 63);
         const int wl = (int)__builtin_ctzll(__ballot(rl == R));
         const int sl = (int)(R & 31u);
