@@ -175,11 +175,9 @@ MFMA_ENTRIES = {
     "hreg_group_split_l2": ("level", _level_work(2)),
     "hreg_group_split_l3": ("level", _level_work(3)),
     "hreg_group6_l2": ("level", _level_work(2)),
-    "hreg_group6x2_l2": ("level", _level_work(2)),
     "hreg_group_split6_l2": ("level", _level_work(2)),
     "hreg_group_split6_l3": ("level", _level_work(3)),
     "hreg_group_split6j_l3": ("level", _level_work(3)),
-    "hreg_group_split6p_l3": ("level", _level_work(3)),
     "hreg_group6_l3": ("level", _level_work(3)),
     "hreg_fine_head": ("head", _fine_work),
     "hreg_nbr_head": ("head", _nbr_work),
@@ -298,13 +296,9 @@ def level_kernel(engine, lv: int) -> str:
     split = engine.SPLIT_L2 if lv == 2 else engine.SPLIT_L3
     b6 = engine.B6_L2 if lv == 2 else engine.B6_L3
     if split:
-        if b6 and lv == 3 and engine.L3_PIECES and engine.LEVEL_PRE:
-            return "group_split6p_kernel"  # activations as bf16x6 pieces in LDS (csrc/group_split6.hip)
         if b6 and lv == 3 and engine.SPLIT_JT and engine.LEVEL_PRE:
             return "group_split6j_kernel"  # two row tiles per workgroup (csrc/group_split6.hip)
         return "group_split6_kernel" if b6 else "group_split_kernel"
-    if b6 and lv == 2 and engine.PAIR_L2 and engine.LEVEL_PRE:
-        return "group_pair6_kernel"
     return "group_fused6_kernel" if b6 else "group_fused_kernel"
 
 
@@ -333,19 +327,27 @@ def pmc_traffic(kernel: str, workload: str):
     return None, None
 
 
-def cpu_baseline(budget_s: float = 30.0, batches=(1, PAIRS_PER_GPU), reps: int = 3):
+def cpu_baseline(budget_s: float = 30.0, batches=(1, PAIRS_PER_GPU), reps: int = 3, v2: bool = False):
     """The oracle (numpy BLAS + the OpenMP C restatement of FPS / kNN, oracle/) on the host
     cores, timed as BASELINE.md section 4 asks: the same synthetic pairs as the GPU run at
-    B=1 and B=8, 1 warm-up, median of `reps` runs each (time.perf_counter).  value = the
-    B=8 median (the GPU line's workload); a batch size whose runs would overrun the budget
-    (estimated from the B=1 time) is skipped and named in `sample`."""
+    B=1 and B=8 (Model_V2: B=1 and 2 at 65536 points), 1 warm-up, median of `reps` runs each
+    (time.perf_counter).  value = the largest batch's median (the GPU line's workload); a batch
+    size whose runs would overrun the budget (estimated from the B=1 time) is skipped and named
+    in `sample`."""
     from oracle import oracle
     from pcd_reg_hregnet_amd import synthetic, weights
-    from pcd_reg_hregnet_amd.models import HRegNet
+    from pcd_reg_hregnet_amd.models import HRegNet, Model_V2
+    points = V2_POINTS if v2 else POINTS
     sd = {k: v.numpy() for k, v in
-          weights.make_state_dict(HRegNet(_Args()).state_dict(), seed=0).items()}
-    s, d, _, _ = synthetic.lidar_batch(max(batches), POINTS, seed0=0)
-    oracle.hregnet_forward(sd, s[:1], d[:1])  # warm-up
+          weights.make_state_dict((Model_V2 if v2 else HRegNet)(_Args()).state_dict(), seed=0).items()}
+    s, d, _, _ = synthetic.lidar_batch(max(batches), points, seed0=0)
+
+    def fwd(B):
+        if v2:  # (the prime shuffles: fixed permutations; their draw is not the measured work)
+            perm = np.roll(np.arange(B), 1)
+            return oracle.model_v2_forward(sd, s[:B], d[:B], perm, perm)
+        return oracle.hregnet_forward(sd, s[:B], d[:B])
+    fwd(1)  # warm-up
     t_start = time.perf_counter()
     per_b, med = {}, {}
     for B in batches:
@@ -354,7 +356,7 @@ def cpu_baseline(budget_s: float = 30.0, batches=(1, PAIRS_PER_GPU), reps: int =
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
-            oracle.hregnet_forward(sd, s[:B], d[:B])
+            fwd(B)
             ts.append(time.perf_counter() - t0)
         med[B] = float(np.median(ts)) / B  # s per pair
         per_b[f"B={B}"] = {"pairs_per_s": round(1.0 / med[B], 4),
@@ -369,9 +371,9 @@ def cpu_baseline(budget_s: float = 30.0, batches=(1, PAIRS_PER_GPU), reps: int =
     return {"value": round(1.0 / med[best_b], 4), "unit": "pairs/s",
             "cores": min(threads, affinity), "omp_threads": threads, "affinity_cpus": affinity,
             "host_cpus": os.cpu_count(), "kind": "port", "batch": best_b, "per_batch": per_b,
-            "sample": f"2x{POINTS}-pt KITTI-shape synthetic LiDAR pairs (the GPU run's "
-                      f"generator), B in {sorted(med)}, 1 warm-up + median of {reps} each; "
-                      "numpy BLAS + OpenMP C oracle (oracle/); value at B="
+            "sample": f"{'Model_V2' if v2 else 'HRegNet'} forward on 2x{points}-pt KITTI-shape "
+                      f"synthetic LiDAR pairs (the GPU run's generator), B in {sorted(med)}, 1 "
+                      f"warm-up + median of {reps} each; numpy BLAS + OpenMP C oracle (oracle/); value at B="
                       f"{best_b}; {threads} OpenMP/BLAS threads = OMP_NUM_THREADS as the GPU box "
                       "sets it: the box's CPU share per GPU (the host's other CPUs serve the "
                       "other GPUs' jobs; affinity_cpus is the whole mask); reference Python on 8 "
@@ -454,6 +456,14 @@ def _fps_sorted_level(pts, m, reg):
     launch_us = ev[1].elapsed_time(ev[2]) * 1e3
     floor_us = ev[2].elapsed_time(ev[3]) * 1e3
     per = lambda us: round(us / (m - 1), 4)  # noqa: E731
+    if n > engine.FPS_SORTED_N:  # Model_V2's clouds: no floor kernel of this geometry
+        return {"kernel": "fps_blocks_kernel (level 1: one 1024-thread workgroup per cloud, running "
+                          "minima in registers, only the 64-point index blocks the new centre can change "
+                          "read from the spatial index's sorted copy; hreg_fps_indexed)",
+                "clouds": nb, "points": n, "dependent_iterations": m - 1,
+                "index_us": round(index_us, 1), "launch_us": round(launch_us, 1),
+                "us_per_iteration": per(launch_us),
+                "basis": "HIP events around the index and the FPS launch", "cluster_kernel": reg}
     return {"kernel": "fps_sorted_kernel (level 1: 512 threads x 32 points of the spatial index's "
                       "Morton-sorted copy, 256-point groups skipped when their box cannot change them; "
                       "hreg_fps_indexed, engine.FPS_SORTED)",
@@ -495,11 +505,14 @@ def fps_latency(src, dst):
         from pcd_reg_hregnet_amd import engine
         if engine.FPS_SORTED and pts.shape[1] == engine.FPS_SORTED_N:
             out["level1"] = _fps_sorted_level(pts, 1024, out["level1"])
-    else:  # Model_V2's 65536-point clouds: one cloud over up to 64 single-wave workgroups
+    else:  # Model_V2's 65536-point clouds
         out["level1"] = _fps_level(pts, 1024, None, None, None, None,
                                    "fps_cluster_kernel (level 1: one cloud over single-wave "
                                    "workgroups exchanging candidates through L2; hreg_fps_bounded, "
-                                   "one launch at a time, as the batched stage 1 runs it)")
+                                   "one launch at a time, as the r5 batched stage 1 ran it)")
+        from pcd_reg_hregnet_amd import engine
+        if engine.FPS_SORTED and engine.fps_indexed_ok(pts.shape[1]):
+            out["level1"] = _fps_sorted_level(pts, 1024, out["level1"])
     for lvl, n, m, T, kern in ((2, 1024, 512, 64, "fps_reg_kernel<64, 16, 1, weighted> (level 2: 1 wave x 16 points, "
                                                   "fps.hip HREG_FPS_W1024_1W)"),
                                (3, 512, 256, 64, "fps_reg_kernel<64, 8, 1, weighted> (level 3: 1 wave x 8 points)")):
@@ -521,7 +534,7 @@ def fps_latency(src, dst):
     return out
 
 
-def forward_latency(P, src, dst, reps: int = 7):
+def forward_latency(P, src, dst, reps: int = 7, v2: bool = False):
     """Single-batch latency (the reference's callers run one batch at a
     time, test/test_v3.py:82,120): one batch-B forward alone on the device, median of `reps`
     after 2 warm-ups, (a) launched eagerly (engine.hregnet_forward, host launches) and (b) as
@@ -541,10 +554,12 @@ def forward_latency(P, src, dst, reps: int = 7):
         return float(np.median(ts)) * 1e3
     def eager_forward():
         with engine.chain_fork():  # (the spatial index / level input projections beside the chain)
-            engine.hregnet_forward(P, src, dst)
+            out = engine.hregnet_forward(P, src, dst, v2=v2)
+            if v2:
+                engine.model_v2_finish(out)
     with torch.no_grad():
         eager = med(eager_forward)
-        gp = engine.GraphPipeline(P, src, dst, lanes=1)
+        gp = engine.GraphPipeline(P, src, dst, lanes=1, v2=v2)
         graph = med(lambda: gp.run_forwards(1))
         del gp
     B = src.shape[0]
@@ -552,6 +567,31 @@ def forward_latency(P, src, dst, reps: int = 7):
             "pairs_per_s_alone": round(B / graph * 1e3, 1),
             "basis": f"one batch of {B} pairs alone on the GPU, median of {reps} (synchronised); "
                      "graph = 1-lane GraphPipeline (stage-1 graph + rest-of-forward graph)"}
+
+
+def unmerged_line(P, src, dst, steps: int, warmup: int):
+    """the same timed steps with ONE reference batch of B pairs per executor forward
+    (merge 1, steps lanes up to LANES_MAX: the r4 configuration), timed like the headline line
+    (streamed rounds, primed, synchronised) -- reported beside the merged value, never as it."""
+    from pcd_reg_hregnet_amd import engine
+    B = src.shape[0]
+    lanes = steps if steps <= LANES_MAX else max([d for d in range(16, LANES_MAX + 1) if steps % d == 0]
+                                                   or [LANES_MAX])
+    with torch.no_grad():
+        gp = engine.GraphPipeline(P, src, dst, lanes=lanes)
+        gp.prepare(warmup)
+        gp.prepare(steps)
+        gp.run_forwards(warmup, stream=True)
+        gp.prime()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gp.run_forwards(steps, stream=True)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        del gp
+    return {"value": round(B * steps / el, 3), "ms_per_step": round(el / steps * 1e3, 3), "lanes": lanes,
+            "basis": f"the same {steps} timed batches of {B} pairs with one reference batch per executor "
+                     f"forward ({lanes} forwards in flight), measured right after the headline line"}
 
 
 def default_merge(steps: int, v2: bool) -> int:
@@ -732,51 +772,169 @@ def bench_train(args, world, rank, device):
     elapsed = max_over_ranks(elapsed, device)
     value = job_throughput(B, args.steps, world, elapsed)
     if rank == 0:
-        nt_ms, nt_n, nt_fl = timer.result("nt")
-        tn_ms, tn_n, tn_fl = timer.result("tn")
-        ach = (nt_fl + tn_fl) / max(nt_ms + tn_ms, 1e-9) / 1e9
-        fam = {"ts_gemm_kernel / gemm_nt_kernel (forward + input gradients)": {
-                   "launches_per_step": nt_n // args.steps,
-                   "ms_per_step": round(nt_ms / args.steps, 3),
-                   "tflops": round(nt_fl / max(nt_ms, 1e-9) / 1e9, 2)},
-               "gemm_tn_kernel + tn_reduce (weight gradients)": {
-                   "launches_per_step": tn_n // args.steps,
-                   "ms_per_step": round(tn_ms / args.steps, 3),
-                   "tflops": round(tn_fl / max(tn_ms, 1e-9) / 1e9, 2)}}
-        line = {
-            "metric": "point-cloud pairs/sec, HRegNet training step (train_reg_v0), "
-                      "16384-pt pairs",
-            "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded KITTI-shape LiDAR pairs with their ground-truth SE(3); "
-                    "nusc_feats + seeded heads)",
-            "config": {"workload": f"HRegNet train step (train-mode BN, 3-level "
-                                   f"transformation_loss, backward, Adam), batch={B} pairs/GPU, "
-                                   f"2x{args.points}-pt pairs (BASELINE configs[3])",
-                       "global_batch": B * world, "points": args.points,
-                       "parallelism": f"dp{world} (one 9.87 MB gradient all-reduce per step)"},
-            "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
-            "executor": "HIP graphs (two captured steps, ping-pong inputs)" if graphed else "eager",
-            "step_path": ("GraphTrainer (captured step" + (", RCCL all-reduce captured in the graph)"
-                                                          if world > 1 else ", no collective at world 1)")
-                          if graphed else "Trainer (eager step" + (
-                              ", RCCL all-reduce launched eagerly)" if world > 1 else ")")),
-            "provenance": provenance(),
-            "roofline": {"kernel": "fp32 MFMA GEMM family of the step (forward, input- and "
-                                   "weight-gradient GEMMs)",
-                         "timing": ("HIP events on the launch stream, instrumented eager pass of the "
-                                    "same steps after the timed region" if graphed else
-                                    "HIP events on the launch stream inside the timed region"),
-                         "bound": "mfma", "achieved": round(ach, 3),
-                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
-                         "gemm_ms_per_step": round((nt_ms + tn_ms) / args.steps, 3),
-                         "gflop_per_pair": round((nt_fl + tn_fl) / args.steps / B / 1e9, 3),
-                         "families": fam},
-            "cpu_baseline": None,
-        }
+        line = train_line(args, B=B, world=world, value=value, elapsed=elapsed,
+                          losses=[float(x) for x in (losses[0], losses[-1])], nt=timer.result("nt"),
+                          tn=timer.result("tn"), graphed=graphed)
         print(json.dumps(line), flush=True)
+
+
+def train_line(args, *, B, world, value, elapsed, losses, nt, tn, graphed):
+    """The training bench's JSON line from its measurements (no GPU work: assembled on the CPU
+    by tests/test_host_logic.py).  nt / tn: TrainGemmTimer.result of the two GEMM families;
+    losses: the first and last timed step's loss."""
+    nt_ms, nt_n, nt_fl = nt
+    tn_ms, tn_n, tn_fl = tn
+    ach = (nt_fl + tn_fl) / max(nt_ms + tn_ms, 1e-9) / 1e9
+    fam = {"ts_gemm_kernel / gemm_nt_kernel (forward + input gradients)": {
+               "launches_per_step": nt_n // args.steps,
+               "ms_per_step": round(nt_ms / args.steps, 3),
+               "tflops": round(nt_fl / max(nt_ms, 1e-9) / 1e9, 2)},
+           "gemm_tn_kernel + tn_reduce (weight gradients)": {
+               "launches_per_step": tn_n // args.steps,
+               "ms_per_step": round(tn_ms / args.steps, 3),
+               "tflops": round(tn_fl / max(tn_ms, 1e-9) / 1e9, 2)}}
+    line = {
+        "metric": "point-cloud pairs/sec, HRegNet training step (train_reg_v0), "
+                  "16384-pt pairs",
+        "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded KITTI-shape LiDAR pairs with their ground-truth SE(3); "
+                "nusc_feats + seeded heads)",
+        "config": {"workload": f"HRegNet train step (train-mode BN, 3-level "
+                               f"transformation_loss, backward, Adam), batch={B} pairs/GPU, "
+                               f"2x{args.points}-pt pairs (BASELINE configs[3])",
+                   "global_batch": B * world, "points": args.points,
+                   "parallelism": f"dp{world} (one 9.87 MB gradient all-reduce per step)"},
+        "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
+        "executor": "HIP graphs (two captured steps, ping-pong inputs)" if graphed else "eager",
+        "step_path": ("GraphTrainer (captured step" + (", RCCL all-reduce captured in the graph)"
+                                                      if world > 1 else ", no collective at world 1)")
+                      if graphed else "Trainer (eager step" + (
+                          ", RCCL all-reduce launched eagerly)" if world > 1 else ")")),
+        "provenance": provenance(),
+        "roofline": {"kernel": "fp32 MFMA GEMM family of the step (forward, input- and "
+                               "weight-gradient GEMMs)",
+                     "timing": ("HIP events on the launch stream, instrumented eager pass of the "
+                                "same steps after the timed region" if graphed else
+                                "HIP events on the launch stream inside the timed region"),
+                     "bound": "mfma", "achieved": round(ach, 3),
+                     "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                     "gemm_ms_per_step": round((nt_ms + tn_ms) / args.steps, 3),
+                     "gflop_per_pair": round((nt_fl + tn_fl) / args.steps / B / 1e9, 3),
+                     "families": fam},
+        "cpu_baseline": None,
+    }
+    return line
+
+
+def forward_line(args, *, v2, B, merge, world, value, ms_per_step, host_submit_s, res, ent, level_names,
+                 traffic, inexec, fps, lat, cpu, bs1, fs, merge1=None):
+    """The forward bench's JSON line from its measurements (no GPU work here: tests assemble it
+    on the CPU from synthetic measurements, tests/test_host_logic.py).  res: MfmaTimer.result per
+    kind; ent: MfmaTimer.entries; traffic: pmc_traffic's (bytes, source)."""
+    def kind_summary(k):
+        ms, n, fl, nb, xf = res[k]
+        return {"launches_per_step": round(n / args.steps, 3),
+                "avg_launch_us": round(ms / max(n, 1) * 1e3, 2),
+                "ms_per_step": round(ms / args.steps, 3),
+                "tflops": round(fl / max(ms, 1e-9) / 1e9, 2),
+                "gflop_per_pair": round(fl / args.steps / B / 1e9, 3),
+                "executed_tflops": round(xf / max(ms, 1e-9) / 1e9, 2),
+                "executed_gflop_per_pair": round(xf / args.steps / B / 1e9, 3)}
+    # roofline kernel family: the three fused level kernels (keypoint detector +
+    # descriptor, levels 1-3), the largest MFMA family of the step
+    f_ms, f_n, f_fl, f_nb, f_xf = res["level"]
+    per_launch_s = f_ms / max(f_n, 1) / 1e3
+    per_launch_flops = f_fl / max(f_n, 1)
+    achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
+    lev = {n: e for n, e in ent.items() if n in MFMA_ENTRIES and MFMA_ENTRIES[n][0] == "level"}
+    # the family's peak: its FLOPs over the time they need at each kernel's own peak
+    t_peak = sum(e["_flops"] / (e["peak"] * 1e12) for e in lev.values())
+    peak = sum(e["_flops"] for e in lev.values()) / t_peak / 1e12 if t_peak else PEAK_B6_TFLOPS
+    traffic, traffic_src = traffic
+    tot_ms = sum(r[0] for r in res.values())
+    tot_xf = sum(r[4] for r in res.values())
+    alg_fl = ALG_GFLOP_PER_PAIR * 1e9 * B * args.steps
+    per_entry = {n: {k: v for k, v in e.items() if not k.startswith("_")} for n, e in ent.items()}
+    roof = {"kernel": " + ".join(level_names) + " (keypoint detector + descriptor of "
+                      "levels 1-3: every conv/BN/ReLU layer, attention and k-max of a "
+                      "level in one launch)",
+            "timing": "HIP events on the launch stream, " + (
+                "instrumented eager pipelined pass of the same steps after the timed "
+                "graph region" if args.executor == "graph" else "inside the timed region"),
+            "bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1),
+            "unit": "TFLOP/s",
+            "peak_basis": "fp32-accurate products: bf16x6 kernels at the bf16 dense MFMA "
+                          f"peak / 6 = {PEAK_B6_TFLOPS:.1f}, fp32-MFMA kernels at "
+                          f"{PEAK_FP32_MFMA_TFLOPS} (MI355X_MICROARCH.md); FLOP-weighted "
+                          "over the family",
+            "frac": round(achieved / peak, 4),
+            "traffic": None if traffic is None else round(traffic),
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": round(f_nb / max(f_n, 1)),
+            "flop_per_launch": round(per_launch_flops),
+            "executed_flop_per_launch": round(f_xf / max(f_n, 1)),
+            "executed_tflops": round(f_xf / max(f_ms, 1e-9) / 1e9, 3),
+            "launches_per_step": round(f_n / args.steps, 3),
+            "avg_launch_us": round(per_launch_s * 1e6, 2),
+            "other_mfma_kernels": {"gemm_nt_kernel": kind_summary("gemm"),
+                                   "fine/nbr head kernels": kind_summary("head"),
+                                   "mlp_head_kernel": kind_summary("mlp")},
+            "per_entry": per_entry,
+            "all_mfma": {"ms_per_step": round(tot_ms / args.steps, 3),
+                         "gflop_per_pair": ALG_GFLOP_PER_PAIR,
+                         "tflops": round(alg_fl / max(tot_ms, 1e-9) / 1e9, 2),
+                         "executed_gflop_per_pair": round(tot_xf / args.steps / B / 1e9, 3),
+                         "executed_tflops": round(tot_xf / max(tot_ms, 1e-9) / 1e9, 2)}}
+    if not v2 and args.executor == "graph":
+        roof["in_executor"] = inexec
+    # the whole timed step: every MFMA family's algorithmic FLOPs per pair x pairs/s
+    roof["step_tflops"] = round(ALG_GFLOP_PER_PAIR * value / 1e3, 2)
+    roof["step_frac"] = round(ALG_GFLOP_PER_PAIR * value / 1e3 / PEAK_B6_TFLOPS, 4)
+    line = {
+        "metric": ("point-cloud pairs/sec, Model_V2 forward, 65536-pt pairs (config 5)" if v2
+                   else "point-cloud pairs/sec, HRegNet forward, 16384-pt pairs"),
+        "value": round(value, 3), "unit": "pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "host_submit_ms": round(host_submit_s * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "precision": "fp32 throughout; the fused level and head kernels take their fp32 "
+                     "products on the bf16 matrix cores as 3-piece exact splits (bf16x6, "
+                     "6 MFMAs per product, fp32 accumulate: error vs fp64 equal to the "
+                     "fp32 MFMA's, profiles/r2_split_mfma_micro.txt); parity tests at the "
+                     "fp32 bars",
+        "data": "synthetic (seeded KITTI-shape LiDAR pairs; nusc_feats + seeded heads)",
+        "config": {"workload": (f"Model_V2 forward (eval), batch={B} pairs/GPU, 2x{args.points}"
+                                "-pt LiDAR pairs (BASELINE configs[4])") if v2 else (
+                               f"HRegNet forward (eval), batch={B} pairs/GPU, "
+                               f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])"),
+                   "executor": args.executor + ("" if args.executor == "serial" else
+                               " (level-1 FPS of step i+1 overlaps step i)") + (
+                               f", {args.lanes} forwards in flight" if args.lanes > 1 and
+                               args.executor == "graph" else "") + (
+                               f"; {merge} batches of {B} pairs merged per forward (one launch "
+                               "set, every batch's outputs bitwise its own forward's; per-batch "
+                               "SVD fallback" + (" and prime shuffles" if v2 else "") + ")"
+                               if merge > 1 else "") + (
+                               "; batched stage 1 (the level-1 FPS -- fps_blocks_kernel, one workgroup per cloud -- "
+                               "spatial index and kNN as one launch each over every lane's clouds)"
+                               if bs1 and args.points > 16384 else "") + (
+                               "; front streaming: each timed round runs the registration "
+                               "half of its batches and the feature extraction of the next "
+                               "round's (pipeline primed after the warm-up)"
+                               if fs else ""),
+                   "global_batch": B * world, "points": args.points, "merge": merge,
+                   "parallelism": f"dp{world} (pairs sharded, no collective)"},
+        "roofline": roof,
+        "merge1": merge1,
+        "fps": fps,
+        "latency": lat,
+        "cpu_baseline": cpu,
+        "provenance": provenance(),
+    }
+    return line
 
 
 def _free_port() -> int:
@@ -858,6 +1016,8 @@ def main():
                     help="skip the instrumented eager pass after the timed graph region (the "
                          "rocprofv3 trace run behind roofline.in_executor: the timed replays are "
                          "then the last level-kernel dispatches of the run)")
+    ap.add_argument("--no-merge1", action="store_true",
+                    help="skip the unmerged (one reference batch per forward) figure beside a merged line")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-batch latency entry")
     ap.add_argument("--allow-probes", action="store_true",
@@ -1015,6 +1175,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    merge1 = None
+    if (merge > 1 and not v2 and world == 1 and args.executor == "graph" and not args.no_merge1):
+        try:
+            merge1 = unmerged_line(P, src[:B], dst[:B], args.steps * merge, args.warmup * merge)
+        except Exception as e:  # a side figure must never sink the GPU number
+            merge1 = {"error": repr(e)}
     if args.executor == "graph" and not args.no_eager_roofline:
         timer.enabled = True
         with torch.no_grad():
@@ -1030,130 +1196,40 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank == 0:
-        def kind_summary(k):
-            ms, n, fl, nb, xf = res[k]
-            return {"launches_per_step": round(n / args.steps, 3),
-                    "avg_launch_us": round(ms / max(n, 1) * 1e3, 2),
-                    "ms_per_step": round(ms / args.steps, 3),
-                    "tflops": round(fl / max(ms, 1e-9) / 1e9, 2),
-                    "gflop_per_pair": round(fl / args.steps / B / 1e9, 3),
-                    "executed_tflops": round(xf / max(ms, 1e-9) / 1e9, 2),
-                    "executed_gflop_per_pair": round(xf / args.steps / B / 1e9, 3)}
-        # roofline kernel family: the three fused level kernels (keypoint detector +
-        # descriptor, levels 1-3), the largest MFMA family of the step
-        f_ms, f_n, f_fl, f_nb, f_xf = res["level"]
-        per_launch_s = f_ms / max(f_n, 1) / 1e3
-        per_launch_flops = f_fl / max(f_n, 1)
-        achieved = per_launch_flops / per_launch_s / 1e12 if per_launch_s > 0 else 0.0
         ent = timer.entries(args.steps)
-        lev = {n: e for n, e in ent.items() if n in MFMA_ENTRIES and MFMA_ENTRIES[n][0] == "level"}
-        # the family's peak: its FLOPs over the time they need at each kernel's own peak
-        t_peak = sum(e["_flops"] / (e["peak"] * 1e12) for e in lev.values())
-        peak = sum(e["_flops"] for e in lev.values()) / t_peak / 1e12 if t_peak else PEAK_B6_TFLOPS
-        traffic, traffic_src = pmc_traffic(" + ".join(level_names), f"{args.model}:b{B}:n{args.points}"
-                                           + (f":m{merge}" if merge > 1 else ""))
-        tot_ms = sum(r[0] for r in res.values())
-        tot_xf = sum(r[4] for r in res.values())
-        alg_fl = ALG_GFLOP_PER_PAIR * 1e9 * B * args.steps
-        per_entry = {n: {k: v for k, v in e.items() if not k.startswith("_")} for n, e in ent.items()}
-        roof = {"kernel": " + ".join(level_names) + " (keypoint detector + descriptor of "
-                          "levels 1-3: every conv/BN/ReLU layer, attention and k-max of a "
-                          "level in one launch)",
-                "timing": "HIP events on the launch stream, " + (
-                    "instrumented eager pipelined pass of the same steps after the timed "
-                    "graph region" if args.executor == "graph" else "inside the timed region"),
-                "bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1),
-                "unit": "TFLOP/s",
-                "peak_basis": "fp32-accurate products: bf16x6 kernels at the bf16 dense MFMA "
-                              f"peak / 6 = {PEAK_B6_TFLOPS:.1f}, fp32-MFMA kernels at "
-                              f"{PEAK_FP32_MFMA_TFLOPS} (MI355X_MICROARCH.md); FLOP-weighted "
-                              "over the family",
-                "frac": round(achieved / peak, 4),
-                "traffic": None if traffic is None else round(traffic),
-                "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": round(f_nb / max(f_n, 1)),
-                "flop_per_launch": round(per_launch_flops),
-                "executed_flop_per_launch": round(f_xf / max(f_n, 1)),
-                "executed_tflops": round(f_xf / max(f_ms, 1e-9) / 1e9, 3),
-                "launches_per_step": round(f_n / args.steps, 3),
-                "avg_launch_us": round(per_launch_s * 1e6, 2),
-                "other_mfma_kernels": {"gemm_nt_kernel": kind_summary("gemm"),
-                                       "fine/nbr head kernels": kind_summary("head"),
-                                       "mlp_head_kernel": kind_summary("mlp")},
-                "per_entry": per_entry,
-                "all_mfma": {"ms_per_step": round(tot_ms / args.steps, 3),
-                             "gflop_per_pair": ALG_GFLOP_PER_PAIR,
-                             "tflops": round(alg_fl / max(tot_ms, 1e-9) / 1e9, 2),
-                             "executed_gflop_per_pair": round(tot_xf / args.steps / B / 1e9, 3),
-                             "executed_tflops": round(tot_xf / max(tot_ms, 1e-9) / 1e9, 2)}}
+        traffic = pmc_traffic(" + ".join(level_names), f"{args.model}:b{B}:n{args.points}"
+                              + (f":m{merge}" if merge > 1 else ""))
         # level-kernel FLOPs per launch at this batch (groups = 2B clouds x the level's
         # keypoints), by rocprof kernel name: the in-executor figure's numerators
         # (a launch covers the `merge` batches of one executor forward)
         lv_fl = {level_kernel(engine, 1): L1_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[0][0],
                  level_kernel(engine, 2): L2_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[1][0],
                  level_kernel(engine, 3): L3_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[2][0]}
-        if not v2 and args.executor == "graph":
-            roof["in_executor"] = in_executor(args.steps, B, args.points, lv_fl, merge)
-        # the whole timed step: every MFMA family's algorithmic FLOPs per pair x pairs/s
-        roof["step_tflops"] = round(ALG_GFLOP_PER_PAIR * value / 1e3, 2)
-        roof["step_frac"] = round(ALG_GFLOP_PER_PAIR * value / 1e3 / PEAK_B6_TFLOPS, 4)
+        inexec = (in_executor(args.steps, B, args.points, lv_fl, merge)
+                  if not v2 and args.executor == "graph" else None)
         fps = None
         try:
             fps = fps_latency(src[:B], dst[:B])
         except Exception as e:  # a diagnostic must never sink the GPU number
             fps = {"error": repr(e)}
         lat = None
-        if not v2 and not args.no_latency:
+        if not args.no_latency:
             try:
-                lat = forward_latency(P, src[:B], dst[:B])
+                lat = forward_latency(P, src[:B], dst[:B], v2=v2)
             except Exception as e:  # a diagnostic must never sink the GPU number
                 lat = {"error": repr(e)}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not v2:
+        if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(args.cpu_budget)
+                cpu = (cpu_baseline(args.cpu_budget, batches=(1, V2_PAIRS_PER_GPU), v2=True) if v2
+                       else cpu_baseline(args.cpu_budget))
             except Exception as e:  # the baseline must never sink the GPU number
                 cpu = {"error": repr(e)}
-        line = {
-            "metric": ("point-cloud pairs/sec, Model_V2 forward, 65536-pt pairs (config 5)" if v2
-                       else "point-cloud pairs/sec, HRegNet forward, 16384-pt pairs"),
-            "value": round(value, 3), "unit": "pairs/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "host_submit_ms": round(host_submit_s * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "precision": "fp32 throughout; the fused level and head kernels take their fp32 "
-                         "products on the bf16 matrix cores as 3-piece exact splits (bf16x6, "
-                         "6 MFMAs per product, fp32 accumulate: error vs fp64 equal to the "
-                         "fp32 MFMA's, profiles/r2_split_mfma_micro.txt); parity tests at the "
-                         "fp32 bars",
-            "data": "synthetic (seeded KITTI-shape LiDAR pairs; nusc_feats + seeded heads)",
-            "config": {"workload": (f"Model_V2 forward (eval), batch={B} pairs/GPU, 2x{args.points}"
-                                    "-pt LiDAR pairs (BASELINE configs[4])") if v2 else (
-                                   f"HRegNet forward (eval), batch={B} pairs/GPU, "
-                                   f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])"),
-                       "executor": args.executor + ("" if args.executor == "serial" else
-                                   " (level-1 FPS of step i+1 overlaps step i)") + (
-                                   f", {args.lanes} forwards in flight" if args.lanes > 1 and
-                                   args.executor == "graph" else "") + (
-                                   f"; {merge} batches of {B} pairs merged per forward (one launch "
-                                   "set, every batch's outputs bitwise its own forward's; per-batch "
-                                   "SVD fallback" + (" and prime shuffles" if v2 else "") + ")"
-                                   if merge > 1 else "") + (
-                                   "; batched stage 1 (one bounded-concurrency cluster-FPS launch "
-                                   "over every lane's clouds)" if gpipe is not None and gpipe.bs1
-                                   and args.points > 16384 else "") + (
-                                   "; front streaming: each timed round runs the registration "
-                                   "half of its batches and the feature extraction of the next "
-                                   "round's (pipeline primed after the warm-up)"
-                                   if gpipe is not None and gpipe.fs else ""),
-                       "global_batch": B * world, "points": args.points, "merge": merge,
-                       "parallelism": f"dp{world} (pairs sharded, no collective)"},
-            "roofline": roof,
-            "fps": fps,
-            "latency": lat,
-            "cpu_baseline": cpu,
-            "provenance": provenance(),
-        }
+        line = forward_line(args, v2=v2, B=B, merge=merge, world=world, value=value,
+                            ms_per_step=ms_per_step, host_submit_s=host_submit_s, res=res, ent=ent,
+                            level_names=level_names, traffic=traffic, inexec=inexec, fps=fps, lat=lat,
+                            cpu=cpu, bs1=gpipe is not None and gpipe.bs1, fs=gpipe is not None and gpipe.fs,
+                            merge1=merge1)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -82,14 +82,19 @@ enum {
 /* hreg_furthest_point_sampling for a caller that guarantees at most `concurrent` (>= 1)
  * multi-workgroup FPS launches (clouds above 16384 points) of this process run at once -- e.g. a
  * graph whose one stage-1 stream carries all of them: such a launch may keep more clouds' worker
- * waves spinning at once (device capacity / concurrent instead of / GPU_MAX_HW_QUEUES, capped at
- * 1024 waves).  Same results as hreg_furthest_point_sampling. */
+ * waves spinning at once: 3/4 of the kernel's resident waves on the device (occupancy API x CU
+ * count) / concurrent, capped at 4096 waves, instead of resident waves / GPU_MAX_HW_QUEUES capped
+ * at 256.  Same results as hreg_furthest_point_sampling. */
 int hreg_fps_bounded(int b, int n, int m, const float *points, float *temp, int32_t *idx,
                      float *sampled_xyz, int concurrent, void *stream);
-/* FPS of clouds of 16384 points over their spatial index (ws: hreg_spatial_index of the same
- * points, enqueued before): the Morton-sorted copy is scanned in 256-point groups and a group
- * whose box cannot hold a point nearer the new centre than its running minima is skipped (exact:
- * the same idx / temp as hreg_furthest_point_sampling).  Other sizes: hreg_furthest_point_sampling.
+/* FPS over the clouds' spatial index (ws: hreg_spatial_index of the same points, enqueued
+ * before), exact pruning: a point group whose box cannot hold a point nearer the new centre than
+ * its largest running minimum is skipped (the same idx as hreg_furthest_point_sampling; temp, if
+ * not NULL, receives the final running minima [b][n] as the reference leaves them).
+ *   n == 16384: the sorted copy in registers, 256-point groups (one 512-thread workgroup per cloud);
+ *   16384 < n <= 65536, n % 64 == 0 (Model_V2): one 1024-thread workgroup per cloud, running minima
+ *   in registers, the index's 64-point blocks read from ws when their box passes;
+ *   other sizes: hreg_furthest_point_sampling (temp then required above 16384 points).
  * Replaces furthest_point_sampling_kernel for level 1 (furthest_point_sampling_gpu.cu:84-206). */
 int hreg_fps_indexed(int b, int n, int m, const float *points, const void *ws, float *temp,
                      int32_t *idx, float *sampled_xyz, void *stream);
@@ -563,12 +568,6 @@ int hreg_group6_l2_table_floats(void);
 int hreg_group6_l2(const float *table, const float *geom, const float *knn_xyz,
                    const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                    float *desc, const float *pre, void *stream);
-/* hreg_group6_l2 in its pair form: two 32-row groups per wave share every streamed
- * weight chunk (half the L2 -> CU weight bytes per row); same table and arguments, pre
- * required; bitwise-identical outputs. */
-int hreg_group6x2_l2(const float *table, const float *geom, const float *knn_xyz,
-                     const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
-                     float *desc, const float *pre, void *stream);
 /* The channel-split stages (hreg_group_split_l{2,3}) with fp32-accurate products on the
  * bf16 matrix cores (bf16x6, group_split6.hip): same arguments and outputs, table =
  * hreg_group_split6_l{2,3}_table_floats() floats (engine.split_table6), 16-byte aligned. */
@@ -580,13 +579,6 @@ int hreg_group_split6_l3_table_floats(void);
 /* hreg_group_split6_l3 with two 32-row tiles per wave (each streamed weight piece feeds both
  * tiles' MFMAs; the same outputs bit for bit); pre (the precomputed feature block) required */
 int hreg_group_split6j_l3(const float *table, const float *geom, const float *knn_xyz,
-                          const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
-                          float *desc, const float *pre, void *stream);
-/* hreg_group_split6_l3 in the pieces form: activations kept in LDS as their bf16x6 pieces, split
- * once by the wave that produced them (8-wave workgroups of two 32-row tiles); the same table;
- * keypoints and attentive features bitwise hreg_group_split6j_l3's, descriptors to fp32 rounding
- * (mlp1 summed as two K-half partials); pre required */
-int hreg_group_split6p_l3(const float *table, const float *geom, const float *knn_xyz,
                           const int32_t *gidx, const float *feats, int G, float *kp, float *att_feat,
                           float *desc, const float *pre, void *stream);
 int hreg_group_split6_l3(const float *table, const float *geom, const float *knn_xyz,

@@ -85,12 +85,10 @@ _SIGS = {
     "hreg_group_l1_6": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group_l1_6g": [_vp, _vp, _vp, _i, _vp, _vp, _vp, _vp],
     "hreg_group6_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
-    "hreg_group6x2_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group6_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split6_l2": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split6_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_split6j_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
-    "hreg_group_split6p_l3": [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head": [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "hreg_fine_head_table_floats": [_i],
     "hreg_nbr_head": [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp],

@@ -97,20 +97,9 @@ __device__ __forceinline__ void conv_stack(const gfloat *__restrict__ tb, const 
     epilogue<T3>(eb + e3, lane, out);
 }
 
-// gathered feature rows: HREG_ROWS_NT = 1 reads them non-temporally so the random
-// row traffic does not evict the weight table from L2 (experiment switch)
-#ifndef HREG_ROWS_NT
-#define HREG_ROWS_NT 0
-#endif
-__device__ __forceinline__ float4 ld_rows(const float *p) {
-    if constexpr (HREG_ROWS_NT) {
-        typedef float v4 __attribute__((ext_vector_type(4)));
-        const v4 t = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p));
-        return make_float4(t[0], t[1], t[2], t[3]);
-    } else {
-        return *reinterpret_cast<const float4 *>(p);
-    }
-}
+// gathered feature rows (a non-temporal variant that was meant to keep the weight table in L2
+// measured no faster and was removed)
+__device__ __forceinline__ float4 ld_rows(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
 template <class K, bool PRE>
 __global__ __launch_bounds__(256, K::WPS) void group_fused_kernel(

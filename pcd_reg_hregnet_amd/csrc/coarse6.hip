@@ -19,10 +19,9 @@
 // pieces stream from the L2-resident table (engine.coarse_head_table6) one chunk ahead.
 // The channel max of the attention is reduced per wave, then across the 8 waves through
 // LDS; the reductions over a keypoint's 8 rows are 3 DPP steps.
-// chunk c + 1's B split under chunk c's MFMAs in pipe_lds6_jt (split_chain.h): the heads
-// measured 127.8 -> 123.5 (CoarseReg), 56.4 -> 54.2 (FineReg), 66.4 -> 64.4 us (neighbour
-// branch) eager; level 3's group_split6j (same pipe) neutral, so it stays off there
-#define HREG_SPLIT_SWP 1
+// chunk c + 1's B split under chunk c's MFMAs in pipe_lds6_jt (split_chain.h, SWP = true): the
+// heads measured 127.8 -> 123.5 (CoarseReg), 56.4 -> 54.2 (FineReg), 66.4 -> 64.4 us
+// (neighbour branch) eager; level 3's group_split6j (same pipe) neutral, so it stays off there
 #include "split_chain.h"
 
 namespace {
@@ -55,13 +54,11 @@ struct CorrCfg {
 // the 64-row activation buffer (132 KB) leaves one workgroup per CU and measured slower (154
 // vs 134 us): JT = 1 there; at C = 256 (FineReg level-2 head, neighbour branch; 73 KB) two
 // workgroups still fit per CU: JT = 2 (corr_jt; same products and order: the same bits); the
-// C = 128 head (a smaller grid) measured 48 vs 37 us on two tiles and stays on one.
-// HREG_CORR512_JT (A/B): the C = 512 head on two row tiles (145 KB of LDS: one workgroup per CU)
-#ifndef HREG_CORR512_JT
-#define HREG_CORR512_JT 1
-#endif
+// C = 128 head (a smaller grid) measured 48 vs 37 us on two tiles and stays on one.  (The
+// C = 512 head on two row tiles -- 145 KB of LDS, one workgroup per CU -- measured -2.1 % in the
+// bench, r5, and was removed.)
 template <class K>
-constexpr int corr_jt() { return K::C == 256 ? 2 : K::C == 512 ? HREG_CORR512_JT : 1; }
+constexpr int corr_jt() { return K::C == 256 ? 2 : 1; }
 
 // NBR: CoarseReg's neighbour branch (layers.py:315-337, nbr_head6_kernel's job): rows
 // [desc[nbr] C | dxyz, |d|] through convs_2, the descriptor block precomputed per point
@@ -132,7 +129,7 @@ __global__ __launch_bounds__(K::CW * 64) void coarse_head6_kernel(
 #pragma unroll
             for (int i = 0; i < P; ++i) y[i][jt] = yt[i];
         }
-        pipe_lds6_jt<1, P, P, JT>(wt, lane, g1, [&](int jt, int st0, float (&v)[4]) {
+        pipe_lds6_jt<1, P, P, JT, true>(wt, lane, g1, [&](int jt, int st0, float (&v)[4]) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = sm[jt][st0 + k];
         }, y, carry, g2, ca);
@@ -156,7 +153,7 @@ __global__ __launch_bounds__(K::CW * 64) void coarse_head6_kernel(
         for (int jt = 0; jt < JT; ++jt)
 #pragma unroll
             for (int i = 0; i < P; ++i) load_tiles<1>(*reinterpret_cast<f32x16(*)[1]>(&y[i][jt]), ep + 3 * C + (c0 + i) * 32, h);
-        pipe_lds6_jt<NCH, P, P, JT>(wt, lane, g2, ChanBJ<LDSW>{sA + j * LDSW, h}, y, ca, g3, cb);
+        pipe_lds6_jt<NCH, P, P, JT, true>(wt, lane, g2, ChanBJ<LDSW>{sA + j * LDSW, h}, y, ca, g3, cb);
 #pragma unroll
         for (int i = 0; i < P; ++i)
 #pragma unroll
@@ -175,7 +172,7 @@ __global__ __launch_bounds__(K::CW * 64) void coarse_head6_kernel(
         for (int jt = 0; jt < JT; ++jt)
 #pragma unroll
             for (int i = 0; i < P; ++i) load_tiles<1>(*reinterpret_cast<f32x16(*)[1]>(&y[i][jt]), ep + 5 * C + (c0 + i) * 32, h);
-        pipe_lds6_jt<NCH, P, P, JT>(wt, lane, g3, ChanBJ<LDSW>{sA + j * LDSW, h}, y, cb, g1, carry);
+        pipe_lds6_jt<NCH, P, P, JT, true>(wt, lane, g3, ChanBJ<LDSW>{sA + j * LDSW, h}, y, cb, g1, carry);
 #pragma unroll
         for (int i = 0; i < P; ++i)
 #pragma unroll
@@ -256,7 +253,7 @@ template <class K, bool NBR = false>
 int launch_corr6(const float *table, const float *small, const float *ud0, const float *ud1, const int32_t *gidx,
                  const float *knn_xyz, int G, float *corres, float *att, void *stream, int row_tiles = 0) {
     const int jt = row_tiles ? row_tiles : corr_jt<K>();
-    if constexpr (K::C <= 256 || (K::C == 512 && HREG_CORR512_JT == 2)) {
+    if constexpr (K::C <= 256) {
         if (jt == 2) return launch_corr6_jt<K, NBR, 2>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
     }
     if (jt == 1) return launch_corr6_jt<K, NBR, 1>(table, small, ud0, ud1, gidx, knn_xyz, G, corres, att, stream);
@@ -265,25 +262,14 @@ int launch_corr6(const float *table, const float *small, const float *ud0, const
 
 }  // namespace
 
-// output tiles per wave of the CoarseReg (N1 = 512) instance (A/B builds: 1 = 16 waves)
-#ifndef HREG_CORR512_P
-#define HREG_CORR512_P 2
-#endif
-using Corr512 = CorrCfg<512, HREG_CORR512_P>;
-// the FineReg widths and the neighbour head: fewer output tiles per wave = more waves per
-// 32-row tile (their grids are a few hundred to a thousand tiles)
-#ifndef HREG_CORR256_P
-#define HREG_CORR256_P 2
-#endif
-#ifndef HREG_CORR128_P
-#define HREG_CORR128_P 2
-#endif
-#ifndef HREG_NBR_P
-#define HREG_NBR_P 2
-#endif
-using Corr256 = CorrCfg<256, HREG_CORR256_P>;
-using Corr128 = CorrCfg<128, HREG_CORR128_P>;
-using Nbr256 = CorrCfg<256, HREG_NBR_P>;
+// two output tiles per wave throughout (one B split feeds 12 MFMAs): one tile per wave measured
+// faster per launch for the FineReg / neighbour heads (53 / 64.5 vs 54.7 / 67.4 us) but slower
+// in the bench (6910 / 6854 vs 6960 / 6965 pairs/s: every extra wave splits and reads the same B
+// chunks again), and spilled 42 VGPRs for the 512-wide head (r2-r4)
+using Corr512 = CorrCfg<512, 2>;
+using Corr256 = CorrCfg<256, 2>;
+using Corr128 = CorrCfg<128, 2>;
+using Nbr256 = CorrCfg<256, 2>;
 
 extern "C" int hreg_coarse_head6_table_floats(void) { return Corr512::TABLE; }
 

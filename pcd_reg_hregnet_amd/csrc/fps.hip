@@ -29,20 +29,13 @@
 
 #include <stdlib.h>
 
-#ifndef HREG_FPS_BESTMASK
-#define HREG_FPS_BESTMASK 1  // the winner-slot mask from the lane's own max (A/B: 0, from the wave max)
-#endif
-#ifndef HREG_FPS_MAX3
-#define HREG_FPS_MAX3 1  // one v_max3_f32 per slot pair in the scan (A/B: 0, two v_med3)
-#endif
 // The winner's coordinates by a uniform-index register read (r5): the slot coordinates live in
 // one ext_vector per axis (a contiguous VGPR tuple), so VX[sl] with the wave-uniform slot sl
 // is s_set_gpr_idx_on + v_mov + s_set_gpr_idx_off, then v_readlane -- instead of a log2(S)-deep
 // tree of uniform branches (whose structurised Flow blocks were ~0.2-0.4 us of every
-// iteration).  A/B: 0 keeps the branch tree.
-#ifndef HREG_FPS_MOVREL
-#define HREG_FPS_MOVREL 8  // the smallest slot count that takes the indexed read (A/B: 0 = never)
-#endif
+// iteration).  From FPS_MOVREL_MIN slots up (level 2's 16 and level 1's 32; the 4-slot level-2
+// geometry measured slower with it, r5).
+constexpr int FPS_MOVREL_MIN = 8;
 
 namespace {
 
@@ -53,28 +46,27 @@ __device__ __forceinline__ float dppf(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
 }
 
-// max over each 16-lane row (quad_perm 1032, 2301, row_half_mirror, row_mirror)
-__device__ __forceinline__ float row_max16(float v, float inf) {
-    v = fmax_nc(v, dppf<0xb1>(v), inf);
-    v = fmax_nc(v, dppf<0x4e>(v), inf);
-    v = fmax_nc(v, dppf<0x141>(v), inf);
-    v = fmax_nc(v, dppf<0x140>(v), inf);
-    return v;
+// The running-minimum update d2 = fminf(d, temp) (.cu:130) as one v_min_f32: IEEE minNum returns
+// the non-NaN operand, so a NaN distance (a NaN coordinate, or inf - inf) keeps temp, as the
+// reference's fminf does.  (fmin_nc's v_med3_f32 returns min3 when an input is NaN: temp became
+// -inf, r6 non-finite test.)  Inline asm: fminf itself would add canonicalising v_max around a
+// loop-carried value.
+__device__ __forceinline__ float fmin_ref(float d, float t) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(d), "v"(t));
+    return r;
 }
 
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-// HREG_FPS_DPPMAX (r5): the reductions' DPP folded into the max itself -- v_max_f32_dpp, one
-// VOP2 per step instead of v_mov_b32_dpp + v_med3_f32 (the VOP3 med3 takes no DPP on gfx9) --
-// and the wave max finished by row_bcast:15 / row_bcast:31 into lane 63 (one v_readlane
-// instead of four + three maxima).  The values are never NaN (distances, -inf for invalid
-// slots); max returns one of its inputs, so the winners are the same bits.  gfx9 DPP reads a
-// VGPR two wait states after its VALU write at the earliest: the s_nop 1s.  A/B: 0 = med3.
-#ifndef HREG_FPS_DPPMAX
-#define HREG_FPS_DPPMAX 1
-#endif
+// Row / wave maxima with the DPP folded into the max itself (r5) -- v_max_f32_dpp, one VOP2 per
+// step instead of v_mov_b32_dpp + v_med3_f32 (the VOP3 med3 takes no DPP on gfx9) -- and the wave
+// max finished by row_bcast:15 / row_bcast:31 into lane 63 (one v_readlane instead of four +
+// three maxima).  The values are never NaN (running minima, -inf for invalid slots); max returns
+// one of its inputs, so the winners are the same bits.  gfx9 DPP reads a VGPR two wait states
+// after its VALU write at the earliest: the s_nop 1s.
 
 __device__ __forceinline__ float row_max16_dpp(float v) {
     float r;
@@ -102,12 +94,7 @@ __device__ __forceinline__ float wave_max_to63_dpp(float v) {
     return r;
 }
 
-__device__ __forceinline__ float wave_max_uniform(float v, float inf) {
-    if constexpr (HREG_FPS_DPPMAX) return readlane_f(wave_max_to63_dpp(v), 63);
-    v = row_max16(v, inf);
-    return fmax_nc(fmax_nc(readlane_f(v, 0), readlane_f(v, 16), inf),
-                   fmax_nc(readlane_f(v, 32), readlane_f(v, 48), inf), inf);
-}
+__device__ __forceinline__ float wave_max_uniform(float v) { return readlane_f(wave_max_to63_dpp(v), 63); }
 
 __device__ __forceinline__ uint64_t stamp() {
     uint64_t t;
@@ -133,54 +120,15 @@ __device__ __forceinline__ void pick_slot_pairs(int sl, int wl, const f2 (&PX)[N
     }
 }
 
-// HREG_FPS_PAIRMASK (r5): the lane's first slot of its maximum found over the pair maxima
-// (16 compares at 32 slots instead of 32), then, for the winning lane only, the pair's x / y
-// slot by one uniform-index register read of the temps; used from this many slots up.
-// Measured (bench lines, one box): level 1 (32 slots) 1.567 -> 1.43 us per iteration; level 2
-// (4 slots) 0.545 -> 0.60, so the small geometries keep the per-slot mask.  A/B: 0 = never.
-#ifndef HREG_FPS_PAIRMASK
-#define HREG_FPS_PAIRMASK 16
-#endif
-// HREG_FPS_L1_WIDE (A/B): level 1 (n = 16384) on 1024 threads x 16 points instead of 512 x 32
-#ifndef HREG_FPS_L1_WIDE
-#define HREG_FPS_L1_WIDE 0
-#endif
-// HREG_FPS_POLL_SLEEP: s_sleep between unsuccessful exchange polls of the cluster kernel
-// (its spinning participants share SIMDs with the other lanes' kernels; a poll is four
-// agent-scope loads per lane and a wave-wide vote).  0 = off.
-#ifndef HREG_FPS_POLL_SLEEP
-#define HREG_FPS_POLL_SLEEP 0
-#endif
-// HREG_FPS_PRIO: s_setprio for the FPS waves (they share SIMDs with the MFMA kernels of other
-// lanes, and every iteration waits for the slowest wave / participant).  0 = off.
-#ifndef HREG_FPS_PRIO
-#define HREG_FPS_PRIO 0
-#endif
-#ifndef HREG_FPS_W1024_1W
-#define HREG_FPS_W1024_1W 1
-#endif
-// threads of the one-slot geometries at bs = 1024 (level 2) / 512 (level 3): 64 = one wave
-// (A/B: 128 = two waves with the LDS hand-off)
-#ifndef HREG_FPS_WT1024
-#define HREG_FPS_WT1024 64
-#endif
-#ifndef HREG_FPS_WT512
-#define HREG_FPS_WT512 64
-#endif
-// HREG_FPS_QUAD (r5): from this many slots up, each lane's maximum is located over quad maxima
-// (2 VALU per 4 slots, a select chain over S / 4 entries) instead of pair maxima (3 per 4, a
-// chain over S / 2), and the winning lane's slot inside its quad by three indexed reads + ballots.
-// 0 = pairs.
-#ifndef HREG_FPS_QUAD
-#define HREG_FPS_QUAD 32
-#endif
-#ifndef HREG_FPS_LANEWRITE
-#define HREG_FPS_LANEWRITE 1
-#endif
-// HREG_FPS_SLOTCHAIN (r5): see the slot search in fps_reg_kernel.  A/B: 0 = bit mask + ctz.
-#ifndef HREG_FPS_SLOTCHAIN
-#define HREG_FPS_SLOTCHAIN 1
-#endif
+// The lane's first slot of its maximum (r5), found over coarser maxima from these slot counts up
+// (measured, bench lines on one box): pair maxima (16 compares at 32 slots instead of 32; level 1
+// 1.567 -> 1.43 us per iteration; level 2's 4-slot geometry 0.545 -> 0.60, so the small geometries
+// keep the per-slot search), then quad maxima (2 VALU per 4 slots, a select chain over S / 4
+// entries, the winning lane's slot inside its quad by three indexed reads + ballots: level 1 252 ->
+// 236 VALU per iteration, 1.251 -> 1.18 us; level 2 0.459 -> 0.468, so level 1 only).  Each lane's
+// first maximal slot / pair / quad is a compare/select chain from the top (no bit mask, OR tree
+// or find-first-set).
+constexpr int FPS_PAIRMASK_MIN = 16, FPS_QUAD_MIN = 32;
 
 // per-axis slot coordinates of a thread: one contiguous VGPR tuple
 template <int N>
@@ -194,14 +142,14 @@ __device__ __forceinline__ f2 pair_of(const V &v, int s) {
     return f2{v[2 * s], v[2 * s + 1]};
 }
 
-// The winner's coordinates: slot sl (wave-uniform) of lane wl.  HREG_FPS_MOVREL: one indexed
+// The winner's coordinates: slot sl (wave-uniform) of lane wl.  FPS_MOVREL_MIN: one indexed
 // register read per axis (s_set_gpr_idx_on) + v_readlane; else a binary tree of uniform
 // branches down to the slot.
 template <int LO, int HI, class V>
 __device__ __forceinline__ void pick_slot(int sl, int wl, const V &VX, const V &VY, const V &VZ, float &x,
                                           float &y, float &z) {
     constexpr int N = sizeof(V) / sizeof(float);
-    if constexpr (HREG_FPS_MOVREL && N >= HREG_FPS_MOVREL) {
+    if constexpr (N >= FPS_MOVREL_MIN) {
         x = readlane_f(VX[sl], wl);
         y = readlane_f(VY[sl], wl);
         z = readlane_f(VZ[sl], wl);
@@ -229,16 +177,15 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
     constexpr int S = G * QT;
     constexpr int S2 = (S + 1) / 2;
     constexpr int NW = T / HREG_WAVE;
-    constexpr bool PM = HREG_FPS_PAIRMASK && 2 * S2 >= HREG_FPS_PAIRMASK;
-    // quad maxima (HREG_FPS_QUAD, above): the pair-maxima search one level coarser
-    constexpr bool QM = PM && HREG_FPS_SLOTCHAIN && HREG_FPS_QUAD && 2 * S2 >= HREG_FPS_QUAD && S2 % 2 == 0;
+    constexpr bool PM = 2 * S2 >= FPS_PAIRMASK_MIN;
+    // quad maxima (above): the pair-maxima search one level coarser
+    constexpr bool QM = PM && 2 * S2 >= FPS_QUAD_MIN && S2 % 2 == 0;
     static_assert(NW <= 16, "block winner reduction uses one 16-lane row");
     static_assert(2 * S2 <= 32, "slot mask is 32 bits");
     __shared__ float4 s_cand[2][NW];
     __shared__ int s_k[2][NW];
     uint64_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, r0 = 0, c0 = 0;
 
-    if constexpr (HREG_FPS_PRIO > 0) __builtin_amdgcn_s_setprio(HREG_FPS_PRIO);
     const int cloud = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -302,8 +249,8 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             f2 d = (dx * dx + dy * dy) + dz * dz;
             if (WEIGHTED) d = PW[s] * d;
             f2 t;
-            t.x = fmin_nc(d.x, tget(2 * s), inf);
-            t.y = fmin_nc(d.y, tget(2 * s + 1), inf);
+            t.x = fmin_ref(d.x, tget(2 * s));
+            t.y = fmin_ref(d.y, tget(2 * s + 1));
             if constexpr (PM) {
                 VT[2 * s] = t.x;
                 VT[2 * s + 1] = t.y;
@@ -323,55 +270,28 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
                 pmx[s] = fmax_nc(t.x, t.y, inf);
                 if (s & 1) asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(pmx[s - 1]), "v"(pmx[s]));
                 else if (s + 1 == S2) best = fmax_nc(best, pmx[s], inf);
-            } else if constexpr (HREG_FPS_MAX3) {
+            } else {
                 // one v_max3_f32 per pair instead of two v_med3 (t and best are never NaN):
                 // level-1 FPS 1.634 -> 1.588 us per iteration, bench +0.7 % (A/B on one box, r4)
                 asm("v_max3_f32 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(t.x), "v"(t.y));
-            } else {
-                best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
             }
         }
         (void)pmx;
         if constexpr (STAMP) t1 = stamp();
-        uint32_t smask = 0;
-        float wmax;
-        int myslot;
-        if constexpr (HREG_FPS_SLOTCHAIN) {
-            // the lane's first pair (PM) / slot holding its own maximum by a select chain from
-            // the top: one compare + one select per entry, no mask, OR tree or find-first-set
-            myslot = 0;
-            if constexpr (QM) {
+        // the lane's first quad (QM) / pair (PM) / slot holding its own maximum by a select chain
+        // from the top: one compare + one select per entry
+        int myslot = 0;
+        if constexpr (QM) {
 #pragma unroll
-                for (int q = S2 / 2 - 1; q >= 0; --q) myslot = pmx[q] == best ? q : myslot;
-            } else if constexpr (PM) {
-#pragma unroll
-                for (int s = S2 - 1; s >= 0; --s) myslot = pmx[s] == best ? s : myslot;
-            } else {
-#pragma unroll
-                for (int s = 2 * S2 - 1; s >= 0; --s) myslot = tget(s) == best ? s : myslot;
-            }
-            wmax = wave_max_uniform(best, inf);
+            for (int q = S2 / 2 - 1; q >= 0; --q) myslot = pmx[q] == best ? q : myslot;
         } else if constexpr (PM) {
-            // this lane's first PAIR holding its own maximum (16 compares at 32 slots); the
-            // winning lane's slot inside that pair comes after the wave reduction (below)
 #pragma unroll
-            for (int s = 0; s < S2; ++s) smask |= (pmx[s] == best) ? (1u << s) : 0u;
-            wmax = wave_max_uniform(best, inf);
-        } else if constexpr (HREG_FPS_BESTMASK) {
-            // this lane's first slot holding its own maximum (the winning lane's own maximum is
-            // the wave max, and only its slot is read): no dependence on the wave reduction, so
-            // these compares fill that reduction's latency
-#pragma unroll
-            for (int s = 0; s < 2 * S2; ++s) smask |= (tget(s) == best) ? (1u << s) : 0u;
-            wmax = wave_max_uniform(best, inf);
+            for (int s = S2 - 1; s >= 0; --s) myslot = pmx[s] == best ? s : myslot;
         } else {
-            wmax = wave_max_uniform(best, inf);
-            // this lane's first slot holding the wave max (bit mask + find-first-set)
 #pragma unroll
-            for (int s = 0; s < 2 * S2; ++s) smask |= (tget(s) == wmax) ? (1u << s) : 0u;
+            for (int s = 2 * S2 - 1; s >= 0; --s) myslot = tget(s) == best ? s : myslot;
         }
-        if constexpr (!HREG_FPS_SLOTCHAIN) myslot = smask ? (int)__builtin_ctz(smask) : 0;
-        (void)smask;
+        const float wmax = wave_max_uniform(best);
         const uint64_t hit = __ballot(best == wmax);
         const int wl = (int)__builtin_ctzll(hit);  // lowest lane = lowest reference order
         int sl;
@@ -396,10 +316,10 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         const int rp = (wvu * 64 + wl) * G + sl / QT;  // (uniform: the index on the scalar unit)
         int kwin = (int)bitrev_bits((uint32_t)rp, L) + (sl % QT) * bs;
         asm volatile("" : "+s"(kwin));  // (kept scalar: else it is rebuilt per lane in the write below)
-        // HREG_FPS_LANEWRITE: with several waves the winner's coordinates only go to LDS, so lane
-        // wl writes its own slot sl (one indexed read per axis) instead of three v_readlane and
-        // four v_mov for a lane-0 write
-        constexpr bool LW = HREG_FPS_LANEWRITE && NW > 1;
+        // with several waves the winner's coordinates only go to LDS, so lane wl writes its own
+        // slot sl (one indexed read per axis) instead of three v_readlane and four v_mov for a
+        // lane-0 write (r5)
+        constexpr bool LW = NW > 1;
         float wx = 0.f, wy = 0.f, wz = 0.f;
         if constexpr (LW) {
             wx = VX[sl];
@@ -434,7 +354,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
             // both loads issue before the reduction (else the compiler sinks x/y/z/k into the
             // branch below: a second LDS round trip on the dependent chain)
             asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(ck));
-            const float gmax = readlane_f(HREG_FPS_DPPMAX ? row_max16_dpp(c.w) : row_max16(c.w, inf), 0);
+            const float gmax = readlane_f(row_max16_dpp(c.w), 0);
             const uint64_t ghit = __ballot(c.w == gmax);
             const int gw = (int)__builtin_ctzll(ghit);  // lowest wave = lowest reference order
             // (a uniform branch here: the selects of the one-wave path measured 0.26 vs 0.22 us
@@ -609,7 +529,6 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                                                          float inf, uint32_t polls_max, int stall) {
     constexpr int S2 = S / 2;
     static_assert(S % 2 == 0 && S <= 32, "slots");
-    if constexpr (HREG_FPS_PRIO > 0) __builtin_amdgcn_s_setprio(HREG_FPS_PRIO);
     const int p = blockIdx.x;  // participant
     const int lane = threadIdx.x;
     for (int cloud = blockIdx.y; cloud < b; cloud += gridDim.y) {
@@ -650,12 +569,12 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                 f2 d = (dx * dx + dy * dy) + dz * dz;
                 if (WEIGHTED) d = PW[s] * d;
                 f2 t;
-                t.x = fmin_nc(d.x, PT[s].x, inf);
-                t.y = fmin_nc(d.y, PT[s].y, inf);
+                t.x = fmin_ref(d.x, PT[s].x);
+                t.y = fmin_ref(d.y, PT[s].y);
                 PT[s] = t;
                 best = fmax_nc(best, fmax_nc(t.x, t.y, inf), inf);
             }
-            const float wmax = wave_max_uniform(best, inf);
+            const float wmax = wave_max_uniform(best);
             uint32_t smask = 0;
 #pragma unroll
             for (int s = 0; s < S; ++s) smask |= (PT[s / 2][s % 2] == wmax) ? (1u << s) : 0u;
@@ -697,7 +616,6 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                             (w2 >> 32) == (uint64_t)j && (w3 >> 32) == (uint64_t)j;
                 }
                 if (__all(fresh)) break;
-                if constexpr (HREG_FPS_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(HREG_FPS_POLL_SLEEP);
                 if (++polls > polls_max) {
                     timed_out = true;
                     break;
@@ -710,7 +628,7 @@ __global__ __launch_bounds__(64) void fps_cluster_kernel(const float *__restrict
                 return;
             }
             const float cd = lane < NP ? __uint_as_float((uint32_t)(w0 >> 32)) : -__builtin_huge_valf();
-            const float gmax = wave_max_uniform(cd, inf);
+            const float gmax = wave_max_uniform(cd);
             const int gl = (int)__builtin_ctzll(__ballot(lane < NP && cd == gmax));
             int old;
             if (gmax > -1.0f) {
@@ -739,23 +657,23 @@ template <bool WEIGHTED, bool STAMP = false>
 bool launch_reg(int T, int G, int QT, int b, int n, int m, int bs, int L, const float *xyz,
                 const float *w, float *temp, int32_t *idx, float *sampled, uint64_t *stamps,
                 hipStream_t st) {
-#define HREG_FPS_CASE(TT, GG, QQ)                                                              \
+#define FPS_CASE(TT, GG, QQ)                                                              \
     if (T == TT && G == GG && QT == QQ) {                                                      \
         hipLaunchKernelGGL((fps_reg_kernel<TT, GG, QQ, WEIGHTED, STAMP>), dim3(b), dim3(TT), 0, \
                            st, xyz, w, temp, idx, sampled, n, m, bs, L, __builtin_huge_valf(), \
                            stamps);                                                            \
         return true;                                                                           \
     }
-    HREG_FPS_CASE(1024, 1, 1) HREG_FPS_CASE(1024, 1, 2) HREG_FPS_CASE(1024, 1, 4)
-    HREG_FPS_CASE(1024, 1, 8)
+    FPS_CASE(1024, 1, 1) FPS_CASE(1024, 1, 2) FPS_CASE(1024, 1, 4)
+    FPS_CASE(1024, 1, 8)
     // (512, 2, 16) unweighted only: the weighted form needs 32 more VGPRs and spills
-    if constexpr (!WEIGHTED) { HREG_FPS_CASE(1024, 1, 16) HREG_FPS_CASE(512, 2, 16) }
-    HREG_FPS_CASE(512, 1, 1) HREG_FPS_CASE(512, 1, 2)
-    HREG_FPS_CASE(256, 4, 1) HREG_FPS_CASE(256, 1, 1) HREG_FPS_CASE(256, 1, 2)
-    HREG_FPS_CASE(128, 4, 1) HREG_FPS_CASE(128, 1, 1) HREG_FPS_CASE(128, 1, 2)
-    HREG_FPS_CASE(64, 16, 1) HREG_FPS_CASE(64, 8, 1) HREG_FPS_CASE(128, 8, 1)
-    HREG_FPS_CASE(64, 4, 1) HREG_FPS_CASE(64, 1, 1) HREG_FPS_CASE(64, 1, 2)
-#undef HREG_FPS_CASE
+    if constexpr (!WEIGHTED) { FPS_CASE(1024, 1, 16) FPS_CASE(512, 2, 16) }
+    FPS_CASE(512, 1, 1) FPS_CASE(512, 1, 2)
+    FPS_CASE(256, 4, 1) FPS_CASE(256, 1, 1) FPS_CASE(256, 1, 2)
+    FPS_CASE(128, 4, 1) FPS_CASE(128, 1, 1) FPS_CASE(128, 1, 2)
+    FPS_CASE(64, 16, 1) FPS_CASE(64, 8, 1) FPS_CASE(128, 8, 1)
+    FPS_CASE(64, 4, 1) FPS_CASE(64, 1, 1) FPS_CASE(64, 1, 2)
+#undef FPS_CASE
     return false;
 }
 
@@ -768,11 +686,11 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     if (Q == 1 && bs >= 256) {
         // one wave (no barrier) while its scan stays short; 4 waves at bs = 1024
         // (measured, 16 clouds: n=512 0.130 ms at 1 wave vs 0.150 at 2; n=1024 (r1) 0.300 ms
-        // at 4 waves vs 0.331 at 1.  r5, HREG_FPS_W1024_1W: with the pair-maxima slot search
-        // and the indexed winner read, one wave x 16 weighted points per lane runs level 2 at
-        // 0.484 vs 0.564 us per iteration, single-batch latency 3.26 vs 3.32 ms, bench lines
-        // within noise -- on)
-        T = bs >= 1024 ? (HREG_FPS_W1024_1W ? HREG_FPS_WT1024 : bs / 4) : bs >= 512 ? HREG_FPS_WT512 : 64;
+        // at 4 waves vs 0.331 at 1.  r5: with the pair-maxima slot search and the indexed
+        // winner read, one wave x 16 weighted points per lane runs level 2 at 0.484 vs 0.564 us
+        // per iteration, single-batch latency 3.26 vs 3.32 ms; two waves with the leaner
+        // exchange measured 0.58 (level 2) / 0.47 (level 3) vs 0.46 / 0.38 -- one wave throughout)
+        T = 64;
         G = bs / T;
         QT = 1;
         return;
@@ -785,7 +703,8 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
     // work per SIMD, half the per-wave reduction/winner overhead; both fill a CU's VGPRs
     // (127 x 1024 vs 254 x 512).  768 clouds (the batched level-1 stage) 5.70 -> 5.19 ms,
     // identical indices (tools/micro/fps_l1_geom.py).
-    if (!HREG_FPS_L1_WIDE && !weighted && T == 1024 && QT == 16) {
+    // (1024 threads x 16 points measured 1.58 vs 1.43 us per iteration, r5)
+    if (!weighted && T == 1024 && QT == 16) {
         T = 512; G = 2;
     }
 }
@@ -809,31 +728,21 @@ void choose_geometry(int n, bool weighted, int &T, int &G, int &QT) {
 // MI355X_MICROARCH.md Residency: every other kernel's waves are finite and drain, so the
 // spinning participants of one launch all become resident once they fit on the chip alone).
 // 0: the hardware-queue bound above.
-#ifndef HREG_FPS_CAP_BOUNDED
-#define HREG_FPS_CAP_BOUNDED 4096
-#endif
 // The fewest slots per lane of a cluster participant (r5): 32 slots = 32 single-wave
 // participants for a 65536-point cloud (253 VGPRs) instead of 64 x 16 slots (129 VGPRs).
 // With the bounded budget of the batched Model_V2 stage 1 every lane's clouds then run at once
 // (64 clouds of 32 waves): Model_V2 line 1410 -> 3279 pairs/s (merge 8, 2 lanes, one box;
-// 16 slots with a 2048-wave cap: 1685).  A/B: 8 (the r4 sizing).
-#ifndef HREG_FPS_CL_SMIN
-#define HREG_FPS_CL_SMIN 32
-#endif
-constexpr int FPS_SPIN_CAP = 256, FPS_SPIN_CAP_BOUNDED = HREG_FPS_CAP_BOUNDED;
-int cluster_wave_budget(int S, bool weighted, int concurrent = 0) {
-    static int cache[2][3] = {{-1, -1, -1}, {-1, -1, -1}};  // resident waves of the variant
-    const int si = S == 8 ? 0 : S == 16 ? 1 : 2;
-    int &c = cache[weighted ? 1 : 0][si];
+// 16 slots with a 2048-wave cap: 1685).  (r6: Model_V2's clouds now run fps_blocks_kernel; the
+// cluster kernel stays the boundary's path for hreg_furthest_point_sampling above 16384 points.)
+constexpr int FPS_SPIN_CAP = 256, FPS_SPIN_CAP_BOUNDED = 4096, FPS_CL_S = 32;
+int cluster_wave_budget(bool weighted, int concurrent = 0) {
+    static int cache[2] = {-1, -1};  // resident waves of the variant
+    int &c = cache[weighted ? 1 : 0];
     if (c < 0) {
         int dev = 0, cus = 0, per_cu = 0;
-        const void *fn = nullptr;
-#define HREG_FPS_CLK(SS, WW) \
-    if (S == SS && weighted == WW) fn = reinterpret_cast<const void *>(&fps_cluster_kernel<SS, WW>);
-        HREG_FPS_CLK(8, false) HREG_FPS_CLK(16, false) HREG_FPS_CLK(32, false)
-        HREG_FPS_CLK(8, true) HREG_FPS_CLK(16, true) HREG_FPS_CLK(32, true)
-#undef HREG_FPS_CLK
-        if (!fn || hipGetDevice(&dev) != hipSuccess ||
+        const void *fn = weighted ? reinterpret_cast<const void *>(&fps_cluster_kernel<FPS_CL_S, true>)
+                                  : reinterpret_cast<const void *>(&fps_cluster_kernel<FPS_CL_S, false>);
+        if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, 0) != hipSuccess) {
             (void)hipGetLastError();
@@ -874,13 +783,10 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
     // large clouds: the caller's temp buffer is required (sync slots / running minima)
     if (temp == nullptr) return HREG_ERR_INVALID;
     const long ranks = (long)bs * Q;
-    int S = 0;
-    for (int s : {8, 16, 32})
-        if (s >= HREG_FPS_CL_SMIN)
-        if (ranks <= (long)FPS_CL_MAXP * 64 * s) { S = s; break; }
+    const int S = ranks <= (long)FPS_CL_MAXP * 64 * FPS_CL_S ? FPS_CL_S : 0;
     const size_t slot_bytes = (size_t)2 * FPS_CL_MAXP * sizeof(SyncSlot);
     const int NP = S ? (int)((ranks + 64L * S - 1) / (64L * S)) : 0;
-    const int spin = S ? cluster_wave_budget(S, WEIGHTED, concurrent) : 0;
+    const int spin = S ? cluster_wave_budget(WEIGHTED, concurrent) : 0;
     if (S && (size_t)n * sizeof(float) >= slot_bytes && spin >= NP) {
         const int clusters = b < spin / NP ? b : spin / NP;
         SyncSlot *slots = reinterpret_cast<SyncSlot *>(temp);
@@ -890,13 +796,8 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
             (sampled && hipMemsetAsync(sampled, 0, (size_t)b * m * 3 * sizeof(float), st) != hipSuccess))
             return HREG_ERR_LAUNCH;
         const dim3 grid(NP, clusters);
-#define HREG_FPS_CL(SS)                                                                         \
-    if (S == SS)                                                                                \
-        hipLaunchKernelGGL((fps_cluster_kernel<SS, WEIGHTED>), grid, dim3(64), 0, st, xyz, w,     \
-                           slots, idx, sampled, b, n, m, bs, L, Q, NP, __builtin_huge_valf(),   \
-                           polls_max, stall);
-        HREG_FPS_CL(8) HREG_FPS_CL(16) HREG_FPS_CL(32)
-#undef HREG_FPS_CL
+        hipLaunchKernelGGL((fps_cluster_kernel<FPS_CL_S, WEIGHTED>), grid, dim3(64), 0, st, xyz, w, slots, idx,
+                           sampled, b, n, m, bs, L, Q, NP, __builtin_huge_valf(), polls_max, stall);
         HREG_CHECK_LAUNCH();
         return HREG_OK;
     }
@@ -929,24 +830,8 @@ int launch_fps(int b, int n, int m, const float *xyz, const float *w, float *tem
 // candidate per group is (max T, min rank among its slots at that T), the wave's is (max T, min
 // rank), and the workgroup's the same over the 8 waves.
 constexpr int FS_T = 512, FS_NW = 8, FS_S = 32, FS_NG = 8, FS_N = FS_T * FS_S;
-// A/B switches, both measured no faster (gpurun_out/r5ag, the FPS alone, 16 clouds, three
-// alternations: 0.956-0.958 us per iteration with neither, 0.967-0.972 with the tree,
-// 0.959-0.961 with both).  HREG_FS_TREE: the lane's candidate rank at the wave max as 8
-// independent selects + a v_min3_u32 tree instead of a serial select/min chain.  HREG_FS_EXPECT:
-// the group scans laid out as unlikely, so a skipped group falls through.
-#ifndef HREG_FS_TREE
-#define HREG_FS_TREE 0
-#endif
-#ifndef HREG_FS_EXPECT
-#define HREG_FS_EXPECT 0
-#endif
-
-__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-
+// (measured no faster, r5 gpurun_out/r5ag, and removed: the lane's candidate rank at the wave max
+// as 8 independent selects + a v_min3_u32 tree, and the group scans laid out as unlikely)
 __device__ __forceinline__ uint32_t row_min16_u32_dpp(uint32_t v) {
     uint32_t r;
     asm("s_nop 1\n\t"
@@ -1055,13 +940,13 @@ __global__ __launch_bounds__(FS_T) void fps_sorted_kernel(const float4 *__restri
         const f2 X1 = {x1, x1}, Y1 = {y1, y1}, Z1 = {z1, z1};
 #pragma unroll
         for (int g = 0; g < FS_NG; ++g) {
-            if (HREG_FS_EXPECT ? __builtin_expect((amask >> g) & 1u, 0u) : (amask >> g) & 1u) {
+            if ((amask >> g) & 1u) {
 #pragma unroll
                 for (int s = 2 * g; s < 2 * g + 2; ++s) {
                     const f2 dx = pair_of(VX, s) - X1, dy = pair_of(VY, s) - Y1, dz = pair_of(VZ, s) - Z1;
                     const f2 d = (dx * dx + dy * dy) + dz * dz;
-                    VT[2 * s] = fmin_nc(d.x, VT[2 * s], inf);
-                    VT[2 * s + 1] = fmin_nc(d.y, VT[2 * s + 1], inf);
+                    VT[2 * s] = fmin_ref(d.x, VT[2 * s]);
+                    VT[2 * s + 1] = fmin_ref(d.y, VT[2 * s + 1]);
                 }
                 float m4;
                 asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m4) : "v"(VT[4 * g]), "v"(VT[4 * g + 1]), "v"(VT[4 * g + 2]));
@@ -1079,15 +964,8 @@ __global__ __launch_bounds__(FS_T) void fps_sorted_kernel(const float4 *__restri
         // one lane holds the max measured 1.04 vs 0.96 us per iteration)
         const float W = readlane_f(row_max16_dpp(gm), 0);
         uint32_t rl = 0xffffffffu;
-        if constexpr (HREG_FS_TREE) {
-            uint32_t c[FS_NG];
 #pragma unroll
-            for (int g = 0; g < FS_NG; ++g) c[g] = tg[g] == W ? rg[g] : 0xffffffffu;
-            rl = min(umin3(c[0], c[1], c[2]), umin3(c[3], c[4], umin3(c[5], c[6], c[7])));
-        } else {
-#pragma unroll
-            for (int g = 0; g < FS_NG; ++g) rl = tg[g] == W ? min(rl, rg[g]) : rl;
-        }
+        for (int g = 0; g < FS_NG; ++g) rl = tg[g] == W ? min(rl, rg[g]) : rl;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)wave_min_to63_u32_dpp(rl), 63);
         const int wl = (int)__builtin_ctzll(__ballot(rl == R));
         const int sl = (int)(R & 31u);
@@ -1126,6 +1004,180 @@ __global__ __launch_bounds__(FS_T) void fps_sorted_kernel(const float4 *__restri
         float *tp = temp_out + (size_t)cloud * FS_N;
 #pragma unroll
         for (int s = 0; s < FS_S; ++s) tp[__float_as_int(SP[soff(s)].w)] = VT[s];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Level-1 FPS of large clouds (16384 < n <= 65536, n % 64 == 0: Model_V2's 65536-point clouds,
+// configs[4]) on ONE workgroup, with exact pruning per 64-point block of the spatial index (r6).
+//
+// A 65536-point cloud's coordinates do not fit one CU's registers, which is why the cluster kernel
+// above spreads it over 32 single-wave workgroups exchanging candidates through memory every
+// iteration (~2 us per iteration in the Model_V2 step, with 32 spinning waves per cloud).  With
+// pruning, an iteration only reads the few blocks its new centre can change (~28 of 1024 blocks
+// on KITTI-shape clouds with the 15-bit index, knn.hip spatial_index_kernel<true>), so here the
+// running minima T stay in registers (64 slots per lane) and the coordinates of the blocks to
+// scan are read from the index's sorted float4 copy (L2-resident, 1 MB per cloud) each time:
+//   * 16 waves; wave w's slot r of lane l is sorted point (16 r + w) * 64 + l, i.e. wave w owns
+//     the index blocks 16 r + w (consecutive blocks in different waves: a centre's affected
+//     blocks are spatial neighbours, so they spread over the waves), and lane r of wave w holds
+//     block 16 r + w's box (the index's) and its candidate: the block's largest T and the
+//     smallest reference rank R among its points at that T;
+//   * per iteration a block is scanned only if its box lower bound to the new centre is below
+//     the block's largest T (fps_sorted_kernel's exactness argument, per block), up to 4 blocks'
+//     loads in flight per wave;
+//   * the winner is max T, then min R over the blocks, waves (LDS, one barrier) -- R = the
+//     reference rank (bitrev_L(k mod bs) * Q + k div bs, SURVEY.md 8a's tie rule) << 16 | the
+//     sorted position -- and its coordinates and index come from the sorted copy.
+// No spinning participants: one CU per cloud, ~100 VGPRs per lane, so the other lanes' level
+// kernels share its CU.
+// Measured (tools/fps_blocks_time.py, 8 / 64 KITTI-shape clouds, r6): up to 4 blocks' loads in
+// flight per wave 1.53 / 1.87 us per iteration (2: 1.63 / 1.84; 8: 2.43 / 2.78, register
+// pressure); skipping the block's min-rank reduction when one lane holds its maximum 1.73 ->
+// 1.53; carrying the candidates' coordinates through the exchange instead of reading the
+// winner's from the index after it 1.66 (no gain: three readlanes per scanned block).
+// 64 clouds run slower than 8: their sorted copies (64 MB) exceed the L2s, so blocks come from
+// the MALL.  The cluster kernel on the same clouds: 1.97 / 5.6 us per iteration.
+constexpr int FB_T = 1024, FB_NW = 16, FB_A = 4;
+
+__device__ __forceinline__ uint32_t fb_rank(uint32_t id, int L, int Q) {
+    return bitrev_bits(id & ((1u << L) - 1u), L) * (uint32_t)Q + (id >> L);
+}
+
+__global__ __launch_bounds__(FB_T) void fps_blocks_kernel(const float4 *__restrict__ spts,
+                                                          const float4 *__restrict__ boxes, int np,
+                                                          const float *__restrict__ xyz,
+                                                          float *__restrict__ temp_out,
+                                                          int32_t *__restrict__ idx_out,
+                                                          float *__restrict__ sampled_out, int n, int m,
+                                                          int L, int Q, float inf) {
+    typedef typename SlotVec<32>::type V;
+    __shared__ float s_w[2][FB_NW];  // the waves' candidates: max T, min R
+    __shared__ uint32_t s_r[2][FB_NW];
+    const int cloud = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(wv);
+    const int rows = n >> 6;
+    const float4 *SP = spts + (size_t)cloud * np;
+    const float4 *BX = boxes + (size_t)cloud * (np / 64) * 2;
+
+    // this lane's block (16 lane + w): box and candidate; -inf: no block
+    const int myrow = 16 * lane + w;
+    float lx = 0.f, ly = 0.f, lz = 0.f, hx = 0.f, hy = 0.f, hz = 0.f;
+    float rmT = -__builtin_huge_valf();
+    uint32_t rR = 0xffffffffu;
+    if (myrow < rows) {
+        const float4 a = BX[2 * myrow], b = BX[2 * myrow + 1];
+        lx = a.x; ly = a.y; lz = a.z; hx = b.x; hy = b.y; hz = b.z;
+        rmT = 1e10f;
+    }
+    // running minima: slot r in T0 (r < 32) / T1; the block's smallest rank into its lane
+    V T0, T1;
+#pragma unroll
+    for (int r = 0; r < 64; ++r) {
+        if (r < 32) T0[r] = 1e10f;
+        else T1[r - 32] = 1e10f;
+        if (16 * r + w < rows) {  // (uniform)
+            const int pos = (16 * r + w) * 64 + lane;
+            const uint32_t R = (fb_rank((uint32_t)__float_as_int(SP[pos].w), L, Q) << 16) | (uint32_t)pos;
+            const uint32_t Rm = (uint32_t)__builtin_amdgcn_readlane((int)wave_min_to63_u32_dpp(R), 63);
+            if (lane == r) rR = Rm;
+        }
+    }
+
+    const float *P = xyz + (size_t)cloud * n * 3;
+    float x1 = P[0], y1 = P[1], z1 = P[2];
+    if (tid == 0) {
+        idx_out[(size_t)cloud * m] = 0;
+        if (sampled_out) {
+            float *o = sampled_out + (size_t)cloud * m * 3;
+            o[0] = x1; o[1] = y1; o[2] = z1;
+        }
+    }
+
+    for (int j = 1; j < m; ++j) {
+        // which of this wave's blocks can change: box lower bound below the block's largest T
+        const float qx = fminf(fmaxf(x1, lx), hx), qy = fminf(fmaxf(y1, ly), hy), qz = fminf(fmaxf(z1, lz), hz);
+        const float lb = sqdist3(x1, y1, z1, qx, qy, qz);
+        const uint64_t act = __ballot(lb < rmT);
+        // slots 0..31 (T0), then 32..63 (T1): a separate loop per register tuple, so every
+        // access is one indexed register read / write (s_set_gpr_idx) with the slot in an SGPR
+        auto scan = [&](V &T, uint32_t act32, int r0) {
+            while (act32) {
+                int ra[FB_A];
+                float4 v[FB_A];
+                int cnt = 0;
+#pragma unroll
+                for (int a = 0; a < FB_A; ++a) {
+                    ra[a] = 0;
+                    if (act32) {  // (uniform) the next block's points, loads in flight together
+                        const int r = (int)__builtin_ctz(act32);
+                        act32 &= act32 - 1;
+                        ra[a] = r;
+                        cnt = a + 1;
+                        v[a] = SP[(16 * (r0 + r) + w) * 64 + lane];
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < FB_A; ++a) {
+                    if (a < cnt) {
+                        const int r = ra[a];
+                        // the reference arithmetic (.cu:129-130): two-rounding squared distance, min
+                        const float d = sqdist3(v[a].x, v[a].y, v[a].z, x1, y1, z1);
+                        const float t = fmin_ref(d, T[r]);
+                        T[r] = t;
+                        const uint32_t pos = (uint32_t)((16 * (r0 + r) + w) * 64 + lane);
+                        const uint32_t R = (fb_rank((uint32_t)__float_as_int(v[a].w), L, Q) << 16) | pos;
+                        // the block's candidate: max T, then min R -- one lane at the max (the
+                        // usual case) needs no second reduction
+                        const float mx = readlane_f(wave_max_to63_dpp(t), 63);
+                        const uint64_t at = __ballot(t == mx);
+                        const uint32_t Rm =
+                            __builtin_popcountll(at) == 1  // (uniform)
+                                ? (uint32_t)__builtin_amdgcn_readlane((int)R, (int)__builtin_ctzll(at))
+                                : (uint32_t)__builtin_amdgcn_readlane(
+                                      (int)wave_min_to63_u32_dpp(t == mx ? R : 0xffffffffu), 63);
+                        if (lane == r0 + r) {
+                            rmT = mx;
+                            rR = Rm;
+                        }
+                    }
+                }
+            }
+        };
+        scan(T0, (uint32_t)act, 0);
+        scan(T1, (uint32_t)(act >> 32), 32);
+        // the wave's candidate, then the workgroup's: max T, then min R
+        const float W = readlane_f(wave_max_to63_dpp(rmT), 63);
+        const uint32_t Rw =
+            (uint32_t)__builtin_amdgcn_readlane((int)wave_min_to63_u32_dpp(rmT == W ? rR : 0xffffffffu), 63);
+        const int buf = j & 1;
+        if (lane == 0) {
+            s_w[buf][wv] = W;
+            s_r[buf][wv] = Rw;
+        }
+        lds_barrier();
+        const float cw = s_w[buf][lane & (FB_NW - 1)];
+        const uint32_t cr = s_r[buf][lane & (FB_NW - 1)];
+        const float gmax = readlane_f(row_max16_dpp(cw), 0);
+        const uint32_t Rg =
+            (uint32_t)__builtin_amdgcn_readlane((int)row_min16_u32_dpp(cw == gmax ? cr : 0xffffffffu), 0);
+        const float4 q = SP[Rg & 0xffffu];  // (uniform address: the winner from the sorted copy)
+        x1 = q.x;
+        y1 = q.y;
+        z1 = q.z;
+        if (tid == 0) {
+            idx_out[(size_t)cloud * m + j] = __float_as_int(q.w);
+            if (sampled_out) {
+                float *o = sampled_out + ((size_t)cloud * m + j) * 3;
+                o[0] = x1; o[1] = y1; o[2] = z1;
+            }
+        }
+    }
+    if (temp_out) {
+        float *tp = temp_out + (size_t)cloud * n;
+#pragma unroll
+        for (int r = 0; r < 64; ++r)
+            if (16 * r + w < rows) tp[__float_as_int(SP[(16 * r + w) * 64 + lane].w)] = r < 32 ? T0[r] : T1[r - 32];
     }
 }
 
@@ -1219,6 +1271,18 @@ extern "C" int hreg_fps_indexed(int b, int n, int m, const float *points, const 
     if (b < 0 || n <= 0 || !points || !idx || !ws) return HREG_ERR_INVALID;
     if (b == 0 || m <= 0) return HREG_OK;
     const int bs = hreg_opt_n_threads(n);
+    if (n > FS_N && n <= 65536 && n % 64 == 0 && !(reinterpret_cast<uintptr_t>(ws) & 15)) {
+        // large clouds: one workgroup, T in registers, blocks read from the index (above)
+        size_t np = 64;
+        while (np < (size_t)n) np <<= 1;
+        const float4 *spts = static_cast<const float4 *>(ws);
+        const int L = hreg_ilog2(bs), Q = (n + bs - 1) / bs;
+        hipLaunchKernelGGL(fps_blocks_kernel, dim3(b), dim3(FB_T), 0, as_stream(stream), spts,
+                           spts + (size_t)b * np, (int)np, points, temp, idx, sampled_xyz, n, m, L, Q,
+                           __builtin_huge_valf());
+        HREG_CHECK_LAUNCH();
+        return HREG_OK;
+    }
     if (n != FS_N || bs * (n / bs) != n || (n / bs) > 32 || (reinterpret_cast<uintptr_t>(ws) & 15))
         return launch_fps<false>(b, n, m, points, nullptr, temp, idx, sampled_xyz, as_stream(stream));
     const int L = hreg_ilog2(bs), LQ = hreg_ilog2(n / bs);

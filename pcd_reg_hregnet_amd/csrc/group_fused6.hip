@@ -88,38 +88,23 @@ __device__ __forceinline__ void conv_stack6(WT &&wt, const float *eb, int gg, in
     relu_tiles(out);
 }
 
-// HREG_RING (level 2): the weight pieces through the workgroup-shared LDS stream
-// (mfma_chain.h Ring6) instead of one register stream per wave
-#ifndef HREG_RING
-#define HREG_RING 1
-#endif
-#ifndef HREG_RING_WPS
-#define HREG_RING_WPS 3  // waves per SIMD the ring kernel's register budget targets
-#endif
-// level 3 on the ring (engine.SPLIT_L3 off selects it; A/B against the channel-split kernel)
-#ifndef HREG_RING_L3
-#define HREG_RING_L3 1
-#endif
-#ifndef HREG_RING_WPS_L3
-#define HREG_RING_WPS_L3 1
-#endif
+// The weight pieces through the workgroup-shared LDS stream (mfma_chain.h Ring6) instead of one
+// register stream per wave (r2, level 2: 187 -> 171 us, TD 86 -> 59 % busy), at 3 waves per SIMD
+// (2: 192 us); level 3 on the ring (engine.SPLIT_L3 off: the checker form) at one wave per SIMD.
 template <class K>
-constexpr bool ring_on() { return HREG_RING && (K::KN == 32 || HREG_RING_L3); }
+constexpr bool ring_on() { return true; }
 template <class K>
-constexpr int ring_wps() { return K::KN == 32 ? HREG_RING_WPS : HREG_RING_WPS_L3; }
+constexpr int ring_wps() { return K::KN == 32 ? 3 : 1; }
 
-// HREG_L2_X2B (level 2 on the ring): mlp1's x2 block batched over the workgroup.  x2 (the
-// k-max row of the descriptor stack, layers.py:204-206) is the same for all 32 rows of a
-// group, so the per-wave block (N3 chunks x TM1 tiles, 96 MFMAs) computes one column 32
-// times.  Batched: the 4 waves' x2 rows go to LDS as the 4 columns of one B operand and the
-// block's TM1 x N3 chunk-tiles are dealt out, one tile and half of the chunks per wave (24
-// MFMAs, 4 ring steps instead of 8); the partial columns meet in LDS and each wave adds its
-// group's (lower-half + upper-half chunks) to mlp1 after the x1d block.
-#ifndef HREG_L2_X2B
-#define HREG_L2_X2B 1
-#endif
+// Level 2 on the ring: mlp1's x2 block batched over the workgroup.  x2 (the k-max row of the
+// descriptor stack, layers.py:204-206) is the same for all 32 rows of a group, so the per-wave
+// block (N3 chunks x TM1 tiles, 96 MFMAs) computes one column 32 times.  Batched: the 4 waves' x2
+// rows go to LDS as the 4 columns of one B operand and the block's TM1 x N3 chunk-tiles are dealt
+// out, one tile and half of the chunks per wave (24 MFMAs, 4 ring steps instead of 8); the
+// partial columns meet in LDS and each wave adds its group's (lower-half + upper-half chunks) to
+// mlp1 after the x1d block (r5: 158.6 -> 153.7 us).
 template <class K, bool RING>
-constexpr bool x2b_on() { return HREG_L2_X2B && RING && K::KN == 32 && K::TM1 == 2 && WAVES == 4; }
+constexpr bool x2b_on() { return RING && K::KN == 32 && K::TM1 == 2 && WAVES == 4; }
 
 // the batched x2 block (x2b_on): P (zeroed here) <- this wave's tile (w & 1) of W_x2 over
 // chunks 4 (w >> 1) .. + 3, the B columns = the workgroup's x2 rows (sX[col][channel]).
@@ -394,202 +379,6 @@ int launch_group6(const float *table, const float *geom, const float *knn_xyz, c
 }
 
 
-// ------------------------------------------------------------------------
-// Pair form (hreg_group6x2_l2): one wave owns TWO 32-row groups (JT = 2 row tiles,
-// mfma_jt.h), so every weight-piece chunk streamed from L2 feeds the MFMAs of 64 rows
-// instead of 32 -- the one-group kernel above needs 512 B of pieces per MFMA, about what
-// the L2 -> CU path delivers at half the MFMA rate.  Same table, same arithmetic per
-// row (bitwise-identical results); 1 wave per SIMD (the doubled accumulators), PRE only.
-using namespace hreg_jt;
-
-template <class K, int NC>
-__device__ __forceinline__ void conv_stack_jt6(const gu32x4 *__restrict__ wt, const float *eb, int gg, int g2,
-                                               int g3, int e2, int e3, int lane, const float2 (&gin)[JT],
-                                               const float *const (&pre_row)[JT], f32x16 (&out)[K::T3][JT],
-                                               const Carry &cin, FragSeq next, Carry &cout) {
-    constexpr int T1 = K::T1, T3 = K::T3, N1 = K::N1;
-    f32x16 h1[T1][JT], h2[T1][JT];
-    Carry c2, c3;
-    const int h = lane >> 5;
-#pragma unroll
-    for (int jt = 0; jt < JT; ++jt)
-#pragma unroll
-        for (int co = 0; co < T1; ++co)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float4 a = *reinterpret_cast<const float4 *>(pre_row[jt] + co * 32 + 8 * r + 4 * h);
-                h1[co][jt][4 * r] = a.x; h1[co][jt][4 * r + 1] = a.y;
-                h1[co][jt][4 * r + 2] = a.z; h1[co][jt][4 * r + 3] = a.w;
-            }
-    // geometry chunk: f32 k-steps 0, 1 (channels 2h, 2h + 1), the rest zero
-    pipe6_jt<1, T1, T1, false>(
-        wt, lane, FragSeq{gg, 1},
-        [&](int jt, int st) { return st == 0 ? gin[jt].x : st == 1 ? gin[jt].y : 0.f; }, h1, cin,
-        FragSeq{g2, N1}, c2);
-    relu_jt(h1);
-    beta_jt<T1>(eb + e2, lane, h2);
-    pipe6_jt<N1, T1, T3, false>(wt, lane, FragSeq{g2, N1}, [&](int jt, int st) { return h1[st >> 4][jt][st & 15]; },
-                                h2, c2, FragSeq{g3, N1}, c3);
-    relu_jt(h2);
-    beta_jt<T3>(eb + e3, lane, out);
-    pipe6_jt<N1, T3, NC, false>(wt, lane, FragSeq{g3, N1}, [&](int jt, int st) { return h2[st >> 4][jt][st & 15]; },
-                                out, c3, next, cout);
-    relu_jt(out);
-}
-
-template <class K>
-__global__ __launch_bounds__(256, 1) void group_pair6_kernel(
-    const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
-    const int32_t *__restrict__ gidx, int G, float *__restrict__ kp, float *__restrict__ att_feat,
-    float *__restrict__ desc, const float *__restrict__ pre) {
-    static_assert(K::KN == 32, "one 32-row tile per group");
-    constexpr int C3 = K::T3 * 32, CM2 = K::TM2 * 32;
-    constexpr int T1 = K::T1, T3 = K::T3, TM1 = K::TM1, TM2 = K::TM2, N3 = K::N3, NM1 = K::NM1;
-    constexpr int NE = K::TABLE - K::F_END;
-    __shared__ float ep[NE];
-    for (int i = threadIdx.x; i < NE; i += blockDim.x) ep[i] = table[K::F_END + i];
-    __syncthreads();
-    const float *eb = ep - K::F_END;
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int h = lane >> 5, j = lane & 31;
-    const int NP = (G + 1) / 2;  // group pairs; an odd G's last pair recomputes its group
-
-    const FragSeq det_g{K::G_DG, 1}, desc_g{K::G_EG, 1};
-    const FragSeq m1x2{K::G_M1, 3 * N3}, m1x1{K::G_M1 + N3, 3 * N3}, m1em{K::G_M1 + 2 * N3, 3 * N3};
-    const FragSeq m2{K::G_M2, NM1};
-
-    Carry carry;
-    {
-        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(reinterpret_cast<uint64_t>(table));
-#pragma unroll
-        for (int co = 0; co < T1; ++co) ld6(wt, det_g.base + co, lane, carry[co]);
-    }
-    for (int pp = blockIdx.x * WAVES + w; pp < NP; pp += gridDim.x * WAVES) {
-        uint64_t tba = reinterpret_cast<uint64_t>(table);
-        asm volatile("" : "+s"(tba));
-        const gu32x4 *wt = reinterpret_cast<const gu32x4 *>(tba);
-        int g[JT];
-        size_t row[JT];
-        float2 gin[JT];
-        const float *pr[JT], *pr2[JT];
-#pragma unroll
-        for (int jt = 0; jt < JT; ++jt) {
-            g[jt] = min(2 * pp + jt, G - 1);
-            row[jt] = (size_t)g[jt] * 32 + j;
-            gin[jt] = *reinterpret_cast<const float2 *>(geom + row[jt] * 4 + 2 * h);
-            pr[jt] = pre + (size_t)gidx[row[jt]] * (2 * T1 * 32);  // [det C1 | desc C1]
-            pr2[jt] = pr[jt] + T1 * 32;
-        }
-        Carry ca, cb;
-
-        // ---- detector convs -> emb
-        f32x16 emb[T3][JT];
-        conv_stack_jt6<K, TM1>(wt, eb, K::G_DG, K::G_D2, K::G_D3, K::E_D2, K::E_D3, lane, gin, pr, emb, carry,
-                               m1em, ca);
-
-        // ---- attention per group: x1 = max_c emb, softmax over the 32 rows
-        float a[JT];
-#pragma unroll
-        for (int jt = 0; jt < JT; ++jt) {
-            int mi = __float_as_int(emb[0][jt][0]);
-#pragma unroll
-            for (int co = 0; co < T3; ++co)
-#pragma unroll
-                for (int q = 0; q < 16; ++q) mi = max(mi, __float_as_int(emb[co][jt][q]));
-            const float x1 = __int_as_float(max(mi, __shfl_xor(mi, 32)));
-            const float mx = half_bcast(half_max_hi_nonneg(x1), h);
-            const float e = expf(fsub_rn(x1, mx));
-            a[jt] = e / half_bcast(half_sum_hi(e), h);
-            const float *p = knn_xyz + row[jt] * 3;
-            const float kx = half_sum_hi(fmul_rn(a[jt], p[0]));
-            const float ky = half_sum_hi(fmul_rn(a[jt], p[1]));
-            const float kz = half_sum_hi(fmul_rn(a[jt], p[2]));
-            if (j == 31 && h == 0) {
-                kp[(size_t)g[jt] * 3 + 0] = kx;
-                kp[(size_t)g[jt] * 3 + 1] = ky;
-                kp[(size_t)g[jt] * 3 + 2] = kz;
-            }
-#pragma unroll
-            for (int co = 0; co < T3; ++co) {
-                float v[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = fmul_rn(emb[co][jt][q], a[jt]);
-                reduce_store<32, Sum>(att_feat + (size_t)g[jt] * C3, co, v, lane);
-            }
-        }
-
-        // ---- mlp1 = W [x2 | x1d | emb * a] -> CM1, the emb * a part first
-        f32x16 y1[TM1][JT];
-        beta_jt<TM1>(eb + K::E_M1, lane, y1);
-        pipe6_jt<N3, TM1, T1, false>(
-            wt, lane, m1em, [&](int jt, int st) { return fmul_rn(emb[st >> 4][jt][st & 15], a[jt]); }, y1, ca,
-            desc_g, cb);
-
-        // ---- descriptor convs -> x1d
-        f32x16 x1d[T3][JT];
-        conv_stack_jt6<K, TM1>(wt, eb, K::G_EG, K::G_E2, K::G_E3, K::E_E2, K::E_E3, lane, gin, pr2, x1d, cb, m1x2,
-                               ca);
-#pragma unroll
-        for (int ct = 0; ct < T3; ++ct) {
-            float x2[JT][16];
-#pragma unroll
-            for (int jt = 0; jt < JT; ++jt) {
-#pragma unroll
-                for (int q = 0; q < 16; ++q) x2[jt][q] = x1d[ct][jt][q];
-                bfly32<MaxNN>(x2[jt], lane);
-                bcast32(x2[jt], lane);
-            }
-            const FragSeq cur{m1x2.base + ct * 2, m1x2.stride};
-            const FragSeq nxt = ct + 1 < T3 ? FragSeq{m1x2.base + (ct + 1) * 2, m1x2.stride} : m1x1;
-            if (ct & 1)
-                pipe6_jt<2, TM1, TM1, false>(wt, lane, cur, [&](int jt, int st) { return x2[jt][st]; }, y1, cb, nxt,
-                                             ca);
-            else
-                pipe6_jt<2, TM1, TM1, false>(wt, lane, cur, [&](int jt, int st) { return x2[jt][st]; }, y1, ca, nxt,
-                                             cb);
-        }
-        static_assert(T3 % 2 == 0, "carry parity");
-        pipe6_jt<N3, TM1, TM2, false>(wt, lane, m1x1, [&](int jt, int st) { return x1d[st >> 4][jt][st & 15]; }, y1,
-                                      ca, m2, cb);
-        relu_jt(y1);
-
-        // ---- mlp2 + k-max -> descriptor; prefetches the next pair's first chunk
-        f32x16 y2[TM2][JT];
-        beta_jt<TM2>(eb + K::E_M2, lane, y2);
-        pipe6_jt<NM1, TM2, T1, false>(wt, lane, m2, [&](int jt, int st) { return y1[st >> 4][jt][st & 15]; }, y2, cb,
-                                      det_g, carry);
-        relu_jt(y2);
-#pragma unroll
-        for (int jt = 0; jt < JT; ++jt)
-#pragma unroll
-            for (int co = 0; co < TM2; ++co) {
-                float v[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = y2[co][jt][q];
-                reduce_store<32, MaxNN>(desc + (size_t)g[jt] * CM2, co, v, lane);
-            }
-    }
-}
-
-template <class K>
-int launch_pair6(const float *table, const float *geom, const float *knn_xyz, const int32_t *gidx,
-                 const float *feats, int G, float *kp, float *att_feat, float *desc, const float *pre,
-                 void *stream) {
-    if (!table || !geom || !knn_xyz || !gidx || !feats || !kp || !att_feat || !desc || !pre || G < 0)
-        return HREG_ERR_INVALID;
-    if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(pre) & 15) ||
-        (reinterpret_cast<uintptr_t>(geom) & 7) || (reinterpret_cast<uintptr_t>(att_feat) & 15) ||
-        (reinterpret_cast<uintptr_t>(desc) & 15))
-        return HREG_ERR_INVALID;
-    if (!G) return HREG_OK;
-    const int NP = (G + 1) / 2;
-    int grid = (NP + WAVES - 1) / WAVES;
-    if (grid > 1024) grid = 1024;  // four rounds of one resident workgroup per CU
-    hipLaunchKernelGGL((group_pair6_kernel<K>), dim3(grid), dim3(256), 0, as_stream(stream), table, geom, knn_xyz,
-                       gidx, G, kp, att_feat, desc, pre);
-    HREG_CHECK_LAUNCH();
-    return HREG_OK;
-}
 }  // namespace
 
 extern "C" int hreg_group6_l2_table_floats(void) { return L2::TABLE; }
@@ -605,11 +394,4 @@ extern "C" int hreg_group6_l3(const float *table, const float *geom, const float
                               const float *feats, int G, float *kp, float *att_feat, float *desc,
                               const float *pre, void *stream) {
     return launch_group6<L3>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre, stream);
-}
-
-// the pair form of hreg_group6_l2 (two groups per wave; pre required, same table)
-extern "C" int hreg_group6x2_l2(const float *table, const float *geom, const float *knn_xyz, const int32_t *gidx,
-                                const float *feats, int G, float *kp, float *att_feat, float *desc,
-                                const float *pre, void *stream) {
-    return launch_pair6<L2>(table, geom, knn_xyz, gidx, feats, G, kp, att_feat, desc, pre, stream);
 }

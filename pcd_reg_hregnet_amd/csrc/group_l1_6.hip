@@ -25,7 +25,6 @@
 #include "mfma_chain.h"
 // weight table resident in LDS (below: the LDSW kernel form, hreg_group_l1_6) or streamed
 // from global memory (hreg_group_l1_6g)
-#define HREG_PIN_PREFETCH 1  // (mfma_jt.h: applies to the LDS-table form only)
 namespace hreg_chain {
 __device__ __forceinline__ void ld6(const __attribute__((address_space(3))) u32x4 *wt, int f, int lane,
                                     u32x4 (&o)[3]) {
@@ -85,25 +84,16 @@ __device__ __forceinline__ void conv_stack6(WP wt, const float *eb, int g1, int 
     relu_jt(out);
 }
 
-#ifndef HREG_L16_WPS
-#define HREG_L16_WPS 2  // waves per SIMD the register budget targets (A/B builds: 3)
-#endif
-// HREG_L1_X2ONE: mlp1's x2 block (the k-max row repeated over the 64 rows, layers.py:204-206)
-// on one row tile's MFMAs instead of both -- 24 of the group's 360 MFMAs fewer
-#ifndef HREG_L1_X2ONE
-#define HREG_L1_X2ONE 1
-#endif
-// HREG_L1_PRIO: the second half of the 8-wave workgroup (each SIMD's younger wave) at
-// s_setprio 1 for the whole kernel (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-#ifndef HREG_L1_PRIO
-#define HREG_L1_PRIO 0
-#endif
+// waves per SIMD the register budget targets (the global-table form; 3 spills 49 VGPRs)
+constexpr int L16_WPS = 2;
+// (measured and removed, r5: the younger half of the 8-wave workgroup at s_setprio 1, 180.7 ->
+// 183.3 us)
 // LDSW (hreg_group_l1_6): the whole weight-piece table (90 KB) resident in LDS -- each 8-wave
 // workgroup copies it once and loops over 16+ groups; chunk fragments are ds_read_b128
 // (the per-wave weight streams through the vector-memory path keep the CU's texture-data
 // return unit ~70-87 % busy).  The epilogue constants then come through vector memory so
 // that the LDS counter tracks the fragment reads alone, and the prefetch is pinned ahead
-// of each chunk's MFMAs (mfma_jt.h HREG_PIN_PREFETCH).  Measured: 172.7 vs 175.2 us in the
+// of each chunk's MFMAs (mfma_jt.h).  Measured: 172.7 vs 175.2 us in the
 // bench, 328k vs 340k cycles standalone.  But the 92 KB of LDS leave no room beside a
 // co-running kernel that holds LDS on every CU -- Model_V2's cluster FPS (clouds > 16384
 // points) -- so that configuration runs the global-table form (LDSW false, 4-wave
@@ -113,7 +103,7 @@ constexpr int l1_waves() { return LDSW ? 8 : WAVES; }
 typedef __attribute__((address_space(3))) const u32x4 lu32x4;
 
 template <bool LDSW>
-__global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : HREG_L16_WPS) void group_l1_6_kernel(
+__global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : L16_WPS) void group_l1_6_kernel(
     const float *__restrict__ table, const float *__restrict__ geom, const float *__restrict__ knn_xyz,
     int G, float *__restrict__ kp, float *__restrict__ att_feat, float *__restrict__ desc) {
     constexpr int L1_WAVES = l1_waves<LDSW>();
@@ -128,9 +118,6 @@ __global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : HREG_L16_WPS) voi
     __syncthreads();
     const float *eb = LDSW ? table : ep - F_END;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if constexpr (HREG_L1_PRIO && LDSW) {
-        if (w >= 4) __builtin_amdgcn_s_setprio(1);
-    }
     const int h = lane >> 5, j = lane & 31;
     const FragSeq m1x2{G_M1, 12}, m1x1{G_M1 + 4, 12}, m1em{G_M1 + 8, 12}, m2{G_M2, 2};
     // opaque per-group table pointer: keeps the loop-invariant weight loads in the loop
@@ -218,9 +205,10 @@ __global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : HREG_L16_WPS) voi
             bfly32<MaxNN>(x2[co], lane);
             bcast32(x2[co], lane);
         }
-        if constexpr (HREG_L1_X2ONE) {
-            // the x2 block once (its B, and so its product, is the same for both row tiles),
-            // added to both tiles after the x1d block
+        {
+            // the x2 block (the k-max row repeated over the 64 rows, layers.py:204-206) once: its
+            // B, and so its product, is the same for both row tiles; added to both tiles after
+            // the x1d block (24 of the group's 360 MFMAs fewer: 177.6 -> 173.1 us, r5)
             f32x16 z[1][1];
             z[0][0] = zero16();
             pipe6_jt<4, 1, 1, true>(wt, lane, m1x2, [&](int, int st) { return x2[st >> 4][st & 15]; }, z, ca,
@@ -231,11 +219,6 @@ __global__ __launch_bounds__(l1_waves<LDSW>() * 64, LDSW ? 1 : HREG_L16_WPS) voi
             for (int jt = 0; jt < JT; ++jt)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) y1[0][jt][q] = fadd_rn(y1[0][jt][q], z[0][0][q]);
-        } else {
-            pipe6_jt<4, 1, 1, true>(wt, lane, m1x2, [&](int, int st) { return x2[st >> 4][st & 15]; }, y1, ca,
-                                    m1x1, cb);
-            pipe6_jt<4, 1, 2, false>(wt, lane, m1x1, [&](int jt, int st) { return x1d[st >> 4][jt][st & 15]; },
-                                     y1, cb, m2, ca);
         }
         relu_jt(y1);
 

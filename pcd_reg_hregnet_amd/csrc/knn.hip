@@ -17,10 +17,6 @@
 // sum_d (q_d - p_d)^2, non-contracted, sequential in d.
 #include "common.h"
 
-#ifndef HREG_KNN_MULTI
-#define HREG_KNN_MULTI 1  // (A/B: blocks per best-first round trip in the indexed kNN)
-#endif
-
 namespace {
 
 constexpr int WAVES = 4;
@@ -115,12 +111,10 @@ __device__ void knn3_query(const float *__restrict__ P, int n2, float qx, float 
 }
 
 // QW queries (of one cloud) per wave: every database point a lane loads feeds QW distances;
-// each query keeps its own list, buffer and distance order (the lists of knn3_query).
-// HREG_KNN3_QW (A/B; the launchers fall back to 1 when the per-cloud query count is not a
-// multiple).
-#ifndef HREG_KNN3_QW
-#define HREG_KNN3_QW 1
-#endif
+// each query keeps its own list, buffer and distance order (the lists of knn3_query).  The xyz
+// kNNs run QW = 1: with 3 floats per point the load is not their cost (r5, bench lines 8392 /
+// 8294 at QW 1 vs 8296 / 8024 at QW 4, gpurun_out/r5w); the descriptor kNN shares its rows
+// (knnd_wave_kernel, KNND_QW).
 template <int K, int QW>
 __device__ void knn3_query_multi(const float *__restrict__ P, int n2, const float (&qx)[QW], const float (&qy)[QW],
                                  const float (&qz)[QW], uint64_t (*buf)[128], int lane, WaveList (&L)[QW]) {
@@ -315,15 +309,14 @@ __global__ __launch_bounds__(256) void knnd_kernel(const float *__restrict__ q,
 // of 16 barrier-separated staging round trips; this is 2048 independent waves.
 // Same distance order (q - p, squared, added in d order) and the same offer/merge:
 // bit-identical lists.
-// HREG_KNND_QW: queries per wave.  Every database row a lane loads (1 KB at 256 dims) feeds
+// KNND_QW: queries per wave.  Every database row a lane loads (1 KB at 256 dims) feeds
 // QW queries' distances, so the L2 -> CU row stream per query drops QW-fold; each query keeps
 // its own candidate list (WaveList + LDS buffer) and its own accumulation order (bit-identical
 // distances and lists).  The QW queries of a wave belong to one cloud (n1 % QW == 0, else 1).
 // Measured (gpurun_out/r5r): CoarseReg's kNN over 32 pairs (256 x 256 x 256 dims) 0.274 ->
 // 0.091 ms at QW = 4; bench lines at --steps 20 7990 -> 8178 pairs/s (paired, one box).
-#ifndef HREG_KNND_QW
-#define HREG_KNND_QW 4
-#endif
+// QW = 8: 0.158 ms (more VGPRs, fewer waves).
+constexpr int KNND_QW = 4;
 template <int K, int QW>
 __global__ __launch_bounds__(256) void knnd_wave_kernel(const float *__restrict__ q,
                                                         const float *__restrict__ p, int nb, int n1,
@@ -406,9 +399,11 @@ __device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits -> every 
     return v;
 }
 
+// (NaN coordinates map to cell 0: !(t > 0) holds for NaN, so the float -> uint conversion only
+// ever sees values in (0, 1023))
 __device__ __forceinline__ uint32_t quant10(float x, float lo, float sc) {
     const float t = (x - lo) * sc;
-    return t <= 0.f ? 0u : (t >= 1023.f ? 1023u : (uint32_t)t);
+    return !(t > 0.f) ? 0u : (t >= 1023.f ? 1023u : (uint32_t)t);
 }
 
 __device__ __forceinline__ float box_lb(float qx, float qy, float qz, float4 lo, float4 hi) {
@@ -418,24 +413,26 @@ __device__ __forceinline__ float box_lb(float qx, float qy, float qz, float4 lo,
     return sqdist3(qx, qy, qz, cx, cy, cz);
 }
 
-constexpr int SI_CELLS = 4096;  // 12-bit Morton prefix: a 16 x 16 x 16 grid
+// Large clouds (SI_LDSN < n <= SI_MAXN, Model_V2): a counting sort by a 15-bit Morton prefix
+// (32 cells per axis, 128 KB of LDS counters); inside a cell the order is the LDS atomics', so the
+// cell size bounds a 64-point block's box.  On KITTI-shape 65536-point clouds (numpy model of the
+// pruned FPS, fps.hip fps_blocks_kernel) 15-bit cells leave ~28 blocks to scan per FPS iteration
+// against ~47 with the 12-bit cells of r1-r5 (a full 18-bit order: ~23).  The rank list does not
+// fit LDS, so points are scattered to their sorted slot in HBM directly and the boxes read them
+// back (this workgroup's own stores; fenced at agent scope).  The kNN and FPS results do not
+// depend on the order inside a cell.
+constexpr int SI_CELLS_BIG = 32768;
 
-template <bool BIG>
 __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *__restrict__ p, int n,
                                                                    float4 *__restrict__ spts,
                                                                    float4 *__restrict__ boxes) {
-    // counting sort of the points by the top 12 bits of their Morton code (the order
-    // inside a cell is whatever the LDS atomics give: it only shapes the boxes, the
-    // kNN result does not depend on it).  BIG (n > SI_LDSN): the sorted rank list does
-    // not fit LDS, so points are scattered to their sorted slot in HBM directly and
-    // the boxes read them back (this workgroup's own stores; fenced at agent scope)
-    __shared__ uint32_t cnt[SI_CELLS];
-    __shared__ int sidx[BIG ? 1 : SI_LDSN];
+    constexpr int CELLS = SI_CELLS_BIG;
+    __shared__ uint32_t cnt[CELLS];
     __shared__ float red[6][SI_THREADS / 64];
     __shared__ uint32_t wsum[SI_THREADS / 64];
     const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const float *P = p + (size_t)c * n * 3;
-    for (int i = tid; i < SI_CELLS; i += SI_THREADS) cnt[i] = 0;
+    for (int i = tid; i < CELLS; i += SI_THREADS) cnt[i] = 0;
     // cloud bounding box
     float mn[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
     float mx[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
@@ -464,12 +461,12 @@ __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *
         const uint32_t code = spread10(quant10(P[i * 3], lo[0], sc[0])) |
                               (spread10(quant10(P[i * 3 + 1], lo[1], sc[1])) << 1) |
                               (spread10(quant10(P[i * 3 + 2], lo[2], sc[2])) << 2);
-        return code >> 18;
+        return code >> 15;
     };
     for (int i = tid; i < n; i += SI_THREADS) atomicAdd(&cnt[cell_of(i)], 1u);
     __syncthreads();
-    // exclusive prefix over the 4096 cells: 4 per thread, wave scans, wave totals
-    constexpr int PER = SI_CELLS / SI_THREADS;
+    // exclusive prefix over the cells: CELLS / SI_THREADS per thread, wave scans, wave totals
+    constexpr int PER = CELLS / SI_THREADS;
     uint32_t v[PER], tsum = 0;
 #pragma unroll
     for (int e = 0; e < PER; ++e) { v[e] = cnt[tid * PER + e]; tsum += v[e]; }
@@ -490,35 +487,19 @@ __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *
     int np = 64;
     while (np < n) np <<= 1;
     float4 *S = spts + (size_t)c * np;
-    if constexpr (BIG) {
-        for (int i = tid; i < n; i += SI_THREADS)
-            S[atomicAdd(&cnt[cell_of(i)], 1u)] =
-                make_float4(P[i * 3], P[i * 3 + 1], P[i * 3 + 2], __int_as_float(i));
-        __threadfence();  // release: the scattered stores complete before the barrier
-        __syncthreads();
-        __threadfence();  // acquire: no stale L1 lines for the reads below
-    } else {
-        for (int i = tid; i < n; i += SI_THREADS) sidx[atomicAdd(&cnt[cell_of(i)], 1u)] = i;
-        __syncthreads();
-        for (int i = tid; i < n; i += SI_THREADS) {
-            const int id = sidx[i];
-            S[i] = make_float4(P[id * 3], P[id * 3 + 1], P[id * 3 + 2], __int_as_float(id));
-        }
-    }
+    for (int i = tid; i < n; i += SI_THREADS)
+        S[atomicAdd(&cnt[cell_of(i)], 1u)] = make_float4(P[i * 3], P[i * 3 + 1], P[i * 3 + 2], __int_as_float(i));
+    __threadfence();  // release: the scattered stores complete before the barrier
+    __syncthreads();
+    __threadfence();  // acquire: no stale L1 lines for the reads below
     const int nblk = (n + 63) / 64;
     float4 *B = boxes + (size_t)c * (np / 64) * 2;
     for (int b = w; b < nblk; b += SI_THREADS / 64) {
         const int i = b * 64 + lane;
         float v3[3], u3[3];
         if (i < n) {
-            if constexpr (BIG) {
-                const float4 v = S[i];
-                v3[0] = u3[0] = v.x; v3[1] = u3[1] = v.y; v3[2] = u3[2] = v.z;
-            } else {
-                const int id = sidx[i];
-#pragma unroll
-                for (int d = 0; d < 3; ++d) v3[d] = u3[d] = P[id * 3 + d];
-            }
+            const float4 q = S[i];
+            v3[0] = u3[0] = q.x; v3[1] = u3[1] = q.y; v3[2] = u3[2] = q.z;
         } else {
 #pragma unroll
             for (int d = 0; d < 3; ++d) { v3[d] = __builtin_huge_valf(); u3[d] = -__builtin_huge_valf(); }
@@ -532,7 +513,7 @@ __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *
     }
 }
 
-// HREG_SI_MORTON (clouds of <= SI_LDSN points): the points ordered by an 18-bit Morton prefix
+// Clouds of <= SI_LDSN points: the points ordered by an 18-bit Morton prefix
 // (64 cells per axis; ties by index) instead of the 12-bit cell alone.  Inside a 12-bit cell
 // (1/16 of the cloud's extent per axis) the counting sort leaves the points in atomic order,
 // so a 64-point block spans most of its cell and a level-1 query (k = 64 of 16384 LiDAR
@@ -542,9 +523,6 @@ __global__ __launch_bounds__(SI_THREADS) void spatial_index_kernel(const float *
 // passes of 6-bit digits in LDS (ping-pong, 2 x 64 KB); each wave owns a contiguous range of
 // the keys, so per-(digit, wave) offsets plus the in-chunk rank among lanes holding the same
 // digit (6 ballots) keep every pass stable.
-#ifndef HREG_SI_MORTON
-#define HREG_SI_MORTON 1
-#endif
 constexpr int SI_DIG = 6, SI_BUCKETS = 1 << SI_DIG, SI_WAVES = SI_THREADS / 64;
 
 __global__ __launch_bounds__(SI_THREADS) void spatial_index_morton_kernel(const float *__restrict__ p, int n,
@@ -744,41 +722,13 @@ __global__ __launch_bounds__(256) void knn_group_indexed_kernel(
         uint32_t lbb = 0;
         const int b = next_block(tau_bits, lbb);
         if (b < 0) break;
-#if HREG_KNN_MULTI > 1
-        // (r4) the next best blocks too, their points loaded in the same round trip: fewer
-        // dependent L2 round trips per query.  Exact: a block whose bound exceeds tau is
-        // skipped, every offered point is filtered by the running K-th key, and the stop test
-        // is unchanged (any extra block visited only offers more candidates).
-        constexpr int NV = HREG_KNN_MULTI;
-        int bv[NV];
-        uint32_t lbv[NV];
-        bv[0] = b;
-        lbv[0] = lbb;
-        const bool first = L.tau == KEY_INF;
-#pragma unroll
-        for (int t = 1; t < NV; ++t) {
-            lbv[t] = 0xffffffffu;
-            bv[t] = first ? -1 : next_block(tau_bits, lbv[t]);
-        }
-        float4 v[NV];
-#pragma unroll
-        for (int t = 0; t < NV; ++t) {
-            const int i = bv[t] * 64 + lane;
-            v[t] = (bv[t] >= 0 && lbv[t] <= tau_bits && i < n) ? S[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int t = 0; t < NV; ++t) {
-            if (bv[t] < 0 || lbv[t] > tau_bits) continue;
-            offer<K>(L, sbuf[w], block_key(v[t], bv[t] * 64 + lane), lane);
-            if (t == 0 && L.tau == KEY_INF && L.cnt > 0) flush64<K>(L, sbuf[w], lane);  // first tau early
-        }
-#else
+        // (r4: the next best blocks loaded in the same round trip, 2 or 4 per step, measured
+        // neutral and removed)
         if (lbb > tau_bits) continue;
         const int i = b * 64 + lane;
         const float4 v = i < n ? S[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         offer<K>(L, sbuf[w], block_key(v, i), lane);
         if (L.tau == KEY_INF && L.cnt > 0) flush64<K>(L, sbuf[w], lane);  // first tau early
-#endif
     }
     if (L.cnt > 0) flush64<K>(L, sbuf[w], lane);
 
@@ -805,17 +755,11 @@ int launch_knn(const float *p1, const float *p2, int b, int n1, int n2, int dim,
                float *dists, int64_t *idx64, int32_t *idx32, float *nn, hipStream_t st) {
     const int nq = b * n1;
     if (dim == 3) {
-        if (HREG_KNN3_QW > 1 && n1 % HREG_KNN3_QW == 0) {
-            constexpr int QW = HREG_KNN3_QW;
-            hipLaunchKernelGGL((knn3_kernel<K, QW>), dim3((nq / QW + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
-                               p2, b, n1, n2, dists, idx64, idx32, nn, k);
-        } else {
-            hipLaunchKernelGGL((knn3_kernel<K, 1>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1,
-                               p2, b, n1, n2, dists, idx64, idx32, nn, k);
-        }
+        hipLaunchKernelGGL((knn3_kernel<K, 1>), dim3((nq + WAVES - 1) / WAVES), dim3(256), 0, st, p1, p2, b,
+                           n1, n2, dists, idx64, idx32, nn, k);
     } else if (dim % 4 == 0 && !((reinterpret_cast<uintptr_t>(p1) | reinterpret_cast<uintptr_t>(p2)) & 15)) {
-        if (HREG_KNND_QW > 1 && n1 % HREG_KNND_QW == 0) {
-            constexpr int QW = HREG_KNND_QW;
+        if (n1 % KNND_QW == 0) {
+            constexpr int QW = KNND_QW;
             hipLaunchKernelGGL((knnd_wave_kernel<K, QW>), dim3((nq / QW + WAVES - 1) / WAVES), dim3(256), 0, st,
                                p1, p2, b, n1, n2, dim, dists, idx64, idx32, nn, k);
         } else {
@@ -902,14 +846,11 @@ extern "C" int hreg_spatial_index(const float *p, int nb, int n, void *ws, void 
     float4 *spts = static_cast<float4 *>(ws);
     float4 *boxes = spts + (size_t)nb * np;
     if (n > SI_LDSN)
-        hipLaunchKernelGGL(spatial_index_kernel<true>, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream),
-                           p, n, spts, boxes);
-    else if (HREG_SI_MORTON)
+        hipLaunchKernelGGL(spatial_index_kernel, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream), p, n, spts,
+                           boxes);
+    else
         hipLaunchKernelGGL(spatial_index_morton_kernel, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream), p, n,
                            spts, boxes);
-    else
-        hipLaunchKernelGGL(spatial_index_kernel<false>, dim3(nb), dim3(SI_THREADS), 0, as_stream(stream),
-                           p, n, spts, boxes);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -926,18 +867,18 @@ extern "C" int hreg_knn_group_indexed(const float *q, const float *p, const void
     const float4 *boxes = spts + (size_t)nb * np;
     hipStream_t st = as_stream(stream);
     dim3 grid((nb * m + WAVES - 1) / WAVES);
-#define HREG_KGI(KK)                                                                              \
+#define KGI_CASE(KK)                                                                              \
     if (n > SI_LDSN)                                                                              \
         hipLaunchKernelGGL((knn_group_indexed_kernel<KK, SI_MAXN / 4096>), grid, dim3(256), 0, st, q, \
                            p, spts, boxes, nb, m, n, k, gidx, geom, knn_xyz);                      \
     else                                                                                          \
         hipLaunchKernelGGL((knn_group_indexed_kernel<KK, SI_LDSN / 4096>), grid, dim3(256), 0, st, q, \
                            p, spts, boxes, nb, m, n, k, gidx, geom, knn_xyz)
-    if (k <= 8) { HREG_KGI(8); }
-    else if (k <= 16) { HREG_KGI(16); }
-    else if (k <= 32) { HREG_KGI(32); }
-    else { HREG_KGI(64); }
-#undef HREG_KGI
+    if (k <= 8) { KGI_CASE(8); }
+    else if (k <= 16) { KGI_CASE(16); }
+    else if (k <= 32) { KGI_CASE(32); }
+    else { KGI_CASE(64); }
+#undef KGI_CASE
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }
@@ -948,22 +889,14 @@ extern "C" int hreg_knn_group(const float *q, const float *p, int nb, int m, int
     if (k > 64) return HREG_ERR_UNSUPPORTED;
     if (nb == 0 || m == 0) return HREG_OK;
     hipStream_t st = as_stream(stream);
-    const bool multi = HREG_KNN3_QW > 1 && m % HREG_KNN3_QW == 0;
-    dim3 grid(multi ? (nb * m / HREG_KNN3_QW + WAVES - 1) / WAVES : (nb * m + WAVES - 1) / WAVES);
-#define HREG_KG(KK)                                                                                          \
-    do {                                                                                                    \
-        if (multi)                                                                                          \
-            hipLaunchKernelGGL((knn_group_kernel<KK, HREG_KNN3_QW>), grid, dim3(256), 0, st, q, p, nb, m, n,  \
-                               k, gidx, geom, knn_xyz);                                                     \
-        else                                                                                                \
-            hipLaunchKernelGGL((knn_group_kernel<KK, 1>), grid, dim3(256), 0, st, q, p, nb, m, n, k, gidx,   \
-                               geom, knn_xyz);                                                              \
-    } while (0)
-    if (k <= 8) HREG_KG(8);
-    else if (k <= 16) HREG_KG(16);
-    else if (k <= 32) HREG_KG(32);
-    else HREG_KG(64);
-#undef HREG_KG
+    dim3 grid((nb * m + WAVES - 1) / WAVES);
+#define KG_CASE(KK) \
+    hipLaunchKernelGGL((knn_group_kernel<KK, 1>), grid, dim3(256), 0, st, q, p, nb, m, n, k, gidx, geom, knn_xyz)
+    if (k <= 8) KG_CASE(8);
+    else if (k <= 16) KG_CASE(16);
+    else if (k <= 32) KG_CASE(32);
+    else KG_CASE(64);
+#undef KG_CASE
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

@@ -297,14 +297,11 @@ __device__ __forceinline__ void ld6(const gu32x4 *__restrict__ wt, int f, int la
     for (int p = 0; p < 3; ++p) o[p] = fp[p * 64 + lane];
 }
 
-// Software-pipelined split (HREG_SWP, default on): chunk c + 1's B operand is split into its
-// pieces while chunk c's MFMAs run, the scheduler asked (sched_group_barrier) to place
-// about NVALU / NMFMA VALU instructions after each MFMA -- an MFMA holds the SIMD's vector
-// issue for 8 of its 32 cycles, so ~5 independent VALU per 32x32x16 MFMA issue in its
-// shadow instead of as a 44-instruction block between two MFMAs.
-#ifndef HREG_SWP
-#define HREG_SWP 1
-#endif
+// Software-pipelined split: chunk c + 1's B operand is split into its pieces while chunk c's
+// MFMAs run, the scheduler asked (sched_group_barrier) to place about NVALU / NMFMA VALU
+// instructions after each MFMA -- an MFMA holds the SIMD's vector issue for 8 of its 32 cycles,
+// so ~5 independent VALU per 32x32x16 MFMA issue in its shadow instead of as a 44-instruction
+// block between two MFMAs (measured neutral, +-2 %, r2; kept).
 
 template <int NMFMA, int NVALU>
 __device__ __forceinline__ void interleave_mfma_valu() {
@@ -343,10 +340,9 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
 #pragma unroll
             for (int p = 0; p < 3; ++p) rb[co][p] = cin[co][p];
         u32x4 bs[2][3];
-        if constexpr (HREG_SWP) split_chunk(bval, 0, bs[0]);
+        split_chunk(bval, 0, bs[0]);
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
-            if constexpr (!HREG_SWP) split_chunk(bval, c, bs[c & 1]);
 #pragma unroll
             for (int co = 0; co < COUT_T; ++co) {
                 acc[co] = mma6(rb[co], bs[c & 1], acc[co]);
@@ -354,14 +350,11 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
                     ld6(wt, f.base + co * f.stride + c + 1, lane, rb[co]);
                 else if (co < NCOUT)
                     ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
-                if constexpr (!HREG_SWP) __builtin_amdgcn_sched_barrier(0);
             }
-            if constexpr (HREG_SWP) {
-                if (c + 1 < NCH) {
-                    split_chunk(bval, c + 1, bs[(c + 1) & 1]);
-                    interleave_mfma_valu<6 * COUT_T, 48>();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+            if (c + 1 < NCH) {
+                split_chunk(bval, c + 1, bs[(c + 1) & 1]);
+                interleave_mfma_valu<6 * COUT_T, 48>();
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
 #pragma unroll
@@ -374,7 +367,7 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
 #pragma unroll
         for (int p = 0; p < 3; ++p) buf[0][co][p] = cin[co][p];
     u32x4 bs[2][3];
-    if constexpr (HREG_SWP) split_chunk(bval, 0, bs[0]);
+    split_chunk(bval, 0, bs[0]);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         if (c + 1 < NCH) {
@@ -384,23 +377,20 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
 #pragma unroll
             for (int co = 0; co < NCOUT; ++co) ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
         }
-        if constexpr (!HREG_SWP) split_chunk(bval, c, bs[c & 1]);
 #pragma unroll
         for (int co = 0; co < COUT_T; ++co) acc[co] = mma6(buf[c & 1][co], bs[c & 1], acc[co]);
-        if constexpr (HREG_SWP) {
-            if (c + 1 < NCH) {
-                split_chunk(bval, c + 1, bs[(c + 1) & 1]);
-                interleave_mfma_valu<6 * COUT_T, 48>();
-            }
+        if (c + 1 < NCH) {
+            split_chunk(bval, c + 1, bs[(c + 1) & 1]);
+            interleave_mfma_valu<6 * COUT_T, 48>();
         }
-        // HREG_SWP: no barrier after the last chunk -- the next call's ReLU + first split
-        // (which waits only for tile 0's result) may issue under this chunk's last MFMAs
-        if (!HREG_SWP || c + 1 < NCH) __builtin_amdgcn_sched_barrier(0);
+        // no barrier after the last chunk -- the next call's ReLU + first split (which waits
+        // only for tile 0's result) may issue under this chunk's last MFMAs
+        if (c + 1 < NCH) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // ------------------------------------------------------------------------
-// Workgroup-shared weight stream (group_fused6.hip, HREG_RING): the 4 waves of a workgroup
+// Workgroup-shared weight stream (group_fused6.hip, level 2): the 4 waves of a workgroup
 // run the same chunk sequence on different row tiles, so each step's weight pieces are
 // brought into LDS ONCE per workgroup by LDS-DMA (global_load_lds_dwordx4, the 3 x NCO
 // pieces of a step spread over the waves) and every wave reads them with ds_read_b128 --
@@ -411,14 +401,8 @@ __device__ __forceinline__ void mfma_pipe6(const gu32x4 *__restrict__ wt, int la
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
 
-// HREG_RING_SWP: chunk c + 1's B split in the shadow of tile 0's MFMAs of chunk c
-#ifndef HREG_RING_SWP
-#define HREG_RING_SWP 0
-#endif
-// pieces of tile co + 1 read while tile co's MFMAs run (2) or right before them (1)
-#ifndef HREG_RING_ABUF
-#define HREG_RING_ABUF 2
-#endif
+// (measured neutral and removed, r2: chunk c + 1's B split in the shadow of tile 0's MFMAs of
+// chunk c; tile co + 1's pieces read right before its MFMAs instead of under tile co's)
 
 template <int SLOT_TILES, int NWAVES>
 struct Ring6 {
@@ -453,8 +437,7 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
                                            f32x16 (&acc)[COUT_T], const u32x4 (&)[CARRY6][3], FragSeq nf,
                                            u32x4 (&)[CARRY6][3]) {
     static_assert(NWV == 4, "4 waves share the stream");
-    u32x4 b[3], bn[3];
-    (void)bn;
+    u32x4 b[3];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of this step landed
@@ -464,7 +447,7 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
             ring_fill<COUT_T>(ring, cur ^ 1, f, c + 1, lane);
         else
             ring_fill<NCOUT>(ring, cur ^ 1, nf, 0, lane);
-        if (!HREG_RING_SWP || c == 0) split_chunk(bval, c, b);
+        split_chunk(bval, c, b);
         const lds_cu32x4 *sp = ring.lds + cur * Ring6<ST, NWV>::SLOT + lane;
         // tile co + 1's pieces are read while tile co's six MFMAs run (one tile of pieces
         // in flight: 12 VGPRs, not the whole step's)
@@ -473,21 +456,12 @@ __device__ __forceinline__ void mfma_pipe6(Ring6<ST, NWV> &ring, int lane, FragS
         for (int p = 0; p < 3; ++p) a[0][p] = sp[p * 64];
 #pragma unroll
         for (int co = 0; co < COUT_T; ++co) {
-            if (HREG_RING_ABUF == 1 && co > 0) {
-#pragma unroll
-                for (int p = 0; p < 3; ++p) a[co & 1][p] = sp[(co * 3 + p) * 64];
-            }
-            if (HREG_RING_ABUF == 2 && co + 1 < COUT_T) {
+            if (co + 1 < COUT_T) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) a[(co + 1) & 1][p] = sp[((co + 1) * 3 + p) * 64];
             }
             acc[co] = mma6(a[co & 1], b, acc[co]);
-            if (HREG_RING_SWP && co == 0 && c + 1 < NCH) split_chunk(bval, c + 1, bn);  // under tile 0's MFMAs
             __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (HREG_RING_SWP) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p) b[p] = bn[p];
         }
         ++ring.step;
     }

@@ -48,7 +48,7 @@ __device__ __forceinline__ void pipe6_jt(WP wt, int lane, FragSeq f, BVal bval,
         }
     };
     u32x4 b[2][NB][3];
-    if constexpr (HREG_SWP) split_jt(0, b[0]);
+    split_jt(0, b[0]);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         if (c + 1 < NCH) {
@@ -58,24 +58,19 @@ __device__ __forceinline__ void pipe6_jt(WP wt, int lane, FragSeq f, BVal bval,
 #pragma unroll
             for (int co = 0; co < NCOUT; ++co) ld6(wt, nf.base + co * nf.stride, lane, cout[co]);
         }
-#ifdef HREG_PIN_PREFETCH
-        // keep the prefetch ahead of this chunk's MFMAs (LDS-resident tables: the compiler
-        // otherwise sinks each ds_read next to its MFMA)
+        // keep the prefetch ahead of this chunk's MFMAs (LDS-resident tables, group_l1_6.hip: the
+        // compiler otherwise sinks each ds_read next to its MFMA, 260 vs 173 us)
         if constexpr (is_lds_table<WP>::value) __builtin_amdgcn_sched_barrier(0);
-#endif
-        if constexpr (!HREG_SWP) split_jt(c, b[c & 1]);
 #pragma unroll
         for (int co = 0; co < COUT_T; ++co)
 #pragma unroll
             for (int jt = 0; jt < NJ; ++jt)
                 acc[co][jt] = mma6(buf[c & 1][co], b[c & 1][SAMEB ? 0 : jt], acc[co][jt]);
-        if constexpr (HREG_SWP) {
-            if (c + 1 < NCH) {  // next chunk's split in this chunk's MFMA shadow (mfma_chain.h)
-                split_jt(c + 1, b[(c + 1) & 1]);
-                interleave_mfma_valu<6 * COUT_T * NJ, 48 * NB>();
-            }
+        if (c + 1 < NCH) {  // next chunk's split in this chunk's MFMA shadow (mfma_chain.h)
+            split_jt(c + 1, b[(c + 1) & 1]);
+            interleave_mfma_valu<6 * COUT_T * NJ, 48 * NB>();
+            __builtin_amdgcn_sched_barrier(0);
         }
-        if (!HREG_SWP || c + 1 < NCH) __builtin_amdgcn_sched_barrier(0);
     }
 }
 

@@ -170,16 +170,13 @@ __global__ __launch_bounds__(K::THREADS) void mlp_head_kernel(const float *__res
     }
 }
 
-// HREG_HEAD_JT (bf16x6 only): one workgroup of CW waves owns JT row tiles at once and every
+// bf16x6 heads: one workgroup of CW waves owns JT row tiles at once and every
 // wave multiplies each chunk of weight pieces it streams from L2 into all JT row tiles
 // (split_chain.h pipe_lds6_jt), so a head moves JT x fewer weight bytes per MFMA -- the
 // pieces of a C = 512 head are 3 MB per pass, and that stream, not the matrix cores, set
 // the kernel's CU time.  Per row the arithmetic is the JT = 1 kernel's, in the same order,
 // whatever row tiles share a workgroup (test_gpu_model.py: a pair alone and inside a batch,
-// ragged row-tile counts).
-#ifndef HREG_HEAD_JT
-#define HREG_HEAD_JT 1
-#endif
+// ragged row-tile counts).  CU time -16 %, bench +1 % (r4).
 
 template <int C> struct HeadJT { static constexpr int v = C >= 256 ? 2 : 4; };
 
@@ -233,7 +230,7 @@ __global__ __launch_bounds__(K::CW * 64) void mlp_head6_jt_kernel(const float *_
 #pragma unroll
                 for (int jt = 0; jt < JT; ++jt) y[i][jt] = b[i];
         }
-        pipe_lds6_jt<NCH, P, P, JT>(wt, lane, g1, xb, y, carry6, g2, ca6);
+        pipe_lds6_jt<NCH, P, P, JT, false>(wt, lane, g1, xb, y, carry6, g2, ca6);
 #pragma unroll
         for (int i = 0; i < P; ++i) relu_tiles(y[i]);
         tile_sync();  // every wave has read x from sA
@@ -251,7 +248,7 @@ __global__ __launch_bounds__(K::CW * 64) void mlp_head6_jt_kernel(const float *_
 #pragma unroll
                 for (int jt = 0; jt < JT; ++jt) y[i][jt] = b[i];
         }
-        pipe_lds6_jt<NCH, P, P, JT>(wt, lane, g2, xb, y, ca6, g1, carry6);
+        pipe_lds6_jt<NCH, P, P, JT, false>(wt, lane, g2, xb, y, ca6, g1, carry6);
 #pragma unroll
         for (int i = 0; i < P; ++i) relu_tiles(y[i]);
 
@@ -295,7 +292,7 @@ int launch_head(const float *table, const float *x, int ldx, int G, int mode, fl
                 int row_tiles = 0) {
     const int NT = G / 32;
     if (B6 && (reinterpret_cast<uintptr_t>(table) & 15)) return HREG_ERR_INVALID;
-    if constexpr (B6 && HREG_HEAD_JT) {
+    if constexpr (B6) {
         constexpr int JT = HeadJT<K::C>::v;
         const int jt = row_tiles == 1 ? 1 : JT;
         int grid = (NT + jt - 1) / jt;

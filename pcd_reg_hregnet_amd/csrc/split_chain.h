@@ -136,14 +136,11 @@ __device__ __forceinline__ void pipe_lds6(const gu32x4 *__restrict__ wt, int lan
     }
 }
 
-// HREG_SPLIT_SWP: pipe_lds6_jt splits chunk c + 1's B under chunk c's MFMAs
-#ifndef HREG_SPLIT_SWP
-#define HREG_SPLIT_SWP 0
-#endif
-
 // pipe_lds6 over JT row tiles: each chunk's weight pieces (P tiles) feed the MFMAs of
-// every row tile (JT x fewer weight bytes per MFMA); B of row tile jt through bl(jt, st0, v)
-template <int NCH, int P, int NP, int JT, class BL>
+// every row tile (JT x fewer weight bytes per MFMA); B of row tile jt through bl(jt, st0, v).
+// SWP: chunk c + 1's B split under chunk c's MFMAs (r5: the CoarseReg / FineReg / neighbour
+// heads 127.8 / 56.4 / 66.4 -> 123.5 / 54.2 / 64.4 us; level 3 174 -> 175, so not there).
+template <int NCH, int P, int NP, int JT, bool SWP, class BL>
 __device__ __forceinline__ void pipe_lds6_jt(const gu32x4 *__restrict__ wt, int lane, FragSeq f, BL bl,
                                              f32x16 (&acc)[P][JT], const Carry6 &cin, FragSeq nf, Carry6 &cout) {
     static_assert(P <= CARRY6 && NP <= CARRY6, "carry");
@@ -166,8 +163,8 @@ __device__ __forceinline__ void pipe_lds6_jt(const gu32x4 *__restrict__ wt, int 
         }
     };
     ldb(0, bb[0]);
-    if constexpr (HREG_SPLIT_SWP) {
-        // chunk c + 1's B split in chunk c's MFMA shadow (mfma_chain.h HREG_SWP), the VALU
+    if constexpr (SWP) {
+        // chunk c + 1's B split in chunk c's MFMA shadow (mfma_chain.h), the VALU
         // placed between the MFMAs by sched_group_barrier
         u32x4 bs[2][JT][3];
 #pragma unroll
@@ -213,88 +210,6 @@ __device__ __forceinline__ void pipe_lds6_jt(const gu32x4 *__restrict__ wt, int 
             for (int i = 0; i < P; ++i) acc[i][jt] = mma6(abuf[c & 1][i], b, acc[i][jt]);
         }
         __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// ------------------------------------------------------------------------
-// Channel-split form of the workgroup-shared weight stream (mfma_chain.h Ring6;
-// group_split6.hip HREG_SPLIT_RING): the workgroup holds RT row tiles x NCW channel
-// groups of waves; a step's slot holds the pieces of EVERY channel group's P tiles
-// ([cw][co][p] x 64 lanes x 16 B), brought in once by LDS-DMA spread over all the waves, so
-// the RT waves of one channel group (different row tiles) share them.  Every wave runs the
-// same steps; fragment sequences of different channel groups differ by P x stride (the
-// channel group's first tile).
-template <int SLOT_TILES, int NWAVES, int NCW>
-struct RingCW {
-    static constexpr int SLOT = SLOT_TILES * 192, NW = NWAVES, CW = NCW;
-    const gu32x4 *wt;  // the table (global)
-    lds_u32x4 *lds;    // 2 slots
-    int step, w, cw;   // uniform: steps so far, wave index, this wave's channel group
-};
-
-// the pieces of chunk c of NCO tiles of every channel group into slot `slot`; f0: channel
-// group 0's sequence, cws: the fragment offset between channel groups
-template <int NCO, class R>
-__device__ __forceinline__ void ring_fill_cw(R &ring, int slot, FragSeq f0, int cws, int c, int lane) {
-    constexpr int NP = 3 * NCO * R::CW;
-    static_assert(NCO * R::CW * 192 <= R::SLOT, "slot");
-#pragma unroll
-    for (int i0 = 0; i0 < NP; i0 += R::NW) {
-        const int i = i0 + ring.w;  // piece (cw * NCO + co) * 3 + p
-        if (i < NP) {
-            const int q = i / 3, p = i - 3 * q, g = q / NCO, co = q - g * NCO;
-            const gu32x4 *src = ring.wt + (f0.base + g * cws + co * f0.stride + c) * 192 + p * 64 + lane;
-#if __HIP_DEVICE_COMPILE__  // (the gfx950 builtin does not exist in the host pass)
-            __builtin_amdgcn_global_load_lds(src, ring.lds + slot * R::SLOT + i * 64, 16, 0, 0);
-#else
-            (void)src;
-#endif
-        }
-    }
-}
-
-// pipe_lds6 on the ring (same arguments; the carries are unused: the ring's next slot holds
-// the next call's first chunk).  B of chunk c is read from LDS after the step's barrier.
-template <int NCH, int P, int NP, class BL, int ST, int NWV, int NCW>
-__device__ __forceinline__ void pipe_lds6(RingCW<ST, NWV, NCW> &ring, int lane, FragSeq f, BL bl,
-                                          f32x16 (&acc)[P], const Carry6 &, FragSeq nf, Carry6 &) {
-    const FragSeq f0{f.base - ring.cw * P * f.stride, f.stride};
-    const FragSeq nf0{nf.base - ring.cw * NP * nf.stride, nf.stride};
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of this step landed
-        __syncthreads();
-        const int cur = ring.step & 1;
-        if (c + 1 < NCH)
-            ring_fill_cw<P>(ring, cur ^ 1, f0, P * f.stride, c + 1, lane);
-        else
-            ring_fill_cw<NP>(ring, cur ^ 1, nf0, NP * nf.stride, 0, lane);
-        float x[8];
-        {
-            float v[4];
-            bl(8 * c, v);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) x[k] = v[k];
-            bl(8 * c + 4, v);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) x[4 + k] = v[k];
-        }
-        u32x4 b[3];
-        split8(x, b);
-        const lds_cu32x4 *sp = ring.lds + cur * RingCW<ST, NWV, NCW>::SLOT + ring.cw * P * 192 + lane;
-        u32x4 a[2][3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) a[0][p] = sp[p * 64];
-#pragma unroll
-        for (int co = 0; co < P; ++co) {
-            if (co + 1 < P) {
-#pragma unroll
-                for (int p = 0; p < 3; ++p) a[(co + 1) & 1][p] = sp[((co + 1) * 3 + p) * 64];
-            }
-            acc[co] = mma6(a[co & 1], b, acc[co]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        ++ring.step;
     }
 }
 

@@ -275,18 +275,18 @@ int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans
     if (lds > TS_LDS_FLOATS * sizeof(float)) return -HREG_ERR_UNSUPPORTED;  // (ts_nt's budget)
     const bool tail = (K & 15) != 0, full = scale != nullptr || relu;
     if (STATS && full) return -HREG_ERR_UNSUPPORTED;
-#define HREG_TS(NTT, TT, FF)                                                                                   \
+#define TS_CASE(NTT, TT, FF)                                                                                   \
     if (nt == NTT && tail == TT && full == FF) {                                                              \
         hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF, STATS>), dim3(gx, gy), dim3(256), lds, st, A, lda, R, K, \
                            W, w_trans, N, scale, shift, relu, out, ldo, part);                                 \
         if (hipGetLastError() != hipSuccess) return -HREG_ERR_LAUNCH;                                          \
         return gx;                                                                                             \
     }
-#define HREG_TS_NT(NTT) HREG_TS(NTT, false, false) HREG_TS(NTT, true, false)                           \
-    if constexpr (!STATS) { HREG_TS(NTT, false, true) HREG_TS(NTT, true, true) }
-    HREG_TS_NT(1) HREG_TS_NT(2) HREG_TS_NT(4) HREG_TS_NT(8)
-#undef HREG_TS_NT
-#undef HREG_TS
+#define TS_NT_CASE(NTT) TS_CASE(NTT, false, false) TS_CASE(NTT, true, false)                           \
+    if constexpr (!STATS) { TS_CASE(NTT, false, true) TS_CASE(NTT, true, true) }
+    TS_NT_CASE(1) TS_NT_CASE(2) TS_NT_CASE(4) TS_NT_CASE(8)
+#undef TS_NT_CASE
+#undef TS_CASE
     return -HREG_ERR_UNSUPPORTED;
 }
 

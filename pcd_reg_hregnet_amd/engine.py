@@ -35,40 +35,59 @@ LEVELS = (
     (256, 16, 128, (128, 128, 256), (128, 128, 256), 256),
 )
 K_HEAD = 8  # CoarseReg/FineReg k (models.py:71-73)
+# ---- the product path's kernel forms.  Plain attributes: the defaults ARE the product path; the
+# alternatives are test checkers (the layer-by-layer GEMM paths, the fp32-MFMA twins in
+# libhregnet_checkers.so, the unsplit / unfused forms), set by tests with monkeypatch.
 FUSED_L1 = True  # level 1 through the fused group_l1 kernel (False: layer-by-layer GEMMs)
 FUSED_L2 = True  # level 2 through the fused group_fused kernel (k = 32)
 FUSED_L3 = True  # level 3 through the fused group_fused kernel (k = 16)
-# levels 2 / 3 on the channel-split kernel (group_split.hip) instead of the
-# accumulator-chained one (group_fused.hip); measured per level (tools/group_bench.py)
-SPLIT_L2 = switches.flag("SPLIT_L2", False)
-SPLIT_L3 = switches.flag("SPLIT_L3", True)
-# level 3 on the two-row-tile form of the channel-split kernel (hreg_group_split6j_l3)
-SPLIT_JT = True
-# level 3 on the pieces form (hreg_group_split6p_l3: activations split into bf16 pieces once by
-# their producer and stored in LDS as pieces; 8-wave workgroups; group_split6.hip)
-L3_PIECES = switches.flag("L3_PIECES", False)
+# levels 2 / 3 on the channel-split kernel (group_split6.hip) instead of the accumulator-chained
+# one (group_fused6.hip); measured per level (r2-r3: level 3 split, level 2 chained + LDS ring)
+SPLIT_L2 = False
+SPLIT_L3 = True
+SPLIT_JT = True  # level 3 on the two-row-tile form of the channel-split kernel (hreg_group_split6j_l3)
 # 32-row tiles per workgroup of the channel-split FineReg / neighbour heads (0: the library's
 # default, two at N1 <= 256; hreg_corr_head6x / hreg_nbr_head6sx)
 HEAD_ROW_TILES = 0
-# the accumulator-chained level kernels on the bf16 matrix cores at fp32 accuracy
-# (bf16x6 split products, group_fused6.hip) instead of v_mfma_f32_32x32x2_f32
-B6_L2 = switches.flag("B6_L2", True)
-# level 2 on the pair form of the bf16x6 kernel (two groups per wave: half the weight
-# bytes streamed per row, hreg_group6x2_l2).  Off: at one wave per SIMD it measured level
-# with the one-group kernel (183 vs 184 us; tools/b6_experiment.py: 180 vs 182 us)
-PAIR_L2 = switches.flag("PAIR_L2", False)
-# GraphPipeline: level-1 stage of all lanes as one batched launch per kernel (one side
-# stream) instead of one per lane
+# the fused kernels on the bf16 matrix cores at fp32 accuracy (bf16x6 split products) instead of
+# their v_mfma_f32_32x32x2_f32 twins (checkers)
+B6_L1 = B6_L2 = B6_L3 = True
+B6_GEMM = True  # the big plain GEMMs (CoarseReg convs_1 layers 2-3) on hreg_gemm6
+B6_MLP = True  # mlp heads on hreg_mlp_head6
+B6_HEADS = True  # FineReg / CoarseReg-neighbour heads (group_head.hip *_head6_kernel)
+FUSED_COARSE = True  # CoarseReg convs_1 (split first layer) + attention in one launch (coarse6.hip)
+SPLIT_FINE = True  # FineReg heads on coarse6.hip's channel-split correspondence kernel
+SPLIT_NBR = True  # the neighbour branch likewise
+FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
+FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
+FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip)
+# CoarseReg convs_1[0] as [small] GEMM + per-keypoint desc / knn_desc products added in the
+# epilogue (distributivity over the concatenation, layers.py:364-384; False: one 528-deep GEMM)
+COARSE_SPLIT = True
+# the same for the fused FineReg heads (descriptor blocks of convs_1[0]) and the CoarseReg
+# neighbour branch (descriptor block of convs_2[0]): per-point products precomputed, the
+# fused kernels multiply only the small / geometry columns per row
+HEAD_PRE = True
+# levels 2 / 3: the feature blocks of the detector's and the descriptor's first conv,
+# W_f f per level-(l-1) feature row, precomputed once (one GEMM) instead of once per
+# grouped row (k = 32 / 16 rows gather each feature row)
+LEVEL_PRE = True
+# level 1 with its weight table resident in LDS (hreg_group_l1_6) for clouds up to this many
+# points; above, the global-table form (hreg_group_l1_6g): r2, beside Model_V2's cluster FPS on
+# every CU the 92 KB LDS claim waited for it (942 vs 856 pairs/s)
+L1_LDS_MAX_N = 16384
+
+# ---- executor switches (HREG_SWITCHES, whole-process A/B of the measured choices)
+# GraphPipeline: level-1 stage of all lanes as one batched launch per kernel (one side stream)
+# instead of one per lane (r2: 5424 -> 6213 pairs/s)
 BATCH_STAGE1 = switches.flag("BATCH_STAGE1", True)
 V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", True)  # GraphPipeline(v2=True): see bs1
-V2_FRONT_STREAM = switches.flag("V2_FRONT_STREAM", False)  # GraphPipeline(v2=True): front streaming
-FRONT_STREAM = switches.flag("FRONT_STREAM", True)  # GraphPipeline: halves of a forward in consecutive rounds
-FRONT_ORDER = switches.integer("FRONT_ORDER", 3)  # per lane: 0 back then front, 1 front then back, 2 by lane parity, 3 on two streams
-# front streaming pays for a round's tail; with many lanes the tail is a small part of the round
-# (measured, 3 paired lines each: 20 lanes 7084 -> 7141 pairs/s with order 0, -> 7311 with
-# order 3; 48 lanes 7456 -> 7417 / 7388)
-FRONT_STREAM_MAX_LANES = switches.integer("FRONT_STREAM_MAX_LANES", 24)
-FRONT_FOREACH = switches.flag("FRONT_FOREACH", True)  # front outputs -> static buffers: one foreach copy
+# GraphPipeline: halves of a forward in consecutive rounds, the two halves of a lane on two
+# streams (r4: 20 lanes 7084 -> 7311 pairs/s; off above FRONT_STREAM_MAX_LANES: 48 lanes 7456 ->
+# 7388; off for Model_V2)
+FRONT_STREAM = switches.flag("FRONT_STREAM", True)
+FRONT_STREAM_MAX_LANES = 24
+V2_FRONT_STREAM = switches.flag("V2_FRONT_STREAM", False)  # (Model_V2: front streaming, r6 A/B)
 # Single-batch latency (one forward alone on the GPU is one dependent chain of ~50 kernels): work
 # that does not depend on the chain's previous kernel runs beside it on a side stream -- the
 # level-1 spatial index (input points only) beside the level-1 FPS, the level-2/3 input
@@ -78,55 +97,18 @@ FRONT_FOREACH = switches.flag("FRONT_FOREACH", True)  # front outputs -> static 
 # chain_fork() enables it (the 1-lane GraphPipeline and bench.py's eager latency figure): with
 # many lanes in flight the chip is already full and a fork only adds streams.
 CHAIN_FORK = switches.flag("CHAIN_FORK", True)
-# Level-1 FPS over the spatial index's Morton-sorted copy with exact group pruning
-# (fps.hip fps_sorted_kernel, hreg_fps_indexed): the index is built first and the FPS skips the
-# 256-point groups its new centre cannot change; the same selections.  Clouds of FPS_SORTED_N.
+# Level-1 FPS over the spatial index's sorted copy with exact pruning (hreg_fps_indexed): the
+# index is built first and the FPS skips the point groups its new centre cannot change; the same
+# selections.  Clouds of FPS_SORTED_N points (fps.hip fps_sorted_kernel: points in registers) and,
+# r6, 16384 < n <= 65536 with n % 64 == 0 (fps_blocks_kernel: Model_V2's 65536-point clouds on ONE
+# workgroup each instead of the cluster kernel's 32 spinning single-wave participants).
 FPS_SORTED = switches.flag("FPS_SORTED", True)
 FPS_SORTED_N = 16384
-# timing probe (tools only): the level-1 grouping into preallocated buffers skips its FPS (1), its
-# spatial index + kNN (2) or its spatial index (3), leaving the buffers' previous values (static
-# inputs: unchanged)
-PROBE_S1_SKIP = switches.integer("PROBE_S1_SKIP", 0)
-# timing probe (tools only): rounds without the streamed batched stage 1 of the next round
-PROBE_NO_S1 = switches.flag("PROBE_NO_S1", False)
-B6_L1 = switches.flag("B6_L1", True)  # group_l1_6.hip for level 1
-# level 3 (and level 2 when SPLIT_L2) on the channel-split kernel with bf16x6 products
-# (group_split6.hip)
-B6_L3 = switches.flag("B6_L3", True)
-# the big plain GEMMs (CoarseReg convs_1 layers 2-3, 512 -> 512 over B*256*8 rows) on
-# hreg_gemm6 (bf16x6 products)
-B6_GEMM = switches.flag("B6_GEMM", True)
-# every addend-free GEMM (the precomputed first-layer blocks, the batched descriptor
-# products, the cosine similarities) on hreg_gemm6 (bf16x6, 128 x 128 tiles)
-B6_MLP = switches.flag("B6_MLP", True)  # mlp heads on hreg_mlp_head6
-# CoarseReg convs_1 (split first layer) + attention in one launch (coarse6.hip, bf16x6)
-FUSED_COARSE = switches.flag("FUSED_COARSE", True)
-# the FineReg / CoarseReg-neighbour head kernels on bf16x6 (group_head.hip *_head6_kernel;
-# precomputed-block form, HEAD_PRE)
-B6_HEADS = switches.flag("B6_HEADS", True)
-# the FineReg heads on coarse6.hip's channel-split correspondence kernel (hreg_corr_head6:
-# N1/64 waves of two output tiles, activations through LDS, ~136 VGPRs) instead of the
-# register-chained fine_head6_kernel (one wave per SIMD at N1 = 256)
-# level 1 with its weight table resident in LDS (hreg_group_l1_6) for clouds up to this many
-# points; above, the cluster FPS co-runs on every CU and the 92 KB LDS claim would wait for
-# it, so the global-table form (hreg_group_l1_6g) runs: Model_V2 942 vs 856 pairs/s
-L1_LDS_MAX_N = switches.integer("L1_LDS_MAX_N", 16384)
-SPLIT_FINE = switches.flag("SPLIT_FINE", True)
-SPLIT_NBR = switches.flag("SPLIT_NBR", True)  # the neighbour branch likewise
-FUSED_FINE = True  # FineReg convs_1 + attention through group_head.hip
-FUSED_NBR = True  # CoarseReg neighbour branch (convs_2 + attention) through group_head.hip
-FUSED_HEAD = True  # mlp1 -> mlp2 -> mlp3 heads in one launch each (mlp_head.hip)
-# CoarseReg convs_1[0] as [small] GEMM + per-keypoint desc / knn_desc products added in the
-# epilogue (distributivity over the concatenation, layers.py:364-384; False: one 528-deep GEMM)
-COARSE_SPLIT = switches.flag("COARSE_SPLIT", True)
-# the same for the fused FineReg heads (descriptor blocks of convs_1[0]) and the CoarseReg
-# neighbour branch (descriptor block of convs_2[0]): per-point products precomputed, the
-# fused kernels multiply only the small / geometry columns per row
-HEAD_PRE = switches.flag("HEAD_PRE", True)
-# levels 2 / 3: the feature blocks of the detector's and the descriptor's first conv,
-# W_f f per level-(l-1) feature row, precomputed once (one GEMM) instead of once per
-# grouped row (k = 32 / 16 rows gather each feature row)
-LEVEL_PRE = switches.flag("LEVEL_PRE", True)
+
+
+def fps_indexed_ok(n: int) -> bool:
+    """clouds of n points that hreg_fps_indexed's pruned kernels take"""
+    return n == FPS_SORTED_N or (FPS_SORTED_N < n <= 65536 and n % 64 == 0)
 
 
 @dataclass
@@ -631,8 +613,6 @@ def gemm(segs, lin: Lin, R: int, out: torch.Tensor | None = None, adds=(), b6=Fa
     if out is None:
         out = torch.empty((R, lin.N), device=lin.W.device, dtype=torch.float32)
     g = _gemm_struct(segs, lin, R, out, adds)
-    if PROBE_SKIP_GEMM:
-        return out
     if b6 and B6_GEMM and not adds:
         _lib.gemm6(g)
     else:
@@ -699,8 +679,7 @@ def _batched_desc_struct(lin: Lin, desc3, rows: int, C: int, out) -> Gemm:
 
 def cosine_gemm(a, b, na, nb_, nb: int, n1: int, n2: int, C: int, out):
     """S[b][i][j] = <a_i, b_j> / (|a_i||b_j| + 1e-6) per pair (layers.py:29-41)."""
-    if not PROBE_SKIP_GEMM:
-        _lib.gemm(_cosine_struct(a, b, na, nb_, nb, n1, n2, C, out))
+    _lib.gemm(_cosine_struct(a, b, na, nb_, nb, n1, n2, C, out))
     return out
 
 
@@ -825,7 +804,7 @@ def fps(xyz, npoint, weights=None, out=None, concurrent=0):
 
 
 def fps_indexed(xyz, npoint, ws, out=None):
-    """FPS of nb clouds of FPS_SORTED_N points over their spatial index in ws (hreg_spatial_index
+    """FPS of nb clouds (fps_indexed_ok sizes) over their spatial index in ws (hreg_spatial_index
     already enqueued): hreg_fps_indexed, bitwise fps(xyz, npoint)."""
     nb, n, _ = xyz.shape
     if out is None:
@@ -906,7 +885,7 @@ def knn_group_indexed(q, p, k, ws, out=None, build=True):
         kx = _empty(R, 3, device=dev)
     else:
         gidx, geom, kx = out
-    if build and (PROBE_S1_SKIP != 3 or out is None):
+    if build:
         call("hreg_spatial_index", p, nb, n, ws, _stream())
     call("hreg_knn_group_indexed", q, p, ws, nb, m, n, k, gidx, geom, kx, _stream())
     return gidx, geom, kx
@@ -983,8 +962,7 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_co
     M, k = LEVELS[lvl][:2]
     nb, n, _ = xyz.shape
     use_si = SPATIAL_KNN_MIN <= n <= SPATIAL_KNN_MAX
-    if (FPS_SORTED and use_si and n == FPS_SORTED_N and weights is None and sample is None
-            and not PROBE_S1_SKIP):
+    if FPS_SORTED and use_si and fps_indexed_ok(n) and weights is None and sample is None:
         # the index first: the FPS reads its Morton-sorted copy (fps_indexed), the kNN its blocks
         if ws is None:
             ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
@@ -994,7 +972,7 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_co
                                            build=False)
         _record_knn(f"knn_{lvl + 1}", gidx, nb, n, k, True)
         return idx, sampled, gidx, geom, kx
-    fk = _fork_begin() if (_fork_on and use_si and sample is None and not PROBE_S1_SKIP) else None
+    fk = _fork_begin() if (_fork_on and use_si and sample is None) else None
     if fk is not None:
         if ws is None:
             ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
@@ -1010,14 +988,10 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_co
         return idx, sampled, gidx, geom, kx
     if sample is not None:
         idx, sampled = sample, gather_xyz(xyz, sample)
-    elif PROBE_S1_SKIP == 1 and out is not None and lvl == 0:
-        idx, sampled = out[0], out[1]  # (timing probe: the buffers' previous selection)
     else:
         idx, sampled = fps(xyz, M, None if weights is None else weights.view(nb, n),
                            out=None if out is None else out[:2], concurrent=fps_concurrent)
     kout = None if out is None else out[2:5]
-    if PROBE_S1_SKIP == 2 and out is not None and lvl == 0:
-        return idx, sampled, out[2], out[3], out[4]
     if use_si:
         if ws is None:
             ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
@@ -1052,7 +1026,7 @@ def _fused23_kernel(P: PreparedWeights, lvl: int):
     (its input projection then uses the bf16x6 table too)."""
     split = (SPLIT_L2, SPLIT_L3)[lvl - 1]
     if lvl == 1 and B6_L2 and not SPLIT_L2:
-        name, table = ("hreg_group6x2_l2" if PAIR_L2 and LEVEL_PRE else "hreg_group6_l2"), P.l2_table6
+        name, table = "hreg_group6_l2", P.l2_table6
     elif lvl == 2 and B6_L3 and not SPLIT_L3:
         name, table = "hreg_group6_l3", P.l3_table6
     elif split and (B6_L2, B6_L3)[lvl - 1]:
@@ -1064,7 +1038,7 @@ def _fused23_kernel(P: PreparedWeights, lvl: int):
     else:
         name, table = (("hreg_group_l2", P.l2_table) if lvl == 1 else
                        ("hreg_group_l3", P.l3_table))
-    b6 = name in ("hreg_group6_l2", "hreg_group6x2_l2", "hreg_group6_l3", "hreg_group_split6_l2",
+    b6 = name in ("hreg_group6_l2", "hreg_group6_l3", "hreg_group_split6_l2",
                   "hreg_group_split6_l3")
     return name, table, b6
 
@@ -1118,8 +1092,8 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         name, table, b6 = _fused23_kernel(P, lvl)
         if pre is None and LEVEL_PRE:
             pre = gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl], feats.shape[0])
-        if name == "hreg_group_split6_l3" and pre is not None and (SPLIT_JT or L3_PIECES):
-            name = "hreg_group_split6p_l3" if L3_PIECES else "hreg_group_split6j_l3"
+        if name == "hreg_group_split6_l3" and pre is not None and SPLIT_JT:
+            name = "hreg_group_split6j_l3"
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())
         sig, wnext = mlp_head(P, ("det", lvl), att_feat, nb, M, _lib.HREG_HEAD_SOFTPLUS,
                               want_weights=True)
@@ -1185,11 +1159,6 @@ def mlp_head(P: PreparedWeights, key, x, nclouds, rows, mode, want_weights=False
         dev = x.device
         out = _empty(nclouds * rows, device=dev)
         wout = _empty(nclouds * rows, device=dev) if want_weights else None
-        if PROBE_SKIP_MLP:
-            out.fill_(1.0)
-            if wout is not None:
-                wout.fill_(1.0)
-            return out, wout
         if B6_MLP:
             # (chain_fork: a forward alone) one row tile per workgroup -- a batch-8 head is 32-128
             # workgroups at the default 2-4 tiles each
@@ -1211,17 +1180,13 @@ def _mlp_weights(P: PreparedWeights, key, x, nclouds, rows):
     return w
 
 
-# Timing probes (results WRONG, A/B timing only; tools/gpu_abn.sh sw:...): skip the plain /
-# grouped GEMM launches, or replace the mlp heads by constant fills
-PROBE_SKIP_GEMM = switches.flag("PROBE_SKIP_GEMM", False)
-PROBE_SKIP_MLP = switches.flag("PROBE_SKIP_MLP", False)
-
 # The registration heads' products of the feature-extraction outputs -- CoarseReg's neighbour
 # branch block (W_desc desc3), its convs_1 desc / knn_desc blocks, the original cosine
 # similarity, and both FineReg heads' descriptor blocks -- depend on nothing but desc_1..3, so
 # they run as ONE grouped launch right after the feature extraction (hreg_gemm_grouped: the
-# same bits as five separate hreg_gemm launches, one launch instead of five small ones)
-GROUPED_HEAD_GEMMS = switches.flag("GROUPED_HEAD_GEMMS", True)
+# same bits as five separate hreg_gemm launches, one launch instead of five small ones; test
+# checker: False, the separate launches)
+GROUPED_HEAD_GEMMS = True
 
 
 def _grouped_heads_ok(C3: int) -> bool:
@@ -1250,8 +1215,7 @@ def head_products(P: PreparedWeights, B: int, desc):
         pre = _empty(2, B * M, P.fine[name][0][0].W.shape[0], device=dev)
         gs.append(_batched_desc_struct(P.fine_pre6[name], dl, B * M, Cl, pre))
         fine[name] = pre
-    if not PROBE_SKIP_GEMM:
-        _lib.gemm_grouped(gs)
+    _lib.gemm_grouped(gs)
     return {"nbr_pre": nbr_pre, "ud": ud, "S": S, "fine_pre": fine}
 
 
@@ -1711,7 +1675,7 @@ def check_hw_queues(streams: int, env=None) -> int:
 
 def fork_width(lanes: int, batched_stage1: bool, front_two_streams: bool) -> int:
     """Streams one replay of the executor forks: a stream per lane (lane 0 the capture
-    stream), a second per lane for the front half (FRONT_ORDER 3), and the stage-1 side
+    stream), a second per lane for the front half, and the stage-1 side
     stream(s) -- one batched, or one per lane."""
     return lanes * (2 if front_two_streams else 1) + (1 if batched_stage1 else lanes)
 
@@ -1769,7 +1733,7 @@ class GraphPipeline:
         # that runs multi-workgroup FPS -- instead of one launch per lane on per-lane side streams,
         # which shared the 4 hardware queues with the lanes' own streams)
         self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1 and (N <= 16384 or (v2 and V2_BATCH_STAGE1))
-        check_hw_queues(fork_width(lanes, self.bs1, FRONT_STREAM and FRONT_ORDER == 3 and self.bs1
+        check_hw_queues(fork_width(lanes, self.bs1, FRONT_STREAM and self.bs1
                                    and (not v2 or V2_FRONT_STREAM) and lanes <= FRONT_STREAM_MAX_LANES))
         if self.bs1:
             self.src_all = src.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
@@ -1832,17 +1796,14 @@ class GraphPipeline:
                            for _ in (0, 1)]
                 del fe0
                 self.g_fs, self.outs_fs, self.g_prime = [], [], []
-                if FRONT_ORDER == 3:
-                    self.lane_streams2 = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
+                # the two halves of a lane on two streams (r4: 7084 -> 7311 pairs/s, against 7141
+                # with both halves on the lane's stream)
+                self.lane_streams2 = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
                 for cur in (0, 1):
                     g = torch.cuda.CUDAGraph()
                     with capture.graph(g, pool=self.pool):
-                        if FRONT_ORDER == 3:  # the two halves of a lane on two streams
-                            out = self._fork(lambda ln: hregnet_back(P, self.fe[1 - cur][ln], B, v2, sub_batch),
-                                             body2=lambda ln: self._front_into(ln, cur),
-                                             **self._side_kw(1 - cur))
-                        else:
-                            out = self._fork(lambda ln: self._halves(ln, cur), **self._side_kw(1 - cur))
+                        out = self._fork(lambda ln: hregnet_back(P, self.fe[1 - cur][ln], B, v2, sub_batch),
+                                         body2=lambda ln: self._front_into(ln, cur), **self._side_kw(1 - cur))
                     self.g_fs.append(g)
                     self.outs_fs.append(out)
                     g = torch.cuda.CUDAGraph()
@@ -1879,8 +1840,6 @@ class GraphPipeline:
         """_fork keywords for the next batch's stage 1 into buffer set ab (batched: one job
         for all lanes; per lane: lanes < side_lanes)."""
         if self.bs1:
-            if PROBE_NO_S1:  # (timing probe: static inputs keep the stage-1 buffers valid)
-                return {}
             return {"side_all": lambda: self._stage1_all(ab)}
         return {"side": lambda ln: stage1_into(self.bufs[ln][ab], self.src[ln], self.dst[ln]),
                 "side_lanes": side_lanes}
@@ -1930,24 +1889,10 @@ class GraphPipeline:
         """Lane ln's feature extraction from stage-1 set cur, copied into fe[cur][ln]."""
         pts, g = self.bufs[ln][cur]
         fe = hregnet_front(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g, pts=pts)
-        # one multi-tensor copy per dtype instead of 12 copy kernels per lane and round
+        # one multi-tensor copy per dtype instead of 12 copy kernels per lane and round (r5:
+        # neutral, 7964 vs 7943 pairs/s, kept)
         dst = self.fe[cur][ln]
-        if FRONT_FOREACH:
-            torch._foreach_copy_([dst[k] for k in FRONT_KEYS], [fe[k] for k in FRONT_KEYS])
-        else:
-            for k in FRONT_KEYS:
-                dst[k].copy_(fe[k])
-
-    def _halves(self, ln, cur):
-        """One front-streamed round of lane ln: the registration half from fe[1 - cur] and the
-        next batch's feature extraction from stage-1 set cur into fe[cur] (FRONT_ORDER 0, the
-        default: in that order; 1: the other way round; 2: by lane parity)."""
-        if FRONT_ORDER == 1 or (FRONT_ORDER == 2 and ln % 2):
-            self._front_into(ln, cur)
-            return hregnet_back(self.P, self.fe[1 - cur][ln], self.B, self.v2, self.sub_batch)
-        out = hregnet_back(self.P, self.fe[1 - cur][ln], self.B, self.v2, self.sub_batch)
-        self._front_into(ln, cur)
-        return out
+        torch._foreach_copy_([dst[k] for k in FRONT_KEYS], [fe[k] for k in FRONT_KEYS])
 
     def prime(self):
         """Front streaming: run the next round's feature extraction (and the stage 1 of the

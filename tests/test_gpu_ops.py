@@ -65,14 +65,16 @@ def test_fps_vs_oracle(n, m, weighted):
     np.testing.assert_array_equal(idx.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("n", [16384, 65536, 40000])
 @pytest.mark.parametrize("kind", ["lidar", "uniform_ties", "grid_dups", "line"])
-def test_fps_indexed_matches_fps(kind):
-    """hreg_fps_indexed (level-1 FPS over the spatial index's sorted copy, exact group pruning):
-    indices and running minima bitwise those of hreg_furthest_point_sampling and the oracle's --
-    including clouds whose ties the reference order must break (rounded coordinates, an integer
-    grid with ~16 copies of every point, whose last selections are all at T = 0, and a line)."""
+def test_fps_indexed_matches_fps(kind, n):
+    """hreg_fps_indexed (level-1 FPS over the spatial index's sorted copy, exact pruning:
+    fps_sorted_kernel at 16384 points, fps_blocks_kernel above): indices and running minima
+    bitwise those of hreg_furthest_point_sampling and the oracle's -- including clouds whose ties
+    the reference order must break (rounded coordinates, an integer grid with ~16 copies of every
+    point (at 16384), whose last selections are all at T = 0, and a line)."""
     from pcd_reg_hregnet_amd import engine, synthetic, _lib
-    n, m, B = 16384, 1024, 3
+    m, B = 1024, 3
     rng = np.random.default_rng({"lidar": 1, "uniform_ties": 2, "grid_dups": 3, "line": 4}[kind])
     if kind == "lidar":
         s, d, _, _ = synthetic.lidar_batch(2, n, seed0=12)
@@ -96,9 +98,59 @@ def test_fps_indexed_matches_fps(kind):
     rtemp = torch.full((B, n), -2.0, device="cuda")
     _lib.call("hreg_furthest_point_sampling", B, n, m, x, rtemp, ref, None, _lib.stream_handle())
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(idx.cpu().numpy(), ref.cpu().numpy())
-    assert torch.equal(temp, rtemp)
-    np.testing.assert_array_equal(idx.cpu().numpy()[:1], oracle.fps(xyz[:1], m, None))
+    got = idx.cpu().numpy()
+    np.testing.assert_array_equal(got, ref.cpu().numpy())
+    if n == 16384:
+        assert torch.equal(temp, rtemp)
+    else:  # (the cluster kernel keeps its exchange slots in temp): the reference's final running
+        # minima, min over the centres idx[0 .. m-2] of the two-rounding fp32 distance (.cu:129-130)
+        for c in range(B):
+            t = np.full(n, 1e10, np.float32)
+            p = xyz[c]
+            for k in got[c, :-1]:
+                d = p - p[k]
+                t = np.minimum(t, (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])
+            np.testing.assert_array_equal(temp[c].cpu().numpy(), t)
+    np.testing.assert_array_equal(got[:1], oracle.fps(xyz[:1], m, None))
+
+
+@pytest.mark.parametrize("n", [16384, 65536])
+def test_fps_and_indexed_knn_nonfinite_coordinates(n):
+    """NaN / inf coordinates: the reference's d2 = fminf(d, temp) (.cu:130)
+    keeps temp when d is NaN (a NaN coordinate, inf - inf) or inf, so such a point keeps 1e10 and
+    is chosen at the first iteration whose maximum it holds, and from a non-finite centre no
+    running minimum moves.  Every GPU FPS path (pruned over the spatial index -- whose Morton key
+    maps NaN to cell 0 -- and the register / cluster kernels) must give the oracle's indices; the
+    indexed kNN must stay bit-identical to the brute-force scan on the same clouds."""
+    from pcd_reg_hregnet_amd import engine, _lib
+    from pcd_reg_hregnet_amd import point_utils_cuda as pu
+    rng = np.random.default_rng(77 + n)
+    B, m = 4, 96
+    xyz = rng.uniform(-40, 40, (B, n, 3)).astype(np.float32)
+    xyz[:, ::5] = np.round(xyz[:, ::5])
+    nanp = rng.integers(1, n, 3)
+    xyz[0, nanp[0], 1] = np.nan  # one NaN coordinate
+    xyz[1, nanp[1], 0] = np.inf  # +inf
+    xyz[1, nanp[2], 2] = -np.inf  # and -inf in the same cloud
+    xyz[2, rng.integers(1, n, 40)] = np.nan  # many NaN points
+    # cloud 3 stays finite (the pruning must be unaffected beside the others)
+    x = dev(xyz)
+    ref = oracle.fps(xyz, m, None)
+    ws = torch.empty(engine.spatial_index_bytes(B, n), dtype=torch.uint8, device="cuda")
+    _lib.call("hreg_spatial_index", x, B, n, ws, _lib.stream_handle())
+    a = torch.full((B, m), -1, dtype=torch.int32, device="cuda")
+    _lib.call("hreg_fps_indexed", B, n, m, x, ws, None, a, None, _lib.stream_handle())
+    b = torch.full((B, m), -2, dtype=torch.int32, device="cuda")
+    pu.furthest_point_sampling_wrapper(B, n, m, x, torch.full((B, n), 1e10, device="cuda"), b)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a.cpu().numpy(), ref)
+    np.testing.assert_array_equal(b.cpu().numpy(), ref)
+    # the indexed kNN around the selected centres (finite and not) == the brute-force scan
+    q = torch.from_numpy(np.ascontiguousarray(xyz[np.arange(B)[:, None], ref])).cuda()
+    gi = engine.knn_group_indexed(q, x, 16, ws)
+    gb = engine.knn_group(q, x, 16)
+    torch.cuda.synchronize()
+    assert torch.equal(gi[0], gb[0])
 
 
 def test_fps_cluster_many_clouds_and_mem_path():

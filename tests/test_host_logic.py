@@ -342,8 +342,8 @@ def test_bench_entry_peaks():
     fp32-MFMA kernels at the f32 matrix peak.  r3: hreg_group_split6j_l3, hreg_corr_head6x and
     hreg_nbr_head6sx were priced at the fp32 peak (roofline.frac 0.71 instead of 0.45)."""
     import bench
-    b6 = {"hreg_group_l1_6", "hreg_group_l1_6g", "hreg_group6_l2", "hreg_group6x2_l2",
-          "hreg_group_split6_l2", "hreg_group_split6_l3", "hreg_group_split6j_l3", "hreg_group_split6p_l3",
+    b6 = {"hreg_group_l1_6", "hreg_group_l1_6g", "hreg_group6_l2",
+          "hreg_group_split6_l2", "hreg_group_split6_l3", "hreg_group_split6j_l3",
           "hreg_group6_l3",
           "hreg_fine_head6", "hreg_nbr_head6", "hreg_nbr_head6s", "hreg_nbr_head6sx",
           "hreg_coarse_head6", "hreg_corr_head6", "hreg_corr_head6x", "hreg_mlp_head6", "hreg_mlp_head6x",
@@ -385,3 +385,60 @@ def test_bench_default_merge_divides_steps():
         for v2 in (False, True):
             m = bench.default_merge(steps, v2)
             assert steps % m == 0 and 1 <= m <= (12 if v2 else 4)
+
+
+def _fake_forward_inputs(bench, v2):
+    import argparse
+    args = argparse.Namespace(steps=20, warmup=8, executor="graph", lanes=5, points=65536 if v2 else 16384,
+                              model="v2" if v2 else "hregnet", batch=2 if v2 else 8)
+    # MfmaTimer.result per kind: (ms, launches, FLOPs, bytes, executed FLOPs)
+    res = {k: (10.0 + i, 40 + i, 3e12 + i, 1e9, 2.5e12) for i, k in enumerate(bench.MfmaTimer.KINDS)}
+    ent = {name: {"launches_per_step": 1.0, "avg_launch_us": 500.0, "tflops": 200.0,
+                  "peak": bench.entry_peak(name), "_ms": 10.0, "_flops": 2e12}
+           for name in ("hreg_group_l1_6", "hreg_group6_l2", "hreg_group_split6j_l3", "hreg_mlp_head6x")}
+    return args, res, ent
+
+
+def _check_line(line, metric_word):
+    import json
+    d = json.loads(json.dumps(line))  # serialisable, nothing left as a tensor / numpy scalar
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert metric_word in d["metric"] and d["unit"] == "pairs/s" and d["higher_is_better"] is True
+    assert "workload" in d["config"]
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    return d
+
+
+@pytest.mark.parametrize("model", ["hregnet", "v2"])
+def test_bench_forward_line_assembles_on_cpu(model):
+    """every bench mode's JSON line is assembled by a pure function from its
+    measurements, so a NameError in the assembly (r5's bench_train `merge`) fails here, on the
+    CPU, before it can reach a GPU run."""
+    import bench
+    v2 = model == "v2"
+    args, res, ent = _fake_forward_inputs(bench, v2)
+    line = bench.forward_line(
+        args, v2=v2, B=args.batch, merge=4, world=1, value=8000.0, ms_per_step=1.0, host_submit_s=0.002,
+        res=res, ent=ent, level_names=["a (level 1)", "b (level 2)", "c (level 3)"], traffic=(3e8, "x.json"),
+        inexec=None, fps={"level1": {"us_per_iteration": 1.0}}, lat={"graph_ms": 2.7},
+        cpu={"value": 1.8, "unit": "pairs/s", "cores": 16, "kind": "port", "sample": "s"}, bs1=True, fs=not v2,
+        merge1=None if v2 else {"value": 7400.0, "ms_per_step": 1.08})
+    d = _check_line(line, "Model_V2" if v2 else "HRegNet")
+    assert d["value"] == 8000.0 and d["config"]["merge"] == 4
+    assert ("configs[4]" if v2 else "configs[1]") in d["config"]["workload"]
+    assert d["cpu_baseline"]["kind"] == "port"
+
+
+def test_bench_train_line_assembles_on_cpu():
+    import argparse
+    import bench
+    args = argparse.Namespace(steps=10, warmup=2, points=16384, batch=8)
+    line = bench.train_line(args, B=8, world=1, value=418.0, elapsed=0.19, losses=[1.44, 5.93],
+                            nt=(80.0, 1000, 1e13), tn=(60.0, 900, 8e12), graphed=True)
+    d = _check_line(line, "training")
+    assert d["loss_first_last"] == [1.44, 5.93] and "configs[3]" in d["config"]["workload"]

@@ -19,7 +19,7 @@ import json
 import os
 import sys
 
-LEVEL_KERNELS = ("group_l1_6_kernel", "group_fused6_kernel", "group_split6j_kernel", "group_split6p_kernel")
+LEVEL_KERNELS = ("group_l1_6_kernel", "group_fused6_kernel", "group_split6j_kernel")
 
 
 def short(name):
