@@ -43,7 +43,7 @@ PAIRS_PER_GPU = 8
 LANES_MAX = 48         # graph executor: most batches in flight (memory: one forward's buffers each)
 V2_POINTS = 65536      # config 5 (MANTruckScenes-shape): B=16 over 8 GPUs -> 2 pairs/GPU
 V2_PAIRS_PER_GPU = 2
-V2_LANES = 2           # Model_V2 graph executor: lanes (forwards in flight)
+V2_LANES = 4           # Model_V2 graph executor: lanes (forwards in flight; 2 when --steps / merge is odd)
 # Model_V2: reference batches merged per forward (--merge; the largest divisor of --steps up to
 # this).  48 steps, paired lines (gpurun_out/r5p): merge 8 / 12 / 24 -> 2999 / 3164 / 3137 pairs/s
 V2_MERGE = 12
@@ -594,11 +594,13 @@ def unmerged_line(P, src, dst, steps: int, warmup: int):
                      f"forward ({lanes} forwards in flight), measured right after the headline line"}
 
 
-def default_merge(steps: int, v2: bool) -> int:
+def default_merge(steps: int, v2: bool, batch: int = PAIRS_PER_GPU) -> int:
     """Reference batches merged per executor forward when --merge is not given: the largest
     divisor of --steps up to the model's factor (HREGNET_MERGE / V2_MERGE), so any step count
-    still times exactly --steps batches."""
-    cap = V2_MERGE if v2 else HREGNET_MERGE
+    still times exactly --steps batches.  A batch of 32 pairs or more (configs[2]) already fills
+    the chip: one batch per forward (r6, --steps 20, one box: merge 1 / 2 / 4 at B = 32 ran 8555 /
+    8675 / 8502 pairs/s, gpurun_out/r6b32)."""
+    cap = V2_MERGE if v2 else (HREGNET_MERGE if batch < 32 else 1)
     return max(m for m in range(1, cap + 1) if steps % m == 0) if steps > 0 else 1
 
 
@@ -909,7 +911,9 @@ def forward_line(args, *, v2, B, merge, world, value, ms_per_step, host_submit_s
         "config": {"workload": (f"Model_V2 forward (eval), batch={B} pairs/GPU, 2x{args.points}"
                                 "-pt LiDAR pairs (BASELINE configs[4])") if v2 else (
                                f"HRegNet forward (eval), batch={B} pairs/GPU, "
-                               f"2x{args.points}-pt KITTI-shape pairs (BASELINE configs[1])"),
+                               f"2x{args.points}-pt KITTI-shape pairs (BASELINE "
+                               + ("configs[2]: 3-level coarse-to-fine + weighted SVD, MFMA similarity"
+                                  if B == 32 else "configs[1]") + ")"),
                    "executor": args.executor + ("" if args.executor == "serial" else
                                " (level-1 FPS of step i+1 overlaps step i)") + (
                                f", {args.lanes} forwards in flight" if args.lanes > 1 and
@@ -1062,7 +1066,7 @@ def main():
     # --batch pairs merged into one launch set (engine.hregnet_forward sub_batch: every pair's
     # result bitwise that of its own batch's forward, the weighted SVD's identity fallback and
     # the prime shuffles per batch); a step is still one batch of --batch pairs
-    merge = default_merge(args.steps, v2) if args.merge is None else args.merge
+    merge = default_merge(args.steps, v2, args.batch) if args.merge is None else args.merge
     if merge < 1 or args.steps % merge:
         raise SystemExit(f"bench: --steps {args.steps} is not a multiple of --merge {merge}")
     args.warmup = -(-args.warmup // merge) * merge  # (untimed: rounded up to whole forwards)
@@ -1078,7 +1082,9 @@ def main():
         # 6295 / 6432 pairs/s; --steps 48 on 16 / 24 / 48 lanes 6802 / 6697 / 6891), else
         # LANES_MAX with a final partial round (GraphPipeline.run_forwards); v2: 4
         if v2:
-            args.lanes = V2_LANES if args.steps % V2_LANES == 0 else 1
+            # (r6, --steps 48, gpurun_out/r6v2: 4 lanes x 12 merged 6646 pairs/s, 2 x 12 6329,
+            # 2 x 24 6574, 8 x 6 6278, 4 x 6 5947)
+            args.lanes = max(ln for ln in (V2_LANES, 2, 1) if args.steps % ln == 0)
         elif args.steps <= LANES_MAX:
             args.lanes = max(args.steps, 1)
         else:

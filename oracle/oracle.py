@@ -297,9 +297,12 @@ def _nbr_desc(sd, pre, xyz, desc, k, rec=None, name=None):
     return np.sum(feats * w[..., None], axis=2).astype(np.float32)
 
 
-def coarse_reg(sd, pre, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w, k=8, rec=None):
-    """CoarseReg.forward, layers.py:273-396 (use_sim = use_neighbor = True); rec: the
-    neighbour branch's xyz kNN selections (coarse_nbr_src / coarse_nbr_dst)."""
+def coarse_reg(sd, pre, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w, k=8, rec=None,
+               use_sim=True, use_neighbor=True):
+    """CoarseReg.forward, layers.py:273-396; rec: the neighbour branch's xyz kNN selections
+    (coarse_nbr_src / coarse_nbr_dst).  use_sim / use_neighbor: the constructor's variants
+    (layers.py:237-244: convs_1 over 2C + 16 / 14 / 12 inputs; the similarity features
+    layers.py:368-379 -- original, neighbour-aware, both or none)."""
     sdsc = np.ascontiguousarray(src_desc.transpose(0, 2, 1))
     ddsc = np.ascontiguousarray(dst_desc.transpose(0, 2, 1))
     _, kidx = knn(sdsc, ddsc, k)
@@ -311,13 +314,16 @@ def coarse_reg(sd, pre, src_xyz, src_desc, dst_xyz, dst_desc, src_w, dst_w, k=8,
     dist = np.sqrt(np.sum(rela * rela, axis=-1, keepdims=True)).astype(np.float32)
     w_e = np.repeat(src_w[:, :, None, None], k, axis=2)
     knn_w = knn_gather(dst_w[..., None], kidx)
-    sd_cos, ds_cos = _sim_feats(sdsc, ddsc, kidx)
-    snb = _nbr_desc(sd, pre, src_xyz, sdsc, k, rec, "coarse_nbr_src")
-    dnb = _nbr_desc(sd, pre, dst_xyz, ddsc, k, rec, "coarse_nbr_dst")
-    sd_ncos, ds_ncos = _sim_feats(snb, dnb, kidx)
-    feats = np.concatenate([rela, dist, xyz_e, knn_xyz, desc_e, knn_desc, w_e, knn_w,
-                            sd_cos[..., None], ds_cos[..., None], sd_ncos[..., None],
-                            ds_ncos[..., None]], axis=-1)
+    sims = []
+    if use_sim:
+        sd_cos, ds_cos = _sim_feats(sdsc, ddsc, kidx)
+        sims += [sd_cos[..., None], ds_cos[..., None]]
+    if use_neighbor:
+        snb = _nbr_desc(sd, pre, src_xyz, sdsc, k, rec, "coarse_nbr_src")
+        dnb = _nbr_desc(sd, pre, dst_xyz, ddsc, k, rec, "coarse_nbr_dst")
+        sd_ncos, ds_ncos = _sim_feats(snb, dnb, kidx)
+        sims += [sd_ncos[..., None], ds_ncos[..., None]]
+    feats = np.concatenate([rela, dist, xyz_e, knn_xyz, desc_e, knn_desc, w_e, knn_w] + sims, axis=-1)
     f = _conv_stack(np.ascontiguousarray(feats.transpose(0, 3, 1, 2)), sd, pre + ".convs_1", 3)
     a = _softmax(np.max(f, axis=1), -1)
     corres = np.sum(a[..., None] * knn_xyz, axis=2).astype(np.float32)

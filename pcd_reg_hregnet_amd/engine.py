@@ -75,7 +75,7 @@ LEVEL_PRE = True
 # level 1 with its weight table resident in LDS (hreg_group_l1_6) for clouds up to this many
 # points; above, the global-table form (hreg_group_l1_6g): r2, beside Model_V2's cluster FPS on
 # every CU the 92 KB LDS claim waited for it (942 vs 856 pairs/s)
-L1_LDS_MAX_N = 16384
+L1_LDS_MAX_N = 16384  # (r6, beside the one-workgroup V2 FPS: 65536 measured within noise, 6407 / 6749 / 6517 vs 6329 / 6574 / 6646)
 
 # ---- executor switches (HREG_SWITCHES, whole-process A/B of the measured choices)
 # GraphPipeline: level-1 stage of all lanes as one batched launch per kernel (one side stream)
@@ -84,10 +84,10 @@ BATCH_STAGE1 = switches.flag("BATCH_STAGE1", True)
 V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", True)  # GraphPipeline(v2=True): see bs1
 # GraphPipeline: halves of a forward in consecutive rounds, the two halves of a lane on two
 # streams (r4: 20 lanes 7084 -> 7311 pairs/s; off above FRONT_STREAM_MAX_LANES: 48 lanes 7456 ->
-# 7388; off for Model_V2)
+# 7388; off for Model_V2: r6, 6142 / 6966 / 6423 vs 6329 / 6574 / 6646 pairs/s at 2 x 12, 2 x 24,
+# 4 x 12 lanes x merged batches, gpurun_out/r6v2)
 FRONT_STREAM = switches.flag("FRONT_STREAM", True)
 FRONT_STREAM_MAX_LANES = 24
-V2_FRONT_STREAM = switches.flag("V2_FRONT_STREAM", False)  # (Model_V2: front streaming, r6 A/B)
 # Single-batch latency (one forward alone on the GPU is one dependent chain of ~50 kernels): work
 # that does not depend on the chain's previous kernel runs beside it on a side stream -- the
 # level-1 spatial index (input points only) beside the level-1 FPS, the level-2/3 input
@@ -189,13 +189,45 @@ def _perm_fine(C):
             + list(range(10 + C, 10 + 2 * C)))
 
 
-class PreparedWeights:
-    """Device-resident folded weights for one HRegNet state dict."""
+def _pad_coarse_convs1(sd: dict, use_sim: bool, use_neighbor: bool) -> None:
+    """CoarseReg's variants (layers.py:237-244): convs_1[0] over 2C + 14 inputs (one pair of
+    similarity features) or 2C + 12 (none).  In place: the weight is widened to the 2C + 16
+    layout of use_sim = use_neighbor = True ([geom 10 | desc C | knn_desc C | w 2 | cos 2 |
+    nbr cos 2], layers.py:368-379) with zero columns where a variant has no feature -- the
+    engine then feeds zeros there, and every product of a zero column is an exact 0, so the
+    fused kernels compute the variant's function."""
+    key = "coarse_corres.convs_1.0.weight"
+    W = sd.get(key)
+    if W is None:
+        return
+    n = W.shape[1] - 12 - 2 * (use_sim + use_neighbor)  # 2C
+    C = sd["coarse_corres.convs_2.0.weight"].shape[0] if "coarse_corres.convs_2.0.weight" in sd else n // 2
+    if n != 2 * C:
+        raise ValueError(f"coarse_corres.convs_1.0.weight has {W.shape[1]} inputs: not a CoarseReg over "
+                         f"{C} channels with use_sim={use_sim}, use_neighbor={use_neighbor}")
+    if use_sim and use_neighbor:
+        return
+    W16 = torch.zeros((W.shape[0], n + 16) + tuple(W.shape[2:]), dtype=W.dtype)
+    W16[:, :n + 12] = W[:, :n + 12]
+    o = n + 12
+    if use_sim:
+        W16[:, n + 12:n + 14] = W[:, o:o + 2]
+        o += 2
+    if use_neighbor:
+        W16[:, n + 14:n + 16] = W[:, o:o + 2]
+    sd[key] = W16
 
-    def __init__(self, sd: dict, device):
+
+class PreparedWeights:
+    """Device-resident folded weights for one HRegNet state dict (coarse_variant: the CoarseReg
+    head's (use_sim, use_neighbor), layers.py:229-244)."""
+
+    def __init__(self, sd: dict, device, coarse_variant=(True, True)):
         # fold on the host in fp32, then move the folded tensors to the device
         sd = {k: v.detach().to("cpu", torch.float32) if v.is_floating_point() else v
               for k, v in sd.items()}
+        self.coarse_use_sim, self.coarse_use_nbr = (bool(v) for v in coarse_variant)
+        _pad_coarse_convs1(sd, self.coarse_use_sim, self.coarse_use_nbr)
         fe = "feature_extraction."
         self.det, self.det_head, self.desc, self.desc_mlp = [], [], [], []
         for lvl in range(3):
@@ -1260,8 +1292,9 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3, prod=None, knns=None):
     R2 = G2 * k
     b6 = B6_HEADS and HEAD_PRE
     # (chain_fork) the fused neighbour head beside the first similarity gather
-    fk = (_fork_begin() if (_fork_on and prod is not None and FUSED_NBR and C == 256 and b6 and SPLIT_NBR)
-          else None)
+    use_sim, use_nbr = P.coarse_use_sim, P.coarse_use_nbr
+    fk = (_fork_begin() if (_fork_on and use_nbr and prod is not None and FUSED_NBR and C == 256 and b6
+                            and SPLIT_NBR) else None)
     if fk is not None:
         nbr = _empty(G2, C, device=dev)
         main, side = fk
@@ -1275,11 +1308,16 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3, prod=None, knns=None):
         norms = row_norms(desc3)
         S = _empty(B, N1, N1, device=dev)
         cosine_gemm(s_desc, d_desc, norms[:B * N1], norms[B * N1:], B, N1, N1, C, S)
-    sims_a = _empty(B * N1 * k, 2, device=dev)
     maxes = _empty(B, 2 * N1, device=dev)
-    call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_a, 2, _stream())
+    if use_sim:
+        sims_a = _empty(B * N1 * k, 2, device=dev)
+        call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_a, 2, _stream())
+    else:  # (variant: zero features under zero weight columns, _pad_coarse_convs1)
+        sims_a = torch.zeros(B * N1 * k, 2, device=dev)
     # neighbour-aware descriptors for src and dst together (layers.py:315-337)
-    if fk is not None:
+    if not use_nbr:
+        nbr = None
+    elif fk is not None:
         main.wait_stream(side)
     elif FUSED_NBR and C == 256:
         nbr = _empty(G2, C, device=dev)
@@ -1301,10 +1339,13 @@ def coarse_reg(P: PreparedWeights, B, xyz3, desc3, sig3, prod=None, knns=None):
         h = gemm([_seg(h, 0, h.shape[1])], P.coarse_convs2[1], R2)
         h = gemm([_seg(h, 0, h.shape[1])], P.coarse_convs2[2], R2)
         _, nbr, _ = attend(h, G2, k, vals=desc3, vgather=gself)
-    nnorm = row_norms(nbr)
-    cosine_gemm(nbr[:B * N1], nbr[B * N1:], nnorm[:B * N1], nnorm[B * N1:], B, N1, N1, C, S)
-    sims_b = _empty(B * N1 * k, 2, device=dev)
-    call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_b, 2, _stream())
+    if use_nbr:
+        nnorm = row_norms(nbr)
+        cosine_gemm(nbr[:B * N1], nbr[B * N1:], nnorm[:B * N1], nnorm[B * N1:], B, N1, N1, C, S)
+        sims_b = _empty(B * N1 * k, 2, device=dev)
+        call("hreg_sim_gather", S, B, N1, N1, kidx, k, maxes, sims_b, 2, _stream())
+    else:
+        sims_b = torch.zeros(B * N1 * k, 2, device=dev)
     # correspondence features + convs_1 (layers.py:364-384)
     R = B * N1 * k
     small = _empty(R, 16, device=dev)
@@ -1733,8 +1774,8 @@ class GraphPipeline:
         # that runs multi-workgroup FPS -- instead of one launch per lane on per-lane side streams,
         # which shared the 4 hardware queues with the lanes' own streams)
         self.bs1 = BATCH_STAGE1 and FUSED_L1 and lanes > 1 and (N <= 16384 or (v2 and V2_BATCH_STAGE1))
-        check_hw_queues(fork_width(lanes, self.bs1, FRONT_STREAM and self.bs1
-                                   and (not v2 or V2_FRONT_STREAM) and lanes <= FRONT_STREAM_MAX_LANES))
+        check_hw_queues(fork_width(lanes, self.bs1, FRONT_STREAM and self.bs1 and not v2
+                                   and lanes <= FRONT_STREAM_MAX_LANES))
         if self.bs1:
             self.src_all = src.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
             self.dst_all = dst.unsqueeze(0).repeat(lanes, 1, 1, 1).contiguous()
@@ -1785,7 +1826,7 @@ class GraphPipeline:
             # front streaming: fe[c][ln] = static copies of a lane's feature-extraction dict;
             # fready = c: the fronts for the next round are in fe[1 - c] and its next stage 1
             # in bufs[c], so the next replay is g_fs[c]
-            self.fs = (FRONT_STREAM and self.bs1 and (not v2 or V2_FRONT_STREAM)
+            self.fs = (FRONT_STREAM and self.bs1 and not v2
                        and lanes <= FRONT_STREAM_MAX_LANES)
             self.fready = None
             if self.fs:

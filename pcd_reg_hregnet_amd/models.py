@@ -70,18 +70,42 @@ class DescExtractor(_HIPOnly):
         self.mlp2 = nn.Sequential(*_conv_bn_relu(chans[-2], desc_dim))
 
 
-class CoarseReg(_HIPOnly):
-    """Parameter layout of layers.py:229-268."""
+class CoarseReg(nn.Module):
+    """layers.py:229-396: the parameter layout of every (use_sim, use_neighbor) variant --
+    convs_1 over 2C + 16 / 14 / 14 / 12 inputs (layers.py:237-244); convs_2 exists in all of them,
+    as in the reference -- and, in eval mode, the reference's forward on the HIP library:
+    (src_xyz [B,N,3], src_desc [B,C,N], dst_xyz, dst_desc, src_weights [B,N], dst_weights) ->
+    (corres_xyz [B,N,3], weights [B,N]).  HRegNet / Model_V2 run the True / True head fused inside
+    their own forward; a variant there, or this module alone, runs engine.coarse_reg with the
+    variant's absent similarity features as zero columns (engine._pad_coarse_convs1)."""
 
     def __init__(self, k, in_channels, use_sim=True, use_neighbor=True):
         super().__init__()
-        if not (use_sim and use_neighbor):
-            raise NotImplementedError("CoarseReg: only use_sim=use_neighbor=True (as HRegNet uses)")
-        self.k, self.use_sim, self.use_neighbor = k, use_sim, use_neighbor
+        self.k, self.use_sim, self.use_neighbor = k, bool(use_sim), bool(use_neighbor)
         C = in_channels
-        self.convs_1 = _stack([2 * C + 16, 2 * C, 2 * C, 2 * C])
+        extra = 12 + 2 * self.use_sim + 2 * self.use_neighbor
+        self.convs_1 = _stack([2 * C + extra, 2 * C, 2 * C, 2 * C])
         self.convs_2 = _stack([C + 4, C, C, C])
         self.mlp1, self.mlp2, self.mlp3 = _head(2 * C)
+        self._prep = _Prepared()
+
+    @property
+    def variant(self):
+        return (self.use_sim, self.use_neighbor)
+
+    def forward(self, src_xyz, src_desc, dst_xyz, dst_desc, src_weights, dst_weights):
+        if self.training:
+            raise NotImplementedError("CoarseReg alone runs in eval mode (the training step runs "
+                                      "inside HRegNet.train(), train_graph.py)")
+        B, N, _ = src_xyz.shape
+        C = src_desc.shape[1]
+        P = self._prep.get(_PrefixedHead(self, "coarse_corres"), src_xyz.device, self.variant)
+        xyz3 = torch.cat([src_xyz, dst_xyz]).float().contiguous()
+        desc3 = torch.cat([src_desc, dst_desc]).transpose(1, 2).reshape(2 * B * N, C).float().contiguous()
+        sig3 = torch.cat([src_weights, dst_weights]).reshape(-1).float().contiguous()
+        with torch.no_grad():
+            corres, w = engine.coarse_reg(P, B, xyz3, desc3, sig3)
+        return corres, w
 
 
 class FineReg(_HIPOnly):
@@ -127,10 +151,10 @@ class _Prepared:
         self.key = None
         self.value = None
 
-    def get(self, module, device):
-        key = _weights_key(module, device)
+    def get(self, module, device, coarse_variant=(True, True)):
+        key = _weights_key(module, device) + (tuple(coarse_variant),)
         if key != self.key:
-            self.value = engine.PreparedWeights(module.state_dict(), device)
+            self.value = engine.PreparedWeights(module.state_dict(), device, coarse_variant)
             self.key = key
         return self.value
 
@@ -193,7 +217,37 @@ class _Prefixed(nn.Module):
         return sd
 
 
+class _PrefixedHead(nn.Module):
+    """A registration head's state dict under its HRegNet name (prefix) beside dummy (never
+    used) feature-extraction and other head weights, so PreparedWeights can fold it alone."""
+
+    def __init__(self, head, prefix):
+        super().__init__()
+        object.__setattr__(self, "_h", head)
+        object.__setattr__(self, "_prefix", prefix)
+
+    def state_dict(self, *a, keep_vars=False, **k):
+        sd = {k_: v for k_, v in _dummy_heads().items() if not k_.startswith(self._prefix + ".")}
+        sd.update(_dummy_features())
+        sd.update({self._prefix + "." + n: v for n, v in self._h.state_dict(keep_vars=keep_vars).items()
+                   if not n.startswith("_")})
+        return sd
+
+
 _DUMMY = None
+_DUMMY_FE = None
+
+
+def _dummy_features():
+    global _DUMMY_FE
+    if _DUMMY_FE is None:
+        class _A:
+            use_fps = use_weights = True
+            freeze_detector = freeze_feats = False
+        with torch.random.fork_rng(devices=[]):
+            fe = HierFeatureExtraction(_A())
+        _DUMMY_FE = {"feature_extraction." + k: v for k, v in fe.state_dict().items()}
+    return _DUMMY_FE
 
 
 def _dummy_heads():
@@ -224,7 +278,7 @@ class HRegNet(nn.Module):
         self._prep = _Prepared()
 
     def prepared(self, device):
-        return self._prep.get(self, device)
+        return self._prep.get(self, device, self.coarse_corres.variant)
 
     def forward(self, src_points, dst_points):
         if self.training:
@@ -261,7 +315,7 @@ class Model_V2(nn.Module):
         self._prep = _Prepared()
 
     def prepared(self, device):
-        return self._prep.get(self, device)
+        return self._prep.get(self, device, self.coarse_corres.variant)
 
     def forward(self, src_points, dst_points):
         if self.training:

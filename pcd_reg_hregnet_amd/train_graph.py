@@ -730,6 +730,9 @@ def coarse_reg(m, s_xyz, s_desc, d_xyz, d_desc, s_w, d_w, hook=None, keep=None):
     the src neighbour branch on the side stream (gradient side 0), the dst one on the current
     stream (side 1, BN running updates queued into keep and applied after the src ones on the
     side stream; the caller joins it)."""
+    if not (getattr(m, "use_sim", True) and getattr(m, "use_neighbor", True)):
+        raise NotImplementedError("the training step builds CoarseReg(use_sim=True, use_neighbor=True) "
+                                  "only (as HRegNet, models.py:71); the variants run in eval mode")
     k = m.k
     B, N1, _ = s_xyz.shape
     N2 = d_xyz.shape[1]

@@ -968,3 +968,46 @@ def test_coarse_head_row_tiles(net, G):
     with pytest.raises(RuntimeError, match="(?i)unsupported"):
         _lib.call("hreg_corr_head6x", P.coarse_table6, 512, small, ud0, ud1, gidx, kx, G, corres, att, 2,
                   _lib.stream_handle())
+
+
+@pytest.mark.parametrize("use_sim,use_neighbor", [(True, True), (True, False), (False, True), (False, False)])
+def test_coarse_reg_variants_vs_oracle(net, use_sim, use_neighbor):
+    """CoarseReg(use_sim, use_neighbor) alone in eval mode (layers.py:237-244,
+    290, 315, 368-379) against the oracle's restatement of every variant, on the network's own
+    level-3 keypoints and descriptors of a LiDAR pair: the same descriptor-space and neighbour
+    kNN selections (canonical order), correspondences within the R/t bar and weights within
+    1e-5.  The variant's weights are the trained head's with the absent features' columns
+    dropped."""
+    from oracle import oracle
+    from pcd_reg_hregnet_amd import models, synthetic
+    s, d, _, _ = synthetic.lidar_batch(2, 16384, seed0=31)
+    with torch.no_grad():
+        out = net(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda())
+    sx, sdsc = out["src_feats"]["xyz_3"], out["src_feats"]["desc_3"]
+    dx, ddsc = out["dst_feats"]["xyz_3"], out["dst_feats"]["desc_3"]
+    B, N = sx.shape[:2]
+    g = torch.Generator().manual_seed(3)
+    sw = (0.5 + torch.rand(B, N, generator=g)).cuda()
+    dw = (0.5 + torch.rand(B, N, generator=g)).cuda()
+    m = models.CoarseReg(8, 256, use_sim, use_neighbor).cuda().eval()
+    ref = net.coarse_corres.state_dict()
+    keep = list(range(524)) + ([524, 525] if use_sim else []) + ([526, 527] if use_neighbor else [])
+    sd = dict(ref)
+    sd["convs_1.0.weight"] = ref["convs_1.0.weight"][:, keep].contiguous()
+    m.load_state_dict(sd)
+    corres, w = m(sx, sdsc, dx, ddsc, sw, dw)
+    torch.cuda.synchronize()
+    npsd = {"c." + k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    oc, ow, _ = oracle.coarse_reg(npsd, "c", sx.cpu().numpy(), sdsc.cpu().numpy(), dx.cpu().numpy(),
+                                  ddsc.cpu().numpy(), sw.cpu().numpy(), dw.cpu().numpy(),
+                                  use_sim=use_sim, use_neighbor=use_neighbor)
+    np.testing.assert_allclose(corres.cpu().numpy(), oc, rtol=0, atol=1e-4)
+    np.testing.assert_allclose(w.cpu().numpy(), ow, rtol=0, atol=1e-5)
+    if use_sim and use_neighbor:  # the module alone == the head inside HRegNet's forward
+        full = net.prepared(torch.device("cuda"))
+        from pcd_reg_hregnet_amd import engine
+        with torch.no_grad():
+            c2, w2 = engine.coarse_reg(full, B, torch.cat([sx, dx]).contiguous(),
+                                       torch.cat([sdsc, ddsc]).transpose(1, 2).reshape(2 * B * N, -1).contiguous(),
+                                       torch.cat([sw, dw]).reshape(-1).contiguous())
+        assert torch.equal(c2, corres) and torch.equal(w2, w)

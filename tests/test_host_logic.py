@@ -442,3 +442,32 @@ def test_bench_train_line_assembles_on_cpu():
                             nt=(80.0, 1000, 1e13), tn=(60.0, 900, 8e12), graphed=True)
     d = _check_line(line, "training")
     assert d["loss_first_last"] == [1.44, 5.93] and "configs[3]" in d["config"]["workload"]
+
+
+@pytest.mark.parametrize("use_sim,use_neighbor", [(True, True), (True, False), (False, True), (False, False)])
+def test_coarse_reg_variants_layout_and_padding(use_sim, use_neighbor):
+    """CoarseReg(use_sim, use_neighbor) (layers.py:237-244): convs_1 over 2C + 16 / 14 / 14 / 12
+    inputs, convs_2 present in every variant; PreparedWeights widens convs_1[0] to the 2C + 16
+    layout with zero columns exactly where the variant has no similarity feature."""
+    from pcd_reg_hregnet_amd import engine, models
+    C = 256
+    m = models.CoarseReg(8, C, use_sim, use_neighbor)
+    W = m.convs_1[0].weight.detach().clone()
+    assert W.shape[1] == 2 * C + 12 + 2 * use_sim + 2 * use_neighbor
+    assert m.convs_2[0].weight.shape[1] == C + 4
+    sd = {"coarse_corres.convs_1.0.weight": W.clone(), "coarse_corres.convs_2.0.weight": m.convs_2[0].weight}
+    engine._pad_coarse_convs1(sd, use_sim, use_neighbor)
+    W16 = sd["coarse_corres.convs_1.0.weight"]
+    assert W16.shape[1] == 2 * C + 16
+    assert torch.equal(W16[:, :2 * C + 12], W[:, :2 * C + 12])
+    sims = W16[:, 2 * C + 12:]
+    present = [use_sim, use_sim, use_neighbor, use_neighbor]
+    src = iter(range(2 * C + 12, W.shape[1]))
+    for j, p in enumerate(present):
+        if p:
+            assert torch.equal(sims[:, j], W[:, next(src)])
+        else:
+            assert not sims[:, j].any()
+    with pytest.raises(ValueError):
+        engine._pad_coarse_convs1({"coarse_corres.convs_1.0.weight": W[:, :-2].clone(),
+                                   "coarse_corres.convs_2.0.weight": m.convs_2[0].weight}, use_sim, use_neighbor)
