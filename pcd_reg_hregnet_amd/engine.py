@@ -934,7 +934,7 @@ def knn_idx32(p1, p2, k, out=None):
 # ------------------------------------------------------------------ stages
 
 SPATIAL_KNN_MIN = 4096  # clouds at least this large group through the spatial index
-SPATIAL_KNN_MAX = switches.integer("SPATIAL_KNN_MAX", 65536)  # <= csrc/knn.hip SI_MAXN
+SPATIAL_KNN_MAX = 65536  # = csrc/knn.hip SI_MAXN
 
 
 # Tests set this to a dict to receive every kNN selection of an eager forward as cloud-

@@ -35,7 +35,7 @@ BN_EPS = 1e-5
 # level, tools/train_ab.sh) and the reference-gradient test's d/d dst_sigmas_3 error moves
 # to 1.16x its bar.
 TRAIN_B6 = switches.flag("TRAIN_B6", False)
-TRAIN_B6_MIN_N = switches.integer("TRAIN_B6_MIN_N", 128)
+TRAIN_B6_MIN_N = 128
 
 
 def _stream():
