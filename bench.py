@@ -388,7 +388,7 @@ def _fps_level(pts, m, weights, floor_call, floor_pts, floor_w, kernel):
     nb, n, _ = pts.shape
     st_ = _lib.stream_handle()
     idx = torch.empty(nb, m, dtype=torch.int32, device=pts.device)
-    temp = torch.empty(nb, n, device=pts.device)
+    temp = torch.full((nb, n), 1e10, device=pts.device)  # (the initial running minima, models/utils.py:25)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     name = "hreg_weighted_furthest_point_sampling" if weights is not None else "hreg_furthest_point_sampling"
     args = (nb, n, m, pts, weights, temp, idx, None, st_) if weights is not None else \

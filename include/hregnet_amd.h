@@ -74,11 +74,14 @@ enum {
 
 /* ---------------- point_utils_cuda boundary ---------------- */
 
-/* points [b,n,3] f32, temp [b,n] f32 scratch (required for n > 16384, may be NULL
- * below; for n <= 16384 it receives the final running-min distances, above its
- * contents are unspecified -- it holds the workgroups' exchange slots; the
- * reference's caller discards temp, models/utils.py:24-27), idx [b,m] int32 (out),
- * sampled_xyz [b,m,3] (optional out: gathered coordinates of idx). */
+/* points [b,n,3] f32, temp [b,n] f32 (required for n > 16384, may be NULL below): for n <=
+ * 16384 (weighted: 8192) its contents are the initial running minima, read as the reference's
+ * kernel reads them (.cu:130, d2 = min(d, temp[k]); its callers fill 1e10, models/utils.py:25;
+ * NULL: 1e10) and it receives the final running minima; above, the multi-workgroup kernel keeps
+ * its exchange slots there (contents not read, unspecified after), and the single-workgroup
+ * memory kernel (when the spin budget cannot hold a cluster) its running minima (read and
+ * written as the reference's), idx [b,m] int32 (out), sampled_xyz [b,m,3] (optional out:
+ * gathered coordinates of idx). */
 /* hreg_furthest_point_sampling for a caller that guarantees at most `concurrent` (>= 1)
  * multi-workgroup FPS launches (clouds above 16384 points) of this process run at once -- e.g. a
  * graph whose one stage-1 stream carries all of them: such a launch may keep more clouds' worker

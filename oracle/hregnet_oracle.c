@@ -49,12 +49,13 @@ int oracle_opt_n_threads(int work_size) {
 }
 
 /* .cu:84-206 / .cu:254-375, one cloud.  weights may be NULL (plain FPS).
- * temp is caller scratch [n] (filled with 1e10 here, as models/utils.py:25). */
-static void fps_one_cloud(const float *xyz, const float *w, int n, int m,
+ * temp is scratch [n]: the initial running minima are temp0's (the caller's temp, .cu:130), or
+ * 1e10 when temp0 is NULL (as models/utils.py:25 fills it). */
+static void fps_one_cloud(const float *xyz, const float *w, const float *temp0, int n, int m,
                           float *temp, float *dists, int *dists_i, int32_t *idx) {
     const int bs = oracle_opt_n_threads(n);
     if (m <= 0) return;
-    for (int k = 0; k < n; ++k) temp[k] = 1e10f;
+    for (int k = 0; k < n; ++k) temp[k] = temp0 ? temp0[k] : 1e10f;
     int old = 0;
     idx[0] = old;
     for (int j = 1; j < m; ++j) {
@@ -88,8 +89,10 @@ static void fps_one_cloud(const float *xyz, const float *w, int n, int m,
     }
 }
 
-/* furthest_point_sampling_wrapper (fps.cpp:33-43) semantics over b clouds. */
-int oracle_fps(const float *xyz, const float *weights, int b, int n, int m, int32_t *idx) {
+/* furthest_point_sampling_wrapper (fps.cpp:33-43) semantics over b clouds; temp0 [b][n] the
+ * caller's temp contents (NULL: 1e10). */
+int oracle_fps_temp(const float *xyz, const float *weights, const float *temp0, int b, int n, int m,
+                    int32_t *idx) {
     if (b <= 0 || n <= 0 || m <= 0) return 0;
     int rc = 0;
 #pragma omp parallel for schedule(dynamic, 1)
@@ -100,12 +103,17 @@ int oracle_fps(const float *xyz, const float *weights, int b, int n, int m, int3
         if (!temp || !dists || !dists_i) {
             rc = -1;
         } else {
-            fps_one_cloud(xyz + (size_t)c * n * 3, weights ? weights + (size_t)c * n : NULL, n, m,
-                          temp, dists, dists_i, idx + (size_t)c * m);
+            fps_one_cloud(xyz + (size_t)c * n * 3, weights ? weights + (size_t)c * n : NULL,
+                          temp0 ? temp0 + (size_t)c * n : NULL, n, m, temp, dists, dists_i,
+                          idx + (size_t)c * m);
         }
         free(temp); free(dists); free(dists_i);
     }
     return rc;
+}
+
+int oracle_fps(const float *xyz, const float *weights, int b, int n, int m, int32_t *idx) {
+    return oracle_fps_temp(xyz, weights, NULL, b, n, m, idx);
 }
 
 /* gather_points_kernel_fast (.cu:7-21): out[b,c,j] = points[b,c,idx[b,j]] */

@@ -41,6 +41,8 @@ def lib():
         L.oracle_opt_n_threads.restype = ctypes.c_int
         L.oracle_fps.argtypes = [f32p, f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, i32p]
         L.oracle_fps.restype = ctypes.c_int
+        L.oracle_fps_temp.argtypes = [f32p, f32p, f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, i32p]
+        L.oracle_fps_temp.restype = ctypes.c_int
         L.oracle_knn.argtypes = [f32p, f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, i32p, f32p]
         L.oracle_knn.restype = ctypes.c_int
@@ -68,10 +70,12 @@ def opt_n_threads(n: int) -> int:
     return lib().oracle_opt_n_threads(int(n))
 
 
-def fps(xyz: np.ndarray, npoint: int, weights: np.ndarray | None = None) -> np.ndarray:
+def fps(xyz: np.ndarray, npoint: int, weights: np.ndarray | None = None,
+        temp0: np.ndarray | None = None) -> np.ndarray:
     """furthest_point_sampling_gpu.cu:84-206 (weights=None) / :254-375 (weighted).
 
-    xyz [B,N,3] f32, weights [B,N] f32 -> idx [B,npoint] int32.
+    xyz [B,N,3] f32, weights [B,N] f32 -> idx [B,npoint] int32.  temp0 [B,N]: the caller's temp
+    contents, the kernel's initial running minima (.cu:130); None: 1e10 (models/utils.py:25).
     """
     xyz = np.ascontiguousarray(xyz, dtype=np.float32)
     B, N, _ = xyz.shape
@@ -80,7 +84,10 @@ def fps(xyz: np.ndarray, npoint: int, weights: np.ndarray | None = None) -> np.n
     if weights is not None:
         w = np.ascontiguousarray(weights, dtype=np.float32)
         assert w.shape == (B, N)
-    rc = lib().oracle_fps(_fp(xyz), _fp(w) if w is not None else None, B, N, npoint, _ip(out))
+    t0 = None if temp0 is None else np.ascontiguousarray(temp0, dtype=np.float32)
+    assert t0 is None or t0.shape == (B, N)
+    rc = lib().oracle_fps_temp(_fp(xyz), _fp(w) if w is not None else None,
+                               _fp(t0) if t0 is not None else None, B, N, npoint, _ip(out))
     assert rc == 0
     return out
 

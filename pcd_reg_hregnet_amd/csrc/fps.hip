@@ -215,9 +215,12 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
         VY[s] = P[kk * 3 + 1];
         VZ[s] = P[kk * 3 + 2];
         PW[s / 2][s % 2] = WEIGHTED ? W[kk] : 1.0f;
-        // invalid slots can never be selected: d2 = -inf never reaches the max
-        if constexpr (PM) VT[s] = ok ? 1e10f : -__builtin_huge_valf();
-        else PT[s / 2][s % 2] = ok ? 1e10f : -__builtin_huge_valf();
+        // the caller's temp is the initial running minimum, as the reference reads it (.cu:130:
+        // d2 = min(d, temp[k]); models/utils.py:25 fills 1e10); without one, 1e10.  Invalid
+        // slots can never be selected: d2 = -inf never reaches the max
+        const float t0 = temp_out ? temp_out[(size_t)cloud * n + kk] : 1e10f;
+        if constexpr (PM) VT[s] = ok ? t0 : -__builtin_huge_valf();
+        else PT[s / 2][s % 2] = ok ? t0 : -__builtin_huge_valf();
     }
     // opaque: pick_slot must read its coordinates from these tuples, not from the loaded
     // scalars (otherwise every point stays live twice: +96 VGPRs at 32 slots)
@@ -407,7 +410,8 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float *__restrict__ xy
 }
 
 // Fallback for clouds too large for the register-resident path (n > 16384):
-// temp lives in the caller's buffer; same key, same winner.
+// temp lives in the caller's buffer (its contents are the initial running minima, as in the
+// reference); same key, same winner.
 template <bool WEIGHTED>
 __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__ xyz,
                                                       const float *__restrict__ wts,
@@ -423,8 +427,6 @@ __global__ __launch_bounds__(1024) void fps_mem_kernel(const float *__restrict__
     const float *W = WEIGHTED ? wts + (size_t)cloud * n : nullptr;
     float *tp = temp + (size_t)cloud * n;
     const int G = bs / T > 0 ? bs / T : 1;
-    for (int k = tid; k < n; k += T) tp[k] = 1e10f;
-    __syncthreads();
     float x1 = P[0], y1 = P[1], z1 = P[2];
     if (tid == 0) {
         idx_out[(size_t)cloud * m] = 0;

@@ -103,6 +103,8 @@ CHAIN_FORK = switches.flag("CHAIN_FORK", True)
 # r6, 16384 < n <= 65536 with n % 64 == 0 (fps_blocks_kernel: Model_V2's 65536-point clouds on ONE
 # workgroup each instead of the cluster kernel's 32 spinning single-wave participants).
 FPS_SORTED = switches.flag("FPS_SORTED", True)
+# the level-2/3 input projections (LEVEL_PRE) on hreg_gemm6 instead of the fp32-MFMA hreg_gemm
+LEVEL_PRE_B6 = switches.flag("LEVEL_PRE_B6", False)
 FPS_SORTED_N = 16384
 
 
@@ -821,9 +823,12 @@ def fps(xyz, npoint, weights=None, out=None, concurrent=0):
         sampled = _empty(nb, npoint, 3, device=dev)
     else:
         idx, sampled = out
-    # temp: exchange slots of the multi-workgroup kernel, which also takes weighted
-    # clouds above 8192 points (their register geometry has no single-workgroup case)
-    temp = _empty(nb, n, device=dev) if n > 8192 else None
+    # temp: the register kernels read a caller's temp as the initial running minima (the
+    # reference's semantics), so they get none (1e10); above their sizes (n > 16384, weighted
+    # n > 8192) the multi-workgroup kernel keeps its exchange slots there, or the memory kernel its
+    # running minima (then from 1e10, models/utils.py:25)
+    big = n > 16384 or (weights is not None and n > 8192)
+    temp = torch.full((nb, n), 1e10, device=dev) if big else None
     _status_pending |= n > 16384 or (weights is not None and n > 8192)
     if weights is None and concurrent > 0:
         call("hreg_fps_bounded", nb, n, npoint, xyz, temp, idx, sampled, concurrent, _stream())
@@ -1097,7 +1102,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         pre = _empty(feats.shape[0], lin.N, device=feats.device)
         main, side = fk
         with torch.cuda.stream(side):
-            gemm([_seg(feats, 0, Cf)], lin, feats.shape[0], out=pre)
+            gemm([_seg(feats, 0, Cf)], lin, feats.shape[0], out=pre, b6=LEVEL_PRE_B6)
         grouped = grouping(xyz, lvl, weights, sample=sample)
         main.wait_stream(side)
     elif grouped is None:
@@ -1123,7 +1128,8 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         desc = _empty(G, LEVELS[lvl][5], device=dev)
         name, table, b6 = _fused23_kernel(P, lvl)
         if pre is None and LEVEL_PRE:
-            pre = gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl], feats.shape[0])
+            pre = gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl], feats.shape[0],
+                       b6=LEVEL_PRE_B6)
         if name == "hreg_group_split6_l3" and pre is not None and SPLIT_JT:
             name = "hreg_group_split6j_l3"
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())

@@ -95,7 +95,7 @@ def test_fps_indexed_matches_fps(kind, n):
     temp = torch.full((B, n), -1.0, device="cuda")
     _lib.call("hreg_fps_indexed", B, n, m, x, ws, temp, idx, None, _lib.stream_handle())
     ref = torch.full((B, m), -2, dtype=torch.int32, device="cuda")
-    rtemp = torch.full((B, n), -2.0, device="cuda")
+    rtemp = torch.full((B, n), 1e10, device="cuda")  # (read: the reference's initial running minima)
     _lib.call("hreg_furthest_point_sampling", B, n, m, x, rtemp, ref, None, _lib.stream_handle())
     torch.cuda.synchronize()
     got = idx.cpu().numpy()
@@ -175,6 +175,29 @@ def test_fps_cluster_many_clouds_and_mem_path():
         del os.environ["HREG_FPS_MEM"]
     np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
     np.testing.assert_array_equal(a.cpu().numpy()[:2], oracle.fps(xyz[:2], m, None))
+
+
+@pytest.mark.parametrize("n,m,weighted", [(16384, 256, False), (1024, 200, True), (700, 100, False)])
+def test_fps_reads_callers_temp(n, m, weighted):
+    """The caller's temp is the initial running minimum (.cu:130: d2 = min(d, temp[k]); the
+    reference's callers fill 1e10, models/utils.py:25, but the boundary's contract is the
+    kernel's): random initial minima, some below every distance (those points are never taken),
+    against the oracle with the same temp."""
+    from pcd_reg_hregnet_amd import point_utils_cuda as pu
+    rng = np.random.default_rng(n + m)
+    B = 3
+    xyz = rng.uniform(-40, 40, (B, n, 3)).astype(np.float32)
+    t0 = rng.uniform(0, 3000, (B, n)).astype(np.float32)
+    t0[:, ::7] = 1e10
+    t0[:, 3::11] = 0.0
+    w = rng.uniform(0.1, 2.0, (B, n)).astype(np.float32) if weighted else None
+    idx = torch.empty((B, m), dtype=torch.int32, device="cuda")
+    temp = dev(t0)
+    if weighted:
+        pu.weighted_furthest_point_sampling_wrapper(B, n, m, dev(xyz), dev(w), temp, idx)
+    else:
+        pu.furthest_point_sampling_wrapper(B, n, m, dev(xyz), temp, idx)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oracle.fps(xyz, m, w, temp0=t0))
 
 
 def test_fps_zero_points_requested():
