@@ -103,8 +103,6 @@ CHAIN_FORK = switches.flag("CHAIN_FORK", True)
 # r6, 16384 < n <= 65536 with n % 64 == 0 (fps_blocks_kernel: Model_V2's 65536-point clouds on ONE
 # workgroup each instead of the cluster kernel's 32 spinning single-wave participants).
 FPS_SORTED = switches.flag("FPS_SORTED", True)
-# the level-2/3 input projections (LEVEL_PRE) on hreg_gemm6 instead of the fp32-MFMA hreg_gemm
-LEVEL_PRE_B6 = switches.flag("LEVEL_PRE_B6", False)
 FPS_SORTED_N = 16384
 
 
@@ -1102,7 +1100,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         pre = _empty(feats.shape[0], lin.N, device=feats.device)
         main, side = fk
         with torch.cuda.stream(side):
-            gemm([_seg(feats, 0, Cf)], lin, feats.shape[0], out=pre, b6=LEVEL_PRE_B6)
+            gemm([_seg(feats, 0, Cf)], lin, feats.shape[0], out=pre)
         grouped = grouping(xyz, lvl, weights, sample=sample)
         main.wait_stream(side)
     elif grouped is None:
@@ -1128,8 +1126,7 @@ def keypoint_level(P: PreparedWeights, lvl: int, xyz, feats, weights, grouped=No
         desc = _empty(G, LEVELS[lvl][5], device=dev)
         name, table, b6 = _fused23_kernel(P, lvl)
         if pre is None and LEVEL_PRE:
-            pre = gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl], feats.shape[0],
-                       b6=LEVEL_PRE_B6)
+            pre = gemm([_seg(feats, 0, Cf)], (P.level_pre6 if b6 else P.level_pre)[lvl], feats.shape[0])
         if name == "hreg_group_split6_l3" and pre is not None and SPLIT_JT:
             name = "hreg_group_split6j_l3"
         call(name, table, geom, kx, gidx, feats, G, kp, att_feat, desc, pre, _stream())

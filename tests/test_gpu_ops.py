@@ -662,3 +662,35 @@ def test_engine_fps_weighted_mid_size():
         torch.cuda.synchronize()
         np.testing.assert_array_equal(idx.cpu().numpy(), oracle.fps(xyz, m, w))
     engine.check_device_status()
+
+
+@pytest.mark.parametrize("K", [8, 64])
+def test_knn_points_ragged_lengths(K):
+    """knn_points(lengths1, lengths2) (pytorch3d's ragged batches, r6): every cloud's valid
+    rows are the dense kernel's selections over its first lengths2[b] points (oracle.knn on
+    the sliced clouds, bit-exact); padded rows and slots beyond lengths2 are dist 0 / idx -1
+    (padding values parity unpinned); return_nn / knn_gather(lengths) zero those slots."""
+    from pcd_reg_hregnet_amd.knn import knn_gather, knn_points
+    rng = np.random.default_rng(K)
+    B, N1, N2 = 4, 300, 500
+    p1 = rng.normal(size=(B, N1, 3)).astype(np.float32)
+    p2 = rng.normal(size=(B, N2, 3)).astype(np.float32)
+    l1 = np.array([300, 0, 17, 250])
+    l2 = np.array([500, 40, 5, 64])
+    d, i, nn = knn_points(dev(p1), dev(p2), lengths1=dev(l1), lengths2=dev(l2), K=K, return_nn=True)
+    d, i, nn = d.cpu().numpy(), i.cpu().numpy(), nn.cpu().numpy()
+    for b in range(B):
+        if l1[b]:
+            rd, ri = oracle.knn(p1[b:b + 1, :l1[b]], p2[b:b + 1, :l2[b]], K)
+            np.testing.assert_array_equal(i[b, :l1[b]], ri[0])
+            np.testing.assert_array_equal(d[b, :l1[b]], rd[0])
+            want_nn = oracle.knn_gather(p2[b:b + 1, :l2[b]], np.maximum(ri, 0))[0]
+            want_nn[ri[0] < 0] = 0.0  # slots beyond the cloud's points
+            np.testing.assert_array_equal(nn[b, :l1[b]], want_nn)
+        assert (i[b, l1[b]:] == -1).all() and (d[b, l1[b]:] == 0).all()
+    # knn_gather's own lengths mask on a dense index
+    idx = rng.integers(0, N2, (B, 7, K)).astype(np.int64)
+    out = knn_gather(dev(p2), dev(idx), lengths=dev(l2)).cpu().numpy()
+    want = oracle.knn_gather(p2, idx)
+    want[np.arange(K)[None, None, :] >= l2[:, None, None]] = 0.0
+    np.testing.assert_array_equal(out, want)

@@ -4,7 +4,9 @@ captured while its switches are set (engine module attributes) and created in mi
 (A B B A) to cancel the creation-order bias; the timed rounds then alternate over all of them
 exactly as bench.py times one (barrier-free: one GPU).
 
-usage: python tools/ab_graph.py [--steps 20] [--reps 8] VARIANT [VARIANT ...]
+usage: python tools/ab_graph.py [--steps 12] [--merge 4] [--reps 8] VARIANT [VARIANT ...]
+  (--steps: executor forwards of --merge reference batches each, one lane per forward: the
+  bench's default graph executor, 48 batches = 12 merged forwards on 12 lanes)
   VARIANT = comma-separated key=value (or "base"): engine.FLAG=0, or probe.nofps1=1 / probe.nostage1=1
   (timing probes, results wrong: the level-1 FPS, or the whole level-1 grouping, replaced by a
   copy of a cached result, to price its share of the step)
@@ -91,8 +93,9 @@ def revert(undo, lib, engine):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--merge", type=int, default=bench.HREGNET_MERGE)
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
@@ -101,7 +104,8 @@ def main():
     dev = torch.device("cuda")
     net = bench.make_model(dev)
     P = net.prepared(dev)
-    s, d, _, _ = bench.shard_batch(0, bench.PAIRS_PER_GPU, bench.POINTS)
+    s, d, _, _ = bench.shard_batch(0, bench.PAIRS_PER_GPU * a.merge, bench.POINTS)
+    sb = bench.PAIRS_PER_GPU if a.merge > 1 else None
     src, dst = torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev)
     # every variant twice, created in mirrored order (A B ... B A): pipelines created earlier
     # measured ~3-4 % faster than later ones in the same process (the same variant in first and
@@ -112,7 +116,7 @@ def main():
         for v in order:
             undo = apply(v, lib, engine)
             engine.grouping(torch.cat([src, dst], 0), 0)  # (fills a probe's cache uncaptured)
-            g = engine.GraphPipeline(P, src, dst, lanes=a.steps)
+            g = engine.GraphPipeline(P, src, dst, lanes=a.steps, sub_batch=sb)
             g.prepare(a.warmup)
             g.prepare(a.steps)
             g.run_forwards(a.warmup, stream=True)
@@ -141,7 +145,7 @@ def main():
     out = {}
     for v in a.variants:
         med = statistics.median(times[v])
-        out[v] = {"ms_per_step_median": round(med, 4), "pairs_per_s": round(bench.PAIRS_PER_GPU / med * 1e3, 1),
+        out[v] = {"ms_per_step_median": round(med, 4), "pairs_per_s": round(bench.PAIRS_PER_GPU * a.merge / med * 1e3, 1),
                   "vs_first": round(base / med, 4), "all": [round(t, 4) for t in times[v]]}
     print(json.dumps(out))
 

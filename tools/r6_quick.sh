@@ -19,6 +19,8 @@ fi
 i=0
 for A in "$@"; do
   i=$((i+1))
-  env $(echo "$A" | grep -o '^HREG_[A-Z_]*=[^ ]*') timeout -k 10 400 python bench.py ${A#HREG_*=* } > $O/bench$i.json 2> $O/bench$i.err || { echo "bench $i failed"; tail $O/bench$i.err; exit 1; }
+  ENVS=(); ARGS="$A"
+  while [[ $ARGS == HREG_* ]]; do ENVS+=("${ARGS%% *}"); [[ $ARGS == *" "* ]] && ARGS="${ARGS#* }" || ARGS=""; done
+  env "${ENVS[@]}" timeout -k 10 400 python bench.py $ARGS > $O/bench$i.json 2> $O/bench$i.err || { echo "bench $i failed"; tail $O/bench$i.err; exit 1; }
   python -c "import json; d=json.load(open('$O/bench$i.json')); print('$A', '->', d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('frac'), (d.get('fps') or {}).get('level1', {}).get('us_per_iteration') if isinstance(d.get('fps'), dict) else None)"
 done

@@ -24,7 +24,7 @@ import sys
 from collections import defaultdict
 
 FAMILIES = ("gemm_nt_kernel", "group_l1_kernel", "group_l1_6_kernel", "group_fused_kernel",
-            "group_fused6_kernel", "group_split_kernel", "group_split6_kernel", "group_split6j_kernel", "group_split6p_kernel", "fine_head_kernel",
+            "group_fused6_kernel", "group_split_kernel", "group_split6_kernel", "group_split6j_kernel", "fine_head_kernel",
             "fine_head6_kernel", "nbr_head_kernel", "nbr_head6_kernel", "mlp_head_kernel", "fps_reg_kernel", "knn_group", "spatial_index_kernel",
             "attend_kernel", "knnd_kernel", "knnd_wave_kernel", "coarse_head6_kernel")
 
