@@ -396,6 +396,121 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float *__restrict__ 
     }
 }
 
+// gemm_tn_kernel with the operands staged through LDS (r6): each 64-row step of a workgroup
+// is loaded by all 256 threads as 16-byte row segments (4 + 4 buffer_load_dwordx4 per thread
+// at 64 x 64 instead of 32 + 32 dword loads per lane, which kept the weight-gradient GEMMs at
+// ~2.4 TB/s), one step ahead in registers; each wave then reads its 16 rows' MFMA operands
+// from LDS.  Wave w still takes rows 16 w .. 16 w + 15 of every step in the same k-step order,
+// so every output is the same sum as gemm_tn_kernel's (that kernel stays for row strides or
+// bases that are not 16-byte aligned).
+template <int TNN, int TNK>
+__global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__ A, int lda,
+                                                       const float *__restrict__ Bm, int ldb, int R,
+                                                       int N, int K, int rows_per_split,
+                                                       float *__restrict__ ws) {
+    constexpr int WA = 32 * TNN, WB = 32 * TNK, TW = WB;  // tile widths (floats)
+    constexpr int FA = WA / 4, FB = WB / 4;               // float4 per row
+    constexpr int LA = TN_ROWS * FA / 256, LB = TN_ROWS * FB / 256;  // float4 loads per thread
+    constexpr int STAGE = TN_ROWS * (WA + WB);
+    constexpr int RED = 3 * WA * WB;
+    __shared__ __attribute__((aligned(16))) float lds[STAGE > RED ? STAGE : RED];
+    float *As = lds, *Bs = lds + TN_ROWS * WA;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int h = lane >> 5, j = lane & 31;
+    const int n0 = blockIdx.x * WA, k0 = blockIdx.y * WB;
+    const int r0 = blockIdx.z * rows_per_split;
+    const int r1 = min(R, r0 + rows_per_split);
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(A), (short)0,
+                                                      (int)((size_t)R * lda * sizeof(float)), 0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Bm), (short)0,
+                                                      (int)((size_t)R * ldb * sizeof(float)), 0x00020000);
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    f32x16 acc[TNN][TNK];
+#pragma unroll
+    for (int a = 0; a < TNN; ++a)
+#pragma unroll
+        for (int b = 0; b < TNK; ++b)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+    v4f ga[LA], gb[LB];
+    // rows past R read 0 (buffer bounds); columns past N / K feed only accumulator entries that
+    // are never stored (the tile's columns stay inside the row: lda >= N, ldb >= K, 4 | lda, ldb)
+    auto gload = [&](int base) {
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+            const int e = tid + 256 * i, r = e / FA, c4 = e - r * FA;
+            const uint32_t off = ((uint32_t)(base + r) * (uint32_t)lda + n0 + 4 * c4) * 4u;
+            ga[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+            const int e = tid + 256 * i, r = e / FB, c4 = e - r * FB;
+            const uint32_t off = ((uint32_t)(base + r) * (uint32_t)ldb + k0 + 4 * c4) * 4u;
+            gb[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0));
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < LA; ++i) *reinterpret_cast<v4f *>(As + 4 * (tid + 256 * i)) = ga[i];
+#pragma unroll
+        for (int i = 0; i < LB; ++i) *reinterpret_cast<v4f *>(Bs + 4 * (tid + 256 * i)) = gb[i];
+    };
+    const int nit = r1 > r0 ? (r1 - r0 + TN_ROWS - 1) / TN_ROWS : 0;
+    if (nit) gload(r0);
+    for (int it = 0; it < nit; ++it) {
+        __syncthreads();  // the previous step's operand reads are done
+        lstore();
+        __syncthreads();
+        if (it + 1 < nit) gload(r0 + (it + 1) * TN_ROWS);
+        // k-step s of wave w: rows 16 w + 2 s + h (gemm_tn_kernel's order)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int r = 16 * w + 2 * s + h;
+            float va[TNN], vb[TNK];
+#pragma unroll
+            for (int a = 0; a < TNN; ++a) va[a] = As[r * WA + 32 * a + j];
+#pragma unroll
+            for (int b = 0; b < TNK; ++b) vb[b] = Bs[r * WB + 32 * b + j];
+#pragma unroll
+            for (int a = 0; a < TNN; ++a)
+#pragma unroll
+                for (int b = 0; b < TNK; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(va[a], vb[b], acc[a][b], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // the staging buffer becomes the cross-wave reduction buffer
+    // acc[a][b][q]: tile row n = 32 a + (q&3) + 8(q>>2) + 4h, column k = 32 b + j
+    if (w > 0) {
+        float *o = lds + (w - 1) * WA * WB;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
+#pragma unroll
+            for (int a = 0; a < TNN; ++a)
+#pragma unroll
+                for (int b = 0; b < TNK; ++b) o[(32 * a + n) * TW + 32 * b + j] = acc[a][b][q];
+        }
+    }
+    __syncthreads();
+    if (w != 0) return;
+    float *o = ws + (size_t)blockIdx.z * N * K;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
+#pragma unroll
+        for (int a = 0; a < TNN; ++a)
+#pragma unroll
+            for (int b = 0; b < TNK; ++b) {
+                const int nn = 32 * a + n, kk = 32 * b + j;
+                float v = acc[a][b][q];
+                v = fadd_rn(v, lds[0 * WA * WB + nn * TW + kk]);
+                v = fadd_rn(v, lds[1 * WA * WB + nn * TW + kk]);
+                v = fadd_rn(v, lds[2 * WA * WB + nn * TW + kk]);
+                if (n0 + nn < N && k0 + kk < K) o[(size_t)(n0 + nn) * K + k0 + kk] = v;
+            }
+    }
+}
+
 // out[i] = beta * out[i] + sum_z ws[z][i], z in order.  With many splits a workgroup
 // takes 16 outputs x 16 split lanes (lane l sums z = l, l+16, ... in order, then the 16
 // lanes in order); with few, one thread per output.
@@ -651,14 +766,26 @@ static int gemm_tn_launch(const float *A, int lda, const float *B, int ldb, int 
     // tile of MFMAs across it instead of two
     const int tnn = N <= 32 ? 1 : 2, tnk = K <= 32 ? 1 : 2;
     const dim3 grid((N + 32 * tnn - 1) / (32 * tnn), (K + 32 * tnk - 1) / (32 * tnk), S);
-    if (tnn == 1 && tnk == 1)
-        hipLaunchKernelGGL((gemm_tn_kernel<1, 1>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws);
-    else if (tnn == 1)
-        hipLaunchKernelGGL((gemm_tn_kernel<1, 2>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws);
-    else if (tnk == 1)
-        hipLaunchKernelGGL((gemm_tn_kernel<2, 1>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws);
-    else
-        hipLaunchKernelGGL((gemm_tn_kernel<2, 2>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws);
+    // 16-byte row segments through LDS when the rows allow them (gemm_tn4_kernel: the same sums)
+    // (r6, train bench paired on one box: 422 / 426 vs 413 / 419 pairs/s, gpurun_out/r6tn)
+    const bool v4 = !(lda & 3) && !(ldb & 3) && !(reinterpret_cast<uintptr_t>(A) & 15) &&
+                    !(reinterpret_cast<uintptr_t>(B) & 15);
+#define TN_LAUNCH(KER, a, b)                                                                           \
+    hipLaunchKernelGGL((KER<a, b>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, (float *)ws)
+#define TN_CASE(a, b)                        \
+    if (v4) TN_LAUNCH(gemm_tn4_kernel, a, b); \
+    else TN_LAUNCH(gemm_tn_kernel, a, b)
+    if (tnn == 1 && tnk == 1) {
+        TN_CASE(1, 1);
+    } else if (tnn == 1) {
+        TN_CASE(1, 2);
+    } else if (tnk == 1) {
+        TN_CASE(2, 1);
+    } else {
+        TN_CASE(2, 2);
+    }
+#undef TN_CASE
+#undef TN_LAUNCH
     HREG_CHECK_LAUNCH();
     const size_t NK = (size_t)N * K;
     if (S >= 16)

@@ -692,5 +692,5 @@ def test_knn_points_ragged_lengths(K):
     idx = rng.integers(0, N2, (B, 7, K)).astype(np.int64)
     out = knn_gather(dev(p2), dev(idx), lengths=dev(l2)).cpu().numpy()
     want = oracle.knn_gather(p2, idx)
-    want[np.arange(K)[None, None, :] >= l2[:, None, None]] = 0.0
+    want[np.broadcast_to(np.arange(K)[None, None, :] >= l2[:, None, None], want.shape[:3])] = 0.0
     np.testing.assert_array_equal(out, want)

@@ -159,6 +159,26 @@ def test_gemm_tn_and_transpose():
         assert torch.equal(transpose(A), A.t().contiguous())
 
 
+@pytest.mark.parametrize("R,N,K", [(70000, 64, 64), (4096, 64, 32), (1000, 32, 32), (12345, 128, 260), (64, 96, 8)])
+def test_gemm_tn_lds_staged_bitwise(R, N, K):
+    """r6: the 16-byte-row LDS-staged weight-gradient kernel (gemm_tn4_kernel, taken when row
+    strides and bases are 16-byte aligned) gives the dword-load kernel's bits (taken here through
+    row strides N + 1, K + 1: the same rows in the same k-step order per wave)."""
+    from pcd_reg_hregnet_amd.train import gemm_tn
+    g = torch.Generator(device="cpu").manual_seed(R + N + K)
+    A = torch.randn(R, N, generator=g).cuda()
+    B = torch.randn(R, K, generator=g).cuda()
+    A1 = torch.zeros(R, N + 1, device="cuda")[:, :N]
+    B1 = torch.zeros(R, K + 1, device="cuda")[:, :K]
+    A1.copy_(A)
+    B1.copy_(B)
+    assert A1.stride(0) % 4 and B1.stride(0) % 4
+    staged, plain = gemm_tn(A, B), gemm_tn(A1, B1)
+    assert torch.equal(staged, plain)
+    ref = A.double().t() @ B.double()
+    torch.testing.assert_close(staged.double(), ref, rtol=1e-4, atol=1e-3 * R ** 0.5 / 100)
+
+
 def test_bn_stats_deterministic_and_accurate():
     from pcd_reg_hregnet_amd.train import bn_stats
     y = (torch.randn(300000, 48, generator=torch.Generator().manual_seed(1)) * 3 + 100).cuda()
