@@ -414,14 +414,16 @@ def _check_line(line, metric_word):
     return d
 
 
-@pytest.mark.parametrize("model", ["hregnet", "v2"])
+@pytest.mark.parametrize("model", ["hregnet", "v2", "b32"])
 def test_bench_forward_line_assembles_on_cpu(model):
     """every bench mode's JSON line is assembled by a pure function from its
     measurements, so a NameError in the assembly (r5's bench_train `merge`) fails here, on the
-    CPU, before it can reach a GPU run."""
+    CPU, before it can reach a GPU run.  b32: configs[2] (bench.py --batch 32)."""
     import bench
     v2 = model == "v2"
     args, res, ent = _fake_forward_inputs(bench, v2)
+    if model == "b32":
+        args.batch = 32
     line = bench.forward_line(
         args, v2=v2, B=args.batch, merge=4, world=1, value=8000.0, ms_per_step=1.0, host_submit_s=0.002,
         res=res, ent=ent, level_names=["a (level 1)", "b (level 2)", "c (level 3)"], traffic=(3e8, "x.json"),
@@ -430,7 +432,7 @@ def test_bench_forward_line_assembles_on_cpu(model):
         merge1=None if v2 else {"value": 7400.0, "ms_per_step": 1.08})
     d = _check_line(line, "Model_V2" if v2 else "HRegNet")
     assert d["value"] == 8000.0 and d["config"]["merge"] == 4
-    assert ("configs[4]" if v2 else "configs[1]") in d["config"]["workload"]
+    assert ("configs[4]" if v2 else "configs[2]" if model == "b32" else "configs[1]") in d["config"]["workload"]
     assert d["cpu_baseline"]["kind"] == "port"
 
 
