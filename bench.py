@@ -311,7 +311,7 @@ def pmc_traffic(kernel: str, workload: str):
     The latest round that measured every kernel of the family; (None, None) when no pass of
     this workload exists."""
     names = [n.split(" (")[0] for n in kernel.split(" + ")]
-    for rnd in ("r5", "r4", "r3", "r2", "r1"):
+    for rnd in ("r6", "r5", "r4", "r3", "r2", "r1"):
         path = os.path.join(REPO, "profiles", f"{rnd}_traffic.json")
         try:
             d = json.load(open(path))
@@ -613,7 +613,7 @@ def in_executor(steps: int, B: int, points: int, entries_flops: dict, merge: int
     workload is committed (key: batch, points, timed steps and merge factor; the timed region
     holds steps / merge launches of each level kernel)."""
     key = f"hregnet:b{B}:n{points}:s{steps}" + (f":m{merge}" if merge > 1 else "")
-    for rnd in ("r5",):
+    for rnd in ("r6", "r5"):
         path = os.path.join(REPO, "profiles", f"{rnd}_in_executor.json")
         try:
             d = json.load(open(path))[key]

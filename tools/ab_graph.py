@@ -24,23 +24,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 def _nofps1(engine):
-    """engine.fps with the level-1 (unweighted, 16384-point) selection served from a cache
-    (one D2D copy per call) -- a timing probe only"""
-    real = engine.fps
+    """engine.fps_indexed (the level-1 FPS over the spatial index, 16384-point clouds) with its
+    selection served from a cache (one D2D copy per call) -- a timing probe only"""
+    real = engine.fps_indexed
     cache = {}
 
-    def fps(xyz, npoint, weights=None, out=None):
-        if weights is not None or xyz.shape[1] != bench.POINTS:
-            return real(xyz, npoint, weights, out)
+    def fps_indexed(xyz, npoint, ws, out=None):
         key = tuple(xyz.shape)
         if key not in cache:
-            cache[key] = tuple(t.clone() for t in real(xyz, npoint))
+            cache[key] = tuple(t.clone() for t in real(xyz, npoint, ws))
         if out is None:
             return tuple(t.clone() for t in cache[key])
         for o, c in zip(out, cache[key]):
             o.copy_(c)
         return out
-    return fps
+    return fps_indexed
 
 
 def _nostage1(engine):
@@ -49,9 +47,9 @@ def _nostage1(engine):
     real = engine.grouping
     cache = {}
 
-    def grouping(xyz, lvl, weights=None, out=None, ws=None, sample=None):
+    def grouping(xyz, lvl, weights=None, out=None, ws=None, sample=None, **kw):
         if lvl != 0 or sample is not None or xyz.shape[1] != bench.POINTS:
-            return real(xyz, lvl, weights, out, ws, sample)
+            return real(xyz, lvl, weights, out, ws, sample, **kw)
         key = tuple(xyz.shape)
         if key not in cache:
             cache[key] = tuple(t.clone() for t in real(xyz, lvl, weights, None, None, None))
@@ -79,8 +77,8 @@ def apply(variant, lib, engine):
             undo.append(("engine", "grouping", engine.grouping))
             engine.grouping = _nostage1(engine)
         elif k == "probe.nofps1" and int(v):
-            undo.append(("engine", "fps", engine.fps))
-            engine.fps = _nofps1(engine)
+            undo.append(("engine", "fps_indexed", engine.fps_indexed))
+            engine.fps_indexed = _nofps1(engine)
         else:
             raise ValueError(f"unknown switch {k}")
     return undo
