@@ -101,6 +101,11 @@ int hreg_fps_bounded(int b, int n, int m, const float *points, float *temp, int3
  * Replaces furthest_point_sampling_kernel for level 1 (furthest_point_sampling_gpu.cu:84-206). */
 int hreg_fps_indexed(int b, int n, int m, const float *points, const void *ws, float *temp,
                      int32_t *idx, float *sampled_xyz, void *stream);
+/* hreg_fps_indexed for 16384-point clouds on the small-footprint pruned kernel (4 waves, running
+ * minima in registers, block coordinates read from the index; the throughput executor's batched
+ * level-1 stage); the same selections and temp.  Other sizes: hreg_fps_indexed. */
+int hreg_fps_indexed_lean(int b, int n, int m, const float *points, const void *ws, float *temp,
+                          int32_t *idx, float *sampled_xyz, void *stream);
 int hreg_furthest_point_sampling(int b, int n, int m, const float *points, float *temp,
                                  int32_t *idx, float *sampled_xyz, void *stream);
 

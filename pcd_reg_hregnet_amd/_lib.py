@@ -78,6 +78,7 @@ _SIGS = {
     "hreg_weighted_svd": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_weighted_svd_grouped": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_fps_indexed": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_fps_indexed_lean": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_weighted_svd_tr": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp],
     "hreg_transform_points": [_vp, _vp, _vp, _i, _i, _vp, _vp],
     "hreg_transformation_loss": [_vp, _vp, _vp, _vp, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,

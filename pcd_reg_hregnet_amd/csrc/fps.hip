@@ -1040,13 +1040,18 @@ __global__ __launch_bounds__(FS_T) void fps_sorted_kernel(const float4 *__restri
 // winner's from the index after it 1.66 (no gain: three readlanes per scanned block).
 // 64 clouds run slower than 8: their sorted copies (64 MB) exceed the L2s, so blocks come from
 // the MALL.  The cluster kernel on the same clouds: 1.97 / 5.6 us per iteration.
-constexpr int FB_T = 1024, FB_NW = 16, FB_A = 4;
+// NW waves (a power of two <= 16): 16 for Model_V2's 65536-point clouds; r6, 4 for 16384-point
+// clouds in the throughput executor's batched level-1 stage (fps_lean: 256 blocks, every lane one;
+// 4 waves x 108 VGPRs leave the CU's other SIMD slots to the lanes' level kernels, where
+// fps_sorted_kernel's 8 waves x 229 VGPRs hold the whole register file)
+constexpr int FB_A = 4;
 
 __device__ __forceinline__ uint32_t fb_rank(uint32_t id, int L, int Q) {
     return bitrev_bits(id & ((1u << L) - 1u), L) * (uint32_t)Q + (id >> L);
 }
 
-__global__ __launch_bounds__(FB_T) void fps_blocks_kernel(const float4 *__restrict__ spts,
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void fps_blocks_kernel(const float4 *__restrict__ spts,
                                                           const float4 *__restrict__ boxes, int np,
                                                           const float *__restrict__ xyz,
                                                           float *__restrict__ temp_out,
@@ -1054,16 +1059,16 @@ __global__ __launch_bounds__(FB_T) void fps_blocks_kernel(const float4 *__restri
                                                           float *__restrict__ sampled_out, int n, int m,
                                                           int L, int Q, float inf) {
     typedef typename SlotVec<32>::type V;
-    __shared__ float s_w[2][FB_NW];  // the waves' candidates: max T, min R
-    __shared__ uint32_t s_r[2][FB_NW];
+    __shared__ float s_w[2][NW];  // the waves' candidates: max T, min R
+    __shared__ uint32_t s_r[2][NW];
     const int cloud = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int w = __builtin_amdgcn_readfirstlane(wv);
     const int rows = n >> 6;
     const float4 *SP = spts + (size_t)cloud * np;
     const float4 *BX = boxes + (size_t)cloud * (np / 64) * 2;
 
-    // this lane's block (16 lane + w): box and candidate; -inf: no block
-    const int myrow = 16 * lane + w;
+    // this lane's block (NW lane + w): box and candidate; -inf: no block
+    const int myrow = NW * lane + w;
     float lx = 0.f, ly = 0.f, lz = 0.f, hx = 0.f, hy = 0.f, hz = 0.f;
     float rmT = -__builtin_huge_valf();
     uint32_t rR = 0xffffffffu;
@@ -1078,8 +1083,8 @@ __global__ __launch_bounds__(FB_T) void fps_blocks_kernel(const float4 *__restri
     for (int r = 0; r < 64; ++r) {
         if (r < 32) T0[r] = 1e10f;
         else T1[r - 32] = 1e10f;
-        if (16 * r + w < rows) {  // (uniform)
-            const int pos = (16 * r + w) * 64 + lane;
+        if (NW * r + w < rows) {  // (uniform)
+            const int pos = (NW * r + w) * 64 + lane;
             const uint32_t R = (fb_rank((uint32_t)__float_as_int(SP[pos].w), L, Q) << 16) | (uint32_t)pos;
             const uint32_t Rm = (uint32_t)__builtin_amdgcn_readlane((int)wave_min_to63_u32_dpp(R), 63);
             if (lane == r) rR = Rm;
@@ -1116,7 +1121,7 @@ __global__ __launch_bounds__(FB_T) void fps_blocks_kernel(const float4 *__restri
                         act32 &= act32 - 1;
                         ra[a] = r;
                         cnt = a + 1;
-                        v[a] = SP[(16 * (r0 + r) + w) * 64 + lane];
+                        v[a] = SP[(NW * (r0 + r) + w) * 64 + lane];
                     }
                 }
 #pragma unroll
@@ -1127,7 +1132,7 @@ __global__ __launch_bounds__(FB_T) void fps_blocks_kernel(const float4 *__restri
                         const float d = sqdist3(v[a].x, v[a].y, v[a].z, x1, y1, z1);
                         const float t = fmin_ref(d, T[r]);
                         T[r] = t;
-                        const uint32_t pos = (uint32_t)((16 * (r0 + r) + w) * 64 + lane);
+                        const uint32_t pos = (uint32_t)((NW * (r0 + r) + w) * 64 + lane);
                         const uint32_t R = (fb_rank((uint32_t)__float_as_int(v[a].w), L, Q) << 16) | pos;
                         // the block's candidate: max T, then min R -- one lane at the max (the
                         // usual case) needs no second reduction
@@ -1158,8 +1163,8 @@ __global__ __launch_bounds__(FB_T) void fps_blocks_kernel(const float4 *__restri
             s_r[buf][wv] = Rw;
         }
         lds_barrier();
-        const float cw = s_w[buf][lane & (FB_NW - 1)];
-        const uint32_t cr = s_r[buf][lane & (FB_NW - 1)];
+        const float cw = s_w[buf][lane & (NW - 1)];
+        const uint32_t cr = s_r[buf][lane & (NW - 1)];
         const float gmax = readlane_f(row_max16_dpp(cw), 0);
         const uint32_t Rg =
             (uint32_t)__builtin_amdgcn_readlane((int)row_min16_u32_dpp(cw == gmax ? cr : 0xffffffffu), 0);
@@ -1179,7 +1184,7 @@ __global__ __launch_bounds__(FB_T) void fps_blocks_kernel(const float4 *__restri
         float *tp = temp_out + (size_t)cloud * n;
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            if (16 * r + w < rows) tp[__float_as_int(SP[(16 * r + w) * 64 + lane].w)] = r < 32 ? T0[r] : T1[r - 32];
+            if (NW * r + w < rows) tp[__float_as_int(SP[(NW * r + w) * 64 + lane].w)] = r < 32 ? T0[r] : T1[r - 32];
     }
 }
 
@@ -1279,7 +1284,7 @@ extern "C" int hreg_fps_indexed(int b, int n, int m, const float *points, const 
         while (np < (size_t)n) np <<= 1;
         const float4 *spts = static_cast<const float4 *>(ws);
         const int L = hreg_ilog2(bs), Q = (n + bs - 1) / bs;
-        hipLaunchKernelGGL(fps_blocks_kernel, dim3(b), dim3(FB_T), 0, as_stream(stream), spts,
+        hipLaunchKernelGGL(fps_blocks_kernel<16>, dim3(b), dim3(16 * 64), 0, as_stream(stream), spts,
                            spts + (size_t)b * np, (int)np, points, temp, idx, sampled_xyz, n, m, L, Q,
                            __builtin_huge_valf());
         HREG_CHECK_LAUNCH();
@@ -1291,6 +1296,25 @@ extern "C" int hreg_fps_indexed(int b, int n, int m, const float *points, const 
     hipLaunchKernelGGL(fps_sorted_kernel, dim3(b), dim3(FS_T), 0, as_stream(stream),
                        static_cast<const float4 *>(ws), FS_N, points, temp, idx, sampled_xyz, m, bs, L, LQ,
                        __builtin_huge_valf());
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+// hreg_fps_indexed for the throughput executor's batched level-1 stage (r6): 16384-point clouds on
+// fps_blocks_kernel<4> (T in registers, block coordinates from the index's sorted copy: a small
+// register footprint per cloud at a longer iteration) instead of fps_sorted_kernel; the same
+// selections.  Other sizes: hreg_fps_indexed.
+extern "C" int hreg_fps_indexed_lean(int b, int n, int m, const float *points, const void *ws, float *temp,
+                                     int32_t *idx, float *sampled_xyz, void *stream) {
+    if (b < 0 || n <= 0 || !points || !idx || !ws) return HREG_ERR_INVALID;
+    if (b == 0 || m <= 0) return HREG_OK;
+    if (n != FS_N || (reinterpret_cast<uintptr_t>(ws) & 15))
+        return hreg_fps_indexed(b, n, m, points, ws, temp, idx, sampled_xyz, stream);
+    const int bs = hreg_opt_n_threads(n);
+    const float4 *spts = static_cast<const float4 *>(ws);
+    const int L = hreg_ilog2(bs), Q = (n + bs - 1) / bs;
+    hipLaunchKernelGGL(fps_blocks_kernel<4>, dim3(b), dim3(4 * 64), 0, as_stream(stream), spts,
+                       spts + (size_t)b * n, n, points, temp, idx, sampled_xyz, n, m, L, Q, __builtin_huge_valf());
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

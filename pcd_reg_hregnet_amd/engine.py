@@ -103,6 +103,13 @@ CHAIN_FORK = switches.flag("CHAIN_FORK", True)
 # r6, 16384 < n <= 65536 with n % 64 == 0 (fps_blocks_kernel: Model_V2's 65536-point clouds on ONE
 # workgroup each instead of the cluster kernel's 32 spinning single-wave participants).
 FPS_SORTED = switches.flag("FPS_SORTED", True)
+# the multi-lane executor's batched level-1 stage on the small-footprint pruned FPS
+# (hreg_fps_indexed_lean: 4 waves x 108 VGPRs per cloud instead of 8 x 229, so the lanes' level
+# kernels keep most of a CU while its cloud's FPS runs).  r6, tools/ab_graph.py paired in one
+# process (gpurun_out/r6pr): 8842 vs 8624 pairs/s; the level-1 FPS served from a cache (probe)
+# 9255, the whole level-1 grouping 10203.  The single-batch path keeps fps_sorted_kernel (its
+# shorter iteration is the latency).
+FPS_LEAN = switches.flag("FPS_LEAN", True)
 FPS_SORTED_N = 16384
 
 
@@ -838,16 +845,18 @@ def fps(xyz, npoint, weights=None, out=None, concurrent=0):
     return idx, sampled
 
 
-def fps_indexed(xyz, npoint, ws, out=None):
+def fps_indexed(xyz, npoint, ws, out=None, lean=False):
     """FPS of nb clouds (fps_indexed_ok sizes) over their spatial index in ws (hreg_spatial_index
-    already enqueued): hreg_fps_indexed, bitwise fps(xyz, npoint)."""
+    already enqueued): hreg_fps_indexed, bitwise fps(xyz, npoint).  lean: 16384-point clouds on
+    the small-footprint kernel (hreg_fps_indexed_lean; the throughput executor's batched stage)."""
     nb, n, _ = xyz.shape
     if out is None:
         idx = _empty(nb, npoint, dtype=torch.int32, device=xyz.device)
         sampled = _empty(nb, npoint, 3, device=xyz.device)
     else:
         idx, sampled = out
-    call("hreg_fps_indexed", nb, n, npoint, xyz, ws, None, idx, sampled, _stream())
+    call("hreg_fps_indexed_lean" if lean else "hreg_fps_indexed", nb, n, npoint, xyz, ws, None, idx, sampled,
+         _stream())
     return idx, sampled
 
 
@@ -988,7 +997,7 @@ def gather_xyz(xyz, idx):
     return out
 
 
-def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_concurrent=0):
+def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_concurrent=0, fps_lean=False):
     """FPS/WFPS + knn_group of one level (layers.py:136-149): (idx, sampled, gidx, geom, knn_xyz).
     out: optional preallocated tensors of the same tuple; ws: spatial-index workspace
     (uint8, spatial_index_bytes) for large clouds; sample: the level's random-sampling
@@ -1002,7 +1011,7 @@ def grouping(xyz, lvl: int, weights=None, out=None, ws=None, sample=None, fps_co
         if ws is None:
             ws = _empty(spatial_index_bytes(nb, n), dtype=torch.uint8, device=xyz.device)
         call("hreg_spatial_index", xyz, nb, n, ws, _stream())
-        idx, sampled = fps_indexed(xyz, M, ws, out=None if out is None else out[:2])
+        idx, sampled = fps_indexed(xyz, M, ws, out=None if out is None else out[:2], lean=fps_lean)
         gidx, geom, kx = knn_group_indexed(sampled, xyz, k, ws, out=None if out is None else out[2:5],
                                            build=False)
         _record_knn(f"knn_{lvl + 1}", gidx, nb, n, k, True)
@@ -1872,7 +1881,7 @@ class GraphPipeline:
         v = pts.view(self.lanes, 2, self.B, self.N, 3)
         v[:, 0].copy_(self.src_all)
         v[:, 1].copy_(self.dst_all)
-        grouping(pts, 0, out=g, ws=g[5], fps_concurrent=1 if self.N > 16384 else 0)
+        grouping(pts, 0, out=g, ws=g[5], fps_concurrent=1 if self.N > 16384 else 0, fps_lean=FPS_LEAN)
 
     def _first_stage1(self, lanes=None):
         if self.bs1:

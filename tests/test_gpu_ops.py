@@ -102,6 +102,16 @@ def test_fps_indexed_matches_fps(kind, n):
     np.testing.assert_array_equal(got, ref.cpu().numpy())
     if n == 16384:
         assert torch.equal(temp, rtemp)
+        # the throughput executor's small-footprint kernel (hreg_fps_indexed_lean,
+        # fps_blocks_kernel<4>): the same selections and final running minima
+        idx2 = torch.full((B, m), -3, dtype=torch.int32, device="cuda")
+        temp2 = torch.full((B, n), -1.0, device="cuda")
+        sampled2 = torch.empty(B, m, 3, device="cuda")
+        _lib.call("hreg_fps_indexed_lean", B, n, m, x, ws, temp2, idx2, sampled2, _lib.stream_handle())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(idx2.cpu().numpy(), got)
+        assert torch.equal(temp2, rtemp)
+        np.testing.assert_array_equal(sampled2.cpu().numpy(), xyz[np.arange(B)[:, None], got])
     else:  # (the cluster kernel keeps its exchange slots in temp): the reference's final running
         # minima, min over the centres idx[0 .. m-2] of the two-rounding fp32 distance (.cu:129-130)
         for c in range(B):

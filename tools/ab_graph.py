@@ -29,10 +29,10 @@ def _nofps1(engine):
     real = engine.fps_indexed
     cache = {}
 
-    def fps_indexed(xyz, npoint, ws, out=None):
+    def fps_indexed(xyz, npoint, ws, out=None, **kw):
         key = tuple(xyz.shape)
         if key not in cache:
-            cache[key] = tuple(t.clone() for t in real(xyz, npoint, ws))
+            cache[key] = tuple(t.clone() for t in real(xyz, npoint, ws, **kw))
         if out is None:
             return tuple(t.clone() for t in cache[key])
         for o, c in zip(out, cache[key]):
