@@ -410,6 +410,14 @@ int hreg_ts_gemm_bn(const float *A, int lda, int R, int K, const float *W, int w
                     const float *shift, float *out, int ldo, float eps, float momentum, void *ws,
                     float *mean, float *invstd, float *var_unbiased, float *running_mean,
                     float *running_var, void *stream);
+/* hreg_ts_gemm_bn over the descriptor tail's rows without the concatenation (layers.py:204-206):
+ * A = cat([x2 repeated over the k rows of each group, x1, att]), x2 [R/k][C1], x1 [R][C1],
+ * att [R][Ca], C1 and Ca multiples of 16, W [N][2 C1 + Ca]; the same sums as hreg_ts_gemm_bn on
+ * the materialised matrix.  ws = hreg_ts_gemm_bn_ws_bytes(R, 2 C1 + Ca, N) bytes. */
+int hreg_ts_gemm_bn_tail(const float *x2, int k, const float *x1, int C1, const float *att, int Ca, int R,
+                         const float *W, int N, const float *shift, float *out, int ldo, float eps,
+                         float momentum, void *ws, float *mean, float *invstd, float *var_unbiased,
+                         float *running_mean, float *running_var, void *stream);
 /* out = act(gamma * (y - mean) * invstd + beta), act = ReLU if relu (out may alias y) */
 int hreg_bn_apply(const float *y, int R, int C, const float *mean, const float *invstd,
                   const float *gamma, const float *beta, int relu, float *out, void *stream);
@@ -431,6 +439,12 @@ int hreg_col_sum(const float *x, int R, int C, void *ws, float *out, int accumul
 size_t hreg_gemm_tn_ws_bytes(int R, int N, int K);
 int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N, int K, float beta,
                  void *ws, float *out, void *stream);
+/* hreg_gemm_tn with B = cat([x2 repeated over the k rows of each group, x1, att]) read in place
+ * (the descriptor tail's weight gradient): x2 [R/k][C1], x1 [R][C1], att [R][Ca], C1 and Ca
+ * multiples of 64, out [N][2 C1 + Ca]; the same sums as hreg_gemm_tn on the materialised matrix.
+ * ws = hreg_gemm_tn_ws_bytes(R, N, 2 C1 + Ca) bytes. */
+int hreg_gemm_tn_tail(const float *A, int lda, const float *x2, int k, const float *x1, int C1,
+                      const float *att, int Ca, int R, int N, float beta, void *ws, float *out, void *stream);
 /* out [C][R] = in [R][C]^T */
 int hreg_transpose(const float *in, int R, int C, float *out, void *stream);
 /* y[i] += x[i] (fp32, one rounding) over n floats: the second gradient bucket of the

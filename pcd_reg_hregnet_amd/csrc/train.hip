@@ -403,11 +403,19 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float *__restrict__ 
 // from LDS.  Wave w still takes rows 16 w .. 16 w + 15 of every step in the same k-step order,
 // so every output is the same sum as gemm_tn_kernel's (that kernel stays for row strides or
 // bases that are not 16-byte aligned).
-template <int TNN, int TNK>
+// (SEG, r6) B = column segments: columns [kend[s-1], kend[s]) are segment s's row r / div[s]
+// (rows[s] rows, stride ld[s]); every kend a multiple of 64, so a 64-wide k-block reads one segment
+// (the descriptor tail's cat([x2 repeated over k rows, x1, att_map]) without materialising it)
+struct TnSeg {
+    const float *base[3];
+    int ld[3], div[3], kend[3], rows[3];
+};
+
+template <int TNN, int TNK, bool SEG = false>
 __global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__ A, int lda,
                                                        const float *__restrict__ Bm, int ldb, int R,
                                                        int N, int K, int rows_per_split,
-                                                       float *__restrict__ ws) {
+                                                       float *__restrict__ ws, TnSeg sg = {}) {
     constexpr int WA = 32 * TNN, WB = 32 * TNK, TW = WB;  // tile widths (floats)
     constexpr int FA = WA / 4, FB = WB / 4;               // float4 per row
     constexpr int LA = TN_ROWS * FA / 256, LB = TN_ROWS * FB / 256;  // float4 loads per thread
@@ -422,8 +430,19 @@ __global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__
     const int r1 = min(R, r0 + rows_per_split);
     const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(A), (short)0,
                                                       (int)((size_t)R * lda * sizeof(float)), 0x00020000);
-    const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Bm), (short)0,
-                                                      (int)((size_t)R * ldb * sizeof(float)), 0x00020000);
+    int bdiv = 1, bcol = k0;  // B row divisor and this block's first column in its source
+    const float *Bsrc = Bm;
+    int brows = R;
+    if constexpr (SEG) {
+        const int s = k0 < sg.kend[0] ? 0 : k0 < sg.kend[1] ? 1 : 2;  // (uniform)
+        Bsrc = sg.base[s];
+        ldb = sg.ld[s];
+        bdiv = sg.div[s];
+        bcol = k0 - (s == 0 ? 0 : sg.kend[s - 1]);
+        brows = sg.rows[s];
+    }
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Bsrc), (short)0,
+                                                      (int)((size_t)brows * ldb * sizeof(float)), 0x00020000);
     typedef float v4f __attribute__((ext_vector_type(4)));
     f32x16 acc[TNN][TNK];
 #pragma unroll
@@ -445,7 +464,8 @@ __global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__
 #pragma unroll
         for (int i = 0; i < LB; ++i) {
             const int e = tid + 256 * i, r = e / FB, c4 = e - r * FB;
-            const uint32_t off = ((uint32_t)(base + r) * (uint32_t)ldb + k0 + 4 * c4) * 4u;
+            const uint32_t br = SEG ? (uint32_t)(base + r) / (uint32_t)bdiv : (uint32_t)(base + r);
+            const uint32_t off = (br * (uint32_t)ldb + bcol + 4 * c4) * 4u;
             gb[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0));
         }
     };
@@ -801,6 +821,50 @@ static int gemm_tn_launch(const float *A, int lda, const float *B, int ldb, int 
 extern "C" int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N, int K,
                             float beta, void *ws, float *out, void *stream) {
     return gemm_tn_launch(A, lda, B, ldb, R, N, K, beta, ws, out, stream, R > 0 ? tn_splits(R, N, K) : 1);
+}
+
+// hreg_gemm_tn with B = cat([x2 repeated over the k rows of each group, x1, att]) (the descriptor
+// tail, layers.py:204-206) read in place: x2 [R/k][C1], x1 [R][C1], att [R][Ca], C1 and Ca
+// multiples of 64; out [N][2 C1 + Ca] (r6).  The same sums as hreg_gemm_tn on the materialised
+// matrix (the same values in the same row order per wave).  ws: hreg_gemm_tn_ws_bytes(R, N, 2C1+Ca).
+extern "C" int hreg_gemm_tn_tail(const float *A, int lda, const float *x2, int k, const float *x1, int C1,
+                                 const float *att, int Ca, int R, int N, float beta, void *ws, float *out,
+                                 void *stream) {
+    const int K = 2 * C1 + Ca;
+    if (!A || !x2 || !x1 || !att || !ws || !out || R <= 0 || N <= 0 || k <= 0 || R % k || lda < N || (lda & 3) ||
+        (C1 & 63) || (Ca & 63) ||
+        ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(x2) | reinterpret_cast<uintptr_t>(x1) |
+          reinterpret_cast<uintptr_t>(att)) & 15))
+        return HREG_ERR_INVALID;
+    if ((size_t)R * lda * sizeof(float) >= ((size_t)1 << 31) || (size_t)R * Ca * sizeof(float) >= ((size_t)1 << 31) ||
+        (size_t)R * C1 * sizeof(float) >= ((size_t)1 << 31))
+        return HREG_ERR_UNSUPPORTED;
+    const int S = tn_splits(R, N, K);
+    int rps = (R + S - 1) / S;
+    rps = (rps + TN_ROWS - 1) / TN_ROWS * TN_ROWS;
+    TnSeg sg;
+    sg.base[0] = x2; sg.ld[0] = C1; sg.div[0] = k; sg.kend[0] = C1; sg.rows[0] = R / k;
+    sg.base[1] = x1; sg.ld[1] = C1; sg.div[1] = 1; sg.kend[1] = 2 * C1; sg.rows[1] = R;
+    sg.base[2] = att; sg.ld[2] = Ca; sg.div[2] = 1; sg.kend[2] = K; sg.rows[2] = R;
+    hipStream_t st = as_stream(stream);
+    const int tnn = N <= 32 ? 1 : 2;  // (gemm_tn_launch's tiles: the same sums as its launch)
+    const dim3 grid((N + 32 * tnn - 1) / (32 * tnn), K / 64, S);
+    if (tnn == 1)
+        hipLaunchKernelGGL((gemm_tn4_kernel<1, 2, true>), grid, dim3(256), 0, st, A, lda, x1, C1, R, N, K, rps,
+                           (float *)ws, sg);
+    else
+        hipLaunchKernelGGL((gemm_tn4_kernel<2, 2, true>), grid, dim3(256), 0, st, A, lda, x1, C1, R, N, K, rps,
+                           (float *)ws, sg);
+    HREG_CHECK_LAUNCH();
+    const size_t NK = (size_t)N * K;
+    if (S >= 16)
+        hipLaunchKernelGGL(tn_reduce_kernel<16>, dim3((unsigned)((NK + 15) / 16)), dim3(256), 0, st,
+                           (const float *)ws, S, NK, beta, out);
+    else
+        hipLaunchKernelGGL(tn_reduce_kernel<1>, dim3(grid1d(NK)), dim3(256), 0, st, (const float *)ws, S, NK, beta,
+                           out);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
 }
 
 // tools only (tools/tn_split_sweep.py): the same GEMM with S row splits (ws: S * N * K floats)

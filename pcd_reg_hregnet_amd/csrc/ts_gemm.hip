@@ -26,6 +26,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int TS_LDS_FLOATS = 16384;  // W' column group: NT * 32 rows x (K16 + 4) floats
 constexpr int TS_GRP = 4;             // 16-deep sub-chunks per A load group (k = 64)
 
+// (SEG, r6) A assembled from column segments instead of one matrix: columns [kend[s-1], kend[s])
+// are segment s's row r / div[s] (stride ld[s]); every kend a multiple of 16, so a lane's 8-column
+// load never straddles two segments.  The descriptor tail's cat([x2 repeated over k rows, x1,
+// att_map]) (layers.py:204-206) without materialising it: the same values in the same k order,
+// so the same sums as the concatenated matrix.
+struct TsSeg {
+    const float *base[3];
+    int ld[3], div[3], kend[3];
+};
+
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
 // STATS: the train-mode BatchNorm statistics of the output ride along in the epilogue (the
@@ -33,13 +43,13 @@ __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast
 // squares (exact products) over its rows, in its fixed tile order; the lane halves, then the
 // four waves (in order, through LDS) combine, and each workgroup writes its partial
 // [blockIdx.x][N][2] for col_finalize (train.hip) to sum over workgroups in order.
-template <int NT, bool TAIL, bool FULL, bool STATS = false>
+template <int NT, bool TAIL, bool FULL, bool STATS = false, bool SEG = false>
 __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict__ A, int lda, int R, int K,
                                                          const float *__restrict__ W, int w_trans, int N,
                                                          const float *__restrict__ scale,
                                                          const float *__restrict__ shift, int relu,
                                                          float *__restrict__ out, int ldo,
-                                                         double *__restrict__ part = nullptr) {
+                                                         double *__restrict__ part = nullptr, TsSeg sg = {}) {
     extern __shared__ __attribute__((aligned(16))) float Ws[];
     const int K16 = (K + 15) & ~15, KP = K16 + 4, nsub = K16 / 16;
     const int ngrp = (nsub + TS_GRP - 1) / TS_GRP;
@@ -84,6 +94,19 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
     auto load_group = [&](int tt, int g, float4 (&v)[2 * TS_GRP]) {
         int r = tt * 32 + j;
         r = r < R ? r : R - 1;
+        if constexpr (SEG) {
+#pragma unroll
+            for (int u = 0; u < TS_GRP; ++u) {
+                const int k0 = (g * TS_GRP + u) * 16;  // (uniform) sub-chunk -> its segment
+                const int s = k0 < sg.kend[0] ? 0 : k0 < sg.kend[1] ? 1 : 2;
+                const int kb = s == 0 ? 0 : sg.kend[s - 1];
+                const int kk = k0 < K ? k0 - kb + 8 * h : 8 * h;  // (past K: a valid row, masked by W' = 0)
+                const float *src = sg.base[s] + (size_t)(r / sg.div[s]) * sg.ld[s] + kk;
+                v[2 * u] = *reinterpret_cast<const float4 *>(src);
+                v[2 * u + 1] = *reinterpret_cast<const float4 *>(src + 4);
+            }
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < TS_GRP; ++u) {
             const int k = (g * TS_GRP + u) * 16 + 8 * h;
@@ -258,13 +281,14 @@ namespace {
 
 // launch (STATS: the workgroups' statistic partials into part, see ts_gemm_kernel); returns
 // the number of workgroups along the rows (the partials' count), or a negative HREG_ERR_*
-template <bool STATS>
+template <bool STATS, bool SEG = false>
 int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans, int N, const float *scale,
-              const float *shift, int relu, float *out, int ldo, double *part, hipStream_t st) {
+              const float *shift, int relu, float *out, int ldo, double *part, hipStream_t st, TsSeg sg = {}) {
     if (!A || !W || !out || R <= 0 || K <= 0 || N <= 0 || lda < K || ldo < N || (K & 3) || (N & 3) ||
         (lda & 3) || (ldo & 3) || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W) |
                                      reinterpret_cast<uintptr_t>(out)) & 15))
         return -HREG_ERR_INVALID;
+    if (SEG && (K & 15)) return -HREG_ERR_INVALID;
     if ((size_t)R * lda * sizeof(float) >= ((size_t)1 << 31)) return -HREG_ERR_UNSUPPORTED;
     const int nt = ts_nt(K, N, STATS);
     if (nt <= 0) return -HREG_ERR_UNSUPPORTED;
@@ -277,8 +301,8 @@ int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans
     if (STATS && full) return -HREG_ERR_UNSUPPORTED;
 #define TS_CASE(NTT, TT, FF)                                                                                   \
     if (nt == NTT && tail == TT && full == FF) {                                                              \
-        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF, STATS>), dim3(gx, gy), dim3(256), lds, st, A, lda, R, K, \
-                           W, w_trans, N, scale, shift, relu, out, ldo, part);                                 \
+        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF, STATS, SEG>), dim3(gx, gy), dim3(256), lds, st, A, lda, R, \
+                           K, W, w_trans, N, scale, shift, relu, out, ldo, part, sg);                          \
         if (hipGetLastError() != hipSuccess) return -HREG_ERR_LAUNCH;                                          \
         return gx;                                                                                             \
     }
@@ -315,6 +339,32 @@ extern "C" int hreg_ts_gemm_bn(const float *A, int lda, int R, int K, const floa
     hipStream_t st = as_stream(stream);
     const int S = ts_launch<true>(A, lda, R, K, W, w_trans, N, nullptr, shift, 0, out, ldo,
                                   static_cast<double *>(ws), st);
+    if (S < 0) return -S;
+    return hreg_bn_finalize_stats(static_cast<const double *>(ws), S, R, N, eps, mean, invstd, var_unbiased,
+                                  momentum, running_mean, running_var, st);
+}
+
+// hreg_ts_gemm_bn over the descriptor tail's rows without the concatenation (r6): A = cat([x2
+// repeated over the k rows of each group, x1, att]) (layers.py:204-206), x2 [R/k][C1], x1 [R][C1],
+// att [R][Ca]; C1, Ca multiples of 16.  The same sums as hreg_ts_gemm_bn on the materialised
+// [R][2 C1 + Ca] matrix (the same values in the same k order).
+extern "C" int hreg_ts_gemm_bn_tail(const float *x2, int k, const float *x1, int C1, const float *att, int Ca,
+                                    int R, const float *W, int N, const float *shift, float *out, int ldo,
+                                    float eps, float momentum, void *ws, float *mean, float *invstd,
+                                    float *var_unbiased, float *running_mean, float *running_var, void *stream) {
+    if (!x2 || !x1 || !att || !ws || !mean || !invstd || R <= 0 || k <= 0 || R % k || (C1 & 15) || (Ca & 15) ||
+        ((running_mean == nullptr) != (running_var == nullptr)) || (running_mean && !var_unbiased) ||
+        ((reinterpret_cast<uintptr_t>(x2) | reinterpret_cast<uintptr_t>(x1) | reinterpret_cast<uintptr_t>(att)) & 15))
+        return HREG_ERR_INVALID;
+    const int K = 2 * C1 + Ca;
+    TsSeg sg;
+    sg.base[0] = x2; sg.ld[0] = C1; sg.div[0] = k; sg.kend[0] = C1;
+    sg.base[1] = x1; sg.ld[1] = C1; sg.div[1] = 1; sg.kend[1] = 2 * C1;
+    sg.base[2] = att; sg.ld[2] = Ca; sg.div[2] = 1; sg.kend[2] = K;
+    hipStream_t st = as_stream(stream);
+    // (A / lda: the validity checks of the plain form; the segments are read through sg)
+    const int S = ts_launch<true, true>(x1, K, R, K, W, 0, N, nullptr, shift, 0, out, ldo, static_cast<double *>(ws),
+                                        st, sg);
     if (S < 0) return -S;
     return hreg_bn_finalize_stats(static_cast<const double *>(ws), S, R, N, eps, mean, invstd, var_unbiased,
                                   momentum, running_mean, running_var, st);

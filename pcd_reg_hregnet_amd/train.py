@@ -300,6 +300,112 @@ def conv_bn_act(x, W, bias, gamma, beta, running_mean=None, running_var=None, re
                             relu, momentum, eps, wparam if wparam is not None else W)
 
 
+def tail_fusable(R: int, k: int, C1: int, Ca: int, N: int) -> bool:
+    """_TailConvBNAct's kernels take this shape (else the concatenation path runs)"""
+    K = 2 * C1 + Ca
+    return (TS_GEMM and TS_BN and R >= TS_MIN_ROWS and R % k == 0 and C1 % 64 == 0 and Ca % 64 == 0
+            and bool(_lib.load().hreg_ts_gemm_supported(R, K, N, 1)))
+
+
+class _TailConvBNAct(torch.autograd.Function):
+    """The descriptor's mlp1 (Conv1x1 + train-mode BN + ReLU) over cat([x2 repeated over each
+    group's k rows, x1, att_map]) (layers.py:202-209) without materialising the concatenation
+    (r6): the forward GEMM + statistics (hreg_ts_gemm_bn_tail) and the weight gradient
+    (hreg_gemm_tn_tail) read the three blocks in place.  Every kernel computes the concatenation
+    path's sums in its order (the same values in the same k / row order), and the input gradients
+    are the concatenation path's (the [R][2 C1 + Ca] gradient, its x2 block summed per group and
+    sent to the argmax rows), so outputs and gradients are bitwise those of desc_tail +
+    conv_bn_act."""
+
+    @staticmethod
+    def forward(ctx, x1, att, W, bias, gamma, beta, running_mean, running_var, k, momentum, eps, wparam=None):
+        R, C1 = x1.shape
+        Ca = att.shape[1]
+        G = R // k
+        N = W.shape[0]
+        dev = x1.device
+        st = _stream()
+        x2 = torch.empty(G, C1, device=dev)
+        arg = torch.empty(G, C1, dtype=torch.int32, device=dev)
+        _lib.call("hreg_group_max_arg", x1, C1, G, k, C1, x2, C1, arg, st)
+        defer = DEFERRED_RUNNING is not None and running_mean is not None
+        rm, rv = (None, None) if defer else (running_mean, running_var)
+        y = torch.empty(R, N, device=dev)
+        mean, invstd, var = (torch.empty(N, device=dev) for _ in range(3))
+        ws = _ws(_lib.load().hreg_ts_gemm_bn_ws_bytes(R, 2 * C1 + Ca, N), dev)
+        _lib.call("hreg_ts_gemm_bn_tail", x2, k, x1, C1, att, Ca, R, W.contiguous(), N,
+                  None if bias is None else bias.contiguous(), y, N, float(eps), float(momentum), ws, mean, invstd,
+                  var, rm, rv, st)
+        if defer:
+            DEFERRED_RUNNING.append((mean, var, running_mean, running_var, momentum))
+        out = torch.empty_like(y)
+        _lib.call("hreg_bn_apply", y, R, N, mean, invstd, gamma, beta, 1, out, st)
+        ctx.save_for_backward(x1, att, x2, arg, W, y, mean, invstd, gamma, beta)
+        ctx.side = _SIDE
+        ctx.k = k
+        ctx.has_bias = bias is not None
+        ctx.params = (wparam, bias, gamma, beta)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x1, att, x2, arg, W, y, mean, invstd, gamma, beta = ctx.saved_tensors
+        dout = dout.contiguous()
+        R, N = y.shape
+        C1, Ca = x1.shape[1], att.shape[1]
+        k = ctx.k
+        G = R // k
+        K = 2 * C1 + Ca
+        dev = y.device
+        st = _stream()
+        wp, bp, gp, btp = ctx.params
+        gw = _grad_slot(wp, ctx.side) if ctx.needs_input_grad[2] else None
+        gb = _grad_slot(bp, ctx.side) if ctx.has_bias and ctx.needs_input_grad[3] else None
+        gg, gbt = _grad_slot(gp, ctx.side), _grad_slot(btp, ctx.side)
+        acc = gg is not None and gbt is not None and ctx.needs_input_grad[4] and ctx.needs_input_grad[5]
+        dgamma = gg if acc else torch.empty(N, device=dev)
+        dbeta = gbt if acc else torch.empty(N, device=dev)
+        dy = torch.empty_like(y)
+        _lib.call("hreg_bn_backward", dout, None, y, R, N, mean, invstd, gamma, beta, 1,
+                  col_reduce_ws(R, N, dev), dy, dgamma, dbeta, 1 if acc else 0, st)
+        dW = None
+        if ctx.needs_input_grad[2]:
+            out = gw.view(W.shape) if gw is not None else torch.empty(N, K, device=dev)
+            ws = _ws(_lib.load().hreg_gemm_tn_ws_bytes(R, N, K), dev)
+            _lib.call("hreg_gemm_tn_tail", dy, N, x2, k, x1, C1, att, Ca, R, N, 1.0 if gw is not None else 0.0,
+                      ws, out, st)
+            if gw is None:
+                dW = out
+        dbias = None
+        if ctx.has_bias and ctx.needs_input_grad[3]:
+            if gb is not None:
+                col_sum(dy, into=gb)
+            else:
+                dbias = col_sum(dy)
+        dx1 = datt = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            dcat = _conv_gemm(dy, W, None, w_trans=True)  # [R][K] (desc_tail's backward from here)
+            if ctx.needs_input_grad[0]:
+                dx2 = torch.empty(G, C1, device=dev)
+                _lib.call("hreg_group_sum", dcat, K, G, k, C1, dx2, C1, 0, st)
+                dx1 = torch.empty(R, C1, device=dev)
+                _lib.call("hreg_copy_rows", dcat[:, C1:], K, 1, R, C1, dx1, C1, 0, st)
+                _lib.call("hreg_group_max_bwd", dx2, C1, arg, G, k, C1, dx1, C1, 1, st)
+            if ctx.needs_input_grad[1]:
+                datt = dcat[:, 2 * C1:]
+        if acc:
+            dgamma = dbeta = None
+        return dx1, datt, dW, dbias, dgamma, dbeta, None, None, None, None, None, None
+
+
+def tail_conv_bn_act(x1, att, k, W, bias, gamma, beta, running_mean=None, running_var=None,
+                     momentum=BN_MOMENTUM, eps=BN_EPS, wparam=None):
+    """Conv1x1 + train-mode BN + ReLU over cat([max_k x1 repeated over k rows, x1, att]) without
+    the concatenation (_TailConvBNAct; the caller checks tail_fusable); W [N][2 C1 + Ca]."""
+    return _TailConvBNAct.apply(x1.contiguous(), att.contiguous(), W, bias, gamma, beta, running_mean,
+                                running_var, k, momentum, eps, wparam if wparam is not None else W)
+
+
 class ConvBNAct(torch.nn.Module):
     """Parameters of one 1x1 conv + BatchNorm (+ ReLU) layer, reference naming:
     ``conv.weight [N][K(,1,1)]``, ``conv.bias``, ``bn.weight/bias/running_*``."""

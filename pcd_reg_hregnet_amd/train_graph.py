@@ -589,6 +589,11 @@ def _flush_bn_counters():
         _BN_COUNTERS.clear()
 
 
+# the descriptor's mlp1 without its input concatenation (train.tail_conv_bn_act, r6; bitwise the
+# concatenation path, which stays as the test checker and for shapes its kernels do not take)
+TAIL_FUSED = True
+
+
 def conv_bn(x, conv, bn, relu=True):
     """Conv(1x1) + train-mode BatchNorm (+ ReLU) over rows (num_batches_tracked += 1)."""
     W = conv.weight.view(conv.out_channels, -1)
@@ -664,8 +669,17 @@ def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src", u
                            nb, M, want_weights=True)
     # descriptor (layers.py:200-209)
     x1 = seq_convs(grouped_rows, desc.convs)
-    y = desc_tail(x1, att_map, k)  # cat([max_k x1 repeated, x1, att_map])
-    y = conv_bn(y, desc.mlp1[0], desc.mlp1[1])
+    conv, bn = desc.mlp1[0], desc.mlp1[1]
+    if TAIL_FUSED and train.tail_fusable(x1.shape[0], k, x1.shape[1], att_map.shape[1], conv.out_channels):
+        # mlp1 over cat([max_k x1 repeated, x1, att_map]) without materialising it (the same bits)
+        y = train.tail_conv_bn_act(x1, att_map, k, conv.weight.view(conv.out_channels, -1), conv.bias,
+                                   bn.weight, bn.bias, bn.running_mean, bn.running_var, momentum=bn.momentum,
+                                   eps=bn.eps, wparam=conv.weight)
+        if bn.num_batches_tracked is not None:
+            _BN_COUNTERS.append(bn.num_batches_tracked)
+    else:
+        y = desc_tail(x1, att_map, k)  # cat([max_k x1 repeated, x1, att_map])
+        y = conv_bn(y, conv, bn)
     y = conv_bn(y, desc.mlp2[0], desc.mlp2[1])
     d = group_max(y, k)
     return kp.view(nb, M, 3), sig, att_feat, d, wnext, fps_loc

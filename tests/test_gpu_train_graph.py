@@ -143,6 +143,34 @@ def test_attention(tg, k, C, Cv, same):
         _close(x, y, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("k,C1,Ca,N,G", [(64, 64, 64, 32, 512), (32, 128, 128, 64, 1024), (16, 64, 128, 96, 2048)])
+def test_tail_conv_bn_act_bitwise(tg, k, C1, Ca, N, G):
+    """r6: the descriptor's mlp1 without its concatenation (train.tail_conv_bn_act: the forward
+    GEMM + statistics and the weight gradient read x2 / x1 / att_map in place) gives desc_tail +
+    conv_bn_act's bits -- output, running statistics and every gradient -- at levels 1 and 2's
+    widths (k, C1 = Ca, N; level 3's 768-wide W' exceeds ts_gemm's LDS and stays on the
+    concatenation path) and a mixed-width case."""
+    from pcd_reg_hregnet_amd import train
+    R = G * k
+    assert train.tail_fusable(R, k, C1, Ca, N)
+    ins = [_rand(R, C1, seed=1), _rand(R, Ca, seed=2), _rand(N, 2 * C1 + Ca, seed=3, scale=0.05),
+           _rand(N, seed=4, scale=0.1), 1 + _rand(N, seed=5, scale=0.1), _rand(N, seed=6, scale=0.1)]
+    rms = [(torch.zeros(N, device=DEV), torch.ones(N, device=DEV)) for _ in range(2)]
+
+    def fused(x1, att, W, b, ga, be):
+        return train.tail_conv_bn_act(x1, att, k, W, b, ga, be, *rms[0])
+
+    def cat(x1, att, W, b, ga, be):
+        return train.conv_bn_act(tg.desc_tail(x1, att, k), W, b, ga, be, *rms[1])
+
+    o1, g1 = _grads(fused, ins)
+    o2, g2 = _grads(cat, ins)
+    assert torch.equal(o1[0], o2[0])
+    assert torch.equal(rms[0][0], rms[1][0]) and torch.equal(rms[0][1], rms[1][1])
+    for a, b, nm in zip(g1, g2, ("x1", "att", "W", "bias", "gamma", "beta")):
+        assert torch.equal(a, b), nm
+
+
 def test_group_max(tg):
     G, k, C = 30, 16, 40
     x = _rand(G * k, C, seed=11)
@@ -573,7 +601,7 @@ def test_train_descriptor_backward_replay():
     sides see the same inputs."""
     import copy
 
-    from pcd_reg_hregnet_amd import engine, train_graph
+    from pcd_reg_hregnet_amd import engine, train, train_graph
     fx = _ref_fixture()
     net = _train_net()
     ref_net = copy.deepcopy(net).double()
@@ -594,11 +622,17 @@ def test_train_descriptor_backward_replay():
             rec["att_map"] = att_map.detach().clone()
             return o_tail(x1, att_map, k)
 
-        train_graph.seq_convs, train_graph.desc_tail = seq, tail
+        o_fused = train.tail_conv_bn_act
+
+        def fused(x1, att_map, k, *a, **kw):  # the same, without materialising it (r6)
+            rec["att_map"] = att_map.detach().clone()
+            return o_fused(x1, att_map, k, *a, **kw)
+
+        train_graph.seq_convs, train_graph.desc_tail, train.tail_conv_bn_act = seq, tail, fused
         try:
             out = orig_kl(det, desc, lvl, xyz, feats, weights, hook, part, use_fps)
         finally:
-            train_graph.seq_convs, train_graph.desc_tail = o_seq, o_tail
+            train_graph.seq_convs, train_graph.desc_tail, train.tail_conv_bn_act = o_seq, o_tail, o_fused
         out[3].retain_grad()
         rec["d"] = out[3]
         caps.append(rec)
