@@ -619,6 +619,8 @@ def in_executor(steps: int, B: int, points: int, entries_flops: dict, merge: int
             d = json.load(open(path))[key]
         except (OSError, KeyError, ValueError):
             continue
+        if not isinstance(d, dict) or not isinstance(d.get("avg_us"), dict):
+            continue    # malformed entry: no in-executor figure rather than no bench line
         t = 0.0
         fl = 0.0
         per = {}
