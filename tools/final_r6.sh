@@ -4,6 +4,7 @@
 #   t: GPU suite (+ parity tables) + smoke      b: bench default line + the driver's --steps 20 line
 #   x: kernel traces (graph + eager) + in-executor figure     p: FETCH / WRITE / MFMA PMC passes
 #   v: Model_V2 line          r: training line           k: issue / wait counters (pmc_kernels)
+#   q: training step kernel trace
 set -o pipefail
 TAG=${1:-r6f}; PARTS=${2:-tbx}
 O=gpurun_out/$TAG; mkdir -p $O
@@ -60,6 +61,11 @@ fi
 if [[ $PARTS == *r* ]]; then
   timeout -k 10 300 python bench.py --model train --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_train.json 2> $O/bench_train.err \
     || { echo train failed; tail $O/bench_train.err; exit 1; }
+fi
+if [[ $PARTS == *q* ]]; then  # training step kernel trace
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/traintrace -o run -- \
+    python3 bench.py --model train --steps 6 --warmup 2 --no-cpu-baseline \
+    > $O/traintrace.log 2>&1 || { echo traintrace failed; tail $O/traintrace.log; exit 1; }
 fi
 if [[ $PARTS == *k* ]]; then
   bash tools/pmc_kernels.sh $TAG/pmck "--steps 4 --warmup 4" > /dev/null 2>&1 || echo "pmc_kernels failed"
