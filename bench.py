@@ -1213,8 +1213,12 @@ def main():
         lv_fl = {level_kernel(engine, 1): L1_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[0][0],
                  level_kernel(engine, 2): L2_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[1][0],
                  level_kernel(engine, 3): L3_FLOPS_PER_GROUP * 2 * B * merge * engine.LEVELS[2][0]}
-        inexec = (in_executor(args.steps, B, args.points, lv_fl, merge)
-                  if not v2 and args.executor == "graph" else None)
+        inexec = None
+        if not v2 and args.executor == "graph":
+            try:
+                inexec = in_executor(args.steps, B, args.points, lv_fl, merge)
+            except Exception as e:  # a committed-trace figure must never sink the GPU number
+                inexec = {"error": repr(e)}
         fps = None
         try:
             fps = fps_latency(src[:B], dst[:B])
