@@ -88,6 +88,10 @@ V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", True)  # GraphPipeline(v2=Tru
 # 4 x 12 lanes x merged batches, gpurun_out/r6v2)
 FRONT_STREAM = switches.flag("FRONT_STREAM", True)
 FRONT_STREAM_MAX_LANES = 24
+# capture order of a front-streaming round's jobs (GraphPipeline._fork): 0 = per lane (back,
+# front); 1 = every front first, then the backs (the graph's branches reach the 4 hardware
+# queues in capture order, round robin)
+FORK_ORDER = 0
 # Single-batch latency (one forward alone on the GPU is one dependent chain of ~50 kernels): work
 # that does not depend on the chain's previous kernel runs beside it on a side stream -- the
 # level-1 spatial index (input points only) beside the level-1 FPS, the level-2/3 input
@@ -1910,11 +1914,15 @@ class GraphPipeline:
         jobs = []
         if side_all is not None:
             jobs.append((self.side[0], lambda _ln: side_all(), -1))
+        seconds_first = body2 is not None and FORK_ORDER == 1
+        if seconds_first:
+            # (FORK_ORDER 1: every lane's second job captured first, then the first jobs)
+            jobs += [(self.lane_streams2[ln], body2, ln) for ln in range(lanes)]
         for ln in range(lanes):
             if side is not None and ln < side_lanes:
                 jobs.append((self.side[ln], side, ln))
             jobs.append((None if ln == 0 else self.lane_streams[ln], body, ln))
-            if body2 is not None:  # (a second job per lane on its own stream)
+            if body2 is not None and not seconds_first:  # (a second job per lane on its own stream)
                 jobs.append((self.lane_streams2[ln], body2, ln))
         for st, _, _ in jobs:
             if st is not None:
