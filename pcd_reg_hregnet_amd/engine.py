@@ -1911,19 +1911,21 @@ class GraphPipeline:
         main = torch.cuda.current_stream()
         lanes = self.lanes if lanes is None else lanes
         side_lanes = lanes if side_lanes is None else side_lanes
-        jobs = []
-        if side_all is not None:
-            jobs.append((self.side[0], lambda _ln: side_all(), -1))
-        seconds_first = body2 is not None and FORK_ORDER == 1
-        if seconds_first:
-            # (FORK_ORDER 1: every lane's second job captured first, then the first jobs)
-            jobs += [(self.lane_streams2[ln], body2, ln) for ln in range(lanes)]
+        sj = [(self.side[0], lambda _ln: side_all(), -1)] if side_all is not None else []
+        firsts, seconds, pairs = [], [], []
         for ln in range(lanes):
-            if side is not None and ln < side_lanes:
-                jobs.append((self.side[ln], side, ln))
-            jobs.append((None if ln == 0 else self.lane_streams[ln], body, ln))
-            if body2 is not None and not seconds_first:  # (a second job per lane on its own stream)
-                jobs.append((self.lane_streams2[ln], body2, ln))
+            lj = [(self.side[ln], side, ln)] if side is not None and ln < side_lanes else []
+            lj.append((None if ln == 0 else self.lane_streams[ln], body, ln))
+            firsts += lj
+            pairs += lj
+            if body2 is not None:  # (a second job per lane on its own stream)
+                seconds.append((self.lane_streams2[ln], body2, ln))
+                pairs.append(seconds[-1])
+        order = FORK_ORDER if body2 is not None else 0
+        # (FORK_ORDER, front streaming: 1 every front first, 2 every back first, 3 the batched
+        # stage 1 last)
+        jobs = (sj + pairs if order == 0 else sj + seconds + firsts if order == 1 else
+                sj + firsts + seconds if order == 2 else pairs + sj)
         for st, _, _ in jobs:
             if st is not None:
                 st.wait_stream(main)
