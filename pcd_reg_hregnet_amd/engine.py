@@ -88,10 +88,6 @@ V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", True)  # GraphPipeline(v2=Tru
 # 4 x 12 lanes x merged batches, gpurun_out/r6v2)
 FRONT_STREAM = switches.flag("FRONT_STREAM", True)
 FRONT_STREAM_MAX_LANES = 24
-# capture order of a front-streaming round's jobs (GraphPipeline._fork): 0 = per lane (back,
-# front); 1 = every front first, then the backs (the graph's branches reach the 4 hardware
-# queues in capture order, round robin)
-FORK_ORDER = 0
 # Single-batch latency (one forward alone on the GPU is one dependent chain of ~50 kernels): work
 # that does not depend on the chain's previous kernel runs beside it on a side stream -- the
 # level-1 spatial index (input points only) beside the level-1 FPS, the level-2/3 input
@@ -1911,21 +1907,15 @@ class GraphPipeline:
         main = torch.cuda.current_stream()
         lanes = self.lanes if lanes is None else lanes
         side_lanes = lanes if side_lanes is None else side_lanes
-        sj = [(self.side[0], lambda _ln: side_all(), -1)] if side_all is not None else []
-        firsts, seconds, pairs = [], [], []
+        jobs = []
+        if side_all is not None:
+            jobs.append((self.side[0], lambda _ln: side_all(), -1))
         for ln in range(lanes):
-            lj = [(self.side[ln], side, ln)] if side is not None and ln < side_lanes else []
-            lj.append((None if ln == 0 else self.lane_streams[ln], body, ln))
-            firsts += lj
-            pairs += lj
+            if side is not None and ln < side_lanes:
+                jobs.append((self.side[ln], side, ln))
+            jobs.append((None if ln == 0 else self.lane_streams[ln], body, ln))
             if body2 is not None:  # (a second job per lane on its own stream)
-                seconds.append((self.lane_streams2[ln], body2, ln))
-                pairs.append(seconds[-1])
-        order = FORK_ORDER if body2 is not None else 0
-        # (FORK_ORDER, front streaming: 1 every front first, 2 every back first, 3 the batched
-        # stage 1 last)
-        jobs = (sj + pairs if order == 0 else sj + seconds + firsts if order == 1 else
-                sj + firsts + seconds if order == 2 else pairs + sj)
+                jobs.append((self.lane_streams2[ln], body2, ln))
         for st, _, _ in jobs:
             if st is not None:
                 st.wait_stream(main)
