@@ -88,7 +88,6 @@ V2_BATCH_STAGE1 = switches.flag("V2_BATCH_STAGE1", True)  # GraphPipeline(v2=Tru
 # 4 x 12 lanes x merged batches, gpurun_out/r6v2)
 FRONT_STREAM = switches.flag("FRONT_STREAM", True)
 FRONT_STREAM_MAX_LANES = 24
-FORK_PERM = ""  # (probe: capture order of a front-streaming round's jobs, '-'-joined indices)
 # Single-batch latency (one forward alone on the GPU is one dependent chain of ~50 kernels): work
 # that does not depend on the chain's previous kernel runs beside it on a side stream -- the
 # level-1 spatial index (input points only) beside the level-1 FPS, the level-2/3 input
@@ -1917,10 +1916,6 @@ class GraphPipeline:
             jobs.append((None if ln == 0 else self.lane_streams[ln], body, ln))
             if body2 is not None:  # (a second job per lane on its own stream)
                 jobs.append((self.lane_streams2[ln], body2, ln))
-        if FORK_PERM and body2 is not None:
-            idx = [int(x) for x in FORK_PERM.split("-")]
-            if sorted(idx) == list(range(len(jobs))):
-                jobs = [jobs[i] for i in idx]
         for st, _, _ in jobs:
             if st is not None:
                 st.wait_stream(main)
