@@ -418,6 +418,19 @@ int hreg_ts_gemm_bn_tail(const float *x2, int k, const float *x1, int C1, const 
                          const float *W, int N, const float *shift, float *out, int ldo, float eps,
                          float momentum, void *ws, float *mean, float *invstd, float *var_unbiased,
                          float *running_mean, float *running_var, void *stream);
+/* hreg_ts_gemm_bn (w_trans 0) with A = the previous layer's pre-BatchNorm output [R][K]: every A
+ * value enters as act(pre_gamma * (A - pre_mean) * pre_invstd + pre_beta) (act = ReLU if
+ * pre_relu; hreg_bn_apply's arithmetic, per column k), so out and the statistics are those of
+ * hreg_bn_apply followed by hreg_ts_gemm_bn, without the activation materialised (the
+ * train-mode Conv+BN+ReLU chains of layers.py:115-130, 183-198; r6).  hreg_ts_gemm_pre_supported
+ * != 0 when the kernel takes the shape (K <= 512, up to 4 output tiles of 32 per workgroup).
+ * ws = hreg_ts_gemm_bn_ws_bytes(R, K, N) bytes. */
+int hreg_ts_gemm_pre_supported(int R, int K, int N);
+int hreg_ts_gemm_bn_pre(const float *A, int lda, int R, int K, const float *W, int N, const float *shift,
+                        float *out, int ldo, float eps, float momentum, void *ws, float *mean, float *invstd,
+                        float *var_unbiased, float *running_mean, float *running_var, const float *pre_mean,
+                        const float *pre_invstd, const float *pre_gamma, const float *pre_beta, int pre_relu,
+                        void *stream);
 /* out = act(gamma * (y - mean) * invstd + beta), act = ReLU if relu (out may alias y) */
 int hreg_bn_apply(const float *y, int R, int C, const float *mean, const float *invstd,
                   const float *gamma, const float *beta, int relu, float *out, void *stream);
@@ -445,6 +458,14 @@ int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N,
  * ws = hreg_gemm_tn_ws_bytes(R, N, 2 C1 + Ca) bytes. */
 int hreg_gemm_tn_tail(const float *A, int lda, const float *x2, int k, const float *x1, int C1,
                       const float *att, int Ca, int R, int N, float beta, void *ws, float *out, void *stream);
+/* hreg_gemm_tn with B = the previous layer's pre-BatchNorm output [R][K]: B enters as
+ * act(pre_gamma * (B - pre_mean) * pre_invstd + pre_beta) per column (hreg_bn_apply's arithmetic);
+ * the same splits and sums as hreg_gemm_tn over the materialised activation (the weight gradient
+ * of a Conv whose input is the previous Conv+BN+ReLU's output; r6).  lda, ldb multiples of 4,
+ * 16-byte aligned A and B (else HREG_ERR_UNSUPPORTED).  ws = hreg_gemm_tn_ws_bytes(R, N, K). */
+int hreg_gemm_tn_pre(const float *A, int lda, const float *B, int ldb, int R, int N, int K, float beta, void *ws,
+                     float *out, const float *pre_mean, const float *pre_invstd, const float *pre_gamma,
+                     const float *pre_beta, int pre_relu, void *stream);
 /* out [C][R] = in [R][C]^T */
 int hreg_transpose(const float *in, int R, int C, float *out, void *stream);
 /* y[i] += x[i] (fp32, one rounding) over n floats: the second gradient bucket of the

@@ -138,6 +138,10 @@ _SIGS = {
     "hreg_gemm_tn_tail": [_vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp],
     "hreg_ts_gemm_bn": [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, ctypes.c_float, ctypes.c_float, _vp,
                         _vp, _vp, _vp, _vp, _vp, _vp],
+    "hreg_ts_gemm_pre_supported": [_i, _i, _i],
+    "hreg_ts_gemm_bn_pre": [_vp, _i, _i, _i, _vp, _i, _vp, _vp, _i, ctypes.c_float, ctypes.c_float, _vp,
+                            _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp],
+    "hreg_gemm_tn_pre": [_vp, _i, _vp, _i, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp],
     "hreg_transpose": [_vp, _i, _i, _vp, _vp],
     "hreg_add_into": [_vp, _vp, ctypes.c_size_t, _vp],
     "hreg_adam_step": [_vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_float, ctypes.c_float,

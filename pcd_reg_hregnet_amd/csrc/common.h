@@ -54,6 +54,15 @@ __device__ __forceinline__ float fmul_rn(float a, float b) { return __fmul_rn(a,
 __device__ __forceinline__ float fadd_rn(float a, float b) { return __fadd_rn(a, b); }
 __device__ __forceinline__ float fsub_rn(float a, float b) { return __fsub_rn(a, b); }
 
+// Train-mode BatchNorm apply (+ ReLU) of one value: act(gamma * ((y - mean) * invstd) + beta),
+// the one arithmetic of hreg_bn_apply and of the GEMMs that apply it on load (train.hip,
+// ts_gemm.hip)
+__device__ __forceinline__ float bn_act(float y, float mu, float is, float ga, float be, int relu) {
+    const float xh = fmul_rn(fsub_rn(y, mu), is);
+    const float v = fadd_rn(fmul_rn(xh, ga), be);
+    return relu ? fmaxf(v, 0.f) : v;
+}
+
 // Squared distance in the reference's order: (dx*dx + dy*dy) + dz*dz, two
 // roundings per term (furthest_point_sampling_gpu.cu:129; pytorch3d knn loop).
 __device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx, float by,

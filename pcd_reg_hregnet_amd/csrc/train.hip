@@ -199,12 +199,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const float4 *__restrict
         const float *yp = &yv.x, *mp = &mu.x, *ip = &is.x, *gp = &ga.x, *bp = &be.x;
         float o[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float xh = fmul_rn(fsub_rn(yp[u], mp[u]), ip[u]);
-            float v = fadd_rn(fmul_rn(xh, gp[u]), bp[u]);
-            if (relu) v = fmaxf(v, 0.f);
-            o[u] = v;
-        }
+        for (int u = 0; u < 4; ++u) o[u] = bn_act(yp[u], mp[u], ip[u], gp[u], bp[u], relu);
         out[i] = make_float4(o[0], o[1], o[2], o[3]);
     }
 }
@@ -246,10 +241,7 @@ __global__ void bn_apply_kernel(const float *__restrict__ y, const float *__rest
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (size_t)gridDim.x * blockDim.x) {
         const int c = (int)(i % C);
-        const float xh = fmul_rn(fsub_rn(y[i], mean[c]), invstd[c]);
-        float v = fadd_rn(fmul_rn(xh, gamma[c]), beta[c]);
-        if (relu) v = fmaxf(v, 0.f);
-        out[i] = v;
+        out[i] = bn_act(y[i], mean[c], invstd[c], gamma[c], beta[c], relu);
     }
 }
 
@@ -410,12 +402,19 @@ struct TnSeg {
     const float *base[3];
     int ld[3], div[3], kend[3], rows[3];
 };
+// (PREB, r6) B is the previous layer's pre-BatchNorm output: each staged B value is
+// bn_act(B, mean[k], invstd[k], gamma[k], beta[k], relu) (hreg_bn_apply's arithmetic; rows past
+// R stay 0), so the sums are those over the materialised activation
+struct TnPre {
+    const float *mean, *invstd, *gamma, *beta;
+    int relu;
+};
 
-template <int TNN, int TNK, bool SEG = false>
+template <int TNN, int TNK, bool SEG = false, bool PREB = false>
 __global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__ A, int lda,
                                                        const float *__restrict__ Bm, int ldb, int R,
                                                        int N, int K, int rows_per_split,
-                                                       float *__restrict__ ws, TnSeg sg = {}) {
+                                                       float *__restrict__ ws, TnSeg sg = {}, TnPre pb = {}) {
     constexpr int WA = 32 * TNN, WB = 32 * TNK, TW = WB;  // tile widths (floats)
     constexpr int FA = WA / 4, FB = WB / 4;               // float4 per row
     constexpr int LA = TN_ROWS * FA / 256, LB = TN_ROWS * FB / 256;  // float4 loads per thread
@@ -452,9 +451,25 @@ __global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
     v4f ga[LA], gb[LB];
+    // (PREB) this thread's 4 B columns are the same in every staged row (256 % FB == 0)
+    v4f pm = {}, pi = {}, pg = {}, pbe = {};
+    int gbase = 0;
+    if constexpr (PREB) {
+        static_assert(256 % FB == 0, "B column per thread");
+        const int c0 = bcol + 4 * (tid % FB);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool ok = c0 + u < K;
+            pm[u] = ok ? pb.mean[c0 + u] : 0.f;
+            pi[u] = ok ? pb.invstd[c0 + u] : 0.f;
+            pg[u] = ok ? pb.gamma[c0 + u] : 0.f;
+            pbe[u] = ok ? pb.beta[c0 + u] : 0.f;
+        }
+    }
     // rows past R read 0 (buffer bounds); columns past N / K feed only accumulator entries that
     // are never stored (the tile's columns stay inside the row: lda >= N, ldb >= K, 4 | lda, ldb)
     auto gload = [&](int base) {
+        gbase = base;
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
             const int e = tid + 256 * i, r = e / FA, c4 = e - r * FA;
@@ -473,7 +488,15 @@ __global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__
 #pragma unroll
         for (int i = 0; i < LA; ++i) *reinterpret_cast<v4f *>(As + 4 * (tid + 256 * i)) = ga[i];
 #pragma unroll
-        for (int i = 0; i < LB; ++i) *reinterpret_cast<v4f *>(Bs + 4 * (tid + 256 * i)) = gb[i];
+        for (int i = 0; i < LB; ++i) {
+            v4f v = gb[i];
+            if constexpr (PREB) {
+                const bool live = gbase + (tid + 256 * i) / FB < R;  // (rows past R stay 0)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = live ? bn_act(v[u], pm[u], pi[u], pg[u], pbe[u], pb.relu) : 0.f;
+            }
+            *reinterpret_cast<v4f *>(Bs + 4 * (tid + 256 * i)) = v;
+        }
     };
     const int nit = r1 > r0 ? (r1 - r0 + TN_ROWS - 1) / TN_ROWS : 0;
     if (nit) gload(r0);
@@ -821,6 +844,46 @@ static int gemm_tn_launch(const float *A, int lda, const float *B, int ldb, int 
 extern "C" int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N, int K,
                             float beta, void *ws, float *out, void *stream) {
     return gemm_tn_launch(A, lda, B, ldb, R, N, K, beta, ws, out, stream, R > 0 ? tn_splits(R, N, K) : 1);
+}
+
+// hreg_gemm_tn with B = the previous layer's pre-BatchNorm output: B enters as
+// bn_act(B, pre_mean, pre_invstd, pre_gamma, pre_beta, pre_relu) per column (the weight gradient
+// dW = dY^T act(y_in) of train.py _ConvStats without the activation materialised); the same
+// splits and sums as hreg_gemm_tn over the materialised B.  16-byte aligned rows only.
+extern "C" int hreg_gemm_tn_pre(const float *A, int lda, const float *B, int ldb, int R, int N, int K, float beta,
+                                void *ws, float *out, const float *pre_mean, const float *pre_invstd,
+                                const float *pre_gamma, const float *pre_beta, int pre_relu, void *stream) {
+    if (!A || !B || !ws || !out || R <= 0 || N <= 0 || K <= 0 || lda < N || ldb < K || !pre_mean || !pre_invstd ||
+        !pre_gamma || !pre_beta)
+        return HREG_ERR_INVALID;
+    if ((lda & 3) || (ldb & 3) || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) ||
+        (size_t)R * lda * sizeof(float) >= ((size_t)1 << 31) || (size_t)R * ldb * sizeof(float) >= ((size_t)1 << 31))
+        return HREG_ERR_UNSUPPORTED;
+    const int S = tn_splits(R, N, K);
+    int rps = (R + S - 1) / S;
+    rps = (rps + TN_ROWS - 1) / TN_ROWS * TN_ROWS;
+    hipStream_t st = as_stream(stream);
+    const int tnn = N <= 32 ? 1 : 2, tnk = K <= 32 ? 1 : 2;
+    const dim3 grid((N + 32 * tnn - 1) / (32 * tnn), (K + 32 * tnk - 1) / (32 * tnk), S);
+    const TnPre pre{pre_mean, pre_invstd, pre_gamma, pre_beta, pre_relu ? 1 : 0};
+#define TNP_CASE(a, b)                                                                                          \
+    hipLaunchKernelGGL((gemm_tn4_kernel<a, b, false, true>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, \
+                       (float *)ws, TnSeg{}, pre)
+    if (tnn == 1 && tnk == 1) TNP_CASE(1, 1);
+    else if (tnn == 1) TNP_CASE(1, 2);
+    else if (tnk == 1) TNP_CASE(2, 1);
+    else TNP_CASE(2, 2);
+#undef TNP_CASE
+    HREG_CHECK_LAUNCH();
+    const size_t NK = (size_t)N * K;
+    if (S >= 16)
+        hipLaunchKernelGGL(tn_reduce_kernel<16>, dim3((unsigned)((NK + 15) / 16)), dim3(256), 0, st,
+                           (const float *)ws, S, NK, beta, out);
+    else
+        hipLaunchKernelGGL(tn_reduce_kernel<1>, dim3(grid1d(NK)), dim3(256), 0, st, (const float *)ws,
+                           S, NK, beta, out);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
 }
 
 // hreg_gemm_tn with B = cat([x2 repeated over the k rows of each group, x1, att]) (the descriptor

@@ -25,6 +25,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int TS_LDS_FLOATS = 16384;  // W' column group: NT * 32 rows x (K16 + 4) floats
 constexpr int TS_GRP = 4;             // 16-deep sub-chunks per A load group (k = 64)
+constexpr int TS_PRE_FLOATS = 2048;   // (PRE) the input's BatchNorm parameters: K <= 512
 
 // (SEG, r6) A assembled from column segments instead of one matrix: columns [kend[s-1], kend[s])
 // are segment s's row r / div[s] (stride ld[s]); every kend a multiple of 16, so a lane's 8-column
@@ -38,18 +39,27 @@ struct TsSeg {
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
+// (PRE, r6) A is the previous layer's pre-BatchNorm output: every A value is replaced on load by
+// bn_act(A, mean[k], invstd[k], gamma[k], beta[k], relu) -- hreg_bn_apply's arithmetic, so the
+// products are those of the materialised activation (train.py _ConvStats)
+struct TsPre {
+    const float *mean, *invstd, *gamma, *beta;
+    int relu;
+};
+
 // STATS: the train-mode BatchNorm statistics of the output ride along in the epilogue (the
 // col_reduce pass over y it replaces): every lane keeps fp64 sums of its column's values and
 // squares (exact products) over its rows, in its fixed tile order; the lane halves, then the
 // four waves (in order, through LDS) combine, and each workgroup writes its partial
 // [blockIdx.x][N][2] for col_finalize (train.hip) to sum over workgroups in order.
-template <int NT, bool TAIL, bool FULL, bool STATS = false, bool SEG = false>
+template <int NT, bool TAIL, bool FULL, bool STATS = false, bool SEG = false, bool PRE = false>
 __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict__ A, int lda, int R, int K,
                                                          const float *__restrict__ W, int w_trans, int N,
                                                          const float *__restrict__ scale,
                                                          const float *__restrict__ shift, int relu,
                                                          float *__restrict__ out, int ldo,
-                                                         double *__restrict__ part = nullptr, TsSeg sg = {}) {
+                                                         double *__restrict__ part = nullptr, TsSeg sg = {},
+                                                         TsPre pre = {}) {
     extern __shared__ __attribute__((aligned(16))) float Ws[];
     const int K16 = (K + 15) & ~15, KP = K16 + 4, nsub = K16 / 16;
     const int ngrp = (nsub + TS_GRP - 1) / TS_GRP;
@@ -77,6 +87,18 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
         const int n = n0 + i;
         Sh[i] = (shift && n < N) ? shift[n] : 0.f;
         if (FULL) Sc[i] = (scale && n < N) ? scale[n] : 1.f;
+    }
+    // (PRE) the input's BatchNorm parameters per k, past the statistics' partials (zero past K:
+    // finite values the zero columns of W' cancel)
+    float *Pm = Sh + 2 * NR + (STATS ? 16 * NR : 0);
+    if constexpr (PRE) {
+        for (int i = threadIdx.x; i < K16; i += 256) {
+            const bool ok = i < K;
+            Pm[i] = ok ? pre.mean[i] : 0.f;
+            Pm[K16 + i] = ok ? pre.invstd[i] : 0.f;
+            Pm[2 * K16 + i] = ok ? pre.gamma[i] : 0.f;
+            Pm[3 * K16 + i] = ok ? pre.beta[i] : 0.f;
+        }
     }
     __syncthreads();
 
@@ -144,6 +166,18 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
             if (sub < nsub) {
                 float bv[8] = {cu[2 * u].x,     cu[2 * u].y,     cu[2 * u].z,     cu[2 * u].w,
                                cu[2 * u + 1].x, cu[2 * u + 1].y, cu[2 * u + 1].z, cu[2 * u + 1].w};
+                if constexpr (PRE) {
+                    const float *pk = Pm + sub * 16 + 8 * h;
+                    const float4 m0 = ld4(pk), m1 = ld4(pk + 4), i0 = ld4(pk + K16), i1 = ld4(pk + K16 + 4),
+                                 g0 = ld4(pk + 2 * K16), g1 = ld4(pk + 2 * K16 + 4), b0 = ld4(pk + 3 * K16),
+                                 b1 = ld4(pk + 3 * K16 + 4);
+                    const float mv[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+                    const float iv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+                    const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+                    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bv[e] = bn_act(bv[e], mv[e], iv[e], gv[e], bb[e], pre.relu);
+                }
                 if (TAIL && sub == nsub - 1) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) bv[e] = sub * 16 + 8 * h + e < K ? bv[e] : 0.f;
@@ -281,9 +315,10 @@ namespace {
 
 // launch (STATS: the workgroups' statistic partials into part, see ts_gemm_kernel); returns
 // the number of workgroups along the rows (the partials' count), or a negative HREG_ERR_*
-template <bool STATS, bool SEG = false>
+template <bool STATS, bool SEG = false, bool PRE = false>
 int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans, int N, const float *scale,
-              const float *shift, int relu, float *out, int ldo, double *part, hipStream_t st, TsSeg sg = {}) {
+              const float *shift, int relu, float *out, int ldo, double *part, hipStream_t st, TsSeg sg = {},
+              TsPre pre = {}) {
     if (!A || !W || !out || R <= 0 || K <= 0 || N <= 0 || lda < K || ldo < N || (K & 3) || (N & 3) ||
         (lda & 3) || (ldo & 3) || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W) |
                                      reinterpret_cast<uintptr_t>(out)) & 15))
@@ -294,21 +329,25 @@ int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans
     if (nt <= 0) return -HREG_ERR_UNSUPPORTED;
     const int gx = ts_grid_x(R, K, N, STATS);
     const int gy = (N + nt * 32 - 1) / (nt * 32);
-    const size_t lds = ((size_t)nt * 32 * (((K + 15) & ~15) + 4) + 2 * nt * 32 + (STATS ? 16 * nt * 32 : 0)) *
-                       sizeof(float);
-    if (lds > TS_LDS_FLOATS * sizeof(float)) return -HREG_ERR_UNSUPPORTED;  // (ts_nt's budget)
+    const size_t lds0 = ((size_t)nt * 32 * (((K + 15) & ~15) + 4) + 2 * nt * 32 + (STATS ? 16 * nt * 32 : 0)) *
+                        sizeof(float);
+    if (lds0 > TS_LDS_FLOATS * sizeof(float)) return -HREG_ERR_UNSUPPORTED;  // (ts_nt's budget)
+    // (PRE: + the input's 4 x K16 BatchNorm parameters, <= TS_PRE_FLOATS beyond the budget)
+    const size_t lds = lds0 + (PRE ? (size_t)4 * ((K + 15) & ~15) * sizeof(float) : 0);
+    if (PRE && 4 * ((K + 15) & ~15) > TS_PRE_FLOATS) return -HREG_ERR_UNSUPPORTED;
     const bool tail = (K & 15) != 0, full = scale != nullptr || relu;
     if (STATS && full) return -HREG_ERR_UNSUPPORTED;
 #define TS_CASE(NTT, TT, FF)                                                                                   \
     if (nt == NTT && tail == TT && full == FF) {                                                              \
-        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF, STATS, SEG>), dim3(gx, gy), dim3(256), lds, st, A, lda, R, \
-                           K, W, w_trans, N, scale, shift, relu, out, ldo, part, sg);                          \
+        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF, STATS, SEG, PRE>), dim3(gx, gy), dim3(256), lds, st, A, lda, \
+                           R, K, W, w_trans, N, scale, shift, relu, out, ldo, part, sg, pre);                  \
         if (hipGetLastError() != hipSuccess) return -HREG_ERR_LAUNCH;                                          \
         return gx;                                                                                             \
     }
 #define TS_NT_CASE(NTT) TS_CASE(NTT, false, false) TS_CASE(NTT, true, false)                           \
     if constexpr (!STATS) { TS_CASE(NTT, false, true) TS_CASE(NTT, true, true) }
-    TS_NT_CASE(1) TS_NT_CASE(2) TS_NT_CASE(4) TS_NT_CASE(8)
+    TS_NT_CASE(1) TS_NT_CASE(2) TS_NT_CASE(4)
+    if constexpr (!PRE) { TS_NT_CASE(8) }  // (PRE at 8 tiles spills: <= 4, ts_pre_ok)
 #undef TS_NT_CASE
 #undef TS_CASE
     return -HREG_ERR_UNSUPPORTED;
@@ -342,6 +381,31 @@ extern "C" int hreg_ts_gemm_bn(const float *A, int lda, int R, int K, const floa
     if (S < 0) return -S;
     return hreg_bn_finalize_stats(static_cast<const double *>(ws), S, R, N, eps, mean, invstd, var_unbiased,
                                   momentum, running_mean, running_var, st);
+}
+
+// hreg_ts_gemm_bn with A = the previous layer's pre-BatchNorm output y_in [R][K]: every value of
+// A enters as bn_act(y_in, pre_mean, pre_invstd, pre_gamma, pre_beta, pre_relu) (hreg_bn_apply's
+// arithmetic), so out, the statistics and the running update are those of hreg_bn_apply followed
+// by hreg_ts_gemm_bn, without the activation's write and read (r6, train.py _ConvStats).
+extern "C" int hreg_ts_gemm_bn_pre(const float *A, int lda, int R, int K, const float *W, int N,
+                                   const float *shift, float *out, int ldo, float eps, float momentum, void *ws,
+                                   float *mean, float *invstd, float *var_unbiased, float *running_mean,
+                                   float *running_var, const float *pre_mean, const float *pre_invstd,
+                                   const float *pre_gamma, const float *pre_beta, int pre_relu, void *stream) {
+    if (!ws || !mean || !invstd || R <= 0 || ((running_mean == nullptr) != (running_var == nullptr)) ||
+        (running_mean && !var_unbiased) || !pre_mean || !pre_invstd || !pre_gamma || !pre_beta)
+        return HREG_ERR_INVALID;
+    hipStream_t st = as_stream(stream);
+    TsPre pre{pre_mean, pre_invstd, pre_gamma, pre_beta, pre_relu ? 1 : 0};
+    const int S = ts_launch<true, false, true>(A, lda, R, K, W, 0, N, nullptr, shift, 0, out, ldo,
+                                               static_cast<double *>(ws), st, {}, pre);
+    if (S < 0) return -S;
+    return hreg_bn_finalize_stats(static_cast<const double *>(ws), S, R, N, eps, mean, invstd, var_unbiased,
+                                  momentum, running_mean, running_var, st);
+}
+
+extern "C" int hreg_ts_gemm_pre_supported(int R, int K, int N) {
+    return hreg_ts_gemm_supported(R, K, N, 1) && 4 * ((K + 15) & ~15) <= TS_PRE_FLOATS && ts_nt(K, N, true) <= 4;
 }
 
 // hreg_ts_gemm_bn over the descriptor tail's rows without the concatenation (r6): A = cat([x2

@@ -406,6 +406,152 @@ def tail_conv_bn_act(x1, att, k, W, bias, gamma, beta, running_mean=None, runnin
                                 running_var, k, momentum, eps, wparam if wparam is not None else W)
 
 
+# Chains of Conv + train-mode BN + ReLU layers (nn.Sequential, layers.py:115-130, 183-198) with the
+# inner activations never materialised (r6): each conv after the first reads the previous layer's
+# pre-BN output and applies that BN + ReLU on load (hreg_ts_gemm_bn_pre forward, hreg_gemm_tn_pre
+# weight gradient), and only the chain's last activation is written (_BNAct).  Every kernel
+# computes conv_bn_act's values in its order, so outputs and gradients are bitwise its own.
+CHAIN_FUSED = switches.flag("CHAIN_FUSED", True)
+
+
+class _ConvStats(torch.autograd.Function):
+    """y = act_prev(x) W^T + bias with this layer's train-mode BN statistics (and running update);
+    act_prev = the previous layer's BN + ReLU (pre_* tensors) or the identity (the chain's first
+    layer).  -> y (pre-BN), mean, invstd.  The backward returns dL/dx through act_prev: the
+    previous layer's BN backward runs here (its dgamma / dbeta into the previous BN's .grad)."""
+
+    @staticmethod
+    def forward(ctx, x, W, bias, pre_mean, pre_invstd, pre_gamma, pre_beta, running_mean, running_var,
+                momentum, eps, wparam):
+        R, K = x.shape
+        N = W.shape[0]
+        dev = x.device
+        st = _stream()
+        defer = DEFERRED_RUNNING is not None and running_mean is not None
+        rm, rv = (None, None) if defer else (running_mean, running_var)
+        y = torch.empty(R, N, device=dev)
+        mean, invstd, var = (torch.empty(N, device=dev) for _ in range(3))
+        ws = _ws(_lib.load().hreg_ts_gemm_bn_ws_bytes(R, K, N), dev)
+        shift = None if bias is None else bias.contiguous()
+        if pre_mean is None:
+            _lib.call("hreg_ts_gemm_bn", x, K, R, K, W, 0, N, shift, y, N, float(eps), float(momentum), ws,
+                      mean, invstd, var, rm, rv, st)
+        else:
+            _lib.call("hreg_ts_gemm_bn_pre", x, K, R, K, W, N, shift, y, N, float(eps), float(momentum), ws,
+                      mean, invstd, var, rm, rv, pre_mean, pre_invstd, pre_gamma, pre_beta, 1, st)
+        if defer:
+            DEFERRED_RUNNING.append((mean, var, running_mean, running_var, momentum))
+        ctx.save_for_backward(x, W, pre_mean, pre_invstd, pre_gamma, pre_beta)
+        ctx.side = _SIDE
+        ctx.pre = pre_mean is not None
+        ctx.has_bias = bias is not None
+        ctx.params = (wparam, bias, pre_gamma, pre_beta)
+        ctx.mark_non_differentiable(mean, invstd)
+        return y, mean, invstd
+
+    @staticmethod
+    def backward(ctx, dy, _dmean, _dinvstd):
+        x, W, pm, pi, pg, pbt = ctx.saved_tensors
+        dy = dy.contiguous()
+        R, N = dy.shape
+        K = x.shape[1]
+        dev = dy.device
+        st = _stream()
+        wp, bp, gp, btp = ctx.params
+        gw = _grad_slot(wp, ctx.side) if ctx.needs_input_grad[1] else None
+        gb = _grad_slot(bp, ctx.side) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        dW = None
+        if ctx.needs_input_grad[1]:
+            if ctx.pre:
+                out = gw.view(W.shape) if gw is not None else torch.empty(N, K, device=dev)
+                ws = _ws(_lib.load().hreg_gemm_tn_ws_bytes(R, N, K), dev)
+                _lib.call("hreg_gemm_tn_pre", dy, N, x, K, R, N, K, 1.0 if gw is not None else 0.0, ws, out,
+                          pm, pi, pg, pbt, 1, st)
+                if gw is None:
+                    dW = out
+            elif gw is not None:
+                gemm_tn(dy, x, into=gw.view(W.shape))
+            else:
+                dW = gemm_tn(dy, x)
+        dbias = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            if gb is not None:
+                col_sum(dy, into=gb)
+            else:
+                dbias = col_sum(dy)
+        dx = dgamma = dbeta = None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_gemm(dy, W, None, w_trans=True)  # d act_prev(x)
+            if ctx.pre:
+                # the previous layer's BN + ReLU backward (conv_bn_act's, with its ReLU mask from x)
+                gg, gbt = _grad_slot(gp, ctx.side), _grad_slot(btp, ctx.side)
+                acc = gg is not None and gbt is not None and ctx.needs_input_grad[5] and ctx.needs_input_grad[6]
+                dgamma = gg if acc else torch.empty(K, device=dev)
+                dbeta = gbt if acc else torch.empty(K, device=dev)
+                dxy = torch.empty_like(x)
+                _lib.call("hreg_bn_backward", dx, None, x, R, K, pm, pi, pg, pbt, 1, col_reduce_ws(R, K, dev), dxy,
+                          dgamma, dbeta, 1 if acc else 0, st)
+                dx = dxy
+                if acc:
+                    dgamma = dbeta = None
+        return dx, dW, dbias, None, None, dgamma, dbeta, None, None, None, None, None
+
+
+class _BNAct(torch.autograd.Function):
+    """out = ReLU(BN(y)) with the statistics _ConvStats made (the chain's last activation)"""
+
+    @staticmethod
+    def forward(ctx, y, mean, invstd, gamma, beta):
+        R, C = y.shape
+        out = torch.empty_like(y)
+        _lib.call("hreg_bn_apply", y, R, C, mean, invstd, gamma, beta, 1, out, _stream())
+        ctx.save_for_backward(y, mean, invstd, gamma, beta)
+        ctx.side = _SIDE
+        ctx.params = (gamma, beta)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, mean, invstd, gamma, beta = ctx.saved_tensors
+        dout = dout.contiguous()
+        R, C = y.shape
+        dev = y.device
+        gg, gbt = _grad_slot(ctx.params[0], ctx.side), _grad_slot(ctx.params[1], ctx.side)
+        acc = gg is not None and gbt is not None and ctx.needs_input_grad[3] and ctx.needs_input_grad[4]
+        dgamma = gg if acc else torch.empty(C, device=dev)
+        dbeta = gbt if acc else torch.empty(C, device=dev)
+        dy = torch.empty_like(y)
+        _lib.call("hreg_bn_backward", dout, None, y, R, C, mean, invstd, gamma, beta, 1, col_reduce_ws(R, C, dev), dy,
+                  dgamma, dbeta, 1 if acc else 0, _stream())
+        if acc:
+            dgamma = dbeta = None
+        return dy, None, None, dgamma, dbeta
+
+
+def chain_fusable(R: int, widths) -> bool:
+    """conv_bn_chain takes a chain of R rows and channel widths [K0, N0, N1, ...]"""
+    if not (CHAIN_FUSED and TS_GEMM and TS_BN and R >= TS_MIN_ROWS and len(widths) >= 3):
+        return False
+    lib = _lib.load()
+    return (bool(lib.hreg_ts_gemm_supported(R, widths[0], widths[1], 1)) and
+            all(w % 4 == 0 for w in widths) and
+            all(lib.hreg_ts_gemm_pre_supported(R, widths[i], widths[i + 1]) for i in range(1, len(widths) - 1)))
+
+
+def conv_bn_chain(x, layers):
+    """Conv1x1 + train-mode BN + ReLU for each (W [N][K], bias, gamma, beta, running_mean,
+    running_var, momentum, eps, wparam) in order, over rows x [R][K0]; the inner activations are
+    never written (the caller checks chain_fusable).  Bitwise the conv_bn_act sequence."""
+    x = x.contiguous()
+    pre = (None, None, None, None)
+    y = x
+    for W, bias, gamma, beta, rm, rv, momentum, eps, wparam in layers:
+        y, mean, invstd = _ConvStats.apply(y, W, bias, *pre, rm, rv, momentum, eps,
+                                           wparam if wparam is not None else W)
+        pre = (mean, invstd, gamma, beta)
+    return _BNAct.apply(y, *pre)
+
+
 class ConvBNAct(torch.nn.Module):
     """Parameters of one 1x1 conv + BatchNorm (+ ReLU) layer, reference naming:
     ``conv.weight [N][K(,1,1)]``, ``conv.bias``, ``bn.weight/bias/running_*``."""

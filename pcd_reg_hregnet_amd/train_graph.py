@@ -604,18 +604,33 @@ def conv_bn(x, conv, bn, relu=True):
     return y
 
 
+def conv_bn_seq(x, pairs):
+    """[(conv, bn)] each Conv(1x1) + train-mode BN + ReLU in order: one fused chain
+    (train.conv_bn_chain: the inner activations never written, the same bits) when its kernels
+    take the shapes, else layer by layer."""
+    widths = [x.shape[1]] + [conv.out_channels for conv, _ in pairs]
+    if len(pairs) >= 2 and train.chain_fusable(x.shape[0], widths):
+        layers = [(conv.weight.view(conv.out_channels, -1), conv.bias, bn.weight, bn.bias, bn.running_mean,
+                   bn.running_var, bn.momentum, bn.eps, conv.weight) for conv, bn in pairs]
+        y = train.conv_bn_chain(x, layers)
+        for _, bn in pairs:
+            if bn.num_batches_tracked is not None:
+                _BN_COUNTERS.append(bn.num_batches_tracked)
+        return y
+    for conv, bn in pairs:
+        x = conv_bn(x, conv, bn, relu=True)
+    return x
+
+
 def seq_convs(x, seq):
     """nn.Sequential of [Conv, BN, ReLU] * n."""
     mods = list(seq)
-    for i in range(0, len(mods), 3):
-        x = conv_bn(x, mods[i], mods[i + 1], relu=True)
-    return x
+    return conv_bn_seq(x, [(mods[i], mods[i + 1]) for i in range(0, len(mods), 3)])
 
 
 def _mlp_head(x, head_mods, mode, nclouds, rows, want_weights=False):
     m1, m2, m3 = head_mods
-    s = conv_bn(x, m1[0], m1[1])
-    s = conv_bn(s, m2[0], m2[1])
+    s = conv_bn_seq(x, [(m1[0], m1[1]), (m2[0], m2[1])])
     return head_out(s, m3[0], mode, nclouds, rows, want_weights)
 
 

@@ -171,6 +171,59 @@ def test_tail_conv_bn_act_bitwise(tg, k, C1, Ca, N, G):
         assert torch.equal(a, b), nm
 
 
+@pytest.mark.parametrize("R,widths,bias", [(131072, (4, 32, 32, 64), False), (32768, (64, 64, 64, 128), True),
+                                           (16384, (132, 128, 128), True), (20000, (64, 256, 256), False)])
+def test_conv_bn_chain_bitwise(tg, R, widths, bias):
+    """r6: a Conv + train-mode BN + ReLU chain with its inner activations never written
+    (train.conv_bn_chain: each later conv applies the previous BN + ReLU on load in its forward
+    GEMM and weight-gradient GEMM, the previous BN's backward in its own) gives conv_bn_act's
+    bits, layer by layer: output, running statistics and every gradient (input and parameters,
+    returned to autograd and added in place into existing .grad buffers)."""
+    from pcd_reg_hregnet_amd import train
+    assert train.chain_fusable(R, list(widths))
+    L = len(widths) - 1
+    ins = [_rand(R, widths[0], seed=1)]
+    for i in range(L):
+        K, N = widths[i], widths[i + 1]
+        ins += [_rand(N, K, seed=10 + i, scale=1.0 / K ** 0.5), _rand(N, seed=20 + i, scale=0.1),
+                1 + _rand(N, seed=30 + i, scale=0.1), _rand(N, seed=40 + i, scale=0.1)]
+    rms = [[(torch.zeros(widths[i + 1], device=DEV), torch.ones(widths[i + 1], device=DEV)) for i in range(L)]
+           for _ in range(2)]
+
+    def chain(x, *ps):
+        layers = [(ps[4 * i], ps[4 * i + 1] if bias else None, ps[4 * i + 2], ps[4 * i + 3], *rms[0][i], 0.1, 1e-5,
+                   None) for i in range(L)]
+        return train.conv_bn_chain(x, layers)
+
+    def layerwise(x, *ps):
+        for i in range(L):
+            x = train.conv_bn_act(x, ps[4 * i], ps[4 * i + 1] if bias else None, ps[4 * i + 2], ps[4 * i + 3],
+                                  *rms[1][i])
+        return x
+
+    o1, g1 = _grads(chain, ins)
+    o2, g2 = _grads(layerwise, ins)
+    assert torch.equal(o1[0], o2[0])
+    for (a, b), (c, d) in zip(rms[0], rms[1]):
+        assert torch.equal(a, c) and torch.equal(b, d)
+    for i, (a, b) in enumerate(zip(g1, g2)):
+        if i % 4 == 2 and not bias:
+            continue  # (no bias: its input is unused)
+        assert torch.equal(a, b), i
+    # the trainers' direct accumulation into existing .grad buffers: the same sums
+    accs = []
+    for fn in (chain, layerwise):
+        ps = [p.detach().clone().requires_grad_(True) for p in ins]
+        for p in ps[1:]:
+            p.grad = _rand(*p.shape, seed=99)
+        with train.direct_gradients():
+            out = fn(*ps)
+            (out * _rand(*out.shape, seed=7)).sum().backward()
+        accs.append([p.grad for p in ps])
+    for i, (a, b) in enumerate(zip(*accs)):
+        assert torch.equal(a, b), i
+
+
 def test_group_max(tg):
     G, k, C = 30, 16, 40
     x = _rand(G * k, C, seed=11)
