@@ -491,9 +491,13 @@ __global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__
         for (int i = 0; i < LB; ++i) {
             v4f v = gb[i];
             if constexpr (PREB) {
-                const bool live = gbase + (tid + 256 * i) / FB < R;  // (rows past R stay 0)
 #pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = live ? bn_act(v[u], pm[u], pi[u], pg[u], pbe[u], pb.relu) : 0.f;
+                for (int u = 0; u < 4; ++u) v[u] = bn_act(v[u], pm[u], pi[u], pg[u], pbe[u], pb.relu);
+                if (gbase + TN_ROWS > R) {  // (the last step: rows past R stay 0)
+                    const bool live = gbase + (tid + 256 * i) / FB < R;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = live ? v[u] : 0.f;
+                }
             }
             *reinterpret_cast<v4f *>(Bs + 4 * (tid + 256 * i)) = v;
         }
