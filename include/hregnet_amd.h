@@ -419,8 +419,8 @@ int hreg_ts_gemm_bn_tail(const float *x2, int k, const float *x1, int C1, const 
                          float momentum, void *ws, float *mean, float *invstd, float *var_unbiased,
                          float *running_mean, float *running_var, void *stream);
 /* hreg_ts_gemm_bn (w_trans 0) with A = the previous layer's pre-BatchNorm output [R][K]: every A
- * value enters as act(pre_gamma * (A - pre_mean) * pre_invstd + pre_beta) (act = ReLU if
- * pre_relu; hreg_bn_apply's arithmetic, per column k), so out and the statistics are those of
+ * value enters as ReLU(pre_gamma * (A - pre_mean) * pre_invstd + pre_beta) (pre_relu must be 1,
+ * else HREG_ERR_UNSUPPORTED; hreg_bn_apply's arithmetic, per column k), so out and the statistics are those of
  * hreg_bn_apply followed by hreg_ts_gemm_bn, without the activation materialised (the
  * train-mode Conv+BN+ReLU chains of layers.py:115-130, 183-198; r6).  hreg_ts_gemm_pre_supported
  * != 0 when the kernel takes the shape (K <= 512, up to 4 output tiles of 32 per workgroup).
@@ -459,7 +459,8 @@ int hreg_gemm_tn(const float *A, int lda, const float *B, int ldb, int R, int N,
 int hreg_gemm_tn_tail(const float *A, int lda, const float *x2, int k, const float *x1, int C1,
                       const float *att, int Ca, int R, int N, float beta, void *ws, float *out, void *stream);
 /* hreg_gemm_tn with B = the previous layer's pre-BatchNorm output [R][K]: B enters as
- * act(pre_gamma * (B - pre_mean) * pre_invstd + pre_beta) per column (hreg_bn_apply's arithmetic);
+ * ReLU(pre_gamma * (B - pre_mean) * pre_invstd + pre_beta) per column (pre_relu must be 1;
+ * hreg_bn_apply's arithmetic);
  * the same splits and sums as hreg_gemm_tn over the materialised activation (the weight gradient
  * of a Conv whose input is the previous Conv+BN+ReLU's output; r6).  lda, ldb multiples of 4,
  * 16-byte aligned A and B (else HREG_ERR_UNSUPPORTED).  ws = hreg_gemm_tn_ws_bytes(R, N, K). */

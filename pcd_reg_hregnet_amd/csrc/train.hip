@@ -403,11 +403,10 @@ struct TnSeg {
     int ld[3], div[3], kend[3], rows[3];
 };
 // (PREB, r6) B is the previous layer's pre-BatchNorm output: each staged B value is
-// bn_act(B, mean[k], invstd[k], gamma[k], beta[k], relu) (hreg_bn_apply's arithmetic; rows past
+// bn_act(B, mean[k], invstd[k], gamma[k], beta[k], ReLU) (hreg_bn_apply's arithmetic; rows past
 // R stay 0), so the sums are those over the materialised activation
 struct TnPre {
     const float *mean, *invstd, *gamma, *beta;
-    int relu;
 };
 
 template <int TNN, int TNK, bool SEG = false, bool PREB = false>
@@ -492,7 +491,7 @@ __global__ __launch_bounds__(256) void gemm_tn4_kernel(const float *__restrict__
             v4f v = gb[i];
             if constexpr (PREB) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = bn_act(v[u], pm[u], pi[u], pg[u], pbe[u], pb.relu);
+                for (int u = 0; u < 4; ++u) v[u] = bn_act(v[u], pm[u], pi[u], pg[u], pbe[u], 1);
                 if (gbase + TN_ROWS > R) {  // (the last step: rows past R stay 0)
                     const bool live = gbase + (tid + 256 * i) / FB < R;
 #pragma unroll
@@ -860,6 +859,7 @@ extern "C" int hreg_gemm_tn_pre(const float *A, int lda, const float *B, int ldb
     if (!A || !B || !ws || !out || R <= 0 || N <= 0 || K <= 0 || lda < N || ldb < K || !pre_mean || !pre_invstd ||
         !pre_gamma || !pre_beta)
         return HREG_ERR_INVALID;
+    if (!pre_relu) return HREG_ERR_UNSUPPORTED;  // (the chains' activations are all ReLU)
     if ((lda & 3) || (ldb & 3) || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) ||
         (size_t)R * lda * sizeof(float) >= ((size_t)1 << 31) || (size_t)R * ldb * sizeof(float) >= ((size_t)1 << 31))
         return HREG_ERR_UNSUPPORTED;
@@ -869,7 +869,7 @@ extern "C" int hreg_gemm_tn_pre(const float *A, int lda, const float *B, int ldb
     hipStream_t st = as_stream(stream);
     const int tnn = N <= 32 ? 1 : 2, tnk = K <= 32 ? 1 : 2;
     const dim3 grid((N + 32 * tnn - 1) / (32 * tnn), (K + 32 * tnk - 1) / (32 * tnk), S);
-    const TnPre pre{pre_mean, pre_invstd, pre_gamma, pre_beta, pre_relu ? 1 : 0};
+    const TnPre pre{pre_mean, pre_invstd, pre_gamma, pre_beta};
 #define TNP_CASE(a, b)                                                                                          \
     hipLaunchKernelGGL((gemm_tn4_kernel<a, b, false, true>), grid, dim3(256), 0, st, A, lda, B, ldb, R, N, K, rps, \
                        (float *)ws, TnSeg{}, pre)

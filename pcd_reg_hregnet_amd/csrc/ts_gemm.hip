@@ -40,11 +40,10 @@ struct TsSeg {
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
 // (PRE, r6) A is the previous layer's pre-BatchNorm output: every A value is replaced on load by
-// bn_act(A, mean[k], invstd[k], gamma[k], beta[k], relu) -- hreg_bn_apply's arithmetic, so the
+// bn_act(A, mean[k], invstd[k], gamma[k], beta[k], ReLU) -- hreg_bn_apply's arithmetic, so the
 // products are those of the materialised activation (train.py _ConvStats)
 struct TsPre {
     const float *mean, *invstd, *gamma, *beta;
-    int relu;
 };
 
 // STATS: the train-mode BatchNorm statistics of the output ride along in the epilogue (the
@@ -176,7 +175,7 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
                     const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
                     const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) bv[e] = bn_act(bv[e], mv[e], iv[e], gv[e], bb[e], pre.relu);
+                    for (int e = 0; e < 8; ++e) bv[e] = bn_act(bv[e], mv[e], iv[e], gv[e], bb[e], 1);
                 }
                 if (TAIL && sub == nsub - 1) {
 #pragma unroll
@@ -395,8 +394,9 @@ extern "C" int hreg_ts_gemm_bn_pre(const float *A, int lda, int R, int K, const 
     if (!ws || !mean || !invstd || R <= 0 || ((running_mean == nullptr) != (running_var == nullptr)) ||
         (running_mean && !var_unbiased) || !pre_mean || !pre_invstd || !pre_gamma || !pre_beta)
         return HREG_ERR_INVALID;
+    if (!pre_relu) return HREG_ERR_UNSUPPORTED;  // (the chains' activations are all ReLU)
     hipStream_t st = as_stream(stream);
-    TsPre pre{pre_mean, pre_invstd, pre_gamma, pre_beta, pre_relu ? 1 : 0};
+    TsPre pre{pre_mean, pre_invstd, pre_gamma, pre_beta};
     const int S = ts_launch<true, false, true>(A, lda, R, K, W, 0, N, nullptr, shift, 0, out, ldo,
                                                static_cast<double *>(ws), st, {}, pre);
     if (S < 0) return -S;
