@@ -307,6 +307,71 @@ def tail_fusable(R: int, k: int, C1: int, Ca: int, N: int) -> bool:
             and bool(_lib.load().hreg_ts_gemm_supported(R, K, N, 1)))
 
 
+def _tail_forward(x1, att, W, bias, running_mean, running_var, k, momentum, eps):
+    """The tail conv's pre-BN output and statistics -> (y, mean, invstd, x2, arg)"""
+    R, C1 = x1.shape
+    Ca = att.shape[1]
+    G = R // k
+    N = W.shape[0]
+    dev = x1.device
+    st = _stream()
+    x2 = torch.empty(G, C1, device=dev)
+    arg = torch.empty(G, C1, dtype=torch.int32, device=dev)
+    _lib.call("hreg_group_max_arg", x1, C1, G, k, C1, x2, C1, arg, st)
+    defer = DEFERRED_RUNNING is not None and running_mean is not None
+    rm, rv = (None, None) if defer else (running_mean, running_var)
+    y = torch.empty(R, N, device=dev)
+    mean, invstd, var = (torch.empty(N, device=dev) for _ in range(3))
+    ws = _ws(_lib.load().hreg_ts_gemm_bn_ws_bytes(R, 2 * C1 + Ca, N), dev)
+    _lib.call("hreg_ts_gemm_bn_tail", x2, k, x1, C1, att, Ca, R, W.contiguous(), N,
+              None if bias is None else bias.contiguous(), y, N, float(eps), float(momentum), ws, mean, invstd,
+              var, rm, rv, st)
+    if defer:
+        DEFERRED_RUNNING.append((mean, var, running_mean, running_var, momentum))
+    return y, mean, invstd, x2, arg
+
+
+def _tail_backward(ctx, dy, x1, att, x2, arg, W, need_x1, need_att, need_W, need_b):
+    """The tail conv's backward from dL/dy (pre-BN) -> (dx1, datt, dW, dbias); W / bias
+    gradients added into their .grad buffers in place when the trainers attach them"""
+    R, N = dy.shape
+    C1, Ca = x1.shape[1], att.shape[1]
+    k = ctx.k
+    G = R // k
+    K = 2 * C1 + Ca
+    dev = dy.device
+    st = _stream()
+    wp, bp = ctx.params[:2]
+    gw = _grad_slot(wp, ctx.side) if need_W else None
+    gb = _grad_slot(bp, ctx.side) if ctx.has_bias and need_b else None
+    dW = None
+    if need_W:
+        out = gw.view(W.shape) if gw is not None else torch.empty(N, K, device=dev)
+        ws = _ws(_lib.load().hreg_gemm_tn_ws_bytes(R, N, K), dev)
+        _lib.call("hreg_gemm_tn_tail", dy, N, x2, k, x1, C1, att, Ca, R, N, 1.0 if gw is not None else 0.0,
+                  ws, out, st)
+        if gw is None:
+            dW = out
+    dbias = None
+    if ctx.has_bias and need_b:
+        if gb is not None:
+            col_sum(dy, into=gb)
+        else:
+            dbias = col_sum(dy)
+    dx1 = datt = None
+    if need_x1 or need_att:
+        dcat = _conv_gemm(dy, W, None, w_trans=True)  # [R][K] (desc_tail's backward from here)
+        if need_x1:
+            dx2 = torch.empty(G, C1, device=dev)
+            _lib.call("hreg_group_sum", dcat, K, G, k, C1, dx2, C1, 0, st)
+            dx1 = torch.empty(R, C1, device=dev)
+            _lib.call("hreg_copy_rows", dcat[:, C1:], K, 1, R, C1, dx1, C1, 0, st)
+            _lib.call("hreg_group_max_bwd", dx2, C1, arg, G, k, C1, dx1, C1, 1, st)
+        if need_att:
+            datt = dcat[:, 2 * C1:]
+    return dx1, datt, dW, dbias
+
+
 class _TailConvBNAct(torch.autograd.Function):
     """The descriptor's mlp1 (Conv1x1 + train-mode BN + ReLU) over cat([x2 repeated over each
     group's k rows, x1, att_map]) (layers.py:202-209) without materialising the concatenation
@@ -319,27 +384,10 @@ class _TailConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x1, att, W, bias, gamma, beta, running_mean, running_var, k, momentum, eps, wparam=None):
-        R, C1 = x1.shape
-        Ca = att.shape[1]
-        G = R // k
-        N = W.shape[0]
-        dev = x1.device
-        st = _stream()
-        x2 = torch.empty(G, C1, device=dev)
-        arg = torch.empty(G, C1, dtype=torch.int32, device=dev)
-        _lib.call("hreg_group_max_arg", x1, C1, G, k, C1, x2, C1, arg, st)
-        defer = DEFERRED_RUNNING is not None and running_mean is not None
-        rm, rv = (None, None) if defer else (running_mean, running_var)
-        y = torch.empty(R, N, device=dev)
-        mean, invstd, var = (torch.empty(N, device=dev) for _ in range(3))
-        ws = _ws(_lib.load().hreg_ts_gemm_bn_ws_bytes(R, 2 * C1 + Ca, N), dev)
-        _lib.call("hreg_ts_gemm_bn_tail", x2, k, x1, C1, att, Ca, R, W.contiguous(), N,
-                  None if bias is None else bias.contiguous(), y, N, float(eps), float(momentum), ws, mean, invstd,
-                  var, rm, rv, st)
-        if defer:
-            DEFERRED_RUNNING.append((mean, var, running_mean, running_var, momentum))
+        y, mean, invstd, x2, arg = _tail_forward(x1, att, W, bias, running_mean, running_var, k, momentum, eps)
+        R, N = y.shape
         out = torch.empty_like(y)
-        _lib.call("hreg_bn_apply", y, R, N, mean, invstd, gamma, beta, 1, out, st)
+        _lib.call("hreg_bn_apply", y, R, N, mean, invstd, gamma, beta, 1, out, _stream())
         ctx.save_for_backward(x1, att, x2, arg, W, y, mean, invstd, gamma, beta)
         ctx.side = _SIDE
         ctx.k = k
@@ -352,50 +400,41 @@ class _TailConvBNAct(torch.autograd.Function):
         x1, att, x2, arg, W, y, mean, invstd, gamma, beta = ctx.saved_tensors
         dout = dout.contiguous()
         R, N = y.shape
-        C1, Ca = x1.shape[1], att.shape[1]
-        k = ctx.k
-        G = R // k
-        K = 2 * C1 + Ca
         dev = y.device
-        st = _stream()
-        wp, bp, gp, btp = ctx.params
-        gw = _grad_slot(wp, ctx.side) if ctx.needs_input_grad[2] else None
-        gb = _grad_slot(bp, ctx.side) if ctx.has_bias and ctx.needs_input_grad[3] else None
+        gp, btp = ctx.params[2:]
         gg, gbt = _grad_slot(gp, ctx.side), _grad_slot(btp, ctx.side)
         acc = gg is not None and gbt is not None and ctx.needs_input_grad[4] and ctx.needs_input_grad[5]
         dgamma = gg if acc else torch.empty(N, device=dev)
         dbeta = gbt if acc else torch.empty(N, device=dev)
         dy = torch.empty_like(y)
         _lib.call("hreg_bn_backward", dout, None, y, R, N, mean, invstd, gamma, beta, 1,
-                  col_reduce_ws(R, N, dev), dy, dgamma, dbeta, 1 if acc else 0, st)
-        dW = None
-        if ctx.needs_input_grad[2]:
-            out = gw.view(W.shape) if gw is not None else torch.empty(N, K, device=dev)
-            ws = _ws(_lib.load().hreg_gemm_tn_ws_bytes(R, N, K), dev)
-            _lib.call("hreg_gemm_tn_tail", dy, N, x2, k, x1, C1, att, Ca, R, N, 1.0 if gw is not None else 0.0,
-                      ws, out, st)
-            if gw is None:
-                dW = out
-        dbias = None
-        if ctx.has_bias and ctx.needs_input_grad[3]:
-            if gb is not None:
-                col_sum(dy, into=gb)
-            else:
-                dbias = col_sum(dy)
-        dx1 = datt = None
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            dcat = _conv_gemm(dy, W, None, w_trans=True)  # [R][K] (desc_tail's backward from here)
-            if ctx.needs_input_grad[0]:
-                dx2 = torch.empty(G, C1, device=dev)
-                _lib.call("hreg_group_sum", dcat, K, G, k, C1, dx2, C1, 0, st)
-                dx1 = torch.empty(R, C1, device=dev)
-                _lib.call("hreg_copy_rows", dcat[:, C1:], K, 1, R, C1, dx1, C1, 0, st)
-                _lib.call("hreg_group_max_bwd", dx2, C1, arg, G, k, C1, dx1, C1, 1, st)
-            if ctx.needs_input_grad[1]:
-                datt = dcat[:, 2 * C1:]
+                  col_reduce_ws(R, N, dev), dy, dgamma, dbeta, 1 if acc else 0, _stream())
+        dx1, datt, dW, dbias = _tail_backward(ctx, dy, x1, att, x2, arg, W, *ctx.needs_input_grad[:4])
         if acc:
             dgamma = dbeta = None
         return dx1, datt, dW, dbias, dgamma, dbeta, None, None, None, None, None, None
+
+
+class _TailConvStats(torch.autograd.Function):
+    """_TailConvBNAct without its BN apply: -> (y pre-BN, mean, invstd) for a chain's next conv to
+    apply on load (tail_conv_bn_chain)."""
+
+    @staticmethod
+    def forward(ctx, x1, att, W, bias, running_mean, running_var, k, momentum, eps, wparam):
+        y, mean, invstd, x2, arg = _tail_forward(x1, att, W, bias, running_mean, running_var, k, momentum, eps)
+        ctx.save_for_backward(x1, att, x2, arg, W)
+        ctx.side = _SIDE
+        ctx.k = k
+        ctx.has_bias = bias is not None
+        ctx.params = (wparam, bias)
+        ctx.mark_non_differentiable(mean, invstd)
+        return y, mean, invstd
+
+    @staticmethod
+    def backward(ctx, dy, _dmean, _dinvstd):
+        x1, att, x2, arg, W = ctx.saved_tensors
+        dx1, datt, dW, dbias = _tail_backward(ctx, dy.contiguous(), x1, att, x2, arg, W, *ctx.needs_input_grad[:4])
+        return dx1, datt, dW, dbias, None, None, None, None, None, None
 
 
 def tail_conv_bn_act(x1, att, k, W, bias, gamma, beta, running_mean=None, running_var=None,
@@ -404,6 +443,28 @@ def tail_conv_bn_act(x1, att, k, W, bias, gamma, beta, running_mean=None, runnin
     the concatenation (_TailConvBNAct; the caller checks tail_fusable); W [N][2 C1 + Ca]."""
     return _TailConvBNAct.apply(x1.contiguous(), att.contiguous(), W, bias, gamma, beta, running_mean,
                                 running_var, k, momentum, eps, wparam if wparam is not None else W)
+
+
+def tail_chain_fusable(R: int, k: int, C1: int, Ca: int, widths) -> bool:
+    """tail_conv_bn_chain takes the tail conv (widths[0] = its N) and the convs after it"""
+    return (CHAIN_FUSED and len(widths) >= 2 and tail_fusable(R, k, C1, Ca, widths[0]) and
+            all(w % 4 == 0 for w in widths) and
+            all(_lib.load().hreg_ts_gemm_pre_supported(R, widths[i], widths[i + 1]) for i in range(len(widths) - 1)))
+
+
+def tail_conv_bn_chain(x1, att, k, tail, layers):
+    """tail_conv_bn_act followed by conv_bn_act for each of `layers` (conv_bn_chain's tuples),
+    the inner activations never written; tail = (W, bias, gamma, beta, running_mean, running_var,
+    momentum, eps, wparam).  Bitwise the layerwise path (the caller checks tail_chain_fusable)."""
+    W, bias, gamma, beta, rm, rv, momentum, eps, wparam = tail
+    y, mean, invstd = _TailConvStats.apply(x1.contiguous(), att.contiguous(), W, bias, rm, rv, k, momentum, eps,
+                                           wparam if wparam is not None else W)
+    pre = (mean, invstd, gamma, beta)
+    for W, bias, gamma, beta, rm, rv, momentum, eps, wparam in layers:
+        y, mean, invstd = _ConvStats.apply(y, W, bias, *pre, rm, rv, momentum, eps,
+                                           wparam if wparam is not None else W)
+        pre = (mean, invstd, gamma, beta)
+    return _BNAct.apply(y, *pre)
 
 
 # Chains of Conv + train-mode BN + ReLU layers (nn.Sequential, layers.py:115-130, 183-198) with the

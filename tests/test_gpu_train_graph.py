@@ -171,6 +171,37 @@ def test_tail_conv_bn_act_bitwise(tg, k, C1, Ca, N, G):
         assert torch.equal(a, b), nm
 
 
+@pytest.mark.parametrize("k,C1,Ca,N,N2,G", [(64, 64, 64, 64, 64, 512), (32, 128, 128, 128, 128, 1024)])
+def test_tail_conv_bn_chain_bitwise(tg, k, C1, Ca, N, N2, G):
+    """r6: the descriptor's mlp1 (no concatenation) and mlp2 with mlp1's activation never written
+    (train.tail_conv_bn_chain) give tail_conv_bn_act + conv_bn_act's bits: output, both layers'
+    running statistics and every gradient, at levels 1 and 2's widths."""
+    from pcd_reg_hregnet_amd import train
+    R = G * k
+    assert train.tail_chain_fusable(R, k, C1, Ca, [N, N2])
+    ins = [_rand(R, C1, seed=1), _rand(R, Ca, seed=2), _rand(N, 2 * C1 + Ca, seed=3, scale=0.05),
+           _rand(N, seed=4, scale=0.1), 1 + _rand(N, seed=5, scale=0.1), _rand(N, seed=6, scale=0.1),
+           _rand(N2, N, seed=7, scale=0.1), _rand(N2, seed=8, scale=0.1), 1 + _rand(N2, seed=9, scale=0.1),
+           _rand(N2, seed=10, scale=0.1)]
+    rms = [[(torch.zeros(n, device=DEV), torch.ones(n, device=DEV)) for n in (N, N2)] for _ in range(2)]
+
+    def chain(x1, att, W, b, ga, be, W2, b2, ga2, be2):
+        return train.tail_conv_bn_chain(x1, att, k, (W, b, ga, be, *rms[0][0], 0.1, 1e-5, None),
+                                        [(W2, b2, ga2, be2, *rms[0][1], 0.1, 1e-5, None)])
+
+    def layerwise(x1, att, W, b, ga, be, W2, b2, ga2, be2):
+        y = train.tail_conv_bn_act(x1, att, k, W, b, ga, be, *rms[1][0])
+        return train.conv_bn_act(y, W2, b2, ga2, be2, *rms[1][1])
+
+    o1, g1 = _grads(chain, ins)
+    o2, g2 = _grads(layerwise, ins)
+    assert torch.equal(o1[0], o2[0])
+    for (a, b), (c, d) in zip(rms[0], rms[1]):
+        assert torch.equal(a, c) and torch.equal(b, d)
+    for i, (a, b) in enumerate(zip(g1, g2)):
+        assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize("R,widths,bias", [(131072, (4, 32, 32, 64), False), (32768, (64, 64, 64, 128), True),
                                            (16384, (132, 128, 128), True), (20000, (64, 256, 256), False)])
 def test_conv_bn_chain_bitwise(tg, R, widths, bias):
@@ -675,17 +706,23 @@ def test_train_descriptor_backward_replay():
             rec["att_map"] = att_map.detach().clone()
             return o_tail(x1, att_map, k)
 
-        o_fused = train.tail_conv_bn_act
+        o_fused, o_chain = train.tail_conv_bn_act, train.tail_conv_bn_chain
 
         def fused(x1, att_map, k, *a, **kw):  # the same, without materialising it (r6)
             rec["att_map"] = att_map.detach().clone()
             return o_fused(x1, att_map, k, *a, **kw)
 
-        train_graph.seq_convs, train_graph.desc_tail, train.tail_conv_bn_act = seq, tail, fused
+        def chain(x1, att_map, k, *a, **kw):  # (and with mlp2 applying mlp1's BN on load)
+            rec["att_map"] = att_map.detach().clone()
+            return o_chain(x1, att_map, k, *a, **kw)
+
+        train_graph.seq_convs, train_graph.desc_tail = seq, tail
+        train.tail_conv_bn_act, train.tail_conv_bn_chain = fused, chain
         try:
             out = orig_kl(det, desc, lvl, xyz, feats, weights, hook, part, use_fps)
         finally:
-            train_graph.seq_convs, train_graph.desc_tail, train.tail_conv_bn_act = o_seq, o_tail, o_fused
+            train_graph.seq_convs, train_graph.desc_tail = o_seq, o_tail
+            train.tail_conv_bn_act, train.tail_conv_bn_chain = o_fused, o_chain
         out[3].retain_grad()
         rec["d"] = out[3]
         caps.append(rec)
