@@ -178,9 +178,11 @@ def _plain_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None) ->
 
 
 # conv GEMMs of >= TS_MIN_ROWS rows on hreg_ts_gemm (the tall-skinny kernel: W in LDS, A
-# streamed from HBM; the same fp32 sums as hreg_gemm); the input gradient reads W in place
+# streamed from HBM; the same fp32 sums as hreg_gemm); the input gradient reads W in place.
+# (r6: 4096 -- the level-1 / level-2 detector heads' 8192 / 4096 rows join it, and with it the
+# fused statistics and the chains: eager step 22.10 -> 21.27 ms, 1024 21.65; r5: 16384)
 TS_GEMM = True
-TS_MIN_ROWS = 16384
+TS_MIN_ROWS = 4096
 
 
 def _conv_gemm(x: torch.Tensor, W: torch.Tensor, shift: torch.Tensor | None,
