@@ -529,6 +529,12 @@ int hreg_attention_bwd(const float *logits, int ldl, int C, const float *vals, i
 /* out[g][c] = max_j x[g*k+j][c], arg = first maximising j  (layers.py:202, 208) */
 int hreg_group_max_arg(const float *x, int ldx, int G, int k, int C, float *out, int ldo,
                        int32_t *arg, void *stream);
+/* hreg_group_max_arg over ReLU(gamma * (x - mean) * invstd + beta) (per column c; x the
+ * pre-BatchNorm output, hreg_bn_apply's values): the maxima and arguments over the activation
+ * without materialising it (r6, the descriptor's last k-max, train.py _BNActGroupMax) */
+int hreg_group_max_arg_pre(const float *x, int ldx, int G, int k, int C, float *out, int ldo, int32_t *arg,
+                           const float *mean, const float *invstd, const float *gamma, const float *beta,
+                           void *stream);
 int hreg_group_max_bwd(const float *dout, int ldd, const int32_t *arg, int G, int k, int C,
                        float *dx, int ldx, int accumulate, void *stream);
 /* backward of hreg_head_out's activation: dz [G] = dy * act'(x.w3 + b3), dx = dz w3^T */

@@ -461,15 +461,30 @@ __global__ __launch_bounds__(TB) void attention_bwd_kernel(
 }
 
 // --------------------------------------------------------------- group max
+// PRE (r6): x is a pre-BatchNorm output and every value enters as bn_act(x, mean[c], invstd[c],
+// gamma[c], beta[c], ReLU) -- hreg_bn_apply's values, so the same maxima and arguments as over the
+// materialised activation
+template <bool PRE = false>
 __global__ void group_max_arg_kernel(const float *__restrict__ x, int ldx, int G, int k, int C,
-                                     float *__restrict__ out, int ldo, int32_t *__restrict__ arg) {
+                                     float *__restrict__ out, int ldo, int32_t *__restrict__ arg,
+                                     const float *__restrict__ mean = nullptr, const float *__restrict__ invstd = nullptr,
+                                     const float *__restrict__ gamma = nullptr,
+                                     const float *__restrict__ beta = nullptr) {
     GRID_STRIDE(i, (size_t)G * C) {
         const int g = (int)(i / C), c = (int)(i % C);
         const float *p = x + (size_t)g * k * ldx + c;
-        float b = p[0];
+        float mu = 0.f, is = 0.f, ga = 0.f, be = 0.f;
+        if constexpr (PRE) {
+            mu = mean[c];
+            is = invstd[c];
+            ga = gamma[c];
+            be = beta[c];
+        }
+        auto val = [&](float v) { return PRE ? bn_act(v, mu, is, ga, be, 1) : v; };
+        float b = val(p[0]);
         int bi = 0;
         for (int j = 1; j < k; ++j) {
-            const float v = p[(size_t)j * ldx];
+            const float v = val(p[(size_t)j * ldx]);
             if (v > b) { b = v; bi = j; }
         }
         out[(size_t)g * ldo + c] = b;
@@ -1265,8 +1280,21 @@ extern "C" int hreg_group_max_arg(const float *x, int ldx, int G, int k, int C, 
                                   int ldo, int32_t *arg, void *stream) {
     if (!x || !out || !arg || G < 0 || k < 1 || C < 0 || ldx < C || ldo < C) return HREG_ERR_INVALID;
     if (!G || !C) return HREG_OK;
-    hipLaunchKernelGGL(group_max_arg_kernel, dim3(g1d((size_t)G * C)), dim3(TB), 0,
-                       as_stream(stream), x, ldx, G, k, C, out, ldo, arg);
+    hipLaunchKernelGGL(group_max_arg_kernel<false>, dim3(g1d((size_t)G * C)), dim3(TB), 0,
+                       as_stream(stream), x, ldx, G, k, C, out, ldo, arg, nullptr, nullptr, nullptr, nullptr);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_group_max_arg_pre(const float *x, int ldx, int G, int k, int C, float *out, int ldo,
+                                      int32_t *arg, const float *mean, const float *invstd, const float *gamma,
+                                      const float *beta, void *stream) {
+    if (!x || !out || !arg || !mean || !invstd || !gamma || !beta || G < 0 || k < 1 || C < 0 || ldx < C ||
+        ldo < C)
+        return HREG_ERR_INVALID;
+    if (!G || !C) return HREG_OK;
+    hipLaunchKernelGGL(group_max_arg_kernel<true>, dim3(g1d((size_t)G * C)), dim3(TB), 0,
+                       as_stream(stream), x, ldx, G, k, C, out, ldo, arg, mean, invstd, gamma, beta);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

@@ -454,10 +454,12 @@ def tail_chain_fusable(R: int, k: int, C1: int, Ca: int, widths) -> bool:
             all(_lib.load().hreg_ts_gemm_pre_supported(R, widths[i], widths[i + 1]) for i in range(len(widths) - 1)))
 
 
-def tail_conv_bn_chain(x1, att, k, tail, layers):
+def tail_conv_bn_chain(x1, att, k, tail, layers, group_max=False):
     """tail_conv_bn_act followed by conv_bn_act for each of `layers` (conv_bn_chain's tuples),
     the inner activations never written; tail = (W, bias, gamma, beta, running_mean, running_var,
-    momentum, eps, wparam).  Bitwise the layerwise path (the caller checks tail_chain_fusable)."""
+    momentum, eps, wparam); group_max: the max over each group's k rows of the last activation
+    instead of the activation (not written either).  Bitwise the layerwise path (the caller checks
+    tail_chain_fusable)."""
     W, bias, gamma, beta, rm, rv, momentum, eps, wparam = tail
     y, mean, invstd = _TailConvStats.apply(x1.contiguous(), att.contiguous(), W, bias, rm, rv, k, momentum, eps,
                                            wparam if wparam is not None else W)
@@ -591,6 +593,44 @@ class _BNAct(torch.autograd.Function):
         return dy, None, None, dgamma, dbeta
 
 
+class _BNActGroupMax(torch.autograd.Function):
+    """d = max over each group's k rows of ReLU(BN(y)) with the statistics _ConvStats made: the
+    chain's last activation never written either (the descriptor's k-max, layers.py:208-209)"""
+
+    @staticmethod
+    def forward(ctx, y, mean, invstd, gamma, beta, k):
+        R, C = y.shape
+        G = R // k
+        d = torch.empty(G, C, device=y.device)
+        arg = torch.empty(G, C, dtype=torch.int32, device=y.device)
+        _lib.call("hreg_group_max_arg_pre", y, C, G, k, C, d, C, arg, mean, invstd, gamma, beta, _stream())
+        ctx.save_for_backward(y, mean, invstd, gamma, beta, arg)
+        ctx.side = _SIDE
+        ctx.k = k
+        ctx.params = (gamma, beta)
+        return d
+
+    @staticmethod
+    def backward(ctx, dd):
+        y, mean, invstd, gamma, beta, arg = ctx.saved_tensors
+        dd = dd.contiguous()
+        R, C = y.shape
+        dev = y.device
+        st = _stream()
+        dout = torch.empty_like(y)  # (group_max's backward: dd at each group's argument rows)
+        _lib.call("hreg_group_max_bwd", dd, C, arg, R // ctx.k, ctx.k, C, dout, C, 0, st)
+        gg, gbt = _grad_slot(ctx.params[0], ctx.side), _grad_slot(ctx.params[1], ctx.side)
+        acc = gg is not None and gbt is not None and ctx.needs_input_grad[3] and ctx.needs_input_grad[4]
+        dgamma = gg if acc else torch.empty(C, device=dev)
+        dbeta = gbt if acc else torch.empty(C, device=dev)
+        dy = torch.empty_like(y)
+        _lib.call("hreg_bn_backward", dout, None, y, R, C, mean, invstd, gamma, beta, 1, col_reduce_ws(R, C, dev), dy,
+                  dgamma, dbeta, 1 if acc else 0, st)
+        if acc:
+            dgamma = dbeta = None
+        return dy, None, None, dgamma, dbeta, None
+
+
 def chain_fusable(R: int, widths) -> bool:
     """conv_bn_chain takes a chain of R rows and channel widths [K0, N0, N1, ...]"""
     if not (CHAIN_FUSED and TS_GEMM and TS_BN and R >= TS_MIN_ROWS and len(widths) >= 3):
@@ -612,7 +652,7 @@ def conv_bn_chain(x, layers):
         y, mean, invstd = _ConvStats.apply(y, W, bias, *pre, rm, rv, momentum, eps,
                                            wparam if wparam is not None else W)
         pre = (mean, invstd, gamma, beta)
-    return _BNAct.apply(y, *pre)
+    return _BNActGroupMax.apply(y, *pre, k) if group_max else _BNAct.apply(y, *pre)
 
 
 class ConvBNAct(torch.nn.Module):

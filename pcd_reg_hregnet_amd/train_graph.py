@@ -688,19 +688,18 @@ def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src", u
     conv2, bn2 = desc.mlp2[0], desc.mlp2[1]
     if TAIL_FUSED and train.tail_chain_fusable(x1.shape[0], k, x1.shape[1], att_map.shape[1],
                                                [conv.out_channels, conv2.out_channels]):
-        # mlp1 without its input concatenation and mlp2 applying mlp1's BN + ReLU on load (the
-        # same bits as the layerwise path)
+        # mlp1 without its input concatenation, mlp2 applying mlp1's BN + ReLU on load and the k-max
+        # mlp2's (the same bits as the layerwise path)
         y = train.tail_conv_bn_chain(
             x1, att_map, k,
             (conv.weight.view(conv.out_channels, -1), conv.bias, bn.weight, bn.bias, bn.running_mean,
              bn.running_var, bn.momentum, bn.eps, conv.weight),
             [(conv2.weight.view(conv2.out_channels, -1), conv2.bias, bn2.weight, bn2.bias, bn2.running_mean,
-              bn2.running_var, bn2.momentum, bn2.eps, conv2.weight)])
+              bn2.running_var, bn2.momentum, bn2.eps, conv2.weight)], group_max=True)
         for b_ in (bn, bn2):
             if b_.num_batches_tracked is not None:
                 _BN_COUNTERS.append(b_.num_batches_tracked)
-        d = group_max(y, k)
-        return kp.view(nb, M, 3), sig, att_feat, d, wnext, fps_loc
+        return kp.view(nb, M, 3), sig, att_feat, y, wnext, fps_loc
     if TAIL_FUSED and train.tail_fusable(x1.shape[0], k, x1.shape[1], att_map.shape[1], conv.out_channels):
         # mlp1 over cat([max_k x1 repeated, x1, att_map]) without materialising it (the same bits)
         y = train.tail_conv_bn_act(x1, att_map, k, conv.weight.view(conv.out_channels, -1), conv.bias,

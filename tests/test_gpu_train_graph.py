@@ -171,11 +171,13 @@ def test_tail_conv_bn_act_bitwise(tg, k, C1, Ca, N, G):
         assert torch.equal(a, b), nm
 
 
+@pytest.mark.parametrize("gm", [False, True])
 @pytest.mark.parametrize("k,C1,Ca,N,N2,G", [(64, 64, 64, 64, 64, 512), (32, 128, 128, 128, 128, 1024)])
-def test_tail_conv_bn_chain_bitwise(tg, k, C1, Ca, N, N2, G):
+def test_tail_conv_bn_chain_bitwise(tg, k, C1, Ca, N, N2, G, gm):
     """r6: the descriptor's mlp1 (no concatenation) and mlp2 with mlp1's activation never written
-    (train.tail_conv_bn_chain) give tail_conv_bn_act + conv_bn_act's bits: output, both layers'
-    running statistics and every gradient, at levels 1 and 2's widths."""
+    (train.tail_conv_bn_chain; gm: and the k-max of mlp2's activation, not written either) give
+    tail_conv_bn_act + conv_bn_act (+ group_max)'s bits: output, both layers' running statistics
+    and every gradient, at levels 1 and 2's widths."""
     from pcd_reg_hregnet_amd import train
     R = G * k
     assert train.tail_chain_fusable(R, k, C1, Ca, [N, N2])
@@ -187,11 +189,12 @@ def test_tail_conv_bn_chain_bitwise(tg, k, C1, Ca, N, N2, G):
 
     def chain(x1, att, W, b, ga, be, W2, b2, ga2, be2):
         return train.tail_conv_bn_chain(x1, att, k, (W, b, ga, be, *rms[0][0], 0.1, 1e-5, None),
-                                        [(W2, b2, ga2, be2, *rms[0][1], 0.1, 1e-5, None)])
+                                        [(W2, b2, ga2, be2, *rms[0][1], 0.1, 1e-5, None)], group_max=gm)
 
     def layerwise(x1, att, W, b, ga, be, W2, b2, ga2, be2):
         y = train.tail_conv_bn_act(x1, att, k, W, b, ga, be, *rms[1][0])
-        return train.conv_bn_act(y, W2, b2, ga2, be2, *rms[1][1])
+        y = train.conv_bn_act(y, W2, b2, ga2, be2, *rms[1][1])
+        return tg.group_max(y, k) if gm else y
 
     o1, g1 = _grads(chain, ins)
     o2, g2 = _grads(layerwise, ins)
