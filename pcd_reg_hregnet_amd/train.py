@@ -468,7 +468,7 @@ def tail_conv_bn_chain(x1, att, k, tail, layers, group_max=False):
         y, mean, invstd = _ConvStats.apply(y, W, bias, *pre, rm, rv, momentum, eps,
                                            wparam if wparam is not None else W)
         pre = (mean, invstd, gamma, beta)
-    return _BNAct.apply(y, *pre)
+    return _BNActGroupMax.apply(y, *pre, k) if group_max else _BNAct.apply(y, *pre)
 
 
 # Chains of Conv + train-mode BN + ReLU layers (nn.Sequential, layers.py:115-130, 183-198) with the
@@ -652,7 +652,7 @@ def conv_bn_chain(x, layers):
         y, mean, invstd = _ConvStats.apply(y, W, bias, *pre, rm, rv, momentum, eps,
                                            wparam if wparam is not None else W)
         pre = (mean, invstd, gamma, beta)
-    return _BNActGroupMax.apply(y, *pre, k) if group_max else _BNAct.apply(y, *pre)
+    return _BNAct.apply(y, *pre)
 
 
 class ConvBNAct(torch.nn.Module):
