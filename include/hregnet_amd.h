@@ -526,6 +526,17 @@ int hreg_attention_bwd(const float *logits, int ldl, int C, const float *vals, i
                        const float *dkp, const float *dvmap, int lddm, const float *dvsum,
                        int ldds, int same, float *dlogits, int lddl, float *dvals, int lddv,
                        float *dknn, void *stream);
+/* hreg_attention_fwd / _bwd with logits = vals = ReLU(gamma * (y - mean) * invstd + beta) of a
+ * pre-BatchNorm y [G*k][C] (per channel; hreg_bn_apply's values, never materialised: the
+ * detector's last Conv+BN+ReLU, layers.py:150-159; r6); the backward writes dact = the gradient
+ * with respect to that activation (the BN backward follows) and dknn */
+int hreg_attention_fwd_pre(const float *y, int ldy, int C, const float *mean, const float *invstd,
+                           const float *gamma, const float *beta, const float *knn_xyz, int G, int k, float *a,
+                           int32_t *amax, float *kp, float *vmap, int ldm, float *vsum, int lds, void *stream);
+int hreg_attention_bwd_pre(const float *y, int ldy, int C, const float *mean, const float *invstd,
+                           const float *gamma, const float *beta, const float *knn_xyz, int G, int k,
+                           const float *a, const int32_t *amax, const float *dkp, const float *dvmap, int lddm,
+                           const float *dvsum, int ldds, float *dact, int ldda, float *dknn, void *stream);
 /* out[g][c] = max_j x[g*k+j][c], arg = first maximising j  (layers.py:202, 208) */
 int hreg_group_max_arg(const float *x, int ldx, int G, int k, int C, float *out, int ldo,
                        int32_t *arg, void *stream);

@@ -160,6 +160,9 @@ _SIGS = {
     "hreg_attention_bwd": [_vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp,
                            _i, _i, _vp, _i, _vp, _i, _vp, _vp],
     "hreg_group_max_arg": [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp],
+    "hreg_attention_fwd_pre": [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp],
+    "hreg_attention_bwd_pre": [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp,
+                               _i, _vp, _vp],
     "hreg_group_max_arg_pre": [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "hreg_group_max_bwd": [_vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp],
     "hreg_head_out_bwd": [_vp, _i, _i, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _vp],

@@ -342,11 +342,23 @@ __global__ void geom_rows_bwd_kernel(const float *__restrict__ geom, int ldg,
 // ----------------------------------------------------------------- attention
 // One workgroup per group of k <= 64 rows.  x1 = max_c logits (first index),
 // a = softmax_k(x1), kp = sum a*kx, vmap = vals*a, vsum = sum_k vmap.
+// (PRE, r6) BatchNorm parameters of a pre-BN input: every logits / vals value enters as
+// bn_act(x, mean[c], invstd[c], gamma[c], beta[c], ReLU) (hreg_bn_apply's values; the detector's
+// last conv activation, never written: train.py _BNActAttention)
+struct AttPre {
+    const float *mean, *invstd, *gamma, *beta;
+};
+template <bool PRE>
+__device__ __forceinline__ float att_in(const float *p, size_t i, int c, const AttPre &pp) {
+    return PRE ? bn_act(p[i], pp.mean[c], pp.invstd[c], pp.gamma[c], pp.beta[c], 1) : p[i];
+}
+
+template <bool PRE = false>
 __global__ __launch_bounds__(TB) void attention_fwd_kernel(
     const float *__restrict__ logits, int ldl, int C, const float *__restrict__ vals, int ldv,
     int Cv, const float *__restrict__ kx, int k, float *__restrict__ a_out,
     int32_t *__restrict__ amax, float *__restrict__ kp, float *__restrict__ vmap, int ldm,
-    float *__restrict__ vsum, int lds) {
+    float *__restrict__ vsum, int lds, AttPre pp = {}) {
     __shared__ float x1[64], aw[64];
     const int g = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -355,7 +367,7 @@ __global__ __launch_bounds__(TB) void attention_fwd_kernel(
         float best = -INFINITY;
         int bi = 0x7fffffff;
         for (int c = lane; c < C; c += 64) {
-            const float v = row[c];
+            const float v = att_in<PRE>(row, c, c, pp);
             if (v > best) { best = v; bi = c; }
         }
         for (int m = 32; m >= 1; m >>= 1) {
@@ -391,7 +403,7 @@ __global__ __launch_bounds__(TB) void attention_fwd_kernel(
         for (int c = threadIdx.x; c < Cv; c += TB) {
             float s = 0.f;
             for (int j = 0; j < k; ++j) {
-                const float v = fmul_rn(vals[((size_t)g * k + j) * ldv + c], aw[j]);
+                const float v = fmul_rn(att_in<PRE>(vals, ((size_t)g * k + j) * ldv + c, c, pp), aw[j]);
                 if (vmap) vmap[((size_t)g * k + j) * ldm + c] = v;
                 s = fadd_rn(s, v);
             }
@@ -401,13 +413,14 @@ __global__ __launch_bounds__(TB) void attention_fwd_kernel(
 
 // dve = dvmap + dvsum[g]; dvals = a*dve; da = sum_c vals*dve + kx.dkp;
 // dx1 = a*(da - sum a da); dlogits = onehot(amax)*dx1 (+ dvals when vals == logits)
+template <bool PRE = false>
 __global__ __launch_bounds__(TB) void attention_bwd_kernel(
     const float *__restrict__ logits, int ldl, int C, const float *__restrict__ vals, int ldv,
     int Cv, const float *__restrict__ kx, int k, const float *__restrict__ a_in,
     const int32_t *__restrict__ amax, const float *__restrict__ dkp,
     const float *__restrict__ dvmap, int lddm, const float *__restrict__ dvsum, int ldds,
     int same, float *__restrict__ dlogits, int lddl, float *__restrict__ dvals, int lddv,
-    float *__restrict__ dkx) {
+    float *__restrict__ dkx, AttPre pp = {}) {
     __shared__ float aw[64], da[64], dx1[64];
     const int g = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -421,7 +434,7 @@ __global__ __launch_bounds__(TB) void attention_bwd_kernel(
                 float d = 0.f;
                 if (dvmap) d = dvmap[r * lddm + c];
                 if (dvsum) d = fadd_rn(d, dvsum[(size_t)g * ldds + c]);
-                part = fadd_rn(part, fmul_rn(vals[r * ldv + c], d));
+                part = fadd_rn(part, fmul_rn(att_in<PRE>(vals, r * ldv + c, c, pp), d));
                 if (dvals && !same) dvals[r * lddv + c] = fmul_rn(aw[j], d);
             }
         part = wave_sum_f32(part);
@@ -1254,7 +1267,7 @@ extern "C" int hreg_attention_fwd(const float *logits, int ldl, int C, const flo
     if (vals && (ldv < Cv || Cv < 1)) return HREG_ERR_INVALID;
     if (kp && !knn_xyz) return HREG_ERR_INVALID;
     if (!G) return HREG_OK;
-    hipLaunchKernelGGL(attention_fwd_kernel, dim3(G), dim3(TB), 0, as_stream(stream), logits, ldl,
+    hipLaunchKernelGGL(attention_fwd_kernel<false>, dim3(G), dim3(TB), 0, as_stream(stream), logits, ldl,
                        C, vals, ldv, Cv, knn_xyz, k, a, amax, kp, vmap, ldm, vsum, lds);
     HREG_CHECK_LAUNCH();
     return HREG_OK;
@@ -1269,9 +1282,43 @@ extern "C" int hreg_attention_bwd(const float *logits, int ldl, int C, const flo
     if (!logits || !a || !amax || G < 0 || k < 1 || k > 64 || C < 1) return HREG_ERR_INVALID;
     if (dkp && !knn_xyz) return HREG_ERR_INVALID;
     if (!G) return HREG_OK;
-    hipLaunchKernelGGL(attention_bwd_kernel, dim3(G), dim3(TB), 0, as_stream(stream), logits, ldl,
+    hipLaunchKernelGGL(attention_bwd_kernel<false>, dim3(G), dim3(TB), 0, as_stream(stream), logits, ldl,
                        C, vals, ldv, Cv, knn_xyz, k, a, amax, dkp, dvmap, lddm, dvsum, ldds, same,
                        dlogits, lddl, dvals, lddv, dknn);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+// hreg_attention_fwd / _bwd over logits = vals = ReLU(BN(y)) of a pre-BN y [G*k][C] (the
+// detector's last conv activation, never written; r6): every value of y enters as bn_act
+// (hreg_bn_apply's arithmetic), so the outputs are those over the materialised activation; the
+// backward's dlogits is d/d(activation) (the BN backward follows, train.py _BNActAttention)
+extern "C" int hreg_attention_fwd_pre(const float *y, int ldy, int C, const float *mean, const float *invstd,
+                                      const float *gamma, const float *beta, const float *knn_xyz, int G, int k,
+                                      float *a, int32_t *amax, float *kp, float *vmap, int ldm, float *vsum,
+                                      int lds, void *stream) {
+    if (!y || !mean || !invstd || !gamma || !beta || G < 0 || k < 1 || k > 64 || C < 1 || ldy < C)
+        return HREG_ERR_INVALID;
+    if (kp && !knn_xyz) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    hipLaunchKernelGGL(attention_fwd_kernel<true>, dim3(G), dim3(TB), 0, as_stream(stream), y, ldy, C, y, ldy, C,
+                       knn_xyz, k, a, amax, kp, vmap, ldm, vsum, lds, AttPre{mean, invstd, gamma, beta});
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
+extern "C" int hreg_attention_bwd_pre(const float *y, int ldy, int C, const float *mean, const float *invstd,
+                                      const float *gamma, const float *beta, const float *knn_xyz, int G, int k,
+                                      const float *a, const int32_t *amax, const float *dkp, const float *dvmap,
+                                      int lddm, const float *dvsum, int ldds, float *dact, int ldda, float *dknn,
+                                      void *stream) {
+    if (!y || !mean || !invstd || !gamma || !beta || !a || !amax || !dact || G < 0 || k < 1 || k > 64 || C < 1)
+        return HREG_ERR_INVALID;
+    if (dkp && !knn_xyz) return HREG_ERR_INVALID;
+    if (!G) return HREG_OK;
+    hipLaunchKernelGGL(attention_bwd_kernel<true>, dim3(G), dim3(TB), 0, as_stream(stream), y, ldy, C, y, ldy, C,
+                       knn_xyz, k, a, amax, dkp, dvmap, lddm, dvsum, ldds, 1, dact, ldda, nullptr, 0, dknn,
+                       AttPre{mean, invstd, gamma, beta});
     HREG_CHECK_LAUNCH();
     return HREG_OK;
 }

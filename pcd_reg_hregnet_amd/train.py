@@ -641,18 +641,86 @@ def chain_fusable(R: int, widths) -> bool:
             all(lib.hreg_ts_gemm_pre_supported(R, widths[i], widths[i + 1]) for i in range(1, len(widths) - 1)))
 
 
-def conv_bn_chain(x, layers):
-    """Conv1x1 + train-mode BN + ReLU for each (W [N][K], bias, gamma, beta, running_mean,
-    running_var, momentum, eps, wparam) in order, over rows x [R][K0]; the inner activations are
-    never written (the caller checks chain_fusable).  Bitwise the conv_bn_act sequence."""
-    x = x.contiguous()
+def _chain_pre(x, layers):
+    """the chain up to its last layer's pre-BN output -> (y, (mean, invstd, gamma, beta))"""
     pre = (None, None, None, None)
-    y = x
+    y = x.contiguous()
     for W, bias, gamma, beta, rm, rv, momentum, eps, wparam in layers:
         y, mean, invstd = _ConvStats.apply(y, W, bias, *pre, rm, rv, momentum, eps,
                                            wparam if wparam is not None else W)
         pre = (mean, invstd, gamma, beta)
+    return y, pre
+
+
+def conv_bn_chain(x, layers):
+    """Conv1x1 + train-mode BN + ReLU for each (W [N][K], bias, gamma, beta, running_mean,
+    running_var, momentum, eps, wparam) in order, over rows x [R][K0]; the inner activations are
+    never written (the caller checks chain_fusable).  Bitwise the conv_bn_act sequence."""
+    y, pre = _chain_pre(x, layers)
     return _BNAct.apply(y, *pre)
+
+
+class _BNActAttention(torch.autograd.Function):
+    """The detector's attention (train_graph.attention with vals = logits, layers.py:150-159)
+    over ReLU(BN(y)) with the statistics _ConvStats made: the detector's last activation never
+    written.  -> (kp [G][3], vmap [R][C], vsum [G][C]); its backward runs the BN backward."""
+
+    @staticmethod
+    def forward(ctx, y, mean, invstd, gamma, beta, kx, k):
+        R, C = y.shape
+        G = R // k
+        dev = y.device
+        a = torch.empty(R, device=dev)
+        amax = torch.empty(R, dtype=torch.int32, device=dev)
+        kp = torch.empty(G, 3, device=dev)
+        vmap = torch.empty(R, C, device=dev)
+        vsum = torch.empty(G, C, device=dev)
+        _lib.call("hreg_attention_fwd_pre", y, C, C, mean, invstd, gamma, beta, kx, G, k, a, amax, kp, vmap, C,
+                  vsum, C, _stream())
+        ctx.save_for_backward(y, mean, invstd, gamma, beta, kx, a, amax)
+        ctx.side = _SIDE
+        ctx.k = k
+        ctx.params = (gamma, beta)
+        ctx.set_materialize_grads(False)
+        return kp, vmap, vsum
+
+    @staticmethod
+    def backward(ctx, dkp, dvmap, dvsum):
+        y, mean, invstd, gamma, beta, kx, a, amax = ctx.saved_tensors
+        k = ctx.k
+        R, C = y.shape
+        G = R // k
+        dev = y.device
+        st = _stream()
+        dkp = dkp.contiguous() if dkp is not None else None
+        lddm = C
+        if dvmap is not None:
+            if not (dvmap.dim() == 2 and dvmap.stride(1) == 1 and dvmap.stride(0) >= C):
+                dvmap = dvmap.contiguous()
+            lddm = dvmap.stride(0)
+        dvsum = dvsum.contiguous() if dvsum is not None else None
+        dact = torch.empty(R, C, device=dev)
+        dkx = torch.empty(R, 3, device=dev) if (dkp is not None and ctx.needs_input_grad[5]) else None
+        _lib.call("hreg_attention_bwd_pre", y, C, C, mean, invstd, gamma, beta, kx, G, k, a, amax, dkp, dvmap, lddm,
+                  dvsum, C, dact, C, dkx, st)
+        gg, gbt = _grad_slot(ctx.params[0], ctx.side), _grad_slot(ctx.params[1], ctx.side)
+        acc = gg is not None and gbt is not None and ctx.needs_input_grad[3] and ctx.needs_input_grad[4]
+        dgamma = gg if acc else torch.empty(C, device=dev)
+        dbeta = gbt if acc else torch.empty(C, device=dev)
+        dy = torch.empty_like(y)
+        _lib.call("hreg_bn_backward", dact, None, y, R, C, mean, invstd, gamma, beta, 1, col_reduce_ws(R, C, dev), dy,
+                  dgamma, dbeta, 1 if acc else 0, st)
+        if acc:
+            dgamma = dbeta = None
+        return dy, None, None, dgamma, dbeta, dkx, None
+
+
+def conv_bn_chain_attention(x, layers, k, kx):
+    """conv_bn_chain followed by the detector's attention over its activation (vals = logits,
+    want_map, want_sum), the activation never written -> (kp, vmap, vsum); bitwise
+    conv_bn_chain + train_graph.attention (the caller checks chain_fusable)"""
+    y, pre = _chain_pre(x, layers)
+    return _BNActAttention.apply(y, *pre, kx.contiguous(), k)
 
 
 class ConvBNAct(torch.nn.Module):

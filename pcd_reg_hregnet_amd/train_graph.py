@@ -678,8 +678,21 @@ def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src", u
     else:
         grouped_rows = geom
     # detector (layers.py:150-165)
-    emb = seq_convs(grouped_rows, det.convs)
-    kp, att_map, att_feat = attention(emb, k, kx=kx, want_map=True, want_sum=True)
+    kp = None
+    dmods = list(det.convs)
+    dpairs = [(dmods[i], dmods[i + 1]) for i in range(0, len(dmods), 3)]
+    if train.chain_fusable(grouped_rows.shape[0], [grouped_rows.shape[1]] + [c.out_channels for c, _ in dpairs]) \
+            and k <= 64:
+        # the detector's convs and its attention with the last activation never written (the same bits)
+        kp, att_map, att_feat = train.conv_bn_chain_attention(
+            grouped_rows, [(c.weight.view(c.out_channels, -1), c.bias, b.weight, b.bias, b.running_mean,
+                            b.running_var, b.momentum, b.eps, c.weight) for c, b in dpairs], k, kx)
+        for _, b in dpairs:
+            if b.num_batches_tracked is not None:
+                _BN_COUNTERS.append(b.num_batches_tracked)
+    else:
+        emb = seq_convs(grouped_rows, det.convs)
+        kp, att_map, att_feat = attention(emb, k, kx=kx, want_map=True, want_sum=True)
     sig, wnext = _mlp_head(att_feat, (det.mlp1, det.mlp2, det.mlp3), _lib.HREG_HEAD_SOFTPLUS,
                            nb, M, want_weights=True)
     # descriptor (layers.py:200-209)

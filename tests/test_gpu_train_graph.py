@@ -205,6 +205,45 @@ def test_tail_conv_bn_chain_bitwise(tg, k, C1, Ca, N, N2, G, gm):
         assert torch.equal(a, b), i
 
 
+@pytest.mark.parametrize("k,widths,G", [(64, (4, 32, 32, 64), 2048), (32, (68, 64, 64, 128), 1024),
+                                         (16, (132, 128, 128, 256), 1024)])
+def test_conv_bn_chain_attention_bitwise(tg, k, widths, G):
+    """r6: the detector's convs and attention with the last activation never written
+    (train.conv_bn_chain_attention: the attention reads the pre-BN output and applies the BN + ReLU
+    on load, its backward runs the BN backward) give conv_bn_act x n + attention's bits: kp, the
+    attended map and sum, running statistics and every gradient (kx's included), at the three
+    levels' widths."""
+    from pcd_reg_hregnet_amd import train
+    R = G * k
+    assert train.chain_fusable(R, list(widths))
+    L = len(widths) - 1
+    ins = [_rand(R, widths[0], seed=1), _rand(R, 3, seed=2, scale=3)]
+    for i in range(L):
+        K, N = widths[i], widths[i + 1]
+        ins += [_rand(N, K, seed=10 + i, scale=1.0 / K ** 0.5), 1 + _rand(N, seed=30 + i, scale=0.1),
+                _rand(N, seed=40 + i, scale=0.1)]
+    rms = [[(torch.zeros(widths[i + 1], device=DEV), torch.ones(widths[i + 1], device=DEV)) for i in range(L)]
+           for _ in range(2)]
+
+    def chain(x, kx, *ps):
+        layers = [(ps[3 * i], None, ps[3 * i + 1], ps[3 * i + 2], *rms[0][i], 0.1, 1e-5, None) for i in range(L)]
+        return train.conv_bn_chain_attention(x, layers, k, kx)
+
+    def layerwise(x, kx, *ps):
+        for i in range(L):
+            x = train.conv_bn_act(x, ps[3 * i], None, ps[3 * i + 1], ps[3 * i + 2], *rms[1][i])
+        return tg.attention(x, k, kx=kx, want_map=True, want_sum=True)
+
+    o1, g1 = _grads(chain, ins)
+    o2, g2 = _grads(layerwise, ins)
+    for a, b in zip(o1, o2):
+        assert torch.equal(a, b)
+    for (a, b), (c, d) in zip(rms[0], rms[1]):
+        assert torch.equal(a, c) and torch.equal(b, d)
+    for i, (a, b) in enumerate(zip(g1, g2)):
+        assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize("R,widths,bias", [(131072, (4, 32, 32, 64), False), (32768, (64, 64, 64, 128), True),
                                            (16384, (132, 128, 128), True), (20000, (64, 256, 256), False)])
 def test_conv_bn_chain_bitwise(tg, R, widths, bias):
