@@ -604,18 +604,33 @@ def conv_bn(x, conv, bn, relu=True):
     return y
 
 
+def _layer(conv, bn):
+    """a (Conv, BN) pair as train.conv_bn_chain's layer tuple"""
+    return (conv.weight.view(conv.out_channels, -1), conv.bias, bn.weight, bn.bias, bn.running_mean,
+            bn.running_var, bn.momentum, bn.eps, conv.weight)
+
+
+def _count_bn(*bns):
+    """num_batches_tracked += 1 for each BN called (flushed once per forward)"""
+    for bn in bns:
+        if bn.num_batches_tracked is not None:
+            _BN_COUNTERS.append(bn.num_batches_tracked)
+
+
+def _pairs(seq):
+    """nn.Sequential of [Conv, BN, ReLU] * n -> [(conv, bn)]"""
+    mods = list(seq)
+    return [(mods[i], mods[i + 1]) for i in range(0, len(mods), 3)]
+
+
 def conv_bn_seq(x, pairs):
     """[(conv, bn)] each Conv(1x1) + train-mode BN + ReLU in order: one fused chain
     (train.conv_bn_chain: the inner activations never written, the same bits) when its kernels
     take the shapes, else layer by layer."""
     widths = [x.shape[1]] + [conv.out_channels for conv, _ in pairs]
     if len(pairs) >= 2 and train.chain_fusable(x.shape[0], widths):
-        layers = [(conv.weight.view(conv.out_channels, -1), conv.bias, bn.weight, bn.bias, bn.running_mean,
-                   bn.running_var, bn.momentum, bn.eps, conv.weight) for conv, bn in pairs]
-        y = train.conv_bn_chain(x, layers)
-        for _, bn in pairs:
-            if bn.num_batches_tracked is not None:
-                _BN_COUNTERS.append(bn.num_batches_tracked)
+        y = train.conv_bn_chain(x, [_layer(c, b) for c, b in pairs])
+        _count_bn(*(b for _, b in pairs))
         return y
     for conv, bn in pairs:
         x = conv_bn(x, conv, bn, relu=True)
@@ -624,8 +639,7 @@ def conv_bn_seq(x, pairs):
 
 def seq_convs(x, seq):
     """nn.Sequential of [Conv, BN, ReLU] * n."""
-    mods = list(seq)
-    return conv_bn_seq(x, [(mods[i], mods[i + 1]) for i in range(0, len(mods), 3)])
+    return conv_bn_seq(x, _pairs(seq))
 
 
 def _mlp_head(x, head_mods, mode, nclouds, rows, want_weights=False):
@@ -678,18 +692,13 @@ def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src", u
     else:
         grouped_rows = geom
     # detector (layers.py:150-165)
-    kp = None
-    dmods = list(det.convs)
-    dpairs = [(dmods[i], dmods[i + 1]) for i in range(0, len(dmods), 3)]
-    if train.chain_fusable(grouped_rows.shape[0], [grouped_rows.shape[1]] + [c.out_channels for c, _ in dpairs]) \
-            and k <= 64:
+    dpairs = _pairs(det.convs)
+    if k <= 64 and train.chain_fusable(grouped_rows.shape[0],
+                                       [grouped_rows.shape[1]] + [c.out_channels for c, _ in dpairs]):
         # the detector's convs and its attention with the last activation never written (the same bits)
-        kp, att_map, att_feat = train.conv_bn_chain_attention(
-            grouped_rows, [(c.weight.view(c.out_channels, -1), c.bias, b.weight, b.bias, b.running_mean,
-                            b.running_var, b.momentum, b.eps, c.weight) for c, b in dpairs], k, kx)
-        for _, b in dpairs:
-            if b.num_batches_tracked is not None:
-                _BN_COUNTERS.append(b.num_batches_tracked)
+        kp, att_map, att_feat = train.conv_bn_chain_attention(grouped_rows, [_layer(c, b) for c, b in dpairs],
+                                                              k, kx)
+        _count_bn(*(b for _, b in dpairs))
     else:
         emb = seq_convs(grouped_rows, det.convs)
         kp, att_map, att_feat = attention(emb, k, kx=kx, want_map=True, want_sum=True)
@@ -703,16 +712,9 @@ def keypoint_level(det, desc, lvl, xyz, feats, weights, hook=None, part="src", u
                                                [conv.out_channels, conv2.out_channels]):
         # mlp1 without its input concatenation, mlp2 applying mlp1's BN + ReLU on load and the k-max
         # mlp2's (the same bits as the layerwise path)
-        y = train.tail_conv_bn_chain(
-            x1, att_map, k,
-            (conv.weight.view(conv.out_channels, -1), conv.bias, bn.weight, bn.bias, bn.running_mean,
-             bn.running_var, bn.momentum, bn.eps, conv.weight),
-            [(conv2.weight.view(conv2.out_channels, -1), conv2.bias, bn2.weight, bn2.bias, bn2.running_mean,
-              bn2.running_var, bn2.momentum, bn2.eps, conv2.weight)], group_max=True)
-        for b_ in (bn, bn2):
-            if b_.num_batches_tracked is not None:
-                _BN_COUNTERS.append(b_.num_batches_tracked)
-        return kp.view(nb, M, 3), sig, att_feat, y, wnext, fps_loc
+        d = train.tail_conv_bn_chain(x1, att_map, k, _layer(conv, bn), [_layer(conv2, bn2)], group_max=True)
+        _count_bn(bn, bn2)
+        return kp.view(nb, M, 3), sig, att_feat, d, wnext, fps_loc
     if TAIL_FUSED and train.tail_fusable(x1.shape[0], k, x1.shape[1], att_map.shape[1], conv.out_channels):
         # mlp1 over cat([max_k x1 repeated, x1, att_map]) without materialising it (the same bits)
         y = train.tail_conv_bn_act(x1, att_map, k, conv.weight.view(conv.out_channels, -1), conv.bias,
