@@ -400,6 +400,14 @@ int hreg_bn_stats(const float *y, int R, int C, float eps, void *ws, float *mean
 int hreg_ts_gemm_supported(int R, int K, int N, int stats);
 int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
                  const float *scale, const float *shift, int relu, float *out, int ldo, void *stream);
+/* hreg_ts_gemm (no scale / shift / activation) with its output [R][N] split by columns: [0, n1)
+ * -> out0 (row stride ld0), [n1, n2) -> out1 (ld1), [n2, N) -> out2 (ld2; NULL when n2 = N); n1
+ * and n2 multiples of 32 (n2 may equal N), 16-byte aligned outputs.  The same values as
+ * hreg_ts_gemm's (r6: the descriptor tail's input gradient, layers.py:204-206, written straight
+ * into its x2-block / x1 / att_map gradients). */
+int hreg_ts_gemm_split_out(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
+                           float *out0, int ld0, int n1, float *out1, int ld1, int n2, float *out2, int ld2,
+                           void *stream);
 /* hreg_ts_gemm (no scale / activation) with the output's train-mode BatchNorm statistics
  * computed in its epilogue (fp64 sums, fixed order; the hreg_bn_stats pass over out it
  * replaces): mean, invstd, var_unbiased as hreg_bn_stats (var_unbiased may be NULL without

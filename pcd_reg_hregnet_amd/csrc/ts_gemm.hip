@@ -46,19 +46,27 @@ struct TsPre {
     const float *mean, *invstd, *gamma, *beta;
 };
 
+// (OSEG, r6) the output as column segments: columns [nend[s-1], nend[s]) go to segment s's
+// matrix (stride ld[s]); every nend a multiple of 32, so an output tile writes one segment (the
+// descriptor tail's input gradient straight into its x2 / x1 / att_map blocks)
+struct TsOut {
+    float *base[3];
+    int ld[3], nend[3];
+};
+
 // STATS: the train-mode BatchNorm statistics of the output ride along in the epilogue (the
 // col_reduce pass over y it replaces): every lane keeps fp64 sums of its column's values and
 // squares (exact products) over its rows, in its fixed tile order; the lane halves, then the
 // four waves (in order, through LDS) combine, and each workgroup writes its partial
 // [blockIdx.x][N][2] for col_finalize (train.hip) to sum over workgroups in order.
-template <int NT, bool TAIL, bool FULL, bool STATS = false, bool SEG = false, bool PRE = false>
+template <int NT, bool TAIL, bool FULL, bool STATS = false, bool SEG = false, bool PRE = false, bool OSEG = false>
 __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict__ A, int lda, int R, int K,
                                                          const float *__restrict__ W, int w_trans, int N,
                                                          const float *__restrict__ scale,
                                                          const float *__restrict__ shift, int relu,
                                                          float *__restrict__ out, int ldo,
                                                          double *__restrict__ part = nullptr, TsSeg sg = {},
-                                                         TsPre pre = {}) {
+                                                         TsPre pre = {}, TsOut os = {}) {
     extern __shared__ __attribute__((aligned(16))) float Ws[];
     const int K16 = (K + 15) & ~15, KP = K16 + 4, nsub = K16 / 16;
     const int ngrp = (nsub + TS_GRP - 1) / TS_GRP;
@@ -205,6 +213,15 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
 #pragma unroll
             for (int co = 0; co < NT; ++co) {
                 const int nl = co * 32 + j, n = n0 + nl;
+                float *obase = out;
+                int old_ = ldo, ncol = n;
+                if constexpr (OSEG) {
+                    const int nt0 = n0 + co * 32;  // (uniform) the tile's segment
+                    const int sgi = nt0 < os.nend[0] ? 0 : nt0 < os.nend[1] ? 1 : 2;
+                    obase = os.base[sgi];
+                    old_ = os.ld[sgi];
+                    ncol = n - (sgi == 0 ? 0 : os.nend[sgi - 1]);
+                }
                 if (n < N) {
                     const float sh = Sh[nl];
                     const float sc = FULL ? Sc[nl] : 1.f;
@@ -219,7 +236,7 @@ __global__ __launch_bounds__(256, 2) void ts_gemm_kernel(const float *__restrict
                             } else {
                                 v = fadd_rn(v, sh);
                             }
-                            out[(size_t)r * ldo + n] = v;
+                            obase[(size_t)r * old_ + ncol] = v;
                             if constexpr (STATS) {
                                 const double d = (double)v;
                                 st1[co] += d;
@@ -314,10 +331,10 @@ namespace {
 
 // launch (STATS: the workgroups' statistic partials into part, see ts_gemm_kernel); returns
 // the number of workgroups along the rows (the partials' count), or a negative HREG_ERR_*
-template <bool STATS, bool SEG = false, bool PRE = false>
+template <bool STATS, bool SEG = false, bool PRE = false, bool OSEG = false>
 int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans, int N, const float *scale,
               const float *shift, int relu, float *out, int ldo, double *part, hipStream_t st, TsSeg sg = {},
-              TsPre pre = {}) {
+              TsPre pre = {}, TsOut os = {}) {
     if (!A || !W || !out || R <= 0 || K <= 0 || N <= 0 || lda < K || ldo < N || (K & 3) || (N & 3) ||
         (lda & 3) || (ldo & 3) || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W) |
                                      reinterpret_cast<uintptr_t>(out)) & 15))
@@ -338,8 +355,8 @@ int ts_launch(const float *A, int lda, int R, int K, const float *W, int w_trans
     if (STATS && full) return -HREG_ERR_UNSUPPORTED;
 #define TS_CASE(NTT, TT, FF)                                                                                   \
     if (nt == NTT && tail == TT && full == FF) {                                                              \
-        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF, STATS, SEG, PRE>), dim3(gx, gy), dim3(256), lds, st, A, lda, \
-                           R, K, W, w_trans, N, scale, shift, relu, out, ldo, part, sg, pre);                  \
+        hipLaunchKernelGGL((ts_gemm_kernel<NTT, TT, FF, STATS, SEG, PRE, OSEG>), dim3(gx, gy), dim3(256), lds, st, A, \
+                           lda, R, K, W, w_trans, N, scale, shift, relu, out, ldo, part, sg, pre, os);         \
         if (hipGetLastError() != hipSuccess) return -HREG_ERR_LAUNCH;                                          \
         return gx;                                                                                             \
     }
@@ -359,6 +376,28 @@ extern "C" int hreg_ts_gemm(const float *A, int lda, int R, int K, const float *
     if (R == 0 && A && W && out) return HREG_OK;
     const int rc = ts_launch<false>(A, lda, R, K, W, w_trans, N, scale, shift, relu, out, ldo, nullptr,
                                     as_stream(stream));
+    return rc < 0 ? -rc : HREG_OK;
+}
+
+// hreg_ts_gemm (no scale / shift / activation) with the output [R][N] split by columns into up to
+// three matrices: columns [0, n1) -> out0 (stride ld0), [n1, n2) -> out1, [n2, N) -> out2; n1, n2
+// multiples of 32 (n2 = N: two segments).  The same values as hreg_ts_gemm's (r6: the descriptor
+// tail's input gradient written straight into its x2-block / x1 / att_map gradients).
+extern "C" int hreg_ts_gemm_split_out(const float *A, int lda, int R, int K, const float *W, int w_trans, int N,
+                                      float *out0, int ld0, int n1, float *out1, int ld1, int n2, float *out2,
+                                      int ld2, void *stream) {
+    if (!out0 || !out1 || n1 <= 0 || n2 < n1 || n2 > N || (n1 & 31) || ((n2 & 31) && n2 != N) ||
+        (n2 < N && !out2) || ld0 < n1 || ld1 < n2 - n1 || (n2 < N && ld2 < N - n2) || ((ld0 | ld1 | ld2) & 3) ||
+        ((reinterpret_cast<uintptr_t>(out0) | reinterpret_cast<uintptr_t>(out1) | reinterpret_cast<uintptr_t>(out2)) & 15))
+        return HREG_ERR_INVALID;
+    if (R == 0 && A && W) return HREG_OK;
+    TsOut os;
+    os.base[0] = out0; os.ld[0] = ld0; os.nend[0] = n1;
+    os.base[1] = out1; os.ld[1] = ld1; os.nend[1] = n2;
+    os.base[2] = out2 ? out2 : out1; os.ld[2] = out2 ? ld2 : ld1; os.nend[2] = N;
+    // (out / ldo: the validity checks of the plain form; the tiles are written through os)
+    const int rc = ts_launch<false, false, false, true>(A, lda, R, K, W, w_trans, N, nullptr, nullptr, 0, out0, N,
+                                                        nullptr, as_stream(stream), {}, {}, os);
     return rc < 0 ? -rc : HREG_OK;
 }
 

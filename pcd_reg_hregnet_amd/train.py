@@ -362,15 +362,27 @@ def _tail_backward(ctx, dy, x1, att, x2, arg, W, need_x1, need_att, need_W, need
             dbias = col_sum(dy)
     dx1 = datt = None
     if need_x1 or need_att:
-        dcat = _conv_gemm(dy, W, None, w_trans=True)  # [R][K] (desc_tail's backward from here)
-        if need_x1:
-            dx2 = torch.empty(G, C1, device=dev)
-            _lib.call("hreg_group_sum", dcat, K, G, k, C1, dx2, C1, 0, st)
+        # the [R][K] input gradient (desc_tail's backward from here): its x1 and att_map blocks
+        # written straight into their own gradients when the tall-skinny GEMM takes the shape
+        if (TS_GEMM and R >= TS_MIN_ROWS and C1 % 32 == 0 and W.is_contiguous() and
+                _lib.load().hreg_ts_gemm_supported(R, N, K, 0)):
+            drep = torch.empty(R, C1, device=dev)
+            dx1 = torch.empty(R, C1, device=dev)
+            datt = torch.empty(R, Ca, device=dev)
+            _lib.call("hreg_ts_gemm_split_out", dy, N, R, N, W, 1, K, drep, C1, C1, dx1, C1, 2 * C1, datt, Ca, st)
+        else:
+            dcat = _conv_gemm(dy, W, None, w_trans=True)
+            drep, datt = dcat, dcat[:, 2 * C1:]
             dx1 = torch.empty(R, C1, device=dev)
             _lib.call("hreg_copy_rows", dcat[:, C1:], K, 1, R, C1, dx1, C1, 0, st)
+        if need_x1:
+            dx2 = torch.empty(G, C1, device=dev)
+            _lib.call("hreg_group_sum", drep, drep.stride(0), G, k, C1, dx2, C1, 0, st)
             _lib.call("hreg_group_max_bwd", dx2, C1, arg, G, k, C1, dx1, C1, 1, st)
-        if need_att:
-            datt = dcat[:, 2 * C1:]
+        else:
+            dx1 = None
+        if not need_att:
+            datt = None
     return dx1, datt, dW, dbias
 
 
