@@ -494,6 +494,9 @@ int hreg_adam_step_dev(float *param, const float *grad, float *exp_avg, float *e
  * .train()), wired into autograd by pcd_reg_hregnet_amd/train_graph.py.  Rows are
  * point-major [rows][ld]; a group of k neighbours is k consecutive rows.  Backward
  * sums run in a fixed order (no float atomics): same bits every run. */
+/* count (<= 16) device-to-device copies src[i] -> dst[i] of nbytes[i] bytes (multiples of 4; host
+ * arrays, read at the call) in one launch */
+int hreg_copy_many(int count, const void *const *src, void *const *dst, const size_t *nbytes, void *stream);
 /* dst[r][c] (+)= src[r / row_div][c]  (torch.cat / repeat over k; accumulate != 0 adds) */
 int hreg_copy_rows(const float *src, int lds, int row_div, int R, int C, float *dst, int ldd,
                    int accumulate, void *stream);

@@ -132,6 +132,7 @@ _SIGS = {
     "hreg_debug_gemm_tn_s": [_vp, _i, _vp, _i, _i, _i, _i, ctypes.c_float, _vp, _vp, _vp, _i],
     "hreg_ts_gemm_supported": [_i, _i, _i, _i],
     "hreg_ts_gemm": [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _vp],
+    "hreg_copy_many": [_i, _vp, _vp, _vp, _vp],
     "hreg_ts_gemm_split_out": [_vp, _i, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _vp],
     "hreg_ts_gemm_bn_tail": [_vp, _i, _vp, _i, _vp, _i, _i, _vp, _i, _vp, _vp, _i, ctypes.c_float, ctypes.c_float,
                              _vp, _vp, _vp, _vp,

@@ -1135,6 +1135,50 @@ __global__ void loss_bwd_kernel(const float *__restrict__ pR, const float *__res
 
 // ======================================================================= C ABI
 
+// up to COPY_MANY contiguous byte ranges in one launch (blockIdx.y = range): 16-byte words when
+// both ends and the size allow, else 4-byte words (every range a multiple of 4 bytes)
+constexpr int COPY_MANY = 16;
+struct CopyMany {
+    const void *src[COPY_MANY];
+    void *dst[COPY_MANY];
+    size_t nbytes[COPY_MANY];
+};
+
+__global__ __launch_bounds__(TB) void copy_many_kernel(CopyMany cm) {
+    const int e = blockIdx.y;
+    const size_t nb = cm.nbytes[e];
+    const uintptr_t a = reinterpret_cast<uintptr_t>(cm.src[e]) | reinterpret_cast<uintptr_t>(cm.dst[e]);
+    if (!((a | nb) & 15)) {
+        const uint4 *s = static_cast<const uint4 *>(cm.src[e]);
+        uint4 *d = static_cast<uint4 *>(cm.dst[e]);
+        for (size_t i = (size_t)blockIdx.x * TB + threadIdx.x; i < nb / 16; i += (size_t)gridDim.x * TB) d[i] = s[i];
+    } else {
+        const uint32_t *s = static_cast<const uint32_t *>(cm.src[e]);
+        uint32_t *d = static_cast<uint32_t *>(cm.dst[e]);
+        for (size_t i = (size_t)blockIdx.x * TB + threadIdx.x; i < nb / 4; i += (size_t)gridDim.x * TB) d[i] = s[i];
+    }
+}
+
+// count (<= 16) device-to-device copies of nbytes[i] (multiples of 4) in one launch: the graph
+// executor's per-round copies of a lane's feature-extraction outputs (r6: 12 copy nodes -> 1)
+extern "C" int hreg_copy_many(int count, const void *const *src, void *const *dst, const size_t *nbytes,
+                              void *stream) {
+    if (count < 0 || count > COPY_MANY || (count && (!src || !dst || !nbytes))) return HREG_ERR_INVALID;
+    CopyMany cm{};
+    size_t most = 0;
+    for (int i = 0; i < count; ++i) {
+        if (!src[i] || !dst[i] || (nbytes[i] & 3)) return HREG_ERR_INVALID;
+        cm.src[i] = src[i];
+        cm.dst[i] = dst[i];
+        cm.nbytes[i] = nbytes[i];
+        most = nbytes[i] > most ? nbytes[i] : most;
+    }
+    if (!count || !most) return HREG_OK;
+    hipLaunchKernelGGL(copy_many_kernel, dim3(g1d((most + 15) / 16), count), dim3(TB), 0, as_stream(stream), cm);
+    HREG_CHECK_LAUNCH();
+    return HREG_OK;
+}
+
 extern "C" int hreg_copy_rows(const float *src, int lds, int row_div, int R, int C, float *dst,
                               int ldd, int accumulate, void *stream) {
     if (!src || !dst || R < 0 || C < 0 || row_div < 1 || lds < C || ldd < C) return HREG_ERR_INVALID;

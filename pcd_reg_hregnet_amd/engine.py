@@ -1733,6 +1733,25 @@ def fork_width(lanes: int, batched_stage1: bool, front_two_streams: bool) -> int
     return lanes * (2 if front_two_streams else 1) + (1 if batched_stage1 else lanes)
 
 
+def copy_many(dsts, srcs) -> None:
+    """dst.copy_(src) for each pair (same dtype and shape, contiguous) in one hreg_copy_many launch
+    per 16 pairs; any other pair through torch"""
+    import ctypes
+    pairs = [(d, s) for d, s in zip(dsts, srcs)
+             if d.is_contiguous() and s.is_contiguous() and d.dtype == s.dtype and d.shape == s.shape
+             and (d.numel() * d.element_size()) % 4 == 0]
+    rest = [(d, s) for d, s in zip(dsts, srcs) if not any(d is p for p, _ in pairs)]
+    for i in range(0, len(pairs), 16):
+        chunk = pairs[i:i + 16]
+        n = len(chunk)
+        src = (ctypes.c_void_p * n)(*[s.data_ptr() for _, s in chunk])
+        dst = (ctypes.c_void_p * n)(*[d.data_ptr() for d, _ in chunk])
+        nb = (ctypes.c_size_t * n)(*[d.numel() * d.element_size() for d, _ in chunk])
+        call("hreg_copy_many", n, src, dst, nb, _stream())
+    for d, s in rest:
+        d.copy_(s)
+
+
 class GraphPipeline:
     """The pipelined forward captured as HIP graphs (kernel boundaries ~1.5 us
     instead of a host launch each).
@@ -1942,10 +1961,9 @@ class GraphPipeline:
         """Lane ln's feature extraction from stage-1 set cur, copied into fe[cur][ln]."""
         pts, g = self.bufs[ln][cur]
         fe = hregnet_front(self.P, self.src[ln], self.dst[ln], self.use_weights, l1=g, pts=pts)
-        # one multi-tensor copy per dtype instead of 12 copy kernels per lane and round (r5:
-        # neutral, 7964 vs 7943 pairs/s, kept)
+        # the 12 tensors in one launch (hreg_copy_many) instead of 12 copy nodes per lane and round
         dst = self.fe[cur][ln]
-        torch._foreach_copy_([dst[k] for k in FRONT_KEYS], [fe[k] for k in FRONT_KEYS])
+        copy_many([dst[k] for k in FRONT_KEYS], [fe[k] for k in FRONT_KEYS])
 
     def prime(self):
         """Front streaming: run the next round's feature extraction (and the stage 1 of the

@@ -76,6 +76,9 @@ def apply(variant, lib, engine):
         elif k == "probe.nostage1" and int(v):
             undo.append(("engine", "grouping", engine.grouping))
             engine.grouping = _nostage1(engine)
+        elif k == "alt.torchcopy" and int(v):  # (r6: the front copies through torch._foreach_copy_)
+            undo.append(("engine", "copy_many", engine.copy_many))
+            engine.copy_many = lambda dsts, srcs: torch._foreach_copy_(list(dsts), list(srcs))
         elif k == "probe.nofps1" and int(v):
             undo.append(("engine", "fps_indexed", engine.fps_indexed))
             engine.fps_indexed = _nofps1(engine)
